@@ -1,0 +1,146 @@
+"""ctypes bindings for the test oracles.  TEST INFRASTRUCTURE ONLY.
+
+`Oracle()` loads oracle/build/liboracle.so (the in-repo C restatement,
+oracle/xcodec_oracle.c); `Oracle(ref=True)` loads oracle/_ref/libxcref.so (the
+real reference hot path compiled from /root/reference by oracle/Makefile).
+Both expose the same batch encode / decode / hash surface so tests can check
+one against the other and both against the GPU engine.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEG = 2048
+
+MODE_INDEPENDENT, MODE_STREAM, MODE_NULL = 0, 1, 2
+
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def build():
+    import subprocess
+    subprocess.run(['make', '-s', '-C', HERE], check=True)
+
+
+class Oracle:
+    def __init__(self, ref: bool = False):
+        self.ref = ref
+        path = os.path.join(HERE, '_ref/libxcref.so' if ref else 'build/liboracle.so')
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = self.lib = C.CDLL(path)
+        pre = 'xcr_' if ref else 'xco_'
+        self._hash = getattr(L, pre + 'hash')
+        self._hash.restype = C.c_uint64
+        self._hash.argtypes = [_u8p]
+        self._wh = getattr(L, pre + 'window_hashes')
+        self._wh.argtypes = [_u8p, C.c_uint64, _u64p]
+        self._cnew = getattr(L, pre + "cache_new")
+        self._cnew.restype = C.c_void_p
+        self._cfree = getattr(L, pre + 'cache_free')
+        self._cfree.argtypes = [C.c_void_p]
+        self._eb = getattr(L, pre + 'encode_batch')
+        if ref:
+            self._eb.argtypes = [C.c_void_p, _u8p, _u64p, _u32p, C.c_uint32, C.c_int, _u8p, _u64p, _u64p]
+        else:
+            self._eb.argtypes = [C.c_void_p, _u8p, _u64p, _u32p, C.c_uint32, C.c_int, C.c_int, _u8p, _u64p, _u64p]
+        self._eb.restype = C.c_int
+        self._dec = getattr(L, pre + 'decode') if ref else None
+        if ref:
+            self._dec.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u64p, _u64p, C.c_uint64]
+            self._dec.restype = C.c_int
+        else:
+            L.xco_decoder_new.restype = C.c_void_p
+            L.xco_decoder_new.argtypes = [C.c_void_p]
+            L.xco_decoder_free.argtypes = [C.c_void_p]
+            L.xco_decode.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u64p, _u64p, C.c_uint64]
+            L.xco_decode.restype = C.c_int
+            L.xco_cache_size.restype = C.c_uint64
+            L.xco_cache_size.argtypes = [C.c_void_p]
+            L.xco_cache_enter.argtypes = [C.c_void_p, C.c_uint64, _u8p]
+            L.xco_cache_enter.restype = C.c_int
+            L.xco_cache_export.argtypes = [C.c_void_p, _u64p, _u8p, C.c_uint64]
+            L.xco_cache_export.restype = C.c_uint64
+
+    # ------------------------------------------------------------------ hash
+    def hash(self, w: bytes) -> int:
+        a = np.frombuffer(w, dtype=np.uint8)
+        assert a.size >= SEG
+        return int(self._hash(_p(a, _u8p)))
+
+    def window_hashes(self, x: bytes) -> np.ndarray:
+        a = np.frombuffer(x, dtype=np.uint8)
+        n = max(0, a.size - SEG + 1)
+        out = np.zeros(n, dtype=np.uint64)
+        if n:
+            self._wh(_p(a, _u8p), a.size, _p(out, _u64p))
+        return out
+
+    # ----------------------------------------------------------------- cache
+    def cache_new(self):
+        return self._cnew()
+
+    def cache_free(self, c):
+        self._cfree(c)
+
+    # ---------------------------------------------------------------- encode
+    def encode_batch(self, data, offs, lens, mode=MODE_INDEPENDENT, oob=False, cache=None):
+        """Encode chunks data[offs[i]:offs[i]+lens[i]]; returns list of bytes."""
+        a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = offs.size
+        bounds = 2 * lens.astype(np.uint64) + 16
+        oo = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            oo[1:] = np.cumsum(bounds)[:-1]
+        out = np.zeros(int(bounds.sum()) + 1, dtype=np.uint8)
+        ol = np.zeros(n, dtype=np.uint64)
+        if self.ref:
+            assert oob == (mode == MODE_NULL), 'reference OOB mode is the null cache'
+            rc = self._eb(cache, _p(a, _u8p), _p(offs, _u64p), _p(lens, _u32p), n, mode,
+                          _p(out, _u8p), _p(oo, _u64p), _p(ol, _u64p))
+        else:
+            rc = self._eb(cache, _p(a, _u8p), _p(offs, _u64p), _p(lens, _u32p), n, mode, int(oob),
+                          _p(out, _u8p), _p(oo, _u64p), _p(ol, _u64p))
+        if rc != 0:
+            raise RuntimeError('oracle encode failed')
+        return [out[int(oo[i]):int(oo[i] + ol[i])].tobytes() for i in range(n)]
+
+    def encode_stream(self, data: bytes, chunk=65536, mode=MODE_STREAM, oob=False, cache=None) -> bytes:
+        from wanproxy_amd.synth import chunks_of
+        offs, lens = chunks_of(data, chunk)
+        return b''.join(self.encode_batch(data, offs, lens, mode=mode, oob=oob, cache=cache))
+
+    # ---------------------------------------------------------------- decode
+    def decode(self, enc: bytes, cache, out_cap=None, decoder=None):
+        """One XCodecDecoder::decode over `enc`.  Returns (ok, out, consumed, unknown)."""
+        a = np.frombuffer(enc, dtype=np.uint8)
+        cap = out_cap or (a.size // 10 + 1) * SEG + a.size
+        out = np.zeros(cap, dtype=np.uint8)
+        ol = np.zeros(1, dtype=np.uint64)
+        cons = np.zeros(1, dtype=np.uint64)
+        unk = np.zeros(4096, dtype=np.uint64)
+        nunk = np.zeros(1, dtype=np.uint64)
+        if self.ref:
+            rc = self._dec(cache, _p(a, _u8p), a.size, _p(out, _u8p), cap, _p(ol, _u64p), _p(cons, _u64p),
+                           _p(unk, _u64p), _p(nunk, _u64p), unk.size)
+        else:
+            d = decoder if decoder is not None else self.lib.xco_decoder_new(cache)
+            rc = self.lib.xco_decode(d, _p(a, _u8p), a.size, _p(out, _u8p), cap, _p(ol, _u64p), _p(cons, _u64p),
+                                     _p(unk, _u64p), _p(nunk, _u64p), unk.size)
+            if decoder is None:
+                self.lib.xco_decoder_free(d)
+        if rc < 0:
+            raise RuntimeError('decode overflow')
+        return bool(rc), out[:int(ol[0])].tobytes(), int(cons[0]), [int(u) for u in unk[:int(nunk[0])]]

@@ -1,0 +1,141 @@
+/*
+ * ref_driver.cc -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * A thin extern "C" harness around the REAL reference classes, compiled by
+ * oracle/Makefile directly from the reference sources where they lie under
+ * /root/reference (xcodec/xcodec_encoder.cc, xcodec/xcodec_decoder.cc,
+ * xcodec/xcodec_cache.cc, common/buffer.cc, common/log.cc).  No reference
+ * source is copied into this repository; the build output goes only to
+ * oracle/_ref/.  This file plays the role of the reference's own drivers
+ * (programs/tack/tack.cc:298-359, xcodec/test/xcodec-encode-decode1).
+ */
+#include <common/buffer.h>
+#include <common/endian.h>
+#include <xcodec/xcodec.h>
+#include <xcodec/xcodec_cache.h>
+#include <xcodec/xcodec_decoder.h>
+#include <xcodec/xcodec_encoder.h>
+#include <xcodec/xcodec_hash.h>
+
+#include <string.h>
+
+/* Out-of-band null cache: the same contract as tack's TackNullCache
+ * (programs/tack/tack.cc:70-101): lookups miss, enter is a no-op. */
+class RefNullCache : public XCodecCache {
+public:
+	RefNullCache(const UUID& uuid) : XCodecCache(uuid) { }
+	XCodecCache *connect(const UUID&) { return NULL; }
+	void enter(const uint64_t&, BufferSegment *) { }
+	void replace(const uint64_t&, BufferSegment *) { }
+	BufferSegment *lookup(const uint64_t&) { return NULL; }
+	bool out_of_band(void) const { return true; }
+};
+
+static uint64_t drain(Buffer *b, uint8_t *out, uint64_t cap)
+{
+	uint64_t n = b->length();
+	if (n > cap)
+		return ~(uint64_t)0;
+	b->copyout(out, n);
+	b->clear();
+	return n;
+}
+
+extern "C" {
+
+uint64_t xcr_hash(const uint8_t *data)
+{
+	return XCodecHash::hash(data);
+}
+
+/* Per-window XCodecHash values exactly as the encoder's rolling loop sees
+ * them (add() x 2048 then roll()), xcodec_encoder.cc:126-176. */
+void xcr_window_hashes(const uint8_t *x, uint64_t len, uint64_t *out)
+{
+	if (len < XCODEC_SEGMENT_LENGTH)
+		return;
+	XCodecHash h;
+	for (unsigned i = 0; i < XCODEC_SEGMENT_LENGTH; i++)
+		h.add(x[i]);
+	for (uint64_t s = 0;; s++) {
+		out[s] = h.mix();
+		if (s + XCODEC_SEGMENT_LENGTH >= len)
+			break;
+		h.roll(x[s + XCODEC_SEGMENT_LENGTH]);
+	}
+}
+
+void *xcr_cache_new(void)
+{
+	UUID uuid;
+	return new XCodecMemoryCache(uuid);
+}
+
+void xcr_cache_free(void *c)
+{
+	delete (XCodecCache *)c;
+}
+
+/* mode 0: fresh XCodecMemoryCache per chunk; mode 1: one cache + one encoder
+ * for the whole batch (tack's loop); mode 2: RefNullCache (tack -N).
+ * cache may carry a pre-state for mode 1 (NULL = a fresh one). */
+int xcr_encode_batch(void *cache, const uint8_t *in, const uint64_t *off, const uint32_t *len, uint32_t n,
+                     int mode, uint8_t *out, const uint64_t *out_off, uint64_t *out_len)
+{
+	UUID uuid;
+	XCodecCache *stream_cache = (XCodecCache *)cache;
+	bool own = false;
+	if (mode == 1 && stream_cache == NULL) {
+		stream_cache = new XCodecMemoryCache(uuid);
+		own = true;
+	}
+	if (mode == 2)
+		stream_cache = new RefNullCache(uuid);
+	XCodecEncoder *stream_enc = (mode != 0) ? new XCodecEncoder(stream_cache) : NULL;
+	int rc = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		Buffer input, output;
+		input.append(in + off[i], len[i]);
+		if (mode == 0) {
+			XCodecMemoryCache c(uuid);
+			XCodecEncoder e(&c);
+			e.encode(&output, &input);
+		} else {
+			stream_enc->encode(&output, &input);
+		}
+		uint64_t r = drain(&output, out + out_off[i], 2 * (uint64_t)len[i] + 16);
+		if (r == ~(uint64_t)0) {
+			rc = -1;
+			break;
+		}
+		out_len[i] = r;
+	}
+	delete stream_enc;
+	if (own || mode == 2)
+		delete stream_cache;
+	return rc;
+}
+
+/* One XCodecDecoder::decode over a whole buffer with cache `cache`
+ * (tack -d, programs/tack/tack.cc:329-359).  Returns 1/0 like decode(),
+ * -1 on overflow; *consumed = bytes parsed; *nunk = unknown hashes. */
+int xcr_decode(void *cache, const uint8_t *x, uint64_t len, uint8_t *out, uint64_t cap,
+               uint64_t *out_len, uint64_t *consumed, uint64_t *unk, uint64_t *nunk, uint64_t unk_max)
+{
+	XCodecDecoder d((XCodecCache *)cache);
+	Buffer input, output;
+	input.append(x, len);
+	std::set<uint64_t> unknown;
+	bool ok = d.decode(&output, &input, unknown);
+	*consumed = len - input.length();
+	*nunk = 0;
+	for (std::set<uint64_t>::const_iterator it = unknown.begin(); it != unknown.end() && *nunk < unk_max; ++it)
+		unk[(*nunk)++] = *it;
+	uint64_t r = drain(&output, out, cap);
+	if (r == ~(uint64_t)0)
+		return -1;
+	*out_len = r;
+	return ok ? 1 : 0;
+}
+
+}
