@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""XCodec encode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 4096 x 64 KiB chunks of
+the survey generator (seed 0xC2, 50 % duplicate 2 KiB segments), each chunk
+one independent XCodecEncoder::encode call with its own fresh
+XCodecMemoryCache (XCG_SEM_INDEPENDENT).  A step = one batched encode launch
+over all chunks; inputs, offsets and output slots are resident in HBM before
+the timed region.  Output is bit-exact with the reference encoder (checked
+against the CPU oracle on a sample every run).
+
+Multi-GPU (torchrun, one rank per GPU): every rank encodes its own 4096-chunk
+shard (seed 0xC2 + rank) with no collective in the timed loop -> weak scaling.
+
+rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CHUNK = 65536
+NCHUNKS = 4096
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--chunks', type=int, default=NCHUNKS)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-passes', type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(data: np.ndarray, offs, lens, passes: int):
+    """Reference XCodecEncoder (oracle/_ref, compiled from the reference
+    sources) on this host's cores: contiguous chunk shards, one thread each,
+    independent-chunk semantics (same output as the GPU run)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.lib import Oracle
+    kind = 'reference'
+    try:
+        o = Oracle(ref=True)
+    except FileNotFoundError:
+        o, kind = Oracle(), 'port'
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = offs.size
+    shards = np.array_split(np.arange(n), threads)
+
+    def run(idx):
+        if idx.size:
+            o.encode_batch(data, offs[idx], lens[idx], mode=0)
+
+    total = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        for _ in range(passes):
+            list(ex.map(run, shards))
+            total += int(lens.astype(np.int64).sum())
+    dt = time.perf_counter() - t0
+    gib = total / 2**30
+    return {'value': round(gib / dt, 4), 'unit': 'GiB/s', 'cores': threads, 'kind': kind,
+            'sample': f'{passes} passes over the full {n} x 64 KiB batch ({total / 2**20:.0f} MiB), '
+                      f'{threads} threads x contiguous shards, fresh XCodecMemoryCache per chunk; {dt:.1f} s wall'}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device('cuda', torch.cuda.current_device())
+
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+
+    n = args.chunks
+    data = np.frombuffer(synth.stream(0xC2 + rank, n * CHUNK, 50, 0), dtype=np.uint8)
+    offs, lens = synth.chunks_of(data.tobytes(), CHUNK)
+    bounds = 2 * lens.astype(np.uint64) + 16
+    oo = np.zeros(n, dtype=np.uint64)
+    oo[1:] = np.cumsum(bounds)[:-1]
+
+    d_in = torch.from_numpy(data.copy()).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_oo = torch.from_numpy(oo.view(np.int64)).to(dev)
+    d_out = torch.empty(int(bounds.sum()), dtype=torch.uint8, device=dev)
+    d_ol = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_st = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+    ctx = Context(dev.index)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.status()
+
+    # Parity check of this run's output against the CPU oracle (sampled chunks).
+    from oracle.lib import Oracle
+    ol = d_ol.cpu().numpy()
+    sample = np.unique(np.linspace(0, n - 1, 16).astype(np.int64))
+    exp = Oracle().encode_batch(data, offs[sample], lens[sample], mode=0)
+    outh = d_out.cpu().numpy()
+    for k, i in enumerate(sample):
+        got = outh[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()
+        if got != exp[k]:
+            raise SystemExit(f'PARITY FAILURE on chunk {i}')
+    out_bytes = int(ol.sum())
+    in_bytes = int(lens.astype(np.int64).sum())
+
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP events on the launch stream
+    ctx.status()
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(in_bytes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(tot, op=torch.distributed.ReduceOp.SUM)
+    wall = float(t.item())
+    total_bytes = float(tot.item()) * args.steps
+    value = total_bytes / 2**30 / wall
+
+    if rank == 0:
+        achieved = (in_bytes + out_bytes) / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        line = {
+            'metric': 'XCodec encode GiB/s device-resident, batched 64 KiB chunks, 1/2/4/8 GPU',
+            'value': round(value, 3),
+            'unit': 'GiB/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(wall * 1e3 / args.steps, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'u8',
+            'data': 'synthetic (survey splitmix64 generator, seed 0xC2+rank, 50% duplicate 2 KiB segments)',
+            'config': {'workload': 'C2: 4096 x 64 KiB independent chunks per GPU, 50% dup segments, '
+                                   'fresh XCodecMemoryCache per chunk (XCG_SEM_INDEPENDENT)',
+                       'chunks_per_gpu': n, 'chunk_bytes': CHUNK, 'out_in_ratio': round(out_bytes / in_bytes, 5),
+                       'parallelism': f'dp{world} (shard per GPU, no collective)'},
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / PEAK_HBM_GBS, 5), 'traffic': traffic,
+                         'kernel': 'encode_independent_kernel', 'kernel_ms': round(kern_ms, 4),
+                         'algorithmic_bytes_per_launch': in_bytes + out_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_passes)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

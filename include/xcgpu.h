@@ -1,0 +1,107 @@
+/*
+ * xcgpu.h -- C ABI of the MI355X-native XCodec engine (libxcgpu.so).
+ *
+ * Plain pointers and sizes only.  Every `d_` pointer is device memory (HBM)
+ * of the context's device; `stream` is a hipStream_t passed as void* (NULL =
+ * the default stream).  Functions return 0 (XCG_OK) or a negative XCG_E*
+ * status; no exceptions cross the ABI.  One context per host thread, or
+ * external locking -- the reference calls its codec under
+ * XCodecPipePair::mtx_ (xcodec/xcodec_pipe_pair.h:45) from one EventThread.
+ *
+ * Reference interfaces replaced (paths relative to wanproxy's tree):
+ *   xcg_ctx_create / xcg_ctx_destroy
+ *       XCodecEncoder::XCodecEncoder(XCodecCache *)   xcodec/xcodec_encoder.cc:40-46
+ *       XCodecMemoryCache(const UUID&, size_t)         xcodec/xcodec_cache.h:277-288
+ *       XCodecCache::out_of_band()                     xcodec/xcodec_cache.h:89
+ *   xcg_encode_batch / xcg_encode_host
+ *       void XCodecEncoder::encode(Buffer *output, Buffer *input,
+ *                                  std::map<uint64_t, BufferSegment *> *refmap)
+ *                                                      xcodec/xcodec_encoder.h:42,
+ *                                                      xcodec/xcodec_encoder.cc:74-274
+ *       (one encode() call per chunk, exactly as tack / XCodecPipePair issue
+ *        them: programs/tack/tack.cc:308-321, xcodec/xcodec_pipe_pair.cc:596-630)
+ *   xcg_window_hashes
+ *       XCodecHash::{add,roll,mix}                     xcodec/xcodec_hash.h:93-164
+ *   xcg_segment_hashes
+ *       XCodecHash::hash per 2048-byte segment          xcodec/xcodec_hash.h:166-174
+ *       (tack -h, programs/tack/tack.cc:368-414)
+ */
+#ifndef XCGPU_H
+#define XCGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XCG_SEGMENT_LENGTH 2048u   /* XCODEC_SEGMENT_LENGTH, xcodec/xcodec.h:87 */
+
+/* Context / call flags. */
+#define XCG_FLAG_OOB 0x1u          /* out-of-band declarations (F1 02 BE64 instead of
+                                      F1 01 + data): XCodecCache::out_of_band() == true,
+                                      xcodec/xcodec_encoder.cc:44,288-295 */
+#define XCG_FLAG_NULLCACHE 0x2u    /* lookups always miss, enter is a no-op: tack -N's
+                                      TackNullCache, programs/tack/tack.cc:70-101 */
+
+/* Batch semantics. */
+#define XCG_SEM_INDEPENDENT 0      /* chunk i = one encode() with a fresh, empty
+                                      XCodecMemoryCache (no cross-chunk state) */
+
+/* Status codes. */
+#define XCG_OK 0
+#define XCG_EHIP (-5)              /* a HIP runtime call failed */
+#define XCG_ENOMEM (-12)
+#define XCG_EINVAL (-22)
+#define XCG_EOVERFLOW (-75)        /* internal table overflow (reported, never silent) */
+#define XCG_ENOTSUP (-95)
+
+typedef struct xcg_ctx xcg_ctx;
+
+/* Library build / version string. */
+const char *xcg_version(void);
+const char *xcg_strerror(int status);
+
+/* Worst-case encoded size of one encode() call over `len` input bytes:
+ * every byte literal and 0xF1 (each escaped to two bytes). */
+uint64_t xcg_encode_bound(uint32_t len);
+
+int xcg_ctx_create(int device, uint32_t flags, xcg_ctx **out);
+void xcg_ctx_destroy(xcg_ctx *ctx);
+
+/*
+ * Encode n chunks in one launch.  Chunk i is d_in[d_chunk_off[i] ..
+ * d_chunk_off[i] + d_chunk_len[i]); its encoding (bit-exact with one
+ * XCodecEncoder::encode call over it) is written to d_out + d_out_off[i], which
+ * must have room for xcg_encode_bound(d_chunk_len[i]) bytes; its length goes to
+ * d_out_len[i].  max_chunk_len bounds every d_chunk_len[i] (<= 512 KiB, the
+ * XCodecPipePair frame cap, xcodec/xcodec_pipe_pair.cc:596-604).
+ * d_stats (nullable): 4 u32 per chunk {EXTRACT or OOB declarations, REFs,
+ * hash collisions, pieces}.  Asynchronous on `stream`.
+ */
+int xcg_encode_batch(xcg_ctx *ctx, int semantics, const uint8_t *d_in, const uint64_t *d_chunk_off,
+                     const uint32_t *d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t *d_out,
+                     const uint64_t *d_out_off, uint64_t *d_out_len, uint32_t *d_stats, void *stream);
+
+/* Synchronous host-memory convenience over xcg_encode_batch (copies in, encodes,
+ * copies out, checks the internal status word).  h_out_off[i] slots as above. */
+int xcg_encode_host(xcg_ctx *ctx, int semantics, const uint8_t *h_in, uint64_t in_len,
+                    const uint64_t *h_chunk_off, const uint32_t *h_chunk_len, uint32_t n, uint8_t *h_out,
+                    uint64_t out_cap, const uint64_t *h_out_off, uint64_t *h_out_len);
+
+/* Status word of the context (sticky; nonzero = an internal overflow happened
+ * in an earlier asynchronous call).  Synchronises the context's device. */
+int xcg_ctx_status(xcg_ctx *ctx);
+
+/* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for
+ * s in [0, len - 2048]. */
+int xcg_window_hashes(xcg_ctx *ctx, const uint8_t *d_x, uint64_t len, uint64_t *d_hash, void *stream);
+
+/* tack -h: XCodecHash::hash of each whole 2048-byte segment, big-endian u64. */
+int xcg_segment_hashes(xcg_ctx *ctx, const uint8_t *d_x, uint64_t len, uint64_t *d_hash_be, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XCGPU_H */

@@ -1,0 +1,29 @@
+"""Build libxcgpu.so in-tree for gfx950 (hipcc; no JIT cache, so the .so
+travels with the repository snapshot to the GPU box)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_hash.hip']
+OUT = os.path.join(HERE, 'libxcgpu.so')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    srcs = [os.path.join(HERE, s) for s in SRCS]
+    deps = srcs + [os.path.join(HERE, 'csrc/xcg_device.h'), os.path.join(HERE, '..', 'include', 'xcgpu.h')]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+        return OUT
+    cmd = [HIPCC, '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
+           '-o', OUT + '.tmp'] + srcs
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.run(cmd, check=True, cwd=HERE)
+    os.replace(OUT + '.tmp', OUT)
+    return OUT
+
+
+if __name__ == '__main__':
+    print(build_lib(force=True, verbose=True))

@@ -1,0 +1,526 @@
+// XCodec encoder, MI355X (gfx950) HIP kernels.
+//
+// Restates XCodecEncoder::encode (xcodec/xcodec_encoder.cc:74-274) for a batch
+// of independent encode() calls: one wave64 per chunk, so a 64 KiB chunk (the
+// unit tack and wanproxy hand to encode(), programs/tack/tack.cc:308-321,
+// io/io_system_handle.cc:39) is parsed by 64 lanes with no inter-wave sync.
+//
+// The reference walks every byte offset sequentially: roll the 2048-byte
+// XCodecHash (xcodec_hash.h:93-163), probe the cache (find_reference,
+// xcodec_encoder.cc:374-416), and run a greedy candidate / declare / reference
+// state machine (:183-248).  Here a chunk is parsed in PIECES of 2048 window
+// positions:
+//
+//   1. vector phase: lane i rolls the hash over the 32 positions
+//      [p + 32 i, p + 32 i + 32) -- its start sums come from wave prefix scans
+//      over 32-byte segment sums -- and probes a per-wave LDS fingerprint table
+//      of the declarations made so far, producing a 32-bit event mask;
+//   2. resolve phase (wave-uniform): the state machine jumps from event to
+//      event through those masks.  Within 2048 positions of the parse point at
+//      most ONE declaration can become visible (the candidate pending at piece
+//      start, visible from cand + 2048), which the vector phase covers with a
+//      gated compare, so every event the masks miss is a true miss.
+//
+// Events are re-checked exactly (full 64-bit hash, then byte compare against
+// the declared segment) before a REF or a collision skip is emitted, so the
+// fingerprint table can be approximate without affecting output.  Output ops
+// (ESCAPE / EXTRACT / REF, xcodec_encoder.cc:276-372) are written by the whole
+// wave as they are resolved, into the chunk's output slot.
+#include "xcg_device.h"
+#include "../../include/xcgpu.h"
+
+namespace xcg {
+
+// Per-wave LDS state: a 2-slot-bucket fingerprint table over the chunk's own
+// declarations (the XCodecMemoryCache of an independent encode() call,
+// xcodec_cache.h:245-365) plus the exact records it points to.
+template <int LOGNB, int MAXD>
+struct WaveTable {
+  static constexpr int NB = 1 << LOGNB;
+  uint32_t fp[2 * NB];        // slot fingerprint (lo | 1), 0 = empty
+  uint16_t idx[2 * NB];       // declaration index of the slot
+  uint32_t rlo[MAXD], rhi[MAXD], rc[MAXD];  // exact hash + chunk position
+  uint32_t ovf_fp[8];         // keys whose bucket was full
+  uint32_t ovf_idx[8];
+};
+
+struct EncParams {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint32_t flags;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint64_t* out_len;
+  uint32_t* stats;     // optional: per chunk {n_extract, n_ref, n_collision, n_pieces}
+  int32_t* status;     // optional: nonzero on internal overflow
+};
+
+__device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t bh, int logNB) {
+  // bh = bits_hash; only bits 0..27 survive mix()'s << 36, and only bits
+  // 5..5+logNB (< 28) are used here, so bh and (hi >> 4) give the same bucket.
+  return ((lo ^ bh) >> 5) & ((1u << logNB) - 1u);
+}
+
+// ------------------------------------------------------------------ emission
+
+// Copy n bytes src -> dst (any alignment), whole wave.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const int l = lane_id();
+  for (uint32_t base = 0; base < n; base += 1024) {
+    uint32_t off = base + 16u * l;
+    if (off + 16 <= n) {
+      *(u32x4_u*)(dst + off) = *(const u32x4_u*)(src + off);
+    } else if (off < n) {
+      for (uint32_t k = off; k < n; ++k) dst[k] = src[k];
+    }
+  }
+}
+
+// encode_escape (xcodec_encoder.cc:315-340): x[a..b) with F1 -> F1 00.
+// Returns bytes written (uniform).
+__device__ __noinline__ uint32_t wave_escape(uint8_t* dst, const uint8_t* x, uint32_t a, uint32_t b) {
+  const int l = lane_id();
+  const uint32_t n = b - a;
+  uint32_t written = 0;
+  for (uint32_t base = 0; base < n; base += 1024) {
+    uint32_t off = base + 16u * l;
+    uint32_t cnt = off < n ? min(16u, n - off) : 0u;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (cnt == 16) {
+      v = *(const u32x4_u*)(x + a + off);
+    } else {
+      for (uint32_t k = 0; k < cnt; ++k) v[k >> 2] |= (uint32_t)x[a + off + k] << (8 * (k & 3));
+    }
+    uint32_t nm = count_magic(v[0]) + count_magic(v[1]) + count_magic(v[2]) + count_magic(v[3]);
+    if (cnt < 16) {
+      // padding bytes are 0 (never magic) unless the chunk byte was; recount exactly
+      nm = 0;
+      for (uint32_t k = 0; k < cnt; ++k) nm += byte_of(v[k >> 2], k & 3) == MAGIC;
+    }
+    uint32_t olen = cnt + nm;
+    uint32_t incl = wave_incl_scan(olen);
+    uint32_t pos = written + incl - olen;
+    if (nm == 0) {
+      if (cnt == 16) {
+        *(u32x4_u*)(dst + pos) = v;
+      } else {
+        for (uint32_t k = 0; k < cnt; ++k) dst[pos + k] = (uint8_t)byte_of(v[k >> 2], k & 3);
+      }
+    } else {
+      uint32_t o = pos;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        uint32_t c = byte_of(v[k >> 2], k & 3);
+        dst[o++] = (uint8_t)c;
+        if (c == MAGIC) dst[o++] = (uint8_t)OP_ESCAPE;
+      }
+    }
+    written += readlane(incl, 63);
+  }
+  return written;
+}
+
+// F1 02 BE64(hash): encode_reference, xcodec_encoder.cc:357-360.
+__device__ __forceinline__ void wave_put_ref(uint8_t* dst, uint32_t lo, uint32_t hi) {
+  const int l = lane_id();
+  if (l < 10) {
+    uint32_t v;
+    if (l == 0) v = MAGIC;
+    else if (l == 1) v = OP_REF;
+    else if (l < 6) v = hi >> (8 * (5 - l));
+    else v = lo >> (8 * (9 - l));
+    dst[l] = (uint8_t)v;
+  }
+}
+
+// ------------------------------------------------------------ exact checks
+
+// XCodecHash::hash of the 2048-byte window at w (xcodec_hash.h:166-174),
+// whole wave: lane l sums bytes [16l, 16l+16) and [1024+16l, +16).
+__device__ __noinline__ void wave_window_hash(const uint8_t* w, uint32_t& lo_out, uint32_t& hi_out) {
+  const int l = lane_id();
+  uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t k0 = 1024u * h + 16u * l;
+    u32x4 v = *(const u32x4_u*)(w + k0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      uint32_t x = byte_of(v[k >> 2], k & 3);
+      uint32_t f = ffbl(x) + 1u;
+      uint32_t wt = 2048u - (k0 + k);
+      X1 += x; X2 += wt * x; F1 += f; F2 += wt * f;
+    }
+  }
+  X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
+  lo_out = (X1 << 20) + X2 + CLO;
+  hi_out = ((F1 << 16) + F2) << 4;
+}
+
+// Byte-equality of two 2048-byte segments (BufferSegment::equal in
+// find_reference, xcodec_encoder.cc:383-390), whole wave.
+__device__ __noinline__ bool wave_equal2048(const uint8_t* a, const uint8_t* b) {
+  const int l = lane_id();
+  bool ok = true;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t k0 = 1024u * h + 16u * l;
+    u32x4 va = *(const u32x4_u*)(a + k0);
+    u32x4 vb = *(const u32x4_u*)(b + k0);
+    ok = ok && va[0] == vb[0] && va[1] == vb[1] && va[2] == vb[2] && va[3] == vb[3];
+  }
+  return ballot(!ok) == 0;
+}
+
+// ------------------------------------------------------------ vector phase
+
+struct Piece {
+  u32x4 a0, a1;   // bytes [q0, q0+32): the windows' leaving bytes
+  u32x4 b0, b1;   // bytes [q0+2048, q0+2080): the entering bytes
+  // segment sums of the A and B segments (j = offset within the segment)
+  uint32_t sxa, sqxa, sfa, sqfa;
+  uint32_t sxb, sqxb, sfb, sqfb;
+};
+
+__device__ __forceinline__ void seg_sums(const u32x4 d0, const u32x4 d1, uint32_t& sx, uint32_t& sqx,
+                                         uint32_t& sf, uint32_t& sqf) {
+  const uint32_t d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+  sx = 0; sqx = 0; sf = 0; sqf = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t wts = (4u * k) | ((4u * k + 1) << 8) | ((4u * k + 2) << 16) | ((4u * k + 3) << 24);
+    sx = __builtin_amdgcn_udot4(d[k], 0x01010101u, sx, false);
+    sqx = __builtin_amdgcn_udot4(d[k], wts, sqx, false);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      uint32_t f = ffbl(byte_of(d[k], b)) + 1u;
+      sf += f;
+      sqf += (4u * k + b) * f;
+    }
+  }
+}
+
+// Roll the hash over the lane's 32 positions; bit j of the result is set when
+// position q0 + j is a possible cache hit.  C0: the pending candidate c0 is
+// not in the table yet and becomes visible at local index jvis.  OVF: probe
+// the (rare) overflow keys too.
+template <int LOGNB, bool C0, bool OVF>
+__device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint32_t X2c, uint32_t F1,
+                                               uint32_t F2, const uint32_t* fptab, uint32_t c0fp, int jvis,
+                                               const uint32_t* ovf, uint32_t& lo0, uint32_t& bh0) {
+  const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
+  const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
+  uint32_t o[8];
+  if (OVF) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = ovf[k];
+  }
+  uint32_t ev = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint32_t lo = (X1 << 20) + X2c;
+    const uint32_t bh = (F1 << 16) + F2;
+    if (j == 0) { lo0 = lo; bh0 = bh; }
+    const uint32_t fp = lo | 1u;
+    const uint32_t b = bucket_of(lo, bh, LOGNB);
+    const uint2 e = *(const uint2*)(fptab + 2 * b);
+    bool hit = (e.x == fp) | (e.y == fp);
+    if (C0) hit |= (fp == c0fp) & (j >= jvis);
+    if (OVF) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) hit |= (o[k] == fp);
+    }
+    ev |= hit ? (1u << j) : 0u;
+    if (j < 31) {
+      const uint32_t xo = byte_of(xa[j >> 2], j & 3);
+      const uint32_t xn = byte_of(xb[j >> 2], j & 3);
+      const uint32_t ro = ffbl(xo), rn = ffbl(xn);
+      X1 = X1 + xn - xo;                         // RollingHash::roll, xcodec_hash.h:57-70
+      X2c = X2c + X1 - (xo << 11);
+      F1 = F1 + rn - ro;                         // (ffbl+1) - (ffbl+1)
+      F2 = F2 + F1 - (ro << 11) - 2048u;         // - 2048 * ffs(dead)
+    }
+  }
+  return ev;
+}
+
+// ------------------------------------------------------------------ kernel
+
+template <int LOGNB, int MAXD>
+__global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) {
+  __shared__ WaveTable<LOGNB, MAXD> tabs[4];
+  constexpr int NB = 1 << LOGNB;
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  WaveTable<LOGNB, MAXD>& T = tabs[wv];
+
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const int L = (int)prm.chunk_len[chunk];
+  uint8_t* const out = prm.out + prm.out_off[chunk];
+  const bool oob = (prm.flags & XCG_FLAG_OOB) != 0;
+  const bool nullcache = (prm.flags & XCG_FLAG_NULLCACHE) != 0;
+  uint32_t olen = 0;
+  uint32_t n_extract = 0, n_ref = 0, n_coll = 0, n_pieces = 0;
+
+  if (L < SEG) {                                   // xcodec_encoder.cc:77-83
+    if (L > 0) olen = wave_escape(out, x, 0, (uint32_t)L);
+    if (l == 0) prm.out_len[chunk] = olen;
+    return;
+  }
+
+  for (int k = l; k < 2 * NB; k += 64) T.fp[k] = 0u;
+  uint32_t ndecl = 0, novf = 0;
+
+  const int last = L - SEG;                        // last window start
+  const int mis = (int)(reinterpret_cast<uintptr_t>(x) & 15u);
+  int s = 0, base = 0;
+  bool have_cand = false;
+  int cand = 0;
+  uint32_t cand_lo = 0, cand_hi = 0;
+  bool c0_in_table = true;                         // pending candidate already inserted?
+
+  Piece P;
+  int p_prev = INT32_MIN;
+  uint32_t totXA = 0, totTA = 0, totFA = 0, totTFA = 0;   // sums over the A half (carried)
+
+  // Insert a declaration into the LDS table (XCodecMemoryCache::enter,
+  // xcodec_cache.h:303-325) -- by lane 0, visible to later LDS reads of the
+  // wave (LDS ops of one wave complete in order).
+  auto insert = [&](uint32_t lo, uint32_t hi, uint32_t c) {
+    const uint32_t d = ndecl++;
+    const uint32_t fp = lo | 1u;
+    const uint32_t b = bucket_of(lo, hi >> 4, LOGNB);
+    const uint32_t s0 = readfirst(T.fp[2 * b]), s1 = readfirst(T.fp[2 * b + 1]);
+    if (l == 0) {
+      T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
+      if (s0 == 0u) { T.fp[2 * b] = fp; T.idx[2 * b] = (uint16_t)d; }
+      else if (s1 == 0u) { T.fp[2 * b + 1] = fp; T.idx[2 * b + 1] = (uint16_t)d; }
+      else if (novf < 8) { T.ovf_fp[novf] = fp; T.ovf_idx[novf] = d; }
+    }
+    if (s0 != 0u && s1 != 0u) {
+      if (novf < 8) ++novf;
+      else if (l == 0 && prm.status) atomicOr(prm.status, 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  // Exact lookup: declaration index whose hash is (lo, hi), or -1.
+  auto lookup = [&](uint32_t lo, uint32_t hi) -> int {
+    const uint32_t fp = lo | 1u;
+    const uint32_t b = bucket_of(lo, hi >> 4, LOGNB);
+    int found = -1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (readfirst(T.fp[2 * b + k]) == fp) {
+        const uint32_t d = readfirst(T.idx[2 * b + k]);
+        if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
+      }
+    }
+    for (uint32_t k = 0; k < novf && found < 0; ++k) {
+      if (readfirst(T.ovf_fp[k]) == fp) {
+        const uint32_t d = readfirst(T.ovf_idx[k]);
+        if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
+      }
+    }
+    return found;
+  };
+
+  // encode_declaration (xcodec_encoder.cc:276-313).
+  auto declare = [&]() {
+    if (cand > base) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)cand);
+    if (!nullcache && !c0_in_table) insert(cand_lo, cand_hi, (uint32_t)cand);
+    if (oob) {
+      wave_put_ref(out + olen, cand_lo, cand_hi);           // :288-295
+      olen += 10;
+    } else {
+      if (l < 2) out[olen + l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);   // :300-302
+      wave_copy(out + olen + 2, x + cand, SEG);
+      olen += 2 + SEG;
+    }
+    ++n_extract;
+    base = cand + SEG;
+    have_cand = false;
+    c0_in_table = true;
+  };
+
+  while (s <= last) {
+    // ---- piece geometry: q0 = p + 32 lane, loads 16-byte aligned in memory
+    const int p = s - (int)(((uint32_t)mis + (uint32_t)s) & 15u);
+    const int q0 = p + 32 * l;
+    const bool contig = (p == p_prev + SEG);
+    ++n_pieces;
+    if (contig) {
+      P.a0 = P.b0; P.a1 = P.b1;
+      P.sxa = P.sxb; P.sqxa = P.sqxb; P.sfa = P.sfb; P.sqfa = P.sqfb;
+    } else {
+      P.a0 = load16_guarded(x, q0, L);
+      P.a1 = load16_guarded(x, q0 + 16, L);
+      seg_sums(P.a0, P.a1, P.sxa, P.sqxa, P.sfa, P.sqfa);
+    }
+    P.b0 = load16_guarded(x, q0 + SEG, L);
+    P.b1 = load16_guarded(x, q0 + SEG + 16, L);
+    seg_sums(P.b0, P.b1, P.sxb, P.sqxb, P.sfb, P.sqfb);
+    p_prev = p;
+
+    // ---- start sums of lane l's first window (positions relative to p)
+    const uint32_t qa = 32u * (uint32_t)l, qb = 2048u + 32u * (uint32_t)l;
+    const uint32_t ta = qa * P.sxa + P.sqxa, tb = qb * P.sxb + P.sqxb;
+    const uint32_t tfa = qa * P.sfa + P.sqfa, tfb = qb * P.sfb + P.sqfb;
+    if (!contig) {
+      totXA = wave_sum(P.sxa); totTA = wave_sum(ta);
+      totFA = wave_sum(P.sfa); totTFA = wave_sum(tfa);
+    }
+    const uint32_t dx = P.sxb - P.sxa, dt = tb - ta, df = P.sfb - P.sfa, dtf = tfb - tfa;
+    const uint32_t ix = wave_incl_scan(dx), it = wave_incl_scan(dt);
+    const uint32_t ifv = wave_incl_scan(df), itf = wave_incl_scan(dtf);
+    const uint32_t X1 = totXA + ix - dx;
+    const uint32_t TT = totTA + it - dt;
+    const uint32_t F1 = totFA + ifv - df;
+    const uint32_t TF = totTFA + itf - dtf;
+    const uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
+    const uint32_t F2 = (2048u + qa) * F1 - TF;
+    // Next piece's A half (if contiguous) is this B half, shifted by 2048.
+    const uint32_t totXB = totXA + readlane(ix, 63);
+    const uint32_t totTB = totTA + readlane(it, 63) - 2048u * totXB;
+    const uint32_t totFB = totFA + readlane(ifv, 63);
+    const uint32_t totTFB = totTFA + readlane(itf, 63) - 2048u * totFB;
+
+    // ---- vector phase
+    uint32_t ev = 0, lo0 = 0, bh0 = 0;
+    const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
+    if (!nullcache) {
+      // c0 = the pending candidate; once it is visible from the piece start on,
+      // it goes straight into the table (a REF can no longer cancel it).
+      if (have_cand && !c0_in_table && cand + SEG <= p) {
+        insert(cand_lo, cand_hi, (uint32_t)cand);
+        c0_in_table = true;
+      }
+      const bool c0 = have_cand && !c0_in_table;
+      const int vis = cand + SEG;
+      const int jvis = c0 ? (vis - q0) : 0;
+      const uint32_t c0fp = cand_lo | 1u;
+      uint32_t ovfv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ovfv[k] = (uint32_t)k < novf ? readfirst(T.ovf_fp[k]) : 0u;
+      if (c0) {
+        if (novf) ev = roll_probe<LOGNB, true, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
+        else ev = roll_probe<LOGNB, true, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
+      } else {
+        if (novf) ev = roll_probe<LOGNB, false, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
+        else ev = roll_probe<LOGNB, false, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
+      }
+      // positions past the last window are not positions
+      const int nvalid = pe - q0;
+      if (nvalid <= 0) ev = 0;
+      else if (nvalid < 32) ev &= (1u << nvalid) - 1u;
+    } else {
+      lo0 = (X1 << 20) + X2c;
+      bh0 = (F1 << 16) + F2;
+    }
+
+    // ---- resolve phase (wave-uniform)
+    auto next_event = [&](int from) -> int {
+      const int rel = from - p;
+      const int ls = rel >> 5, bs = rel & 31;
+      uint32_t m = l < ls ? 0u : (l == ls ? (ev & (0xFFFFFFFFu << bs)) : ev);
+      const uint64_t bal = ballot(m != 0u);
+      if (bal == 0) return INT32_MAX;
+      const int lw = __builtin_ctzll(bal);
+      const uint32_t mm = readlane(m, lw);
+      return p + 32 * lw + __builtin_ctz(mm);
+    };
+    auto hash_at = [&](int pos, uint32_t& lo, uint32_t& hi) {
+      const int rel = pos - p;
+      if ((rel & 31) == 0) {
+        lo = readlane(lo0, rel >> 5);
+        hi = readlane(bh0, rel >> 5) << 4;
+      } else {
+        wave_window_hash(x + pos, lo, hi);
+      }
+    };
+
+    while (s < pe) {
+      if (have_cand && cand + SEG <= s) declare();            // :183-190
+      const int e = nullcache ? INT32_MAX : next_event(s);
+      if (e == s) {
+        // Exact re-check of the probe (find_reference, :374-416).
+        uint32_t lo, hi;
+        wave_window_hash(x + s, lo, hi);
+        const int d = lookup(lo, hi);
+        if (d >= 0) {
+          if (wave_equal2048(x + readfirst(T.rc[d]), x + s)) {
+            if (s > base) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)s);
+            wave_put_ref(out + olen, lo, hi);                 // encode_reference :342-372
+            olen += 10;
+            ++n_ref;
+            base = s + SEG;
+            s = base;
+            have_cand = false;                                // :208
+            c0_in_table = true;
+            continue;
+          }
+          ++n_coll;                                           // collision, :390-406 / :215-216
+          ++s;
+          continue;
+        }
+        // fingerprint false positive: an ordinary miss
+        if (!have_cand) {
+          have_cand = true; cand = s; cand_lo = lo; cand_hi = hi; c0_in_table = false;
+        }
+        ++s;
+        continue;
+      }
+      if (!have_cand) {                                       // :246-248
+        hash_at(s, cand_lo, cand_hi);
+        have_cand = true;
+        cand = s;
+        c0_in_table = false;
+        ++s;
+        continue;
+      }
+      // Non-event positions before the next milestone change nothing.
+      s = min(min(e, cand + SEG), pe);
+    }
+    // The table holds every declaration once the piece is done; a still
+    // pending candidate stays out of it until declared.
+    totXA = totXB; totTA = totTB; totFA = totFB; totTFA = totTFB;
+  }
+
+  if (have_cand) declare();                                   // :257-261
+  if (base < L) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
+  if (l == 0) {
+    prm.out_len[chunk] = olen;
+    if (prm.stats) {
+      prm.stats[4 * chunk + 0] = n_extract;
+      prm.stats[4 * chunk + 1] = n_ref;
+      prm.stats[4 * chunk + 2] = n_coll;
+      prm.stats[4 * chunk + 3] = n_pieces;
+    }
+  }
+}
+
+template __global__ void encode_independent_kernel<9, 72>(EncParams);
+template __global__ void encode_independent_kernel<11, 264>(EncParams);
+
+}  // namespace xcg
+
+extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t* d_chunk_off,
+                                             const uint32_t* d_chunk_len, uint32_t n, uint32_t max_chunk_len,
+                                             uint32_t flags, uint8_t* d_out, const uint64_t* d_out_off,
+                                             uint64_t* d_out_len, uint32_t* d_stats, int32_t* d_status,
+                                             hipStream_t stream) {
+  if (n == 0) return 0;
+  xcg::EncParams prm{d_in, d_chunk_off, d_chunk_len, n, flags, d_out, d_out_off, d_out_len, d_stats, d_status};
+  dim3 grid((n + 3) / 4), block(256);
+  if (max_chunk_len <= (1u << 17)) {
+    hipLaunchKernelGGL((xcg::encode_independent_kernel<9, 72>), grid, block, 0, stream, prm);
+  } else if (max_chunk_len <= (1u << 19)) {
+    hipLaunchKernelGGL((xcg::encode_independent_kernel<11, 264>), grid, block, 0, stream, prm);
+  } else {
+    return -22;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

@@ -1,0 +1,188 @@
+"""ctypes binding of libxcgpu.so (include/xcgpu.h) plus a host-side mirror of
+the reference's XCodec encoder interface.
+
+The product path is the HIP library; this module only moves buffers (torch is
+used for device memory and streams) and never falls back to a CPU codec: if
+the library or a GPU is missing, every entry point raises.
+
+Reference interface mirrored (wanproxy tree):
+  XCodecEncoder(XCodecCache*) / encode(Buffer*, Buffer*)   xcodec/xcodec_encoder.h:40-43
+  XCodecMemoryCache / TackNullCache / out_of_band()         xcodec/xcodec_cache.h:245-365,
+                                                            programs/tack/tack.cc:70-101
+  XCodecHash::hash / mix                                    xcodec/xcodec_hash.h:155-174
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libxcgpu.so')
+SEG = 2048
+
+XCG_FLAG_OOB = 0x1
+XCG_FLAG_NULLCACHE = 0x2
+XCG_SEM_INDEPENDENT = 0
+
+_lib = None
+
+
+class XCGError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libxcgpu.so (after torch, so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- load torch's libamdhip64 first
+    if not os.path.exists(LIB_PATH):
+        raise XCGError(f'{LIB_PATH} missing: run `python -c "import __graft_entry__ as g; g.build()"`')
+    L = C.CDLL(LIB_PATH)
+    vp, u8p, u32p, u64p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.xcg_version.restype = C.c_char_p
+    L.xcg_strerror.restype = C.c_char_p
+    L.xcg_strerror.argtypes = [C.c_int]
+    L.xcg_encode_bound.restype = C.c_uint64
+    L.xcg_encode_bound.argtypes = [C.c_uint32]
+    L.xcg_ctx_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create.restype = C.c_int
+    L.xcg_ctx_destroy.argtypes = [vp]
+    L.xcg_ctx_status.argtypes = [vp]
+    L.xcg_ctx_status.restype = C.c_int
+    L.xcg_encode_batch.argtypes = [vp, C.c_int, u8p, u64p, u32p, C.c_uint32, C.c_uint32, u8p, u64p, u64p, u32p, vp]
+    L.xcg_encode_batch.restype = C.c_int
+    L.xcg_encode_host.argtypes = [vp, C.c_int, u8p, C.c_uint64, u64p, u32p, C.c_uint32, u8p, C.c_uint64, u64p, u64p]
+    L.xcg_encode_host.restype = C.c_int
+    L.xcg_window_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
+    L.xcg_window_hashes.restype = C.c_int
+    L.xcg_segment_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
+    L.xcg_segment_hashes.restype = C.c_int
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise XCGError(f'xcgpu: {lib().xcg_strerror(rc).decode()} ({rc})')
+
+
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def encode_bound(n: int) -> int:
+    return 2 * int(n) + 16
+
+
+class Context:
+    """An XCodecEncoder + cache configuration bound to one GPU."""
+
+    def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False):
+        import torch
+        if not torch.cuda.is_available():
+            raise XCGError('no GPU: the XCodec engine has no CPU path')
+        self.device = device
+        self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
+        h = C.c_void_p()
+        _check(lib().xcg_ctx_create(device, self.flags, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().xcg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def status(self):
+        _check(lib().xcg_ctx_status(self.h))
+
+    # ------------------------------------------------------------- device API
+    def encode_batch_device(self, d_in, d_off, d_len, n, max_len, d_out, d_out_off, d_out_len,
+                            d_stats=None, stream=None, semantics=XCG_SEM_INDEPENDENT):
+        """Raw launch on device tensors (all torch tensors on this device)."""
+        _check(lib().xcg_encode_batch(
+            self.h, semantics, C.c_void_p(d_in.data_ptr()), C.c_void_p(d_off.data_ptr()),
+            C.c_void_p(d_len.data_ptr()), int(n), int(max_len), C.c_void_p(d_out.data_ptr()),
+            C.c_void_p(d_out_off.data_ptr()), C.c_void_p(d_out_len.data_ptr()),
+            C.c_void_p(d_stats.data_ptr()) if d_stats is not None else None, _stream_ptr(stream)))
+
+    def encode_chunks(self, data, offs, lens, with_stats=False):
+        """Encode chunks of host `data` (bytes / np.uint8) on the GPU; returns a
+        list of encoded bytes objects (and per-chunk stats if asked)."""
+        import torch
+        dev = torch.device('cuda', self.device)
+        a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = int(offs.size)
+        if n == 0:
+            return ([], np.zeros((0, 4), np.uint32)) if with_stats else []
+        bounds = 2 * lens.astype(np.uint64) + 16
+        oo = np.zeros(n, dtype=np.uint64)
+        oo[1:] = np.cumsum(bounds)[:-1]
+        d_in = torch.from_numpy(a.copy() if a.size else np.zeros(1, np.uint8)).to(dev)
+        d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        d_oo = torch.from_numpy(oo.view(np.int64)).to(dev)
+        d_out = torch.zeros(int(bounds.sum()), dtype=torch.uint8, device=dev)
+        d_ol = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_st = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+        self.encode_batch_device(d_in, d_off, d_len, n, int(lens.max()), d_out, d_oo, d_ol, d_st)
+        torch.cuda.synchronize(dev)
+        self.status()
+        out = d_out.cpu().numpy()
+        ol = d_ol.cpu().numpy().astype(np.uint64)
+        res = [out[int(oo[i]):int(oo[i] + ol[i])].tobytes() for i in range(n)]
+        if with_stats:
+            return res, d_st.cpu().numpy().view(np.uint32).reshape(n, 4)
+        return res
+
+    def window_hashes(self, data) -> np.ndarray:
+        import torch
+        dev = torch.device('cuda', self.device)
+        a = np.frombuffer(data, dtype=np.uint8)
+        n = max(0, a.size - SEG + 1)
+        if n == 0:
+            return np.zeros(0, np.uint64)
+        d_x = torch.from_numpy(a.copy()).to(dev)
+        d_h = torch.zeros(n, dtype=torch.int64, device=dev)
+        _check(lib().xcg_window_hashes(self.h, C.c_void_p(d_x.data_ptr()), a.size, C.c_void_p(d_h.data_ptr()),
+                                       _stream_ptr(None)))
+        torch.cuda.synchronize(dev)
+        return d_h.cpu().numpy().view(np.uint64)
+
+    def segment_hashes_be(self, data) -> bytes:
+        import torch
+        dev = torch.device('cuda', self.device)
+        a = np.frombuffer(data, dtype=np.uint8)
+        n = a.size // SEG
+        if n == 0:
+            return b''
+        d_x = torch.from_numpy(a.copy()).to(dev)
+        d_h = torch.zeros(n, dtype=torch.int64, device=dev)
+        _check(lib().xcg_segment_hashes(self.h, C.c_void_p(d_x.data_ptr()), a.size, C.c_void_p(d_h.data_ptr()),
+                                        _stream_ptr(None)))
+        torch.cuda.synchronize(dev)
+        return d_h.cpu().numpy().tobytes()
+
+
+class XCodecEncoder:
+    """Mirror of XCodecEncoder for independent encode() calls: each call is one
+    chunk with a fresh XCodecMemoryCache (xcodec_encoder.cc:74-274)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def encode(self, data: bytes) -> bytes:
+        return self.ctx.encode_chunks(data, np.array([0]), np.array([len(data)]))[0]
