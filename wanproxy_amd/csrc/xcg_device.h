@@ -27,6 +27,14 @@ typedef uint32_t __attribute__((aligned(1))) u32_u;
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// A copy of v the optimiser cannot see through: values derived from it are
+// recomputed where used instead of being hoisted and held live across a big
+// loop (register pressure control).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -83,6 +91,18 @@ __device__ __forceinline__ u32x4 load16_guarded(const uint8_t* x, int64_t q, int
     uint32_t b = (i >= 0 && i < len) ? (uint32_t)x[i] : 0u;
     r[k >> 2] |= b << (8 * (k & 3));
   }
+  return r;
+}
+
+// 16 bytes at chunk position q where x + q is 16-byte aligned.  A 16-byte
+// aligned block that overlaps [0, len) lies inside one page of the caller's
+// buffer, so it is loaded whole; blocks wholly outside read as 0.  Bytes
+// outside the chunk only ever enter windows of non-positions (s > len-2048 or
+// s < 0), and a rolling sum removes exactly what it added, so their values
+// never reach a valid window hash.
+__device__ __forceinline__ u32x4 load16_aligned_safe(const uint8_t* x, int q, int len) {
+  u32x4 r = {0u, 0u, 0u, 0u};
+  if (q > -16 && q < len) r = *(const u32x4*)(x + q);
   return r;
 }
 

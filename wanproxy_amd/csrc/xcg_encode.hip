@@ -66,7 +66,7 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t bh, int logN
 // ------------------------------------------------------------------ emission
 
 // Copy n bytes src -> dst (any alignment), whole wave.
-__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+__device__ __noinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
   const int l = lane_id();
   for (uint32_t base = 0; base < n; base += 1024) {
     uint32_t off = base + 16u * l;
@@ -138,7 +138,7 @@ __device__ __forceinline__ void wave_put_ref(uint8_t* dst, uint32_t lo, uint32_t
 
 // XCodecHash::hash of the 2048-byte window at w (xcodec_hash.h:166-174),
 // whole wave: lane l sums bytes [16l, 16l+16) and [1024+16l, +16).
-__device__ __noinline__ void wave_window_hash(const uint8_t* w, uint32_t& lo_out, uint32_t& hi_out) {
+__device__ __noinline__ uint2 wave_window_hash(const uint8_t* w) {
   const int l = lane_id();
   uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
 #pragma unroll
@@ -154,8 +154,7 @@ __device__ __noinline__ void wave_window_hash(const uint8_t* w, uint32_t& lo_out
     }
   }
   X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
-  lo_out = (X1 << 20) + X2 + CLO;
-  hi_out = ((F1 << 16) + F2) << 4;
+  return make_uint2((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4);
 }
 
 // Byte-equality of two 2048-byte segments (BufferSegment::equal in
@@ -171,6 +170,20 @@ __device__ __noinline__ bool wave_equal2048(const uint8_t* a, const uint8_t* b) 
     ok = ok && va[0] == vb[0] && va[1] == vb[1] && va[2] == vb[2] && va[3] == vb[3];
   }
   return ballot(!ok) == 0;
+}
+
+// Call-site wrappers: a non-inlined call returns in VGPRs, which hipcc must
+// treat as divergent; these values are wave-uniform, and saying so keeps the
+// whole parse state machine in SGPRs / scalar branches.
+__device__ __forceinline__ uint32_t escape_u(uint8_t* dst, const uint8_t* x, uint32_t a, uint32_t b) {
+  return readfirst(wave_escape(dst, x, a, b));
+}
+__device__ __forceinline__ uint2 window_hash_u(const uint8_t* w) {
+  const uint2 h = wave_window_hash(w);
+  return make_uint2(readfirst(h.x), readfirst(h.y));
+}
+__device__ __forceinline__ bool equal2048_u(const uint8_t* a, const uint8_t* b) {
+  return readfirst((uint32_t)wave_equal2048(a, b)) != 0u;
 }
 
 // ------------------------------------------------------------ vector phase
@@ -205,42 +218,56 @@ __device__ __forceinline__ void seg_sums(const u32x4 d0, const u32x4 d1, uint32_
 // position q0 + j is a possible cache hit.  C0: the pending candidate c0 is
 // not in the table yet and becomes visible at local index jvis.  OVF: probe
 // the (rare) overflow keys too.
-template <int LOGNB, bool C0, bool OVF>
+template <int LOGNB, bool C0>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint32_t X2c, uint32_t F1,
                                                uint32_t F2, const uint32_t* fptab, uint32_t c0fp, int jvis,
-                                               const uint32_t* ovf, uint32_t& lo0, uint32_t& bh0) {
+                                               const uint32_t* ovf, uint32_t novf, uint32_t& lo0,
+                                               uint32_t& bh0) {
   const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
   const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
-  uint32_t o[8];
-  if (OVF) {
+  uint32_t o[8];   // overflow keys (uniform, SGPRs); novf == 0 almost always
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = ovf[k];
-  }
+  for (int k = 0; k < 8; ++k) o[k] = ovf[k];
   uint32_t ev = 0;
+  // Groups of 4 positions: the sched_barrier keeps hipcc from hoisting all 32
+  // LDS probes (and their operands) at once, which would cost ~100 VGPRs.
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const uint32_t lo = (X1 << 20) + X2c;
-    const uint32_t bh = (F1 << 16) + F2;
-    if (j == 0) { lo0 = lo; bh0 = bh; }
-    const uint32_t fp = lo | 1u;
-    const uint32_t b = bucket_of(lo, bh, LOGNB);
-    const uint2 e = *(const uint2*)(fptab + 2 * b);
-    bool hit = (e.x == fp) | (e.y == fp);
-    if (C0) hit |= (fp == c0fp) & (j >= jvis);
-    if (OVF) {
+  for (int g = 0; g < 8; ++g) {
+    uint32_t fpv[4], bkt[4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) hit |= (o[k] == fp);
+    for (int t = 0; t < 4; ++t) {
+      const int j = 4 * g + t;
+      const uint32_t lo = (X1 << 20) + X2c;
+      const uint32_t bh = (F1 << 16) + F2;
+      if (j == 0) { lo0 = lo; bh0 = bh; }
+      fpv[t] = lo | 1u;
+      bkt[t] = bucket_of(lo, bh, LOGNB);
+      if (j < 31) {
+        const uint32_t xo = byte_of(xa[j >> 2], j & 3);
+        const uint32_t xn = byte_of(xb[j >> 2], j & 3);
+        const uint32_t ro = ffbl(xo), rn = ffbl(xn);
+        X1 = X1 + xn - xo;                         // RollingHash::roll, xcodec_hash.h:57-70
+        X2c = X2c + X1 - (xo << 11);
+        F1 = F1 + rn - ro;                         // (ffbl+1) - (ffbl+1)
+        F2 = F2 + F1 - (ro << 11) - 2048u;         // - 2048 * ffs(dead)
+      }
     }
-    ev |= hit ? (1u << j) : 0u;
-    if (j < 31) {
-      const uint32_t xo = byte_of(xa[j >> 2], j & 3);
-      const uint32_t xn = byte_of(xb[j >> 2], j & 3);
-      const uint32_t ro = ffbl(xo), rn = ffbl(xn);
-      X1 = X1 + xn - xo;                         // RollingHash::roll, xcodec_hash.h:57-70
-      X2c = X2c + X1 - (xo << 11);
-      F1 = F1 + rn - ro;                         // (ffbl+1) - (ffbl+1)
-      F2 = F2 + F1 - (ro << 11) - 2048u;         // - 2048 * ffs(dead)
+    uint2 e[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(fptab + 2 * bkt[t]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = 4 * g + t;
+      bool hit = (e[t].x == fpv[t]) | (e[t].y == fpv[t]);
+      if (C0) hit |= (fpv[t] == c0fp) & (j >= jvis);
+      if (novf) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) hit |= (o[k] == fpv[t]);
+      }
+      ev |= (uint32_t)hit << j;
     }
+    asm volatile("" : "+v"(ev));   // materialise this group's bits before the next group
+    __builtin_amdgcn_sched_barrier(0);
   }
   return ev;
 }
@@ -251,7 +278,7 @@ template <int LOGNB, int MAXD>
 __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) {
   __shared__ WaveTable<LOGNB, MAXD> tabs[4];
   constexpr int NB = 1 << LOGNB;
-  const int wv = threadIdx.x >> 6;
+  const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const int l = lane_id();
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
   if (chunk >= prm.n) return;
@@ -266,7 +293,7 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
   uint32_t n_extract = 0, n_ref = 0, n_coll = 0, n_pieces = 0;
 
   if (L < SEG) {                                   // xcodec_encoder.cc:77-83
-    if (L > 0) olen = wave_escape(out, x, 0, (uint32_t)L);
+    if (L > 0) olen = escape_u(out, x, 0, (uint32_t)L);
     if (l == 0) prm.out_len[chunk] = olen;
     return;
   }
@@ -284,6 +311,16 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
 
   Piece P;
   int p_prev = INT32_MIN;
+  // Registers that already hold window bytes: the previous piece's A half
+  // (bytes [p_prev, p_prev + 2048) across the wave) and the next piece's
+  // prefetched B half.
+  u32x4 nb0 = {0u, 0u, 0u, 0u}, nb1 = nb0;
+  int nb_start = INT32_MIN;
+  // A candidate set at the piece start has its whole segment in the wave's A
+  // registers; its EXTRACT body is written to the output right then, at the
+  // offset the declaration will have if nothing cancels it (spec_olen).
+  int spec_cand = -1;
+  uint32_t spec_olen = 0;
   uint32_t totXA = 0, totTA = 0, totFA = 0, totTFA = 0;   // sums over the A half (carried)
 
   // Insert a declaration into the LDS table (XCodecMemoryCache::enter,
@@ -330,14 +367,14 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
 
   // encode_declaration (xcodec_encoder.cc:276-313).
   auto declare = [&]() {
-    if (cand > base) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)cand);
+    if (cand > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)cand);
     if (!nullcache && !c0_in_table) insert(cand_lo, cand_hi, (uint32_t)cand);
     if (oob) {
       wave_put_ref(out + olen, cand_lo, cand_hi);           // :288-295
       olen += 10;
     } else {
       if (l < 2) out[olen + l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);   // :300-302
-      wave_copy(out + olen + 2, x + cand, SEG);
+      if (!(cand == spec_cand && olen == spec_olen)) wave_copy(out + olen + 2, x + cand, SEG);
       olen += 2 + SEG;
     }
     ++n_extract;
@@ -349,6 +386,7 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
   while (s <= last) {
     // ---- piece geometry: q0 = p + 32 lane, loads 16-byte aligned in memory
     const int p = s - (int)(((uint32_t)mis + (uint32_t)s) & 15u);
+    const int l = opaque(lane_id());
     const int q0 = p + 32 * l;
     const bool contig = (p == p_prev + SEG);
     ++n_pieces;
@@ -356,12 +394,23 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
       P.a0 = P.b0; P.a1 = P.b1;
       P.sxa = P.sxb; P.sqxa = P.sqxb; P.sfa = P.sfb; P.sqfa = P.sqfb;
     } else {
-      P.a0 = load16_guarded(x, q0, L);
-      P.a1 = load16_guarded(x, q0 + 16, L);
+      P.a0 = load16_aligned_safe(x, q0, L);
+      P.a1 = load16_aligned_safe(x, q0 + 16, L);
       seg_sums(P.a0, P.a1, P.sxa, P.sqxa, P.sfa, P.sqfa);
     }
-    P.b0 = load16_guarded(x, q0 + SEG, L);
-    P.b1 = load16_guarded(x, q0 + SEG + 16, L);
+    if (nb_start == p) {
+      P.b0 = nb0; P.b1 = nb1;
+    } else {
+      P.b0 = load16_aligned_safe(x, q0 + SEG, L);
+      P.b1 = load16_aligned_safe(x, q0 + SEG + 16, L);
+    }
+    // Prefetch the next contiguous piece's entering bytes; they land while
+    // this piece rolls.
+    nb_start = p + SEG;
+    if (nb_start <= last) {
+      nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
+      nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
+    }
     seg_sums(P.b0, P.b1, P.sxb, P.sqxb, P.sfb, P.sqfb);
     p_prev = p;
 
@@ -405,17 +454,12 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
       uint32_t ovfv[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) ovfv[k] = (uint32_t)k < novf ? readfirst(T.ovf_fp[k]) : 0u;
-      if (c0) {
-        if (novf) ev = roll_probe<LOGNB, true, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
-        else ev = roll_probe<LOGNB, true, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
-      } else {
-        if (novf) ev = roll_probe<LOGNB, false, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
-        else ev = roll_probe<LOGNB, false, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, lo0, bh0);
-      }
-      // positions past the last window are not positions
+      if (c0) ev = roll_probe<LOGNB, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0);
+      else ev = roll_probe<LOGNB, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0);
+      // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
-      if (nvalid <= 0) ev = 0;
-      else if (nvalid < 32) ev &= (1u << nvalid) - 1u;
+      const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
+      ev &= vm;
     } else {
       lo0 = (X1 << 20) + X2c;
       bh0 = (F1 << 16) + F2;
@@ -438,7 +482,8 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
         lo = readlane(lo0, rel >> 5);
         hi = readlane(bh0, rel >> 5) << 4;
       } else {
-        wave_window_hash(x + pos, lo, hi);
+        const uint2 h = window_hash_u(x + pos);
+        lo = h.x; hi = h.y;
       }
     };
 
@@ -447,12 +492,13 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
       const int e = nullcache ? INT32_MAX : next_event(s);
       if (e == s) {
         // Exact re-check of the probe (find_reference, :374-416).
-        uint32_t lo, hi;
-        wave_window_hash(x + s, lo, hi);
+        const uint2 hh = window_hash_u(x + s);
+        const uint32_t lo = hh.x, hi = hh.y;
         const int d = lookup(lo, hi);
         if (d >= 0) {
-          if (wave_equal2048(x + readfirst(T.rc[d]), x + s)) {
-            if (s > base) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)s);
+          if (equal2048_u(x + readfirst(T.rc[d]), x + s)) {
+            if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
+            if (s > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)s);
             wave_put_ref(out + olen, lo, hi);                 // encode_reference :342-372
             olen += 10;
             ++n_ref;
@@ -478,6 +524,14 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
         have_cand = true;
         cand = s;
         c0_in_table = false;
+        if (s == p && base == s && !oob) {
+          // Declaration body = bytes [p, p + 2048) = the A registers.
+          uint8_t* dst = out + olen + 2 + 32 * lane_id();
+          *(u32x4_u*)dst = P.a0;
+          *(u32x4_u*)(dst + 16) = P.a1;
+          spec_cand = s;
+          spec_olen = olen;
+        }
         ++s;
         continue;
       }
@@ -490,7 +544,7 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
   }
 
   if (have_cand) declare();                                   // :257-261
-  if (base < L) olen += wave_escape(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
+  if (base < L) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
   if (l == 0) {
     prm.out_len[chunk] = olen;
     if (prm.stats) {
