@@ -39,7 +39,7 @@ def parse():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--chunks', type=int, default=NCHUNKS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-passes', type=int, default=2)
+    ap.add_argument('--cpu-passes', type=int, default=8)
     return ap.parse_args()
 
 
