@@ -47,6 +47,12 @@ extern "C" {
 /* Batch semantics. */
 #define XCG_SEM_INDEPENDENT 0      /* chunk i = one encode() with a fresh, empty
                                       XCodecMemoryCache (no cross-chunk state) */
+#define XCG_SEM_STREAM 1           /* chunks 0..n-1 = successive encode() calls of ONE
+                                      XCodecEncoder on the context's persistent cache
+                                      (tack's loop, programs/tack/tack.cc:308-321); the
+                                      batch's declarations are committed to the cache */
+
+#define XCG_DEFAULT_CACHE_SEGMENTS (1u << 19)   /* 1 GiB of segments */
 
 /* Status codes. */
 #define XCG_OK 0
@@ -67,7 +73,20 @@ const char *xcg_strerror(int status);
 uint64_t xcg_encode_bound(uint32_t len);
 
 int xcg_ctx_create(int device, uint32_t flags, xcg_ctx **out);
+/* As xcg_ctx_create with an explicit persistent-cache capacity in 2 KiB
+ * segments (XCodecMemoryCache(uuid, limit), xcodec/xcodec_cache.h:277; here
+ * exceeding it is an error, XCG_EOVERFLOW, not an LRU eviction). */
+int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_ctx **out);
 void xcg_ctx_destroy(xcg_ctx *ctx);
+
+/* Persistent cache: number of segments held / drop everything. */
+uint64_t xcg_cache_size(xcg_ctx *ctx);
+int xcg_cache_clear(xcg_ctx *ctx);
+/* Rounds the last XCG_SEM_STREAM batch needed to reach its fixed point. */
+int xcg_last_rounds(xcg_ctx *ctx);
+/* Diagnostics: copy the persistent cache's lane filters to host memory
+ * (h_filt: 2^19 bits; h_ftab: up to ftab_words u32; *h_fmask = buckets - 1). */
+int xcg_debug_cache_dump(xcg_ctx *ctx, uint32_t *h_filt, uint32_t *h_ftab, uint64_t ftab_words, uint32_t *h_fmask);
 
 /*
  * Encode n chunks in one launch.  Chunk i is d_in[d_chunk_off[i] ..
@@ -77,7 +96,8 @@ void xcg_ctx_destroy(xcg_ctx *ctx);
  * d_out_len[i].  max_chunk_len bounds every d_chunk_len[i] (<= 512 KiB, the
  * XCodecPipePair frame cap, xcodec/xcodec_pipe_pair.cc:596-604).
  * d_stats (nullable): 4 u32 per chunk {EXTRACT or OOB declarations, REFs,
- * hash collisions, pieces}.  Asynchronous on `stream`.
+ * hash collisions, pieces}.  XCG_SEM_INDEPENDENT is asynchronous on `stream`;
+ * XCG_SEM_STREAM (chunks <= 128 KiB) synchronises `stream` once per round.
  */
 int xcg_encode_batch(xcg_ctx *ctx, int semantics, const uint8_t *d_in, const uint64_t *d_chunk_off,
                      const uint32_t *d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t *d_out,

@@ -18,12 +18,78 @@ extern "C" int xcg_launch_encode_independent(const uint8_t*, const uint64_t*, co
                                              uint32_t, uint8_t*, const uint64_t*, uint64_t*, uint32_t*, int32_t*,
                                              hipStream_t);
 extern "C" int xcg_launch_window_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
+
+struct XcgStreamArgs {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint32_t flags;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint64_t* out_len;
+  uint32_t* stats;
+  int32_t* status;
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  uint64_t* b_keys;
+  uint64_t* b_vals;
+  uint32_t b_mask;
+  uint32_t* r_filt;
+  uint32_t* r_ftab;
+  void* decl;
+  uint32_t* ndecl;
+  uint32_t maxd;
+  uint32_t* changed;
+  uint32_t* h_changed;
+};
+extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
+
+// The persistent segment cache of a context: XCodecMemoryCache's
+// hash_map<Tag64, BufferSegment*> (xcodec/xcodec_cache.h:270) as an
+// open-addressed table in HBM plus a segment pool, and the two lane-probe
+// filters over it (see xcg_cache.h).
+struct GpuCache {
+  uint64_t* keys = nullptr;
+  uint64_t* vals = nullptr;
+  uint32_t mask = 0;
+  uint8_t* pool = nullptr;
+  uint32_t seg_cap = 0;
+  uint32_t* nseg = nullptr;     // device counter
+  uint32_t* filt = nullptr;     // FILT_WORDS
+  uint32_t* ftab = nullptr;     // fbuckets * 4
+  uint32_t fmask = 0;
+};
+
+struct BatchScratch {
+  uint32_t n_cap = 0, maxd = 0;
+  uint64_t* b_keys = nullptr;
+  uint64_t* b_vals = nullptr;
+  uint32_t b_mask = 0;
+  uint32_t* r_filt = nullptr;
+  uint32_t* r_ftab = nullptr;
+  void* decl = nullptr;
+  uint32_t* ndecl = nullptr;
+  uint32_t* changed = nullptr;
+  uint32_t* h_changed = nullptr;   // pinned
+};
 
 struct xcg_ctx {
   int device;
   uint32_t flags;
   int32_t* d_status;   // sticky internal-overflow word
+  uint64_t cache_segments;
+  GpuCache g;
+  BatchScratch bs;
+  int last_rounds;
 };
 
 namespace {
@@ -38,6 +104,77 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+constexpr uint32_t FILT_WORDS = (1u << 19) / 32;   // xcg_cache.h FILT_LOG2
+
+uint32_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return (uint32_t)p;
+}
+
+void free_cache(GpuCache& g) {
+  (void)hipFree(g.keys); (void)hipFree(g.vals); (void)hipFree(g.pool); (void)hipFree(g.nseg);
+  (void)hipFree(g.filt); (void)hipFree(g.ftab);
+  g = GpuCache{};
+}
+
+void free_scratch(BatchScratch& b) {
+  (void)hipFree(b.b_keys); (void)hipFree(b.b_vals); (void)hipFree(b.r_filt); (void)hipFree(b.r_ftab);
+  (void)hipFree(b.decl); (void)hipFree(b.ndecl); (void)hipFree(b.changed);
+  if (b.h_changed) (void)hipHostFree(b.h_changed);
+  b = BatchScratch{};
+}
+
+int clear_cache(GpuCache& g) {
+  if (hipMemset(g.keys, 0xFF, 8ull * (g.mask + 1)) != hipSuccess ||
+      hipMemset(g.vals, 0xFF, 8ull * (g.mask + 1)) != hipSuccess || hipMemset(g.nseg, 0, 4) != hipSuccess ||
+      hipMemset(g.filt, 0, 4ull * FILT_WORDS) != hipSuccess ||
+      hipMemset(g.ftab, 0, 16ull * (g.fmask + 1)) != hipSuccess)
+    return XCG_EHIP;
+  return XCG_OK;
+}
+
+// Lazily allocate the persistent cache (segments * 2 KiB of pool).
+int ensure_cache(xcg_ctx* c) {
+  if (c->g.keys) return XCG_OK;
+  GpuCache& g = c->g;
+  const uint64_t segs = c->cache_segments;
+  g.seg_cap = (uint32_t)segs;
+  const uint32_t cap = pow2_at_least(2 * segs + 1024);
+  g.mask = cap - 1;
+  const uint32_t fb = pow2_at_least(2 * segs + 4096);
+  g.fmask = fb - 1;
+  if (hipMalloc(&g.keys, 8ull * cap) != hipSuccess || hipMalloc(&g.vals, 8ull * cap) != hipSuccess ||
+      hipMalloc(&g.pool, segs * (uint64_t)XCG_SEGMENT_LENGTH + 16) != hipSuccess ||
+      hipMalloc(&g.nseg, 16) != hipSuccess || hipMalloc(&g.filt, 4ull * FILT_WORDS) != hipSuccess ||
+      hipMalloc(&g.ftab, 16ull * fb) != hipSuccess) {
+    free_cache(g);
+    return XCG_ENOMEM;
+  }
+  int rc = clear_cache(g);
+  if (rc) free_cache(g);
+  return rc;
+}
+
+int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
+  BatchScratch& b = c->bs;
+  if (b.decl && n <= b.n_cap && maxd <= b.maxd) return XCG_OK;
+  free_scratch(b);
+  b.n_cap = n;
+  b.maxd = maxd;
+  const uint32_t cap = pow2_at_least(2ull * n * maxd + 1024);
+  b.b_mask = cap - 1;
+  if (hipMalloc(&b.b_keys, 8ull * cap) != hipSuccess || hipMalloc(&b.b_vals, 8ull * cap) != hipSuccess ||
+      hipMalloc(&b.r_filt, 4ull * FILT_WORDS) != hipSuccess ||
+      hipMalloc(&b.r_ftab, 16ull * (c->g.fmask + 1)) != hipSuccess ||
+      hipMalloc(&b.decl, 16ull * n * maxd) != hipSuccess || hipMalloc(&b.ndecl, 4ull * n) != hipSuccess ||
+      hipMalloc(&b.changed, 16) != hipSuccess || hipHostMalloc(&b.h_changed, 16) != hipSuccess) {
+    free_scratch(b);
+    return XCG_ENOMEM;
+  }
+  return XCG_OK;
+}
 
 }  // namespace
 
@@ -60,13 +197,17 @@ const char* xcg_strerror(int status) {
 uint64_t xcg_encode_bound(uint32_t len) { return 2ull * len + 16ull; }
 
 int xcg_ctx_create(int device, uint32_t flags, xcg_ctx** out) {
-  if (!out) return XCG_EINVAL;
+  return xcg_ctx_create_ex(device, flags, XCG_DEFAULT_CACHE_SEGMENTS, out);
+}
+
+int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_ctx** out) {
+  if (!out || cache_segments == 0 || cache_segments > (1ull << 30)) return XCG_EINVAL;
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
   if (flags & ~(XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) return XCG_EINVAL;
   DeviceGuard g(device);
-  xcg_ctx* c = new xcg_ctx{device, flags, nullptr};
+  xcg_ctx* c = new xcg_ctx{device, flags, nullptr, cache_segments, GpuCache{}, BatchScratch{}, 0};
   if (hipMalloc(&c->d_status, 16) != hipSuccess) {
     delete c;
     return XCG_ENOMEM;
@@ -84,7 +225,41 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipFree(c->d_status);
+  free_cache(c->g);
+  free_scratch(c->bs);
   delete c;
+}
+
+uint64_t xcg_cache_size(xcg_ctx* c) {
+  if (!c || !c->g.keys) return 0;
+  DeviceGuard g(c->device);
+  uint32_t n = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&n, c->g.nseg, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return n < c->g.seg_cap ? n : c->g.seg_cap;
+}
+
+int xcg_cache_clear(xcg_ctx* c) {
+  if (!c) return XCG_EINVAL;
+  if (!c->g.keys) return XCG_OK;
+  DeviceGuard g(c->device);
+  if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
+  return clear_cache(c->g);
+}
+
+int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
+
+int xcg_debug_cache_dump(xcg_ctx* c, uint32_t* h_filt, uint32_t* h_ftab, uint64_t ftab_words, uint32_t* h_fmask) {
+  if (!c || !c->g.keys) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  *h_fmask = c->g.fmask;
+  if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
+  if (h_filt && hipMemcpy(h_filt, c->g.filt, 4ull * FILT_WORDS, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+  const uint64_t tw = 4ull * (c->g.fmask + 1);
+  if (h_ftab && hipMemcpy(h_ftab, c->g.ftab, 4ull * (ftab_words < tw ? ftab_words : tw), hipMemcpyDeviceToHost) !=
+                    hipSuccess)
+    return XCG_EHIP;
+  return XCG_OK;
 }
 
 int xcg_ctx_status(xcg_ctx* c) {
@@ -102,9 +277,24 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
   if (!c) return XCG_EINVAL;
   if (n == 0) return XCG_OK;
   if (!d_in || !d_chunk_off || !d_chunk_len || !d_out || !d_out_off || !d_out_len) return XCG_EINVAL;
-  if (semantics != XCG_SEM_INDEPENDENT) return XCG_ENOTSUP;
+  if (semantics != XCG_SEM_INDEPENDENT && semantics != XCG_SEM_STREAM) return XCG_EINVAL;
   if (max_chunk_len > (1u << 19)) return XCG_EINVAL;
   DeviceGuard g(c->device);
+  // A null cache has no state to carry: both semantics are the same pass.
+  if (semantics == XCG_SEM_STREAM && !(c->flags & XCG_FLAG_NULLCACHE)) {
+    if (max_chunk_len > (1u << 17)) return XCG_ENOTSUP;
+    int rc = ensure_cache(c);
+    if (rc == XCG_OK) rc = ensure_scratch(c, n, 72);
+    if (rc != XCG_OK) return rc;
+    XcgStreamArgs a{d_in, d_chunk_off, d_chunk_len, n, c->flags, d_out, d_out_off, d_out_len, d_stats,
+                    c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
+                    c->g.filt, c->g.ftab, c->g.fmask, c->bs.b_keys, c->bs.b_vals, c->bs.b_mask,
+                    c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, 72, c->bs.changed, c->bs.h_changed};
+    int rounds = 0;
+    rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
+    c->last_rounds = rounds;
+    return rc == 0 ? XCG_OK : XCG_EHIP;
+  }
   int rc = xcg_launch_encode_independent(d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, c->flags, d_out,
                                          d_out_off, d_out_len, d_stats, c->d_status, (hipStream_t)stream);
   return rc == 0 ? XCG_OK : (rc == -22 ? XCG_EINVAL : XCG_EHIP);

@@ -1,0 +1,115 @@
+// GPU-resident XCodec segment cache (XCodecMemoryCache, xcodec/xcodec_cache.h:
+// 245-365, unbounded variant) and the per-batch declaration table used by the
+// stream-semantics encoder.  Device views are plain structs of pointers.
+//
+// Layout in HBM (see DESIGN.md "Data layout"):
+//   keys[cap]  u64   XCodecHash of the segment; EMPTY = all ones (a real hash
+//                    always has bits 32..35 clear: mix() shifts bits_hash by 36)
+//   vals[cap]  u64   G: segment index into pool;  B: (chunk << 32) | position
+//   pool[nseg_cap * 2048]  segment bytes (G only)
+//   ftab[fbuckets * 4] u32  lane-probe fingerprint buckets: 3 slots of (lo | 1)
+//                    + an overflow word, one 16-byte load per probe
+//   filt[FILT_BITS / 32] u32  the bitmap a workgroup loads into LDS
+#pragma once
+#include "xcg_device.h"
+
+namespace xcg {
+
+constexpr uint64_t EMPTY_KEY = ~0ull;
+constexpr int FILT_LOG2 = 19;                       // 2^19 bits = 64 KiB of LDS
+constexpr uint32_t FILT_WORDS = (1u << FILT_LOG2) / 32;
+constexpr uint32_t FOVF = 2u;                       // bucket-overflow marker (even: never a fingerprint)
+
+struct HashTab {      // exact open-addressed map u64 -> u64
+  uint64_t* keys;
+  uint64_t* vals;
+  uint32_t mask;      // cap - 1
+};
+
+struct LaneFilter {   // what a lane probes: LDS bitmap (copied from filt) + fingerprint buckets
+  const uint32_t* filt;
+  const u32x4* ftab;
+  uint32_t fmask;     // fbuckets - 1
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 13;
+  return h;
+}
+
+// Exact-table slot of a hash (lo = bytes_hash word, hi = bits_hash << 4).
+__device__ __forceinline__ uint32_t tab_slot(uint32_t lo, uint32_t hi, uint32_t mask) {
+  return mix32(lo, hi) & mask;
+}
+
+// Filter bit and fingerprint bucket are functions of (fp, bh) where fp =
+// lo | 1 and bh = bits_hash = hi >> 4 -- both computable inside the rolling
+// loop.  (bh's bits 28..31 never reach the hash, so they are masked.)
+__device__ __forceinline__ uint32_t filt_bit(uint32_t fp, uint32_t bh) {
+  bh &= 0x0FFFFFFFu;
+  return (fp ^ (bh << 3) ^ (bh >> 13)) & ((1u << FILT_LOG2) - 1u);
+}
+__device__ __forceinline__ uint32_t fbucket(uint32_t fp, uint32_t bh, uint32_t fmask) {
+  bh &= 0x0FFFFFFFu;
+  return ((fp >> 7) ^ (bh * 0x9E37u) ^ (fp << 9)) & fmask;
+}
+
+// Wave-uniform 64-bit value (readfirstlane per 32-bit half; no sign extension).
+__device__ __forceinline__ uint64_t readfirst64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Uniform (wave-level) exact lookup: value or ~0 when absent.
+__device__ __forceinline__ uint64_t tab_lookup(const HashTab& t, uint32_t lo, uint32_t hi) {
+  const uint64_t key = ((uint64_t)hi << 32) | lo;
+  uint32_t i = tab_slot(lo, hi, t.mask);
+  for (uint32_t n = 0; n <= t.mask; ++n) {
+    const uint64_t k = readfirst64(t.keys[i]);
+    if (k == key) return readfirst64(t.vals[i]);
+    if (k == EMPTY_KEY) break;
+    i = (i + 1) & t.mask;
+  }
+  return ~0ull;
+}
+
+// Per-thread insert (keys unique per call site).  For B, `val` is combined with
+// atomicMin so the earliest (chunk, position) declaring a hash wins.
+__device__ __forceinline__ bool tab_insert_min(HashTab t, uint32_t lo, uint32_t hi, uint64_t val) {
+  const uint64_t key = ((uint64_t)hi << 32) | lo;
+  uint32_t i = tab_slot(lo, hi, t.mask);
+  for (uint32_t n = 0; n <= t.mask; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&t.keys[i], (unsigned long long)EMPTY_KEY,
+                                    (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) {
+      atomicMin((unsigned long long*)&t.vals[i], (unsigned long long)val);
+      return true;
+    }
+    i = (i + 1) & t.mask;
+  }
+  return false;
+}
+
+// Fingerprint bucket insert: first free of 3 slots, else mark overflow (lanes
+// then report an event there and the resolver decides exactly).
+__device__ __forceinline__ void ftab_insert(uint32_t* ftab, uint32_t fmask, uint32_t lo, uint32_t hi) {
+  const uint32_t fp = lo | 1u;
+  const uint32_t b = fbucket(fp, hi >> 4, fmask);
+  uint32_t* s = ftab + 4 * b;
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t prev = atomicCAS(s + k, 0u, fp);
+    if (prev == 0u || prev == fp) return;
+  }
+  atomicExch(s + 3, FOVF);
+}
+
+__device__ __forceinline__ void filt_insert(uint32_t* filt, uint32_t lo, uint32_t hi) {
+  const uint32_t bit = filt_bit(lo | 1u, hi >> 4);
+  atomicOr(filt + (bit >> 5), 1u << (bit & 31));
+}
+
+}  // namespace xcg

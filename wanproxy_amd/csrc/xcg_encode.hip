@@ -26,7 +26,7 @@
 // fingerprint table can be approximate without affecting output.  Output ops
 // (ESCAPE / EXTRACT / REF, xcodec_encoder.cc:276-372) are written by the whole
 // wave as they are resolved, into the chunk's output slot.
-#include "xcg_device.h"
+#include "xcg_cache.h"
 #include "../../include/xcgpu.h"
 
 namespace xcg {
@@ -55,6 +55,16 @@ struct EncParams {
   uint64_t* out_len;
   uint32_t* stats;     // optional: per chunk {n_extract, n_ref, n_collision, n_pieces}
   int32_t* status;     // optional: nonzero on internal overflow
+  // ---- stream semantics (XCG_SEM_STREAM) only
+  HashTab g;           // the persistent cache: hash -> segment index
+  const uint8_t* pool; // its segment bytes
+  HashTab b;           // this batch's declarations (earlier rounds): hash -> (chunk << 32 | pos)
+  bool use_b;
+  LaneFilter lf;       // lane probe filter over g + b
+  uint4* decl;         // [n * maxd] (lo, hi, pos, 0) declarations of the chunk, this round
+  uint32_t* ndecl;     // [n]
+  uint32_t maxd;
+  uint32_t* changed;   // set when any chunk's declaration list differs from the last round
 };
 
 __device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t bh, int logNB) {
@@ -218,11 +228,12 @@ __device__ __forceinline__ void seg_sums(const u32x4 d0, const u32x4 d1, uint32_
 // position q0 + j is a possible cache hit.  C0: the pending candidate c0 is
 // not in the table yet and becomes visible at local index jvis.  OVF: probe
 // the (rare) overflow keys too.
-template <int LOGNB, bool C0>
+template <int LOGNB, bool C0, bool GLB>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint32_t X2c, uint32_t F1,
                                                uint32_t F2, const uint32_t* fptab, uint32_t c0fp, int jvis,
                                                const uint32_t* ovf, uint32_t novf, uint32_t& lo0,
-                                               uint32_t& bh0) {
+                                               uint32_t& bh0, const uint32_t* lfilt, const u32x4* ftab,
+                                               uint32_t fmask) {
   const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
   const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
   uint32_t o[8];   // overflow keys (uniform, SGPRs); novf == 0 almost always
@@ -233,7 +244,7 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint
   // LDS probes (and their operands) at once, which would cost ~100 VGPRs.
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    uint32_t fpv[4], bkt[4];
+    uint32_t fpv[4], bkt[4], gbh[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
@@ -242,6 +253,7 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint
       if (j == 0) { lo0 = lo; bh0 = bh; }
       fpv[t] = lo | 1u;
       bkt[t] = bucket_of(lo, bh, LOGNB);
+      gbh[t] = bh;
       if (j < 31) {
         const uint32_t xo = byte_of(xa[j >> 2], j & 3);
         const uint32_t xn = byte_of(xb[j >> 2], j & 3);
@@ -255,10 +267,30 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint
     uint2 e[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(fptab + 2 * bkt[t]);
+    // Global cache + batch declarations: LDS bitmap first, then (rarely) one
+    // 16-byte fingerprint-bucket load; all four loads issued before any use.
+    bool gh[4] = {false, false, false, false};
+    if (GLB) {
+      u32x4 q[4];
+      bool pass[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t fb = filt_bit(fpv[t], gbh[t]);
+        pass[t] = (lfilt[fb >> 5] >> (fb & 31)) & 1u;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        q[t] = u32x4{0u, 0u, 0u, 0u};
+        if (pass[t]) q[t] = ftab[fbucket(fpv[t], gbh[t], fmask)];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        gh[t] = (q[t][0] == fpv[t]) | (q[t][1] == fpv[t]) | (q[t][2] == fpv[t]) | (q[t][3] == FOVF);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
-      bool hit = (e[t].x == fpv[t]) | (e[t].y == fpv[t]);
+      bool hit = (e[t].x == fpv[t]) | (e[t].y == fpv[t]) | gh[t];
       if (C0) hit |= (fpv[t] == c0fp) & (j >= jvis);
       if (novf) {
 #pragma unroll
@@ -274,15 +306,14 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint
 
 // ------------------------------------------------------------------ kernel
 
-template <int LOGNB, int MAXD>
-__global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) {
-  __shared__ WaveTable<LOGNB, MAXD> tabs[4];
+// One wave encodes chunk `chunk` (one XCodecEncoder::encode call).  STREAM:
+// the cache also holds the persistent GPU cache g and the batch declarations
+// b of chunks < chunk, probed through the workgroup's LDS filter lfilt.
+template <int LOGNB, int MAXD, bool STREAM>
+__device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOGNB, MAXD>& T, const uint32_t chunk,
+                                             const uint32_t* lfilt) {
   constexpr int NB = 1 << LOGNB;
-  const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const int l = lane_id();
-  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
-  if (chunk >= prm.n) return;
-  WaveTable<LOGNB, MAXD>& T = tabs[wv];
 
   const uint8_t* x = prm.in + prm.chunk_off[chunk];
   const int L = (int)prm.chunk_len[chunk];
@@ -454,8 +485,12 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
       uint32_t ovfv[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) ovfv[k] = (uint32_t)k < novf ? readfirst(T.ovf_fp[k]) : 0u;
-      if (c0) ev = roll_probe<LOGNB, true>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0);
-      else ev = roll_probe<LOGNB, false>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0);
+      if (c0)
+        ev = roll_probe<LOGNB, true, STREAM>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0, lfilt,
+                                             prm.lf.ftab, prm.lf.fmask);
+      else
+        ev = roll_probe<LOGNB, false, STREAM>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0, lfilt,
+                                              prm.lf.ftab, prm.lf.fmask);
       // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
       const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
@@ -495,8 +530,21 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
         const uint2 hh = window_hash_u(x + s);
         const uint32_t lo = hh.x, hi = hh.y;
         const int d = lookup(lo, hi);
-        if (d >= 0) {
-          if (equal2048_u(x + readfirst(T.rc[d]), x + s)) {
+        // Where the hash is declared: this chunk (d), the persistent cache, or
+        // an earlier chunk of the batch.  src = that segment's bytes.
+        const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
+        if (STREAM && src == nullptr) {
+          const uint64_t gv = tab_lookup(prm.g, lo, hi);
+          if (gv != ~0ull) {
+            src = prm.pool + gv * (uint64_t)SEG;
+          } else if (prm.use_b) {
+            const uint64_t bv = tab_lookup(prm.b, lo, hi);
+            if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk)
+              src = prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
+          }
+        }
+        if (src != nullptr) {
+          if (equal2048_u(src, x + s)) {
             if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
             if (s > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)s);
             wave_put_ref(out + olen, lo, hi);                 // encode_reference :342-372
@@ -545,6 +593,22 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
 
   if (have_cand) declare();                                   // :257-261
   if (base < L) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
+  if (STREAM) {
+    // This round's declarations; flag a change against the previous round's.
+    const uint32_t nold = prm.ndecl[chunk];
+    bool diff = nold != ndecl;
+    uint4* dl = prm.decl + (uint64_t)chunk * prm.maxd;
+    for (uint32_t k = l; k < ndecl; k += 64) {
+      const uint4 nv = make_uint4(T.rlo[k], T.rhi[k], T.rc[k], 0u);
+      if (k < nold) {
+        const uint4 ov = dl[k];
+        diff |= ov.x != nv.x || ov.y != nv.y || ov.z != nv.z;
+      }
+      dl[k] = nv;
+    }
+    if (ballot(diff) != 0 && l == 0) atomicOr(prm.changed, 1u);
+    if (l == 0) prm.ndecl[chunk] = ndecl;
+  }
   if (l == 0) {
     prm.out_len[chunk] = olen;
     if (prm.stats) {
@@ -556,8 +620,35 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
   }
 }
 
+
+template <int LOGNB, int MAXD>
+__global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) {
+  __shared__ WaveTable<LOGNB, MAXD> tabs[4];
+  const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  encode_chunk<LOGNB, MAXD, false>(prm, tabs[wv], chunk, nullptr);
+}
+
+// Stream semantics: persistent workgroups of SW waves share one LDS copy of
+// the lane filter; each wave walks chunks wave_id, wave_id + total_waves, ...
+constexpr int SW = 12;
+template <int LOGNB, int MAXD>
+__global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
+  __shared__ uint32_t lfilt[FILT_WORDS];
+  __shared__ WaveTable<LOGNB, MAXD> tabs[SW];
+  for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
+    ((u32x4*)lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
+  __syncthreads();
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t stride = gridDim.x * SW;
+  for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride)
+    encode_chunk<LOGNB, MAXD, true>(prm, tabs[wv], chunk, lfilt);
+}
+
 template __global__ void encode_independent_kernel<9, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
+template __global__ void encode_stream_kernel<8, 72>(EncParams);
 
 }  // namespace xcg
 
@@ -576,5 +667,146 @@ extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t
   } else {
     return -22;
   }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// ------------------------------------------------------------ stream rounds
+
+namespace xcg {
+
+// B <- every declaration of this round (earliest chunk wins per hash), and the
+// round's lane filter = the persistent cache's filter + B.  One thread per
+// (chunk, declaration).
+__global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
+                                                                uint32_t maxd, HashTab b, uint32_t* filt,
+                                                                uint32_t* ftab, uint32_t fmask, int32_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxd), k = (uint32_t)(i % maxd);
+  if (c >= n || k >= ndecl[c]) return;
+  const uint4 d = decl[i];
+  if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
+  filt_insert(filt, d.x, d.y);
+  ftab_insert(ftab, fmask, d.x, d.y);
+}
+
+// Commit the converged declarations into the persistent cache: one wave per
+// (chunk, declaration) copies the 2048-byte segment into the pool
+// (XCodecMemoryCache::enter, xcodec_cache.h:303-325).
+__global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
+                                                     uint32_t maxd, const uint8_t* in, const uint64_t* chunk_off,
+                                                     HashTab g, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
+                                                     uint32_t* filt, uint32_t* ftab, uint32_t fmask, int32_t* status) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t c = (uint32_t)(w / maxd), k = (uint32_t)(w % maxd);
+  if (c >= n || k >= ndecl[c]) return;
+  const uint4 d = decl[w];
+  uint32_t seg = 0;
+  if (lane_id() == 0) seg = atomicAdd(nseg, 1u);
+  seg = readfirst(seg);
+  if (seg >= seg_cap) {
+    if (lane_id() == 0) atomicOr(status, 4);
+    return;
+  }
+  const uint8_t* src = in + chunk_off[c] + d.z;
+  uint8_t* dst = pool + (uint64_t)seg * SEG;
+  const int l = lane_id();
+  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+  if (l == 0) {
+    if (!tab_insert_min(g, d.x, d.y, seg)) atomicOr(status, 2);
+    filt_insert(filt, d.x, d.y);
+    ftab_insert(ftab, fmask, d.x, d.y);
+  }
+}
+
+}  // namespace xcg
+
+struct XcgStreamArgs {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint32_t flags;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint64_t* out_len;
+  uint32_t* stats;
+  int32_t* status;
+  // persistent cache
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  // batch scratch
+  uint64_t* b_keys;
+  uint64_t* b_vals;
+  uint32_t b_mask;
+  uint32_t* r_filt;
+  uint32_t* r_ftab;
+  uint4* decl;
+  uint32_t* ndecl;
+  uint32_t maxd;
+  uint32_t* changed;
+  uint32_t* h_changed;   // pinned host word
+};
+
+extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
+  using namespace xcg;
+  const uint32_t n = a->n;
+  if (n == 0) return 0;
+  EncParams prm{a->in, a->chunk_off, a->chunk_len, n, a->flags, a->out, a->out_off, a->out_len, a->stats, a->status};
+  prm.g = HashTab{a->g_keys, a->g_vals, a->g_mask};
+  prm.pool = a->pool;
+  prm.b = HashTab{a->b_keys, a->b_vals, a->b_mask};
+  prm.decl = a->decl;
+  prm.ndecl = a->ndecl;
+  prm.maxd = a->maxd;
+  prm.changed = a->changed;
+  const size_t fbytes = (size_t)FILT_WORDS * 4, tbytes = ((size_t)a->fmask + 1) * 16;
+  int dev = 0;
+  hipDeviceProp_t props;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&props, dev) != hipSuccess) return -5;
+  const uint32_t wgs = (uint32_t)props.multiProcessorCount;
+  const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
+  if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess) return -5;
+  // Round 0: every chunk against the persistent cache + its own declarations.
+  prm.use_b = false;
+  prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask};
+  hipLaunchKernelGGL((encode_stream_kernel<8, 72>), sgrid, sblock, 0, stream, prm);
+  int rounds = 1;
+  // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
+  // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
+  // chunk k after round k; a round that changes no declaration list is the
+  // fixed point, which is the sequential result.
+  for (uint32_t r = 1; n > 1 && r <= n; ++r) {
+    if (hipMemsetAsync(a->b_keys, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
+        hipMemsetAsync(a->b_vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
+        hipMemcpyAsync(a->r_filt, a->g_filt, fbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+        hipMemcpyAsync(a->r_ftab, a->g_ftab, tbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+        hipMemsetAsync(a->changed, 0, 4, stream) != hipSuccess)
+      return -5;
+    const uint64_t nthreads = (uint64_t)n * a->maxd;
+    hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
+                       (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, prm.b, a->r_filt, a->r_ftab,
+                       a->fmask, a->status);
+    prm.use_b = true;
+    prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask};
+    hipLaunchKernelGGL((encode_stream_kernel<8, 72>), sgrid, sblock, 0, stream, prm);
+    ++rounds;
+    if (hipMemcpyAsync(a->h_changed, a->changed, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return -5;
+    if (*a->h_changed == 0) break;
+  }
+  const uint64_t nwaves = (uint64_t)n * a->maxd;
+  hipLaunchKernelGGL(commit_kernel, dim3((unsigned)((nwaves * 64 + 255) / 256)), dim3(256), 0, stream,
+                     (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, a->in, a->chunk_off,
+                     prm.g, a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask, a->status);
+  if (rounds_out) *rounds_out = rounds;
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

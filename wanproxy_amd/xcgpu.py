@@ -25,6 +25,7 @@ SEG = 2048
 XCG_FLAG_OOB = 0x1
 XCG_FLAG_NULLCACHE = 0x2
 XCG_SEM_INDEPENDENT = 0
+XCG_SEM_STREAM = 1
 
 _lib = None
 
@@ -50,6 +51,14 @@ def lib():
     L.xcg_encode_bound.argtypes = [C.c_uint32]
     L.xcg_ctx_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create.restype = C.c_int
+    L.xcg_ctx_create_ex.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_ex.restype = C.c_int
+    L.xcg_cache_size.argtypes = [vp]
+    L.xcg_cache_size.restype = C.c_uint64
+    L.xcg_cache_clear.argtypes = [vp]
+    L.xcg_cache_clear.restype = C.c_int
+    L.xcg_last_rounds.argtypes = [vp]
+    L.xcg_last_rounds.restype = C.c_int
     L.xcg_ctx_destroy.argtypes = [vp]
     L.xcg_ctx_status.argtypes = [vp]
     L.xcg_ctx_status.restype = C.c_int
@@ -83,15 +92,26 @@ def encode_bound(n: int) -> int:
 class Context:
     """An XCodecEncoder + cache configuration bound to one GPU."""
 
-    def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False):
+    def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
+                 cache_segments: int = 1 << 19):
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        _check(lib().xcg_ctx_create(device, self.flags, C.byref(h)))
+        _check(lib().xcg_ctx_create_ex(device, self.flags, int(cache_segments), C.byref(h)))
         self.h = h
+
+    # The persistent cache (XCG_SEM_STREAM): XCodecMemoryCache of the encoder.
+    def cache_size(self) -> int:
+        return int(lib().xcg_cache_size(self.h))
+
+    def cache_clear(self):
+        _check(lib().xcg_cache_clear(self.h))
+
+    def last_rounds(self) -> int:
+        return int(lib().xcg_last_rounds(self.h))
 
     def close(self):
         if getattr(self, 'h', None):
@@ -117,7 +137,7 @@ class Context:
             C.c_void_p(d_out_off.data_ptr()), C.c_void_p(d_out_len.data_ptr()),
             C.c_void_p(d_stats.data_ptr()) if d_stats is not None else None, _stream_ptr(stream)))
 
-    def encode_chunks(self, data, offs, lens, with_stats=False):
+    def encode_chunks(self, data, offs, lens, with_stats=False, semantics=XCG_SEM_INDEPENDENT):
         """Encode chunks of host `data` (bytes / np.uint8) on the GPU; returns a
         list of encoded bytes objects (and per-chunk stats if asked)."""
         import torch
@@ -138,7 +158,8 @@ class Context:
         d_out = torch.zeros(int(bounds.sum()), dtype=torch.uint8, device=dev)
         d_ol = torch.zeros(n, dtype=torch.int64, device=dev)
         d_st = torch.zeros(4 * n, dtype=torch.int32, device=dev)
-        self.encode_batch_device(d_in, d_off, d_len, n, int(lens.max()), d_out, d_oo, d_ol, d_st)
+        self.encode_batch_device(d_in, d_off, d_len, n, int(lens.max()), d_out, d_oo, d_ol, d_st,
+                                 semantics=semantics)
         torch.cuda.synchronize(dev)
         self.status()
         out = d_out.cpu().numpy()
@@ -178,11 +199,14 @@ class Context:
 
 
 class XCodecEncoder:
-    """Mirror of XCodecEncoder for independent encode() calls: each call is one
-    chunk with a fresh XCodecMemoryCache (xcodec_encoder.cc:74-274)."""
+    """Mirror of XCodecEncoder(XCodecCache*) (xcodec/xcodec_encoder.h:40-43):
+    successive encode() calls share the context's cache, exactly like tack's
+    loop (programs/tack/tack.cc:301-321)."""
 
     def __init__(self, ctx: Context):
         self.ctx = ctx
 
     def encode(self, data: bytes) -> bytes:
-        return self.ctx.encode_chunks(data, np.array([0]), np.array([len(data)]))[0]
+        if not data:
+            return b''
+        return self.ctx.encode_chunks(data, np.array([0]), np.array([len(data)]), semantics=XCG_SEM_STREAM)[0]
