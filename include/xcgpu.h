@@ -20,6 +20,11 @@
  *                                                      xcodec/xcodec_encoder.cc:74-274
  *       (one encode() call per chunk, exactly as tack / XCodecPipePair issue
  *        them: programs/tack/tack.cc:308-321, xcodec/xcodec_pipe_pair.cc:596-630)
+ *   xcg_decode_batch / xcg_decode_host
+ *       bool XCodecDecoder::decode(Buffer *output, Buffer *input,
+ *                                  std::set<uint64_t>& unknown_hashes)
+ *                                                      xcodec/xcodec_decoder.h:44,
+ *                                                      xcodec/xcodec_decoder.cc:66-272
  *   xcg_window_hashes
  *       XCodecHash::{add,roll,mix}                     xcodec/xcodec_hash.h:93-164
  *   xcg_segment_hashes
@@ -97,7 +102,7 @@ int xcg_debug_cache_dump(xcg_ctx *ctx, uint32_t *h_filt, uint32_t *h_ftab, uint6
  * XCodecPipePair frame cap, xcodec/xcodec_pipe_pair.cc:596-604).
  * d_stats (nullable): 4 u32 per chunk {EXTRACT or OOB declarations, REFs,
  * hash collisions, pieces}.  XCG_SEM_INDEPENDENT is asynchronous on `stream`;
- * XCG_SEM_STREAM (chunks <= 128 KiB) synchronises `stream` once per round.
+ * XCG_SEM_STREAM synchronises `stream` once per round.
  */
 int xcg_encode_batch(xcg_ctx *ctx, int semantics, const uint8_t *d_in, const uint64_t *d_chunk_off,
                      const uint32_t *d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t *d_out,
@@ -108,6 +113,34 @@ int xcg_encode_batch(xcg_ctx *ctx, int semantics, const uint8_t *d_in, const uin
 int xcg_encode_host(xcg_ctx *ctx, int semantics, const uint8_t *h_in, uint64_t in_len,
                     const uint64_t *h_chunk_off, const uint32_t *h_chunk_len, uint32_t n, uint8_t *h_out,
                     uint64_t out_cap, const uint64_t *h_out_off, uint64_t *h_out_len);
+
+/*
+ * Decode n encoded chunks that form ONE stream (successive
+ * XCodecDecoder::decode calls on one decoder whose cache is the context's
+ * persistent cache), xcodec/xcodec_decoder.cc:66-188.  Each chunk should be a
+ * whole encode() output (an XCodecPipePair frame); an op cut at a chunk's end
+ * stops that chunk with status 3 and d_consumed[i] < d_chunk_len[i], as decode()
+ * leaves a partial op in its input.  Decoded bytes are packed contiguously in
+ * d_out (offsets in d_out_off); *h_total_out is the size needed -- if it exceeds
+ * out_cap nothing is written and XCG_EOVERFLOW is returned.
+ * d_chunk_status[i]: 0 decoded, 1 blocked on an unknown REF (decode() returned
+ * true with unknown hashes; later chunks get 2 = not reached), 3 partial op,
+ * -1 bad opcode (decode() returned false).  h_unknown receives the sorted
+ * unknown hashes (decode_skim, :196-272) for the ASK/LEARN protocol.
+ * EXTRACTs decoded before any blocking point enter the persistent cache
+ * (enter / replace, :106-136).  Streams containing BACKREF (never emitted by
+ * XCodecEncoder) return XCG_ENOTSUP.  Synchronises `stream`.
+ */
+int xcg_decode_batch(xcg_ctx *ctx, const uint8_t *d_enc, const uint64_t *d_chunk_off, const uint32_t *d_chunk_len,
+                     uint32_t n, uint32_t max_chunk_len, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                     uint64_t *d_out_len, int32_t *d_chunk_status, uint64_t *d_consumed, uint64_t *h_unknown,
+                     uint32_t unknown_cap, uint32_t *h_nunknown, uint64_t *h_total_out, void *stream);
+
+/* Host-memory convenience over xcg_decode_batch. */
+int xcg_decode_host(xcg_ctx *ctx, const uint8_t *h_enc, uint64_t enc_len, const uint64_t *h_chunk_off,
+                    const uint32_t *h_chunk_len, uint32_t n, uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off,
+                    uint64_t *h_out_len, int32_t *h_chunk_status, uint64_t *h_consumed, uint64_t *h_unknown,
+                    uint32_t unknown_cap, uint32_t *h_nunknown);
 
 /* Status word of the context (sticky; nonzero = an internal overflow happened
  * in an earlier asynchronous call).  Synchronises the context's device. */

@@ -1,0 +1,115 @@
+"""GPU decoder parity (XCodecDecoder::decode, xcodec/xcodec_decoder.cc:66-272)
+against the reference-pinned oracle and the reference harness."""
+import numpy as np
+import pytest
+
+from golden_cases import data
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def dctx():
+    from wanproxy_amd.xcgpu import Context
+    c = Context(0, cache_segments=1 << 18)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize('name', ['kat_a', 'kat_b', 'kat_c', 'kat_z', 'kat_col', 'magic_heavy', 'runs',
+                                  'periodic', 'all_f1', 'c2_small'])
+def test_round_trip_fresh_cache(dctx, oracle, name):
+    # tack -c then tack -d with a fresh cache (programs/tack/tack.cc:298-359).
+    from wanproxy_amd.synth import chunks_of
+    d = data(name)
+    offs, lens = chunks_of(d, 65536)
+    enc = oracle.encode_batch(d, offs, lens, mode=1)
+    dctx.cache_clear()
+    outs, st, cons, unk = dctx.decode_chunks(enc)
+    assert not unk and all(s == 0 for s in st)
+    assert list(cons) == [len(e) for e in enc]
+    assert b''.join(outs) == d
+    assert dctx.cache_size() > 0   # the EXTRACTs entered the decoder's cache
+
+
+def test_char_runs_shared_cache():
+    # xcodec/test/xcodec-encode-decode1: encoder and decoder share ONE cache.
+    from wanproxy_amd.xcgpu import Context, XCodecDecoder, XCodecEncoder
+    for ch in (0, 1, 0x7f, 0xf1, 0xff):
+        ctx = Context(0, cache_segments=1024)
+        run = bytes([ch]) * (2048 << 8)
+        enc = XCodecEncoder(ctx).encode(run)
+        assert len(enc) < len(run)
+        ok, out, consumed, unk = XCodecDecoder(ctx).decode(enc)
+        ctx.close()
+        assert ok and not unk and consumed == len(enc) and out == run
+
+
+def test_split_frames_across_calls(dctx, oracle):
+    # Decoding frame by frame (cache persists) == decoding the batch at once.
+    from wanproxy_amd.synth import chunks_of
+    d = data('kat_b')
+    offs, lens = chunks_of(d, 65536)
+    enc = oracle.encode_batch(d, offs, lens, mode=1)
+    dctx.cache_clear()
+    got = b''
+    i = 0
+    for step in (1, 2, 5, 8):
+        outs, st, cons, unk = dctx.decode_chunks(enc[i:i + step])
+        assert not unk and all(s == 0 for s in st)
+        got += b''.join(outs)
+        i += step
+    assert i == len(enc) and got == d
+
+
+def test_unknown_hashes_block_like_reference(dctx, oracle, ref_oracle):
+    # Decode a stream whose first frames are missing: the first REF to an
+    # unknown hash blocks; the ASK list is decode_skim's set.
+    from wanproxy_amd.synth import chunks_of
+    d = data('kat_a')
+    offs, lens = chunks_of(d, 65536)
+    enc = oracle.encode_batch(d, offs, lens, mode=1)
+    tail = enc[3:]
+    dctx.cache_clear()
+    outs, st, cons, unk = dctx.decode_chunks(tail)
+    # reference: one decode() over the concatenated frames
+    c = ref_oracle.cache_new()
+    ok, rout, rcons, runk = ref_oracle.decode(b''.join(tail), c)
+    ref_oracle.cache_free(c)
+    assert ok and runk
+    assert unk == sorted(runk)
+    k = int(np.nonzero(st == 1)[0][0])
+    assert all(s == 0 for s in st[:k]) and all(s == 2 for s in st[k + 1:])
+    assert b''.join(outs[:k + 1]) == rout
+    assert sum(len(e) for e in tail[:k]) + int(cons[k]) == rcons
+
+
+def test_partial_op_and_bad_opcode(dctx, oracle, ref_oracle):
+    from wanproxy_amd.xcgpu import XCodecDecoder
+    d = data('kat_a')
+    enc = oracle.encode_stream(d)
+    cut = enc.index(b'\xf1\x01', 5000) + 100
+    dctx.cache_clear()
+    ok, out, consumed, unk = XCodecDecoder(dctx).decode(enc[:cut])
+    c = ref_oracle.cache_new()
+    rok, rout, rcons, runk = ref_oracle.decode(enc[:cut], c)
+    ref_oracle.cache_free(c)
+    assert (ok, out, consumed, unk) == (rok, rout, rcons, runk)
+    dctx.cache_clear()
+    ok, out, consumed, unk = XCodecDecoder(dctx).decode(b'abc\xf1\x09def')
+    assert not ok and out == b'abc'
+
+
+def test_gpu_encode_gpu_decode_stream(dctx):
+    # End to end on the GPU: stream-encode C2-like data, decode with a fresh
+    # decoder cache, compare.
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import Context, XCG_SEM_STREAM
+    d = data('c2_small')
+    offs, lens = chunks_of(d, 65536)
+    ectx = Context(0, cache_segments=1 << 16)
+    enc = ectx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+    ectx.close()
+    dctx.cache_clear()
+    outs, st, cons, unk = dctx.decode_chunks(enc)
+    assert b''.join(outs) == d and not unk

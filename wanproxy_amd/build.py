@@ -6,14 +6,14 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_hash.hip']
+SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/xcg_hash.hip']
 OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(HERE, s) for s in SRCS]
-    deps = srcs + [os.path.join(HERE, 'csrc/xcg_device.h'), os.path.join(HERE, '..', 'include', 'xcgpu.h')]
+    deps = srcs + [os.path.join(HERE, 'csrc/xcg_device.h'), os.path.join(HERE, 'csrc/xcg_cache.h'), os.path.join(HERE, '..', 'include', 'xcgpu.h')]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     cmd = [HIPCC, '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',

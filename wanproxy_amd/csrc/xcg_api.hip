@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -53,6 +54,40 @@ struct XcgStreamArgs {
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
 
+struct XcgDecodeArgs {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* out_off;
+  uint64_t* out_len;
+  int32_t* chunk_status;
+  uint64_t* consumed;
+  int32_t* status;
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  uint64_t* x_keys;
+  uint64_t* x_vals;
+  uint64_t* x_latest;
+  uint32_t x_mask;
+  uint64_t* unknown;
+  uint64_t* unknown_pos;
+  uint32_t* nunknown;
+  uint32_t unknown_cap;
+  uint64_t* scratch;
+  uint64_t* h_scratch;
+};
+extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
+
 // The persistent segment cache of a context: XCodecMemoryCache's
 // hash_map<Tag64, BufferSegment*> (xcodec/xcodec_cache.h:270) as an
 // open-addressed table in HBM plus a segment pool, and the two lane-probe
@@ -82,6 +117,19 @@ struct BatchScratch {
   uint32_t* h_changed = nullptr;   // pinned
 };
 
+struct DecodeScratch {
+  uint32_t x_cap = 0;
+  uint64_t* x_keys = nullptr;
+  uint64_t* x_vals = nullptr;
+  uint64_t* x_latest = nullptr;
+  uint64_t* unknown = nullptr;
+  uint64_t* unknown_pos = nullptr;
+  uint32_t* nunknown = nullptr;
+  uint64_t* scratch = nullptr;
+  uint64_t* h_scratch = nullptr;   // pinned
+};
+constexpr uint32_t UNKNOWN_CAP = 1u << 16;
+
 struct xcg_ctx {
   int device;
   uint32_t flags;
@@ -90,6 +138,7 @@ struct xcg_ctx {
   GpuCache g;
   BatchScratch bs;
   int last_rounds;
+  DecodeScratch ds;
 };
 
 namespace {
@@ -176,6 +225,29 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
   return XCG_OK;
 }
 
+void free_dscratch(DecodeScratch& d) {
+  (void)hipFree(d.x_keys); (void)hipFree(d.x_vals); (void)hipFree(d.x_latest); (void)hipFree(d.unknown);
+  (void)hipFree(d.unknown_pos); (void)hipFree(d.nunknown); (void)hipFree(d.scratch);
+  if (d.h_scratch) (void)hipHostFree(d.h_scratch);
+  d = DecodeScratch{};
+}
+
+int ensure_dscratch(xcg_ctx* c, uint64_t max_extracts) {
+  DecodeScratch& d = c->ds;
+  const uint32_t cap = pow2_at_least(2 * max_extracts + 1024);
+  if (d.x_keys && cap <= d.x_cap) return XCG_OK;
+  free_dscratch(d);
+  d.x_cap = cap;
+  if (hipMalloc(&d.x_keys, 8ull * cap) != hipSuccess || hipMalloc(&d.x_vals, 8ull * cap) != hipSuccess ||
+      hipMalloc(&d.x_latest, 8ull * cap) != hipSuccess || hipMalloc(&d.unknown, 8ull * UNKNOWN_CAP) != hipSuccess ||
+      hipMalloc(&d.unknown_pos, 8ull * UNKNOWN_CAP) != hipSuccess || hipMalloc(&d.nunknown, 16) != hipSuccess ||
+      hipMalloc(&d.scratch, 64) != hipSuccess || hipHostMalloc(&d.h_scratch, 64) != hipSuccess) {
+    free_dscratch(d);
+    return XCG_ENOMEM;
+  }
+  return XCG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -207,7 +279,7 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
   if (flags & ~(XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) return XCG_EINVAL;
   DeviceGuard g(device);
-  xcg_ctx* c = new xcg_ctx{device, flags, nullptr, cache_segments, GpuCache{}, BatchScratch{}, 0};
+  xcg_ctx* c = new xcg_ctx{device, flags, nullptr, cache_segments, GpuCache{}, BatchScratch{}, 0, DecodeScratch{}};
   if (hipMalloc(&c->d_status, 16) != hipSuccess) {
     delete c;
     return XCG_ENOMEM;
@@ -227,6 +299,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   (void)hipFree(c->d_status);
   free_cache(c->g);
   free_scratch(c->bs);
+  free_dscratch(c->ds);
   delete c;
 }
 
@@ -282,14 +355,14 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
   DeviceGuard g(c->device);
   // A null cache has no state to carry: both semantics are the same pass.
   if (semantics == XCG_SEM_STREAM && !(c->flags & XCG_FLAG_NULLCACHE)) {
-    if (max_chunk_len > (1u << 17)) return XCG_ENOTSUP;
+    const uint32_t maxd = max_chunk_len > (1u << 17) ? 264 : 72;
     int rc = ensure_cache(c);
-    if (rc == XCG_OK) rc = ensure_scratch(c, n, 72);
+    if (rc == XCG_OK) rc = ensure_scratch(c, n, maxd);
     if (rc != XCG_OK) return rc;
     XcgStreamArgs a{d_in, d_chunk_off, d_chunk_len, n, c->flags, d_out, d_out_off, d_out_len, d_stats,
                     c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                     c->g.filt, c->g.ftab, c->g.fmask, c->bs.b_keys, c->bs.b_vals, c->bs.b_mask,
-                    c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, 72, c->bs.changed, c->bs.h_changed};
+                    c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed};
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
     c->last_rounds = rounds;
@@ -360,6 +433,105 @@ int xcg_encode_host(xcg_ctx* c, int semantics, const uint8_t* h_in, uint64_t in_
   (void)hipFree(d_oo);
   (void)hipFree(d_ol);
   (void)hipFree(d_len);
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
+int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_off, const uint32_t* d_chunk_len,
+                     uint32_t n, uint32_t max_chunk_len, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                     uint64_t* d_out_len, int32_t* d_chunk_status, uint64_t* d_consumed, uint64_t* h_unknown,
+                     uint32_t unknown_cap, uint32_t* h_nunknown, uint64_t* h_total_out, void* stream) {
+  if (!c || (n && (!d_enc || !d_chunk_off || !d_chunk_len || !d_out_off || !d_out_len || !d_chunk_status ||
+                   !d_consumed)))
+    return XCG_EINVAL;
+  if (h_nunknown) *h_nunknown = 0;
+  if (h_total_out) *h_total_out = 0;
+  if (n == 0) return XCG_OK;
+  DeviceGuard g(c->device);
+  int rc = ensure_cache(c);
+  if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));
+  if (rc != XCG_OK) return rc;
+  XcgDecodeArgs a{d_enc, d_chunk_off, d_chunk_len, n, d_out, out_cap, d_out_off, d_out_len, d_chunk_status,
+                  d_consumed, c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
+                  c->g.filt, c->g.ftab, c->g.fmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
+                  c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch};
+  uint64_t total = 0, blockp = 0;
+  uint32_t nunk = 0;
+  const int lrc = xcg_launch_decode(&a, &total, &blockp, &nunk, (hipStream_t)stream);
+  if (h_total_out) *h_total_out = total;
+  if (lrc == -75) return XCG_EOVERFLOW;
+  if (lrc != 0) return XCG_EHIP;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return XCG_EHIP;
+  int32_t st = 0;
+  if (hipMemcpy(&st, c->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+  if (st & ((1 << 8) | (1 << 9))) {
+    (void)hipMemset(c->d_status, 0, 4);
+    return XCG_ENOTSUP;
+  }
+  if (nunk) {
+    // XCodecDecoder::decode_skim (xcodec/xcodec_decoder.cc:196-272): every
+    // REF from the blocking point on that cannot resolve, as a sorted set.
+    const uint32_t m = nunk < UNKNOWN_CAP ? nunk : UNKNOWN_CAP;
+    std::vector<uint64_t> hs(m);
+    if (hipMemcpy(hs.data(), c->ds.unknown, 8ull * m, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+    std::sort(hs.begin(), hs.end());
+    hs.erase(std::unique(hs.begin(), hs.end()), hs.end());
+    const uint32_t k = (uint32_t)hs.size() < unknown_cap ? (uint32_t)hs.size() : unknown_cap;
+    if (h_unknown) memcpy(h_unknown, hs.data(), 8ull * k);
+    if (h_nunknown) *h_nunknown = k;
+  }
+  return XCG_OK;
+}
+
+int xcg_decode_host(xcg_ctx* c, const uint8_t* h_enc, uint64_t enc_len, const uint64_t* h_chunk_off,
+                    const uint32_t* h_chunk_len, uint32_t n, uint8_t* h_out, uint64_t out_cap, uint64_t* h_out_off,
+                    uint64_t* h_out_len, int32_t* h_chunk_status, uint64_t* h_consumed, uint64_t* h_unknown,
+                    uint32_t unknown_cap, uint32_t* h_nunknown) {
+  if (!c || (n && (!h_enc || !h_chunk_off || !h_chunk_len || !h_out_off || !h_out_len || !h_chunk_status ||
+                   !h_consumed)))
+    return XCG_EINVAL;
+  if (n == 0) return XCG_OK;
+  uint32_t maxlen = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (h_chunk_off[i] + h_chunk_len[i] > enc_len) return XCG_EINVAL;
+    if (h_chunk_len[i] > maxlen) maxlen = h_chunk_len[i];
+  }
+  DeviceGuard g(c->device);
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  uint64_t *d_off = nullptr, *d_oo = nullptr, *d_ol = nullptr, *d_cons = nullptr;
+  uint32_t* d_len = nullptr;
+  int32_t* d_st = nullptr;
+  hipStream_t st = nullptr;
+  int rc = XCG_OK;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
+  do {
+    if (hipMalloc(&d_in, enc_len ? enc_len : 1) != hipSuccess || hipMalloc(&d_out, out_cap ? out_cap : 1) != hipSuccess ||
+        hipMalloc(&d_off, 8ull * n) != hipSuccess || hipMalloc(&d_oo, 8ull * n) != hipSuccess ||
+        hipMalloc(&d_ol, 8ull * n) != hipSuccess || hipMalloc(&d_cons, 8ull * n) != hipSuccess ||
+        hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_st, 4ull * n) != hipSuccess) {
+      rc = XCG_ENOMEM;
+      break;
+    }
+    if (hipMemcpyAsync(d_in, h_enc, enc_len, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_off, h_chunk_off, 8ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_len, h_chunk_len, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = XCG_EHIP;
+      break;
+    }
+    uint64_t total = 0;
+    rc = xcg_decode_batch(c, d_in, d_off, d_len, n, maxlen, d_out, out_cap, d_oo, d_ol, d_st, d_cons, h_unknown,
+                          unknown_cap, h_nunknown, &total, st);
+    if (rc != XCG_OK) break;
+    if (hipMemcpyAsync(h_out_off, d_oo, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_out_len, d_ol, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_chunk_status, d_st, 4ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_consumed, d_cons, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_out, d_out, total < out_cap ? total : out_cap, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      rc = XCG_EHIP;
+  } while (0);
+  (void)hipFree(d_in); (void)hipFree(d_out); (void)hipFree(d_off); (void)hipFree(d_oo); (void)hipFree(d_ol);
+  (void)hipFree(d_cons); (void)hipFree(d_len); (void)hipFree(d_st);
   (void)hipStreamDestroy(st);
   return rc;
 }

@@ -1,0 +1,479 @@
+// XCodec decoder, MI355X (gfx950) HIP kernels.
+//
+// Restates XCodecDecoder::decode (xcodec/xcodec_decoder.cc:66-188) for a batch
+// of encoded chunks that form ONE stream (successive decode() calls on one
+// decoder and cache, e.g. tack -d, programs/tack/tack.cc:329-359, or the
+// frames of one XCodecPipePair, xcodec/xcodec_pipe_pair.cc:425-483).
+//
+//   scan   (one wave per chunk): walk the op stream.  Literal runs are found
+//          1 KiB at a time with a wave ballot over the bytes: an 0xF1 followed
+//          by 0x00 is an ESCAPE inside the run, any other 0xF1 starts an op.
+//          EXTRACT payloads are hashed (XCodecHash::hash, :106) and entered in
+//          the batch table X: hash -> earliest / latest stream position.
+//   size   exclusive scan of the decoded lengths -> output offsets.
+//   emit   (one wave per chunk): walk again and write: literal runs with
+//          F1 00 -> F1, EXTRACT payloads, REF segments gathered from the
+//          earliest earlier EXTRACT in the batch or from the persistent cache
+//          (the cache state at that point of the stream, :151-162).  A REF
+//          that neither resolves blocks the stream there (:151-156).
+//   commit EXTRACTs before the blocking point enter the cache
+//          (XCodecMemoryCache::enter / replace, :120-136).
+//
+// BACKREF (:165-181) is never produced by XCodecEncoder (it only declares into
+// its window); streams containing it are rejected with XCG_ENOTSUP.
+#include "xcg_cache.h"
+
+namespace xcg {
+
+struct DecParams {
+  const uint8_t* in;           // encoded chunks
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  HashTab g;                   // persistent cache
+  const uint8_t* pool;
+  HashTab x;                   // batch EXTRACT table: hash -> (earliest, latest) packed positions
+  uint64_t* x_latest;          // parallel to x.vals: latest position (atomicMax)
+  uint64_t* out_len;           // scan: tentative decoded length; emit: final
+  const uint64_t* out_off;     // emit: exclusive scan of scan's out_len
+  uint8_t* out;
+  int32_t* chunk_status;       // 0 ok, 1 blocked (unknown REF), 2 not reached, 3 partial op at end, <0 error
+  uint64_t* consumed;          // input bytes fully parsed per chunk
+  uint64_t* unknown;           // emit: unresolvable REFs (hash), with their positions
+  uint64_t* unknown_pos;
+  uint32_t* nunknown;
+  uint32_t unknown_cap;
+  uint64_t* block_pos;         // min stream position of an unresolvable REF (atomicMin)
+  int32_t* status;             // bit 8: BACKREF seen, bit 9: EXTRACT name reuse inside the batch
+};
+
+__device__ __forceinline__ uint64_t spos(uint32_t chunk, uint32_t off) { return ((uint64_t)chunk << 32) | off; }
+
+// Next real op at or after i in x[0..len): an 0xF1 not followed by 0x00.
+// Returns its position (or len) and the number of ESCAPE pairs before it.
+__device__ __forceinline__ uint32_t next_op(const uint8_t* x, uint32_t i, uint32_t len, uint32_t& nesc) {
+  const int l = lane_id();
+  nesc = 0;
+  // Fast path: the op follows immediately (EXTRACT/REF-dense streams).
+  if (i < len && x[i] == MAGIC && (i + 1 >= len || x[i + 1] != 0u)) return i;
+  for (uint32_t base = i; base < len; base += 1024) {
+    const uint32_t off = base + 16u * l;
+    uint32_t opmask = 0, escmask = 0;
+    if (off < len) {
+      const uint32_t cnt = min(16u, len - off);
+      uint32_t b[17];
+#pragma unroll
+      for (int k = 0; k < 17; ++k) b[k] = (off + k < len) ? (uint32_t)x[off + k] : 0x100u;  // 0x100: past the end
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if ((uint32_t)k < cnt && b[k] == MAGIC) {
+          if (b[k + 1] == 0u) escmask |= 1u << k;
+          else opmask |= 1u << k;
+        }
+      }
+    }
+    // An ESCAPE's 0x00 is never itself scanned as a byte that matters (it is
+    // not 0xF1), so the masks are exact.  First op in this window:
+    const uint64_t bal = ballot(opmask != 0u);
+    if (bal) {
+      const int lw = __builtin_ctzll(bal);
+      const uint32_t om = readlane(opmask, lw);
+      const uint32_t pos = base + 16u * lw + __builtin_ctz(om);
+      // escapes strictly before pos
+      uint32_t e = (uint32_t)l < (uint32_t)lw ? __builtin_popcount(escmask)
+                   : ((uint32_t)l == (uint32_t)lw ? __builtin_popcount(escmask & ((1u << __builtin_ctz(om)) - 1u)) : 0u);
+      nesc += wave_sum(e);
+      return pos;
+    }
+    nesc += wave_sum(__builtin_popcount(escmask));
+  }
+  return len;
+}
+
+// Copy the literal run x[a..b) (which contains only ESCAPE pairs) to dst with
+// F1 00 -> F1.  Returns bytes written.
+__device__ __noinline__ uint32_t wave_unescape(uint8_t* dst, const uint8_t* x, uint32_t a, uint32_t b) {
+  const int l = lane_id();
+  uint32_t written = 0;
+  // An escape pair never straddles 16-byte lanes ambiguously: a 0x00 is an
+  // escape zero iff the byte before it is 0xF1 (runs hold no other 0xF1).
+  for (uint32_t base = a; base < b; base += 1024) {
+    const uint32_t off = base + 16u * l;
+    uint32_t cnt = off < b ? min(16u, b - off) : 0u;
+    uint32_t v[16];
+    uint32_t prev = (off > a && off - 1 < b) ? (uint32_t)x[off - 1] : 0u;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k] = ((uint32_t)k < cnt) ? (uint32_t)x[off + k] : 0u;
+      const bool drop = (uint32_t)k < cnt && v[k] == 0u && prev == MAGIC;
+      if ((uint32_t)k < cnt && !drop) keep |= 1u << k;
+      prev = drop ? 0u : v[k];   // F1 00 F1 00: the 00 resets
+    }
+    const uint32_t nk = __builtin_popcount(keep);
+    const uint32_t incl = wave_incl_scan(nk);
+    uint32_t o = written + incl - nk;
+    if (nk == 16u && cnt == 16u) {
+      u32x4 w;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = v[4 * q] | (v[4 * q + 1] << 8) | (v[4 * q + 2] << 16) | (v[4 * q + 3] << 24);
+      *(u32x4_u*)(dst + o) = w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((keep >> k) & 1u) dst[o++] = (uint8_t)v[k];
+    }
+    written += readlane(incl, 63);
+  }
+  return written;
+}
+
+__device__ __noinline__ uint2 dec_window_hash(const uint8_t* w) {
+  const int l = lane_id();
+  uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t k0 = 1024u * h + 16u * l;
+    const u32x4 v = *(const u32x4_u*)(w + k0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t c = byte_of(v[k >> 2], k & 3);
+      const uint32_t f = ffbl(c) + 1u;
+      const uint32_t wt = 2048u - (k0 + k);
+      X1 += c; X2 += wt * c; F1 += f; F2 += wt * f;
+    }
+  }
+  X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
+  return make_uint2((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4);
+}
+
+__device__ __forceinline__ void wave_copy2048(uint8_t* dst, const uint8_t* src) {
+  const int l = lane_id();
+  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+}
+
+__device__ __noinline__ bool dec_equal2048(const uint8_t* a, const uint8_t* b) {
+  const int l = lane_id();
+  const u32x4 a0 = *(const u32x4_u*)(a + 32 * l), a1 = *(const u32x4_u*)(a + 32 * l + 16);
+  const u32x4 b0 = *(const u32x4_u*)(b + 32 * l), b1 = *(const u32x4_u*)(b + 32 * l + 16);
+  const bool ok = a0[0] == b0[0] && a0[1] == b0[1] && a0[2] == b0[2] && a0[3] == b0[3] && a1[0] == b1[0] &&
+                  a1[1] == b1[1] && a1[2] == b1[2] && a1[3] == b1[3];
+  return ballot(!ok) == 0;
+}
+
+__device__ __forceinline__ uint64_t be64(const uint8_t* p) {
+  uint64_t h = 0;
+  for (int k = 0; k < 8; ++k) h = (h << 8) | p[k];
+  return h;
+}
+
+// Batch table insert with earliest (vals, atomicMin) and latest (atomicMax).
+__device__ __forceinline__ bool xtab_insert(HashTab t, uint64_t* latest, uint32_t lo, uint32_t hi, uint64_t pos,
+                                            bool& existed) {
+  const uint64_t key = ((uint64_t)hi << 32) | lo;
+  uint32_t i = tab_slot(lo, hi, t.mask);
+  for (uint32_t n = 0; n <= t.mask; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&t.keys[i], (unsigned long long)EMPTY_KEY,
+                                    (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) {
+      existed = prev == key;
+      atomicMin((unsigned long long*)&t.vals[i], (unsigned long long)pos);
+      atomicMax((unsigned long long*)&latest[i], (unsigned long long)pos);
+      return true;
+    }
+    i = (i + 1) & t.mask;
+  }
+  return false;
+}
+
+// ------------------------------------------------------------------ kernels
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  const int l = lane_id();
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const uint32_t len = prm.chunk_len[chunk];
+  uint8_t* out = EMIT ? prm.out + prm.out_off[chunk] : nullptr;
+  uint64_t olen = 0;
+  int32_t st = 0;
+  uint32_t i = 0;
+  const uint64_t blockp = EMIT ? readfirst64(*prm.block_pos) : ~0ull;
+  if (EMIT && spos(chunk, 0) > blockp) {      // after the blocking REF: decode() never got here
+    if (l == 0) {
+      prm.out_len[chunk] = 0;
+      prm.chunk_status[chunk] = 2;
+      prm.consumed[chunk] = 0;
+    }
+    return;
+  }
+
+  while (i < len) {
+    uint32_t nesc = 0;
+    const uint32_t m = next_op(x, i, len, nesc);
+    // literal run [i, m) with nesc escape pairs (:71-81 and OP_ESCAPE :91-94)
+    if (m > i) {
+      if (EMIT) olen += readfirst(wave_unescape(out + olen, x, i, m));
+      else olen += (m - i) - nesc;
+    }
+    i = m;
+    if (i >= len) break;
+    if (len - i == 1) { st = 3; break; }                     // :87-88 need the op byte
+    const uint32_t op = x[i + 1];
+    if (op == OP_EXTRACT) {                                  // :96-140
+      if (len - i < 2u + SEG) { st = 3; break; }
+      const uint8_t* seg = x + i + 2;
+      if (EMIT) {
+        wave_copy2048(out + olen, seg);
+      } else {
+        const uint2 h = dec_window_hash(seg);
+        bool existed = false;
+        if (l == 0 && !xtab_insert(prm.x, prm.x_latest, readfirst(h.x), readfirst(h.y), spos(chunk, i + 2),
+                                   existed))
+          atomicOr(prm.status, 1 << 10);
+        (void)existed;
+      }
+      olen += SEG;
+      i += 2 + SEG;
+    } else if (op == OP_REF) {                               // :141-163
+      if (len - i < 10u) { st = 3; break; }
+      const uint64_t h = be64(x + i + 2);
+      const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+      if (EMIT) {
+        const uint64_t here = spos(chunk, i);
+        if (here >= blockp) { st = 1; break; }               // blocked at or before this op
+        const uint8_t* src = nullptr;
+        const uint64_t e = tab_lookup(prm.x, lo, hi);        // earliest EXTRACT of h in the batch
+        if (e != ~0ull && e < here) src = prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
+        if (src == nullptr) {
+          const uint64_t gv = tab_lookup(prm.g, lo, hi);
+          if (gv != ~0ull) src = prm.pool + gv * (uint64_t)SEG;
+        }
+        if (src == nullptr) { st = 1; break; }               // cannot happen: scan found all
+        wave_copy2048(out + olen, src);
+      } else {
+        // Resolvable iff an earlier EXTRACT of h exists in the batch or the
+        // cache holds h; the scan only records the unresolvable ones (the
+        // batch table is complete only after the scan, so defer the check).
+      }
+      olen += SEG;
+      i += 10;
+    } else if (op == OP_BACKREF) {
+      if (l == 0) atomicOr(prm.status, 1 << 8);
+      st = -2;
+      break;
+    } else {
+      st = -1;                                               // :183-184 unsupported opcode
+      break;
+    }
+  }
+  if (l == 0) {
+    prm.out_len[chunk] = olen;
+    if (EMIT) {
+      prm.chunk_status[chunk] = st;
+      prm.consumed[chunk] = i;
+    }
+  }
+}
+
+// Between scan and emit: find unresolvable REFs (no earlier EXTRACT of the
+// hash in the batch, not in the cache) and the first such stream position.
+// One wave per chunk; walks only the op headers.
+__global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const uint32_t len = prm.chunk_len[chunk];
+  uint32_t i = 0;
+  while (i < len) {
+    uint32_t nesc = 0;
+    i = next_op(x, i, len, nesc);
+    if (i + 1 >= len) break;
+    const uint32_t op = x[i + 1];
+    if (op == OP_EXTRACT) {
+      if (len - i < 2u + SEG) break;
+      i += 2 + SEG;
+    } else if (op == OP_REF) {
+      if (len - i < 10u) break;
+      const uint64_t h = be64(x + i + 2);
+      const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+      const uint64_t here = spos(chunk, i);
+      const uint64_t e = tab_lookup(prm.x, lo, hi);
+      bool ok = e != ~0ull && e < here;
+      if (!ok) ok = tab_lookup(prm.g, lo, hi) != ~0ull;
+      if (!ok && lane_id() == 0) {
+        atomicMin((unsigned long long*)prm.block_pos, (unsigned long long)here);
+        const uint32_t k = atomicAdd(prm.nunknown, 1u);
+        if (k < prm.unknown_cap) {
+          prm.unknown[k] = h;
+          prm.unknown_pos[k] = here;
+        }
+      }
+      i += 10;
+    } else {
+      break;
+    }
+  }
+}
+
+// Exclusive scan of n u64 lengths (single workgroup; n up to a few million).
+__global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint64_t* len, uint64_t* off, uint32_t n,
+                                                             uint64_t* total) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t a = min(n, t * per), b = min(n, a + per);
+  uint64_t s = 0;
+  for (uint32_t i = a; i < b; ++i) s += len[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  for (uint32_t i = a; i < b; ++i) {
+    off[i] = run;
+    run += len[i];
+  }
+  if (t == 1023) *total = part[1023];
+}
+
+// Commit: every batch EXTRACT hash whose latest occurrence precedes the
+// blocking point enters the cache (enter, or replace on name reuse).
+// One wave per batch-table slot group.
+__global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8_t* pool, uint32_t* nseg,
+                                                            uint32_t seg_cap, uint32_t* filt, uint32_t* ftab,
+                                                            uint32_t fmask) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w > prm.x.mask) return;
+  const uint64_t key = readfirst64(prm.x.keys[w]);
+  if (key == EMPTY_KEY) return;
+  const uint64_t first = readfirst64(prm.x.vals[w]), last = readfirst64(prm.x_latest[w]);
+  const uint64_t blockp = readfirst64(*prm.block_pos);
+  if (first >= blockp) return;                 // never reached
+  if (last >= blockp && last != first) {       // several EXTRACTs straddle the block: not modelled
+    if (lane_id() == 0) atomicOr(prm.status, 1 << 9);
+    return;
+  }
+  const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+  const uint8_t* src = prm.in + prm.chunk_off[last >> 32] + (uint32_t)last;
+  if (last != first) {
+    // name reuse inside the batch with different bytes would need per-REF
+    // resolution of the latest EXTRACT; the emit pass used the earliest.
+    const uint8_t* s0 = prm.in + prm.chunk_off[first >> 32] + (uint32_t)first;
+    if (!readfirst((uint32_t)dec_equal2048(s0, src))) {
+      if (lane_id() == 0) atomicOr(prm.status, 1 << 9);
+    }
+  }
+  const uint64_t gv = tab_lookup(prm.g, lo, hi);
+  if (gv != ~0ull) {
+    uint8_t* dst = pool + gv * (uint64_t)SEG;
+    if (!readfirst((uint32_t)dec_equal2048(dst, src))) wave_copy2048(dst, src);   // replace (:130)
+    return;
+  }
+  uint32_t seg = 0;
+  if (lane_id() == 0) seg = atomicAdd(nseg, 1u);
+  seg = readfirst(seg);
+  if (seg >= seg_cap) {
+    if (lane_id() == 0) atomicOr(prm.status, 4);
+    return;
+  }
+  wave_copy2048(pool + (uint64_t)seg * SEG, src);
+  if (lane_id() == 0) {
+    if (!tab_insert_min(prm.g, lo, hi, seg)) atomicOr(prm.status, 2);
+    filt_insert(filt, lo, hi);
+    ftab_insert(ftab, fmask, lo, hi);
+  }
+}
+
+}  // namespace xcg
+
+struct XcgDecodeArgs {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* out_off;
+  uint64_t* out_len;
+  int32_t* chunk_status;
+  uint64_t* consumed;
+  int32_t* status;
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  uint64_t* x_keys;
+  uint64_t* x_vals;
+  uint64_t* x_latest;
+  uint32_t x_mask;
+  uint64_t* unknown;
+  uint64_t* unknown_pos;
+  uint32_t* nunknown;
+  uint32_t unknown_cap;
+  uint64_t* scratch;     // [0] total, [1] block_pos
+  uint64_t* h_scratch;   // pinned: [0] total, [1] block_pos, [2] nunknown
+};
+
+extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, uint64_t* block_pos_out,
+                                 uint32_t* nunknown_out, hipStream_t stream) {
+  using namespace xcg;
+  const uint32_t n = a->n;
+  DecParams p{};
+  p.in = a->in;
+  p.chunk_off = a->chunk_off;
+  p.chunk_len = a->chunk_len;
+  p.n = n;
+  p.g = HashTab{a->g_keys, a->g_vals, a->g_mask};
+  p.pool = a->pool;
+  p.x = HashTab{a->x_keys, a->x_vals, a->x_mask};
+  p.x_latest = a->x_latest;
+  p.out_len = a->out_len;
+  p.out_off = a->out_off;
+  p.out = a->out;
+  p.chunk_status = a->chunk_status;
+  p.consumed = a->consumed;
+  p.unknown = a->unknown;
+  p.unknown_pos = a->unknown_pos;
+  p.nunknown = a->nunknown;
+  p.unknown_cap = a->unknown_cap;
+  p.block_pos = a->scratch + 1;
+  p.status = a->status;
+  const dim3 grid((n + 3) / 4), block(256);
+  if (hipMemsetAsync(a->x_keys, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
+      hipMemsetAsync(a->x_vals, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
+      hipMemsetAsync(a->x_latest, 0, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
+      hipMemsetAsync(a->scratch + 1, 0xFF, 8, stream) != hipSuccess ||
+      hipMemsetAsync(a->nunknown, 0, 4, stream) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(decode_kernel<false>, grid, block, 0, stream, p);
+  hipLaunchKernelGGL(decode_refcheck_kernel, grid, block, 0, stream, p);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)a->out_len, a->out_off,
+                     n, a->scratch);
+  if (hipMemcpyAsync(a->h_scratch, a->scratch, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipMemcpyAsync(a->h_scratch + 2, a->nunknown, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return -5;
+  *total_out = a->h_scratch[0];
+  *block_pos_out = a->h_scratch[1];
+  *nunknown_out = (uint32_t)a->h_scratch[2];
+  if (*total_out > a->out_cap) return -75;
+  hipLaunchKernelGGL(decode_kernel<true>, grid, block, 0, stream, p);
+  const uint64_t slots = (uint64_t)a->x_mask + 1;
+  hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots * 64 + 255) / 256)), dim3(256), 0, stream, p,
+                     a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

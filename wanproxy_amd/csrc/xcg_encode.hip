@@ -632,8 +632,7 @@ __global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) 
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
 // the lane filter; each wave walks chunks wave_id, wave_id + total_waves, ...
-constexpr int SW = 12;
-template <int LOGNB, int MAXD>
+template <int LOGNB, int MAXD, int SW>
 __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   __shared__ uint32_t lfilt[FILT_WORDS];
   __shared__ WaveTable<LOGNB, MAXD> tabs[SW];
@@ -648,7 +647,8 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
 
 template __global__ void encode_independent_kernel<9, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
-template __global__ void encode_stream_kernel<8, 72>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 12>(EncParams);
+template __global__ void encode_stream_kernel<11, 264, 2>(EncParams);
 
 }  // namespace xcg
 
@@ -772,12 +772,18 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   hipDeviceProp_t props;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&props, dev) != hipSuccess) return -5;
   const uint32_t wgs = (uint32_t)props.multiProcessorCount;
-  const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
+  const bool big = a->maxd > 72;                     // chunks > 128 KiB (<= 512 KiB frames)
+  const uint32_t SW = big ? 2 : 12;
+  const dim3 sgrid(min(wgs * (big ? 2u : 1u), (n + SW - 1) / SW)), sblock(64 * SW);
+  auto launch = [&]() {
+    if (big) hipLaunchKernelGGL((encode_stream_kernel<11, 264, 2>), sgrid, sblock, 0, stream, prm);
+    else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 12>), sgrid, sblock, 0, stream, prm);
+  };
   if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess) return -5;
   // Round 0: every chunk against the persistent cache + its own declarations.
   prm.use_b = false;
   prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask};
-  hipLaunchKernelGGL((encode_stream_kernel<8, 72>), sgrid, sblock, 0, stream, prm);
+  launch();
   int rounds = 1;
   // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
   // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
@@ -796,7 +802,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
                        a->fmask, a->status);
     prm.use_b = true;
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask};
-    hipLaunchKernelGGL((encode_stream_kernel<8, 72>), sgrid, sblock, 0, stream, prm);
+    launch();
     ++rounds;
     if (hipMemcpyAsync(a->h_changed, a->changed, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)

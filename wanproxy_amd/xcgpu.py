@@ -66,6 +66,9 @@ def lib():
     L.xcg_encode_batch.restype = C.c_int
     L.xcg_encode_host.argtypes = [vp, C.c_int, u8p, C.c_uint64, u64p, u32p, C.c_uint32, u8p, C.c_uint64, u64p, u64p]
     L.xcg_encode_host.restype = C.c_int
+    L.xcg_decode_batch.argtypes = [vp, u8p, u64p, u32p, C.c_uint32, C.c_uint32, u8p, C.c_uint64, u64p, u64p, vp, u64p,
+                                   u64p, C.c_uint32, vp, u64p, vp]
+    L.xcg_decode_batch.restype = C.c_int
     L.xcg_window_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
     L.xcg_window_hashes.restype = C.c_int
     L.xcg_segment_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
@@ -169,6 +172,43 @@ class Context:
             return res, d_st.cpu().numpy().view(np.uint32).reshape(n, 4)
         return res
 
+    def decode_chunks(self, encs):
+        """Decode encoded chunks (one stream, this context's cache) on the GPU.
+        Returns (outs, status, consumed, unknown) -- see xcg_decode_batch."""
+        import torch
+        dev = torch.device('cuda', self.device)
+        n = len(encs)
+        lens = np.array([len(e) for e in encs], dtype=np.uint32)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        blob = np.frombuffer(b''.join(encs) or b'\0', dtype=np.uint8)
+        d_in = torch.from_numpy(blob.copy()).to(dev)
+        d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        d_oo = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_ol = torch.zeros(n, dtype=torch.int64, device=dev)
+        d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+        d_cons = torch.zeros(n, dtype=torch.int64, device=dev)
+        cap = int(lens.astype(np.uint64).sum()) * 205 + 4096   # a 10-byte REF expands to 2048
+        d_out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        unk = np.zeros(1 << 16, dtype=np.uint64)
+        nunk = np.zeros(1, dtype=np.uint32)
+        total = np.zeros(1, dtype=np.uint64)
+        _check(lib().xcg_decode_batch(
+            self.h, C.c_void_p(d_in.data_ptr()), C.c_void_p(d_off.data_ptr()), C.c_void_p(d_len.data_ptr()), n,
+            int(lens.max()) if n else 0, C.c_void_p(d_out.data_ptr()), cap, C.c_void_p(d_oo.data_ptr()),
+            C.c_void_p(d_ol.data_ptr()), C.c_void_p(d_st.data_ptr()), C.c_void_p(d_cons.data_ptr()),
+            unk.ctypes.data, unk.size, nunk.ctypes.data, total.ctypes.data, _stream_ptr(None)))
+        torch.cuda.synchronize(dev)
+        oo = d_oo.cpu().numpy()
+        ol = d_ol.cpu().numpy()
+        st = d_st.cpu().numpy()
+        cons = d_cons.cpu().numpy()
+        out = d_out.cpu().numpy()
+        outs = [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] != 2 else b'' for i in range(n)]
+        return outs, st, cons, [int(u) for u in unk[:int(nunk[0])]]
+
     def window_hashes(self, data) -> np.ndarray:
         import torch
         dev = torch.device('cuda', self.device)
@@ -210,3 +250,19 @@ class XCodecEncoder:
         if not data:
             return b''
         return self.ctx.encode_chunks(data, np.array([0]), np.array([len(data)]), semantics=XCG_SEM_STREAM)[0]
+
+
+class XCodecDecoder:
+    """Mirror of XCodecDecoder(XCodecCache*) (xcodec/xcodec_decoder.h:35-45):
+    decode(input) -> (ok, output, consumed, unknown_hashes), where `consumed`
+    is how much of `input` decode() removed (a partial op stays) and
+    `unknown_hashes` the sorted set an ASK would request."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def decode(self, data: bytes):
+        if not data:
+            return True, b'', 0, []
+        outs, st, cons, unk = self.ctx.decode_chunks([data])
+        return int(st[0]) >= 0, outs[0], int(cons[0]), unk
