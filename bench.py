@@ -40,6 +40,7 @@ def parse():
     ap.add_argument('--chunks', type=int, default=NCHUNKS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-passes', type=int, default=8)
+    ap.add_argument('--no-extras', action='store_true', help='skip the stream / decode / PCIe side measurements')
     return ap.parse_args()
 
 
@@ -73,6 +74,114 @@ def cpu_baseline(data: np.ndarray, offs, lens, passes: int):
     return {'value': round(gib / dt, 4), 'unit': 'GiB/s', 'cores': threads, 'kind': kind,
             'sample': f'{passes} passes over the full {n} x 64 KiB batch ({total / 2**20:.0f} MiB), '
                       f'{threads} threads x contiguous shards, fresh XCodecMemoryCache per chunk; {dt:.1f} s wall'}
+
+
+def timed(fn, steps, stream):
+    import torch
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, ev0.elapsed_time(ev1) / steps * 1e-3
+
+
+def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, d_st, n, stream, dev, rank):
+    """Same C2 batch under stream semantics (one cache, chunk order), its GPU
+    decode, and the host-inclusive (PCIe) encode rate.  Each is checked."""
+    import torch
+    from oracle.lib import Oracle
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    in_bytes = int(lens.astype(np.int64).sum())
+    res = {}
+    # -- stream semantics: every step starts from an empty cache
+    sctx = Context(dev.index, cache_segments=1 << 18)
+
+    def s2():
+        sctx.cache_clear()
+        sctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream,
+                                 semantics=XCG_SEM_STREAM)
+    wall, _ = timed(s2, 5, stream)
+    sctx.status()
+    ol = d_ol.cpu().numpy()
+    outh = d_out.cpu().numpy()
+    oo = d_oo.cpu().numpy()
+    enc = [outh[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)]
+    k = min(n, 256)                       # sequential oracle on a prefix (same stream order)
+    exp = Oracle().encode_batch(data, offs[:k], lens[:k], mode=1)
+    if enc[:k] != exp:
+        raise SystemExit('PARITY FAILURE (stream semantics)')
+    res['stream_semantics'] = {'metric': 'XCodec encode GiB/s, one cache across the batch (tack loop order)',
+                               'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
+                               'rounds': sctx.last_rounds(), 'out_in_ratio': round(int(ol.sum()) / in_bytes, 5),
+                               'includes': 'cache clear + Jacobi rounds + commit'}
+    # -- decode of that stream with a fresh decoder cache
+    dctx = Context(dev.index, cache_segments=1 << 18)
+    elens = ol.astype(np.uint32)
+    eoffs = np.zeros(n, dtype=np.uint64)
+    eoffs[1:] = np.cumsum(elens.astype(np.uint64))[:-1]
+    blob = np.concatenate([np.frombuffer(e, np.uint8) for e in enc])
+    d_enc = torch.from_numpy(blob).to(dev)
+    d_eoff = torch.from_numpy(eoffs.view(np.int64)).to(dev)
+    d_elen = torch.from_numpy(elens.view(np.int32)).to(dev)
+    d_dout = torch.empty(in_bytes + 4096, dtype=torch.uint8, device=dev)
+    d_doo = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_dol = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_dst = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_dcons = torch.zeros(n, dtype=torch.int64, device=dev)
+    import ctypes as C
+    from wanproxy_amd.xcgpu import _check, lib
+    unk = np.zeros(16, np.uint64)
+    nunk = np.zeros(1, np.uint32)
+    tot = np.zeros(1, np.uint64)
+
+    def dec():
+        dctx.cache_clear()
+        _check(lib().xcg_decode_batch(dctx.h, C.c_void_p(d_enc.data_ptr()), C.c_void_p(d_eoff.data_ptr()),
+                                      C.c_void_p(d_elen.data_ptr()), n, int(elens.max()),
+                                      C.c_void_p(d_dout.data_ptr()), d_dout.numel(), C.c_void_p(d_doo.data_ptr()),
+                                      C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
+                                      C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
+                                      tot.ctypes.data, C.c_void_p(stream.cuda_stream)))
+    wall, _ = timed(dec, 5, stream)
+    if int(tot[0]) != in_bytes or d_dout[:in_bytes].cpu().numpy().tobytes() != data.tobytes():
+        raise SystemExit('PARITY FAILURE (decode round trip)')
+    res['decode'] = {'metric': 'XCodec decode GiB/s of decoded bytes (that stream, fresh decoder cache)',
+                     'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
+                     'includes': 'cache clear + scan + size + emit + commit, one host sync'}
+    sctx.close()
+    dctx.close()
+    # -- host-inclusive independent encode: pinned H2D of the input, encode,
+    #    pack the slots, D2H of exactly the encoded bytes
+    ctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream)
+    torch.cuda.synchronize()
+    enc_bytes = int(d_ol.sum().item())
+    h_in = torch.from_numpy(data.copy()).pin_memory()
+    h_out = torch.empty(enc_bytes, dtype=torch.uint8).pin_memory()
+    d_packed = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+    d_poff = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_ptot = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def pcie():
+        d_in.copy_(h_in, non_blocking=True)
+        ctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream)
+        _check(lib().xcg_pack_outputs(ctx.h, C.c_void_p(d_out.data_ptr()), C.c_void_p(d_oo.data_ptr()),
+                                      C.c_void_p(d_ol.data_ptr()), n, C.c_void_p(d_packed.data_ptr()),
+                                      C.c_void_p(d_poff.data_ptr()), C.c_void_p(d_ptot.data_ptr()),
+                                      C.c_void_p(stream.cuda_stream)))
+        h_out.copy_(d_packed[:enc_bytes], non_blocking=True)
+    wall, _ = timed(pcie, 5, stream)
+    if int(d_ptot.item()) != enc_bytes:
+        raise SystemExit('pack size mismatch')
+    res['host_inclusive'] = {'metric': 'independent-chunk encode GiB/s incl. pinned H2D of input and D2H of output',
+                             'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3)}
+    return res
 
 
 def main():
@@ -147,6 +256,9 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP events on the launch stream
     ctx.status()
 
+    extras = {} if args.no_extras else side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol,
+                                                          d_st, n, stream, dev, rank)
+
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     tot = torch.tensor([float(in_bytes)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -181,6 +293,7 @@ def main():
                          'kernel': 'encode_independent_kernel', 'kernel_ms': round(kern_ms, 4),
                          'algorithmic_bytes_per_launch': in_bytes + out_bytes},
         }
+        line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_passes)
         print(json.dumps(line), flush=True)

@@ -142,6 +142,12 @@ int xcg_decode_host(xcg_ctx *ctx, const uint8_t *h_enc, uint64_t enc_len, const 
                     uint64_t *h_out_len, int32_t *h_chunk_status, uint64_t *h_consumed, uint64_t *h_unknown,
                     uint32_t unknown_cap, uint32_t *h_nunknown);
 
+/* Pack n output slots (d_out + d_out_off[i], d_out_len[i] bytes) back to back
+ * into d_packed; d_packed_off[i] receives each chunk's offset and *d_total
+ * (device) the packed size.  Asynchronous on `stream`. */
+int xcg_pack_outputs(xcg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint64_t *d_out_len,
+                     uint32_t n, uint8_t *d_packed, uint64_t *d_packed_off, uint64_t *d_total, void *stream);
+
 /* Status word of the context (sticky; nonzero = an internal overflow happened
  * in an earlier asynchronous call).  Synchronises the context's device. */
 int xcg_ctx_status(xcg_ctx *ctx);

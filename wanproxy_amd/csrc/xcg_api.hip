@@ -86,6 +86,8 @@ struct XcgDecodeArgs {
   uint64_t* scratch;
   uint64_t* h_scratch;
 };
+extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*, uint32_t, uint8_t*, uint64_t*,
+                               uint64_t*, hipStream_t);
 extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 
 // The persistent segment cache of a context: XCodecMemoryCache's
@@ -534,6 +536,15 @@ int xcg_decode_host(xcg_ctx* c, const uint8_t* h_enc, uint64_t enc_len, const ui
   (void)hipFree(d_cons); (void)hipFree(d_len); (void)hipFree(d_st);
   (void)hipStreamDestroy(st);
   return rc;
+}
+
+int xcg_pack_outputs(xcg_ctx* c, const uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
+                     uint32_t n, uint8_t* d_packed, uint64_t* d_packed_off, uint64_t* d_total, void* stream) {
+  if (!c || (n && (!d_out || !d_out_off || !d_out_len || !d_packed || !d_packed_off || !d_total))) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  return xcg_launch_pack(d_out, d_out_off, d_out_len, n, d_packed, d_packed_off, d_total, (hipStream_t)stream) == 0
+             ? XCG_OK
+             : XCG_EHIP;
 }
 
 int xcg_window_hashes(xcg_ctx* c, const uint8_t* d_x, uint64_t len, uint64_t* d_hash, void* stream) {

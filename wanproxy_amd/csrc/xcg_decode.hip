@@ -393,7 +393,33 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
   }
 }
 
+// Pack per-chunk output slots into one contiguous buffer (one wave per chunk).
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                                                   const uint64_t* dst_off, uint8_t* dst, uint32_t n) {
+  const uint32_t c = blockIdx.x * 4u + (uint32_t)readfirst(threadIdx.x >> 6);
+  if (c >= n) return;
+  const uint8_t* s = src + src_off[c];
+  uint8_t* d = dst + dst_off[c];
+  const uint64_t m = len[c];
+  const int l = lane_id();
+  for (uint64_t base = 0; base < m; base += 1024) {
+    const uint64_t off = base + 16u * l;
+    if (off + 16 <= m) *(u32x4_u*)(d + off) = *(const u32x4_u*)(s + off);
+    else for (uint64_t k = off; k < m; ++k) d[k] = s[k];
+  }
+}
+
 }  // namespace xcg
+
+extern "C" int xcg_launch_pack(const uint8_t* src, const uint64_t* src_off, const uint64_t* len, uint32_t n,
+                               uint8_t* dst, uint64_t* dst_off, uint64_t* d_total, hipStream_t stream) {
+  using namespace xcg;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, len, dst_off, n, d_total);
+  hipLaunchKernelGGL(pack_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, src, src_off, len, (const uint64_t*)dst_off,
+                     dst, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 struct XcgDecodeArgs {
   const uint8_t* in;

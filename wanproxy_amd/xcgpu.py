@@ -69,6 +69,8 @@ def lib():
     L.xcg_decode_batch.argtypes = [vp, u8p, u64p, u32p, C.c_uint32, C.c_uint32, u8p, C.c_uint64, u64p, u64p, vp, u64p,
                                    u64p, C.c_uint32, vp, u64p, vp]
     L.xcg_decode_batch.restype = C.c_int
+    L.xcg_pack_outputs.argtypes = [vp, u8p, u64p, u64p, C.c_uint32, u8p, u64p, u64p, vp]
+    L.xcg_pack_outputs.restype = C.c_int
     L.xcg_window_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
     L.xcg_window_hashes.restype = C.c_int
     L.xcg_segment_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
