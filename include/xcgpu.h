@@ -61,6 +61,7 @@ extern "C" {
 
 /* Status codes. */
 #define XCG_OK 0
+#define XCG_ENOENT (-2)            /* hash not in the cache */
 #define XCG_EHIP (-5)              /* a HIP runtime call failed */
 #define XCG_ENOMEM (-12)
 #define XCG_EINVAL (-22)
@@ -89,6 +90,17 @@ uint64_t xcg_cache_size(xcg_ctx *ctx);
 int xcg_cache_clear(xcg_ctx *ctx);
 /* Rounds the last XCG_SEM_STREAM batch needed to reach its fixed point. */
 int xcg_last_rounds(xcg_ctx *ctx);
+/* Single-segment host access to the persistent cache, for host adapters:
+ * XCodecCache::lookup (xcodec/xcodec_cache.h:86) copies the 2048 bytes out
+ * (XCG_ENOENT if absent); XCodecCache::enter/replace (:84-85) -- an existing
+ * hash has its bytes replaced. */
+int xcg_cache_lookup_host(xcg_ctx *ctx, uint64_t hash, uint8_t *seg_out);
+int xcg_cache_enter_host(xcg_ctx *ctx, uint64_t hash, const uint8_t *seg);
+/* Declarations (hash, position in the chunk) chunk `chunk` of the last
+ * XCG_SEM_STREAM batch made, in order: what XCodecEncoder::encode_declaration
+ * entered into the cache (xcodec/xcodec_encoder.cc:276-313). */
+int xcg_last_declarations(xcg_ctx *ctx, uint32_t chunk, uint64_t *h_hash, uint32_t *h_pos, uint32_t cap,
+                          uint32_t *h_count);
 /* Diagnostics: copy the persistent cache's lane filters to host memory
  * (h_filt: 2^19 bits; h_ftab: up to ftab_words u32; *h_fmask = buckets - 1). */
 int xcg_debug_cache_dump(xcg_ctx *ctx, uint32_t *h_filt, uint32_t *h_ftab, uint64_t ftab_words, uint32_t *h_fmask);

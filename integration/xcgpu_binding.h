@@ -1,0 +1,75 @@
+/*
+ * xcgpu_binding.h -- how wanproxy's XCodec classes reach the MI355X engine.
+ *
+ * One xcg_ctx (device memory: the GPU-resident segment cache) per reference
+ * XCodecCache object.  The reference shares one cache among every encoder and
+ * decoder of a codec (programs/wanproxy/wanproxy_config_class_codec.cc:71-79,
+ * xcodec/test/xcodec-encode-decode1.cc:59-82), so the binding is keyed by the
+ * cache pointer and the GPU cache is shared the same way.  The host-side
+ * XCodecCache is kept as a mirror of every entry the engine makes, so the rest
+ * of wanproxy (ASK/LEARN in xcodec_pipe_pair.cc, other caches) sees exactly the
+ * reference's cache contents.
+ */
+#ifndef XCGPU_BINDING_H
+#define XCGPU_BINDING_H
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <typeinfo>
+#include <map>
+
+#include "../include/xcgpu.h"
+
+class XCodecCache;
+
+namespace xcgpu_binding {
+
+/* Cache kinds the engine can mirror exactly: XCodecMemoryCache (unbounded) and
+ * tack's TackNullCache (lookups miss).  Anything else is rejected loudly. */
+inline bool is_null_cache(XCodecCache *cache)
+{
+	return strstr(typeid(*cache).name(), "NullCache") != NULL;
+}
+
+inline std::map<XCodecCache *, xcg_ctx *>& ctx_map()
+{
+	static std::map<XCodecCache *, xcg_ctx *> ctxs;
+	return ctxs;
+}
+
+/* The GPU mirror lives as long as the cache object.  wanproxy and tack keep
+ * their caches for the life of the process; a caller that deletes a cache
+ * must call forget() first (the reference caches have no hook for it). */
+inline void forget(XCodecCache *cache)
+{
+	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctx_map().find(cache);
+	if (it == ctx_map().end())
+		return;
+	xcg_ctx_destroy(it->second);
+	ctx_map().erase(it);
+}
+
+inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
+{
+	std::map<XCodecCache *, xcg_ctx *>& ctxs = ctx_map();
+	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctxs.find(cache);
+	if (it != ctxs.end())
+		return it->second;
+	uint32_t flags = out_of_band ? XCG_FLAG_OOB : 0;
+	if (is_null_cache(cache))
+		flags |= XCG_FLAG_NULLCACHE;
+	xcg_ctx *ctx = NULL;
+	int device = 0;
+	const char *dev = getenv("XCGPU_DEVICE");
+	if (dev != NULL)
+		device = atoi(dev);
+	if (xcg_ctx_create(device, flags, &ctx) != XCG_OK)
+		return NULL;
+	ctxs[cache] = ctx;
+	return ctx;
+}
+
+}  // namespace xcgpu_binding
+
+#endif /* !XCGPU_BINDING_H */

@@ -33,13 +33,21 @@ def build():
 
 
 class Oracle:
-    def __init__(self, ref: bool = False):
-        self.ref = ref
-        path = os.path.join(HERE, '_ref/libxcref.so' if ref else 'build/liboracle.so')
+    def __init__(self, ref: bool = False, dropin: bool = False):
+        # dropin: the reference's own driver and Buffer / cache classes, with
+        # XCodecEncoder / XCodecDecoder provided by integration/ over the GPU
+        # engine (oracle/Makefile libxcdropin.so) -- reference-shaped calls.
+        self.ref = ref or dropin
+        ref = self.ref
+        if dropin:
+            import torch  # noqa: F401  (one HIP runtime shared with libxcgpu.so)
+            path = os.path.join(HERE, '_ref/libxcdropin.so')
+        else:
+            path = os.path.join(HERE, '_ref/libxcref.so' if ref else 'build/liboracle.so')
         if not os.path.exists(path):
             raise FileNotFoundError(path)
         L = self.lib = C.CDLL(path)
-        pre = 'xcr_' if ref else 'xco_'
+        pre = ('xdi_' if dropin else 'xcr_') if ref else 'xco_'
         self._hash = getattr(L, pre + 'hash')
         self._hash.restype = C.c_uint64
         self._hash.argtypes = [_u8p]
@@ -56,6 +64,7 @@ class Oracle:
             self._eb.argtypes = [C.c_void_p, _u8p, _u64p, _u32p, C.c_uint32, C.c_int, C.c_int, _u8p, _u64p, _u64p]
         self._eb.restype = C.c_int
         self._dec = getattr(L, pre + 'decode') if ref else None
+        self._cnew.restype = C.c_void_p
         if ref:
             self._dec.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u64p, _u64p, C.c_uint64]
             self._dec.restype = C.c_int

@@ -19,6 +19,13 @@
 
 #include <string.h>
 
+#ifdef XCGPU_DROPIN
+#include "../integration/xcgpu_binding.h"
+#define RELEASE_CACHE(c) xcgpu_binding::forget(c)
+#else
+#define RELEASE_CACHE(c) do { } while (0)
+#endif
+
 /* Out-of-band null cache: the same contract as tack's TackNullCache
  * (programs/tack/tack.cc:70-101): lookups miss, enter is a no-op. */
 class RefNullCache : public XCodecCache {
@@ -73,6 +80,7 @@ void *xcr_cache_new(void)
 
 void xcr_cache_free(void *c)
 {
+	RELEASE_CACHE((XCodecCache *)c);
 	delete (XCodecCache *)c;
 }
 
@@ -100,6 +108,7 @@ int xcr_encode_batch(void *cache, const uint8_t *in, const uint64_t *off, const 
 			XCodecMemoryCache c(uuid);
 			XCodecEncoder e(&c);
 			e.encode(&output, &input);
+			RELEASE_CACHE(&c);
 		} else {
 			stream_enc->encode(&output, &input);
 		}
@@ -111,8 +120,10 @@ int xcr_encode_batch(void *cache, const uint8_t *in, const uint64_t *off, const 
 		out_len[i] = r;
 	}
 	delete stream_enc;
-	if (own || mode == 2)
+	if (own || mode == 2) {
+		RELEASE_CACHE(stream_cache);
 		delete stream_cache;
+	}
 	return rc;
 }
 

@@ -1,0 +1,63 @@
+"""Drop-in conformance: the reference's own driver code and Buffer / cache
+classes, with XCodecEncoder / XCodecDecoder provided by integration/ on the
+GPU engine (oracle/_ref/libxcdropin.so), against the reference goldens.
+This is the class boundary tack and XCodecPipePair call
+(xcodec/xcodec_encoder.h:40-43, xcodec/xcodec_decoder.h:41-45)."""
+import os
+
+import pytest
+
+from golden_cases import MODES, chunks, data, sha
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope='module')
+def dropin():
+    p = os.path.join(ROOT, 'oracle/_ref/libxcdropin.so')
+    if not os.path.exists(p):
+        pytest.skip('drop-in harness not built (needs the reference sources at build time)')
+    from oracle.lib import Oracle
+    return Oracle(dropin=True)
+
+
+def test_dropin_golden_stream_and_null(dropin, golden):
+    n = 0
+    for case in golden['cases']:
+        if case['mode'] not in ('stream', 'null'):
+            continue
+        d, (offs, lens) = chunks(case)
+        outs = dropin.encode_batch(d, offs, lens, mode=MODES[case['mode']], oob=case['mode'] == 'null')
+        assert [sha(o)[:32] for o in outs] == case['chunk_sha256'], (case['input'], case['chunk'], case['mode'])
+        n += 1
+    assert n >= 15
+
+
+def test_dropin_baseline_tack_shas(dropin, golden):
+    for name, b in golden['baseline'].items():
+        enc = dropin.encode_stream(data(name))
+        assert (len(enc), sha(enc)) == (b['xc_len'], b['xc']), name
+
+
+def test_dropin_decode_round_trip(dropin, ref_oracle):
+    for name in ('kat_a', 'kat_b', 'kat_z', 'kat_col', 'magic_heavy', 'all_f1'):
+        d = data(name)
+        enc = ref_oracle.encode_stream(d)
+        c = dropin.cache_new()
+        ok, out, consumed, unk = dropin.decode(enc, c)
+        dropin.cache_free(c)
+        assert ok and not unk and consumed == len(enc) and out == d, name
+
+
+def test_dropin_decode_unknown_like_reference(dropin, ref_oracle):
+    d = data('kat_a')
+    enc = ref_oracle.encode_stream(d)
+    start = enc.index(b'\xf1\x02')
+    res = []
+    for o in (dropin, ref_oracle):
+        c = o.cache_new()
+        ok, out, consumed, unk = o.decode(enc[start:], c)
+        o.cache_free(c)
+        res.append((ok, out, consumed, sorted(unk)))
+    assert res[0] == res[1]

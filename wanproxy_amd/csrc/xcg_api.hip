@@ -88,6 +88,10 @@ struct XcgDecodeArgs {
 };
 extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*, uint32_t, uint8_t*, uint64_t*,
                                uint64_t*, hipStream_t);
+extern "C" int xcg_launch_cache_lookup(uint64_t*, uint64_t*, uint32_t, const uint8_t*, uint64_t, uint8_t*, int32_t*,
+                                       hipStream_t);
+extern "C" int xcg_launch_cache_enter(uint64_t*, uint64_t*, uint32_t, uint8_t*, uint32_t*, uint32_t, uint32_t*,
+                                      uint32_t*, uint32_t, uint64_t, const uint8_t*, int, int32_t*, hipStream_t);
 extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 
 // The persistent segment cache of a context: XCodecMemoryCache's
@@ -264,6 +268,7 @@ const char* xcg_strerror(int status) {
     case XCG_EINVAL: return "invalid argument";
     case XCG_EOVERFLOW: return "internal table overflow";
     case XCG_ENOTSUP: return "not supported";
+    case XCG_ENOENT: return "no such segment";
     default: return "unknown status";
   }
 }
@@ -323,6 +328,75 @@ int xcg_cache_clear(xcg_ctx* c) {
 }
 
 int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
+
+namespace {
+// A small pinned + device staging area for single-segment host calls.
+int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out_seg, int mode, int32_t* res) {
+  DeviceGuard g(c->device);
+  int rc = ensure_cache(c);
+  if (rc != XCG_OK) return rc;
+  uint8_t* d_seg = nullptr;
+  int32_t* d_res = nullptr;
+  if (hipMalloc(&d_seg, XCG_SEGMENT_LENGTH) != hipSuccess || hipMalloc(&d_res, 4) != hipSuccess) {
+    (void)hipFree(d_seg);
+    return XCG_ENOMEM;
+  }
+  rc = XCG_OK;
+  if (mode == 0) {   // lookup
+    if (xcg_launch_cache_lookup(c->g.keys, c->g.vals, c->g.mask, c->g.pool, hash, d_seg, d_res, nullptr) != 0 ||
+        hipMemcpy(res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (*res && hipMemcpy(out_seg, d_seg, XCG_SEGMENT_LENGTH, hipMemcpyDeviceToHost) != hipSuccess))
+      rc = XCG_EHIP;
+  } else {           // enter (1) / replace (2)
+    if (hipMemcpy(d_seg, in_seg, XCG_SEGMENT_LENGTH, hipMemcpyHostToDevice) != hipSuccess ||
+        xcg_launch_cache_enter(c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap, c->g.filt,
+                               c->g.ftab, c->g.fmask, hash, d_seg, mode == 2, d_res, nullptr) != 0 ||
+        hipMemcpy(res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = XCG_EHIP;
+  }
+  (void)hipFree(d_seg);
+  (void)hipFree(d_res);
+  return rc;
+}
+}  // namespace
+
+int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
+  if (!c || !seg_out) return XCG_EINVAL;
+  int32_t found = 0;
+  const int rc = host_seg_call(c, hash, nullptr, seg_out, 0, &found);
+  if (rc != XCG_OK) return rc;
+  return found ? XCG_OK : XCG_ENOENT;
+}
+
+int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
+  if (!c || !seg) return XCG_EINVAL;
+  int32_t res = 0;
+  const int rc = host_seg_call(c, hash, seg, nullptr, 1, &res);
+  if (rc != XCG_OK) return rc;
+  return res == -2 ? XCG_EOVERFLOW : XCG_OK;
+}
+
+int xcg_last_declarations(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t* h_pos, uint32_t cap,
+                          uint32_t* h_count) {
+  if (!c || !h_count || !c->bs.decl || chunk >= c->bs.n_cap) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  uint32_t nd = 0;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&nd, c->bs.ndecl + chunk, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return XCG_EHIP;
+  *h_count = nd;
+  const uint32_t k = nd < cap ? nd : cap;
+  if (k == 0) return XCG_OK;
+  std::vector<uint32_t> buf(4ull * k);
+  if (hipMemcpy(buf.data(), (const uint8_t*)c->bs.decl + 16ull * chunk * c->bs.maxd, 16ull * k,
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return XCG_EHIP;
+  for (uint32_t i = 0; i < k; ++i) {
+    if (h_hash) h_hash[i] = ((uint64_t)buf[4 * i + 1] << 32) | buf[4 * i];
+    if (h_pos) h_pos[i] = buf[4 * i + 2];
+  }
+  return XCG_OK;
+}
 
 int xcg_debug_cache_dump(xcg_ctx* c, uint32_t* h_filt, uint32_t* h_ftab, uint64_t ftab_words, uint32_t* h_fmask) {
   if (!c || !c->g.keys) return XCG_EINVAL;

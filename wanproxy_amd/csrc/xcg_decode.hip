@@ -409,7 +409,66 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* src, const uin
   }
 }
 
+// Host-driven cache access (one wave): look a hash up and copy its segment
+// out, or enter a segment under a hash (XCodecCache::lookup / enter /
+// replace, xcodec/xcodec_cache.h:83-89).
+__global__ __launch_bounds__(64) void cache_lookup_kernel(HashTab g, const uint8_t* pool, uint64_t key, uint8_t* seg_out,
+                                                          int32_t* found) {
+  const uint64_t v = tab_lookup(g, (uint32_t)key, (uint32_t)(key >> 32));
+  if (v == ~0ull) {
+    if (lane_id() == 0) *found = 0;
+    return;
+  }
+  wave_copy2048(seg_out, pool + v * (uint64_t)SEG);
+  if (lane_id() == 0) *found = 1;
+}
+
+__global__ __launch_bounds__(64) void cache_enter_kernel(HashTab g, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
+                                                         uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint64_t key,
+                                                         const uint8_t* seg, int replace_only, int32_t* result) {
+  const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+  const uint64_t v = tab_lookup(g, lo, hi);
+  if (v != ~0ull) {                          // present: replace the bytes
+    wave_copy2048(pool + v * (uint64_t)SEG, seg);
+    if (lane_id() == 0) *result = 1;
+    return;
+  }
+  if (replace_only) {
+    if (lane_id() == 0) *result = -1;
+    return;
+  }
+  uint32_t s = 0;
+  if (lane_id() == 0) s = atomicAdd(nseg, 1u);
+  s = readfirst(s);
+  if (s >= seg_cap) {
+    if (lane_id() == 0) *result = -2;
+    return;
+  }
+  wave_copy2048(pool + (uint64_t)s * SEG, seg);
+  if (lane_id() == 0) {
+    tab_insert_min(g, lo, hi, s);
+    filt_insert(filt, lo, hi);
+    ftab_insert(ftab, fmask, lo, hi);
+    *result = 0;
+  }
+}
+
 }  // namespace xcg
+
+extern "C" int xcg_launch_cache_lookup(uint64_t* keys, uint64_t* vals, uint32_t mask, const uint8_t* pool, uint64_t key,
+                                       uint8_t* seg_out, int32_t* found, hipStream_t s) {
+  hipLaunchKernelGGL(xcg::cache_lookup_kernel, dim3(1), dim3(64), 0, s, xcg::HashTab{keys, vals, mask}, pool, key,
+                     seg_out, found);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int xcg_launch_cache_enter(uint64_t* keys, uint64_t* vals, uint32_t mask, uint8_t* pool, uint32_t* nseg,
+                                      uint32_t seg_cap, uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint64_t key,
+                                      const uint8_t* seg, int replace_only, int32_t* result, hipStream_t s) {
+  hipLaunchKernelGGL(xcg::cache_enter_kernel, dim3(1), dim3(64), 0, s, xcg::HashTab{keys, vals, mask}, pool, nseg,
+                     seg_cap, filt, ftab, fmask, key, seg, replace_only, result);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 extern "C" int xcg_launch_pack(const uint8_t* src, const uint64_t* src_off, const uint64_t* len, uint32_t n,
                                uint8_t* dst, uint64_t* dst_off, uint64_t* d_total, hipStream_t stream) {
