@@ -76,6 +76,20 @@ def cpu_baseline(data: np.ndarray, offs, lens, passes: int):
                       f'{threads} threads x contiguous shards, fresh XCodecMemoryCache per chunk; {dt:.1f} s wall'}
 
 
+def pmc_traffic(n):
+    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC
+    summary (scripts/profile.sh + scripts/prof_summary.py: FETCH_SIZE doubled
+    per MI355X_MICROARCH.md "HBM", plus WRITE_SIZE), when it was taken on this
+    same workload; PMC counters cannot be read from inside the timed run."""
+    p = os.path.join(ROOT, 'profiles', 'r01_c2_independent_summary.json')
+    if n != NCHUNKS or not os.path.exists(p):
+        return None, None
+    s = json.load(open(p))
+    if 'hbm_traffic_bytes_per_launch' not in s:
+        return None, None
+    return int(s['hbm_traffic_bytes_per_launch']), 'profiles/r01_c2_independent_summary.json (rocprofv3 --pmc)'
+
+
 def timed(fn, steps, stream):
     import torch
     for _ in range(2):
@@ -259,18 +273,14 @@ def main():
     extras = {} if args.no_extras else side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol,
                                                           d_st, n, stream, dev, rank)
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(in_bytes)], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        torch.distributed.all_reduce(tot, op=torch.distributed.ReduceOp.SUM)
-    wall = float(t.item())
-    total_bytes = float(tot.item()) * args.steps
+    from wanproxy_amd.shard import reduce_run
+    wall, job_bytes = reduce_run(wall, in_bytes, device=dev)   # max wall, total bytes over ranks
+    total_bytes = float(job_bytes) * args.steps
     value = total_bytes / 2**30 / wall
 
     if rank == 0:
         achieved = (in_bytes + out_bytes) / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, tsrc = pmc_traffic(n)
         line = {
             'metric': 'XCodec encode GiB/s device-resident, batched 64 KiB chunks, 1/2/4/8 GPU',
             'value': round(value, 3),
@@ -289,7 +299,7 @@ def main():
                        'chunks_per_gpu': n, 'chunk_bytes': CHUNK, 'out_in_ratio': round(out_bytes / in_bytes, 5),
                        'parallelism': f'dp{world} (shard per GPU, no collective)'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / PEAK_HBM_GBS, 5), 'traffic': traffic,
+                         'frac': round(achieved / PEAK_HBM_GBS, 5), 'traffic': traffic, 'traffic_source': tsrc,
                          'kernel': 'encode_independent_kernel', 'kernel_ms': round(kern_ms, 4),
                          'algorithmic_bytes_per_launch': in_bytes + out_bytes},
         }
