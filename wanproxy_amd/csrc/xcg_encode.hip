@@ -622,7 +622,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
 
 
 template <int LOGNB, int MAXD>
-__global__ __launch_bounds__(256) void encode_independent_kernel(EncParams prm) {
+__global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams prm) {
   __shared__ WaveTable<LOGNB, MAXD> tabs[4];
   const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
