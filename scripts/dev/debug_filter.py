@@ -17,8 +17,11 @@ rc = L.xcg_debug_cache_dump(ctx.h, filt.ctypes.data, ftab.ctypes.data, ftab.size
 print('rc', rc, 'fmask', fm[0], 'filt bits set', int(np.unpackbits(filt.view(np.uint8)).sum()), 'ftab nonzero', int((ftab != 0).sum()))
 M=0xFFFFFFFF
 for name, w in (('A', A), ('B', B)):
-    h = o.hash(w.tobytes()); lo = h & M; hi = h >> 32; bh = (hi >> 4) & 0x0FFFFFFF; fp = lo | 1
-    fb = (fp ^ ((bh << 3) & M) ^ (bh >> 13)) & ((1 << 19) - 1)
-    b = ((fp >> 7) ^ ((bh * 0x9E37) & M) ^ ((fp << 9) & M)) & int(fm[0])
+    h = o.hash(w.tobytes()); lo = h & M; k = (-lo) & M; fp = k | 1
+    fb = k & ((1 << 19) - 1)
+    def mix32(a, b):
+        x = ((a * 0x9E3779B1) & M) ^ (((b + 0x7F4A7C15) & M) * 0x85EBCA77 & M)
+        x ^= x >> 15; x = (x * 0x2C1B3C6D) & M; x ^= x >> 13; return x
+    b = mix32(k, 0x5BD1E995) & int(fm[0])
     print(name, hex(h), 'filt bit', fb, bool((filt[fb >> 5] >> (fb & 31)) & 1), 'bucket', b, [hex(v) for v in ftab[4*b:4*b+4]], 'fp', hex(fp))
     print('  nonzero filt words', np.nonzero(filt)[0][:8], 'nonzero ftab idx', np.nonzero(ftab)[0][:8])

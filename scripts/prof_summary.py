@@ -22,7 +22,7 @@ for r in stats:
         out['avg_ns'] = float(r['AverageNs'])
         out['min_ns'] = float(r['MinNs'])
         out['max_ns'] = float(r['MaxNs'])
-for grp in ('fetch', 'write', 'sq'):
+for grp in ('fetch', 'write', 'sq', 'sq2'):
     p = os.path.join(src, grp, 'run_counter_collection.csv')
     if not os.path.exists(p):
         continue

@@ -7,9 +7,9 @@
 //                    always has bits 32..35 clear: mix() shifts bits_hash by 36)
 //   vals[cap]  u64   G: segment index into pool;  B: (chunk << 32) | position
 //   pool[nseg_cap * 2048]  segment bytes (G only)
-//   ftab[fbuckets * 4] u32  lane-probe fingerprint buckets: 3 slots of (lo | 1)
+//   ftab[fbuckets * 4] u32  lane-probe fingerprint buckets: 3 slots of (K | 1)
 //                    + an overflow word, one 16-byte load per probe
-//   filt[FILT_BITS / 32] u32  the bitmap a workgroup loads into LDS
+//   filt[FILT_BITS / 32] u32  the bitmap a workgroup loads into LDS (bit K mod 2^19)
 #pragma once
 #include "xcg_device.h"
 
@@ -45,17 +45,15 @@ __device__ __forceinline__ uint32_t tab_slot(uint32_t lo, uint32_t hi, uint32_t 
   return mix32(lo, hi) & mask;
 }
 
-// Filter bit and fingerprint bucket are functions of (fp, bh) where fp =
-// lo | 1 and bh = bits_hash = hi >> 4 -- both computable inside the rolling
-// loop.  (bh's bits 28..31 never reach the hash, so they are masked.)
-__device__ __forceinline__ uint32_t filt_bit(uint32_t fp, uint32_t bh) {
-  bh &= 0x0FFFFFFFu;
-  return (fp ^ (bh << 3) ^ (bh >> 13)) & ((1u << FILT_LOG2) - 1u);
-}
-__device__ __forceinline__ uint32_t fbucket(uint32_t fp, uint32_t bh, uint32_t fmask) {
-  bh &= 0x0FFFFFFFu;
-  return ((fp >> 7) ^ (bh * 0x9E37u) ^ (fp << 9)) & fmask;
-}
+// Lane-probe key of a hash: K = -lo (mod 2^32).  The encoder's rolling loop
+// keeps negated sums (NX1 = -X1, NX2 = -(X2 + CLO)), so K = (NX1 << 20) + NX2
+// costs one instruction per position, and every table the lanes probe (the
+// per-wave declaration table, the LDS filter, the fingerprint buckets) is
+// keyed by K.  The F (bits_hash) half of the hash is only needed after a K
+// match, by the exact re-check.
+__device__ __forceinline__ uint32_t probe_key(uint32_t lo) { return 0u - lo; }
+__device__ __forceinline__ uint32_t filt_bit(uint32_t k) { return k & ((1u << FILT_LOG2) - 1u); }
+__device__ __forceinline__ uint32_t fbucket(uint32_t k, uint32_t fmask) { return mix32(k, 0x5BD1E995u) & fmask; }
 
 // Wave-uniform 64-bit value (readfirstlane per 32-bit half; no sign extension).
 __device__ __forceinline__ uint64_t readfirst64(uint64_t v) {
@@ -97,8 +95,9 @@ __device__ __forceinline__ bool tab_insert_min(HashTab t, uint32_t lo, uint32_t 
 // Fingerprint bucket insert: first free of 3 slots, else mark overflow (lanes
 // then report an event there and the resolver decides exactly).
 __device__ __forceinline__ void ftab_insert(uint32_t* ftab, uint32_t fmask, uint32_t lo, uint32_t hi) {
-  const uint32_t fp = lo | 1u;
-  const uint32_t b = fbucket(fp, hi >> 4, fmask);
+  (void)hi;
+  const uint32_t k = probe_key(lo), fp = k | 1u;
+  const uint32_t b = fbucket(k, fmask);
   uint32_t* s = ftab + 4 * b;
   for (int k = 0; k < 3; ++k) {
     const uint32_t prev = atomicCAS(s + k, 0u, fp);
@@ -108,7 +107,8 @@ __device__ __forceinline__ void ftab_insert(uint32_t* ftab, uint32_t fmask, uint
 }
 
 __device__ __forceinline__ void filt_insert(uint32_t* filt, uint32_t lo, uint32_t hi) {
-  const uint32_t bit = filt_bit(lo | 1u, hi >> 4);
+  (void)hi;
+  const uint32_t bit = filt_bit(probe_key(lo));
   atomicOr(filt + (bit >> 5), 1u << (bit & 31));
 }
 

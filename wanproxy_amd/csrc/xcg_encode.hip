@@ -31,17 +31,37 @@
 
 namespace xcg {
 
-// Per-wave LDS state: a 2-slot-bucket fingerprint table over the chunk's own
-// declarations (the XCodecMemoryCache of an independent encode() call,
-// xcodec_cache.h:245-365) plus the exact records it points to.
+// Per-wave LDS state of one encode() call's XCodecMemoryCache
+// (xcodec_cache.h:245-365): a 2-slot-bucket table of probe keys K = -lo over
+// the chunk's declarations -- bucket = bits 3.. of K; an empty slot of bucket b
+// holds kempty(b), whose bucket bits are ~b, so it never equals a K probed
+// there -- plus the exact records the slots point to.  The key tables of a
+// block's waves sit first in LDS, 8 << LOGNB bytes each, so a lane's probe
+// address is a single and-or of K.
 template <int LOGNB, int MAXD>
-struct WaveTable {
+struct WaveRecs {
   static constexpr int NB = 1 << LOGNB;
-  uint32_t fp[2 * NB];        // slot fingerprint (lo | 1), 0 = empty
-  uint16_t idx[2 * NB];       // declaration index of the slot
+  uint16_t idx[2 * NB];       // declaration index of the key slot
   uint32_t rlo[MAXD], rhi[MAXD], rc[MAXD];  // exact hash + chunk position
-  uint32_t ovf_fp[8];         // keys whose bucket was full
+  uint32_t ovf_k[8];          // keys whose bucket was full
   uint32_t ovf_idx[8];
+};
+
+template <int LOGNB>
+__device__ __forceinline__ uint32_t kbucket(uint32_t k) { return (k >> 3) & ((1u << LOGNB) - 1u); }
+template <int LOGNB>
+__device__ __forceinline__ uint32_t kempty(uint32_t b) { return (~b & ((1u << LOGNB) - 1u)) << 3; }
+
+template <int LOGNB, int MAXD, int W>
+struct IndepLDS {
+  uint32_t key[W][2 << LOGNB];
+  WaveRecs<LOGNB, MAXD> rec[W];
+};
+template <int LOGNB, int MAXD, int W>
+struct StreamLDS {
+  uint32_t key[W][2 << LOGNB];
+  uint32_t lfilt[FILT_WORDS];
+  WaveRecs<LOGNB, MAXD> rec[W];
 };
 
 struct EncParams {
@@ -66,12 +86,6 @@ struct EncParams {
   uint32_t maxd;
   uint32_t* changed;   // set when any chunk's declaration list differs from the last round
 };
-
-__device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t bh, int logNB) {
-  // bh = bits_hash; only bits 0..27 survive mix()'s << 36, and only bits
-  // 5..5+logNB (< 28) are used here, so bh and (hi >> 4) give the same bucket.
-  return ((lo ^ bh) >> 5) & ((1u << logNB) - 1u);
-}
 
 // ------------------------------------------------------------------ emission
 
@@ -201,117 +215,154 @@ __device__ __forceinline__ bool equal2048_u(const uint8_t* a, const uint8_t* b) 
 struct Piece {
   u32x4 a0, a1;   // bytes [q0, q0+32): the windows' leaving bytes
   u32x4 b0, b1;   // bytes [q0+2048, q0+2080): the entering bytes
-  // segment sums of the A and B segments (j = offset within the segment)
-  uint32_t sxa, sqxa, sfa, sqfa;
-  uint32_t sxb, sqxb, sfb, sqfb;
+  // byte sums of the A and B segments: plain and weighted by j (offset in it)
+  uint32_t sxa, sqxa;
+  uint32_t sxb, sqxb;
 };
 
-__device__ __forceinline__ void seg_sums(const u32x4 d0, const u32x4 d1, uint32_t& sx, uint32_t& sqx,
-                                         uint32_t& sf, uint32_t& sqf) {
+__device__ __forceinline__ void seg_sums(const u32x4 d0, const u32x4 d1, uint32_t& sx, uint32_t& sqx) {
   const uint32_t d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
-  sx = 0; sqx = 0; sf = 0; sqf = 0;
+  sx = 0; sqx = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const uint32_t wts = (4u * k) | ((4u * k + 1) << 8) | ((4u * k + 2) << 16) | ((4u * k + 3) << 24);
     sx = __builtin_amdgcn_udot4(d[k], 0x01010101u, sx, false);
     sqx = __builtin_amdgcn_udot4(d[k], wts, sqx, false);
+  }
+}
+
+// bits_hash half of the hash of the window that starts at lane L's first
+// position (bytes A of lanes >= L, then B of lanes < L), from the registers:
+// hi = ((F1 << 16) + F2) << 4 with F1 = sum ffs(x), F2 = sum (2048 - k) ffs(x_k)
+// (XCodecHash, xcodec_hash.h:93-174).  Only candidates need it.
+__device__ __forceinline__ uint32_t lane_window_hi(const Piece& P, int L) {
+  const int l = lane_id();
+  const bool useA = l >= L;
+  const uint32_t d[8] = {useA ? P.a0[0] : P.b0[0], useA ? P.a0[1] : P.b0[1], useA ? P.a0[2] : P.b0[2],
+                         useA ? P.a0[3] : P.b0[3], useA ? P.a1[0] : P.b1[0], useA ? P.a1[1] : P.b1[1],
+                         useA ? P.a1[2] : P.b1[2], useA ? P.a1[3] : P.b1[3]};
+  uint32_t sf = 0, sqf = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      uint32_t f = ffbl(byte_of(d[k], b)) + 1u;
+      const uint32_t f = ffbl(byte_of(d[k], b)) + 1u;
       sf += f;
       sqf += (4u * k + b) * f;
     }
   }
+  const uint32_t o = 32u * (uint32_t)((l - L) & 63);   // lane's offset in the window
+  const uint32_t F1 = wave_sum(sf), F2 = wave_sum((2048u - o) * sf - sqf);
+  return ((F1 << 16) + F2) << 4;
 }
 
-// Roll the hash over the lane's 32 positions; bit j of the result is set when
-// position q0 + j is a possible cache hit.  C0: the pending candidate c0 is
-// not in the table yet and becomes visible at local index jvis.  OVF: probe
-// the (rare) overflow keys too.
-template <int LOGNB, bool C0, bool GLB>
-__device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t X1, uint32_t X2c, uint32_t F1,
-                                               uint32_t F2, const uint32_t* fptab, uint32_t c0fp, int jvis,
-                                               const uint32_t* ovf, uint32_t novf, uint32_t& lo0,
-                                               uint32_t& bh0, const uint32_t* lfilt, const u32x4* ftab,
-                                               uint32_t fmask) {
+// Lane mask of a == b, straight from v_cmp (a bool would be materialised
+// in a VGPR and compared again before any ballot).
+__device__ __forceinline__ uint64_t lanes_eq(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+
+// ev = 2 ev + (this lane's bit of m) in one v_addc, m being the carry-in: no
+// per-position bit constants, which VOP3 cannot encode as literals on gfx9.
+__device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
+  uint32_t r;
+  uint64_t co;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(ev), "s"(m));
+  return r;
+}
+
+// Roll the probe key over the lane's 32 positions; bit j of the result is set
+// when position q0 + j is a possible cache hit.  NX1 = -X1, NX2 = -(X2 + CLO)
+// at q0 (RollingHash::roll, xcodec_hash.h:57-70, negated), so K = -lo costs one
+// instruction.  C0: the pending candidate (key c0k) is not in the table yet and
+// becomes visible at piece offset rvis (position p + rvis).  OVF: also compare the (rare) overflow
+// keys ovk[8].  GLB: also probe the persistent cache / batch filter.
+template <int LOGNB, bool C0, bool OVF, bool GLB>
+__device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
+                                               uint32_t kofs, uint32_t c0k, int rvis, const uint32_t* ovk,
+                                               const uint32_t* lfilt, const u32x4* ftab, uint32_t fmask) {
+  // bucket mask in a VGPR so that (K & KM) | kofs is one v_and_or_b32 (VOP3
+  // takes no literal and one SGPR on gfx9)
+  const uint32_t KM = (uint32_t)opaque((int)(((1u << LOGNB) - 1u) << 3));
   const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
   const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
-  uint32_t o[8];   // overflow keys (uniform, SGPRs); novf == 0 almost always
+  uint32_t o[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = ovf[k];
+  for (int k = 0; k < 8; ++k) o[k] = OVF ? ovk[k] : 0u;
+  // C0 visibility: lanes l with 32 l + j >= rvis.  With rvis = 32 A + B that is
+  // l >= A + 1 for j < B and l >= A for j >= B -- two masks per piece.
+  uint64_t vis_hi = 0, vis_lo = 0;
+  int vB = 0;
+  if (C0) {
+    const int A = rvis >> 5;
+    vB = rvis & 31;
+    auto from_lane = [](int t) -> uint64_t { return t <= 0 ? ~0ull : (t >= 64 ? 0ull : (~0ull << t)); };
+    vis_hi = from_lane(A + 1);
+    vis_lo = from_lane(A);
+  }
   uint32_t ev = 0;
   // Groups of 4 positions: the sched_barrier keeps hipcc from hoisting all 32
-  // LDS probes (and their operands) at once, which would cost ~100 VGPRs.
+  // LDS probes (and their operands) at once.
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    uint32_t fpv[4], bkt[4], gbh[4];
+    uint32_t kv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
-      const uint32_t lo = (X1 << 20) + X2c;
-      const uint32_t bh = (F1 << 16) + F2;
-      if (j == 0) { lo0 = lo; bh0 = bh; }
-      fpv[t] = lo | 1u;
-      bkt[t] = bucket_of(lo, bh, LOGNB);
-      gbh[t] = bh;
+      kv[t] = (NX1 << 20) + NX2;
       if (j < 31) {
         const uint32_t xo = byte_of(xa[j >> 2], j & 3);
         const uint32_t xn = byte_of(xb[j >> 2], j & 3);
-        const uint32_t ro = ffbl(xo), rn = ffbl(xn);
-        X1 = X1 + xn - xo;                         // RollingHash::roll, xcodec_hash.h:57-70
-        X2c = X2c + X1 - (xo << 11);
-        F1 = F1 + rn - ro;                         // (ffbl+1) - (ffbl+1)
-        F2 = F2 + F1 - (ro << 11) - 2048u;         // - 2048 * ffs(dead)
+        NX1 += xo - xn;
+        NX2 += NX1 + (xo << 11);
       }
     }
     uint2 e[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(fptab + 2 * bkt[t]);
-    // Global cache + batch declarations: LDS bitmap first, then (rarely) one
-    // 16-byte fingerprint-bucket load; all four loads issued before any use.
-    bool gh[4] = {false, false, false, false};
+    for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(kblk + ((kv[t] & KM) | kofs));
+    // Persistent cache + batch declarations: LDS bitmap first, then (rarely)
+    // one 16-byte fingerprint-bucket load; all four loads issued before use.
+    uint64_t gh[4] = {0, 0, 0, 0};
     if (GLB) {
       u32x4 q[4];
       bool pass[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t fb = filt_bit(fpv[t], gbh[t]);
-        pass[t] = (lfilt[fb >> 5] >> (fb & 31)) & 1u;
-      }
+      for (int t = 0; t < 4; ++t) pass[t] = (lfilt[filt_bit(kv[t]) >> 5] >> (kv[t] & 31u)) & 1u;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         q[t] = u32x4{0u, 0u, 0u, 0u};
-        if (pass[t]) q[t] = ftab[fbucket(fpv[t], gbh[t], fmask)];
+        if (pass[t]) q[t] = ftab[fbucket(kv[t], fmask)];
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        gh[t] = (q[t][0] == fpv[t]) | (q[t][1] == fpv[t]) | (q[t][2] == fpv[t]) | (q[t][3] == FOVF);
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t fp = kv[t] | 1u;
+        gh[t] = lanes_eq(q[t][0], fp) | lanes_eq(q[t][1], fp) | lanes_eq(q[t][2], fp) | lanes_eq(q[t][3], FOVF);
+      }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
-      bool hit = (e[t].x == fpv[t]) | (e[t].y == fpv[t]) | gh[t];
-      if (C0) hit |= (fpv[t] == c0fp) & (j >= jvis);
-      if (novf) {
+      uint64_t hit = lanes_eq(e[t].x, kv[t]) | lanes_eq(e[t].y, kv[t]) | gh[t];
+      if (C0) hit |= lanes_eq(kv[t], c0k) & (j < vB ? vis_hi : vis_lo);
+      if (OVF) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) hit |= (o[k] == fpv[t]);
+        for (int k = 0; k < 8; ++k) hit |= lanes_eq(o[k], kv[t]);
       }
-      ev |= (uint32_t)hit << j;
+      ev = shift_in(ev, hit);
     }
     asm volatile("" : "+v"(ev));   // materialise this group's bits before the next group
     __builtin_amdgcn_sched_barrier(0);
   }
-  return ev;
+  return __builtin_bitreverse32(ev);   // position j was shifted in at bit 31 - j
 }
 
 // ------------------------------------------------------------------ kernel
 
-// One wave encodes chunk `chunk` (one XCodecEncoder::encode call).  STREAM:
-// the cache also holds the persistent GPU cache g and the batch declarations
-// b of chunks < chunk, probed through the workgroup's LDS filter lfilt.
+// One wave encodes chunk `chunk` (one XCodecEncoder::encode call).  Its key
+// table is kblk + kofs (LDS), its records T.  STREAM: the cache also holds the
+// persistent GPU cache g and the batch declarations b of chunks < chunk,
+// probed through the workgroup's LDS filter lfilt.
 template <int LOGNB, int MAXD, bool STREAM>
-__device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOGNB, MAXD>& T, const uint32_t chunk,
-                                             const uint32_t* lfilt) {
+__device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, const uint32_t kofs,
+                                             WaveRecs<LOGNB, MAXD>& T, const uint32_t chunk, const uint32_t* lfilt) {
   constexpr int NB = 1 << LOGNB;
   const int l = lane_id();
 
@@ -329,7 +380,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
     return;
   }
 
-  for (int k = l; k < 2 * NB; k += 64) T.fp[k] = 0u;
+  uint32_t* const keyt = (uint32_t*)(kblk + kofs);
+  for (int k = l; k < 2 * NB; k += 64) keyt[k] = kempty<LOGNB>((uint32_t)k >> 1);
   uint32_t ndecl = 0, novf = 0;
 
   const int last = L - SEG;                        // last window start
@@ -352,23 +404,23 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
   // offset the declaration will have if nothing cancels it (spec_olen).
   int spec_cand = -1;
   uint32_t spec_olen = 0;
-  uint32_t totXA = 0, totTA = 0, totFA = 0, totTFA = 0;   // sums over the A half (carried)
+  uint32_t totXA = 0, totTA = 0;                   // sums over the A half (carried)
 
   // Insert a declaration into the LDS table (XCodecMemoryCache::enter,
   // xcodec_cache.h:303-325) -- by lane 0, visible to later LDS reads of the
   // wave (LDS ops of one wave complete in order).
   auto insert = [&](uint32_t lo, uint32_t hi, uint32_t c) {
     const uint32_t d = ndecl++;
-    const uint32_t fp = lo | 1u;
-    const uint32_t b = bucket_of(lo, hi >> 4, LOGNB);
-    const uint32_t s0 = readfirst(T.fp[2 * b]), s1 = readfirst(T.fp[2 * b + 1]);
+    const uint32_t k = probe_key(lo);
+    const uint32_t b = kbucket<LOGNB>(k), ke = kempty<LOGNB>(b);
+    const uint32_t s0 = readfirst(keyt[2 * b]), s1 = readfirst(keyt[2 * b + 1]);
     if (l == 0) {
       T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
-      if (s0 == 0u) { T.fp[2 * b] = fp; T.idx[2 * b] = (uint16_t)d; }
-      else if (s1 == 0u) { T.fp[2 * b + 1] = fp; T.idx[2 * b + 1] = (uint16_t)d; }
-      else if (novf < 8) { T.ovf_fp[novf] = fp; T.ovf_idx[novf] = d; }
+      if (s0 == ke) { keyt[2 * b] = k; T.idx[2 * b] = (uint16_t)d; }
+      else if (s1 == ke) { keyt[2 * b + 1] = k; T.idx[2 * b + 1] = (uint16_t)d; }
+      else if (novf < 8) { T.ovf_k[novf] = k; T.ovf_idx[novf] = d; }
     }
-    if (s0 != 0u && s1 != 0u) {
+    if (s0 != ke && s1 != ke) {
       if (novf < 8) ++novf;
       else if (l == 0 && prm.status) atomicOr(prm.status, 1);
     }
@@ -377,18 +429,18 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
 
   // Exact lookup: declaration index whose hash is (lo, hi), or -1.
   auto lookup = [&](uint32_t lo, uint32_t hi) -> int {
-    const uint32_t fp = lo | 1u;
-    const uint32_t b = bucket_of(lo, hi >> 4, LOGNB);
+    const uint32_t key = probe_key(lo);
+    const uint32_t b = kbucket<LOGNB>(key);
     int found = -1;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      if (readfirst(T.fp[2 * b + k]) == fp) {
+      if (readfirst(keyt[2 * b + k]) == key) {
         const uint32_t d = readfirst(T.idx[2 * b + k]);
         if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
       }
     }
     for (uint32_t k = 0; k < novf && found < 0; ++k) {
-      if (readfirst(T.ovf_fp[k]) == fp) {
+      if (readfirst(T.ovf_k[k]) == key) {
         const uint32_t d = readfirst(T.ovf_idx[k]);
         if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
       }
@@ -423,11 +475,11 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
     ++n_pieces;
     if (contig) {
       P.a0 = P.b0; P.a1 = P.b1;
-      P.sxa = P.sxb; P.sqxa = P.sqxb; P.sfa = P.sfb; P.sqfa = P.sqfb;
+      P.sxa = P.sxb; P.sqxa = P.sqxb;
     } else {
       P.a0 = load16_aligned_safe(x, q0, L);
       P.a1 = load16_aligned_safe(x, q0 + 16, L);
-      seg_sums(P.a0, P.a1, P.sxa, P.sqxa, P.sfa, P.sqfa);
+      seg_sums(P.a0, P.a1, P.sxa, P.sqxa);
     }
     if (nb_start == p) {
       P.b0 = nb0; P.b1 = nb1;
@@ -442,34 +494,29 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
       nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
       nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
     }
-    seg_sums(P.b0, P.b1, P.sxb, P.sqxb, P.sfb, P.sqfb);
+    seg_sums(P.b0, P.b1, P.sxb, P.sqxb);
     p_prev = p;
 
     // ---- start sums of lane l's first window (positions relative to p)
     const uint32_t qa = 32u * (uint32_t)l, qb = 2048u + 32u * (uint32_t)l;
     const uint32_t ta = qa * P.sxa + P.sqxa, tb = qb * P.sxb + P.sqxb;
-    const uint32_t tfa = qa * P.sfa + P.sqfa, tfb = qb * P.sfb + P.sqfb;
     if (!contig) {
       totXA = wave_sum(P.sxa); totTA = wave_sum(ta);
-      totFA = wave_sum(P.sfa); totTFA = wave_sum(tfa);
     }
-    const uint32_t dx = P.sxb - P.sxa, dt = tb - ta, df = P.sfb - P.sfa, dtf = tfb - tfa;
+    const uint32_t dx = P.sxb - P.sxa, dt = tb - ta;
     const uint32_t ix = wave_incl_scan(dx), it = wave_incl_scan(dt);
-    const uint32_t ifv = wave_incl_scan(df), itf = wave_incl_scan(dtf);
     const uint32_t X1 = totXA + ix - dx;
     const uint32_t TT = totTA + it - dt;
-    const uint32_t F1 = totFA + ifv - df;
-    const uint32_t TF = totTFA + itf - dtf;
     const uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
-    const uint32_t F2 = (2048u + qa) * F1 - TF;
     // Next piece's A half (if contiguous) is this B half, shifted by 2048.
     const uint32_t totXB = totXA + readlane(ix, 63);
     const uint32_t totTB = totTA + readlane(it, 63) - 2048u * totXB;
-    const uint32_t totFB = totFA + readlane(ifv, 63);
-    const uint32_t totTFB = totTFA + readlane(itf, 63) - 2048u * totFB;
+    // probe key of the lane's first window
+    const uint32_t NX1 = 0u - X1, NX2 = 0u - X2c;
+    const uint32_t k0 = (NX1 << 20) + NX2;
 
     // ---- vector phase
-    uint32_t ev = 0, lo0 = 0, bh0 = 0;
+    uint32_t ev = 0;
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
     if (!nullcache) {
       // c0 = the pending candidate; once it is visible from the piece start on,
@@ -480,24 +527,30 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
       }
       const bool c0 = have_cand && !c0_in_table;
       const int vis = cand + SEG;
-      const int jvis = c0 ? (vis - q0) : 0;
-      const uint32_t c0fp = cand_lo | 1u;
-      uint32_t ovfv[8];
+      const int rvis = vis - p;
+      const uint32_t c0k = probe_key(cand_lo);
+      const uint32_t* lf = lfilt;
+      const u32x4* ft = prm.lf.ftab;
+      const uint32_t fm = prm.lf.fmask;
+      if (novf == 0) {
+        if (c0)
+          ev = roll_probe<LOGNB, true, false, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, nullptr, lf, ft, fm);
+        else
+          ev = roll_probe<LOGNB, false, false, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, nullptr, lf, ft, fm);
+      } else {
+        // duplicates of a real overflow key pad the unused slots
+        uint32_t ovk[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) ovfv[k] = (uint32_t)k < novf ? readfirst(T.ovf_fp[k]) : 0u;
-      if (c0)
-        ev = roll_probe<LOGNB, true, STREAM>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0, lfilt,
-                                             prm.lf.ftab, prm.lf.fmask);
-      else
-        ev = roll_probe<LOGNB, false, STREAM>(P, X1, X2c, F1, F2, T.fp, c0fp, jvis, ovfv, novf, lo0, bh0, lfilt,
-                                              prm.lf.ftab, prm.lf.fmask);
+        for (int k = 0; k < 8; ++k) ovk[k] = readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]);
+        if (c0)
+          ev = roll_probe<LOGNB, true, true, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+        else
+          ev = roll_probe<LOGNB, false, true, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+      }
       // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
       const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
       ev &= vm;
-    } else {
-      lo0 = (X1 << 20) + X2c;
-      bh0 = (F1 << 16) + F2;
     }
 
     // ---- resolve phase (wave-uniform)
@@ -514,8 +567,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
     auto hash_at = [&](int pos, uint32_t& lo, uint32_t& hi) {
       const int rel = pos - p;
       if ((rel & 31) == 0) {
-        lo = readlane(lo0, rel >> 5);
-        hi = readlane(bh0, rel >> 5) << 4;
+        lo = 0u - readlane(k0, rel >> 5);
+        hi = readfirst(lane_window_hi(P, rel >> 5));
       } else {
         const uint2 h = window_hash_u(x + pos);
         lo = h.x; hi = h.y;
@@ -588,7 +641,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
     }
     // The table holds every declaration once the piece is done; a still
     // pending candidate stays out of it until declared.
-    totXA = totXB; totTA = totTB; totFA = totFB; totTFA = totTFB;
+    totXA = totXB; totTA = totTB;
   }
 
   if (have_cand) declare();                                   // :257-261
@@ -623,26 +676,25 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, WaveTable<LOG
 
 template <int LOGNB, int MAXD>
 __global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams prm) {
-  __shared__ WaveTable<LOGNB, MAXD> tabs[4];
+  __shared__ IndepLDS<LOGNB, MAXD, 4> S;
   const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
   if (chunk >= prm.n) return;
-  encode_chunk<LOGNB, MAXD, false>(prm, tabs[wv], chunk, nullptr);
+  encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, nullptr);
 }
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
 // the lane filter; each wave walks chunks wave_id, wave_id + total_waves, ...
 template <int LOGNB, int MAXD, int SW>
 __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
-  __shared__ uint32_t lfilt[FILT_WORDS];
-  __shared__ WaveTable<LOGNB, MAXD> tabs[SW];
+  __shared__ StreamLDS<LOGNB, MAXD, SW> S;
   for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
-    ((u32x4*)lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
+    ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
   __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
   const uint32_t stride = gridDim.x * SW;
   for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride)
-    encode_chunk<LOGNB, MAXD, true>(prm, tabs[wv], chunk, lfilt);
+    encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, S.lfilt);
 }
 
 template __global__ void encode_independent_kernel<9, 72>(EncParams);
