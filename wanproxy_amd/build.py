@@ -11,18 +11,21 @@ OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
+def build_lib(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Build the library (or, for diagnostics, a variant at `out` with extra
+    -D `defines`, e.g. XCG_TIMING: per-wave timestamps in the stats words)."""
+    out = os.path.abspath(out)
     srcs = [os.path.join(HERE, s) for s in SRCS]
     deps = srcs + [os.path.join(HERE, 'csrc/xcg_device.h'), os.path.join(HERE, 'csrc/xcg_cache.h'), os.path.join(HERE, '..', 'include', 'xcgpu.h')]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     cmd = [HIPCC, '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
-           '-o', OUT + '.tmp'] + srcs
+           '-o', out + '.tmp'] + ['-D' + d for d in defines] + srcs
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True, cwd=HERE)
-    os.replace(OUT + '.tmp', OUT)
-    return OUT
+    os.replace(out + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':

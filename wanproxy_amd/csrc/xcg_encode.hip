@@ -212,6 +212,11 @@ __device__ __forceinline__ bool equal2048_u(const uint8_t* a, const uint8_t* b) 
 
 // ------------------------------------------------------------ vector phase
 
+// Make the registers of v live here (the compiler waits for their load first).
+__device__ __forceinline__ void vuse(const u32x4& v) {
+  asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+}
+
 struct Piece {
   u32x4 a0, a1;   // bytes [q0, q0+32): the windows' leaving bytes
   u32x4 b0, b1;   // bytes [q0+2048, q0+2080): the entering bytes
@@ -265,7 +270,7 @@ __device__ __forceinline__ uint64_t lanes_eq(uint32_t a, uint32_t b) { return __
 __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
   uint32_t r;
   uint64_t co;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(ev), "s"(m));
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(ev), "s"(readfirst64(m)));
   return r;
 }
 
@@ -374,6 +379,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   uint32_t olen = 0;
   uint32_t n_extract = 0, n_ref = 0, n_coll = 0, n_pieces = 0;
 
+#ifdef XCG_TIMING
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   if (L < SEG) {                                   // xcodec_encoder.cc:77-83
     if (L > 0) olen = escape_u(out, x, 0, (uint32_t)L);
     if (l == 0) prm.out_len[chunk] = olen;
@@ -390,6 +398,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   bool have_cand = false;
   int cand = 0;
   uint32_t cand_lo = 0, cand_hi = 0;
+  // In-band independent encoding never outputs a declared hash, and its hi half
+  // only matters when a later window matches the declaration's lo: then it is
+  // computed from the declared bytes (lookup).  HI_LAZY (odd) marks "not yet";
+  // a real hi has its low 4 bits clear (mix(), xcodec_hash.h:155-164).
+  constexpr uint32_t HI_LAZY = 1u;
+  const bool lazy_hi = !STREAM && !oob;
   bool c0_in_table = true;                         // pending candidate already inserted?
 
   Piece P;
@@ -427,23 +441,24 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     __builtin_amdgcn_wave_barrier();
   };
 
-  // Exact lookup: declaration index whose hash is (lo, hi), or -1.
+  // Exact lookup: declaration index whose hash is (lo, hi), or -1; or -2 - d
+  // when record d matches lo but its hi has not been computed yet.
+  auto rec_matches = [&](uint32_t d, uint32_t lo, uint32_t hi, int& found) {
+    if (readfirst(T.rlo[d]) != lo) return;
+    const uint32_t rh = readfirst(T.rhi[d]);
+    if (rh == HI_LAZY) found = -2 - (int)d;
+    else if (rh == hi) found = (int)d;
+  };
   auto lookup = [&](uint32_t lo, uint32_t hi) -> int {
     const uint32_t key = probe_key(lo);
     const uint32_t b = kbucket<LOGNB>(key);
     int found = -1;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      if (readfirst(keyt[2 * b + k]) == key) {
-        const uint32_t d = readfirst(T.idx[2 * b + k]);
-        if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
-      }
+      if (found == -1 && readfirst(keyt[2 * b + k]) == key) rec_matches(readfirst(T.idx[2 * b + k]), lo, hi, found);
     }
-    for (uint32_t k = 0; k < novf && found < 0; ++k) {
-      if (readfirst(T.ovf_k[k]) == key) {
-        const uint32_t d = readfirst(T.ovf_idx[k]);
-        if (readfirst(T.rlo[d]) == lo && readfirst(T.rhi[d]) == hi) found = (int)d;
-      }
+    for (uint32_t k = 0; k < novf && found == -1; ++k) {
+      if (readfirst(T.ovf_k[k]) == key) rec_matches(readfirst(T.ovf_idx[k]), lo, hi, found);
     }
     return found;
   };
@@ -473,26 +488,22 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     const int q0 = p + 32 * l;
     const bool contig = (p == p_prev + SEG);
     ++n_pieces;
+    // vmcnt counts loads and stores together, in order (gfx9): every wait on
+    // a load also waits for all older stores.  So fresh loads are waited for
+    // here, inside their branch, and the prefetch below is waited for after
+    // the vector phase -- never right behind its own issue.
+    // (contig implies nb_start == p: the previous piece prefetched this B.)
     if (contig) {
       P.a0 = P.b0; P.a1 = P.b1;
       P.sxa = P.sxb; P.sqxa = P.sqxb;
+      P.b0 = nb0; P.b1 = nb1;
     } else {
       P.a0 = load16_aligned_safe(x, q0, L);
       P.a1 = load16_aligned_safe(x, q0 + 16, L);
-      seg_sums(P.a0, P.a1, P.sxa, P.sqxa);
-    }
-    if (nb_start == p) {
-      P.b0 = nb0; P.b1 = nb1;
-    } else {
       P.b0 = load16_aligned_safe(x, q0 + SEG, L);
       P.b1 = load16_aligned_safe(x, q0 + SEG + 16, L);
-    }
-    // Prefetch the next contiguous piece's entering bytes; they land while
-    // this piece rolls.
-    nb_start = p + SEG;
-    if (nb_start <= last) {
-      nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
-      nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
+      vuse(P.a0); vuse(P.a1); vuse(P.b0); vuse(P.b1);
+      seg_sums(P.a0, P.a1, P.sxa, P.sqxa);
     }
     seg_sums(P.b0, P.b1, P.sxb, P.sqxb);
     p_prev = p;
@@ -514,6 +525,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // probe key of the lane's first window
     const uint32_t NX1 = 0u - X1, NX2 = 0u - X2c;
     const uint32_t k0 = (NX1 << 20) + NX2;
+
+    // Prefetch the next contiguous piece's entering bytes; they land while
+    // this piece rolls (issued after every use of this piece's loads).
+    nb_start = p + SEG;
+    if (nb_start <= last) {
+      nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
+      nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
+    }
 
     // ---- vector phase
     uint32_t ev = 0;
@@ -552,6 +571,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
       ev &= vm;
     }
+    // The prefetch has had the vector phase to land; take it before the
+    // resolve phase issues this piece's stores.
+    vuse(nb0); vuse(nb1);                          // (unconditional: so the compiler sees them waited)
 
     // ---- resolve phase (wave-uniform)
     auto next_event = [&](int from) -> int {
@@ -568,7 +590,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const int rel = pos - p;
       if ((rel & 31) == 0) {
         lo = 0u - readlane(k0, rel >> 5);
-        hi = readfirst(lane_window_hi(P, rel >> 5));
+        hi = lazy_hi ? HI_LAZY : readfirst(lane_window_hi(P, rel >> 5));
       } else {
         const uint2 h = window_hash_u(x + pos);
         lo = h.x; hi = h.y;
@@ -579,10 +601,24 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       if (have_cand && cand + SEG <= s) declare();            // :183-190
       const int e = nullcache ? INT32_MAX : next_event(s);
       if (e == s) {
-        // Exact re-check of the probe (find_reference, :374-416).
-        const uint2 hh = window_hash_u(x + s);
-        const uint32_t lo = hh.x, hi = hh.y;
-        const int d = lookup(lo, hi);
+        // Exact re-check of the probe (find_reference, :374-416).  A record
+        // still missing its hi gets it from the same (single) hash call site,
+        // then the window is hashed again.
+        uint32_t lo = 0, hi = 0;
+        int d = -1, fill = -1;
+        for (;;) {
+          const uint2 hh = window_hash_u(fill >= 0 ? x + readfirst(T.rc[fill]) : x + s);
+          if (fill >= 0) {
+            if (l == 0) T.rhi[fill] = hh.y;
+            __builtin_amdgcn_wave_barrier();
+            fill = -1;
+            continue;
+          }
+          lo = hh.x; hi = hh.y;
+          d = lookup(lo, hi);
+          if (d >= -1) break;
+          fill = -2 - d;
+        }
         // Where the hash is declared: this chunk (d), the persistent cache, or
         // an earlier chunk of the batch.  src = that segment's bytes.
         const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
@@ -665,10 +701,20 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   if (l == 0) {
     prm.out_len[chunk] = olen;
     if (prm.stats) {
+#ifdef XCG_TIMING
+      // diagnostics build: {start, end} (100 MHz realtime, low words), HW_ID, XCC_ID
+      const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+      prm.stats[4 * chunk + 0] = (uint32_t)t_start;
+      prm.stats[4 * chunk + 1] = (uint32_t)t_end;
+      prm.stats[4 * chunk + 2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+      prm.stats[4 * chunk + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));   // HW_REG_XCC_ID
+      (void)n_extract; (void)n_ref; (void)n_coll; (void)n_pieces;
+#else
       prm.stats[4 * chunk + 0] = n_extract;
       prm.stats[4 * chunk + 1] = n_ref;
       prm.stats[4 * chunk + 2] = n_coll;
       prm.stats[4 * chunk + 3] = n_pieces;
+#endif
     }
   }
 }

@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libxcgpu.so')
+# XCGPU_LIB selects a diagnostic build of the same library (scripts/dev).
+LIB_PATH = os.environ.get('XCGPU_LIB') or os.path.join(HERE, 'libxcgpu.so')
 SEG = 2048
 
 XCG_FLAG_OOB = 0x1
