@@ -20,7 +20,7 @@
  *                                                      xcodec/xcodec_encoder.cc:74-274
  *       (one encode() call per chunk, exactly as tack / XCodecPipePair issue
  *        them: programs/tack/tack.cc:308-321, xcodec/xcodec_pipe_pair.cc:596-630)
- *   xcg_decode_batch / xcg_decode_host
+ *   xcg_decode_batch / xcg_decode_host / xcg_window_*
  *       bool XCodecDecoder::decode(Buffer *output, Buffer *input,
  *                                  std::set<uint64_t>& unknown_hashes)
  *                                                      xcodec/xcodec_decoder.h:44,
@@ -137,16 +137,29 @@ int xcg_encode_host(xcg_ctx *ctx, int semantics, const uint8_t *h_in, uint64_t i
  * out_cap nothing is written and XCG_EOVERFLOW is returned.
  * d_chunk_status[i]: 0 decoded, 1 blocked on an unknown REF (decode() returned
  * true with unknown hashes; later chunks get 2 = not reached), 3 partial op,
- * -1 bad opcode (decode() returned false).  h_unknown receives the sorted
- * unknown hashes (decode_skim, :196-272) for the ASK/LEARN protocol.
- * EXTRACTs decoded before any blocking point enter the persistent cache
- * (enter / replace, :106-136).  Streams containing BACKREF (never emitted by
- * XCodecEncoder) return XCG_ENOTSUP.  Synchronises `stream`.
+ * -1 bad opcode or BACKREF to an empty window slot (decode() returned false;
+ * later chunks get 2).  h_unknown receives the sorted unknown hashes from the
+ * blocking point to the end of the batch (decode_skim, :196-272, over the
+ * frames a pipe pair has buffered) for the ASK/LEARN protocol.
+ * EXTRACTs decoded before the stop point enter the persistent cache
+ * (enter / replace, :106-136) and every EXTRACT / REF declares into the
+ * decoder's BACKREF window.  Synchronises `stream`.
  */
 int xcg_decode_batch(xcg_ctx *ctx, const uint8_t *d_enc, const uint64_t *d_chunk_off, const uint32_t *d_chunk_len,
                      uint32_t n, uint32_t max_chunk_len, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                      uint64_t *d_out_len, int32_t *d_chunk_status, uint64_t *d_consumed, uint64_t *h_unknown,
                      uint32_t unknown_cap, uint32_t *h_nunknown, uint64_t *h_total_out, void *stream);
+
+/* A decoder's BACKREF window (XCodecWindow, xcodec/xcodec_window.h:40-125):
+ * 256 slots of (hash, segment) that EXTRACT and REF declare into and
+ * <BACKREF> index reads (xcodec/xcodec_decoder.cc:137,160,165-181).  It lives
+ * as long as the decoder: one per XCodecDecoder (the cache may be shared).
+ * Decodes use the context's own window unless xcg_decode_set_window selected
+ * another (NULL = back to the context's own). */
+typedef struct xcg_window xcg_window;
+int xcg_window_create(xcg_ctx *ctx, xcg_window **out);
+void xcg_window_destroy(xcg_window *win);
+int xcg_decode_set_window(xcg_ctx *ctx, xcg_window *win);
 
 /* Host-memory convenience over xcg_decode_batch. */
 int xcg_decode_host(xcg_ctx *ctx, const uint8_t *h_enc, uint64_t enc_len, const uint64_t *h_chunk_off,

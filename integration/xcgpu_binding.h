@@ -70,6 +70,36 @@ inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 	return ctx;
 }
 
+/* One BACKREF window per XCodecDecoder object (the reference's
+ * XCodecDecoder::window_ member, xcodec/xcodec_decoder.h:37); the header's
+ * members are unchanged, so the handle is kept beside the object. */
+inline std::map<const void *, xcg_window *>& window_map()
+{
+	static std::map<const void *, xcg_window *> wins;
+	return wins;
+}
+
+inline xcg_window *window_for(const void *decoder, xcg_ctx *ctx)
+{
+	std::map<const void *, xcg_window *>::iterator it = window_map().find(decoder);
+	if (it != window_map().end())
+		return it->second;
+	xcg_window *w = NULL;
+	if (xcg_window_create(ctx, &w) != XCG_OK)
+		return NULL;
+	window_map()[decoder] = w;
+	return w;
+}
+
+inline void forget_window(const void *decoder)
+{
+	std::map<const void *, xcg_window *>::iterator it = window_map().find(decoder);
+	if (it == window_map().end())
+		return;
+	xcg_window_destroy(it->second);
+	window_map().erase(it);
+}
+
 }  // namespace xcgpu_binding
 
 #endif /* !XCGPU_BINDING_H */

@@ -29,7 +29,46 @@ XCodecDecoder::XCodecDecoder(XCodecCache *cache)
 { }
 
 XCodecDecoder::~XCodecDecoder()
-{ }
+{
+	xcgpu_binding::forget_window(this);
+}
+
+/* Host cache mirror of the EXTRACTs in in[a..b) (enter / replace, :106-136). */
+static void
+mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, uint64_t b)
+{
+	uint64_t i = a;
+	while (i + 1 < b) {
+		if (in[i] != XCODEC_MAGIC) {
+			i++;
+			continue;
+		}
+		const uint8_t op = in[i + 1];
+		if (op == XCODEC_OP_EXTRACT) {
+			const uint8_t *p = &in[i + 2];
+			const uint64_t hash = XCodecHash::hash(p);
+			Buffer tmp(p, XCODEC_SEGMENT_LENGTH);
+			BufferSegment *seg;
+			tmp.copyout(&seg, XCODEC_SEGMENT_LENGTH);
+			BufferSegment *oseg = cache->lookup(hash);
+			if (oseg == NULL) {
+				cache->enter(hash, seg);
+			} else {
+				if (!oseg->equal(seg))
+					cache->replace(hash, seg);
+				oseg->unref();
+			}
+			seg->unref();
+			i += 2 + XCODEC_SEGMENT_LENGTH;
+		} else if (op == XCODEC_OP_REF) {
+			i += 10;
+		} else if (op == XCODEC_OP_BACKREF) {
+			i += 3;
+		} else {
+			i += 2;
+		}
+	}
+}
 
 bool
 XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown_hashes)
@@ -39,24 +78,48 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	xcg_ctx *ctx = xcgpu_binding::ctx_for(cache_, cache_->out_of_band());
 	if (ctx == NULL)
 		HALT(log_) << "No MI355X device for the XCodec engine.";
+	xcg_window *win = xcgpu_binding::window_for(this, ctx);
+	if (win == NULL)
+		HALT(log_) << "No device memory for the XCodec window.";
 
 	const uint32_t len = input->length();
 	std::vector<uint8_t> in(len);
 	input->copyout(&in[0], len);
-	const uint64_t off = 0;
-	uint64_t ooff = 0, olen = 0, consumed = 0;
-	int32_t status = 0;
 	std::vector<uint8_t> out((uint64_t)len * 205 + 4096);
 	std::vector<uint64_t> unk(1u << 16);
+	uint64_t pos = 0;
+	int32_t status = 0;
 	uint32_t nunk = 0;
+	xcg_decode_set_window(ctx, win);
+	/*
+	 * The GPU decodes from pos until the end, a bad op, or a REF its cache
+	 * does not hold.  In the last case the hashes the host cache learned
+	 * (ASK/LEARN, xcodec/xcodec_pipe_pair.cc:274-333) go to the GPU and the
+	 * decode continues from the blocking REF, as decode() itself would with
+	 * those hashes in its cache; what stays unknown is returned like
+	 * decode_skim (:196-272).
+	 */
 	for (;;) {
-		int rc = xcg_decode_host(ctx, &in[0], len, &off, &len, 1, &out[0], out.size(), &ooff, &olen, &status,
+		const uint64_t off = 0;
+		const uint32_t rest = (uint32_t)(len - pos);
+		uint64_t ooff = 0, olen = 0, consumed = 0;
+		int rc = xcg_decode_host(ctx, &in[pos], rest, &off, &rest, 1, &out[0], out.size(), &ooff, &olen, &status,
 		                         &consumed, &unk[0], unk.size(), &nunk);
-		if (rc != XCG_OK)
+		if (rc == XCG_EOVERFLOW) {
+			/* BACKREF-dense input: 3 bytes can decode to 2048 (nothing was committed). */
+			out.resize((uint64_t)rest / 3 * XCODEC_SEGMENT_LENGTH + rest + 4096);
+			rc = xcg_decode_host(ctx, &in[pos], rest, &off, &rest, 1, &out[0], out.size(), &ooff, &olen,
+			                     &status, &consumed, &unk[0], unk.size(), &nunk);
+		}
+		if (rc != XCG_OK) {
+			xcg_decode_set_window(ctx, NULL);
 			HALT(log_) << "xcgpu decode failed: " << xcg_strerror(rc);
-		if (status != 1)
+		}
+		mirror_extracts(cache_, in, pos, pos + consumed);
+		output->append(&out[0], olen);
+		pos += consumed;
+		if (status != 1 || pos >= len)
 			break;
-		/* Blocked: anything the host cache learned since goes to the GPU. */
 		unsigned pushed = 0;
 		for (uint32_t k = 0; k < nunk; k++) {
 			BufferSegment *seg = cache_->lookup(unk[k]);
@@ -69,46 +132,18 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		if (pushed == 0)
 			break;
 	}
+	xcg_decode_set_window(ctx, NULL);
 
-	/* Mirror the consumed EXTRACTs into the host cache. */
-	uint64_t i = 0;
-	while (i + 1 < consumed) {
-		if (in[i] != XCODEC_MAGIC) {
-			i++;
-			continue;
-		}
-		const uint8_t op = in[i + 1];
-		if (op == XCODEC_OP_EXTRACT) {
-			const uint8_t *p = &in[i + 2];
-			const uint64_t hash = XCodecHash::hash(p);
-			Buffer tmp(p, XCODEC_SEGMENT_LENGTH);
-			BufferSegment *seg;
-			tmp.copyout(&seg, XCODEC_SEGMENT_LENGTH);
-			BufferSegment *oseg = cache_->lookup(hash);
-			if (oseg == NULL) {
-				cache_->enter(hash, seg);
-			} else {
-				if (!oseg->equal(seg))
-					cache_->replace(hash, seg);
-				oseg->unref();
-			}
-			window_.declare(hash, seg);
-			seg->unref();
-			i += 2 + XCODEC_SEGMENT_LENGTH;
-		} else if (op == XCODEC_OP_REF) {
-			i += 10;
-		} else if (op == XCODEC_OP_BACKREF) {
-			i += 3;
-		} else {
-			i += 2;
-		}
-	}
-
-	output->append(&out[0], olen);
-	input->skip(consumed);
+	input->skip(pos);
 	if (status == 1) {
-		for (uint32_t k = 0; k < nunk; k++)
+		for (uint32_t k = 0; k < nunk; k++) {
+			BufferSegment *seg = cache_->lookup(unk[k]);
+			if (seg != NULL) {
+				seg->unref();
+				continue;
+			}
 			unknown_hashes.insert(unk[k]);
+		}
 		return (true);
 	}
 	return (status >= 0);

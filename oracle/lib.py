@@ -68,6 +68,15 @@ class Oracle:
         if ref:
             self._dec.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u64p, _u64p, C.c_uint64]
             self._dec.restype = C.c_int
+            self._dnew = getattr(L, pre + 'decoder_new')
+            self._dnew.restype = C.c_void_p
+            self._dnew.argtypes = [C.c_void_p]
+            self._dfree = getattr(L, pre + 'decoder_free')
+            self._dfree.argtypes = [C.c_void_p]
+            self._ddec = getattr(L, pre + 'decoder_decode')
+            self._ddec.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u64p, _u64p,
+                                   C.c_uint64]
+            self._ddec.restype = C.c_int
         else:
             L.xco_decoder_new.restype = C.c_void_p
             L.xco_decoder_new.argtypes = [C.c_void_p]
@@ -132,16 +141,30 @@ class Oracle:
         return b''.join(self.encode_batch(data, offs, lens, mode=mode, oob=oob, cache=cache))
 
     # ---------------------------------------------------------------- decode
+    def decoder_new(self, cache):
+        """A persistent XCodecDecoder on `cache` (its BACKREF window lives
+        across decode() calls)."""
+        return self._dnew(cache) if self.ref else self.lib.xco_decoder_new(cache)
+
+    def decoder_free(self, d):
+        if self.ref:
+            self._dfree(d)
+        else:
+            self.lib.xco_decoder_free(d)
+
     def decode(self, enc: bytes, cache, out_cap=None, decoder=None):
         """One XCodecDecoder::decode over `enc`.  Returns (ok, out, consumed, unknown)."""
         a = np.frombuffer(enc, dtype=np.uint8)
-        cap = out_cap or (a.size // 10 + 1) * SEG + a.size
+        cap = out_cap or (a.size // 3 + 1) * SEG + a.size   # a 3-byte BACKREF expands to 2048
         out = np.zeros(cap, dtype=np.uint8)
         ol = np.zeros(1, dtype=np.uint64)
         cons = np.zeros(1, dtype=np.uint64)
         unk = np.zeros(4096, dtype=np.uint64)
         nunk = np.zeros(1, dtype=np.uint64)
-        if self.ref:
+        if self.ref and decoder is not None:
+            rc = self._ddec(decoder, _p(a, _u8p), a.size, _p(out, _u8p), cap, _p(ol, _u64p), _p(cons, _u64p),
+                            _p(unk, _u64p), _p(nunk, _u64p), unk.size)
+        elif self.ref:
             rc = self._dec(cache, _p(a, _u8p), a.size, _p(out, _u8p), cap, _p(ol, _u64p), _p(cons, _u64p),
                            _p(unk, _u64p), _p(nunk, _u64p), unk.size)
         else:

@@ -130,6 +130,28 @@ int xcr_encode_batch(void *cache, const uint8_t *in, const uint64_t *off, const 
 /* One XCodecDecoder::decode over a whole buffer with cache `cache`
  * (tack -d, programs/tack/tack.cc:329-359).  Returns 1/0 like decode(),
  * -1 on overflow; *consumed = bytes parsed; *nunk = unknown hashes. */
+/* A persistent XCodecDecoder (its BACKREF window lives across calls). */
+void *xcr_decoder_new(void *cache) { return new XCodecDecoder((XCodecCache *)cache); }
+void xcr_decoder_free(void *dec) { delete (XCodecDecoder *)dec; }
+
+int xcr_decoder_decode(void *dec, const uint8_t *x, uint64_t len, uint8_t *out, uint64_t cap,
+                       uint64_t *out_len, uint64_t *consumed, uint64_t *unk, uint64_t *nunk, uint64_t unk_max)
+{
+	Buffer input, output;
+	input.append(x, len);
+	std::set<uint64_t> unknown;
+	bool ok = ((XCodecDecoder *)dec)->decode(&output, &input, unknown);
+	*consumed = len - input.length();
+	*nunk = 0;
+	for (std::set<uint64_t>::const_iterator it = unknown.begin(); it != unknown.end() && *nunk < unk_max; ++it)
+		unk[(*nunk)++] = *it;
+	uint64_t r = drain(&output, out, cap);
+	if (r == ~(uint64_t)0)
+		return -1;
+	*out_len = r;
+	return ok ? 1 : 0;
+}
+
 int xcr_decode(void *cache, const uint8_t *x, uint64_t len, uint8_t *out, uint64_t cap,
                uint64_t *out_len, uint64_t *consumed, uint64_t *unk, uint64_t *nunk, uint64_t unk_max)
 {

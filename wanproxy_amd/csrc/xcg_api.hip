@@ -85,6 +85,11 @@ struct XcgDecodeArgs {
   uint32_t unknown_cap;
   uint64_t* scratch;
   uint64_t* h_scratch;
+  uint64_t* chunk_tmp;
+  uint4* d_tail;
+  uint64_t* win_hash;
+  uint8_t* win_seg;
+  uint64_t win_count;
 };
 extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*, uint32_t, uint8_t*, uint64_t*,
                                uint64_t*, hipStream_t);
@@ -92,7 +97,7 @@ extern "C" int xcg_launch_cache_lookup(uint64_t*, uint64_t*, uint32_t, const uin
                                        hipStream_t);
 extern "C" int xcg_launch_cache_enter(uint64_t*, uint64_t*, uint32_t, uint8_t*, uint32_t*, uint32_t, uint32_t*,
                                       uint32_t*, uint32_t, uint64_t, const uint8_t*, int, int32_t*, hipStream_t);
-extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
+extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 
 // The persistent segment cache of a context: XCodecMemoryCache's
 // hash_map<Tag64, BufferSegment*> (xcodec/xcodec_cache.h:270) as an
@@ -133,6 +138,19 @@ struct DecodeScratch {
   uint32_t* nunknown = nullptr;
   uint64_t* scratch = nullptr;
   uint64_t* h_scratch = nullptr;   // pinned
+  uint32_t chunk_cap = 0;
+  uint64_t* chunk_tmp = nullptr;   // 4 u64 per chunk (declare counts / bases)
+  uint4* d_tail = nullptr;         // 256 declare records (window update)
+};
+
+// A decoder's BACKREF window (XCodecWindow, xcodec/xcodec_window.h): 256 slots
+// of (hash, owned 2048-byte copy) and the number of declares made so far
+// (cursor = count mod 256).  One per XCodecDecoder; a context has a default.
+struct xcg_window {
+  int device = 0;
+  uint64_t* hash = nullptr;
+  uint8_t* seg = nullptr;
+  uint64_t count = 0;
 };
 constexpr uint32_t UNKNOWN_CAP = 1u << 16;
 
@@ -145,6 +163,8 @@ struct xcg_ctx {
   BatchScratch bs;
   int last_rounds;
   DecodeScratch ds;
+  xcg_window* own_win = nullptr;   // default window (lazily allocated)
+  xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
 };
 
 namespace {
@@ -234,8 +254,42 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
 void free_dscratch(DecodeScratch& d) {
   (void)hipFree(d.x_keys); (void)hipFree(d.x_vals); (void)hipFree(d.x_latest); (void)hipFree(d.unknown);
   (void)hipFree(d.unknown_pos); (void)hipFree(d.nunknown); (void)hipFree(d.scratch);
+  (void)hipFree(d.chunk_tmp); (void)hipFree(d.d_tail);
   if (d.h_scratch) (void)hipHostFree(d.h_scratch);
   d = DecodeScratch{};
+}
+
+int ensure_dchunks(xcg_ctx* c, uint32_t n) {
+  DecodeScratch& d = c->ds;
+  if (!d.d_tail && hipMalloc(&d.d_tail, 16ull * 256) != hipSuccess) return XCG_ENOMEM;
+  if (d.chunk_tmp && n <= d.chunk_cap) return XCG_OK;
+  (void)hipFree(d.chunk_tmp);
+  d.chunk_tmp = nullptr;
+  d.chunk_cap = n < 1024 ? 1024 : n;
+  if (hipMalloc(&d.chunk_tmp, 32ull * d.chunk_cap) != hipSuccess) {
+    d.chunk_cap = 0;
+    return XCG_ENOMEM;
+  }
+  return XCG_OK;
+}
+
+int window_alloc(int device, xcg_window** out) {
+  xcg_window* w = new xcg_window;
+  w->device = device;
+  if (hipMalloc(&w->hash, 8ull * 256) != hipSuccess || hipMalloc(&w->seg, 256ull * 2048) != hipSuccess ||
+      hipMemset(w->hash, 0, 8ull * 256) != hipSuccess) {
+    (void)hipFree(w->hash); (void)hipFree(w->seg);
+    delete w;
+    return XCG_ENOMEM;
+  }
+  *out = w;
+  return XCG_OK;
+}
+
+void window_free(xcg_window* w) {
+  if (!w) return;
+  (void)hipFree(w->hash); (void)hipFree(w->seg);
+  delete w;
 }
 
 int ensure_dscratch(xcg_ctx* c, uint64_t max_extracts) {
@@ -307,6 +361,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   free_cache(c->g);
   free_scratch(c->bs);
   free_dscratch(c->ds);
+  window_free(c->own_win);
   delete c;
 }
 
@@ -526,27 +581,42 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   DeviceGuard g(c->device);
   int rc = ensure_cache(c);
   if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));
+  if (rc == XCG_OK) rc = ensure_dchunks(c, n);
+  if (rc == XCG_OK && !c->cur_win) {
+    rc = window_alloc(c->device, &c->own_win);
+    c->cur_win = c->own_win;
+  }
   if (rc != XCG_OK) return rc;
+  xcg_window* w = c->cur_win;
   XcgDecodeArgs a{d_enc, d_chunk_off, d_chunk_len, n, d_out, out_cap, d_out_off, d_out_len, d_chunk_status,
                   d_consumed, c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                   c->g.filt, c->g.ftab, c->g.fmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
-                  c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch};
-  uint64_t total = 0, blockp = 0;
+                  c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
+                  c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count};
+  uint64_t total = 0, blockp = 0, berr = 0;
   uint32_t nunk = 0;
-  const int lrc = xcg_launch_decode(&a, &total, &blockp, &nunk, (hipStream_t)stream);
+  const int lrc = xcg_launch_decode(&a, &total, &blockp, &berr, &nunk, (hipStream_t)stream);
   if (h_total_out) *h_total_out = total;
   if (lrc == -75) return XCG_EOVERFLOW;
   if (lrc != 0) return XCG_EHIP;
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return XCG_EHIP;
   int32_t st = 0;
-  if (hipMemcpy(&st, c->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
-  if (st & ((1 << 8) | (1 << 9))) {
+  uint64_t t_end = 0;
+  if (hipMemcpy(&st, c->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&t_end, c->ds.scratch + 5, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return XCG_EHIP;
+  w->count += t_end;                                  // declares made: the window cursor advances
+  if (st & (1 << 9)) {
     (void)hipMemset(c->d_status, 0, 4);
     return XCG_ENOTSUP;
   }
-  if (nunk) {
-    // XCodecDecoder::decode_skim (xcodec/xcodec_decoder.cc:196-272): every
-    // REF from the blocking point on that cannot resolve, as a sorted set.
+  if (nunk && blockp < berr) {
+    // XCodecDecoder::decode_skim (xcodec/xcodec_decoder.cc:196-272): every REF
+    // from the blocking point on that cannot resolve, as a sorted set.  The
+    // batch's frames are one buffered stream (a pipe pair appends each FRAME
+    // to the decoder's input, xcodec/xcodec_pipe_pair.cc:425-483), so the skim
+    // runs to the end of the batch.  (A BACKREF error first: decode() is false,
+    // no ASK.)
     const uint32_t m = nunk < UNKNOWN_CAP ? nunk : UNKNOWN_CAP;
     std::vector<uint64_t> hs(m);
     if (hipMemcpy(hs.data(), c->ds.unknown, 8ull * m, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
@@ -556,6 +626,24 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
     if (h_unknown) memcpy(h_unknown, hs.data(), 8ull * k);
     if (h_nunknown) *h_nunknown = k;
   }
+  return XCG_OK;
+}
+
+int xcg_window_create(xcg_ctx* c, xcg_window** out) {
+  if (!c || !out) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  return window_alloc(c->device, out);
+}
+
+void xcg_window_destroy(xcg_window* w) {
+  if (!w) return;
+  DeviceGuard g(w->device);
+  window_free(w);
+}
+
+int xcg_decode_set_window(xcg_ctx* c, xcg_window* w) {
+  if (!c) return XCG_EINVAL;
+  c->cur_win = w ? w : c->own_win;
   return XCG_OK;
 }
 

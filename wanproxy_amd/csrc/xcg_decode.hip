@@ -19,8 +19,16 @@
 //   commit EXTRACTs before the blocking point enter the cache
 //          (XCodecMemoryCache::enter / replace, :120-136).
 //
-// BACKREF (:165-181) is never produced by XCodecEncoder (it only declares into
-// its window); streams containing it are rejected with XCG_ENOTSUP.
+// BACKREF (:165-181) reads the decoder's XCodecWindow (xcodec/xcodec_window.h):
+// every EXTRACT and resolved REF declares its hash into slot k mod 256 (k =
+// declares made by this decoder so far), emptying the slot that held the same
+// hash before (:68-100).  Slot c at declare count G therefore holds the latest
+// declare g < G with g = c (mod 256) unless that hash was declared again in
+// (g, G).  The scan counts declares per chunk; an exclusive scan numbers them;
+// `decl_record` writes (hash, bytes) records of the declares a BACKREF or the
+// window update can reach; an invalid BACKREF stops the stream like an unknown
+// REF (decode() returns false there, :172-176); `window_update` carries the
+// 256 slots (hash + an owned copy of the bytes) into the next batch.
 #include "xcg_cache.h"
 
 namespace xcg {
@@ -44,7 +52,20 @@ struct DecParams {
   uint32_t* nunknown;
   uint32_t unknown_cap;
   uint64_t* block_pos;         // min stream position of an unresolvable REF (atomicMin)
-  int32_t* status;             // bit 8: BACKREF seen, bit 9: EXTRACT name reuse inside the batch
+  int32_t* status;             // bit 9: EXTRACT name reuse inside the batch
+  // ---- BACKREF window
+  uint64_t* berr_pos;          // min stream position of a BACKREF to an empty slot (atomicMin)
+  uint64_t* n_decl;            // scan: declares (EXTRACT + REF) per chunk
+  uint64_t* n_bref;            // scan: BACKREFs per chunk
+  const uint64_t* decl_base;   // exclusive scan of n_decl: batch index of the chunk's first declare
+  uint64_t* n_decl_emit;       // emit: declares made before the chunk stopped
+  uint64_t* t_end;             // declares of the batch before the stop point
+  uint4* D;                    // declare records (lo, hi, src lo, src hi), batch indices [D_lo, ...)
+  uint64_t D_lo;               // (tail mode: D_lo = max(t_end - 256, 0), read from *t_end)
+  bool D_tail;
+  uint64_t* win_hash;          // the decoder's window: 256 hashes (0 = empty slot)
+  uint8_t* win_seg;            //   and the bytes of each slot
+  uint64_t win_count;          // declares made before this batch
 };
 
 __device__ __forceinline__ uint64_t spos(uint32_t chunk, uint32_t off) { return ((uint64_t)chunk << 32) | off; }
@@ -187,6 +208,54 @@ __device__ __forceinline__ bool xtab_insert(HashTab t, uint64_t* latest, uint32_
   return false;
 }
 
+// ------------------------------------------------------------------ window
+
+__device__ __forceinline__ uint64_t d_lo_of(const DecParams& prm) {
+  if (!prm.D_tail) return prm.D_lo;
+  const uint64_t te = readfirst64(*prm.t_end);
+  return te > 256u ? te - 256u : 0u;
+}
+
+// XCodecWindow::dereference(c) (xcodec/xcodec_window.h:102-111) after T
+// declares of this batch: false if the slot is empty, else the slot's hash
+// and bytes.  Wave-uniform.  `gd` receives the global declare index.
+__device__ bool window_slot(const DecParams& prm, uint64_t T, uint32_t c, uint64_t& h, const uint8_t*& src,
+                            uint64_t& gd) {
+  const uint64_t W = prm.win_count, G = W + T, DL = d_lo_of(prm);
+  if (G == 0) return false;
+  const uint64_t r = (G - 1u - c) & 255u;
+  if (r > G - 1u) return false;                              // slot never written
+  const uint64_t g = G - 1u - r;                              // latest declare with g = c (mod 256)
+  gd = g;
+  if (g < W) {                                               // made before this batch: the window holds it
+    h = readfirst64(prm.win_hash[c]);
+    if (h == 0) return false;                                // emptied by a re-declare (:79-83)
+    src = prm.win_seg + (uint64_t)c * SEG;
+  } else {
+    const uint4 rec = prm.D[g - W - DL];
+    h = ((uint64_t)readfirst(rec.y) << 32) | readfirst(rec.x);
+    src = (const uint8_t*)(((uint64_t)readfirst(rec.w) << 32) | readfirst(rec.z));
+  }
+  // declared again after g (batch declares only; the window state covers the rest)?
+  const uint64_t a = (g + 1u > W ? g + 1u - W : 0u), b = T;
+  bool dup = false;
+  for (uint64_t t = a + lane_id(); t < b; t += 64) {
+    const uint4 e = prm.D[t - DL];
+    dup |= e.x == (uint32_t)h && e.y == (uint32_t)(h >> 32);
+  }
+  return ballot(dup) == 0;
+}
+
+// REF source: the earliest EXTRACT of h in the batch before `here`, else the
+// persistent cache (the cache state at that point of the stream).
+__device__ __forceinline__ const uint8_t* ref_source(const DecParams& prm, uint32_t lo, uint32_t hi, uint64_t here) {
+  const uint64_t e = tab_lookup(prm.x, lo, hi);
+  if (e != ~0ull && e < here) return prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
+  const uint64_t gv = tab_lookup(prm.g, lo, hi);
+  if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+  return nullptr;
+}
+
 // ------------------------------------------------------------------ kernels
 
 template <bool EMIT>
@@ -201,15 +270,18 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
   uint64_t olen = 0;
   int32_t st = 0;
   uint32_t i = 0;
-  const uint64_t blockp = EMIT ? readfirst64(*prm.block_pos) : ~0ull;
-  if (EMIT && spos(chunk, 0) > blockp) {      // after the blocking REF: decode() never got here
+  uint64_t ndecl = 0, nbref = 0;
+  const uint64_t blockp = EMIT ? min(readfirst64(*prm.block_pos), readfirst64(*prm.berr_pos)) : ~0ull;
+  if (EMIT && spos(chunk, 0) > blockp) {      // after the stop point: decode() never got here
     if (l == 0) {
       prm.out_len[chunk] = 0;
       prm.chunk_status[chunk] = 2;
       prm.consumed[chunk] = 0;
+      prm.n_decl_emit[chunk] = 0;
     }
     return;
   }
+  const uint64_t dbase = EMIT ? prm.decl_base[chunk] : 0;
 
   while (i < len) {
     uint32_t nesc = 0;
@@ -238,6 +310,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
       }
       olen += SEG;
       i += 2 + SEG;
+      ++ndecl;                                               // window_.declare, :137
     } else if (op == OP_REF) {                               // :141-163
       if (len - i < 10u) { st = 3; break; }
       const uint64_t h = be64(x + i + 2);
@@ -245,13 +318,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
       if (EMIT) {
         const uint64_t here = spos(chunk, i);
         if (here >= blockp) { st = 1; break; }               // blocked at or before this op
-        const uint8_t* src = nullptr;
-        const uint64_t e = tab_lookup(prm.x, lo, hi);        // earliest EXTRACT of h in the batch
-        if (e != ~0ull && e < here) src = prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
-        if (src == nullptr) {
-          const uint64_t gv = tab_lookup(prm.g, lo, hi);
-          if (gv != ~0ull) src = prm.pool + gv * (uint64_t)SEG;
-        }
+        const uint8_t* src = ref_source(prm, lo, hi, here);
         if (src == nullptr) { st = 1; break; }               // cannot happen: scan found all
         wave_copy2048(out + olen, src);
       } else {
@@ -261,10 +328,19 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
       }
       olen += SEG;
       i += 10;
-    } else if (op == OP_BACKREF) {
-      if (l == 0) atomicOr(prm.status, 1 << 8);
-      st = -2;
-      break;
+      ++ndecl;                                               // window_.declare, :160
+    } else if (op == OP_BACKREF) {                           // :165-181
+      if (len - i < 3u) { st = 3; break; }
+      if (EMIT) {
+        if (spos(chunk, i) >= blockp) { st = -1; i += 3; break; }   // empty slot: moveout precedes the check
+        uint64_t h = 0, gd = 0;
+        const uint8_t* src = nullptr;
+        if (!window_slot(prm, dbase + ndecl, x[i + 2], h, src, gd)) { st = -1; i += 3; break; }
+        wave_copy2048(out + olen, src);
+      }
+      ++nbref;
+      olen += SEG;
+      i += 3;
     } else {
       st = -1;                                               // :183-184 unsupported opcode
       break;
@@ -275,8 +351,123 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
     if (EMIT) {
       prm.chunk_status[chunk] = st;
       prm.consumed[chunk] = i;
+      prm.n_decl_emit[chunk] = ndecl;
+    } else {
+      prm.n_decl[chunk] = ndecl;
+      prm.n_bref[chunk] = nbref;
     }
   }
+}
+
+// Declare records for batch indices [lo_t, hi_t): full (every declare, when
+// the batch holds BACKREFs) or tail (the 256 before the stop point, for the
+// window update).  One wave per chunk.
+__global__ __launch_bounds__(256) void decl_record_kernel(DecParams prm, uint64_t total) {
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  const uint64_t hi_t = prm.D_tail ? readfirst64(*prm.t_end) : total, lo_t = d_lo_of(prm);
+  const uint64_t base = prm.decl_base[chunk], cnt = prm.n_decl[chunk];
+  if (base >= hi_t || base + cnt <= lo_t) return;
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const uint32_t len = prm.chunk_len[chunk];
+  uint64_t t = base;
+  uint32_t i = 0;
+  while (i < len && t < hi_t) {
+    uint32_t nesc = 0;
+    i = next_op(x, i, len, nesc);
+    if (i + 1 >= len) break;
+    const uint32_t op = x[i + 1];
+    if (op == OP_EXTRACT) {
+      if (len - i < 2u + SEG) break;
+      if (t >= lo_t) {
+        const uint2 h = dec_window_hash(x + i + 2);
+        const uint64_t src = (uint64_t)(x + i + 2);
+        if (lane_id() == 0) prm.D[t - lo_t] = make_uint4(readfirst(h.x), readfirst(h.y), (uint32_t)src, (uint32_t)(src >> 32));
+      }
+      ++t;
+      i += 2 + SEG;
+    } else if (op == OP_REF) {
+      if (len - i < 10u) break;
+      if (t >= lo_t) {
+        const uint64_t h = be64(x + i + 2);
+        const uint64_t src = (uint64_t)ref_source(prm, (uint32_t)h, (uint32_t)(h >> 32), spos(chunk, i));
+        if (lane_id() == 0) prm.D[t - lo_t] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)src, (uint32_t)(src >> 32));
+      }
+      ++t;
+      i += 10;
+    } else if (op == OP_BACKREF) {
+      if (len - i < 3u) break;
+      i += 3;
+    } else {
+      break;
+    }
+  }
+}
+
+// Invalid BACKREFs (empty window slot): the first one stops the stream.
+__global__ __launch_bounds__(256) void decode_brefcheck_kernel(DecParams prm) {
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n || prm.n_bref[chunk] == 0) return;
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const uint32_t len = prm.chunk_len[chunk];
+  uint64_t t = prm.decl_base[chunk];
+  uint32_t i = 0;
+  while (i < len) {
+    uint32_t nesc = 0;
+    i = next_op(x, i, len, nesc);
+    if (i + 1 >= len) break;
+    const uint32_t op = x[i + 1];
+    if (op == OP_EXTRACT) {
+      if (len - i < 2u + SEG) break;
+      ++t;
+      i += 2 + SEG;
+    } else if (op == OP_REF) {
+      if (len - i < 10u) break;
+      ++t;
+      i += 10;
+    } else if (op == OP_BACKREF) {
+      if (len - i < 3u) break;
+      uint64_t h = 0, gd = 0;
+      const uint8_t* src = nullptr;
+      if (!window_slot(prm, t, x[i + 2], h, src, gd)) {
+        if (lane_id() == 0) atomicMin((unsigned long long*)prm.berr_pos, (unsigned long long)spos(chunk, i));
+        break;
+      }
+      i += 3;
+    } else {
+      break;
+    }
+  }
+}
+
+// Declares before the stop point (the first unknown REF or invalid BACKREF).
+__global__ void decode_tend_kernel(DecParams prm, uint64_t total) {
+  const uint64_t stop = min(*prm.block_pos, *prm.berr_pos);
+  *prm.t_end = stop == ~0ull ? total : prm.decl_base[stop >> 32] + prm.n_decl_emit[stop >> 32];
+}
+
+// The window after the batch: slot c as window_slot() sees it at t_end, with
+// the bytes copied in (the window holds its own reference to them).  One wave
+// per slot; every source is batch input or pool, never another slot.
+__global__ __launch_bounds__(256) void window_update_kernel(DecParams prm) {
+  const uint32_t c = blockIdx.x * 4u + (uint32_t)readfirst(threadIdx.x >> 6);
+  if (c >= 256u) return;
+  const uint64_t T = readfirst64(*prm.t_end);
+  if (T == 0) return;
+  uint64_t h = 0, gd = 0;
+  const uint8_t* src = nullptr;
+  const bool ok = window_slot(prm, T, c, h, src, gd);
+  const uint64_t G = prm.win_count + T;
+  const bool written = ((G - 1u - c) & 255u) <= G - 1u;
+  if (!written) return;
+  if (!ok) {
+    if (lane_id() == 0) prm.win_hash[c] = 0;
+    return;
+  }
+  if (gd >= prm.win_count) wave_copy2048(prm.win_seg + (uint64_t)c * SEG, src);
+  if (lane_id() == 0) prm.win_hash[c] = h;
 }
 
 // Between scan and emit: find unresolvable REFs (no earlier EXTRACT of the
@@ -314,6 +505,9 @@ __global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
         }
       }
       i += 10;
+    } else if (op == OP_BACKREF) {
+      if (len - i < 3u) break;
+      i += 3;
     } else {
       break;
     }
@@ -356,7 +550,7 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
   const uint64_t key = readfirst64(prm.x.keys[w]);
   if (key == EMPTY_KEY) return;
   const uint64_t first = readfirst64(prm.x.vals[w]), last = readfirst64(prm.x_latest[w]);
-  const uint64_t blockp = readfirst64(*prm.block_pos);
+  const uint64_t blockp = min(readfirst64(*prm.block_pos), readfirst64(*prm.berr_pos));
   if (first >= blockp) return;                 // never reached
   if (last >= blockp && last != first) {       // several EXTRACTs straddle the block: not modelled
     if (lane_id() == 0) atomicOr(prm.status, 1 << 9);
@@ -509,12 +703,19 @@ struct XcgDecodeArgs {
   uint64_t* unknown_pos;
   uint32_t* nunknown;
   uint32_t unknown_cap;
-  uint64_t* scratch;     // [0] total, [1] block_pos
-  uint64_t* h_scratch;   // pinned: [0] total, [1] block_pos, [2] nunknown
+  uint64_t* scratch;     // [0] total out, [1] REF block, [2] BACKREF error, [3] declares, [4] BACKREFs, [5] t_end
+  uint64_t* h_scratch;   // pinned copy of scratch[0..5], [6] nunknown
+  uint64_t* chunk_tmp;   // 4 * n u64: n_decl, n_bref, decl_base, n_decl_emit
+  uint4* d_tail;         // 256 declare records
+  uint64_t* win_hash;    // the decoder's BACKREF window
+  uint8_t* win_seg;
+  uint64_t win_count;
 };
 
+// Returns 0, -75 (output too small) or -5.  Outputs: total decoded bytes, the
+// REF block and BACKREF error positions (~0 = none), unknown-REF count.
 extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, uint64_t* block_pos_out,
-                                 uint32_t* nunknown_out, hipStream_t stream) {
+                                 uint64_t* berr_pos_out, uint32_t* nunknown_out, hipStream_t stream) {
   using namespace xcg;
   const uint32_t n = a->n;
   DecParams p{};
@@ -536,29 +737,71 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   p.nunknown = a->nunknown;
   p.unknown_cap = a->unknown_cap;
   p.block_pos = a->scratch + 1;
+  p.berr_pos = a->scratch + 2;
+  p.t_end = a->scratch + 5;
   p.status = a->status;
+  p.n_decl = a->chunk_tmp;
+  p.n_bref = a->chunk_tmp + n;
+  p.decl_base = a->chunk_tmp + 2ull * n;
+  p.n_decl_emit = a->chunk_tmp + 3ull * n;
+  p.win_hash = a->win_hash;
+  p.win_seg = a->win_seg;
+  p.win_count = a->win_count;
   const dim3 grid((n + 3) / 4), block(256);
   if (hipMemsetAsync(a->x_keys, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->x_vals, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->x_latest, 0, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
-      hipMemsetAsync(a->scratch + 1, 0xFF, 8, stream) != hipSuccess ||
+      hipMemsetAsync(a->scratch + 1, 0xFF, 16, stream) != hipSuccess ||
       hipMemsetAsync(a->nunknown, 0, 4, stream) != hipSuccess)
     return -5;
+  // scan, then number the declares
   hipLaunchKernelGGL(decode_kernel<false>, grid, block, 0, stream, p);
-  hipLaunchKernelGGL(decode_refcheck_kernel, grid, block, 0, stream, p);
-  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)a->out_len, a->out_off,
-                     n, a->scratch);
-  if (hipMemcpyAsync(a->h_scratch, a->scratch, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipMemcpyAsync(a->h_scratch + 2, a->nunknown, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)p.n_decl,
+                     (uint64_t*)p.decl_base, n, a->scratch + 3);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)p.n_bref,
+                     p.n_decl_emit, n, a->scratch + 4);          // (n_decl_emit: scratch output here)
+  if (hipMemcpyAsync(a->h_scratch + 3, a->scratch + 3, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return -5;
+  const uint64_t ndecl = a->h_scratch[3], nbref = a->h_scratch[4];
+  uint4* dfull = nullptr;
+  if (nbref > 0 && ndecl > 0) {
+    // BACKREFs present: records of every declare (rare; never made by XCodecEncoder)
+    if (hipMallocAsync((void**)&dfull, 16ull * ndecl, stream) != hipSuccess) return -5;
+    p.D = dfull;
+    p.D_lo = 0;
+    p.D_tail = false;
+    hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
+  }
+  hipLaunchKernelGGL(decode_refcheck_kernel, grid, block, 0, stream, p);
+  if (nbref > 0) hipLaunchKernelGGL(decode_brefcheck_kernel, grid, block, 0, stream, p);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)a->out_len, a->out_off,
+                     n, a->scratch);
+  if (hipMemcpyAsync(a->h_scratch, a->scratch, 24, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipMemcpyAsync(a->h_scratch + 6, a->nunknown, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess) {
+    if (dfull) (void)hipFreeAsync(dfull, stream);
+    return -5;
+  }
   *total_out = a->h_scratch[0];
   *block_pos_out = a->h_scratch[1];
-  *nunknown_out = (uint32_t)a->h_scratch[2];
-  if (*total_out > a->out_cap) return -75;
+  *berr_pos_out = a->h_scratch[2];
+  *nunknown_out = (uint32_t)(a->h_scratch[6] & 0xFFFFFFFFu);
+  if (*total_out > a->out_cap) {
+    if (dfull) (void)hipFreeAsync(dfull, stream);
+    return -75;
+  }
   hipLaunchKernelGGL(decode_kernel<true>, grid, block, 0, stream, p);
+  hipLaunchKernelGGL(decode_tend_kernel, dim3(1), dim3(1), 0, stream, p, ndecl);
+  if (!dfull) {
+    p.D = a->d_tail;
+    p.D_tail = true;
+    hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
+  }
+  hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
   const uint64_t slots = (uint64_t)a->x_mask + 1;
   hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots * 64 + 255) / 256)), dim3(256), 0, stream, p,
                      a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask);
+  if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

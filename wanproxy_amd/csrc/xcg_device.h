@@ -53,18 +53,17 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
 }
 
 // Inclusive wave64 prefix sum (u32, wrapping).  Rows of 16 by DPP row_shr,
-// then the three row carries by readlane.
+// then the row carries by DPP row_bcast:15 (rows 1, 3 += lane 15 of the row
+// before) and row_bcast:31 (rows 2, 3 += lane 31); disabled rows add 0.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   int x = (int)v;
   x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
   x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
   x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
-  uint32_t r0 = readlane((uint32_t)x, 15), r1 = readlane((uint32_t)x, 31),
-           r2 = readlane((uint32_t)x, 47);
-  int row = lane_id() >> 4;
-  uint32_t add = row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r0 + r1 : r0 + r1 + r2;
-  return (uint32_t)x + add;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)x;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return readlane(wave_incl_scan(v), 63); }

@@ -304,11 +304,11 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     vis_lo = from_lane(A);
   }
   uint32_t ev = 0;
-  // Groups of 4 positions: the sched_barrier keeps hipcc from hoisting all 32
-  // LDS probes (and their operands) at once.
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    uint32_t kv[4];
+  // Groups of 4 positions, software-pipelined: group g+1's keys are rolled and
+  // its 4 LDS probes issued before group g's probes are compared, so each
+  // group's LDS latency overlaps the next group's arithmetic.  The
+  // sched_barrier keeps hipcc from hoisting more than that (VGPRs).
+  auto roll4 = [&](int g, uint32_t (&kv)[4], uint2 (&e)[4]) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
@@ -320,9 +320,17 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
         NX2 += NX1 + (xo << 11);
       }
     }
-    uint2 e[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(kblk + ((kv[t] & KM) | kofs));
+  };
+  uint32_t kc[4];
+  uint2 ec[4];
+  roll4(0, kc, ec);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    uint32_t kn[4];
+    uint2 en[4];
+    if (g < 7) roll4(g + 1, kn, en);
     // Persistent cache + batch declarations: LDS bitmap first, then (rarely)
     // one 16-byte fingerprint-bucket load; all four loads issued before use.
     uint64_t gh[4] = {0, 0, 0, 0};
@@ -330,36 +338,54 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
       u32x4 q[4];
       bool pass[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) pass[t] = (lfilt[filt_bit(kv[t]) >> 5] >> (kv[t] & 31u)) & 1u;
+      for (int t = 0; t < 4; ++t) pass[t] = (lfilt[filt_bit(kc[t]) >> 5] >> (kc[t] & 31u)) & 1u;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         q[t] = u32x4{0u, 0u, 0u, 0u};
-        if (pass[t]) q[t] = ftab[fbucket(kv[t], fmask)];
+        if (pass[t]) q[t] = ftab[fbucket(kc[t], fmask)];
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const uint32_t fp = kv[t] | 1u;
+        const uint32_t fp = kc[t] | 1u;
         gh[t] = lanes_eq(q[t][0], fp) | lanes_eq(q[t][1], fp) | lanes_eq(q[t][2], fp) | lanes_eq(q[t][3], FOVF);
       }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
-      uint64_t hit = lanes_eq(e[t].x, kv[t]) | lanes_eq(e[t].y, kv[t]) | gh[t];
-      if (C0) hit |= lanes_eq(kv[t], c0k) & (j < vB ? vis_hi : vis_lo);
+      uint64_t hit = lanes_eq(ec[t].x, kc[t]) | lanes_eq(ec[t].y, kc[t]) | gh[t];
+      if (C0) hit |= lanes_eq(kc[t], c0k) & (j < vB ? vis_hi : vis_lo);
       if (OVF) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) hit |= lanes_eq(o[k], kv[t]);
+        for (int k = 0; k < 8; ++k) hit |= lanes_eq(o[k], kc[t]);
       }
       ev = shift_in(ev, hit);
     }
     asm volatile("" : "+v"(ev));   // materialise this group's bits before the next group
     __builtin_amdgcn_sched_barrier(0);
+    if (g < 7) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { kc[t] = kn[t]; ec[t] = en[t]; }
+    }
   }
   return __builtin_bitreverse32(ev);   // position j was shifted in at bit 31 - j
 }
 
 // ------------------------------------------------------------------ kernel
+
+// Waves sharing a SIMD issue by priority, then age: with equal priorities the
+// oldest of the four chunk-waves runs ahead and the youngest finishes alone,
+// leaving its SIMD under-used.  A wave's priority falls as it parses its
+// chunk (bands 1/2, 3/4, 15/16: a wave that reaches a band boundary first
+// yields until the others catch up), so the four finish nearly together;
+// only the last 1/16 is age-ordered.
+__device__ __forceinline__ void progress_priority(int s, int L) {
+  const int q = (16 * s) / L;                      // sixteenths of the chunk parsed, uniform
+  if (q < 8) __builtin_amdgcn_s_setprio(3);
+  else if (q < 12) __builtin_amdgcn_s_setprio(2);
+  else if (q < 15) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
 
 // One wave encodes chunk `chunk` (one XCodecEncoder::encode call).  Its key
 // table is kblk + kofs (LDS), its records T.  STREAM: the cache also holds the
@@ -488,6 +514,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     const int q0 = p + 32 * l;
     const bool contig = (p == p_prev + SEG);
     ++n_pieces;
+    if (!STREAM) progress_priority(s, L);
     // vmcnt counts loads and stores together, in order (gfx9): every wait on
     // a load also waits for all older stores.  So fresh loads are waited for
     // here, inside their branch, and the prefetch below is waited for after

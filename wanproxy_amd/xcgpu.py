@@ -27,6 +27,7 @@ XCG_FLAG_OOB = 0x1
 XCG_FLAG_NULLCACHE = 0x2
 XCG_SEM_INDEPENDENT = 0
 XCG_SEM_STREAM = 1
+XCG_EOVERFLOW = -75
 
 _lib = None
 
@@ -70,6 +71,12 @@ def lib():
     L.xcg_decode_batch.argtypes = [vp, u8p, u64p, u32p, C.c_uint32, C.c_uint32, u8p, C.c_uint64, u64p, u64p, vp, u64p,
                                    u64p, C.c_uint32, vp, u64p, vp]
     L.xcg_decode_batch.restype = C.c_int
+    L.xcg_window_create.argtypes = [vp, C.POINTER(C.c_void_p)]
+    L.xcg_window_create.restype = C.c_int
+    L.xcg_window_destroy.argtypes = [vp]
+    L.xcg_window_destroy.restype = None
+    L.xcg_decode_set_window.argtypes = [vp, vp]
+    L.xcg_decode_set_window.restype = C.c_int
     L.xcg_pack_outputs.argtypes = [vp, u8p, u64p, u64p, C.c_uint32, u8p, u64p, u64p, vp]
     L.xcg_pack_outputs.restype = C.c_int
     L.xcg_window_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
@@ -175,8 +182,9 @@ class Context:
             return res, d_st.cpu().numpy().view(np.uint32).reshape(n, 4)
         return res
 
-    def decode_chunks(self, encs):
-        """Decode encoded chunks (one stream, this context's cache) on the GPU.
+    def decode_chunks(self, encs, window: 'Window' = None):
+        """Decode encoded chunks (one stream, this context's cache) on the GPU,
+        with `window` as the decoder's BACKREF window (default: the context's).
         Returns (outs, status, consumed, unknown) -- see xcg_decode_batch."""
         import torch
         dev = torch.device('cuda', self.device)
@@ -194,15 +202,26 @@ class Context:
         d_st = torch.zeros(n, dtype=torch.int32, device=dev)
         d_cons = torch.zeros(n, dtype=torch.int64, device=dev)
         cap = int(lens.astype(np.uint64).sum()) * 205 + 4096   # a 10-byte REF expands to 2048
-        d_out = torch.zeros(cap, dtype=torch.uint8, device=dev)
         unk = np.zeros(1 << 16, dtype=np.uint64)
         nunk = np.zeros(1, dtype=np.uint32)
         total = np.zeros(1, dtype=np.uint64)
-        _check(lib().xcg_decode_batch(
-            self.h, C.c_void_p(d_in.data_ptr()), C.c_void_p(d_off.data_ptr()), C.c_void_p(d_len.data_ptr()), n,
-            int(lens.max()) if n else 0, C.c_void_p(d_out.data_ptr()), cap, C.c_void_p(d_oo.data_ptr()),
-            C.c_void_p(d_ol.data_ptr()), C.c_void_p(d_st.data_ptr()), C.c_void_p(d_cons.data_ptr()),
-            unk.ctypes.data, unk.size, nunk.ctypes.data, total.ctypes.data, _stream_ptr(None)))
+        if window is not None:
+            _check(lib().xcg_decode_set_window(self.h, window.h))
+        try:
+            for _ in range(2):
+                d_out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+                rc = lib().xcg_decode_batch(
+                    self.h, C.c_void_p(d_in.data_ptr()), C.c_void_p(d_off.data_ptr()), C.c_void_p(d_len.data_ptr()),
+                    n, int(lens.max()) if n else 0, C.c_void_p(d_out.data_ptr()), cap, C.c_void_p(d_oo.data_ptr()),
+                    C.c_void_p(d_ol.data_ptr()), C.c_void_p(d_st.data_ptr()), C.c_void_p(d_cons.data_ptr()),
+                    unk.ctypes.data, unk.size, nunk.ctypes.data, total.ctypes.data, _stream_ptr(None))
+                if rc != XCG_EOVERFLOW:
+                    break
+                cap = int(total[0])            # BACKREF-dense: 3 bytes -> 2048; nothing was committed
+            _check(rc)
+        finally:
+            if window is not None:
+                lib().xcg_decode_set_window(self.h, None)
         torch.cuda.synchronize(dev)
         oo = d_oo.cpu().numpy()
         ol = d_ol.cpu().numpy()
@@ -241,6 +260,27 @@ class Context:
         return d_h.cpu().numpy().tobytes()
 
 
+class Window:
+    """A decoder's BACKREF window (XCodecWindow, xcodec/xcodec_window.h)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(lib().xcg_window_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().xcg_window_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class XCodecEncoder:
     """Mirror of XCodecEncoder(XCodecCache*) (xcodec/xcodec_encoder.h:40-43):
     successive encode() calls share the context's cache, exactly like tack's
@@ -263,9 +303,10 @@ class XCodecDecoder:
 
     def __init__(self, ctx: Context):
         self.ctx = ctx
+        self.window = Window(ctx)      # XCodecDecoder::window_, one per decoder
 
     def decode(self, data: bytes):
         if not data:
             return True, b'', 0, []
-        outs, st, cons, unk = self.ctx.decode_chunks([data])
+        outs, st, cons, unk = self.ctx.decode_chunks([data], window=self.window)
         return int(st[0]) >= 0, outs[0], int(cons[0]), unk
