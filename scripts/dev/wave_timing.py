@@ -23,7 +23,12 @@ CH = 65536
 dev = torch.device('cuda', 0)
 data = np.frombuffer(synth.stream(0xC2, N * CH, 50, 0), dtype=np.uint8)
 d_in = torch.from_numpy(data.copy()).to(dev)
+# REVERSE=1: wave w parses data chunk N-1-w (separates data/address effects
+# from dispatch-order effects)
+REV = os.environ.get('REVERSE') == '1'
 d_off = torch.arange(N, dtype=torch.int64, device=dev) * CH
+if REV:
+    d_off = d_off.flip(0).contiguous()
 d_len = torch.full((N,), CH, dtype=torch.int32, device=dev)
 bound = 2 * CH + 16
 d_oo = torch.arange(N, dtype=torch.int64, device=dev) * bound
@@ -71,4 +76,4 @@ print('latest-ending waves: chunk start dur xcc se cu simd')
 for i in o:
     print(f'  {i:5d} {start[i]:7.1f} {dur[i]:7.1f} {xcc[i]} {se[i]} {cu[i]} {simd[i]}')
 os.makedirs('gpurun_out', exist_ok=True)
-np.savez('gpurun_out/wave_timing.npz', start=start, end=end, hw=hw, xcc=xcc)
+np.savez('gpurun_out/wave_timing%s.npz' % ('_rev' if REV else ''), start=start, end=end, hw=hw, xcc=xcc)

@@ -41,10 +41,8 @@ namespace xcg {
 template <int LOGNB, int MAXD>
 struct WaveRecs {
   static constexpr int NB = 1 << LOGNB;
-  uint16_t idx[2 * NB];       // declaration index of the key slot
   uint32_t rlo[MAXD], rhi[MAXD], rc[MAXD];  // exact hash + chunk position
   uint32_t ovf_k[8];          // keys whose bucket was full
-  uint32_t ovf_idx[8];
 };
 
 template <int LOGNB>
@@ -280,7 +278,7 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
 // instruction.  C0: the pending candidate (key c0k) is not in the table yet and
 // becomes visible at piece offset rvis (position p + rvis).  OVF: also compare the (rare) overflow
 // keys ovk[8].  GLB: also probe the persistent cache / batch filter.
-template <int LOGNB, bool C0, bool OVF, bool GLB>
+template <int LOGNB, bool C0, int NOVF, bool GLB>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
                                                uint32_t kofs, uint32_t c0k, int rvis, const uint32_t* ovk,
                                                const uint32_t* lfilt, const u32x4* ftab, uint32_t fmask) {
@@ -291,7 +289,7 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
   const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
   uint32_t o[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = OVF ? ovk[k] : 0u;
+  for (int k = 0; k < 8; ++k) o[k] = k < NOVF ? ovk[k] : 0u;
   // C0 visibility: lanes l with 32 l + j >= rvis.  With rvis = 32 A + B that is
   // l >= A + 1 for j < B and l >= A for j >= B -- two masks per piece.
   uint64_t vis_hi = 0, vis_lo = 0;
@@ -355,10 +353,8 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
       const int j = 4 * g + t;
       uint64_t hit = lanes_eq(ec[t].x, kc[t]) | lanes_eq(ec[t].y, kc[t]) | gh[t];
       if (C0) hit |= lanes_eq(kc[t], c0k) & (j < vB ? vis_hi : vis_lo);
-      if (OVF) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) hit |= lanes_eq(o[k], kc[t]);
-      }
+      for (int k = 0; k < NOVF; ++k) hit |= lanes_eq(o[k], kc[t]);
       ev = shift_in(ev, hit);
     }
     asm volatile("" : "+v"(ev));   // materialise this group's bits before the next group
@@ -456,9 +452,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     const uint32_t s0 = readfirst(keyt[2 * b]), s1 = readfirst(keyt[2 * b + 1]);
     if (l == 0) {
       T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
-      if (s0 == ke) { keyt[2 * b] = k; T.idx[2 * b] = (uint16_t)d; }
-      else if (s1 == ke) { keyt[2 * b + 1] = k; T.idx[2 * b + 1] = (uint16_t)d; }
-      else if (novf < 8) { T.ovf_k[novf] = k; T.ovf_idx[novf] = d; }
+      if (s0 == ke) keyt[2 * b] = k;
+      else if (s1 == ke) keyt[2 * b + 1] = k;
+      else if (novf < 8) T.ovf_k[novf] = k;
     }
     if (s0 != ke && s1 != ke) {
       if (novf < 8) ++novf;
@@ -476,15 +472,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     else if (rh == hi) found = (int)d;
   };
   auto lookup = [&](uint32_t lo, uint32_t hi) -> int {
-    const uint32_t key = probe_key(lo);
-    const uint32_t b = kbucket<LOGNB>(key);
+    // records whose lo matches, by a wave ballot (at most MAXD of them)
     int found = -1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (found == -1 && readfirst(keyt[2 * b + k]) == key) rec_matches(readfirst(T.idx[2 * b + k]), lo, hi, found);
-    }
-    for (uint32_t k = 0; k < novf && found == -1; ++k) {
-      if (readfirst(T.ovf_k[k]) == key) rec_matches(readfirst(T.ovf_idx[k]), lo, hi, found);
+    for (uint32_t base = 0; base < ndecl && found == -1; base += 64) {
+      const uint32_t d = base + (uint32_t)l;
+      uint64_t m = ballot(d < ndecl && T.rlo[d] == lo);
+      while (m && found == -1) {
+        rec_matches(base + (uint32_t)__builtin_ctzll(m), lo, hi, found);
+        m &= m - 1;
+      }
     }
     return found;
   };
@@ -578,20 +574,27 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const uint32_t* lf = lfilt;
       const u32x4* ft = prm.lf.ftab;
       const uint32_t fm = prm.lf.fmask;
+      // Bucket overflows are rare (three of a chunk's keys in one 2-slot
+      // bucket); one overflow key costs one compare, more cost eight.
+      uint32_t ovk[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
       if (novf == 0) {
         if (c0)
-          ev = roll_probe<LOGNB, true, false, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, nullptr, lf, ft, fm);
+          ev = roll_probe<LOGNB, true, 0, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
         else
-          ev = roll_probe<LOGNB, false, false, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, nullptr, lf, ft, fm);
+          ev = roll_probe<LOGNB, false, 0, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+      } else if (novf == 1) {
+        if (c0)
+          ev = roll_probe<LOGNB, true, 1, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+        else
+          ev = roll_probe<LOGNB, false, 1, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
       } else {
         // duplicates of a real overflow key pad the unused slots
-        uint32_t ovk[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ovk[k] = readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]);
         if (c0)
-          ev = roll_probe<LOGNB, true, true, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+          ev = roll_probe<LOGNB, true, 8, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
         else
-          ev = roll_probe<LOGNB, false, true, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+          ev = roll_probe<LOGNB, false, 8, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
       }
       // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
@@ -770,9 +773,9 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
     encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, S.lfilt);
 }
 
-template __global__ void encode_independent_kernel<9, 72>(EncParams);
+template __global__ void encode_independent_kernel<10, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
-template __global__ void encode_stream_kernel<8, 72, 12>(EncParams);
+template __global__ void encode_stream_kernel<9, 72, 12>(EncParams);
 template __global__ void encode_stream_kernel<11, 264, 2>(EncParams);
 
 }  // namespace xcg
@@ -786,7 +789,7 @@ extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t
   xcg::EncParams prm{d_in, d_chunk_off, d_chunk_len, n, flags, d_out, d_out_off, d_out_len, d_stats, d_status};
   dim3 grid((n + 3) / 4), block(256);
   if (max_chunk_len <= (1u << 17)) {
-    hipLaunchKernelGGL((xcg::encode_independent_kernel<9, 72>), grid, block, 0, stream, prm);
+    hipLaunchKernelGGL((xcg::encode_independent_kernel<10, 72>), grid, block, 0, stream, prm);
   } else if (max_chunk_len <= (1u << 19)) {
     hipLaunchKernelGGL((xcg::encode_independent_kernel<11, 264>), grid, block, 0, stream, prm);
   } else {
@@ -902,7 +905,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const dim3 sgrid(min(wgs * (big ? 2u : 1u), (n + SW - 1) / SW)), sblock(64 * SW);
   auto launch = [&]() {
     if (big) hipLaunchKernelGGL((encode_stream_kernel<11, 264, 2>), sgrid, sblock, 0, stream, prm);
-    else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 12>), sgrid, sblock, 0, stream, prm);
+    else hipLaunchKernelGGL((encode_stream_kernel<9, 72, 12>), sgrid, sblock, 0, stream, prm);
   };
   if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess) return -5;
   // Round 0: every chunk against the persistent cache + its own declarations.
