@@ -50,6 +50,7 @@ struct XcgStreamArgs {
   uint32_t maxd;
   uint32_t* changed;
   uint32_t* h_changed;
+  int g_empty;
 };
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
@@ -165,6 +166,7 @@ struct xcg_ctx {
   DecodeScratch ds;
   xcg_window* own_win = nullptr;   // default window (lazily allocated)
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
+  bool g_empty = true;             // nothing entered since the cache was (re)created or cleared
 };
 
 namespace {
@@ -379,7 +381,9 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
   if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
-  return clear_cache(c->g);
+  const int rc = clear_cache(c->g);
+  if (rc == XCG_OK) c->g_empty = true;
+  return rc;
 }
 
 int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
@@ -397,6 +401,7 @@ int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
     return XCG_ENOMEM;
   }
   rc = XCG_OK;
+  if (mode != 0) c->g_empty = false;
   if (mode == 0) {   // lookup
     if (xcg_launch_cache_lookup(c->g.keys, c->g.vals, c->g.mask, c->g.pool, hash, d_seg, d_res, nullptr) != 0 ||
         hipMemcpy(res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -493,9 +498,11 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
     XcgStreamArgs a{d_in, d_chunk_off, d_chunk_len, n, c->flags, d_out, d_out_off, d_out_len, d_stats,
                     c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                     c->g.filt, c->g.ftab, c->g.fmask, c->bs.b_keys, c->bs.b_vals, c->bs.b_mask,
-                    c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed};
+                    c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
+                    c->g_empty ? 1 : 0};
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
+    c->g_empty = false;
     c->last_rounds = rounds;
     return rc == 0 ? XCG_OK : XCG_EHIP;
   }
@@ -595,6 +602,7 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
                   c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count};
   uint64_t total = 0, blockp = 0, berr = 0;
   uint32_t nunk = 0;
+  c->g_empty = false;
   const int lrc = xcg_launch_decode(&a, &total, &blockp, &berr, &nunk, (hipStream_t)stream);
   if (h_total_out) *h_total_out = total;
   if (lrc == -75) return XCG_EOVERFLOW;

@@ -541,49 +541,65 @@ __global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint64_t* le
 
 // Commit: every batch EXTRACT hash whose latest occurrence precedes the
 // blocking point enters the cache (enter, or replace on name reuse).
-// One wave per batch-table slot group.
+// A block takes 256 batch-table slots: one thread per slot decides (enter /
+// replace / skip), new segments are numbered by a block count (one global
+// atomic per block), then the block's waves copy the segments.
 __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8_t* pool, uint32_t* nseg,
                                                             uint32_t seg_cap, uint32_t* filt, uint32_t* ftab,
                                                             uint32_t fmask) {
-  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (w > prm.x.mask) return;
-  const uint64_t key = readfirst64(prm.x.keys[w]);
-  if (key == EMPTY_KEY) return;
-  const uint64_t first = readfirst64(prm.x.vals[w]), last = readfirst64(prm.x_latest[w]);
-  const uint64_t blockp = min(readfirst64(*prm.block_pos), readfirst64(*prm.berr_pos));
-  if (first >= blockp) return;                 // never reached
-  if (last >= blockp && last != first) {       // several EXTRACTs straddle the block: not modelled
-    if (lane_id() == 0) atomicOr(prm.status, 1 << 9);
-    return;
-  }
-  const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
-  const uint8_t* src = prm.in + prm.chunk_off[last >> 32] + (uint32_t)last;
-  if (last != first) {
-    // name reuse inside the batch with different bytes would need per-REF
-    // resolution of the latest EXTRACT; the emit pass used the earliest.
-    const uint8_t* s0 = prm.in + prm.chunk_off[first >> 32] + (uint32_t)first;
-    if (!readfirst((uint32_t)dec_equal2048(s0, src))) {
-      if (lane_id() == 0) atomicOr(prm.status, 1 << 9);
+  __shared__ uint32_t s_cnt, s_base, s_njob;
+  __shared__ uint4 s_job[256];   // (slot, destination segment, kind, -)
+  const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint64_t blockp = min(*prm.block_pos, *prm.berr_pos);
+  int kind = 0;                  // 0 none, 1 enter, 2 replace
+  uint64_t gv = ~0ull;
+  uint64_t key = EMPTY_KEY;
+  if (w <= prm.x.mask) {
+    key = prm.x.keys[w];
+    if (key != EMPTY_KEY) {
+      const uint64_t first = prm.x.vals[w], last = prm.x_latest[w];
+      if (first < blockp) {                      // else never reached
+        if (last >= blockp && last != first) {   // several EXTRACTs straddle the block: not modelled
+          atomicOr(prm.status, 1 << 9);
+        } else {
+          gv = tab_lookup_t(prm.g, (uint32_t)key, (uint32_t)(key >> 32));
+          kind = gv != ~0ull ? 2 : 1;
+        }
+      }
     }
   }
-  const uint64_t gv = tab_lookup(prm.g, lo, hi);
-  if (gv != ~0ull) {
-    uint8_t* dst = pool + gv * (uint64_t)SEG;
-    if (!readfirst((uint32_t)dec_equal2048(dst, src))) wave_copy2048(dst, src);   // replace (:130)
-    return;
+  const uint32_t seg = block_alloc_segs(kind == 1, nseg, &s_cnt, &s_base);
+  if (threadIdx.x == 0) s_njob = 0;
+  __syncthreads();
+  if (kind == 1 && seg >= seg_cap) {
+    atomicOr(prm.status, 4);
+    kind = 0;
   }
-  uint32_t seg = 0;
-  if (lane_id() == 0) seg = atomicAdd(nseg, 1u);
-  seg = readfirst(seg);
-  if (seg >= seg_cap) {
-    if (lane_id() == 0) atomicOr(prm.status, 4);
-    return;
-  }
-  wave_copy2048(pool + (uint64_t)seg * SEG, src);
-  if (lane_id() == 0) {
+  if (kind == 1) {
+    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
     if (!tab_insert_min(prm.g, lo, hi, seg)) atomicOr(prm.status, 2);
     filt_insert(filt, lo, hi);
     ftab_insert(ftab, fmask, lo, hi);
+  }
+  if (kind) {
+    const uint32_t j = atomicAdd(&s_njob, 1u);
+    s_job[j] = make_uint4((uint32_t)w, kind == 1 ? seg : (uint32_t)gv, (uint32_t)kind, 0u);
+  }
+  __syncthreads();
+  const uint32_t njob = s_njob;
+  for (uint32_t j = readfirst(threadIdx.x >> 6); j < njob; j += 4) {
+    const uint4 jb = s_job[j];
+    const uint32_t slot = readfirst(jb.x), dseg = readfirst(jb.y), jkind = readfirst(jb.z);
+    const uint64_t first = readfirst64(prm.x.vals[slot]), last = readfirst64(prm.x_latest[slot]);
+    const uint8_t* src = prm.in + prm.chunk_off[last >> 32] + (uint32_t)last;
+    if (last != first) {
+      // name reuse inside the batch with different bytes would need per-REF
+      // resolution of the latest EXTRACT; the emit pass used the earliest.
+      const uint8_t* s0 = prm.in + prm.chunk_off[first >> 32] + (uint32_t)first;
+      if (!readfirst((uint32_t)dec_equal2048(s0, src)) && lane_id() == 0) atomicOr(prm.status, 1 << 9);
+    }
+    uint8_t* dst = pool + (uint64_t)dseg * SEG;
+    if (jkind == 1 || !readfirst((uint32_t)dec_equal2048(dst, src))) wave_copy2048(dst, src);   // enter / replace (:130)
   }
 }
 
@@ -632,7 +648,7 @@ __global__ __launch_bounds__(64) void cache_enter_kernel(HashTab g, uint8_t* poo
     return;
   }
   uint32_t s = 0;
-  if (lane_id() == 0) s = atomicAdd(nseg, 1u);
+  if (lane_id() == 0) s = atomicAdd(nseg, 1u);   // single-segment host call: one atomic
   s = readfirst(s);
   if (s >= seg_cap) {
     if (lane_id() == 0) *result = -2;
@@ -800,7 +816,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   }
   hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
   const uint64_t slots = (uint64_t)a->x_mask + 1;
-  hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots * 64 + 255) / 256)), dim3(256), 0, stream, p,
+  hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, p,
                      a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask);
   if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;

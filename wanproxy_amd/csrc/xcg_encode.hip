@@ -26,6 +26,10 @@
 // fingerprint table can be approximate without affecting output.  Output ops
 // (ESCAPE / EXTRACT / REF, xcodec_encoder.cc:276-372) are written by the whole
 // wave as they are resolved, into the chunk's output slot.
+#include <stddef.h>
+
+#include <type_traits>
+
 #include "xcg_cache.h"
 #include "../../include/xcgpu.h"
 
@@ -55,10 +59,12 @@ struct IndepLDS {
   uint32_t key[W][2 << LOGNB];
   WaveRecs<LOGNB, MAXD> rec[W];
 };
+constexpr int GSLOTS_DECL = 8;   // = GSLOTS (pass-1 queue depth per lane)
 template <int LOGNB, int MAXD, int W>
 struct StreamLDS {
-  uint32_t key[W][2 << LOGNB];
-  uint32_t lfilt[FILT_WORDS];
+  uint32_t key[W][2 << LOGNB];               // offset 0, as in IndepLDS
+  uint32_t lfilt[FILT_WORDS];                // the lane filter (64 KiB)
+  uint32_t scr[W][GSLOTS_DECL + 1][64];      // pass-1 queues (+ a garbage slot)
   WaveRecs<LOGNB, MAXD> rec[W];
 };
 
@@ -82,7 +88,9 @@ struct EncParams {
   uint4* decl;         // [n * maxd] (lo, hi, pos, 0) declarations of the chunk, this round
   uint32_t* ndecl;     // [n]
   uint32_t maxd;
-  uint32_t* changed;   // set when any chunk's declaration list differs from the last round
+  uint32_t* changed;   // lowest chunk whose declaration list differs from the last round (~0: none)
+  bool glb;            // lane filter non-empty: probe it
+  uint32_t skip_below; // chunks below this keep their last parse (their batch input is unchanged)
 };
 
 // ------------------------------------------------------------------ emission
@@ -272,16 +280,33 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
   return r;
 }
 
+// Stream-semantics probe of the persistent cache + batch declarations, pass 1
+// (inside the roll, LDS only): the key's blocked-Bloom word of the lane
+// filter (xcg_cache.h filt_word/filt_bits); a passing key is queued in the
+// wave's LDS scratch, slot min(passes, GSLOTS) of the lane (slot-major, so a
+// wave's 64 stores are consecutive dwords), and its bit set in pm.  Pass 2
+// (glb_verify) checks the queued keys against the fingerprint buckets in HBM
+// with all of a lane's loads in flight together, instead of one HBM round
+// trip per group of positions.
+constexpr int GSLOTS = 8;
+struct GlbQ {
+  char* lds;        // LDS base of the workgroup's struct (offset 0)
+  uint32_t lfo;     // byte offset of the lane filter
+  uint32_t sa;      // this lane's next scratch slot address (absolute LDS byte address)
+  uint32_t salim;   // its garbage slot (slot GSLOTS)
+  uint32_t pm;      // filter passes, bit per position (built reversed, like ev)
+};
+
 // Roll the probe key over the lane's 32 positions; bit j of the result is set
 // when position q0 + j is a possible cache hit.  NX1 = -X1, NX2 = -(X2 + CLO)
 // at q0 (RollingHash::roll, xcodec_hash.h:57-70, negated), so K = -lo costs one
 // instruction.  C0: the pending candidate (key c0k) is not in the table yet and
 // becomes visible at piece offset rvis (position p + rvis).  OVF: also compare the (rare) overflow
-// keys ovk[8].  GLB: also probe the persistent cache / batch filter.
+// keys ovk[8].  GLB: also run pass 1 of the persistent cache / batch probe (gq).
 template <int LOGNB, bool C0, int NOVF, bool GLB>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
                                                uint32_t kofs, uint32_t c0k, int rvis, const uint32_t* ovk,
-                                               const uint32_t* lfilt, const u32x4* ftab, uint32_t fmask) {
+                                               GlbQ& gq) {
   // bucket mask in a VGPR so that (K & KM) | kofs is one v_and_or_b32 (VOP3
   // takes no literal and one SGPR on gfx9)
   const uint32_t KM = (uint32_t)opaque((int)(((1u << LOGNB) - 1u) << 3));
@@ -306,7 +331,7 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
   // its 4 LDS probes issued before group g's probes are compared, so each
   // group's LDS latency overlaps the next group's arithmetic.  The
   // sched_barrier keeps hipcc from hoisting more than that (VGPRs).
-  auto roll4 = [&](int g, uint32_t (&kv)[4], uint2 (&e)[4]) {
+  auto roll4 = [&](int g, uint32_t (&kv)[4], uint2 (&e)[4], uint32_t (&fw)[4]) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
@@ -320,38 +345,33 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(kblk + ((kv[t] & KM) | kofs));
+    if (GLB) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fw[t] = *(const uint32_t*)(gq.lds + gq.lfo + filt_word_ofs(kv[t]));
+    }
   };
-  uint32_t kc[4];
+  uint32_t kc[4], fc[4];
   uint2 ec[4];
-  roll4(0, kc, ec);
+  roll4(0, kc, ec, fc);
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    uint32_t kn[4];
+    uint32_t kn[4], fn[4];
     uint2 en[4];
-    if (g < 7) roll4(g + 1, kn, en);
-    // Persistent cache + batch declarations: LDS bitmap first, then (rarely)
-    // one 16-byte fingerprint-bucket load; all four loads issued before use.
-    uint64_t gh[4] = {0, 0, 0, 0};
+    if (g < 7) roll4(g + 1, kn, en, fn);
     if (GLB) {
-      u32x4 q[4];
-      bool pass[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) pass[t] = (lfilt[filt_bit(kc[t]) >> 5] >> (kc[t] & 31u)) & 1u;
+      // Persistent cache + batch declarations, pass 1: queue filter passes.
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        q[t] = u32x4{0u, 0u, 0u, 0u};
-        if (pass[t]) q[t] = ftab[fbucket(kc[t], fmask)];
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t fp = kc[t] | 1u;
-        gh[t] = lanes_eq(q[t][0], fp) | lanes_eq(q[t][1], fp) | lanes_eq(q[t][2], fp) | lanes_eq(q[t][3], FOVF);
+        const uint32_t p = filt_test(fc[t], kc[t]);
+        *(uint32_t*)(gq.lds + gq.sa) = kc[t];
+        gq.sa = min(gq.sa + (p << 8), gq.salim);
+        gq.pm = (gq.pm << 1) | p;
       }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = 4 * g + t;
-      uint64_t hit = lanes_eq(ec[t].x, kc[t]) | lanes_eq(ec[t].y, kc[t]) | gh[t];
+      uint64_t hit = lanes_eq(ec[t].x, kc[t]) | lanes_eq(ec[t].y, kc[t]);
       if (C0) hit |= lanes_eq(kc[t], c0k) & (j < vB ? vis_hi : vis_lo);
 #pragma unroll
       for (int k = 0; k < NOVF; ++k) hit |= lanes_eq(o[k], kc[t]);
@@ -361,10 +381,46 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     __builtin_amdgcn_sched_barrier(0);
     if (g < 7) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { kc[t] = kn[t]; ec[t] = en[t]; }
+      for (int t = 0; t < 4; ++t) { kc[t] = kn[t]; ec[t] = en[t]; fc[t] = fn[t]; }
     }
   }
+  if (GLB) gq.pm = __builtin_bitreverse32(gq.pm);
   return __builtin_bitreverse32(ev);   // position j was shifted in at bit 31 - j
+}
+
+// Pass 2 of the stream probe: the lane's queued keys (slots [0, cnt) from
+// sa0) against the fingerprint buckets in HBM, four loads in flight per lane
+// per batch.  The i-th queued key is the i-th set bit of pm (queued in
+// position order).  Passes beyond GSLOTS are reported as events unchecked;
+// the resolver decides them exactly.
+__device__ __forceinline__ uint32_t glb_verify(uint32_t ev, const GlbQ& gq, uint32_t sa0, const u32x4* ftab,
+                                               uint32_t fmask) {
+  const uint32_t cnt = (gq.sa - sa0) >> 8;
+  uint32_t rem = gq.pm;
+#pragma unroll
+  for (int i0 = 0; i0 < GSLOTS; i0 += 4) {
+    if (ballot(cnt > (uint32_t)i0) == 0) break;
+    uint32_t kk[4];
+    u32x4 q[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kk[t] = *(const uint32_t*)(gq.lds + sa0 + 256u * (i0 + t));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      q[t] = u32x4{0u, 0u, 0u, 0u};
+      if ((uint32_t)(i0 + t) < cnt) q[t] = ftab[fbucket(kk[t], fmask)];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if ((uint32_t)(i0 + t) < cnt) {
+        const uint32_t j = (uint32_t)__builtin_ctz(rem);
+        rem &= rem - 1u;
+        const uint32_t fp = kk[t] | 1u;
+        const bool m = q[t][0] == fp || q[t][1] == fp || q[t][2] == fp || q[t][3] == FOVF;
+        ev |= (uint32_t)m << j;
+      }
+    }
+  }
+  return ev | rem;
 }
 
 // ------------------------------------------------------------------ kernel
@@ -387,9 +443,19 @@ __device__ __forceinline__ void progress_priority(int s, int L) {
 // table is kblk + kofs (LDS), its records T.  STREAM: the cache also holds the
 // persistent GPU cache g and the batch declarations b of chunks < chunk,
 // probed through the workgroup's LDS filter lfilt.
+// What a stream wave probes besides its own table: the workgroup's LDS (base
+// = offset 0), where the lane filter sits (lfo), the wave's pass-1 scratch
+// (sofs), and whether the filter holds anything (glb; else pass 1 is skipped).
+struct GlbView {
+  char* lds;
+  uint32_t lfo;
+  uint32_t sofs;
+  bool glb;
+};
+
 template <int LOGNB, int MAXD, bool STREAM>
 __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, const uint32_t kofs,
-                                             WaveRecs<LOGNB, MAXD>& T, const uint32_t chunk, const uint32_t* lfilt) {
+                                             WaveRecs<LOGNB, MAXD>& T, const uint32_t chunk, const GlbView gs) {
   constexpr int NB = 1 << LOGNB;
   const int l = lane_id();
 
@@ -571,30 +637,34 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const int vis = cand + SEG;
       const int rvis = vis - p;
       const uint32_t c0k = probe_key(cand_lo);
-      const uint32_t* lf = lfilt;
-      const u32x4* ft = prm.lf.ftab;
-      const uint32_t fm = prm.lf.fmask;
       // Bucket overflows are rare (three of a chunk's keys in one 2-slot
       // bucket); one overflow key costs one compare, more cost eight.
       uint32_t ovk[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
-      if (novf == 0) {
-        if (c0)
-          ev = roll_probe<LOGNB, true, 0, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
-        else
-          ev = roll_probe<LOGNB, false, 0, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
-      } else if (novf == 1) {
-        if (c0)
-          ev = roll_probe<LOGNB, true, 1, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
-        else
-          ev = roll_probe<LOGNB, false, 1, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
-      } else {
+      const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
+      GlbQ gq{gs.lds, gs.lfo, sa0, sa0 + 256u * GSLOTS, 0u};
+      // G = probe the persistent cache / batch declarations too
+      auto roll = [&](auto c0t, auto novft, auto glbt) {
+        return roll_probe<LOGNB, decltype(c0t)::value, decltype(novft)::value, decltype(glbt)::value>(
+            P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, gq);
+      };
+      using T0 = std::integral_constant<bool, false>;
+      using T1 = std::integral_constant<bool, true>;
+      using N0 = std::integral_constant<int, 0>;
+      using N1 = std::integral_constant<int, 1>;
+      using N8 = std::integral_constant<int, 8>;
+      auto by_novf = [&](auto glbt) {
+        if (novf == 0) return c0 ? roll(T1{}, N0{}, glbt) : roll(T0{}, N0{}, glbt);
+        if (novf == 1) return c0 ? roll(T1{}, N1{}, glbt) : roll(T0{}, N1{}, glbt);
         // duplicates of a real overflow key pad the unused slots
-        if (c0)
-          ev = roll_probe<LOGNB, true, 8, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
-        else
-          ev = roll_probe<LOGNB, false, 8, STREAM>(P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, lf, ft, fm);
+        return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
+      };
+      if (STREAM && gs.glb) {
+        ev = by_novf(std::integral_constant<bool, STREAM>{});
+        ev = glb_verify(ev, gq, sa0, prm.lf.ftab, prm.lf.fmask);
+      } else {
+        ev = by_novf(T0{});
       }
       // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
@@ -725,7 +795,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       }
       dl[k] = nv;
     }
-    if (ballot(diff) != 0 && l == 0) atomicOr(prm.changed, 1u);
+    if (ballot(diff) != 0 && l == 0) atomicMin(prm.changed, chunk);
     if (l == 0) prm.ndecl[chunk] = ndecl;
   }
   if (l == 0) {
@@ -756,27 +826,35 @@ __global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams pr
   const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
   if (chunk >= prm.n) return;
-  encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, nullptr);
+  encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk,
+                                   GlbView{nullptr, 0u, 0u, false});
 }
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
 // the lane filter; each wave walks chunks wave_id, wave_id + total_waves, ...
 template <int LOGNB, int MAXD, int SW>
 __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
-  __shared__ StreamLDS<LOGNB, MAXD, SW> S;
-  for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
-    ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
+  using L = StreamLDS<LOGNB, MAXD, SW>;
+  __shared__ L S;
+  if (prm.glb) {
+    for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
+      ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
+  }
   __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
+  const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
+                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), prm.glb};
   const uint32_t stride = gridDim.x * SW;
-  for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride)
-    encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, S.lfilt);
+  for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
+    if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
+    encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
+  }
 }
 
 template __global__ void encode_independent_kernel<10, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
-template __global__ void encode_stream_kernel<9, 72, 12>(EncParams);
-template __global__ void encode_stream_kernel<11, 264, 2>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 16>(EncParams);
+template __global__ void encode_stream_kernel<10, 264, 6>(EncParams);
 
 }  // namespace xcg
 
@@ -817,33 +895,47 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   ftab_insert(ftab, fmask, d.x, d.y);
 }
 
-// Commit the converged declarations into the persistent cache: one wave per
-// (chunk, declaration) copies the 2048-byte segment into the pool
-// (XCodecMemoryCache::enter, xcodec_cache.h:303-325).
+// Commit the converged declarations into the persistent cache
+// (XCodecMemoryCache::enter, xcodec_cache.h:303-325).  Block (chunk c, part q)
+// takes declarations q*256 .. q*256+255 of chunk c: one thread each inserts
+// the hash (segments numbered by one atomic per block), then the block's
+// waves copy the 2048-byte segments into the pool.
 __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                      uint32_t maxd, const uint8_t* in, const uint64_t* chunk_off,
                                                      HashTab g, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
                                                      uint32_t* filt, uint32_t* ftab, uint32_t fmask, int32_t* status) {
-  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t c = (uint32_t)(w / maxd), k = (uint32_t)(w % maxd);
-  if (c >= n || k >= ndecl[c]) return;
-  const uint4 d = decl[w];
-  uint32_t seg = 0;
-  if (lane_id() == 0) seg = atomicAdd(nseg, 1u);
-  seg = readfirst(seg);
-  if (seg >= seg_cap) {
-    if (lane_id() == 0) atomicOr(status, 4);
-    return;
+  __shared__ uint32_t s_base;
+  const uint32_t parts = (maxd + 255) / 256;
+  const uint32_t c = blockIdx.x / parts, k0 = (blockIdx.x % parts) * 256u;
+  const uint32_t nd = c < n ? ndecl[c] : 0u;
+  const uint32_t cnt = nd > k0 ? min(256u, nd - k0) : 0u;
+  if (cnt == 0) return;                            // uniform over the block
+  if (threadIdx.x == 0) s_base = atomicAdd(nseg, cnt);
+  __syncthreads();
+  const uint32_t k = k0 + threadIdx.x;
+  const bool have = k < nd;
+  const uint32_t seg = s_base + threadIdx.x;
+  if (have) {
+    const uint4 d = decl[(uint64_t)c * maxd + k];
+    if (seg >= seg_cap) {
+      atomicOr(status, 4);
+    } else {
+      if (!tab_insert_min(g, d.x, d.y, seg)) atomicOr(status, 2);
+      filt_insert(filt, d.x, d.y);
+      ftab_insert(ftab, fmask, d.x, d.y);
+    }
   }
-  const uint8_t* src = in + chunk_off[c] + d.z;
-  uint8_t* dst = pool + (uint64_t)seg * SEG;
+  // the block's segments are s_base + (0 .. cnt), in declaration order
+  const uint32_t base = s_base;
   const int l = lane_id();
-  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
-  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
-  if (l == 0) {
-    if (!tab_insert_min(g, d.x, d.y, seg)) atomicOr(status, 2);
-    filt_insert(filt, d.x, d.y);
-    ftab_insert(ftab, fmask, d.x, d.y);
+  const uint8_t* x = in + chunk_off[c];
+  for (uint32_t j = readfirst(threadIdx.x >> 6); j < cnt; j += 4) {
+    const uint32_t sg = base + j;
+    if (sg >= seg_cap) break;
+    const uint8_t* src = x + readfirst(decl[(uint64_t)c * maxd + k0 + j].z);
+    uint8_t* dst = pool + (uint64_t)sg * SEG;
+    *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+    *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
   }
 }
 
@@ -881,6 +973,7 @@ struct XcgStreamArgs {
   uint32_t maxd;
   uint32_t* changed;
   uint32_t* h_changed;   // pinned host word
+  int g_empty;           // the persistent cache is known to be empty
 };
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
@@ -901,44 +994,59 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&props, dev) != hipSuccess) return -5;
   const uint32_t wgs = (uint32_t)props.multiProcessorCount;
   const bool big = a->maxd > 72;                     // chunks > 128 KiB (<= 512 KiB frames)
-  const uint32_t SW = big ? 2 : 12;
-  const dim3 sgrid(min(wgs * (big ? 2u : 1u), (n + SW - 1) / SW)), sblock(64 * SW);
+  const uint32_t SW = big ? 6 : 16;               // one workgroup per CU (LDS)
+  const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
   auto launch = [&]() {
-    if (big) hipLaunchKernelGGL((encode_stream_kernel<11, 264, 2>), sgrid, sblock, 0, stream, prm);
-    else hipLaunchKernelGGL((encode_stream_kernel<9, 72, 12>), sgrid, sblock, 0, stream, prm);
+    if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6>), sgrid, sblock, 0, stream, prm);
+    else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16>), sgrid, sblock, 0, stream, prm);
   };
-  if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess) return -5;
+  // lowest chunk whose declaration list changed in the round just run (~0u: none)
+  auto changed_after = [&](uint32_t& fc) -> bool {
+    if (hipMemcpyAsync(a->h_changed, a->changed, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return false;
+    fc = *a->h_changed;
+    return true;
+  };
+  if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess ||
+      hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
+    return -5;
   // Round 0: every chunk against the persistent cache + its own declarations.
   prm.use_b = false;
+  prm.glb = !a->g_empty;
+  prm.skip_below = 0;
   prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask};
   launch();
   int rounds = 1;
+  uint32_t fc = 0;
+  if (!changed_after(fc)) return -5;
   // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
   // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
   // chunk k after round k; a round that changes no declaration list is the
-  // fixed point, which is the sequential result.
-  for (uint32_t r = 1; n > 1 && r <= n; ++r) {
+  // fixed point, which is the sequential result.  Chunks up to the lowest one
+  // whose list changed in the previous round see the same batch input as then
+  // and keep their parse.  (Round 0's lists are compared with empty ones.)
+  for (uint32_t r = 1; n > 1 && r <= n && fc != ~0u; ++r) {
     if (hipMemsetAsync(a->b_keys, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
         hipMemsetAsync(a->b_vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
         hipMemcpyAsync(a->r_filt, a->g_filt, fbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(a->r_ftab, a->g_ftab, tbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
-        hipMemsetAsync(a->changed, 0, 4, stream) != hipSuccess)
+        hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
       return -5;
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
                        (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, prm.b, a->r_filt, a->r_ftab,
                        a->fmask, a->status);
     prm.use_b = true;
+    prm.glb = true;
+    prm.skip_below = fc + 1;
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask};
     launch();
     ++rounds;
-    if (hipMemcpyAsync(a->h_changed, a->changed, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
-      return -5;
-    if (*a->h_changed == 0) break;
+    if (!changed_after(fc)) return -5;
   }
-  const uint64_t nwaves = (uint64_t)n * a->maxd;
-  hipLaunchKernelGGL(commit_kernel, dim3((unsigned)((nwaves * 64 + 255) / 256)), dim3(256), 0, stream,
+  const uint32_t parts = (a->maxd + 255) / 256;
+  hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream,
                      (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, a->in, a->chunk_off,
                      prm.g, a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask, a->status);
   if (rounds_out) *rounds_out = rounds;
