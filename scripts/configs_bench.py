@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Stream-semantics throughput on BASELINE.json's other configurations, one
+GPU (the headline C2 independent-chunk line
+is bench.py's).  Every figure is checked: a prefix against the CPU oracle
+(sequential XCodecEncoder semantics from an empty cache) and the whole run by
+a GPU decode round trip.
+
+  c2s  4096 x 64 KiB, seed 0xC2, dup 50, one cache, chunk order (tack loop)
+  c3   64 streams x 16 MiB (seeds 100..163, dup 5), chunks round-robin at
+       64 KiB; untimed warm-up encode into one shared cache, then the timed
+       re-encode against the warm cache, and the decode of that output with a
+       decoder cache warmed by decoding the warm-up output
+  c4   131072 x 4 KiB packets (one GPU's shard of 1 M), seed 0xC4, dup 4
+  c5   1 GiB (one GPU's shard of 8 GiB) in 128 KiB chunks, seed 0xC5, dup 20,
+       cold unbounded cache, batches of --batch-mib
+
+Prints one JSON line per config.  --scale shrinks the inputs (tests).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+KiB, MiB = 1024, 1 << 20
+
+
+class Batches:
+    """Host data resident on the GPU, cut into encode() chunks, encoded in
+    batches of `per` chunks with stream semantics on one context."""
+
+    def __init__(self, ctx, data: np.ndarray, offs, lens, per: int):
+        import torch
+        self.ctx, self.per = ctx, per
+        self.dev = torch.device('cuda', ctx.device)
+        self.data = data
+        self.offs = np.ascontiguousarray(offs, np.uint64)
+        self.lens = np.ascontiguousarray(lens, np.uint32)
+        n = self.offs.size
+        self.n = n
+        bounds = 2 * self.lens.astype(np.uint64) + 16
+        self.oo = np.zeros(n, np.uint64)
+        self.oo[1:] = np.cumsum(bounds)[:-1]
+        self.d_in = torch.from_numpy(data).to(self.dev)
+        self.d_off = torch.from_numpy(self.offs.view(np.int64)).to(self.dev)
+        self.d_len = torch.from_numpy(self.lens.view(np.int32)).to(self.dev)
+        self.d_oo = torch.from_numpy(self.oo.view(np.int64)).to(self.dev)
+        self.d_out = torch.empty(int(bounds.sum()), dtype=torch.uint8, device=self.dev)
+        self.d_ol = torch.zeros(n, dtype=torch.int64, device=self.dev)
+        self.maxlen = int(self.lens.max())
+        self.rounds = []
+
+    def encode_all(self):
+        from wanproxy_amd.xcgpu import XCG_SEM_STREAM
+        self.rounds = []
+        for a in range(0, self.n, self.per):
+            b = min(self.n, a + self.per)
+            self.ctx.encode_batch_device(self.d_in, self.d_off[a:b], self.d_len[a:b], b - a, self.maxlen,
+                                         self.d_out, self.d_oo[a:b], self.d_ol[a:b], semantics=XCG_SEM_STREAM)
+            self.rounds.append(self.ctx.last_rounds())
+
+    def outputs(self):
+        out = self.d_out.cpu().numpy()
+        ol = self.d_ol.cpu().numpy()
+        return [out[int(self.oo[i]):int(self.oo[i]) + int(ol[i])].tobytes() for i in range(self.n)]
+
+    def out_bytes(self) -> int:
+        return int(self.d_ol.sum().item())
+
+
+def decode_device(ctx, encs, per: int, chunk: int):
+    """Decode a list of encoded chunks (one stream) on ctx in batches of `per`;
+    returns (decoded bytes, seconds of the timed decode)."""
+    import ctypes as C
+    import torch
+    from wanproxy_amd.xcgpu import _check, lib
+    dev = torch.device('cuda', ctx.device)
+    n = len(encs)
+    lens = np.array([len(e) for e in encs], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+    blob = np.frombuffer(b''.join(encs), np.uint8)
+    d_enc = torch.from_numpy(blob.copy()).to(dev)
+    d_eoff = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_elen = torch.from_numpy(lens.view(np.int32)).to(dev)
+    cap = per * chunk + 4096           # decoded bytes of one batch
+    d_dout = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_doo = torch.zeros(per, dtype=torch.int64, device=dev)
+    d_dol = torch.zeros(per, dtype=torch.int64, device=dev)
+    d_dst = torch.zeros(per, dtype=torch.int32, device=dev)
+    d_dcons = torch.zeros(per, dtype=torch.int64, device=dev)
+    unk = np.zeros(16, np.uint64)
+    nunk = np.zeros(1, np.uint32)
+    tot = np.zeros(1, np.uint64)
+    parts, secs = [], 0.0
+    for a in range(0, n, per):
+        b = min(n, a + per)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        _check(lib().xcg_decode_batch(ctx.h, C.c_void_p(d_enc.data_ptr()), C.c_void_p(d_eoff[a:].data_ptr()),
+                                      C.c_void_p(d_elen[a:].data_ptr()), b - a, int(lens[a:b].max()),
+                                      C.c_void_p(d_dout.data_ptr()), cap, C.c_void_p(d_doo.data_ptr()),
+                                      C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
+                                      C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
+                                      tot.ctypes.data, None))
+        torch.cuda.synchronize(dev)
+        secs += time.perf_counter() - t0
+        st = d_dst[:b - a].cpu().numpy()
+        if (st != 0).any() or nunk[0]:
+            raise SystemExit(f'decode status {np.unique(st)} unknown {int(nunk[0])}')
+        parts.append(d_dout[:int(tot[0])].cpu().numpy().tobytes())
+    return b''.join(parts), secs
+
+
+def check_prefix(data, offs, lens, got, k, what):
+    from oracle.lib import Oracle
+    k = min(k, len(got))
+    exp = Oracle().encode_batch(data, offs[:k], lens[:k], mode=1)
+    if got[:k] != exp:
+        bad = next(i for i in range(k) if got[i] != exp[i])
+        raise SystemExit(f'PARITY FAILURE ({what}) at chunk {bad}')
+    return k
+
+
+def timed_encode(B: 'Batches', reps: int, clear_ctx=True):
+    import torch
+    walls = []
+    for _ in range(reps):
+        if clear_ctx:
+            B.ctx.cache_clear()
+        torch.cuda.synchronize(B.dev)
+        t0 = time.perf_counter()
+        B.encode_all()
+        torch.cuda.synchronize(B.dev)
+        walls.append(time.perf_counter() - t0)
+    B.ctx.status()
+    return min(walls)
+
+
+def run_c2s(args):
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    n = max(16, int(4096 * args.scale))
+    data = np.frombuffer(synth.stream(0xC2, n * 64 * KiB, 50, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 64 * KiB)
+    ctx = Context(0, cache_segments=1 << 18)
+    B = Batches(ctx, data, offs, lens, per=n)
+    wall = timed_encode(B, args.reps)
+    got = B.outputs()
+    k = check_prefix(data, offs, lens, got, 256, 'c2s')
+    dctx = Context(0, cache_segments=1 << 18)
+    dec, dsec = decode_device(dctx, got, per=n, chunk=64 * KiB)
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c2s)')
+    inb = data.size
+    return {'config': 'C2-S2: %d x 64 KiB, dup 50, one cache, chunk order' % n,
+            'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 3),
+            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+            'rounds': B.rounds, 'checked': f'first {k} chunks vs oracle; full decode round trip'}
+
+
+def run_c3(args):
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    nstreams = 64
+    per_stream = max(64 * KiB, int(16 * MiB * args.scale) // (64 * KiB) * 64 * KiB)
+    streams = [np.frombuffer(synth.stream(100 + i, per_stream, 5, 0), np.uint8) for i in range(nstreams)]
+    # round-robin: stream 0 chunk 0, stream 1 chunk 0, ...
+    cps = per_stream // (64 * KiB)
+    data = np.empty(nstreams * per_stream, np.uint8)
+    offs = np.zeros(nstreams * cps, np.uint64)
+    lens = np.full(nstreams * cps, 64 * KiB, np.uint32)
+    o = 0
+    for c in range(cps):
+        for s in range(nstreams):
+            i = c * nstreams + s
+            data[o:o + 64 * KiB] = streams[s][c * 64 * KiB:(c + 1) * 64 * KiB]
+            offs[i] = o
+            o += 64 * KiB
+    segs = int(data.size // 2048 * 1.05) + 4096
+    ctx = Context(0, cache_segments=segs)
+    per = 4096
+    B = Batches(ctx, data, offs, lens, per=per)
+    B.encode_all()                                   # warm-up (untimed)
+    warm = B.outputs()
+    k = check_prefix(data, offs, lens, warm, 128, 'c3 warm-up')
+    warm_rounds = B.rounds
+    import torch
+    torch.cuda.synchronize(B.dev)
+    t0 = time.perf_counter()
+    B.encode_all()                                   # timed: against the warm cache
+    torch.cuda.synchronize(B.dev)
+    wall = time.perf_counter() - t0
+    ctx.status()
+    hot = B.outputs()
+    dctx = Context(0, cache_segments=segs)
+    dec0, _ = decode_device(dctx, warm, per=per, chunk=64 * KiB)     # warms the decoder cache
+    if dec0 != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c3 warm-up)')
+    dec1, dsec = decode_device(dctx, hot, per=per, chunk=64 * KiB)
+    if dec1 != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c3 warm)')
+    inb = data.size
+    return {'config': 'C3: %d streams x %d MiB round-robin 64 KiB chunks, warm shared cache' % (nstreams, per_stream >> 20),
+            'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+            'warm_rounds': warm_rounds, 'rounds': B.rounds, 'batch_chunks': per,
+            'checked': f'warm-up first {k} chunks vs oracle; both passes decoded back to the input'}
+
+
+def run_c4(args):
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    n = max(64, int(131072 * args.scale))
+    data = np.frombuffer(synth.stream(0xC4, n * 4 * KiB, 4, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 4 * KiB)
+    ctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
+    B = Batches(ctx, data, offs, lens, per=args.c4_batch)
+    wall = timed_encode(B, args.reps)
+    got = B.outputs()
+    k = check_prefix(data, offs, lens, got, 2048, 'c4')
+    dctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
+    dec, dsec = decode_device(dctx, got, per=args.c4_batch, chunk=4 * KiB)
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c4)')
+    inb = data.size
+    return {'config': 'C4 shard: %d x 4 KiB packets, dup 4, one cache' % n, 'batch_chunks': args.c4_batch,
+            'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+            'rounds': B.rounds[:8], 'checked': f'first {k} packets vs oracle; full decode round trip'}
+
+
+def run_c5(args):
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
+    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    segs = nbytes // 2048 + 4096
+    ctx = Context(0, cache_segments=segs)
+    per = max(1, args.batch_mib * MiB // (128 * KiB))
+    B = Batches(ctx, data, offs, lens, per=per)
+    wall = timed_encode(B, args.reps)
+    got = B.outputs()
+    k = check_prefix(data, offs, lens, got, 64, 'c5')
+    dctx = Context(0, cache_segments=segs)
+    dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c5)')
+    inb = data.size
+    return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, cold unbounded cache' % (nbytes >> 20),
+            'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+            'rounds': B.rounds, 'checked': f'first {k} chunks vs oracle; full decode round trip'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('configs', nargs='*', default=['c2s', 'c3', 'c4', 'c5'])
+    ap.add_argument('--scale', type=float, default=1.0)
+    ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--batch-mib', type=int, default=256)
+    ap.add_argument('--c4-batch', type=int, default=16384)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5}
+    for c in args.configs:
+        t0 = time.perf_counter()
+        r = fns[c](args)
+        r['wall_s'] = round(time.perf_counter() - t0, 1)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == '__main__':
+    main()

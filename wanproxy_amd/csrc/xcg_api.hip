@@ -50,7 +50,10 @@ struct XcgStreamArgs {
   uint32_t maxd;
   uint32_t* changed;
   uint32_t* h_changed;
-  int g_empty;
+  uint32_t* g_gfilt;
+  uint32_t* r_gfilt;
+  uint32_t gmask;
+  uint32_t* bcount;
 };
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
@@ -76,6 +79,8 @@ struct XcgDecodeArgs {
   uint32_t* g_filt;
   uint32_t* g_ftab;
   uint32_t fmask;
+  uint32_t* g_gfilt;
+  uint32_t gmask;
   uint64_t* x_keys;
   uint64_t* x_vals;
   uint64_t* x_latest;
@@ -97,7 +102,8 @@ extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*,
 extern "C" int xcg_launch_cache_lookup(uint64_t*, uint64_t*, uint32_t, const uint8_t*, uint64_t, uint8_t*, int32_t*,
                                        hipStream_t);
 extern "C" int xcg_launch_cache_enter(uint64_t*, uint64_t*, uint32_t, uint8_t*, uint32_t*, uint32_t, uint32_t*,
-                                      uint32_t*, uint32_t, uint64_t, const uint8_t*, int, int32_t*, hipStream_t);
+                                      uint32_t*, uint32_t, uint32_t*, uint32_t, uint64_t, const uint8_t*, int, int32_t*,
+                                      hipStream_t);
 extern "C" int xcg_launch_decode(const XcgDecodeArgs*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 
 // The persistent segment cache of a context: XCodecMemoryCache's
@@ -114,6 +120,8 @@ struct GpuCache {
   uint32_t* filt = nullptr;     // FILT_WORDS
   uint32_t* ftab = nullptr;     // fbuckets * 4
   uint32_t fmask = 0;
+  uint32_t* gfilt = nullptr;    // global lane filter: gmask + 1 words (~1 per segment)
+  uint32_t gmask = 0;
 };
 
 struct BatchScratch {
@@ -127,6 +135,8 @@ struct BatchScratch {
   uint32_t* ndecl = nullptr;
   uint32_t* changed = nullptr;
   uint32_t* h_changed = nullptr;   // pinned
+  uint32_t* r_gfilt = nullptr;
+  uint32_t* bcount = nullptr;
 };
 
 struct DecodeScratch {
@@ -166,7 +176,6 @@ struct xcg_ctx {
   DecodeScratch ds;
   xcg_window* own_win = nullptr;   // default window (lazily allocated)
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
-  bool g_empty = true;             // nothing entered since the cache was (re)created or cleared
 };
 
 namespace {
@@ -192,13 +201,14 @@ uint32_t pow2_at_least(uint64_t v) {
 
 void free_cache(GpuCache& g) {
   (void)hipFree(g.keys); (void)hipFree(g.vals); (void)hipFree(g.pool); (void)hipFree(g.nseg);
-  (void)hipFree(g.filt); (void)hipFree(g.ftab);
+  (void)hipFree(g.filt); (void)hipFree(g.ftab); (void)hipFree(g.gfilt);
   g = GpuCache{};
 }
 
 void free_scratch(BatchScratch& b) {
   (void)hipFree(b.b_keys); (void)hipFree(b.b_vals); (void)hipFree(b.r_filt); (void)hipFree(b.r_ftab);
-  (void)hipFree(b.decl); (void)hipFree(b.ndecl); (void)hipFree(b.changed);
+  (void)hipFree(b.decl); (void)hipFree(b.ndecl); (void)hipFree(b.changed); (void)hipFree(b.r_gfilt);
+  (void)hipFree(b.bcount);
   if (b.h_changed) (void)hipHostFree(b.h_changed);
   b = BatchScratch{};
 }
@@ -207,7 +217,8 @@ int clear_cache(GpuCache& g) {
   if (hipMemset(g.keys, 0xFF, 8ull * (g.mask + 1)) != hipSuccess ||
       hipMemset(g.vals, 0xFF, 8ull * (g.mask + 1)) != hipSuccess || hipMemset(g.nseg, 0, 4) != hipSuccess ||
       hipMemset(g.filt, 0, 4ull * FILT_WORDS) != hipSuccess ||
-      hipMemset(g.ftab, 0, 16ull * (g.fmask + 1)) != hipSuccess)
+      hipMemset(g.ftab, 0, 16ull * (g.fmask + 1)) != hipSuccess ||
+      hipMemset(g.gfilt, 0, 4ull * (g.gmask + 1)) != hipSuccess)
     return XCG_EHIP;
   return XCG_OK;
 }
@@ -220,12 +231,14 @@ int ensure_cache(xcg_ctx* c) {
   g.seg_cap = (uint32_t)segs;
   const uint32_t cap = pow2_at_least(2 * segs + 1024);
   g.mask = cap - 1;
-  const uint32_t fb = pow2_at_least(2 * segs + 4096);
+  const uint32_t fb = pow2_at_least(segs < 65536 ? 32768 : segs / 2);   // ~2 keys per bucket at capacity
   g.fmask = fb - 1;
+  const uint32_t gw = pow2_at_least(segs < 131072 ? 65536 : segs / 2);
+  g.gmask = gw - 1;
   if (hipMalloc(&g.keys, 8ull * cap) != hipSuccess || hipMalloc(&g.vals, 8ull * cap) != hipSuccess ||
       hipMalloc(&g.pool, segs * (uint64_t)XCG_SEGMENT_LENGTH + 16) != hipSuccess ||
       hipMalloc(&g.nseg, 16) != hipSuccess || hipMalloc(&g.filt, 4ull * FILT_WORDS) != hipSuccess ||
-      hipMalloc(&g.ftab, 16ull * fb) != hipSuccess) {
+      hipMalloc(&g.ftab, 16ull * fb) != hipSuccess || hipMalloc(&g.gfilt, 4ull * gw) != hipSuccess) {
     free_cache(g);
     return XCG_ENOMEM;
   }
@@ -246,7 +259,8 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipMalloc(&b.r_filt, 4ull * FILT_WORDS) != hipSuccess ||
       hipMalloc(&b.r_ftab, 16ull * (c->g.fmask + 1)) != hipSuccess ||
       hipMalloc(&b.decl, 16ull * n * maxd) != hipSuccess || hipMalloc(&b.ndecl, 4ull * n) != hipSuccess ||
-      hipMalloc(&b.changed, 16) != hipSuccess || hipHostMalloc(&b.h_changed, 16) != hipSuccess) {
+      hipMalloc(&b.changed, 16) != hipSuccess || hipHostMalloc(&b.h_changed, 16) != hipSuccess ||
+      hipMalloc(&b.r_gfilt, 4ull * (c->g.gmask + 1)) != hipSuccess || hipMalloc(&b.bcount, 4 * 64) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
@@ -381,9 +395,7 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
   if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
-  const int rc = clear_cache(c->g);
-  if (rc == XCG_OK) c->g_empty = true;
-  return rc;
+  return clear_cache(c->g);
 }
 
 int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
@@ -401,7 +413,6 @@ int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
     return XCG_ENOMEM;
   }
   rc = XCG_OK;
-  if (mode != 0) c->g_empty = false;
   if (mode == 0) {   // lookup
     if (xcg_launch_cache_lookup(c->g.keys, c->g.vals, c->g.mask, c->g.pool, hash, d_seg, d_res, nullptr) != 0 ||
         hipMemcpy(res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -410,7 +421,8 @@ int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
   } else {           // enter (1) / replace (2)
     if (hipMemcpy(d_seg, in_seg, XCG_SEGMENT_LENGTH, hipMemcpyHostToDevice) != hipSuccess ||
         xcg_launch_cache_enter(c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap, c->g.filt,
-                               c->g.ftab, c->g.fmask, hash, d_seg, mode == 2, d_res, nullptr) != 0 ||
+                               c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, hash, d_seg, mode == 2, d_res,
+                               nullptr) != 0 ||
         hipMemcpy(res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess)
       rc = XCG_EHIP;
   }
@@ -491,7 +503,8 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
   DeviceGuard g(c->device);
   // A null cache has no state to carry: both semantics are the same pass.
   if (semantics == XCG_SEM_STREAM && !(c->flags & XCG_FLAG_NULLCACHE)) {
-    const uint32_t maxd = max_chunk_len > (1u << 17) ? 264 : 72;
+    // declaration slots per chunk: a chunk of L bytes declares at most L / 2048
+    const uint32_t maxd = max_chunk_len / XCG_SEGMENT_LENGTH + 1;
     int rc = ensure_cache(c);
     if (rc == XCG_OK) rc = ensure_scratch(c, n, maxd);
     if (rc != XCG_OK) return rc;
@@ -499,10 +512,9 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
                     c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                     c->g.filt, c->g.ftab, c->g.fmask, c->bs.b_keys, c->bs.b_vals, c->bs.b_mask,
                     c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
-                    c->g_empty ? 1 : 0};
+                    c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount};
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
-    c->g_empty = false;
     c->last_rounds = rounds;
     return rc == 0 ? XCG_OK : XCG_EHIP;
   }
@@ -597,12 +609,11 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   xcg_window* w = c->cur_win;
   XcgDecodeArgs a{d_enc, d_chunk_off, d_chunk_len, n, d_out, out_cap, d_out_off, d_out_len, d_chunk_status,
                   d_consumed, c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
-                  c->g.filt, c->g.ftab, c->g.fmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
+                  c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
                   c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
                   c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count};
   uint64_t total = 0, blockp = 0, berr = 0;
   uint32_t nunk = 0;
-  c->g_empty = false;
   const int lrc = xcg_launch_decode(&a, &total, &blockp, &berr, &nunk, (hipStream_t)stream);
   if (h_total_out) *h_total_out = total;
   if (lrc == -75) return XCG_EOVERFLOW;

@@ -7,8 +7,10 @@
 //                    always has bits 32..35 clear: mix() shifts bits_hash by 36)
 //   vals[cap]  u64   G: segment index into pool;  B: (chunk << 32) | position
 //   pool[nseg_cap * 2048]  segment bytes (G only)
-//   ftab[fbuckets * 4] u32  lane-probe fingerprint buckets: 3 slots of (K | 1)
-//                    + an overflow word, one 16-byte load per probe
+//   ftab[fbuckets * 4] u32  lane-probe fingerprint buckets of 16 B: seven 16-bit
+//                    fingerprints of K + an overflow flag, one 16-byte load per
+//                    probe; ~2 keys per bucket at capacity, so the table (2 MiB
+//                    per 2^18 segments) stays in an XCD's L2
 //   filt[FILT_BITS / 32] u32  the bitmap a workgroup loads into LDS (bit K mod 2^19)
 #pragma once
 #include "xcg_device.h"
@@ -18,7 +20,7 @@ namespace xcg {
 constexpr uint64_t EMPTY_KEY = ~0ull;
 constexpr int FILT_LOG2 = 19;                       // 2^19 bits = 64 KiB of LDS
 constexpr uint32_t FILT_WORDS = (1u << FILT_LOG2) / 32;
-constexpr uint32_t FOVF = 2u;                       // bucket-overflow marker (even: never a fingerprint)
+constexpr uint32_t FOVF16 = 2u;                     // bucket-overflow flag in slot 7 (even: never a fingerprint)
 
 struct HashTab {      // exact open-addressed map u64 -> u64
   uint64_t* keys;
@@ -26,10 +28,23 @@ struct HashTab {      // exact open-addressed map u64 -> u64
   uint32_t mask;      // cap - 1
 };
 
-struct LaneFilter {   // what a lane probes: LDS bitmap (copied from filt) + fingerprint buckets
+struct LaneFilter {   // what a lane probes: LDS bitmap (copied from filt) or the global
+                      // filter gfilt, then the fingerprint buckets
   const uint32_t* filt;
   const u32x4* ftab;
   uint32_t fmask;     // fbuckets - 1
+  const uint32_t* gfilt;
+  uint32_t gmask;     // gfilt words - 1
+};
+
+// Every filter kept over a set of hashes (the persistent cache's, or a round's
+// copy extended by the batch declarations).
+struct FiltSet {
+  uint32_t* filt;     // FILT_WORDS: the 64 KiB LDS lane filter
+  uint32_t* ftab;     // (fmask + 1) * 4: fingerprint buckets
+  uint32_t fmask;
+  uint32_t* gfilt;    // (gmask + 1): the global lane filter (large caches)
+  uint32_t gmask;
 };
 
 __device__ __forceinline__ uint32_t mix32(uint32_t a, uint32_t b) {
@@ -62,6 +77,16 @@ __device__ __forceinline__ uint32_t filt_mask(uint32_t k) {
 }
 __device__ __forceinline__ uint32_t filt_test(uint32_t w, uint32_t k) {
   return (w >> ((k >> 16) & 31u)) & (w >> ((k >> 24) & 31u)) & 1u;
+}
+// Global lane filter (caches too large for 64 KiB: >~100 k keys, where the
+// LDS filter saturates): the same two-bits-per-word blocked Bloom filter,
+// ~1 key per word (2 MiB at 2^19 keys, so it stays in an XCD's 4 MiB L2 --
+// random loads run at ~270 G/s from L2-resident tables vs ~60 G/s beyond).
+// word = K bits 10.., bits = K bits 0..4 and 5..9.
+__device__ __forceinline__ uint32_t gfilt_word(uint32_t k, uint32_t gmask) { return (k >> 10) & gmask; }
+__device__ __forceinline__ uint32_t gfilt_mask(uint32_t k) { return (1u << (k & 31u)) | (1u << ((k >> 5) & 31u)); }
+__device__ __forceinline__ uint32_t gfilt_test(uint32_t w, uint32_t k) {
+  return (w >> (k & 31u)) & (w >> ((k >> 5) & 31u)) & 1u;
 }
 __device__ __forceinline__ uint32_t fbucket(uint32_t k, uint32_t fmask) { return mix32(k, 0x5BD1E995u) & fmask; }
 
@@ -136,24 +161,50 @@ __device__ __forceinline__ bool tab_insert_min(HashTab t, uint32_t lo, uint32_t 
   return false;
 }
 
-// Fingerprint bucket insert: first free of 3 slots, else mark overflow (lanes
-// then report an event there and the resolver decides exactly).
+// 16-bit fingerprint of a probe key (odd, so never 0 = empty or FOVF16).
+__device__ __forceinline__ uint32_t fp16_of(uint32_t k) { return (mix32(k, 0x27D4EB2Fu) >> 16) | 1u; }
+
+// Fingerprint bucket insert: first free of the 7 slots, else set the bucket's
+// overflow flag (a probe of that bucket then reports an event and the
+// resolver decides exactly).
 __device__ __forceinline__ void ftab_insert(uint32_t* ftab, uint32_t fmask, uint32_t lo, uint32_t hi) {
   (void)hi;
-  const uint32_t k = probe_key(lo), fp = k | 1u;
-  const uint32_t b = fbucket(k, fmask);
-  uint32_t* s = ftab + 4 * b;
-  for (int k = 0; k < 3; ++k) {
-    const uint32_t prev = atomicCAS(s + k, 0u, fp);
-    if (prev == 0u || prev == fp) return;
+  const uint32_t k = probe_key(lo), fp = fp16_of(k);
+  uint32_t* s = ftab + 4 * fbucket(k, fmask);
+  for (int w = 0; w < 4; ++w) {
+    uint32_t old = s[w];
+    for (;;) {
+      const uint32_t a = old & 0xFFFFu, b = old >> 16;
+      if (a == fp || (w < 3 && b == fp)) return;      // already there
+      uint32_t nw;
+      if (a == 0u) nw = old | fp;
+      else if (w < 3 && b == 0u) nw = old | (fp << 16);
+      else break;                                      // word full (slot 7 is the flag)
+      const uint32_t got = atomicCAS(s + w, old, nw);
+      if (got == old) return;
+      old = got;
+    }
   }
-  atomicExch(s + 3, FOVF);
+  atomicOr(s + 3, FOVF16 << 16);
 }
 
-__device__ __forceinline__ void filt_insert(uint32_t* filt, uint32_t lo, uint32_t hi) {
-  (void)hi;
+// Does the bucket q hold key k (or overflow)?
+__device__ __forceinline__ bool ftab_match(const u32x4 q, uint32_t k) {
+  const uint32_t t = fp16_of(k) * 0x10001u;
+  bool m = (q[3] >> 16) == FOVF16;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t d = q[w] ^ t;
+    m = m || (d & 0xFFFFu) == 0u || (d >> 16) == 0u;
+  }
+  return m;
+}
+
+__device__ __forceinline__ void filt_insert(const FiltSet& f, uint32_t lo, uint32_t hi) {
   const uint32_t k = probe_key(lo);
-  atomicOr(filt + (filt_word_ofs(k) >> 2), filt_mask(k));
+  atomicOr(f.filt + (filt_word_ofs(k) >> 2), filt_mask(k));
+  atomicOr(f.gfilt + gfilt_word(k, f.gmask), gfilt_mask(k));
+  ftab_insert(f.ftab, f.fmask, lo, hi);
 }
 
 }  // namespace xcg

@@ -545,8 +545,7 @@ __global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint64_t* le
 // replace / skip), new segments are numbered by a block count (one global
 // atomic per block), then the block's waves copy the segments.
 __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8_t* pool, uint32_t* nseg,
-                                                            uint32_t seg_cap, uint32_t* filt, uint32_t* ftab,
-                                                            uint32_t fmask) {
+                                                            uint32_t seg_cap, FiltSet fs) {
   __shared__ uint32_t s_cnt, s_base, s_njob;
   __shared__ uint4 s_job[256];   // (slot, destination segment, kind, -)
   const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -578,8 +577,7 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
   if (kind == 1) {
     const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
     if (!tab_insert_min(prm.g, lo, hi, seg)) atomicOr(prm.status, 2);
-    filt_insert(filt, lo, hi);
-    ftab_insert(ftab, fmask, lo, hi);
+    filt_insert(fs, lo, hi);
   }
   if (kind) {
     const uint32_t j = atomicAdd(&s_njob, 1u);
@@ -634,8 +632,8 @@ __global__ __launch_bounds__(64) void cache_lookup_kernel(HashTab g, const uint8
 }
 
 __global__ __launch_bounds__(64) void cache_enter_kernel(HashTab g, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
-                                                         uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint64_t key,
-                                                         const uint8_t* seg, int replace_only, int32_t* result) {
+                                                         FiltSet fs, uint64_t key, const uint8_t* seg,
+                                                         int replace_only, int32_t* result) {
   const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
   const uint64_t v = tab_lookup(g, lo, hi);
   if (v != ~0ull) {                          // present: replace the bytes
@@ -657,8 +655,7 @@ __global__ __launch_bounds__(64) void cache_enter_kernel(HashTab g, uint8_t* poo
   wave_copy2048(pool + (uint64_t)s * SEG, seg);
   if (lane_id() == 0) {
     tab_insert_min(g, lo, hi, s);
-    filt_insert(filt, lo, hi);
-    ftab_insert(ftab, fmask, lo, hi);
+    filt_insert(fs, lo, hi);
     *result = 0;
   }
 }
@@ -673,10 +670,11 @@ extern "C" int xcg_launch_cache_lookup(uint64_t* keys, uint64_t* vals, uint32_t 
 }
 
 extern "C" int xcg_launch_cache_enter(uint64_t* keys, uint64_t* vals, uint32_t mask, uint8_t* pool, uint32_t* nseg,
-                                      uint32_t seg_cap, uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint64_t key,
-                                      const uint8_t* seg, int replace_only, int32_t* result, hipStream_t s) {
+                                      uint32_t seg_cap, uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint32_t* gfilt,
+                                      uint32_t gmask, uint64_t key, const uint8_t* seg, int replace_only,
+                                      int32_t* result, hipStream_t s) {
   hipLaunchKernelGGL(xcg::cache_enter_kernel, dim3(1), dim3(64), 0, s, xcg::HashTab{keys, vals, mask}, pool, nseg,
-                     seg_cap, filt, ftab, fmask, key, seg, replace_only, result);
+                     seg_cap, xcg::FiltSet{filt, ftab, fmask, gfilt, gmask}, key, seg, replace_only, result);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -711,6 +709,8 @@ struct XcgDecodeArgs {
   uint32_t* g_filt;
   uint32_t* g_ftab;
   uint32_t fmask;
+  uint32_t* g_gfilt;
+  uint32_t gmask;
   uint64_t* x_keys;
   uint64_t* x_vals;
   uint64_t* x_latest;
@@ -817,7 +817,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
   const uint64_t slots = (uint64_t)a->x_mask + 1;
   hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, p,
-                     a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask);
+                     a->pool, a->nseg, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask});
   if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

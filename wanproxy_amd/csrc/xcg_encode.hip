@@ -27,6 +27,7 @@
 // (ESCAPE / EXTRACT / REF, xcodec_encoder.cc:276-372) are written by the whole
 // wave as they are resolved, into the chunk's output slot.
 #include <stddef.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -89,7 +90,9 @@ struct EncParams {
   uint32_t* ndecl;     // [n]
   uint32_t maxd;
   uint32_t* changed;   // lowest chunk whose declaration list differs from the last round (~0: none)
-  bool glb;            // lane filter non-empty: probe it
+  uint32_t lds_filter_keys;  // LDS lane filter up to this many keys, else the global one
+  const uint32_t* nseg;    // segments in the persistent cache
+  const uint32_t* bcount;  // [64] partial counts of the batch table's declarations (use_b)
   uint32_t skip_below; // chunks below this keep their last parse (their batch input is unchanged)
 };
 
@@ -280,33 +283,74 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
   return r;
 }
 
-// Stream-semantics probe of the persistent cache + batch declarations, pass 1
-// (inside the roll, LDS only): the key's blocked-Bloom word of the lane
-// filter (xcg_cache.h filt_word/filt_bits); a passing key is queued in the
-// wave's LDS scratch, slot min(passes, GSLOTS) of the lane (slot-major, so a
-// wave's 64 stores are consecutive dwords), and its bit set in pm.  Pass 2
-// (glb_verify) checks the queued keys against the fingerprint buckets in HBM
-// with all of a lane's loads in flight together, instead of one HBM round
-// trip per group of positions.
+// Stream-semantics probe of the persistent cache + batch declarations.
+// Pass 1 (inside the roll): the key's lane-filter word -- the blocked-Bloom
+// LDS filter (xcg_cache.h filt_*) or, for large caches, the global one
+// (gfilt_*); a passing key is queued in the wave's LDS scratch, slot
+// min(passes, GSLOTS) of the lane (slot-major, so a wave's 64 stores are
+// consecutive dwords), and its position bit set in pm.  Pass 2 (glb_flush,
+// after each half of the lane's 32 positions) checks the queued keys against
+// the 16-bit fingerprint buckets (an L2-resident table), all of a lane's
+// loads in flight together instead of one round trip per group of positions.
+// Passes beyond GSLOTS in one half are reported as events unchecked.
 constexpr int GSLOTS = 8;
+constexpr uint32_t LDS_FILTER_KEYS_DEFAULT = 220000;
 struct GlbQ {
   char* lds;        // LDS base of the workgroup's struct (offset 0)
-  uint32_t lfo;     // byte offset of the lane filter
-  uint32_t sa;      // this lane's next scratch slot address (absolute LDS byte address)
+  uint32_t lfo;     // byte offset of the lane filter (FM 1)
+  const uint32_t* gf;   // global lane filter (FM 2)
+  uint32_t gmask;
+  const u32x4* ftab;    // fingerprint buckets
+  uint32_t fmask;
+  uint32_t sa0;     // this lane's scratch slot 0 (absolute LDS byte address)
+  uint32_t sa;      // its next slot
   uint32_t salim;   // its garbage slot (slot GSLOTS)
-  uint32_t pm;      // filter passes, bit per position (built reversed, like ev)
+  uint32_t pm;      // filter passes of the current half, bit j = position j
+  uint32_t gev;     // verified cache / batch hits, bit j = position j
 };
+
+// Pass 2 over the queued keys of the current half; resets the queue.
+__device__ __forceinline__ void glb_flush(GlbQ& gq) {
+  const uint32_t cnt = (gq.sa - gq.sa0) >> 8;
+  uint32_t rem = gq.pm;
+#pragma unroll
+  for (int i0 = 0; i0 < GSLOTS; i0 += 4) {
+    if (ballot(cnt > (uint32_t)i0) == 0) break;
+    uint32_t kk[4];
+    u32x4 q[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kk[t] = *(const uint32_t*)(gq.lds + gq.sa0 + 256u * (i0 + t));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      q[t] = u32x4{0u, 0u, 0u, 0u};
+      if ((uint32_t)(i0 + t) < cnt) q[t] = gq.ftab[fbucket(kk[t], gq.fmask)];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if ((uint32_t)(i0 + t) < cnt) {
+        const uint32_t j = (uint32_t)__builtin_ctz(rem);
+        rem &= rem - 1u;
+        gq.gev |= (uint32_t)ftab_match(q[t], kk[t]) << j;
+      }
+    }
+  }
+  gq.gev |= rem;
+  gq.pm = 0;
+  gq.sa = gq.sa0;
+}
 
 // Roll the probe key over the lane's 32 positions; bit j of the result is set
 // when position q0 + j is a possible cache hit.  NX1 = -X1, NX2 = -(X2 + CLO)
 // at q0 (RollingHash::roll, xcodec_hash.h:57-70, negated), so K = -lo costs one
 // instruction.  C0: the pending candidate (key c0k) is not in the table yet and
 // becomes visible at piece offset rvis (position p + rvis).  OVF: also compare the (rare) overflow
-// keys ovk[8].  GLB: also run pass 1 of the persistent cache / batch probe (gq).
-template <int LOGNB, bool C0, int NOVF, bool GLB>
+// keys ovk[8].  FM: also run pass 1 of the persistent cache / batch probe (gq)
+// through the LDS lane filter (1) or the global one (2); 0: no such probe.
+template <int LOGNB, bool C0, int NOVF, int FM>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
                                                uint32_t kofs, uint32_t c0k, int rvis, const uint32_t* ovk,
                                                GlbQ& gq) {
+  constexpr bool GLB = FM != 0;
   // bucket mask in a VGPR so that (K & KM) | kofs is one v_and_or_b32 (VOP3
   // takes no literal and one SGPR on gfx9)
   const uint32_t KM = (uint32_t)opaque((int)(((1u << LOGNB) - 1u) << 3));
@@ -345,9 +389,12 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(kblk + ((kv[t] & KM) | kofs));
-    if (GLB) {
+    if (FM == 1) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) fw[t] = *(const uint32_t*)(gq.lds + gq.lfo + filt_word_ofs(kv[t]));
+    } else if (FM == 2) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fw[t] = gq.gf[gfilt_word(kv[t], gq.gmask)];
     }
   };
   uint32_t kc[4], fc[4];
@@ -362,10 +409,10 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
       // Persistent cache + batch declarations, pass 1: queue filter passes.
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const uint32_t p = filt_test(fc[t], kc[t]);
+        const uint32_t p = FM == 1 ? filt_test(fc[t], kc[t]) : gfilt_test(fc[t], kc[t]);
         *(uint32_t*)(gq.lds + gq.sa) = kc[t];
         gq.sa = min(gq.sa + (p << 8), gq.salim);
-        gq.pm = (gq.pm << 1) | p;
+        gq.pm |= p << (4 * g + t);
       }
     }
 #pragma unroll
@@ -379,48 +426,13 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     }
     asm volatile("" : "+v"(ev));   // materialise this group's bits before the next group
     __builtin_amdgcn_sched_barrier(0);
+    if (GLB && (g == 3 || g == 7)) glb_flush(gq);
     if (g < 7) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) { kc[t] = kn[t]; ec[t] = en[t]; fc[t] = fn[t]; }
     }
   }
-  if (GLB) gq.pm = __builtin_bitreverse32(gq.pm);
-  return __builtin_bitreverse32(ev);   // position j was shifted in at bit 31 - j
-}
-
-// Pass 2 of the stream probe: the lane's queued keys (slots [0, cnt) from
-// sa0) against the fingerprint buckets in HBM, four loads in flight per lane
-// per batch.  The i-th queued key is the i-th set bit of pm (queued in
-// position order).  Passes beyond GSLOTS are reported as events unchecked;
-// the resolver decides them exactly.
-__device__ __forceinline__ uint32_t glb_verify(uint32_t ev, const GlbQ& gq, uint32_t sa0, const u32x4* ftab,
-                                               uint32_t fmask) {
-  const uint32_t cnt = (gq.sa - sa0) >> 8;
-  uint32_t rem = gq.pm;
-#pragma unroll
-  for (int i0 = 0; i0 < GSLOTS; i0 += 4) {
-    if (ballot(cnt > (uint32_t)i0) == 0) break;
-    uint32_t kk[4];
-    u32x4 q[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) kk[t] = *(const uint32_t*)(gq.lds + sa0 + 256u * (i0 + t));
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      q[t] = u32x4{0u, 0u, 0u, 0u};
-      if ((uint32_t)(i0 + t) < cnt) q[t] = ftab[fbucket(kk[t], fmask)];
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if ((uint32_t)(i0 + t) < cnt) {
-        const uint32_t j = (uint32_t)__builtin_ctz(rem);
-        rem &= rem - 1u;
-        const uint32_t fp = kk[t] | 1u;
-        const bool m = q[t][0] == fp || q[t][1] == fp || q[t][2] == fp || q[t][3] == FOVF;
-        ev |= (uint32_t)m << j;
-      }
-    }
-  }
-  return ev | rem;
+  return __builtin_bitreverse32(ev) | (GLB ? gq.gev : 0u);   // ev: position j was shifted in at bit 31 - j
 }
 
 // ------------------------------------------------------------------ kernel
@@ -445,12 +457,12 @@ __device__ __forceinline__ void progress_priority(int s, int L) {
 // probed through the workgroup's LDS filter lfilt.
 // What a stream wave probes besides its own table: the workgroup's LDS (base
 // = offset 0), where the lane filter sits (lfo), the wave's pass-1 scratch
-// (sofs), and whether the filter holds anything (glb; else pass 1 is skipped).
+// (sofs), and which filter pass 1 reads (fmode; 0 = the filter holds nothing).
 struct GlbView {
   char* lds;
   uint32_t lfo;
   uint32_t sofs;
-  bool glb;
+  int fmode;   // 0: no probe, 1: LDS lane filter, 2: global lane filter
 };
 
 template <int LOGNB, int MAXD, bool STREAM>
@@ -551,6 +563,29 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     return found;
   };
 
+  // Segment bytes of a hash in the persistent cache or, declared by an
+  // earlier chunk of the batch, in the batch input (nullptr if neither).
+  auto cache_src = [&](uint32_t lo, uint32_t hi) -> const uint8_t* {
+    const uint64_t gv = tab_lookup(prm.g, lo, hi);
+    if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+    if (prm.use_b) {
+      const uint64_t bv = tab_lookup(prm.b, lo, hi);
+      if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) return prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
+    }
+    return nullptr;
+  };
+  // Could the cache or the batch hold probe key k?  (lane filter, then the
+  // fingerprint bucket; no false negatives)
+  auto glb_maybe = [&](uint32_t k) -> bool {
+    if (gs.fmode == 0) return false;
+    uint32_t pass;
+    if (gs.fmode == 1) pass = filt_test(*(const uint32_t*)(gs.lds + gs.lfo + filt_word_ofs(k)), k);
+    else pass = gfilt_test(prm.lf.gfilt[gfilt_word(k, prm.lf.gmask)], k);
+    if (readfirst(pass) == 0u) return false;
+    return readfirst((uint32_t)ftab_match(prm.lf.ftab[fbucket(k, prm.lf.fmask)], k)) != 0u;
+  };
+  bool chain = false;                              // the last op was a REF
+
   // encode_declaration (xcodec_encoder.cc:276-313).
   auto declare = [&]() {
     if (cand > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)cand);
@@ -623,6 +658,38 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
     }
 
+    // ---- REF chaining (stream semantics).  The previous piece ended with a
+    // REF, so this piece starts at the parse point with no candidate pending;
+    // in REF-dense streams (warm caches, duplicated runs) the window there is
+    // usually the next REF.  Probe it exactly (lookup, find_reference
+    // xcodec_encoder.cc:374-416) before rolling 2048 positions; a miss goes
+    // through the filters only, and a miss or a collision falls through to
+    // the ordinary vector phase, which decides position s itself.
+    if (STREAM && chain && !nullcache) {
+      chain = false;
+      uint32_t lo, hi;
+      if (s == p) {
+        lo = 0u - readfirst(k0);
+        hi = readfirst(lane_window_hi(P, 0));
+      } else {
+        const uint2 h = window_hash_u(x + s);
+        lo = h.x; hi = h.y;
+      }
+      const int d = lookup(lo, hi);                 // stream records carry their hi
+      const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
+      if (src == nullptr && glb_maybe(probe_key(lo))) src = cache_src(lo, hi);
+      if (src != nullptr && equal2048_u(src, x + s)) {
+        wave_put_ref(out + olen, lo, hi);           // encode_reference :342-372
+        olen += 10;
+        ++n_ref;
+        base = s + SEG;
+        s = base;
+        chain = true;
+        totXA = totXB; totTA = totTB;               // (as at the end of a piece)
+        continue;
+      }
+    }
+
     // ---- vector phase
     uint32_t ev = 0;
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
@@ -643,7 +710,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #pragma unroll
       for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
       const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
-      GlbQ gq{gs.lds, gs.lfo, sa0, sa0 + 256u * GSLOTS, 0u};
+      GlbQ gq{gs.lds, gs.lfo, prm.lf.gfilt, prm.lf.gmask, prm.lf.ftab, prm.lf.fmask, sa0, sa0, sa0 + 256u * GSLOTS,
+              0u, 0u};
       // G = probe the persistent cache / batch declarations too
       auto roll = [&](auto c0t, auto novft, auto glbt) {
         return roll_probe<LOGNB, decltype(c0t)::value, decltype(novft)::value, decltype(glbt)::value>(
@@ -660,11 +728,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // duplicates of a real overflow key pad the unused slots
         return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
       };
-      if (STREAM && gs.glb) {
-        ev = by_novf(std::integral_constant<bool, STREAM>{});
-        ev = glb_verify(ev, gq, sa0, prm.lf.ftab, prm.lf.fmask);
+      if (STREAM && gs.fmode == 1) {
+        ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
+      } else if (STREAM && gs.fmode == 2) {
+        ev = by_novf(std::integral_constant<int, STREAM ? 2 : 0>{});
       } else {
-        ev = by_novf(T0{});
+        ev = by_novf(std::integral_constant<int, 0>{});
       }
       // positions past the last window are not positions (branch-free mask)
       const int nvalid = pe - q0;
@@ -722,16 +791,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // Where the hash is declared: this chunk (d), the persistent cache, or
         // an earlier chunk of the batch.  src = that segment's bytes.
         const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
-        if (STREAM && src == nullptr) {
-          const uint64_t gv = tab_lookup(prm.g, lo, hi);
-          if (gv != ~0ull) {
-            src = prm.pool + gv * (uint64_t)SEG;
-          } else if (prm.use_b) {
-            const uint64_t bv = tab_lookup(prm.b, lo, hi);
-            if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk)
-              src = prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
-          }
-        }
+        if (STREAM && src == nullptr) src = cache_src(lo, hi);
         if (src != nullptr) {
           if (equal2048_u(src, x + s)) {
             if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
@@ -743,6 +803,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
             s = base;
             have_cand = false;                                // :208
             c0_in_table = true;
+            chain = true;
             continue;
           }
           ++n_coll;                                           // collision, :390-406 / :215-216
@@ -827,7 +888,7 @@ __global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams pr
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
   if (chunk >= prm.n) return;
   encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk,
-                                   GlbView{nullptr, 0u, 0u, false});
+                                   GlbView{nullptr, 0u, 0u, 0});
 }
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
@@ -836,14 +897,19 @@ template <int LOGNB, int MAXD, int SW>
 __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   using L = StreamLDS<LOGNB, MAXD, SW>;
   __shared__ L S;
-  if (prm.glb) {
+  // Which lane filter the cache + batch declarations fit: the 64 KiB LDS one
+  // up to LDS_FILTER_KEYS keys (FP <~10 %), else the global one.
+  uint32_t keys = readfirst(*prm.nseg);
+  if (prm.use_b) keys += readfirst(wave_sum(prm.bcount[lane_id()]));
+  const int fmode = keys == 0 ? 0 : (keys <= prm.lds_filter_keys ? 1 : 2);
+  if (fmode == 1) {
     for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
       ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
   }
   __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
   const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
-                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), prm.glb};
+                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode};
   const uint32_t stride = gridDim.x * SW;
   for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
@@ -884,15 +950,17 @@ namespace xcg {
 // round's lane filter = the persistent cache's filter + B.  One thread per
 // (chunk, declaration).
 __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
-                                                                uint32_t maxd, HashTab b, uint32_t* filt,
-                                                                uint32_t* ftab, uint32_t fmask, int32_t* status) {
+                                                                uint32_t maxd, HashTab b, FiltSet fs, uint32_t* bcount,
+                                                                int32_t* status) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = (uint32_t)(i / maxd), k = (uint32_t)(i % maxd);
-  if (c >= n || k >= ndecl[c]) return;
+  const bool have = c < n && k < ndecl[c];
+  const uint64_t m = ballot(have);
+  if (lane_id() == 0 && m) atomicAdd(bcount + ((i >> 6) & 63u), (uint32_t)__builtin_popcountll(m));
+  if (!have) return;
   const uint4 d = decl[i];
   if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
-  filt_insert(filt, d.x, d.y);
-  ftab_insert(ftab, fmask, d.x, d.y);
+  filt_insert(fs, d.x, d.y);
 }
 
 // Commit the converged declarations into the persistent cache
@@ -903,7 +971,7 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
 __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                      uint32_t maxd, const uint8_t* in, const uint64_t* chunk_off,
                                                      HashTab g, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
-                                                     uint32_t* filt, uint32_t* ftab, uint32_t fmask, int32_t* status) {
+                                                     FiltSet fs, int32_t* status) {
   __shared__ uint32_t s_base;
   const uint32_t parts = (maxd + 255) / 256;
   const uint32_t c = blockIdx.x / parts, k0 = (blockIdx.x % parts) * 256u;
@@ -921,8 +989,7 @@ __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const ui
       atomicOr(status, 4);
     } else {
       if (!tab_insert_min(g, d.x, d.y, seg)) atomicOr(status, 2);
-      filt_insert(filt, d.x, d.y);
-      ftab_insert(ftab, fmask, d.x, d.y);
+      filt_insert(fs, d.x, d.y);
     }
   }
   // the block's segments are s_base + (0 .. cnt), in declaration order
@@ -973,7 +1040,10 @@ struct XcgStreamArgs {
   uint32_t maxd;
   uint32_t* changed;
   uint32_t* h_changed;   // pinned host word
-  int g_empty;           // the persistent cache is known to be empty
+  uint32_t* g_gfilt;     // global lane filters: the cache's and the round's copy
+  uint32_t* r_gfilt;
+  uint32_t gmask;
+  uint32_t* bcount;      // [64]
 };
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
@@ -988,12 +1058,20 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.ndecl = a->ndecl;
   prm.maxd = a->maxd;
   prm.changed = a->changed;
+  prm.nseg = a->nseg;
+  prm.bcount = a->bcount;
+  static const uint32_t lfk = [] {   // tuning knob (diagnostics): XCG_LDS_FILTER_KEYS
+    const char* e = getenv("XCG_LDS_FILTER_KEYS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : LDS_FILTER_KEYS_DEFAULT;
+  }();
+  prm.lds_filter_keys = lfk;
   const size_t fbytes = (size_t)FILT_WORDS * 4, tbytes = ((size_t)a->fmask + 1) * 16;
+  const size_t gbytes = ((size_t)a->gmask + 1) * 4;
   int dev = 0;
   hipDeviceProp_t props;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&props, dev) != hipSuccess) return -5;
   const uint32_t wgs = (uint32_t)props.multiProcessorCount;
-  const bool big = a->maxd > 72;                     // chunks > 128 KiB (<= 512 KiB frames)
+  const bool big = a->maxd > 72;                     // chunks > 128 KiB (<= 512 KiB frames): 264 records
   const uint32_t SW = big ? 6 : 16;               // one workgroup per CU (LDS)
   const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
   auto launch = [&]() {
@@ -1013,9 +1091,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     return -5;
   // Round 0: every chunk against the persistent cache + its own declarations.
   prm.use_b = false;
-  prm.glb = !a->g_empty;
   prm.skip_below = 0;
-  prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask};
+  prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask, a->g_gfilt, a->gmask};
   launch();
   int rounds = 1;
   uint32_t fc = 0;
@@ -1031,16 +1108,17 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
         hipMemsetAsync(a->b_vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
         hipMemcpyAsync(a->r_filt, a->g_filt, fbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(a->r_ftab, a->g_ftab, tbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+        hipMemcpyAsync(a->r_gfilt, a->g_gfilt, gbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+        hipMemsetAsync(a->bcount, 0, 4 * 64, stream) != hipSuccess ||
         hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
       return -5;
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
-                       (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, prm.b, a->r_filt, a->r_ftab,
-                       a->fmask, a->status);
+                       (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, prm.b,
+                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
     prm.use_b = true;
-    prm.glb = true;
     prm.skip_below = fc + 1;
-    prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask};
+    prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     launch();
     ++rounds;
     if (!changed_after(fc)) return -5;
@@ -1048,7 +1126,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const uint32_t parts = (a->maxd + 255) / 256;
   hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream,
                      (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, a->in, a->chunk_off,
-                     prm.g, a->pool, a->nseg, a->seg_cap, a->g_filt, a->g_ftab, a->fmask, a->status);
+                     prm.g, a->pool, a->nseg, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask},
+                     a->status);
   if (rounds_out) *rounds_out = rounds;
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
