@@ -177,6 +177,12 @@ int xcg_pack_outputs(xcg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_o
  * in an earlier asynchronous call).  Synchronises the context's device. */
 int xcg_ctx_status(xcg_ctx *ctx);
 
+/* Diagnostics / tests: stream-semantics batches probe the cache through a
+ * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,
+ * else through a global (L2-resident) one; both give the same output.
+ * Returns the previous threshold (default 220000, or XCG_LDS_FILTER_KEYS). */
+uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
+
 /* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for
  * s in [0, len - 2048]. */
 int xcg_window_hashes(xcg_ctx *ctx, const uint8_t *d_x, uint64_t len, uint64_t *d_hash, void *stream);

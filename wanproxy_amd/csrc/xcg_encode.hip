@@ -1046,6 +1046,17 @@ struct XcgStreamArgs {
   uint32_t* bcount;      // [64]
 };
 
+// LDS / global lane filter threshold (keys): XCG_LDS_FILTER_KEYS at load
+// time, or xcg_debug_set_lds_filter_keys (tests force either mode with it).
+static uint32_t g_lds_filter_keys = [] {
+  const char* e = getenv("XCG_LDS_FILTER_KEYS");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : xcg::LDS_FILTER_KEYS_DEFAULT;
+}();
+static uint32_t xcg_lds_filter_keys() { return __atomic_load_n(&g_lds_filter_keys, __ATOMIC_RELAXED); }
+extern "C" uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys) {
+  return __atomic_exchange_n(&g_lds_filter_keys, keys, __ATOMIC_RELAXED);
+}
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
   using namespace xcg;
   const uint32_t n = a->n;
@@ -1060,11 +1071,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.changed = a->changed;
   prm.nseg = a->nseg;
   prm.bcount = a->bcount;
-  static const uint32_t lfk = [] {   // tuning knob (diagnostics): XCG_LDS_FILTER_KEYS
-    const char* e = getenv("XCG_LDS_FILTER_KEYS");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : LDS_FILTER_KEYS_DEFAULT;
-  }();
-  prm.lds_filter_keys = lfk;
+  prm.lds_filter_keys = xcg_lds_filter_keys();
   const size_t fbytes = (size_t)FILT_WORDS * 4, tbytes = ((size_t)a->fmask + 1) * 16;
   const size_t gbytes = ((size_t)a->gmask + 1) * 4;
   int dev = 0;

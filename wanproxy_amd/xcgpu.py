@@ -83,6 +83,8 @@ def lib():
     L.xcg_window_hashes.restype = C.c_int
     L.xcg_segment_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
     L.xcg_segment_hashes.restype = C.c_int
+    L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
+    L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     _lib = L
     return L
 
