@@ -54,6 +54,17 @@ struct XcgStreamArgs {
   uint32_t* r_gfilt;
   uint32_t gmask;
   uint32_t* bcount;
+  uint64_t* b2_keys;
+  uint64_t* b2_vals;
+  uint64_t* r_keys;
+  uint64_t* r_vals;
+  uint32_t r_mask;
+  uint64_t* hits;
+  uint32_t* nhits;
+  uint32_t maxh;
+  uint32_t* need;
+  uint32_t* vflags;
+  uint32_t* h_vflags;
 };
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
@@ -137,6 +148,19 @@ struct BatchScratch {
   uint32_t* h_changed = nullptr;   // pinned
   uint32_t* r_gfilt = nullptr;
   uint32_t* bcount = nullptr;
+  // verification between rounds
+  uint64_t* b2_keys = nullptr;     // second batch table (same mask)
+  uint64_t* b2_vals = nullptr;
+  uint64_t* r_keys = nullptr;      // changed hashes -> chunk range
+  uint64_t* r_vals = nullptr;
+  uint32_t r_mask = 0;
+  uint64_t* hits = nullptr;        // n_cap * maxh batch hits
+  uint32_t* nhits = nullptr;
+  uint32_t maxh = 0;
+  uint32_t* need = nullptr;
+  uint32_t* vflags = nullptr;
+  uint32_t* h_vflags = nullptr;    // pinned
+  uint32_t last_maxd = 0;          // declaration stride of the last stream batch
 };
 
 struct DecodeScratch {
@@ -209,6 +233,9 @@ void free_scratch(BatchScratch& b) {
   (void)hipFree(b.b_keys); (void)hipFree(b.b_vals); (void)hipFree(b.r_filt); (void)hipFree(b.r_ftab);
   (void)hipFree(b.decl); (void)hipFree(b.ndecl); (void)hipFree(b.changed); (void)hipFree(b.r_gfilt);
   (void)hipFree(b.bcount);
+  (void)hipFree(b.b2_keys); (void)hipFree(b.b2_vals); (void)hipFree(b.r_keys); (void)hipFree(b.r_vals);
+  (void)hipFree(b.hits); (void)hipFree(b.nhits); (void)hipFree(b.need); (void)hipFree(b.vflags);
+  if (b.h_vflags) (void)hipHostFree(b.h_vflags);
   if (b.h_changed) (void)hipHostFree(b.h_changed);
   b = BatchScratch{};
 }
@@ -255,12 +282,19 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
   b.maxd = maxd;
   const uint32_t cap = pow2_at_least(2ull * n * maxd + 1024);
   b.b_mask = cap - 1;
+  b.r_mask = 2 * cap - 1;          // union of two rounds' hashes
+  b.maxh = maxd + 8;
   if (hipMalloc(&b.b_keys, 8ull * cap) != hipSuccess || hipMalloc(&b.b_vals, 8ull * cap) != hipSuccess ||
       hipMalloc(&b.r_filt, 4ull * FILT_WORDS) != hipSuccess ||
       hipMalloc(&b.r_ftab, 16ull * (c->g.fmask + 1)) != hipSuccess ||
       hipMalloc(&b.decl, 16ull * n * maxd) != hipSuccess || hipMalloc(&b.ndecl, 4ull * n) != hipSuccess ||
       hipMalloc(&b.changed, 16) != hipSuccess || hipHostMalloc(&b.h_changed, 16) != hipSuccess ||
-      hipMalloc(&b.r_gfilt, 4ull * (c->g.gmask + 1)) != hipSuccess || hipMalloc(&b.bcount, 4 * 64) != hipSuccess) {
+      hipMalloc(&b.r_gfilt, 4ull * (c->g.gmask + 1)) != hipSuccess || hipMalloc(&b.bcount, 4 * 64) != hipSuccess ||
+      hipMalloc(&b.b2_keys, 8ull * cap) != hipSuccess || hipMalloc(&b.b2_vals, 8ull * cap) != hipSuccess ||
+      hipMalloc(&b.r_keys, 16ull * cap) != hipSuccess || hipMalloc(&b.r_vals, 16ull * cap) != hipSuccess ||
+      hipMalloc(&b.hits, 8ull * n * (maxd + 8)) != hipSuccess || hipMalloc(&b.nhits, 4ull * n) != hipSuccess ||
+      hipMalloc(&b.need, 4ull * n) != hipSuccess || hipMalloc(&b.vflags, 16) != hipSuccess ||
+      hipHostMalloc(&b.h_vflags, 16) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
@@ -460,7 +494,7 @@ int xcg_last_declarations(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t
   const uint32_t k = nd < cap ? nd : cap;
   if (k == 0) return XCG_OK;
   std::vector<uint32_t> buf(4ull * k);
-  if (hipMemcpy(buf.data(), (const uint8_t*)c->bs.decl + 16ull * chunk * c->bs.maxd, 16ull * k,
+  if (hipMemcpy(buf.data(), (const uint8_t*)c->bs.decl + 16ull * chunk * c->bs.last_maxd, 16ull * k,
                 hipMemcpyDeviceToHost) != hipSuccess)
     return XCG_EHIP;
   for (uint32_t i = 0; i < k; ++i) {
@@ -508,11 +542,14 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
     int rc = ensure_cache(c);
     if (rc == XCG_OK) rc = ensure_scratch(c, n, maxd);
     if (rc != XCG_OK) return rc;
+    c->bs.last_maxd = maxd;
     XcgStreamArgs a{d_in, d_chunk_off, d_chunk_len, n, c->flags, d_out, d_out_off, d_out_len, d_stats,
                     c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                     c->g.filt, c->g.ftab, c->g.fmask, c->bs.b_keys, c->bs.b_vals, c->bs.b_mask,
                     c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
-                    c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount};
+                    c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount, c->bs.b2_keys, c->bs.b2_vals,
+                    c->bs.r_keys, c->bs.r_vals, c->bs.r_mask, c->bs.hits, c->bs.nhits, c->bs.maxh, c->bs.need,
+                    c->bs.vflags, c->bs.h_vflags};
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
     c->last_rounds = rounds;

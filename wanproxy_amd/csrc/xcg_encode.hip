@@ -94,6 +94,10 @@ struct EncParams {
   const uint32_t* nseg;    // segments in the persistent cache
   const uint32_t* bcount;  // [64] partial counts of the batch table's declarations (use_b)
   uint32_t skip_below; // chunks below this keep their last parse (their batch input is unchanged)
+  const uint32_t* need;  // (verification rounds) parse only chunks with need[c] != 0
+  uint64_t* hits;      // [n * maxh] hashes the chunk found among the batch declarations (REF or collision)
+  uint32_t* nhits;     // [n] (> maxh: overflowed, always re-parsed)
+  uint32_t maxh;
 };
 
 // ------------------------------------------------------------------ emission
@@ -565,12 +569,19 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 
   // Segment bytes of a hash in the persistent cache or, declared by an
   // earlier chunk of the batch, in the batch input (nullptr if neither).
+  // A batch hit is recorded: the verification after the round re-parses the
+  // chunk if that declaration's visibility or bytes change (xcg_verify_*).
+  uint32_t nh = 0;
   auto cache_src = [&](uint32_t lo, uint32_t hi) -> const uint8_t* {
     const uint64_t gv = tab_lookup(prm.g, lo, hi);
     if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
     if (prm.use_b) {
       const uint64_t bv = tab_lookup(prm.b, lo, hi);
-      if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) return prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
+      if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) {
+        if (nh < prm.maxh && l == 0) prm.hits[(uint64_t)chunk * prm.maxh + nh] = ((uint64_t)hi << 32) | lo;
+        ++nh;
+        return prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
+      }
     }
     return nullptr;
   };
@@ -857,7 +868,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       dl[k] = nv;
     }
     if (ballot(diff) != 0 && l == 0) atomicMin(prm.changed, chunk);
-    if (l == 0) prm.ndecl[chunk] = ndecl;
+    if (l == 0) {
+      prm.ndecl[chunk] = ndecl;
+      prm.nhits[chunk] = nh;
+    }
   }
   if (l == 0) {
     prm.out_len[chunk] = olen;
@@ -913,6 +927,7 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   const uint32_t stride = gridDim.x * SW;
   for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
+    if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;   // verified: its parse stands
     encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
   }
 }
@@ -961,6 +976,76 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   const uint4 d = decl[i];
   if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
   filt_insert(fs, d.x, d.y);
+}
+
+// ------------------------------------------------ verification of a round
+//
+// Round r parsed chunk k against V = the batch table of round r-1's
+// declarations; T = the table of round r's.  k's parse depends on the batch
+// only through its lookups, so it stands under T unless, for some hash h,
+// (a) h becomes visible to k (earliest declaring chunk c_T < k <= c_V: a miss
+//     may turn into a hit) -- flagged conservatively for every k > c_T; or
+// (b) k found h in V (a recorded hit) and under T h is invisible to k, or its
+//     earliest declaration has other bytes.
+// The fixed point is reached when no chunk is flagged.
+__device__ __forceinline__ bool v4_ne(u32x4 a, u32x4 b) { return a[0] != b[0] || a[1] != b[1] || a[2] != b[2] || a[3] != b[3]; }
+__device__ __forceinline__ bool seg_equal_t(const uint8_t* a, const uint8_t* b) {   // one thread, 2048 bytes
+  for (int i = 0; i < SEG; i += 16)
+    if (v4_ne(*(const u32x4_u*)(a + i), *(const u32x4_u*)(b + i))) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt, const uint8_t* in,
+                                                          const uint64_t* chunk_off, HashTab rt, uint32_t* a_first,
+                                                          int32_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)tt.mask + 1, nv = (uint64_t)tv.mask + 1;
+  uint64_t h, vt, vv;
+  if (i < nt) {
+    h = tt.keys[i];
+    if (h == EMPTY_KEY) return;
+    vt = tt.vals[i];
+    vv = tab_lookup_t(tv, (uint32_t)h, (uint32_t)(h >> 32));
+  } else if (i < nt + nv) {
+    h = tv.keys[i - nt];
+    if (h == EMPTY_KEY) return;
+    if (tab_lookup_t(tt, (uint32_t)h, (uint32_t)(h >> 32)) != ~0ull) return;   // seen from T's side
+    vt = ~0ull;
+    vv = tv.vals[i - nt];
+  } else {
+    return;
+  }
+  if (vt == vv) return;
+  const uint32_t INF = 0xFFFFFFFFu;
+  const uint32_t ct = vt == ~0ull ? INF : (uint32_t)(vt >> 32), cv = vv == ~0ull ? INF : (uint32_t)(vv >> 32);
+  if (ct < cv) atomicMin(a_first, ct + 1);                                   // (a)
+  bool same = false;
+  if (vt != ~0ull && vv != ~0ull)
+    same = seg_equal_t(in + chunk_off[ct] + (uint32_t)vt, in + chunk_off[cv] + (uint32_t)vv);
+  // (b): chunks in (cv, ct] lose h; with other bytes, every chunk > min(cv, ct) that found h
+  uint32_t rlo = INF, rhi = 0;
+  if (cv < ct) { rlo = cv + 1; rhi = ct == INF ? INF - 1 : ct; }
+  if (!same && ct != INF && cv != INF) { rlo = min(rlo, min(ct, cv) + 1); rhi = INF - 1; }
+  if (rlo <= rhi && !tab_insert_min(rt, (uint32_t)h, (uint32_t)(h >> 32), ((uint64_t)rlo << 32) | rhi))
+    atomicOr(status, 2);
+}
+
+// need[k] for every chunk: (a), an overflowed hit list, or a recorded hit in a
+// changed range (b).  One thread per chunk.
+__global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uint64_t* hits, const uint32_t* nhits,
+                                                           uint32_t maxh, HashTab rt, const uint32_t* a_first,
+                                                           uint32_t* need, uint32_t* any) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t nk = nhits[k];
+  bool f = k >= *a_first || nk > maxh;
+  for (uint32_t i = 0; i < nk && !f; ++i) {
+    const uint64_t h = hits[(uint64_t)k * maxh + i];
+    const uint64_t r = tab_lookup_t(rt, (uint32_t)h, (uint32_t)(h >> 32));
+    f = r != ~0ull && k >= (uint32_t)(r >> 32) && k <= (uint32_t)r;
+  }
+  need[k] = f ? 1u : 0u;
+  if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
 }
 
 // Commit the converged declarations into the persistent cache
@@ -1044,6 +1129,19 @@ struct XcgStreamArgs {
   uint32_t* r_gfilt;
   uint32_t gmask;
   uint32_t* bcount;      // [64]
+  // verification: a second batch table (tables alternate between rounds), the
+  // changed-hash table, per-chunk batch hits, flags
+  uint64_t* b2_keys;
+  uint64_t* b2_vals;
+  uint64_t* r_keys;
+  uint64_t* r_vals;
+  uint32_t r_mask;
+  uint64_t* hits;
+  uint32_t* nhits;
+  uint32_t maxh;
+  uint32_t* need;
+  uint32_t* vflags;      // [0] a_first, [1] any
+  uint32_t* h_vflags;    // pinned
 };
 
 // LDS / global lane filter threshold (keys): XCG_LDS_FILTER_KEYS at load
@@ -1094,8 +1192,13 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     return true;
   };
   if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess ||
+      hipMemsetAsync(a->nhits, 0, 4ull * n, stream) != hipSuccess ||
       hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
     return -5;
+  prm.need = nullptr;
+  prm.hits = a->hits;                              // every stream round writes nhits[chunk]
+  prm.nhits = a->nhits;
+  prm.maxh = a->maxh;
   // Round 0: every chunk against the persistent cache + its own declarations.
   prm.use_b = false;
   prm.skip_below = 0;
@@ -1106,29 +1209,65 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   if (!changed_after(fc)) return -5;
   // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
   // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
-  // chunk k after round k; a round that changes no declaration list is the
-  // fixed point, which is the sequential result.  Chunks up to the lowest one
-  // whose list changed in the previous round see the same batch input as then
-  // and keep their parse.  (Round 0's lists are compared with empty ones.)
-  for (uint32_t r = 1; n > 1 && r <= n && fc != ~0u; ++r) {
-    if (hipMemsetAsync(a->b_keys, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
-        hipMemsetAsync(a->b_vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
+  // chunk k after round k.  Round 1 re-parses every chunk after the first
+  // that declared anything in round 0 (those before it saw an empty batch);
+  // after each later round the verification (verify_*_kernel) compares the
+  // round's batch table with the one the round parsed against and flags the
+  // chunks whose lookups could change; only those are re-parsed.  No flag =
+  // the fixed point, which is the sequential result.
+  HashTab tabs[2] = {HashTab{a->b_keys, a->b_vals, a->b_mask}, HashTab{a->b2_keys, a->b2_vals, a->b_mask}};
+  const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
+  int cur = 0;
+  auto build = [&](int t) -> bool {
+    if (hipMemsetAsync(tabs[t].keys, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
+        hipMemsetAsync(tabs[t].vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
         hipMemcpyAsync(a->r_filt, a->g_filt, fbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(a->r_ftab, a->g_ftab, tbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(a->r_gfilt, a->g_gfilt, gbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
-        hipMemsetAsync(a->bcount, 0, 4 * 64, stream) != hipSuccess ||
-        hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
-      return -5;
+        hipMemsetAsync(a->bcount, 0, 4 * 64, stream) != hipSuccess)
+      return false;
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
-                       (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, prm.b,
+                       (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, tabs[t],
                        FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
+    return true;
+  };
+  if (n > 1 && fc != ~0u) {
+    if (!build(cur) || hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
     prm.use_b = true;
+    prm.b = tabs[cur];
     prm.skip_below = fc + 1;
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     launch();
     ++rounds;
     if (!changed_after(fc)) return -5;
+    prm.skip_below = 0;
+    for (uint32_t r = 2; r <= n + 1 && fc != ~0u; ++r) {
+      // verify round r-1 (parsed against tabs[cur]) against its own declarations
+      const int nxt = cur ^ 1;
+      if (!build(nxt) || hipMemsetAsync(a->r_keys, 0xFF, 8ull * (a->r_mask + 1), stream) != hipSuccess ||
+          hipMemsetAsync(a->r_vals, 0xFF, 8ull * (a->r_mask + 1), stream) != hipSuccess ||
+          hipMemsetAsync(a->vflags, 0xFF, 4, stream) != hipSuccess ||
+          hipMemsetAsync(a->vflags + 1, 0, 4, stream) != hipSuccess)
+        return -5;
+      const uint64_t slots = 2ull * (a->b_mask + 1);
+      hipLaunchKernelGGL(verify_diff_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, tabs[cur],
+                         tabs[nxt], a->in, a->chunk_off, rt, a->vflags, a->status);
+      hipLaunchKernelGGL(verify_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n,
+                         (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt,
+                         (const uint32_t*)a->vflags, a->need, a->vflags + 1);
+      if (hipMemcpyAsync(a->h_vflags, a->vflags, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess)
+        return -5;
+      if (a->h_vflags[1] == 0) break;                  // nothing flagged: fixed point
+      if (hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
+      cur = nxt;
+      prm.b = tabs[cur];
+      prm.need = a->need;
+      launch();
+      ++rounds;
+      if (!changed_after(fc)) return -5;
+    }
   }
   const uint32_t parts = (a->maxd + 255) / 256;
   hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream,
