@@ -41,6 +41,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-passes', type=int, default=8)
     ap.add_argument('--no-extras', action='store_true', help='skip the stream / decode / PCIe side measurements')
+    ap.add_argument('--no-configs', action='store_true',
+                    help='skip the C3 / C4 / C5 stream-configuration figures (scripts/configs_bench.py)')
     return ap.parse_args()
 
 
@@ -198,6 +200,25 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
     return res
 
 
+def other_configs():
+    """BASELINE.json's other configurations on this GPU (stream semantics,
+    one cache; scripts/configs_bench.py): each figure is parity-checked
+    against the oracle on a prefix and decoded back in full.  A failure is
+    reported in the line, never hidden."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('configs_bench', os.path.join(ROOT, 'scripts', 'configs_bench.py'))
+    cb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cb)
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384)
+    out = {}
+    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5)):
+        try:
+            out[name] = fn(a)
+        except BaseException as e:          # SystemExit from a parity check included
+            out[name] = {'error': f'{type(e).__name__}: {e}'}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -304,6 +325,8 @@ def main():
                          'algorithmic_bytes_per_launch': in_bytes + out_bytes},
         }
         line.update(extras)
+        if world == 1 and not args.no_extras and not args.no_configs:
+            line['configs'] = other_configs()
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_passes)
         print(json.dumps(line), flush=True)
