@@ -66,6 +66,7 @@ extern "C" {
 #define XCG_ENOMEM (-12)
 #define XCG_EINVAL (-22)
 #define XCG_EOVERFLOW (-75)        /* internal table overflow (reported, never silent) */
+#define XCG_EPROTO (-71)           /* pipe protocol error (XCodecPipePair::decoder_error) */
 #define XCG_ENOTSUP (-95)
 
 typedef struct xcg_ctx xcg_ctx;
@@ -176,6 +177,41 @@ int xcg_pack_outputs(xcg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_o
 /* Status word of the context (sticky; nonzero = an internal overflow happened
  * in an earlier asynchronous call).  Synchronises the context's device. */
 int xcg_ctx_status(xcg_ctx *ctx);
+
+/*
+ * XCodecPipePair protocol layer (xcodec/xcodec_pipe_pair.cc,
+ * xcodec/xcodec_pipe_protocol.h), host side over the functions above:
+ * <HELLO>, <FRAME> (one encode() per <= 512 KiB of input), <ASK>/<LEARN>,
+ * <ADVANCE>, <EOS>/<EOS_ACK>.  `enc` is the codec's encoder context (its cache
+ * is shared by every pipe of the codec, xcodec/xcodec.h:91-107); `dec` the
+ * decoder context of the peer's cache (XCodecCache::connect(uuid), one per
+ * peer); `uuid` the 36-character UUID string this side sends in <HELLO>.
+ * Each call returns what XCodecPipePair would produce: bytes for the peer
+ * (encoder_produce) and decoded bytes for the local side (decoder_produce),
+ * plus the two EOS signals.  Output buffers belong to the pipe and stay valid
+ * until its next call.  XCG_EPROTO = decoder_error().
+ *   encoder_consume  = XCodecPipePair::encoder_consume (:549-642); len 0 = EOS
+ *   decoder_consume  = XCodecPipePair::decoder_consume (:68-166);  len 0 = EOS
+ *   encoder_consume_many: n pipes sharing one `enc`, their frames encoded in
+ *   ONE GPU batch in the given order (the order one event thread serves them).
+ */
+typedef struct xcg_pipe xcg_pipe;
+typedef struct xcg_pipe_out {
+  const uint8_t *to_peer;
+  uint64_t to_peer_len;
+  const uint8_t *to_local;
+  uint64_t to_local_len;
+  int local_eos;                 /* decoder_produce_eos */
+  int peer_eos;                  /* encoder_produce_eos */
+} xcg_pipe_out;
+int xcg_pipe_create(xcg_ctx *enc, xcg_ctx *dec, const uint8_t *uuid, xcg_pipe **out);
+void xcg_pipe_destroy(xcg_pipe *p);
+int xcg_pipe_encoder_consume(xcg_pipe *p, const uint8_t *data, uint64_t len, xcg_pipe_out *out);
+int xcg_pipe_encoder_consume_many(xcg_pipe *const *pipes, const uint8_t *const *data, const uint64_t *len, uint32_t n,
+                                  xcg_pipe_out *out);
+int xcg_pipe_decoder_consume(xcg_pipe *p, const uint8_t *data, uint64_t len, xcg_pipe_out *out);
+/* Frames whose REF segments the encoder still keeps for <ASK> (not yet <ADVANCE>d). */
+uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
 
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,

@@ -1,0 +1,147 @@
+"""XCodecPipePair protocol layer over the GPU engine (xcg_pipe_*): framing
+against the oracle restatement (oracle/pipe.py), encoder -> decoder round
+trips with <ADVANCE>, the <ASK>/<LEARN> exchange, <EOS>/<EOS_ACK>, batched
+multi-pipe encoding, and the decoder_error() cases (xcodec/xcodec_pipe_pair.cc)."""
+import numpy as np
+import pytest
+
+from golden_cases import data
+
+pytestmark = pytest.mark.gpu
+
+UUID_A = b'0d1f4c8e-95a3-4b2d-8f6e-3c7a9b1d2e4f'
+UUID_B = b'a7c3e9f1-2b4d-4e6f-8a0c-1e3f5a7c9e0b'
+
+
+@pytest.fixture
+def ctxs():
+    from wanproxy_amd.xcgpu import Context
+    cs = [Context(0, cache_segments=1 << 15) for _ in range(2)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+def payload(seed=3, n=1_700_000):
+    rng = np.random.default_rng(seed)
+    blocks = [rng.integers(0, 256, 2048, dtype=np.uint8).tobytes() for _ in range(200)]
+    out = bytearray()
+    while len(out) < n:
+        b = blocks[int(rng.integers(0, len(blocks)))]
+        out += b if rng.random() < 0.7 else rng.integers(0, 256, int(rng.integers(1, 3000)), dtype=np.uint8).tobytes()
+    return bytes(out[:n])
+
+
+def test_framing_vs_oracle(ctxs, oracle):
+    from oracle.pipe import encoder_stream
+    from wanproxy_amd.xcgpu import PipePair
+    enc, dec = ctxs
+    a = PipePair(enc, dec, UUID_A)
+    consumes = [data('kat_a'), payload(), b'x' * 100, data('kat_b')[:70000], b'']
+    got = b''.join(a.encoder_consume(c) for c in consumes)
+    cache = oracle.cache_new()
+    try:
+        exp = encoder_stream(oracle, cache, UUID_A, consumes)
+    finally:
+        oracle.cache_free(cache)
+    assert got == exp
+    assert a.pending_frames() == 2 + 4 + 1 + 1
+
+
+def test_roundtrip_advance_eos(ctxs):
+    from wanproxy_amd.xcgpu import Context, PipePair
+    enc, _ = ctxs
+    benc, bdec = Context(0, cache_segments=1 << 15), Context(0, cache_segments=1 << 15)
+    a = PipePair(enc, ctxs[1], UUID_A)           # a's decoder side hears b's replies
+    b = PipePair(benc, bdec, UUID_B)
+    msgs = [payload(1), payload(2, 900_000), data('kat_c')]
+    for m in msgs:
+        wire = a.encoder_consume(m)
+        to_a, local, leos, peos = b.decoder_consume(wire)
+        assert local == m and not leos and not peos
+        assert to_a[:1] == b'\x01'                   # <ADVANCE> for the frames decoded
+        nframes = -(-len(m) // (512 * 1024))
+        assert int.from_bytes(to_a[1:5], 'big') == nframes
+        assert a.pending_frames() == nframes
+        back, _, _, _ = a.decoder_consume(to_a)
+        assert back == b'' and a.pending_frames() == 0
+    # <EOS> -> <EOS_ACK>, local EOS on b; a hears the ack
+    wire = a.encoder_consume(b'')
+    assert wire == b'\xfc'
+    to_a, local, leos, peos = b.decoder_consume(wire)
+    assert (to_a, local, leos, peos) == (b'\xfb', b'', True, False)
+    back, local, leos, peos = a.decoder_consume(to_a)
+    assert (back, local, leos, peos) == (b'', b'', False, False)
+    benc.close()
+    bdec.close()
+
+
+def test_ask_learn(ctxs):
+    """A decoder whose cache lost segments asks; the encoder answers from the
+    frames it still holds (encoder_reference_frames_); decoding resumes."""
+    from wanproxy_amd.xcgpu import Context, PipePair
+    enc, adec = ctxs
+    bdec = Context(0, cache_segments=1 << 15)
+    a = PipePair(enc, adec, UUID_A)
+    b = PipePair(Context(0, cache_segments=1 << 10), bdec, UUID_B)
+    m = payload(9, 600_000)
+    to_a, local, _, _ = b.decoder_consume(a.encoder_consume(m))
+    assert local == m
+    a.decoder_consume(to_a)                          # <ADVANCE>
+    bdec.cache_clear()                               # b forgets every segment
+    wire = a.encoder_consume(m)                      # now (almost) all REFs
+    to_a, local, _, _ = b.decoder_consume(wire)
+    assert b'\xf0' in to_a                           # <ASK>
+    k = to_a.index(b'\xf0')
+    count = int.from_bytes(to_a[k + 1:k + 3], 'big')
+    assert count > 0
+    learn, _, _, _ = a.decoder_consume(to_a)
+    assert learn[:1] == b'\xf1' and int.from_bytes(learn[1:3], 'big') == count
+    assert len(learn) == 3 + 2048 * count
+    more, local2, _, _ = b.decoder_consume(learn)
+    assert local + local2 == m
+    bdec.close()
+
+
+def test_encoder_consume_many_equals_sequential(ctxs, oracle):
+    from wanproxy_amd.xcgpu import Context, PipePair
+    enc, dec = ctxs
+    uu = [UUID_A, UUID_B] * 2
+    datas = [payload(20 + i, 300_000 + 170_000 * i) for i in range(4)]
+    pipes = [PipePair(enc, dec, u) for u in uu]
+    many = PipePair.encoder_consume_many(pipes, datas)
+    enc2 = Context(0, cache_segments=1 << 15)
+    pipes2 = [PipePair(enc2, dec, u) for u in uu]
+    seq = [p.encoder_consume(d) for p, d in zip(pipes2, datas)]
+    assert many == seq
+    enc2.close()
+
+
+@pytest.mark.parametrize('wire', [
+    b'\x02\x00\x00\x00\x01x',                       # <FRAME> before <HELLO>
+    b'\xff\x24' + UUID_B + b'\xff\x24' + UUID_B,    # <HELLO> twice
+    b'\xff\x05hello',                               # bad <HELLO> length
+    b'\xf0\x00\x01' + b'\x00' * 8,                  # <ASK> before we sent <HELLO>
+    b'\xff\x24' + UUID_B + b'\xf1\x00\x01' + b'\x07' * 2048,   # <LEARN> nobody asked for
+    b'\xff\x24' + UUID_B + b'\x02\x00\x00\x00\x00',            # zero-length frame
+    b'\xfb',                                        # <EOS_ACK> before our <EOS>
+    b'\x55',                                        # unsupported op
+])
+def test_decoder_errors(ctxs, wire):
+    from wanproxy_amd.xcgpu import PipePair, XCGError
+    p = PipePair(ctxs[0], ctxs[1], UUID_A)
+    with pytest.raises(XCGError, match='protocol'):
+        p.decoder_consume(wire)
+
+
+def test_partial_ops_wait_for_more(ctxs):
+    from wanproxy_amd.xcgpu import Context, PipePair
+    a = PipePair(ctxs[0], ctxs[1], UUID_A)
+    b = PipePair(Context(0, cache_segments=1 << 10), Context(0, cache_segments=1 << 15), UUID_B)
+    m = payload(33, 200_000)
+    wire = a.encoder_consume(m)
+    got = b''
+    for i in range(0, len(wire), 777):               # arbitrary TCP segmentation
+        _, local, _, _ = b.decoder_consume(wire[i:i + 777])
+        got += local
+    assert got == m

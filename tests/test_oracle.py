@@ -111,3 +111,29 @@ def test_decode_partial_and_unknown(oracle, ref_oracle):
         res.append((ok, out, consumed, sorted(unk)))   # std::set<uint64_t> order
         o.cache_free(c)
     assert res[0] == res[1] and res[0][0] and res[0][3]
+
+
+def test_pipe_framing_oracle(oracle):
+    """oracle/pipe.py: <HELLO>, 512 KiB <FRAME>s whose payloads decode back, <EOS>."""
+    from golden_cases import data
+    from oracle.pipe import encoder_stream
+    uuid = b'0d1f4c8e-95a3-4b2d-8f6e-3c7a9b1d2e4f'
+    d = data('kat_a')
+    cache = oracle.cache_new()
+    try:
+        wire = encoder_stream(oracle, cache, uuid, [d, b''])
+    finally:
+        oracle.cache_free(cache)
+    assert wire[:2] == bytes([0xFF, 36]) and wire[2:38] == uuid and wire[-1:] == b'\xfc'
+    i, frames = 38, []
+    while wire[i] == 0x02:
+        n = int.from_bytes(wire[i + 1:i + 5], 'big')
+        frames.append(wire[i + 5:i + 5 + n])
+        i += 5 + n
+    assert i == len(wire) - 1 and len(frames) == 2
+    dcache = oracle.cache_new()
+    try:
+        out = b''.join(oracle.decode(f, dcache)[1] for f in frames)
+    finally:
+        oracle.cache_free(dcache)
+    assert out == d

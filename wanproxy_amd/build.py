@@ -6,7 +6,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/xcg_hash.hip']
+SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/xcg_hash.hip', 'csrc/xcg_pipe.cpp']
 OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 

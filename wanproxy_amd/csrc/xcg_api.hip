@@ -373,6 +373,7 @@ const char* xcg_strerror(int status) {
     case XCG_EOVERFLOW: return "internal table overflow";
     case XCG_ENOTSUP: return "not supported";
     case XCG_ENOENT: return "no such segment";
+    case XCG_EPROTO: return "pipe protocol error";
     default: return "unknown status";
   }
 }

@@ -36,6 +36,17 @@ class XCGError(RuntimeError):
     pass
 
 
+class _PipeOut(C.Structure):
+    _fields_ = [('to_peer', C.c_void_p), ('to_peer_len', C.c_uint64), ('to_local', C.c_void_p),
+                ('to_local_len', C.c_uint64), ('local_eos', C.c_int), ('peer_eos', C.c_int)]
+
+    def peer(self) -> bytes:
+        return C.string_at(self.to_peer, self.to_peer_len) if self.to_peer_len else b''
+
+    def local(self) -> bytes:
+        return C.string_at(self.to_local, self.to_local_len) if self.to_local_len else b''
+
+
 def lib():
     """Load libxcgpu.so (after torch, so both share one HIP runtime)."""
     global _lib
@@ -83,6 +94,19 @@ def lib():
     L.xcg_window_hashes.restype = C.c_int
     L.xcg_segment_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
     L.xcg_segment_hashes.restype = C.c_int
+    L.xcg_pipe_create.argtypes = [vp, vp, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.xcg_pipe_create.restype = C.c_int
+    L.xcg_pipe_destroy.argtypes = [vp]
+    L.xcg_pipe_destroy.restype = None
+    L.xcg_pipe_encoder_consume.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(_PipeOut)]
+    L.xcg_pipe_encoder_consume.restype = C.c_int
+    L.xcg_pipe_encoder_consume_many.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
+                                                C.c_uint32, C.POINTER(_PipeOut)]
+    L.xcg_pipe_encoder_consume_many.restype = C.c_int
+    L.xcg_pipe_decoder_consume.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(_PipeOut)]
+    L.xcg_pipe_decoder_consume.restype = C.c_int
+    L.xcg_pipe_pending_frames.argtypes = [vp]
+    L.xcg_pipe_pending_frames.restype = C.c_uint32
     L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     _lib = L
@@ -312,3 +336,52 @@ class XCodecDecoder:
             return True, b'', 0, []
         outs, st, cons, unk = self.ctx.decode_chunks([data], window=self.window)
         return int(st[0]) >= 0, outs[0], int(cons[0]), unk
+
+
+class PipePair:
+    """Mirror of XCodecPipePair (xcodec/xcodec_pipe_pair.h:41-212) over
+    xcg_pipe_*: encoder_consume(data) -> bytes for the peer (b'' input = EOS);
+    decoder_consume(data) -> (to_peer, to_local, local_eos, peer_eos).  `enc`
+    is the codec's context (cache shared by its pipes), `dec` the context of the
+    peer's cache; `uuid` the 36-byte UUID string sent in <HELLO>."""
+
+    def __init__(self, enc: Context, dec: Context, uuid: bytes):
+        self.enc, self.dec = enc, dec
+        h = C.c_void_p()
+        _check(lib().xcg_pipe_create(enc.h, dec.h, uuid, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().xcg_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encoder_consume(self, data: bytes) -> bytes:
+        o = _PipeOut()
+        _check(lib().xcg_pipe_encoder_consume(self.h, data, len(data), C.byref(o)))
+        return o.peer()
+
+    @staticmethod
+    def encoder_consume_many(pipes, datas):
+        n = len(pipes)
+        hs = (C.c_void_p * n)(*[p.h.value for p in pipes])
+        ds = (C.c_char_p * n)(*datas)
+        ls = (C.c_uint64 * n)(*[len(d) for d in datas])
+        outs = (_PipeOut * n)()
+        _check(lib().xcg_pipe_encoder_consume_many(hs, ds, ls, n, outs))
+        return [o.peer() for o in outs]
+
+    def decoder_consume(self, data: bytes):
+        o = _PipeOut()
+        rc = lib().xcg_pipe_decoder_consume(self.h, data, len(data), C.byref(o))
+        _check(rc)
+        return o.peer(), o.local(), bool(o.local_eos), bool(o.peer_eos)
+
+    def pending_frames(self) -> int:
+        return int(lib().xcg_pipe_pending_frames(self.h))
