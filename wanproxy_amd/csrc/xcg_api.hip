@@ -554,7 +554,7 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
     c->last_rounds = rounds;
-    return rc == 0 ? XCG_OK : XCG_EHIP;
+    return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : XCG_EHIP);
   }
   int rc = xcg_launch_encode_independent(d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, c->flags, d_out,
                                          d_out_off, d_out_len, d_stats, c->d_status, (hipStream_t)stream);

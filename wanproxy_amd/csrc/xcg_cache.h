@@ -88,7 +88,11 @@ __device__ __forceinline__ uint32_t gfilt_mask(uint32_t k) { return (1u << (k & 
 __device__ __forceinline__ uint32_t gfilt_test(uint32_t w, uint32_t k) {
   return (w >> (k & 31u)) & (w >> ((k >> 5) & 31u)) & 1u;
 }
-__device__ __forceinline__ uint32_t fbucket(uint32_t k, uint32_t fmask) { return mix32(k, 0x5BD1E995u) & fmask; }
+// Fingerprint bucket = K bits 13.. (K is a sum-based hash; its high bits are
+// well spread), fingerprint = top 16 bits of K * golden ratio: two keys of
+// one bucket differ in bits 0..12, and their products' top halves then agree
+// with probability ~2^-16.  (Two cheap ops each instead of a full mix.)
+__device__ __forceinline__ uint32_t fbucket(uint32_t k, uint32_t fmask) { return (k >> 13) & fmask; }
 
 // Wave-uniform 64-bit value (readfirstlane per 32-bit half; no sign extension).
 __device__ __forceinline__ uint64_t readfirst64(uint64_t v) {
@@ -162,7 +166,7 @@ __device__ __forceinline__ bool tab_insert_min(HashTab t, uint32_t lo, uint32_t 
 }
 
 // 16-bit fingerprint of a probe key (odd, so never 0 = empty or FOVF16).
-__device__ __forceinline__ uint32_t fp16_of(uint32_t k) { return (mix32(k, 0x27D4EB2Fu) >> 16) | 1u; }
+__device__ __forceinline__ uint32_t fp16_of(uint32_t k) { return ((k * 0x9E3779B1u) >> 16) | 1u; }
 
 // Fingerprint bucket insert: first free of the 7 slots, else set the bucket's
 // overflow flag (a probe of that bucket then reports an event and the

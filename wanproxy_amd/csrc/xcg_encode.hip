@@ -622,7 +622,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     const int q0 = p + 32 * l;
     const bool contig = (p == p_prev + SEG);
     ++n_pieces;
-    if (!STREAM) progress_priority(s, L);
+    progress_priority(s, L);
     // vmcnt counts loads and stores together, in order (gfx9): every wait on
     // a load also waits for all older stores.  So fresh loads are waited for
     // here, inside their branch, and the prefetch below is waited for after
@@ -978,6 +978,39 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   filt_insert(fs, d.x, d.y);
 }
 
+// Everything a round clears or copies before its batch table is built, in
+// one launch (six separate memset / copy calls cost ~7 us each in launch
+// gaps): the table, the round's filters (copies of the cache's, or zero while
+// the cache is empty), the key counters, the changed word and, for a
+// verification, the changed-hash table and its flags.
+struct RoundPrep {
+  HashTab tab;
+  uint32_t* r_filt; const uint32_t* g_filt;
+  u32x4* r_ftab; const u32x4* g_ftab; uint32_t ftab_n;      // 16-byte units
+  uint32_t* r_gfilt; const uint32_t* g_gfilt; uint32_t gfilt_n;
+  const uint32_t* nseg;
+  uint32_t* bcount;
+  uint32_t* changed;
+  HashTab rt;           // keys == nullptr: not a verification round
+  uint32_t* vflags;
+};
+__global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool g_empty = *a.nseg == 0u;
+  for (uint64_t i = i0; i <= a.tab.mask; i += stride) { a.tab.keys[i] = EMPTY_KEY; a.tab.vals[i] = ~0ull; }
+  if (a.rt.keys)
+    for (uint64_t i = i0; i <= a.rt.mask; i += stride) { a.rt.keys[i] = EMPTY_KEY; a.rt.vals[i] = ~0ull; }
+  for (uint64_t i = i0; i < FILT_WORDS; i += stride) a.r_filt[i] = g_empty ? 0u : a.g_filt[i];
+  for (uint64_t i = i0; i < a.ftab_n; i += stride) a.r_ftab[i] = g_empty ? u32x4{0u, 0u, 0u, 0u} : a.g_ftab[i];
+  for (uint64_t i = i0; i < a.gfilt_n; i += stride) a.r_gfilt[i] = g_empty ? 0u : a.g_gfilt[i];
+  if (i0 < 64) a.bcount[i0] = 0u;
+  if (i0 == 0) {
+    *a.changed = ~0u;
+    if (a.rt.keys) { a.vflags[0] = ~0u; a.vflags[1] = 0u; }
+  }
+}
+
 // ------------------------------------------------ verification of a round
 //
 // Round r parsed chunk k against V = the batch table of round r-1's
@@ -1218,38 +1251,36 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   HashTab tabs[2] = {HashTab{a->b_keys, a->b_vals, a->b_mask}, HashTab{a->b2_keys, a->b2_vals, a->b_mask}};
   const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
   int cur = 0;
-  auto build = [&](int t) -> bool {
-    if (hipMemsetAsync(tabs[t].keys, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
-        hipMemsetAsync(tabs[t].vals, 0xFF, 8ull * (a->b_mask + 1), stream) != hipSuccess ||
-        hipMemcpyAsync(a->r_filt, a->g_filt, fbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
-        hipMemcpyAsync(a->r_ftab, a->g_ftab, tbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
-        hipMemcpyAsync(a->r_gfilt, a->g_gfilt, gbytes, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
-        hipMemsetAsync(a->bcount, 0, 4 * 64, stream) != hipSuccess)
-      return false;
+  int dev_cus = (int)wgs;
+  auto build = [&](int t, bool verify) -> bool {
+    RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
+                 a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
+                 verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags};
+    hipLaunchKernelGGL(round_prep_kernel, dim3(4 * dev_cus), dim3(256), 0, stream, rp);
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
                        (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, tabs[t],
                        FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
-    return true;
+    return hipGetLastError() == hipSuccess;
   };
   if (n > 1 && fc != ~0u) {
-    if (!build(cur) || hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
+    if (!build(cur, false)) return -5;
     prm.use_b = true;
     prm.b = tabs[cur];
     prm.skip_below = fc + 1;
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     launch();
     ++rounds;
-    if (!changed_after(fc)) return -5;
     prm.skip_below = 0;
-    for (uint32_t r = 2; r <= n + 1 && fc != ~0u; ++r) {
+    // (no host sync here: the verification's own sync tells whether round 1
+    // changed anything that matters)
+    // Each round fixes at least the first flagged chunk (every chunk before
+    // it already stands under the final lists), so n rounds always suffice.
+    bool converged = false;
+    for (uint32_t r = 2; r <= n + 1; ++r) {
       // verify round r-1 (parsed against tabs[cur]) against its own declarations
       const int nxt = cur ^ 1;
-      if (!build(nxt) || hipMemsetAsync(a->r_keys, 0xFF, 8ull * (a->r_mask + 1), stream) != hipSuccess ||
-          hipMemsetAsync(a->r_vals, 0xFF, 8ull * (a->r_mask + 1), stream) != hipSuccess ||
-          hipMemsetAsync(a->vflags, 0xFF, 4, stream) != hipSuccess ||
-          hipMemsetAsync(a->vflags + 1, 0, 4, stream) != hipSuccess)
-        return -5;
+      if (!build(nxt, true)) return -5;
       const uint64_t slots = 2ull * (a->b_mask + 1);
       hipLaunchKernelGGL(verify_diff_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, tabs[cur],
                          tabs[nxt], a->in, a->chunk_off, rt, a->vflags, a->status);
@@ -1259,15 +1290,18 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       if (hipMemcpyAsync(a->h_vflags, a->vflags, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
           hipStreamSynchronize(stream) != hipSuccess)
         return -5;
-      if (a->h_vflags[1] == 0) break;                  // nothing flagged: fixed point
+      if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point
+        converged = true;
+        break;
+      }
       if (hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
       cur = nxt;
       prm.b = tabs[cur];
       prm.need = a->need;
       launch();
       ++rounds;
-      if (!changed_after(fc)) return -5;
     }
+    if (!converged) return -75;
   }
   const uint32_t parts = (a->maxd + 255) / 256;
   hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream,
