@@ -711,45 +711,52 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         insert(cand_lo, cand_hi, (uint32_t)cand);
         c0_in_table = true;
       }
-      const bool c0 = have_cand && !c0_in_table;
-      const int vis = cand + SEG;
-      const int rvis = vis - p;
-      const uint32_t c0k = probe_key(cand_lo);
-      // Bucket overflows are rare (three of a chunk's keys in one 2-slot
-      // bucket); one overflow key costs one compare, more cost eight.
-      uint32_t ovk[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
-      const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
-      GlbQ gq{gs.lds, gs.lfo, prm.lf.gfilt, prm.lf.gmask, prm.lf.ftab, prm.lf.fmask, sa0, sa0, sa0 + 256u * GSLOTS,
-              0u, 0u};
-      // G = probe the persistent cache / batch declarations too
-      auto roll = [&](auto c0t, auto novft, auto glbt) {
-        return roll_probe<LOGNB, decltype(c0t)::value, decltype(novft)::value, decltype(glbt)::value>(
-            P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, gq);
-      };
-      using T0 = std::integral_constant<bool, false>;
-      using T1 = std::integral_constant<bool, true>;
-      using N0 = std::integral_constant<int, 0>;
-      using N1 = std::integral_constant<int, 1>;
-      using N8 = std::integral_constant<int, 8>;
-      auto by_novf = [&](auto glbt) {
-        if (novf == 0) return c0 ? roll(T1{}, N0{}, glbt) : roll(T0{}, N0{}, glbt);
-        if (novf == 1) return c0 ? roll(T1{}, N1{}, glbt) : roll(T0{}, N1{}, glbt);
-        // duplicates of a real overflow key pad the unused slots
-        return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
-      };
-      if (STREAM && gs.fmode == 1) {
-        ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
-      } else if (STREAM && gs.fmode == 2) {
-        ev = by_novf(std::integral_constant<int, STREAM ? 2 : 0>{});
+      if (pe - s <= 2) {
+        // One or two positions left (every chunk of 2048 k bytes ends with a
+        // one-position piece): decide them exactly, as events, instead of
+        // rolling 2048 positions for them.
+        ev = lane_id() == 0 ? ((1u << (uint32_t)(pe - s)) - 1u) << (uint32_t)(s - p) : 0u;
       } else {
-        ev = by_novf(std::integral_constant<int, 0>{});
+        const bool c0 = have_cand && !c0_in_table;
+        const int vis = cand + SEG;
+        const int rvis = vis - p;
+        const uint32_t c0k = probe_key(cand_lo);
+        // Bucket overflows are rare (three of a chunk's keys in one 2-slot
+        // bucket); one overflow key costs one compare, more cost eight.
+        uint32_t ovk[8];
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
+        const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
+        GlbQ gq{gs.lds, gs.lfo, prm.lf.gfilt, prm.lf.gmask, prm.lf.ftab, prm.lf.fmask, sa0, sa0, sa0 + 256u * GSLOTS,
+                0u, 0u};
+        // G = probe the persistent cache / batch declarations too
+        auto roll = [&](auto c0t, auto novft, auto glbt) {
+          return roll_probe<LOGNB, decltype(c0t)::value, decltype(novft)::value, decltype(glbt)::value>(
+              P, NX1, NX2, kblk, kofs, c0k, rvis, ovk, gq);
+        };
+        using T0 = std::integral_constant<bool, false>;
+        using T1 = std::integral_constant<bool, true>;
+        using N0 = std::integral_constant<int, 0>;
+        using N1 = std::integral_constant<int, 1>;
+        using N8 = std::integral_constant<int, 8>;
+        auto by_novf = [&](auto glbt) {
+          if (novf == 0) return c0 ? roll(T1{}, N0{}, glbt) : roll(T0{}, N0{}, glbt);
+          if (novf == 1) return c0 ? roll(T1{}, N1{}, glbt) : roll(T0{}, N1{}, glbt);
+          // duplicates of a real overflow key pad the unused slots
+          return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
+        };
+        if (STREAM && gs.fmode == 1) {
+          ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
+        } else if (STREAM && gs.fmode == 2) {
+          ev = by_novf(std::integral_constant<int, STREAM ? 2 : 0>{});
+        } else {
+          ev = by_novf(std::integral_constant<int, 0>{});
+        }
+        // positions past the last window are not positions (branch-free mask)
+        const int nvalid = pe - q0;
+        const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
+        ev &= vm;
       }
-      // positions past the last window are not positions (branch-free mask)
-      const int nvalid = pe - q0;
-      const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
-      ev &= vm;
     }
     // The prefetch has had the vector phase to land; take it before the
     // resolve phase issues this piece's stores.
