@@ -256,6 +256,62 @@ __device__ __forceinline__ const uint8_t* ref_source(const DecParams& prm, uint3
   return nullptr;
 }
 
+// Per-lane REF source (the same rule as ref_source, each lane its own hash).
+__device__ __forceinline__ const uint8_t* ref_source_t(const DecParams& prm, uint32_t lo, uint32_t hi, uint64_t here) {
+  const uint64_t e = tab_lookup_t(prm.x, lo, hi);
+  if (e != ~0ull && e < here) return prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
+  const uint64_t gv = tab_lookup_t(prm.g, lo, hi);
+  if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+  return nullptr;
+}
+
+// A run of consecutive REF ops from offset i (the op at i is a whole REF
+// before `limit`): lane l takes the l-th REF, at i + 10 l, while every op
+// before it is a REF too (a REF is 10 bytes, so that is where the next op
+// starts).  REF-dense streams (warm caches: one REF per 2 KiB) then pay one
+// round of lane-parallel table lookups per 64 REFs instead of one dependent
+// chain per REF.  Returns the run length (1..64, uniform); lanes < run get
+// their hash and stream position.
+__device__ __forceinline__ uint32_t ref_run(const uint8_t* x, uint32_t i, uint32_t len, uint32_t chunk,
+                                            uint64_t limit, uint64_t& h, uint64_t& here) {
+  const uint32_t l = (uint32_t)lane_id();
+  const uint32_t o = i + 10u * l;
+  here = spos(chunk, o);
+  bool isref = o + 10u <= len && here < limit;
+  if (isref) isref = x[o] == MAGIC && x[o + 1] == OP_REF;
+  const uint64_t bad = ballot(!isref);
+  const uint32_t r = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+  h = 0;
+  if (l < r) h = be64(x + o + 2);
+  return r;
+}
+
+// Copy k segments (pointers held by lanes 0..k-1) to dst, consecutively; the
+// loads of four segments are in flight together.
+__device__ __forceinline__ void copy_segments(uint8_t* dst, const uint8_t* src_lane, uint32_t k) {
+  const int l = lane_id();
+  for (uint32_t a = 0; a < k; a += 4) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (a + j < k) {
+        const uint64_t sp = readlane64((uint64_t)src_lane, (int)(a + j));
+        const uint8_t* sj = (const uint8_t*)sp;
+        v[2 * j] = *(const u32x4_u*)(sj + 32 * l);
+        v[2 * j + 1] = *(const u32x4_u*)(sj + 32 * l + 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (a + j < k) {
+        uint8_t* d = dst + (uint64_t)(a + j) * SEG;
+        *(u32x4_u*)(d + 32 * l) = v[2 * j];
+        *(u32x4_u*)(d + 32 * l + 16) = v[2 * j + 1];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ kernels
 
 template <bool EMIT>
@@ -313,22 +369,27 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
       ++ndecl;                                               // window_.declare, :137
     } else if (op == OP_REF) {                               // :141-163
       if (len - i < 10u) { st = 3; break; }
-      const uint64_t h = be64(x + i + 2);
-      const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+      if (EMIT && spos(chunk, i) >= blockp) { st = 1; break; }   // blocked at or before this op
+      // Resolvability (an earlier EXTRACT of h in the batch, or the cache)
+      // is checked after the scan (decode_refcheck_kernel), once the batch
+      // table is complete; emit resolves a whole run of REFs at a time.
+      uint64_t h, here;
+      uint32_t r = ref_run(x, i, len, chunk, blockp, h, here);
+      bool stop = false;
       if (EMIT) {
-        const uint64_t here = spos(chunk, i);
-        if (here >= blockp) { st = 1; break; }               // blocked at or before this op
-        const uint8_t* src = ref_source(prm, lo, hi, here);
-        if (src == nullptr) { st = 1; break; }               // cannot happen: scan found all
-        wave_copy2048(out + olen, src);
-      } else {
-        // Resolvable iff an earlier EXTRACT of h exists in the batch or the
-        // cache holds h; the scan only records the unresolvable ones (the
-        // batch table is complete only after the scan, so defer the check).
+        const uint8_t* src = nullptr;
+        if ((uint32_t)l < r) src = ref_source_t(prm, (uint32_t)h, (uint32_t)(h >> 32), here);
+        const uint64_t miss = ballot((uint32_t)l < r && src == nullptr);
+        if (miss) {                                          // cannot happen: refcheck found all
+          r = (uint32_t)__builtin_ctzll(miss);
+          stop = true;
+        }
+        copy_segments(out + olen, src, r);
       }
-      olen += SEG;
-      i += 10;
-      ++ndecl;                                               // window_.declare, :160
+      olen += (uint64_t)SEG * r;
+      i += 10u * r;
+      ndecl += r;                                            // window_.declare, :160
+      if (stop) { st = 1; break; }
     } else if (op == OP_BACKREF) {                           // :165-181
       if (len - i < 3u) { st = 3; break; }
       if (EMIT) {
@@ -389,13 +450,15 @@ __global__ __launch_bounds__(256) void decl_record_kernel(DecParams prm, uint64_
       i += 2 + SEG;
     } else if (op == OP_REF) {
       if (len - i < 10u) break;
-      if (t >= lo_t) {
-        const uint64_t h = be64(x + i + 2);
-        const uint64_t src = (uint64_t)ref_source(prm, (uint32_t)h, (uint32_t)(h >> 32), spos(chunk, i));
-        if (lane_id() == 0) prm.D[t - lo_t] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)src, (uint32_t)(src >> 32));
+      uint64_t h, here;
+      const uint32_t r = ref_run(x, i, len, chunk, ~0ull, h, here);
+      const uint64_t tl = t + (uint64_t)lane_id();
+      if ((uint32_t)lane_id() < r && tl >= lo_t && tl < hi_t) {
+        const uint64_t src = (uint64_t)ref_source_t(prm, (uint32_t)h, (uint32_t)(h >> 32), here);
+        prm.D[tl - lo_t] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)src, (uint32_t)(src >> 32));
       }
-      ++t;
-      i += 10;
+      t += r;
+      i += 10u * r;
     } else if (op == OP_BACKREF) {
       if (len - i < 3u) break;
       i += 3;
@@ -490,21 +553,23 @@ __global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
       i += 2 + SEG;
     } else if (op == OP_REF) {
       if (len - i < 10u) break;
-      const uint64_t h = be64(x + i + 2);
-      const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-      const uint64_t here = spos(chunk, i);
-      const uint64_t e = tab_lookup(prm.x, lo, hi);
-      bool ok = e != ~0ull && e < here;
-      if (!ok) ok = tab_lookup(prm.g, lo, hi) != ~0ull;
-      if (!ok && lane_id() == 0) {
-        atomicMin((unsigned long long*)prm.block_pos, (unsigned long long)here);
-        const uint32_t k = atomicAdd(prm.nunknown, 1u);
-        if (k < prm.unknown_cap) {
-          prm.unknown[k] = h;
-          prm.unknown_pos[k] = here;
+      uint64_t h, here;
+      const uint32_t r = ref_run(x, i, len, chunk, ~0ull, h, here);
+      if ((uint32_t)lane_id() < r) {
+        const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+        const uint64_t e = tab_lookup_t(prm.x, lo, hi);
+        bool ok = e != ~0ull && e < here;
+        if (!ok) ok = tab_lookup_t(prm.g, lo, hi) != ~0ull;
+        if (!ok) {
+          atomicMin((unsigned long long*)prm.block_pos, (unsigned long long)here);
+          const uint32_t k = atomicAdd(prm.nunknown, 1u);
+          if (k < prm.unknown_cap) {
+            prm.unknown[k] = h;
+            prm.unknown_pos[k] = here;
+          }
         }
       }
-      i += 10;
+      i += 10u * r;
     } else if (op == OP_BACKREF) {
       if (len - i < 3u) break;
       i += 3;

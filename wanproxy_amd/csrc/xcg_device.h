@@ -42,6 +42,9 @@ __device__ __forceinline__ uint32_t readfirst(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)readlane((uint32_t)(v >> 32), l) << 32) | readlane((uint32_t)v, l);
+}
 
 // v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0.  So
 // ffbl(x) + 1 == POSIX ffs(x) for every x, which is what XCodecHash::add /
