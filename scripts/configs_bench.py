@@ -96,32 +96,34 @@ def decode_device(ctx, encs, per: int, chunk: int, rehearse: bool = True):
     d_eoff = torch.from_numpy(offs.view(np.int64)).to(dev)
     d_elen = torch.from_numpy(lens.view(np.int32)).to(dev)
     cap = per * chunk + 4096           # decoded bytes of one batch
-    d_dout = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_dout = torch.empty(n * chunk + 4096, dtype=torch.uint8, device=dev)   # every batch, back to back
     d_doo = torch.zeros(per, dtype=torch.int64, device=dev)
     d_dol = torch.zeros(per, dtype=torch.int64, device=dev)
-    d_dst = torch.zeros(per, dtype=torch.int32, device=dev)
+    d_dst = torch.zeros(n, dtype=torch.int32, device=dev)
     d_dcons = torch.zeros(per, dtype=torch.int64, device=dev)
     unk = np.zeros(16, np.uint64)
     nunk = np.zeros(1, np.uint32)
     tot = np.zeros(1, np.uint64)
-    parts, secs = [], 0.0
-    for a in range(0, n, per):
+    maxlen = [int(lens[a:min(n, a + per)].max()) for a in range(0, n, per)]
+    o, nbad = 0, 0
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k, a in enumerate(range(0, n, per)):
         b = min(n, a + per)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
         _check(lib().xcg_decode_batch(ctx.h, C.c_void_p(d_enc.data_ptr()), C.c_void_p(d_eoff[a:].data_ptr()),
-                                      C.c_void_p(d_elen[a:].data_ptr()), b - a, int(lens[a:b].max()),
-                                      C.c_void_p(d_dout.data_ptr()), cap, C.c_void_p(d_doo.data_ptr()),
-                                      C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
-                                      C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
-                                      tot.ctypes.data, None))
-        torch.cuda.synchronize(dev)
-        secs += time.perf_counter() - t0
-        st = d_dst[:b - a].cpu().numpy()
-        if (st != 0).any() or nunk[0]:
-            raise SystemExit(f'decode status {np.unique(st)} unknown {int(nunk[0])}')
-        parts.append(d_dout[:int(tot[0])].cpu().numpy().tobytes())
-    return b''.join(parts), secs
+                                      C.c_void_p(d_elen[a:].data_ptr()), b - a, maxlen[k],
+                                      C.c_void_p(d_dout.data_ptr() + o), min(cap, d_dout.numel() - o),
+                                      C.c_void_p(d_doo.data_ptr()), C.c_void_p(d_dol.data_ptr()),
+                                      C.c_void_p(d_dst[a:].data_ptr()), C.c_void_p(d_dcons.data_ptr()),
+                                      unk.ctypes.data, unk.size, nunk.ctypes.data, tot.ctypes.data, None))
+        nbad += int(nunk[0])
+        o += int(tot[0])
+    torch.cuda.synchronize(dev)
+    secs = time.perf_counter() - t0
+    st = d_dst.cpu().numpy()
+    if (st != 0).any() or nbad:
+        raise SystemExit(f'decode status {np.unique(st)} unknown {nbad}')
+    return d_dout[:o].cpu().numpy().tobytes(), secs
 
 
 def check_prefix(data, offs, lens, got, k, what):

@@ -200,6 +200,7 @@ struct xcg_ctx {
   DecodeScratch ds;
   xcg_window* own_win = nullptr;   // default window (lazily allocated)
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
+  int32_t* h_status = nullptr;     // pinned copy of d_status
 };
 
 namespace {
@@ -241,11 +242,15 @@ void free_scratch(BatchScratch& b) {
 }
 
 int clear_cache(GpuCache& g) {
-  if (hipMemset(g.keys, 0xFF, 8ull * (g.mask + 1)) != hipSuccess ||
-      hipMemset(g.vals, 0xFF, 8ull * (g.mask + 1)) != hipSuccess || hipMemset(g.nseg, 0, 4) != hipSuccess ||
-      hipMemset(g.filt, 0, 4ull * FILT_WORDS) != hipSuccess ||
-      hipMemset(g.ftab, 0, 16ull * (g.fmask + 1)) != hipSuccess ||
-      hipMemset(g.gfilt, 0, 4ull * (g.gmask + 1)) != hipSuccess)
+  // (asynchronous fills + one sync: a synchronous hipMemset of a fresh
+  // buffer costs milliseconds)
+  if (hipMemsetAsync(g.keys, 0xFF, 8ull * (g.mask + 1), nullptr) != hipSuccess ||
+      hipMemsetAsync(g.vals, 0xFF, 8ull * (g.mask + 1), nullptr) != hipSuccess ||
+      hipMemsetAsync(g.nseg, 0, 4, nullptr) != hipSuccess ||
+      hipMemsetAsync(g.filt, 0, 4ull * FILT_WORDS, nullptr) != hipSuccess ||
+      hipMemsetAsync(g.ftab, 0, 16ull * (g.fmask + 1), nullptr) != hipSuccess ||
+      hipMemsetAsync(g.gfilt, 0, 4ull * (g.gmask + 1), nullptr) != hipSuccess ||
+      hipStreamSynchronize(nullptr) != hipSuccess)
     return XCG_EHIP;
   return XCG_OK;
 }
@@ -392,7 +397,8 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
   if (flags & ~(XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) return XCG_EINVAL;
   DeviceGuard g(device);
   xcg_ctx* c = new xcg_ctx{device, flags, nullptr, cache_segments, GpuCache{}, BatchScratch{}, 0, DecodeScratch{}};
-  if (hipMalloc(&c->d_status, 16) != hipSuccess) {
+  if (hipMalloc(&c->d_status, 16) != hipSuccess || hipHostMalloc(&c->h_status, 16) != hipSuccess) {
+    (void)hipFree(c->d_status);
     delete c;
     return XCG_ENOMEM;
   }
@@ -409,6 +415,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipFree(c->d_status);
+  if (c->h_status) (void)hipHostFree(c->h_status);
   free_cache(c->g);
   free_scratch(c->bs);
   free_dscratch(c->ds);
@@ -522,8 +529,11 @@ int xcg_ctx_status(xcg_ctx* c) {
   if (!c) return XCG_EINVAL;
   DeviceGuard g(c->device);
   int32_t st = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
-  if (hipMemcpy(&st, c->d_status, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyAsync(c->h_status, c->d_status, sizeof st, hipMemcpyDeviceToHost, nullptr) != hipSuccess ||
+      hipStreamSynchronize(nullptr) != hipSuccess)
+    return XCG_EHIP;
+  st = *c->h_status;
   return st ? XCG_EOVERFLOW : XCG_OK;
 }
 
@@ -612,7 +622,10 @@ int xcg_encode_host(xcg_ctx* c, int semantics, const uint8_t* h_in, uint64_t in_
     }
     if (rc == XCG_OK && hipStreamSynchronize(st) != hipSuccess) rc = XCG_EHIP;
     int32_t status = 0;
-    if (rc == XCG_OK && hipMemcpy(&status, c->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
+    if (rc == XCG_OK && (hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                         hipStreamSynchronize(st) != hipSuccess))
+      rc = XCG_EHIP;
+    status = *c->h_status;
     if (rc == XCG_OK && status) rc = XCG_EOVERFLOW;
   } while (0);
   (void)hipFree(d_in);
@@ -657,14 +670,18 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   if (lrc == -75) return XCG_EOVERFLOW;
   if (lrc != 0) return XCG_EHIP;
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return XCG_EHIP;
-  int32_t st = 0;
-  uint64_t t_end = 0;
-  if (hipMemcpy(&st, c->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(&t_end, c->ds.scratch + 5, 8, hipMemcpyDeviceToHost) != hipSuccess)
+  // status word and the declare count, by async copies into pinned memory
+  // (a synchronous 4-byte hipMemcpy costs milliseconds here)
+  if (hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+      hipMemcpyAsync(c->ds.h_scratch + 7, c->ds.scratch + 5, 8, hipMemcpyDeviceToHost, (hipStream_t)stream) !=
+          hipSuccess ||
+      hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
     return XCG_EHIP;
+  const int32_t st = *c->h_status;
+  const uint64_t t_end = c->ds.h_scratch[7];
   w->count += t_end;                                  // declares made: the window cursor advances
   if (st & (1 << 9)) {
-    (void)hipMemset(c->d_status, 0, 4);
+    (void)hipMemsetAsync(c->d_status, 0, 4, (hipStream_t)stream);
     return XCG_ENOTSUP;
   }
   if (nunk && blockp < berr) {
@@ -676,7 +693,9 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
     // no ASK.)
     const uint32_t m = nunk < UNKNOWN_CAP ? nunk : UNKNOWN_CAP;
     std::vector<uint64_t> hs(m);
-    if (hipMemcpy(hs.data(), c->ds.unknown, 8ull * m, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+    if (hipMemcpyAsync(hs.data(), c->ds.unknown, 8ull * m, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+      return XCG_EHIP;
     std::sort(hs.begin(), hs.end());
     hs.erase(std::unique(hs.begin(), hs.end()), hs.end());
     const uint32_t k = (uint32_t)hs.size() < unknown_cap ? (uint32_t)hs.size() : unknown_cap;
