@@ -579,29 +579,39 @@ __global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
   }
 }
 
-// Exclusive scan of n u64 lengths (single workgroup; n up to a few million).
+// Exclusive scan of n u64 lengths (single workgroup).  Tiles of 4096: each
+// thread loads four consecutive lengths (coalesced), scans them, the block
+// scans the 1024 partial sums in LDS, and a running carry joins the tiles --
+// a handful of load round trips instead of one per element per thread.
 __global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint64_t* len, uint64_t* off, uint32_t n,
                                                              uint64_t* total) {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024;
-  const uint32_t a = min(n, t * per), b = min(n, a + per);
-  uint64_t s = 0;
-  for (uint32_t i = a; i < b; ++i) s += len[i];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint64_t v = t >= d ? part[t - d] : 0;
+  uint64_t carry = 0;
+  for (uint32_t base = 0; base < n; base += 4096) {
+    const uint32_t i0 = base + 4 * t;
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < n ? len[i0 + k] : 0u;
+    const uint64_t s = v[0] + v[1] + v[2] + v[3];
+    part[t] = s;
     __syncthreads();
-    part[t] += v;
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+      const uint64_t u = t >= d ? part[t - d] : 0u;
+      __syncthreads();
+      part[t] += u;
+      __syncthreads();
+    }
+    uint64_t run = carry + part[t] - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < n) off[i0 + k] = run;
+      run += v[k];
+    }
+    carry += part[1023];
     __syncthreads();
   }
-  uint64_t run = part[t] - s;
-  for (uint32_t i = a; i < b; ++i) {
-    off[i] = run;
-    run += len[i];
-  }
-  if (t == 1023) *total = part[1023];
+  if (t == 0) *total = carry;
 }
 
 // Commit: every batch EXTRACT hash whose latest occurrence precedes the

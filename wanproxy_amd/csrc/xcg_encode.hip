@@ -1096,26 +1096,31 @@ __global__ __launch_bounds__(1024) void commit_scan_kernel(const uint32_t* ndecl
                                                            uint32_t* nseg) {
   __shared__ uint32_t part[1024];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024;
-  const uint32_t a = min(n, t * per), b = min(n, a + per);
-  uint32_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += ndecl[i];
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint32_t v = t >= d ? part[t - d] : 0u;
+  uint32_t carry = *nseg;
+  for (uint32_t base = 0; base < n; base += 4096) {     // tiles of 4096 (as exclusive_scan_kernel)
+    const uint32_t i0 = base + 4 * t;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < n ? ndecl[i0 + k] : 0u;
+    const uint32_t sum = v[0] + v[1] + v[2] + v[3];
+    part[t] = sum;
     __syncthreads();
-    part[t] += v;
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+      const uint32_t u = t >= d ? part[t - d] : 0u;
+      __syncthreads();
+      part[t] += u;
+      __syncthreads();
+    }
+    uint32_t run = carry + part[t] - sum;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < n) seg_base[i0 + k] = run;
+      run += v[k];
+    }
+    carry += part[1023];
     __syncthreads();
   }
-  const uint32_t base = *nseg;
-  uint32_t run = base + part[t] - sum;
-  for (uint32_t i = a; i < b; ++i) {
-    seg_base[i] = run;
-    run += ndecl[i];
-  }
-  __syncthreads();
-  if (t == 1023) *nseg = base + part[1023];
+  if (t == 0) *nseg = carry;
 }
 
 // Commit the converged declarations into the persistent cache
