@@ -218,6 +218,12 @@ uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
  * else through a global (L2-resident) one; both give the same output.
  * Returns the previous threshold (default 220000, or XCG_LDS_FILTER_KEYS). */
 uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
+/* Diagnostics / tests: stream batches start either with a parse round against
+ * the cache alone, or -- automatically when the context's previous batch
+ * declared segments -- from each chunk's 2048-byte tiling (its cold parse),
+ * corrected by the verification.  Same output either way.  mode: -1
+ * automatic (default), 0 never seed, 1 always seed.  Returns the previous mode. */
+int xcg_debug_set_stream_seed(int mode);
 
 /* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for
  * s in [0, len - 2048]. */

@@ -34,6 +34,16 @@ def oracle():
     return Oracle()
 
 
+@pytest.fixture(params=[0, 1], ids=['round0', 'seeded'])
+def stream_seed(request):
+    """Both ways the stream encoder starts its rounds (xcg_debug_set_stream_seed):
+    a parse round against the cache alone, or the chunks' tiling seed."""
+    from wanproxy_amd.xcgpu import lib
+    old = lib().xcg_debug_set_stream_seed(request.param)
+    yield request.param
+    lib().xcg_debug_set_stream_seed(old)
+
+
 @pytest.fixture(scope='session')
 def ref_oracle():
     from oracle.lib import Oracle

@@ -35,7 +35,7 @@ def first_diff(got, exp):
     return next((i for i in range(len(exp)) if got[i] != exp[i]), None)
 
 
-def test_c3_warm_shared_cache(filter_mode, oracle):
+def test_c3_warm_shared_cache(filter_mode, stream_seed, oracle):
     """C3: streams interleaved round-robin at 64 KiB, one shared cache; warm-up
     encode then the same data again against the warm cache (nearly all REF)."""
     from wanproxy_amd import synth
@@ -67,7 +67,7 @@ def test_c3_warm_shared_cache(filter_mode, oracle):
     dctx.close()
 
 
-def test_c4_small_packets(filter_mode, oracle):
+def test_c4_small_packets(filter_mode, stream_seed, oracle):
     """C4: 4 KiB packets, each one encode() call, one cache per shard."""
     from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
@@ -81,7 +81,7 @@ def test_c4_small_packets(filter_mode, oracle):
     ctx.close()
 
 
-def test_c5_large_chunks_cold_cache(filter_mode, oracle):
+def test_c5_large_chunks_cold_cache(filter_mode, stream_seed, oracle):
     """C5: 128 KiB chunks, cold unbounded cache growing across batches."""
     from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
@@ -95,7 +95,7 @@ def test_c5_large_chunks_cold_cache(filter_mode, oracle):
     ctx.close()
 
 
-def test_mixed_alphabet_global_filter(filter_mode, oracle):
+def test_mixed_alphabet_global_filter(filter_mode, stream_seed, oracle):
     """Collision-prone and 0xF1-heavy data through both filter modes."""
     from wanproxy_amd.synth import chunks_of
     from wanproxy_amd.xcgpu import Context

@@ -22,7 +22,7 @@ def enc_stream(ctx, d, offs, lens):
     return ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
 
 
-def test_golden_stream(sctx, golden):
+def test_golden_stream(sctx, golden, stream_seed):
     n = 0
     for case in golden['cases']:
         if case['mode'] != 'stream':
@@ -36,7 +36,7 @@ def test_golden_stream(sctx, golden):
     assert n >= 10
 
 
-def test_baseline_kats_stream(sctx, golden):
+def test_baseline_kats_stream(sctx, golden, stream_seed):
     # BASELINE.md "KAT": tack -c over the whole file (64 KiB encode() calls).
     from wanproxy_amd.synth import chunks_of
     for name, b in golden['baseline'].items():
@@ -47,7 +47,7 @@ def test_baseline_kats_stream(sctx, golden):
         assert (len(whole), sha(whole)) == (b['xc_len'], b['xc']), name
 
 
-def test_stream_split_batches(sctx, oracle):
+def test_stream_split_batches(sctx, oracle, stream_seed):
     # The cache persists across calls: one stream fed in batches of 1..64
     # chunks encodes exactly like one batch / the sequential oracle.
     from wanproxy_amd.synth import chunks_of
@@ -64,7 +64,7 @@ def test_stream_split_batches(sctx, oracle):
     assert sctx.cache_size() > 0
 
 
-def test_stream_random_vs_oracle(sctx, oracle):
+def test_stream_random_vs_oracle(sctx, oracle, stream_seed):
     rng = np.random.default_rng(77)
     blocks = [rng.integers(0, 256, size=2048, dtype=np.uint8) for _ in range(40)]
     parts = []

@@ -65,6 +65,8 @@ struct XcgStreamArgs {
   uint32_t* need;
   uint32_t* vflags;
   uint32_t* h_vflags;
+  int seed;
+  uint32_t* decls_out;
 };
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
@@ -201,9 +203,13 @@ struct xcg_ctx {
   xcg_window* own_win = nullptr;   // default window (lazily allocated)
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
   int32_t* h_status = nullptr;     // pinned copy of d_status
+  bool seed_next = false;          // the last stream batch declared something: seed the next one
 };
 
 namespace {
+
+// Stream-round seeding: -1 automatic, 0 never, 1 always (tests exercise both).
+int g_stream_seed = -1;
 
 struct DeviceGuard {
   int prev = -1;
@@ -385,6 +391,10 @@ const char* xcg_strerror(int status) {
 
 uint64_t xcg_encode_bound(uint32_t len) { return 2ull * len + 16ull; }
 
+int xcg_debug_set_stream_seed(int mode) {
+  return __atomic_exchange_n(&g_stream_seed, mode < 0 ? -1 : (mode ? 1 : 0), __ATOMIC_RELAXED);
+}
+
 int xcg_ctx_create(int device, uint32_t flags, xcg_ctx** out) {
   return xcg_ctx_create_ex(device, flags, XCG_DEFAULT_CACHE_SEGMENTS, out);
 }
@@ -560,9 +570,17 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
                     c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
                     c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount, c->bs.b2_keys, c->bs.b2_vals,
                     c->bs.r_keys, c->bs.r_vals, c->bs.r_mask, c->bs.hits, c->bs.nhits, c->bs.maxh, c->bs.need,
-                    c->bs.vflags, c->bs.h_vflags};
+                    c->bs.vflags, c->bs.h_vflags, 0, nullptr};
+    // Seed the rounds with the chunks' 2048-byte tilings instead of a parse
+    // round 0 when the last batch declared segments (cold / growing caches);
+    // a warm cache's all-REF batches keep round 0, which then is all they need.
+    const int mode = __atomic_load_n(&g_stream_seed, __ATOMIC_RELAXED);
+    a.seed = mode < 0 ? (c->seed_next ? 1 : 0) : mode;
+    uint32_t decls = ~0u;
+    a.decls_out = &decls;
     int rounds = 0;
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
+    if (decls != ~0u) c->seed_next = decls > 0;
     c->last_rounds = rounds;
     return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : XCG_EHIP);
   }

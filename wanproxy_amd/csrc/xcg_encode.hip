@@ -985,6 +985,26 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   filt_insert(fs, d.x, d.y);
 }
 
+// Seed for the rounds instead of round 0: a chunk's cold parse (nothing
+// cached, no repeat inside the chunk) declares exactly the 2048-byte tiling
+// 0, 2048, ... ("the cold parse of unique data is an exact
+// 2048-aligned tiling").  Round 1 then parses every chunk against the
+// tiling of the chunks before it; the verification flags every chunk the
+// guess misled, so the result is exact whatever the data.  One wave per
+// (chunk, tile): a hash pass over the batch instead of a full parse.
+__global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, const uint64_t* chunk_off,
+                                                          const uint32_t* chunk_len, uint32_t n, uint32_t maxd,
+                                                          uint4* decl, uint32_t* ndecl) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t c = (uint32_t)(w / maxd), k = (uint32_t)(w % maxd);
+  if (c >= n) return;
+  const uint32_t m = chunk_len[c] / SEG;
+  if (k == 0 && lane_id() == 0) ndecl[c] = m;
+  if (k >= m) return;
+  const uint2 h = window_hash_u(in + chunk_off[c] + (uint64_t)k * SEG);
+  if (lane_id() == 0) decl[(uint64_t)c * maxd + k] = make_uint4(h.x, h.y, k * SEG, 0u);
+}
+
 // Everything a round clears or copies before its batch table is built, in
 // one launch (six separate memset / copy calls cost ~7 us each in launch
 // gaps): the table, the round's filters (copies of the cache's, or zero while
@@ -1086,6 +1106,13 @@ __global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uin
   }
   need[k] = f ? 1u : 0u;
   if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
+}
+
+// Declarations in the batch table just built (for the next batch's seeding
+// policy): vflags[2] = sum of the build's counters.
+__global__ void count_decls_kernel(const uint32_t* bcount, uint32_t* out) {
+  const uint32_t v = wave_sum(bcount[lane_id()]);
+  if (lane_id() == 0) *out = v;
 }
 
 // Segment numbers of the committed declarations: seg_base[c] = nseg + the
@@ -1213,8 +1240,10 @@ struct XcgStreamArgs {
   uint32_t* nhits;
   uint32_t maxh;
   uint32_t* need;
-  uint32_t* vflags;      // [0] a_first, [1] any
+  uint32_t* vflags;      // [0] a_first, [1] any, [2] declarations in the last table built
   uint32_t* h_vflags;    // pinned
+  int seed;              // start from the tiling seed instead of round 0
+  uint32_t* decls_out;   // (host) declarations the batch made, ~0 if unknown
 };
 
 // LDS / global lane filter threshold (keys): XCG_LDS_FILTER_KEYS at load
@@ -1268,6 +1297,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       hipMemsetAsync(a->nhits, 0, 4ull * n, stream) != hipSuccess ||
       hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
     return -5;
+  const bool seeded = a->seed && n > 1;
+  if (a->decls_out) *a->decls_out = ~0u;
   prm.need = nullptr;
   prm.hits = a->hits;                              // every stream round writes nhits[chunk]
   prm.nhits = a->nhits;
@@ -1276,10 +1307,18 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.use_b = false;
   prm.skip_below = 0;
   prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask, a->g_gfilt, a->gmask};
-  launch();
-  int rounds = 1;
+  int rounds = 0;
   uint32_t fc = 0;
-  if (!changed_after(fc)) return -5;
+  if (seeded) {
+    const uint64_t nw = (uint64_t)n * a->maxd;
+    hipLaunchKernelGGL(seed_tiling_kernel, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0, stream, a->in,
+                       a->chunk_off, a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl);
+  } else {
+    launch();
+    rounds = 1;
+    if (!changed_after(fc)) return -5;
+    if (fc == ~0u && a->decls_out) *a->decls_out = 0;   // round 0 declared nothing
+  }
   // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
   // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
   // chunk k after round k.  Round 1 re-parses every chunk after the first
@@ -1307,7 +1346,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     if (!build(cur, false)) return -5;
     prm.use_b = true;
     prm.b = tabs[cur];
-    prm.skip_below = fc + 1;
+    prm.skip_below = seeded ? 0 : fc + 1;            // (seeded: round 1 parses every chunk)
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     launch();
     ++rounds;
@@ -1327,9 +1366,11 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       hipLaunchKernelGGL(verify_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n,
                          (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt,
                          (const uint32_t*)a->vflags, a->need, a->vflags + 1);
-      if (hipMemcpyAsync(a->h_vflags, a->vflags, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipLaunchKernelGGL(count_decls_kernel, dim3(1), dim3(64), 0, stream, (const uint32_t*)a->bcount, a->vflags + 2);
+      if (hipMemcpyAsync(a->h_vflags, a->vflags, 12, hipMemcpyDeviceToHost, stream) != hipSuccess ||
           hipStreamSynchronize(stream) != hipSuccess)
         return -5;
+      if (a->decls_out) *a->decls_out = a->h_vflags[2];
       if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point
         converged = true;
         break;

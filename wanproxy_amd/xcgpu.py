@@ -107,6 +107,8 @@ def lib():
     L.xcg_pipe_decoder_consume.restype = C.c_int
     L.xcg_pipe_pending_frames.argtypes = [vp]
     L.xcg_pipe_pending_frames.restype = C.c_uint32
+    L.xcg_debug_set_stream_seed.argtypes = [C.c_int]
+    L.xcg_debug_set_stream_seed.restype = C.c_int
     L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     _lib = L
