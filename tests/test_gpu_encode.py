@@ -123,3 +123,24 @@ def test_stats_and_roundtrip(ctx, oracle):
         ok, dec, consumed, unk = oracle.decode(outs[i], c)
         oracle.cache_free(c)
         assert ok and not unk and dec == d[int(offs[i]):int(offs[i] + lens[i])]
+
+
+def test_overlong_chunk_is_refused():
+    """A chunk longer than the launch's max_chunk_len is refused loudly (the
+    records sized for the bound would overflow), not encoded wrongly."""
+    import torch
+    from wanproxy_amd.xcgpu import XCG_SEM_INDEPENDENT, XCG_SEM_STREAM, Context, XCGError
+    dev = torch.device('cuda', 0)
+    n, L = 2, 200000
+    d_in = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    d_off = torch.tensor([0, L], dtype=torch.int64, device=dev)
+    d_len = torch.tensor([L, 1000], dtype=torch.int32, device=dev)
+    d_oo = torch.tensor([0, 2 * L + 16], dtype=torch.int64, device=dev)
+    d_out = torch.zeros(4 * L + 64, dtype=torch.uint8, device=dev)
+    d_ol = torch.zeros(n, dtype=torch.int64, device=dev)
+    for sem in (XCG_SEM_INDEPENDENT, XCG_SEM_STREAM):
+        ctx = Context(0, cache_segments=1 << 12)
+        ctx.encode_batch_device(d_in, d_off, d_len, n, 65536, d_out, d_oo, d_ol, semantics=sem)
+        with pytest.raises(XCGError):
+            ctx.status()
+        ctx.close()

@@ -98,6 +98,7 @@ struct EncParams {
   uint64_t* hits;      // [n * maxh] hashes the chunk found among the batch declarations (REF or collision)
   uint32_t* nhits;     // [n] (> maxh: overflowed, always re-parsed)
   uint32_t maxh;
+  uint32_t max_len;    // the caller's bound on every chunk length (sizes LDS records and declaration rows)
 };
 
 // ------------------------------------------------------------------ emission
@@ -486,6 +487,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #ifdef XCG_TIMING
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+  // A chunk longer than the launch's bound would overrun the records sized
+  // for it: refuse it loudly (status bit 3) instead.
+  if ((uint32_t)L > prm.max_len || (uint32_t)L / SEG >= (uint32_t)MAXD) {
+    if (l == 0) {
+      prm.out_len[chunk] = 0;
+      if (prm.status) atomicOr(prm.status, 8);
+    }
+    return;
+  }
   if (L < SEG) {                                   // xcodec_encoder.cc:77-83
     if (L > 0) olen = escape_u(out, x, 0, (uint32_t)L);
     if (l == 0) prm.out_len[chunk] = olen;
@@ -953,6 +963,7 @@ extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t
                                              hipStream_t stream) {
   if (n == 0) return 0;
   xcg::EncParams prm{d_in, d_chunk_off, d_chunk_len, n, flags, d_out, d_out_off, d_out_len, d_stats, d_status};
+  prm.max_len = max_chunk_len;
   dim3 grid((n + 3) / 4), block(256);
   if (max_chunk_len <= (1u << 17)) {
     hipLaunchKernelGGL((xcg::encode_independent_kernel<10, 72>), grid, block, 0, stream, prm);
@@ -998,7 +1009,7 @@ __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, con
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t c = (uint32_t)(w / maxd), k = (uint32_t)(w % maxd);
   if (c >= n) return;
-  const uint32_t m = chunk_len[c] / SEG;
+  const uint32_t m = min(chunk_len[c] / SEG, maxd);   // (an over-long chunk is refused by the round)
   if (k == 0 && lane_id() == 0) ndecl[c] = m;
   if (k >= m) return;
   const uint2 h = window_hash_u(in + chunk_off[c] + (uint64_t)k * SEG);
@@ -1262,6 +1273,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const uint32_t n = a->n;
   if (n == 0) return 0;
   EncParams prm{a->in, a->chunk_off, a->chunk_len, n, a->flags, a->out, a->out_off, a->out_len, a->stats, a->status};
+  prm.max_len = (a->maxd - 1) * SEG + (SEG - 1);     // maxd = max_chunk_len / 2048 + 1
   prm.g = HashTab{a->g_keys, a->g_vals, a->g_mask};
   prm.pool = a->pool;
   prm.b = HashTab{a->b_keys, a->b_vals, a->b_mask};
