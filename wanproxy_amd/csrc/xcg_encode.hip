@@ -1005,15 +1005,47 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
 // (chunk, tile): a hash pass over the batch instead of a full parse.
 __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, const uint64_t* chunk_off,
                                                           const uint32_t* chunk_len, uint32_t n, uint32_t maxd,
-                                                          uint4* decl, uint32_t* ndecl) {
-  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t c = (uint32_t)(w / maxd), k = (uint32_t)(w % maxd);
+                                                          uint4* decl, uint32_t* ndecl, uint32_t* nhits,
+                                                          uint32_t* changed) {
+  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);   // one wave per chunk
+  if (c == 0 && threadIdx.x == 0) *changed = ~0u;
   if (c >= n) return;
-  const uint32_t m = min(chunk_len[c] / SEG, maxd);   // (an over-long chunk is refused by the round)
-  if (k == 0 && lane_id() == 0) ndecl[c] = m;
-  if (k >= m) return;
-  const uint2 h = window_hash_u(in + chunk_off[c] + (uint64_t)k * SEG);
-  if (lane_id() == 0) decl[(uint64_t)c * maxd + k] = make_uint4(h.x, h.y, k * SEG, 0u);
+  const int l = lane_id();
+  const uint32_t m = min(chunk_len[c] / SEG, maxd);    // (an over-long chunk is refused by the round)
+  const uint8_t* x = in + chunk_off[c];
+  if (l == 0) {
+    ndecl[c] = m;
+    nhits[c] = 0u;
+  }
+  // four tiles per step: lane l sums bytes [16 l, 16 l + 16) and [1024 + 16 l, ...) of each
+  for (uint32_t k0 = 0; k0 < m; k0 += 4) {
+    u32x4 v[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        v[t][h] = k0 + t < m ? *(const u32x4_u*)(x + (uint64_t)(k0 + t) * SEG + 1024u * h + 16u * l)
+                             : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (k0 + t >= m) break;
+      uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t q0 = 1024u * h + 16u * l;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t xb = byte_of(v[t][h][k >> 2], k & 3);
+          const uint32_t f = ffbl(xb) + 1u;
+          const uint32_t wt = 2048u - (q0 + k);
+          X1 += xb; X2 += wt * xb; F1 += f; F2 += wt * f;
+        }
+      }
+      X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
+      if (l == 0) decl[(uint64_t)c * maxd + k0 + t] = make_uint4((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4,
+                                                                  (k0 + t) * SEG, 0u);
+    }
+  }
 }
 
 // Everything a round clears or copies before its batch table is built, in
@@ -1101,21 +1133,27 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
     atomicOr(status, 2);
 }
 
-// need[k] for every chunk: (a), an overflowed hit list, or a recorded hit in a
-// changed range (b).  One thread per chunk.
-__global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uint64_t* hits, const uint32_t* nhits,
-                                                           uint32_t maxh, HashTab rt, const uint32_t* a_first,
-                                                           uint32_t* need, uint32_t* any) {
+// need[k] for every chunk: (a) or an overflowed hit list; then (b), one
+// thread per recorded hit (verify_hits_kernel).
+__global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uint32_t* nhits, uint32_t maxh,
+                                                           const uint32_t* a_first, uint32_t* need, uint32_t* any) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const uint32_t nk = nhits[k];
-  bool f = k >= *a_first || nk > maxh;
-  for (uint32_t i = 0; i < nk && !f; ++i) {
-    const uint64_t h = hits[(uint64_t)k * maxh + i];
+  const bool f = k >= *a_first || nhits[k] > maxh;
+  need[k] = f ? 1u : 0u;
+  if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
+}
+__global__ __launch_bounds__(256) void verify_hits_kernel(uint32_t n, const uint64_t* hits, const uint32_t* nhits,
+                                                          uint32_t maxh, HashTab rt, uint32_t* need, uint32_t* any) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = (uint32_t)(j / maxh), i = (uint32_t)(j % maxh);
+  bool f = false;
+  if (k < n && i < nhits[k]) {
+    const uint64_t h = hits[j];
     const uint64_t r = tab_lookup_t(rt, (uint32_t)h, (uint32_t)(h >> 32));
     f = r != ~0ull && k >= (uint32_t)(r >> 32) && k <= (uint32_t)r;
+    if (f) need[k] = 1u;
   }
-  need[k] = f ? 1u : 0u;
   if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
 }
 
@@ -1130,10 +1168,13 @@ __global__ void count_decls_kernel(const uint32_t* bcount, uint32_t* out) {
 // declarations of chunks < c (exclusive scan, one workgroup), and nseg
 // advanced by the total -- no per-block atomic on one counter (16 k of those
 // serialised to ~190 us for a batch of 4 KiB packets).
+// gate (nullable): run only if *gate == 0 -- the commit is queued right
+// behind a verification and does nothing if that verification flagged chunks.
 __global__ __launch_bounds__(1024) void commit_scan_kernel(const uint32_t* ndecl, uint32_t n, uint32_t* seg_base,
-                                                           uint32_t* nseg) {
+                                                           uint32_t* nseg, const uint32_t* gate) {
   __shared__ uint32_t part[1024];
   const uint32_t t = threadIdx.x;
+  if (gate && *gate) return;
   uint32_t carry = *nseg;
   for (uint32_t base = 0; base < n; base += 4096) {     // tiles of 4096 (as exclusive_scan_kernel)
     const uint32_t i0 = base + 4 * t;
@@ -1169,7 +1210,9 @@ __global__ __launch_bounds__(1024) void commit_scan_kernel(const uint32_t* ndecl
 __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                      uint32_t maxd, const uint8_t* in, const uint64_t* chunk_off,
                                                      HashTab g, uint8_t* pool, const uint32_t* seg_base,
-                                                     uint32_t seg_cap, FiltSet fs, int32_t* status) {
+                                                     uint32_t seg_cap, FiltSet fs, int32_t* status,
+                                                     const uint32_t* gate) {
+  if (gate && *gate) return;
   const uint32_t parts = (maxd + 255) / 256;
   const uint32_t c = blockIdx.x / parts, k0 = (blockIdx.x % parts) * 256u;
   const uint32_t nd = c < n ? ndecl[c] : 0u;
@@ -1305,11 +1348,11 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     fc = *a->h_changed;
     return true;
   };
-  if (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess ||
-      hipMemsetAsync(a->nhits, 0, 4ull * n, stream) != hipSuccess ||
-      hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess)
-    return -5;
   const bool seeded = a->seed && n > 1;
+  if (!seeded && (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess ||
+                  hipMemsetAsync(a->nhits, 0, 4ull * n, stream) != hipSuccess ||
+                  hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess))
+    return -5;                                       // (the seed kernel initialises these itself)
   if (a->decls_out) *a->decls_out = ~0u;
   prm.need = nullptr;
   prm.hits = a->hits;                              // every stream round writes nhits[chunk]
@@ -1322,9 +1365,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   int rounds = 0;
   uint32_t fc = 0;
   if (seeded) {
-    const uint64_t nw = (uint64_t)n * a->maxd;
-    hipLaunchKernelGGL(seed_tiling_kernel, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0, stream, a->in,
-                       a->chunk_off, a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl);
+    hipLaunchKernelGGL(seed_tiling_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
+                       a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
   } else {
     launch();
     rounds = 1;
@@ -1343,6 +1385,19 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
   int cur = 0;
   int dev_cus = (int)wgs;
+  // Commit the declaration lists into the persistent cache; with a gate, only
+  // if the verification that precedes it in the stream flagged nothing.
+  bool committed = false;
+  auto commit = [&](const uint32_t* gate) {
+    const uint32_t parts = (a->maxd + 255) / 256;
+    uint32_t* seg_base = (uint32_t*)a->hits;       // (free once the rounds are over: n words)
+    hipLaunchKernelGGL(commit_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)a->ndecl, n, seg_base,
+                       a->nseg, gate);
+    hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream, (const uint4*)a->decl,
+                       (const uint32_t*)a->ndecl, n, a->maxd, a->in, a->chunk_off, prm.g, a->pool,
+                       (const uint32_t*)seg_base, a->seg_cap,
+                       FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask}, a->status, gate);
+  };
   auto build = [&](int t, bool verify) -> bool {
     RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
                  a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
@@ -1376,15 +1431,18 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       hipLaunchKernelGGL(verify_diff_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, tabs[cur],
                          tabs[nxt], a->in, a->chunk_off, rt, a->vflags, a->status);
       hipLaunchKernelGGL(verify_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n,
-                         (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt,
-                         (const uint32_t*)a->vflags, a->need, a->vflags + 1);
+                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)a->vflags, a->need, a->vflags + 1);
+      const uint64_t nh = (uint64_t)n * a->maxh;
+      hipLaunchKernelGGL(verify_hits_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, n,
+                         (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt, a->need, a->vflags + 1);
       hipLaunchKernelGGL(count_decls_kernel, dim3(1), dim3(64), 0, stream, (const uint32_t*)a->bcount, a->vflags + 2);
-      if (hipMemcpyAsync(a->h_vflags, a->vflags, 12, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-          hipStreamSynchronize(stream) != hipSuccess)
-        return -5;
+      if (hipMemcpyAsync(a->h_vflags, a->vflags, 12, hipMemcpyDeviceToHost, stream) != hipSuccess) return -5;
+      commit(a->vflags + 1);                           // runs while the host waits, if nothing was flagged
+      if (hipStreamSynchronize(stream) != hipSuccess) return -5;
       if (a->decls_out) *a->decls_out = a->h_vflags[2];
-      if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point
+      if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point (already committed)
         converged = true;
+        committed = true;
         break;
       }
       if (hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
@@ -1396,13 +1454,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     }
     if (!converged) return -75;
   }
-  const uint32_t parts = (a->maxd + 255) / 256;
-  hipLaunchKernelGGL(commit_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)a->ndecl, n, a->need,
-                     a->nseg);                     // (need[] is free after the rounds: segment bases)
-  hipLaunchKernelGGL(commit_kernel, dim3(n * parts), dim3(256), 0, stream,
-                     (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, a->in, a->chunk_off,
-                     prm.g, a->pool, (const uint32_t*)a->need, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask},
-                     a->status);
+  if (!committed) commit(nullptr);
   if (rounds_out) *rounds_out = rounds;
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
