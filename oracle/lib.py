@@ -55,6 +55,9 @@ class Oracle:
         self._wh.argtypes = [_u8p, C.c_uint64, _u64p]
         self._cnew = getattr(L, pre + "cache_new")
         self._cnew.restype = C.c_void_p
+        self._cnewl = getattr(L, pre + 'cache_new_limited')
+        self._cnewl.restype = C.c_void_p
+        self._cnewl.argtypes = [C.c_uint64]
         self._cfree = getattr(L, pre + 'cache_free')
         self._cfree.argtypes = [C.c_void_p]
         self._eb = getattr(L, pre + 'encode_batch')
@@ -105,8 +108,10 @@ class Oracle:
         return out
 
     # ----------------------------------------------------------------- cache
-    def cache_new(self):
-        return self._cnew()
+    def cache_new(self, limit_bytes: int = 0):
+        """XCodecMemoryCache(uuid) or, with limit_bytes, the bounded LRU variant
+        XCodecMemoryCache(uuid, limit_bytes) (xcodec/xcodec_cache.h:277-288)."""
+        return self._cnewl(limit_bytes) if limit_bytes else self._cnew()
 
     def cache_free(self, c):
         self._cfree(c)

@@ -78,6 +78,14 @@ void *xcr_cache_new(void)
 	return new XCodecMemoryCache(uuid);
 }
 
+/* XCodecMemoryCache(uuid, memory_cache_limit_bytes): the bounded, LRU-evicting
+ * variant (xcodec/xcodec_cache.h:277-288, xcodec/xcodec_lru.h). */
+void *xcr_cache_new_limited(uint64_t limit_bytes)
+{
+	UUID uuid;
+	return new XCodecMemoryCache(uuid, (size_t)limit_bytes);
+}
+
 void xcr_cache_free(void *c)
 {
 	RELEASE_CACHE((XCodecCache *)c);
