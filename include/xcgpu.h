@@ -84,6 +84,17 @@ int xcg_ctx_create(int device, uint32_t flags, xcg_ctx **out);
  * segments (XCodecMemoryCache(uuid, limit), xcodec/xcodec_cache.h:277; here
  * exceeding it is an error, XCG_EOVERFLOW, not an LRU eviction). */
 int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_ctx **out);
+/* A context whose persistent cache is the BOUNDED XCodecMemoryCache(uuid,
+ * memory_cache_limit_bytes) (xcodec/xcodec_cache.h:277-364; wanproxy.conf's
+ * `set <cache>.size`, programs/wanproxy/wanproxy_config_class_cache.cc:66):
+ * limit = bytes / 2048 segments (at least 1); entering at the limit evicts the
+ * least recently entered-or-looked-up segment (XCodecLRU, xcodec/xcodec_lru.h).
+ * XCG_SEM_STREAM batches stay bit-exact with the sequential encoder; a chunk
+ * whose own cache references (declarations + REFs + collision lookups) exceed
+ * the limit is XCG_ENOTSUP, as is XCG_SEM_INDEPENDENT with chunks of more than
+ * limit * 2048 bytes, and (this version) decoding and the single-segment host
+ * calls on a bounded context. */
+int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_ctx **out);
 void xcg_ctx_destroy(xcg_ctx *ctx);
 
 /* Persistent cache: number of segments held / drop everything. */

@@ -14,61 +14,36 @@
 #include <vector>
 
 #include "../../include/xcgpu.h"
+#include "xcg_args.h"
 
 extern "C" int xcg_launch_encode_independent(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t,
                                              uint32_t, uint8_t*, const uint64_t*, uint64_t*, uint32_t*, int32_t*,
                                              hipStream_t);
 extern "C" int xcg_launch_window_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
 
-struct XcgStreamArgs {
-  const uint8_t* in;
-  const uint64_t* chunk_off;
-  const uint32_t* chunk_len;
-  uint32_t n;
-  uint32_t flags;
-  uint8_t* out;
-  const uint64_t* out_off;
-  uint64_t* out_len;
-  uint32_t* stats;
-  int32_t* status;
-  uint64_t* g_keys;
-  uint64_t* g_vals;
-  uint32_t g_mask;
-  uint8_t* pool;
-  uint32_t* nseg;
-  uint32_t seg_cap;
-  uint32_t* g_filt;
-  uint32_t* g_ftab;
-  uint32_t fmask;
-  uint64_t* b_keys;
-  uint64_t* b_vals;
-  uint32_t b_mask;
-  uint32_t* r_filt;
-  uint32_t* r_ftab;
-  void* decl;
-  uint32_t* ndecl;
-  uint32_t maxd;
-  uint32_t* changed;
-  uint32_t* h_changed;
-  uint32_t* g_gfilt;
-  uint32_t* r_gfilt;
-  uint32_t gmask;
-  uint32_t* bcount;
-  uint64_t* b2_keys;
-  uint64_t* b2_vals;
-  uint64_t* r_keys;
-  uint64_t* r_vals;
-  uint32_t r_mask;
-  uint64_t* hits;
-  uint32_t* nhits;
-  uint32_t maxh;
-  uint32_t* need;
-  uint32_t* vflags;
-  uint32_t* h_vflags;
-  int seed;
-  uint32_t* decls_out;
+
+// Bounded cache (xcg_lru.hip).
+struct XcgLruState {
+  uint32_t C;
+  uint64_t* skey;
+  uint64_t* lastref;
+  uint32_t* queue;
+  uint32_t* queue2;
+  uint64_t* ptime;
+  uint64_t* hmin;
+  uint64_t* wpop;
+  uint64_t* tau;
+  uint32_t* alive;
+  uint32_t* freel;
+  uint32_t* evslot;
+  uint64_t* evtime;
+  uint32_t* ev_base;
+  uint32_t* enter_base;
+  uint32_t* tot;
+  uint32_t* h_tot;
+  uint64_t clock;
 };
-extern "C" int xcg_launch_encode_stream(const XcgStreamArgs*, int*, hipStream_t);
+extern "C" int xcg_lru_encode_stream(const XcgStreamArgs*, XcgLruState*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
 
 struct XcgDecodeArgs {
@@ -163,6 +138,12 @@ struct BatchScratch {
   uint32_t* vflags = nullptr;
   uint32_t* h_vflags = nullptr;    // pinned
   uint32_t last_maxd = 0;          // declaration stride of the last stream batch
+  // bounded cache: every chunk's cache references (xcg_lru.hip)
+  void* ev = nullptr;              // n_cap * maxe uint4
+  uint32_t* nev = nullptr;
+  uint32_t maxe = 0;
+  uint32_t* ev_base = nullptr;     // n_cap + 1
+  uint32_t* enter_base = nullptr;  // n_cap + 1
 };
 
 struct DecodeScratch {
@@ -204,6 +185,8 @@ struct xcg_ctx {
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
   int32_t* h_status = nullptr;     // pinned copy of d_status
   bool seed_next = false;          // the last stream batch declared something: seed the next one
+  bool bounded = false;            // XCodecMemoryCache with a limit: LRU eviction (xcg_lru.hip)
+  XcgLruState lru{};
 };
 
 namespace {
@@ -236,6 +219,34 @@ void free_cache(GpuCache& g) {
   g = GpuCache{};
 }
 
+void free_lru(XcgLruState& L) {
+  (void)hipFree(L.skey); (void)hipFree(L.lastref); (void)hipFree(L.queue); (void)hipFree(L.queue2);
+  (void)hipFree(L.ptime); (void)hipFree(L.hmin); (void)hipFree(L.wpop); (void)hipFree(L.tau);
+  (void)hipFree(L.alive); (void)hipFree(L.freel); (void)hipFree(L.evslot); (void)hipFree(L.evtime);
+  (void)hipFree(L.tot);
+  if (L.h_tot) (void)hipHostFree(L.h_tot);
+  const uint32_t C = L.C;
+  L = XcgLruState{};
+  L.C = C;
+}
+
+int alloc_lru(XcgLruState& L) {
+  const uint64_t C = L.C;
+  if (hipMalloc(&L.skey, 8 * C) != hipSuccess || hipMalloc(&L.lastref, 8 * C) != hipSuccess ||
+      hipMalloc(&L.queue, 4 * C) != hipSuccess || hipMalloc(&L.queue2, 4 * C) != hipSuccess ||
+      hipMalloc(&L.ptime, 8 * C) != hipSuccess || hipMalloc(&L.hmin, 8 * C) != hipSuccess ||
+      hipMalloc(&L.wpop, 8 * C) != hipSuccess || hipMalloc(&L.tau, 8 * C) != hipSuccess ||
+      hipMalloc(&L.alive, 4 * C) != hipSuccess || hipMalloc(&L.freel, 4 * C) != hipSuccess ||
+      hipMalloc(&L.evslot, 4 * C) != hipSuccess || hipMalloc(&L.evtime, 8 * C) != hipSuccess ||
+      hipMalloc(&L.tot, 64) != hipSuccess || hipHostMalloc(&L.h_tot, 64) != hipSuccess ||
+      hipMemset(L.lastref, 0, 8 * C) != hipSuccess) {
+    free_lru(L);
+    return XCG_ENOMEM;
+  }
+  L.clock = 1;
+  return XCG_OK;
+}
+
 void free_scratch(BatchScratch& b) {
   (void)hipFree(b.b_keys); (void)hipFree(b.b_vals); (void)hipFree(b.r_filt); (void)hipFree(b.r_ftab);
   (void)hipFree(b.decl); (void)hipFree(b.ndecl); (void)hipFree(b.changed); (void)hipFree(b.r_gfilt);
@@ -244,6 +255,7 @@ void free_scratch(BatchScratch& b) {
   (void)hipFree(b.hits); (void)hipFree(b.nhits); (void)hipFree(b.need); (void)hipFree(b.vflags);
   if (b.h_vflags) (void)hipHostFree(b.h_vflags);
   if (b.h_changed) (void)hipHostFree(b.h_changed);
+  (void)hipFree(b.ev); (void)hipFree(b.nev); (void)hipFree(b.ev_base); (void)hipFree(b.enter_base);
   b = BatchScratch{};
 }
 
@@ -281,6 +293,7 @@ int ensure_cache(xcg_ctx* c) {
     return XCG_ENOMEM;
   }
   int rc = clear_cache(g);
+  if (rc == XCG_OK && c->bounded) rc = alloc_lru(c->lru);
   if (rc) free_cache(g);
   return rc;
 }
@@ -308,6 +321,14 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipHostMalloc(&b.h_vflags, 16) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
+  }
+  if (c->bounded) {
+    b.maxe = 2 * maxd + 64;        // declarations + REFs + collision lookups of one chunk
+    if (hipMalloc(&b.ev, 16ull * n * b.maxe) != hipSuccess || hipMalloc(&b.nev, 4ull * n) != hipSuccess ||
+        hipMalloc(&b.ev_base, 4ull * (n + 1)) != hipSuccess || hipMalloc(&b.enter_base, 4ull * (n + 1)) != hipSuccess) {
+      free_scratch(b);
+      return XCG_ENOMEM;
+    }
   }
   return XCG_OK;
 }
@@ -399,6 +420,19 @@ int xcg_ctx_create(int device, uint32_t flags, xcg_ctx** out) {
   return xcg_ctx_create_ex(device, flags, XCG_DEFAULT_CACHE_SEGMENTS, out);
 }
 
+int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_ctx** out) {
+  if (!out || memory_cache_limit_bytes == 0) return XCG_EINVAL;
+  // memory_cache_limit_ = bytes / XCODEC_SEGMENT_LENGTH, at least 1 (xcodec_cache.h:277-288)
+  uint64_t segs = memory_cache_limit_bytes / XCG_SEGMENT_LENGTH;
+  if (segs == 0) segs = 1;
+  if (segs > (1ull << 29) || (flags & XCG_FLAG_NULLCACHE)) return XCG_EINVAL;
+  const int rc = xcg_ctx_create_ex(device, flags, segs, out);
+  if (rc != XCG_OK) return rc;
+  (*out)->bounded = true;
+  (*out)->lru.C = (uint32_t)segs;
+  return XCG_OK;
+}
+
 int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_ctx** out) {
   if (!out || cache_segments == 0 || cache_segments > (1ull << 30)) return XCG_EINVAL;
   *out = nullptr;
@@ -427,6 +461,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
   free_cache(c->g);
+  free_lru(c->lru);
   free_scratch(c->bs);
   free_dscratch(c->ds);
   window_free(c->own_win);
@@ -447,6 +482,7 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
   if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
+  c->lru.clock = 1;
   return clear_cache(c->g);
 }
 
@@ -486,6 +522,7 @@ int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
 
 int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
   if (!c || !seg_out) return XCG_EINVAL;
+  if (c->bounded) return XCG_ENOTSUP;
   int32_t found = 0;
   const int rc = host_seg_call(c, hash, nullptr, seg_out, 0, &found);
   if (rc != XCG_OK) return rc;
@@ -494,6 +531,7 @@ int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
 
 int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
   if (!c || !seg) return XCG_EINVAL;
+  if (c->bounded) return XCG_ENOTSUP;
   int32_t res = 0;
   const int rc = host_seg_call(c, hash, seg, nullptr, 1, &res);
   if (rc != XCG_OK) return rc;
@@ -570,7 +608,7 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
                     c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
                     c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount, c->bs.b2_keys, c->bs.b2_vals,
                     c->bs.r_keys, c->bs.r_vals, c->bs.r_mask, c->bs.hits, c->bs.nhits, c->bs.maxh, c->bs.need,
-                    c->bs.vflags, c->bs.h_vflags, 0, nullptr};
+                    c->bs.vflags, c->bs.h_vflags, 0, nullptr, nullptr, nullptr, nullptr, 0u, 0, 0};
     // Seed the rounds with the chunks' 2048-byte tilings instead of a parse
     // round 0 when the last batch declared segments (cold / growing caches);
     // a warm cache's all-REF batches keep round 0, which then is all they need.
@@ -579,11 +617,24 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
     uint32_t decls = ~0u;
     a.decls_out = &decls;
     int rounds = 0;
+    if (c->bounded) {
+      a.ev = c->bs.ev;
+      a.nev = c->bs.nev;
+      a.maxe = c->bs.maxe;
+      c->lru.ev_base = c->bs.ev_base;
+      c->lru.enter_base = c->bs.enter_base;
+      rc = xcg_lru_encode_stream(&a, &c->lru, &rounds, (hipStream_t)stream);
+      c->last_rounds = rounds;
+      return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : (rc == -95 ? XCG_ENOTSUP : XCG_EHIP));
+    }
     rc = xcg_launch_encode_stream(&a, &rounds, (hipStream_t)stream);
     if (decls != ~0u) c->seed_next = decls > 0;
     c->last_rounds = rounds;
     return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : XCG_EHIP);
   }
+  // A fresh bounded cache per chunk evicts nothing while the chunk's
+  // declarations fit the limit (at most max_chunk_len / 2048 of them).
+  if (c->bounded && max_chunk_len / XCG_SEGMENT_LENGTH > c->lru.C) return XCG_ENOTSUP;
   int rc = xcg_launch_encode_independent(d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, c->flags, d_out,
                                          d_out_off, d_out_len, d_stats, c->d_status, (hipStream_t)stream);
   return rc == 0 ? XCG_OK : (rc == -22 ? XCG_EINVAL : XCG_EHIP);
@@ -666,6 +717,7 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   if (h_nunknown) *h_nunknown = 0;
   if (h_total_out) *h_total_out = 0;
   if (n == 0) return XCG_OK;
+  if (c->bounded) return XCG_ENOTSUP;
   DeviceGuard g(c->device);
   int rc = ensure_cache(c);
   if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));

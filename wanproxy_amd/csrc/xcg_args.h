@@ -1,0 +1,68 @@
+// Arguments of the stream-semantics encode driver (xcg_launch_encode_stream),
+// shared by xcg_api.hip (the caller) and xcg_lru.hip (the bounded-cache pass).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct XcgStreamArgs {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  uint32_t n;
+  uint32_t flags;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint64_t* out_len;
+  uint32_t* stats;
+  int32_t* status;
+  // persistent cache
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  // batch scratch
+  uint64_t* b_keys;
+  uint64_t* b_vals;
+  uint32_t b_mask;
+  uint32_t* r_filt;
+  uint32_t* r_ftab;
+  void* decl;             // uint4 rows
+  uint32_t* ndecl;
+  uint32_t maxd;
+  uint32_t* changed;
+  uint32_t* h_changed;   // pinned host word
+  uint32_t* g_gfilt;     // global lane filters: the cache's and the round's copy
+  uint32_t* r_gfilt;
+  uint32_t gmask;
+  uint32_t* bcount;      // [64]
+  // verification: a second batch table (tables alternate between rounds), the
+  // changed-hash table, per-chunk batch hits, flags
+  uint64_t* b2_keys;
+  uint64_t* b2_vals;
+  uint64_t* r_keys;
+  uint64_t* r_vals;
+  uint32_t r_mask;
+  uint64_t* hits;
+  uint32_t* nhits;
+  uint32_t maxh;
+  uint32_t* need;
+  uint32_t* vflags;      // [0] a_first, [1] any, [2] declarations in the last table built
+  uint32_t* h_vflags;    // pinned
+  int seed;              // start from the tiling seed instead of round 0
+  uint32_t* decls_out;   // (host) declarations the batch made, ~0 if unknown
+  // bounded (LRU) cache: eviction times per pool slot, the reference lists,
+  // and whether the driver commits (the LRU pass commits itself)
+  const uint64_t* ptime;
+  void* ev;
+  uint32_t* nev;
+  uint32_t maxe;
+  int no_commit;
+  int keep_decls;        // start from the declaration lists already in decl/ndecl
+};
+
+extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);

@@ -22,6 +22,16 @@ constexpr int FILT_LOG2 = 19;                       // 2^19 bits = 64 KiB of LDS
 constexpr uint32_t FILT_WORDS = (1u << FILT_LOG2) / 32;
 constexpr uint32_t FOVF16 = 2u;                     // bucket-overflow flag in slot 7 (even: never a fingerprint)
 
+// Bounded (LRU) cache: kinds of the cache references a stream chunk records
+// (bits 30..31 of an event's .w; the low 30 bits are the declaration index of
+// an ENTER or the pool slot of a GHIT / GMISS).
+//   ENTER  encode_declaration's enter() (xcodec_encoder.cc:284-286)
+//   HIT    a lookup that found a declaration of this batch
+//   GHIT   a lookup that found a persistent entry (lookup() refreshes it)
+//   GMISS  a lookup of a persistent entry the LRU had evicted by then
+constexpr uint32_t EV_ENTER = 0, EV_HIT = 1, EV_GHIT = 2, EV_GMISS = 3;
+constexpr uint32_t EV_REF_MASK = (1u << 30) - 1u;
+
 struct HashTab {      // exact open-addressed map u64 -> u64
   uint64_t* keys;
   uint64_t* vals;

@@ -32,6 +32,7 @@
 #include <type_traits>
 
 #include "xcg_cache.h"
+#include "xcg_args.h"
 #include "../../include/xcgpu.h"
 
 namespace xcg {
@@ -99,6 +100,11 @@ struct EncParams {
   uint32_t* nhits;     // [n] (> maxh: overflowed, always re-parsed)
   uint32_t maxh;
   uint32_t max_len;    // the caller's bound on every chunk length (sizes LDS records and declaration rows)
+  // ---- bounded (LRU) cache only (xcg_lru.hip); null otherwise
+  const uint64_t* ptime;  // [pool slot] batch time from which the entry is evicted (~0: never)
+  uint4* ev;           // [n * maxe] the chunk's cache references in order (lo, hi, time, kind << 30 | ref)
+  uint32_t* nev;       // [n] (> maxe: overflowed)
+  uint32_t maxe;
 };
 
 // ------------------------------------------------------------------ emission
@@ -470,7 +476,7 @@ struct GlbView {
   int fmode;   // 0: no probe, 1: LDS lane filter, 2: global lane filter
 };
 
-template <int LOGNB, int MAXD, bool STREAM>
+template <int LOGNB, int MAXD, bool STREAM, bool LRU = false>
 __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, const uint32_t kofs,
                                              WaveRecs<LOGNB, MAXD>& T, const uint32_t chunk, const GlbView gs) {
   constexpr int NB = 1 << LOGNB;
@@ -582,14 +588,33 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   // A batch hit is recorded: the verification after the round re-parses the
   // chunk if that declaration's visibility or bytes change (xcg_verify_*).
   uint32_t nh = 0;
-  auto cache_src = [&](uint32_t lo, uint32_t hi) -> const uint8_t* {
+  // Bounded cache: every reference the chunk makes to the cache, in order --
+  // enter (declaration d), lookup hit (XCodecMemoryCache::lookup refreshes the
+  // entry's recency whether or not the bytes then match, xcodec_cache.h:348-364),
+  // and a lookup of a persistent entry the LRU has evicted by then.  The
+  // LRU pass (xcg_lru.hip) derives the eviction times from these.
+  uint32_t ne = 0;
+  auto record = [&](uint32_t lo, uint32_t hi, uint32_t t, uint32_t kind, uint32_t ref) {
+    if (ne < prm.maxe && l == 0) prm.ev[(uint64_t)chunk * prm.maxe + ne] = make_uint4(lo, hi, t, (kind << 30) | ref);
+    ++ne;
+  };
+  auto cache_src = [&](uint32_t lo, uint32_t hi, int at) -> const uint8_t* {
     const uint64_t gv = tab_lookup(prm.g, lo, hi);
-    if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+    if (gv != ~0ull) {
+      if (!LRU) return prm.pool + gv * (uint64_t)SEG;
+      const uint32_t t = 2u * (uint32_t)at + 1u;
+      if ((((uint64_t)chunk << 21) | t) < prm.ptime[gv]) {
+        record(lo, hi, t, EV_GHIT, (uint32_t)gv);
+        return prm.pool + gv * (uint64_t)SEG;
+      }
+      record(lo, hi, t, EV_GMISS, (uint32_t)gv);   // evicted earlier in the batch
+    }
     if (prm.use_b) {
       const uint64_t bv = tab_lookup(prm.b, lo, hi);
       if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) {
         if (nh < prm.maxh && l == 0) prm.hits[(uint64_t)chunk * prm.maxh + nh] = ((uint64_t)hi << 32) | lo;
         ++nh;
+        if (LRU) record(lo, hi, 2u * (uint32_t)at + 1u, EV_HIT, 0u);
         return prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
       }
     }
@@ -607,8 +632,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   };
   bool chain = false;                              // the last op was a REF
 
-  // encode_declaration (xcodec_encoder.cc:276-313).
-  auto declare = [&]() {
+  // encode_declaration (xcodec_encoder.cc:276-313), made while examining
+  // window `at` (the enter precedes that window's lookup).
+  auto declare = [&](int at) {
+    if (LRU) record(cand_lo, cand_hi, 2u * (uint32_t)at, EV_ENTER, n_extract);
     if (cand > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)cand);
     if (!nullcache && !c0_in_table) insert(cand_lo, cand_hi, (uint32_t)cand);
     if (oob) {
@@ -698,7 +725,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       }
       const int d = lookup(lo, hi);                 // stream records carry their hi
       const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
-      if (src == nullptr && glb_maybe(probe_key(lo))) src = cache_src(lo, hi);
+      if (LRU && d >= 0) record(lo, hi, 2u * (uint32_t)s + 1u, EV_HIT, 0u);
+      if (src == nullptr && glb_maybe(probe_key(lo))) src = cache_src(lo, hi, s);
       if (src != nullptr && equal2048_u(src, x + s)) {
         wave_put_ref(out + olen, lo, hi);           // encode_reference :342-372
         olen += 10;
@@ -795,7 +823,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     };
 
     while (s < pe) {
-      if (have_cand && cand + SEG <= s) declare();            // :183-190
+      if (have_cand && cand + SEG <= s) declare(s);           // :183-190
       const int e = nullcache ? INT32_MAX : next_event(s);
       if (e == s) {
         // Exact re-check of the probe (find_reference, :374-416).  A record
@@ -819,7 +847,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // Where the hash is declared: this chunk (d), the persistent cache, or
         // an earlier chunk of the batch.  src = that segment's bytes.
         const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
-        if (STREAM && src == nullptr) src = cache_src(lo, hi);
+        if (LRU && d >= 0) record(lo, hi, 2u * (uint32_t)s + 1u, EV_HIT, 0u);
+        if (STREAM && src == nullptr) src = cache_src(lo, hi, s);
         if (src != nullptr) {
           if (equal2048_u(src, x + s)) {
             if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
@@ -869,7 +898,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     totXA = totXB; totTA = totTB;
   }
 
-  if (have_cand) declare();                                   // :257-261
+  if (have_cand) declare(last + 1);                           // :257-261 (after every lookup)
   if (base < L) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
   if (STREAM) {
     // This round's declarations; flag a change against the previous round's.
@@ -888,6 +917,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     if (l == 0) {
       prm.ndecl[chunk] = ndecl;
       prm.nhits[chunk] = nh;
+      if (LRU) prm.nev[chunk] = ne;
     }
   }
   if (l == 0) {
@@ -924,7 +954,7 @@ __global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams pr
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
 // the lane filter; each wave walks chunks wave_id, wave_id + total_waves, ...
-template <int LOGNB, int MAXD, int SW>
+template <int LOGNB, int MAXD, int SW, bool LRU>
 __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   using L = StreamLDS<LOGNB, MAXD, SW>;
   __shared__ L S;
@@ -945,14 +975,16 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
     if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;   // verified: its parse stands
-    encode_chunk<LOGNB, MAXD, true>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
+    encode_chunk<LOGNB, MAXD, true, LRU>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
   }
 }
 
 template __global__ void encode_independent_kernel<10, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
-template __global__ void encode_stream_kernel<8, 72, 16>(EncParams);
-template __global__ void encode_stream_kernel<10, 264, 6>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 16, false>(EncParams);
+template __global__ void encode_stream_kernel<10, 264, 6, false>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 16, true>(EncParams);
+template __global__ void encode_stream_kernel<10, 264, 6, true>(EncParams);
 
 }  // namespace xcg
 
@@ -1247,58 +1279,7 @@ __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const ui
 
 }  // namespace xcg
 
-struct XcgStreamArgs {
-  const uint8_t* in;
-  const uint64_t* chunk_off;
-  const uint32_t* chunk_len;
-  uint32_t n;
-  uint32_t flags;
-  uint8_t* out;
-  const uint64_t* out_off;
-  uint64_t* out_len;
-  uint32_t* stats;
-  int32_t* status;
-  // persistent cache
-  uint64_t* g_keys;
-  uint64_t* g_vals;
-  uint32_t g_mask;
-  uint8_t* pool;
-  uint32_t* nseg;
-  uint32_t seg_cap;
-  uint32_t* g_filt;
-  uint32_t* g_ftab;
-  uint32_t fmask;
-  // batch scratch
-  uint64_t* b_keys;
-  uint64_t* b_vals;
-  uint32_t b_mask;
-  uint32_t* r_filt;
-  uint32_t* r_ftab;
-  uint4* decl;
-  uint32_t* ndecl;
-  uint32_t maxd;
-  uint32_t* changed;
-  uint32_t* h_changed;   // pinned host word
-  uint32_t* g_gfilt;     // global lane filters: the cache's and the round's copy
-  uint32_t* r_gfilt;
-  uint32_t gmask;
-  uint32_t* bcount;      // [64]
-  // verification: a second batch table (tables alternate between rounds), the
-  // changed-hash table, per-chunk batch hits, flags
-  uint64_t* b2_keys;
-  uint64_t* b2_vals;
-  uint64_t* r_keys;
-  uint64_t* r_vals;
-  uint32_t r_mask;
-  uint64_t* hits;
-  uint32_t* nhits;
-  uint32_t maxh;
-  uint32_t* need;
-  uint32_t* vflags;      // [0] a_first, [1] any, [2] declarations in the last table built
-  uint32_t* h_vflags;    // pinned
-  int seed;              // start from the tiling seed instead of round 0
-  uint32_t* decls_out;   // (host) declarations the batch made, ~0 if unknown
-};
+
 
 // LDS / global lane filter threshold (keys): XCG_LDS_FILTER_KEYS at load
 // time, or xcg_debug_set_lds_filter_keys (tests force either mode with it).
@@ -1320,14 +1301,18 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.g = HashTab{a->g_keys, a->g_vals, a->g_mask};
   prm.pool = a->pool;
   prm.b = HashTab{a->b_keys, a->b_vals, a->b_mask};
-  prm.decl = a->decl;
+  prm.decl = (uint4*)a->decl;
   prm.ndecl = a->ndecl;
   prm.maxd = a->maxd;
   prm.changed = a->changed;
   prm.nseg = a->nseg;
   prm.bcount = a->bcount;
   prm.lds_filter_keys = xcg_lds_filter_keys();
-  const size_t fbytes = (size_t)FILT_WORDS * 4, tbytes = ((size_t)a->fmask + 1) * 16;
+  prm.ptime = a->ptime;
+  prm.ev = (uint4*)a->ev;
+  prm.nev = a->nev;
+  prm.maxe = a->maxe;
+  const size_t tbytes = ((size_t)a->fmask + 1) * 16;
   const size_t gbytes = ((size_t)a->gmask + 1) * 4;
   int dev = 0;
   hipDeviceProp_t props;
@@ -1337,8 +1322,13 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const uint32_t SW = big ? 6 : 16;               // one workgroup per CU (LDS)
   const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
   auto launch = [&]() {
-    if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6>), sgrid, sblock, 0, stream, prm);
-    else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16>), sgrid, sblock, 0, stream, prm);
+    if (prm.ev) {   // bounded cache: record the chunks' cache references (xcg_lru.hip)
+      if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6, true>), sgrid, sblock, 0, stream, prm);
+      else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, true>), sgrid, sblock, 0, stream, prm);
+    } else {
+      if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6, false>), sgrid, sblock, 0, stream, prm);
+      else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, false>), sgrid, sblock, 0, stream, prm);
+    }
   };
   // lowest chunk whose declaration list changed in the round just run (~0u: none)
   auto changed_after = [&](uint32_t& fc) -> bool {
@@ -1348,7 +1338,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     fc = *a->h_changed;
     return true;
   };
-  const bool seeded = a->seed && n > 1;
+  const bool keep = a->keep_decls && n > 1;
+  const bool seeded = (a->seed || keep) && n > 1;
   if (!seeded && (hipMemsetAsync(a->ndecl, 0, 4ull * n, stream) != hipSuccess ||
                   hipMemsetAsync(a->nhits, 0, 4ull * n, stream) != hipSuccess ||
                   hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess))
@@ -1364,7 +1355,10 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask, a->g_gfilt, a->gmask};
   int rounds = 0;
   uint32_t fc = 0;
-  if (seeded) {
+  if (keep) {
+    // the previous pass's declaration lists seed round 1 (a bounded cache's
+    // eviction times changed under them)
+  } else if (seeded) {
     hipLaunchKernelGGL(seed_tiling_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
                        a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
   } else {
@@ -1389,6 +1383,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   // if the verification that precedes it in the stream flagged nothing.
   bool committed = false;
   auto commit = [&](const uint32_t* gate) {
+    if (a->no_commit) return;
     const uint32_t parts = (a->maxd + 255) / 256;
     uint32_t* seg_base = (uint32_t*)a->hits;       // (free once the rounds are over: n words)
     hipLaunchKernelGGL(commit_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)a->ndecl, n, seg_base,

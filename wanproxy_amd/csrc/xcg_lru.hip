@@ -1,0 +1,436 @@
+// Bounded persistent cache: XCodecMemoryCache with memory_cache_limit_ != 0
+// (xcodec/xcodec_cache.h:277-364) -- at the limit, enter() first evicts the
+// least recently used entry; lookup() and replace() refresh an entry
+// (XCodecLRU, xcodec/xcodec_lru.h:30-104).  Stream-semantics batches stay
+// bit-exact with the sequential encoder.
+//
+// LRU state in HBM (C = limit in segments = pool slots):
+//   skey[C]     key of the entry in pool slot s
+//   lastref[C]  LRU time of its last enter / lookup (a 64-bit clock: batch
+//               base + (chunk << 21 | 2 * window + 1 for a lookup, 2 * window
+//               for an enter)) -- the order XCodecLRU's counters give
+//   queue[A]    the A live slots, least recently used first
+//
+// Within one batch (at most C references, so nothing the batch itself
+// references can be evicted before the batch ends -- that takes C newer
+// distinct references), the entries evicted are persistent ones: enter number
+// C - A + j (in stream order) evicts the j-th least recently used persistent
+// entry not looked up in the batch before that point.  For a persistent entry
+// of LRU rank r, with S(r) entries below it that the batch looks up, that is
+// eviction j = r - S(r) at tau[j], unless the batch looks it up first.  The
+// parse takes these eviction times (ptime) as given; the pass below recomputes
+// them from the references the parse made and checks every recorded lookup of
+// a persistent entry against them -- a hit must come before the entry's
+// eviction, a miss (GMISS) after it.  All checks passing means the parse is
+// the sequential one (by induction over stream time: every lookup result then
+// equals the LRU state the sequential encoder has at that point); otherwise
+// the batch is parsed again with the new times.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "xcg_cache.h"
+#include "xcg_args.h"
+
+namespace xcg {
+
+constexpr uint64_t NEVER = ~0ull;
+enum : uint32_t { T_E = 0, T_N, T_P, T_A, T_BAD, T_OVF, T_A2, T_NFREE, T_WORDS = 16 };
+
+// Ordered scan by one 1024-thread workgroup over i in [0, n): emit(i, p, v)
+// with p = carry + sum of val(j) for j < i.  Returns carry + the total.
+template <class V, class E>
+__device__ uint32_t wg_scan(uint32_t n, uint32_t carry, V val, E emit) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, w = t >> 6;
+  for (uint32_t base = 0; base < n; base += 4096) {
+    const uint32_t i0 = base + 4 * t;
+    uint32_t x[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = i0 + k < n ? val(i0 + k) : 0u;
+      sum += x[k];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if (lane_id() == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t s = wsum[j];
+      if (j < w) wpre += s;
+      tot += s;
+    }
+    uint32_t run = carry + wpre + inc - sum;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < n) emit(i0 + k, run, x[k]);
+      run += x[k];
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  return carry;
+}
+
+__device__ __forceinline__ uint64_t ev_time(uint32_t c, uint4 e) { return ((uint64_t)c << 21) | e.z; }
+
+__global__ __launch_bounds__(256) void lru_fill64_kernel(uint64_t* p, uint32_t n, uint64_t v) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+__global__ __launch_bounds__(256) void lru_fill32_kernel(uint32_t* p, uint32_t n, uint32_t v) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+
+// Per-chunk reference / enter bases, batch totals, the eviction count.
+__global__ __launch_bounds__(1024) void lru_prep_kernel(uint32_t n, const uint32_t* nev, const uint32_t* ndecl,
+                                                        uint32_t maxe, uint32_t C, const uint32_t* nseg,
+                                                        uint32_t* ev_base, uint32_t* enter_base, uint32_t* tot) {
+  if (threadIdx.x == 0) tot[T_OVF] = 0;
+  __syncthreads();
+  const uint32_t e = wg_scan(
+      n, 0u,
+      [&](uint32_t i) {
+        const uint32_t v = nev[i];
+        if (v > maxe) atomicOr(&tot[T_OVF], 1u);
+        return v < maxe ? v : maxe;
+      },
+      [&](uint32_t i, uint32_t p, uint32_t) { ev_base[i] = p; });
+  const uint32_t ne = wg_scan(n, 0u, [&](uint32_t i) { return ndecl[i]; },
+                              [&](uint32_t i, uint32_t p, uint32_t) { enter_base[i] = p; });
+  if (threadIdx.x == 0) {
+    ev_base[n] = e;
+    enter_base[n] = ne;
+    const uint32_t A = *nseg;
+    tot[T_E] = e;
+    tot[T_N] = ne;
+    tot[T_A] = A;
+    tot[T_P] = A + ne > C ? A + ne - C : 0u;
+    tot[T_BAD] = 0;
+  }
+}
+
+// tau[j] = time of the enter that makes eviction j; hmin[s] = first lookup hit
+// of persistent slot s.
+__global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
+                                                         const uint32_t* nev, const uint32_t* enter_base,
+                                                         const uint32_t* tot, uint32_t C, uint64_t* hmin,
+                                                         uint64_t* tau) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
+  if (c >= n || k >= min(nev[c], maxe)) return;
+  const uint4 e = ev[i];
+  const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+  if (kind == EV_ENTER) {
+    const uint32_t ge = enter_base[c] + ref, thr = C - tot[T_A];
+    if (ge >= thr) tau[ge - thr] = ev_time(c, e);
+  } else if (kind == EV_GHIT) {
+    atomicMin((unsigned long long*)&hmin[ref], (unsigned long long)ev_time(c, e));
+  }
+}
+
+// Walk the persistent entries in LRU order: wpop[s] = when the batch's
+// evictions reach slot s (tau[r - S(r)]), ptime[s] = that, unless the batch
+// looks s up before then (then never).
+__global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, const uint32_t* tot,
+                                                        const uint64_t* hmin, const uint64_t* tau, uint64_t* wpop,
+                                                        uint64_t* ptime) {
+  const uint32_t A = tot[T_A], P = tot[T_P];
+  wg_scan(
+      A, 0u, [&](uint32_t r) { return hmin[queue[r]] != NEVER ? 1u : 0u; },
+      [&](uint32_t r, uint32_t S, uint32_t h) {
+        const uint32_t s = queue[r], j = r - S;
+        const uint64_t w = j < P ? tau[j] : NEVER;
+        wpop[s] = w;
+        ptime[s] = h && hmin[s] < w ? NEVER : w;   // (a hit after the eviction did not happen)
+      });
+}
+
+// Every recorded lookup of a persistent entry against the recomputed times.
+__global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
+                                                        const uint32_t* nev, const uint64_t* hmin,
+                                                        const uint64_t* wpop, uint32_t* tot) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
+  bool bad = false;
+  if (c < n && k < min(nev[c], maxe)) {
+    const uint4 e = ev[i];
+    const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+    const uint64_t t = ev_time(c, e);
+    if (kind == EV_GHIT) bad = t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
+    else if (kind == EV_GMISS) bad = !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
+  }
+  if (ballot(bad) != 0 && lane_id() == 0) atomicAdd(&tot[T_BAD], 1u);
+}
+
+// ---- commit
+
+__global__ __launch_bounds__(256) void lru_mark_kernel(const uint32_t* tot, const uint32_t* queue,
+                                                       const uint64_t* hmin, const uint64_t* wpop, uint32_t* alive) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= tot[T_A]) return;
+  const uint32_t s = queue[r];
+  alive[s] = (hmin[s] == NEVER && wpop[s] != NEVER) ? 0u : 1u;   // evicted in the batch
+}
+
+__global__ __launch_bounds__(1024) void lru_free_kernel(uint32_t C, const uint32_t* alive, uint32_t* freel,
+                                                        uint32_t* tot) {
+  const uint32_t nf = wg_scan(C, 0u, [&](uint32_t s) { return alive[s] ? 0u : 1u; },
+                              [&](uint32_t s, uint32_t p, uint32_t v) {
+                                if (v) freel[p] = s;
+                              });
+  if (threadIdx.x == 0) tot[T_NFREE] = nf;
+}
+
+struct Wipe {
+  HashTab g;
+  uint32_t* filt;
+  u32x4* ftab; uint32_t ftab_n;
+  uint32_t* gfilt; uint32_t gfilt_n;
+};
+__global__ __launch_bounds__(256) void lru_wipe_kernel(Wipe w) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i <= w.g.mask; i += stride) { w.g.keys[i] = EMPTY_KEY; w.g.vals[i] = ~0ull; }
+  for (uint64_t i = i0; i < FILT_WORDS; i += stride) w.filt[i] = 0u;
+  for (uint64_t i = i0; i < w.ftab_n; i += stride) w.ftab[i] = u32x4{0u, 0u, 0u, 0u};
+  for (uint64_t i = i0; i < w.gfilt_n; i += stride) w.gfilt[i] = 0u;
+}
+
+__global__ __launch_bounds__(256) void lru_insert_alive_kernel(uint32_t C, const uint32_t* alive,
+                                                               const uint64_t* skey, HashTab g, FiltSet fs,
+                                                               int32_t* status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= C || !alive[s]) return;
+  const uint64_t k = skey[s];
+  if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), s)) atomicOr(status, 2);
+  filt_insert(fs, (uint32_t)k, (uint32_t)(k >> 32));
+}
+
+// One wave per declaration: its pool slot from the free list, key, table,
+// filters, and the 2048 bytes.
+__global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                             uint32_t maxd, const uint32_t* enter_base,
+                                                             const uint32_t* freel, const uint8_t* in,
+                                                             const uint64_t* chunk_off, uint64_t* skey,
+                                                             uint32_t* alive, HashTab g, uint8_t* pool, FiltSet fs,
+                                                             int32_t* status) {
+  const uint64_t w = (uint64_t)blockIdx.x * 4 + readfirst(threadIdx.x >> 6);
+  const uint32_t c = (uint32_t)(w / maxd), d = (uint32_t)(w % maxd);
+  if (c >= n || d >= ndecl[c]) return;
+  const uint4 dd = decl[(uint64_t)c * maxd + d];
+  const uint32_t s = freel[enter_base[c] + d];
+  if (lane_id() == 0) {
+    skey[s] = ((uint64_t)dd.y << 32) | dd.x;
+    alive[s] = 1u;
+    if (!tab_insert_min(g, dd.x, dd.y, s)) atomicOr(status, 2);
+    filt_insert(fs, dd.x, dd.y);
+  }
+  const uint8_t* src = in + chunk_off[c] + dd.z;
+  uint8_t* dst = pool + (uint64_t)s * SEG;
+  const int l = lane_id();
+  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+}
+
+// Every reference's slot (evslot, in stream order) and time; lastref = the
+// latest reference of each slot.
+__global__ __launch_bounds__(256) void lru_lastref_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
+                                                          const uint32_t* nev, const uint32_t* ev_base,
+                                                          const uint32_t* enter_base, const uint32_t* freel,
+                                                          HashTab g, uint64_t clock, uint64_t* lastref,
+                                                          uint32_t* evslot, uint64_t* evtime) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
+  if (c >= n || k >= min(nev[c], maxe)) return;
+  const uint4 e = ev[i];
+  const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+  uint32_t s = ~0u;
+  if (kind == EV_ENTER) s = freel[enter_base[c] + ref];
+  else if (kind == EV_GHIT) s = ref;
+  else if (kind == EV_HIT) s = (uint32_t)tab_lookup_t(g, e.x, e.y);
+  const uint64_t t = clock + ev_time(c, e);
+  const uint32_t gi = ev_base[c] + k;
+  evslot[gi] = s;
+  evtime[gi] = t;
+  if (s != ~0u) atomicMax((unsigned long long*)&lastref[s], (unsigned long long)t);
+}
+
+// The new LRU order: persistent entries the batch left alone, in their old
+// order, then every entry the batch referenced, by its last reference.
+__global__ __launch_bounds__(1024) void lru_queue_kernel(uint32_t* tot, const uint32_t* queue, const uint32_t* alive,
+                                                         const uint64_t* lastref, uint64_t clock,
+                                                         const uint32_t* evslot, const uint64_t* evtime,
+                                                         uint32_t* queue2, uint32_t* nseg) {
+  const uint32_t A = tot[T_A], E = tot[T_E];
+  const uint32_t p1 = wg_scan(
+      A, 0u,
+      [&](uint32_t r) {
+        const uint32_t s = queue[r];
+        return alive[s] && lastref[s] < clock ? 1u : 0u;
+      },
+      [&](uint32_t r, uint32_t p, uint32_t v) {
+        if (v) queue2[p] = queue[r];
+      });
+  const uint32_t p2 = wg_scan(
+      E, p1,
+      [&](uint32_t i) {
+        const uint32_t s = evslot[i];
+        return s != ~0u && lastref[s] == evtime[i] ? 1u : 0u;
+      },
+      [&](uint32_t i, uint32_t p, uint32_t v) {
+        if (v) queue2[p] = evslot[i];
+      });
+  if (threadIdx.x == 0) {
+    *nseg = p2;
+    tot[T_A2] = p2;
+  }
+}
+
+}  // namespace xcg
+
+struct XcgLruState {
+  uint32_t C;
+  uint64_t* skey;
+  uint64_t* lastref;
+  uint32_t* queue;
+  uint32_t* queue2;
+  uint64_t* ptime;
+  uint64_t* hmin;
+  uint64_t* wpop;
+  uint64_t* tau;
+  uint32_t* alive;
+  uint32_t* freel;
+  uint32_t* evslot;
+  uint64_t* evtime;
+  uint32_t* ev_base;      // [n_cap + 1]
+  uint32_t* enter_base;   // [n_cap + 1]
+  uint32_t* tot;          // [16]
+  uint32_t* h_tot;        // pinned [16]
+  uint64_t clock;
+};
+
+namespace {
+
+bool lru_debug() {
+  static const bool on = getenv("XCG_LRU_DEBUG") != nullptr;
+  return on;
+}
+
+unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
+
+// Recompute eviction times from the parse's references; h_tot gets the totals
+// (T_BAD = inconsistent lookups).  Synchronises `st`.
+int lru_analyze(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+  using namespace xcg;
+  const uint32_t n = a.n, maxe = a.maxe;
+  const uint4* ev = (const uint4*)a.ev;
+  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev,
+                     (const uint32_t*)a.ndecl, maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base,
+                     L->tot);
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
+                     L->hmin, L->C, NEVER);
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
+                     L->tau, L->C, NEVER);
+  const uint64_t ne = (uint64_t)n * maxe;
+  hipLaunchKernelGGL(lru_events_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
+                     (const uint32_t*)L->enter_base, (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
+  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue,
+                     (const uint32_t*)L->tot, (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
+  hipLaunchKernelGGL(lru_check_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
+                     (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->tot);
+  if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return -5;
+  return 0;
+}
+
+int lru_commit(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+  using namespace xcg;
+  const uint32_t n = a.n, maxe = a.maxe, C = L->C;
+  const unsigned cg = grid_for(C) < 1024 ? grid_for(C) : 1024;
+  hipLaunchKernelGGL(lru_fill32_kernel, dim3(cg), dim3(256), 0, st, L->alive, C, 0u);
+  hipLaunchKernelGGL(lru_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, (const uint32_t*)L->tot,
+                     (const uint32_t*)L->queue, (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->alive);
+  hipLaunchKernelGGL(lru_free_kernel, dim3(1), dim3(1024), 0, st, C, (const uint32_t*)L->alive, L->freel, L->tot);
+  const HashTab g{a.g_keys, a.g_vals, a.g_mask};
+  const FiltSet fs{a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask};
+  Wipe w{g, a.g_filt, (u32x4*)a.g_ftab, a.fmask + 1, a.g_gfilt, a.gmask + 1};
+  hipLaunchKernelGGL(lru_wipe_kernel, dim3(1024), dim3(256), 0, st, w);
+  hipLaunchKernelGGL(lru_insert_alive_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, (const uint32_t*)L->alive,
+                     (const uint64_t*)L->skey, g, fs, a.status);
+  const uint64_t waves = (uint64_t)n * a.maxd;
+  hipLaunchKernelGGL(lru_insert_new_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, n,
+                     (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->freel, a.in, a.chunk_off, L->skey, L->alive, g, a.pool, fs, a.status);
+  const uint64_t ne = (uint64_t)n * maxe;
+  hipLaunchKernelGGL(lru_lastref_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, (const uint4*)a.ev,
+                     (const uint32_t*)a.nev, (const uint32_t*)L->ev_base, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->freel, g, L->clock, L->lastref, L->evslot, L->evtime);
+  hipLaunchKernelGGL(lru_queue_kernel, dim3(1), dim3(1024), 0, st, L->tot, (const uint32_t*)L->queue,
+                     (const uint32_t*)L->alive, (const uint64_t*)L->lastref, L->clock, (const uint32_t*)L->evslot,
+                     (const uint64_t*)L->evtime, L->queue2, a.nseg);
+  if (hipGetLastError() != hipSuccess) return -5;
+  uint32_t* q = L->queue;
+  L->queue = L->queue2;
+  L->queue2 = q;
+  L->clock += ((uint64_t)n << 21) + 4;
+  return 0;
+}
+
+}  // namespace
+
+// Stream-semantics encode of a batch on a bounded cache.  The batch is cut
+// into sub-batches of at most C references (the bound the eviction rule above
+// needs; a sub-batch whose references exceed it is halved); each is parsed
+// (xcg_launch_encode_stream, commit off) until its eviction times are
+// consistent, then committed.  Returns 0, -75 (no fixed point / reference
+// list overflow), -95 (one chunk alone makes more than C references), -5.
+extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, int* rounds_out, hipStream_t st) {
+  using namespace xcg;
+  const uint32_t n = a0->n, C = L->C;
+  int rounds = 0;
+  const uint32_t per_chunk = 2 * a0->maxd;         // declarations + REFs a chunk can make (+ collisions)
+  uint32_t per = C / per_chunk ? C / per_chunk : 1u;
+  constexpr int MAX_PASSES = 12;
+  uint32_t i0 = 0;
+  while (i0 < n) {
+    const uint32_t m = per < n - i0 ? per : n - i0;
+    XcgStreamArgs a = *a0;
+    a.n = m;
+    a.chunk_off += i0;
+    a.chunk_len += i0;
+    a.out_off += i0;
+    a.out_len += i0;
+    if (a.stats) a.stats += 4ull * i0;
+    a.ptime = L->ptime;
+    a.no_commit = 1;
+    hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(C) < 1024 ? grid_for(C) : 1024), dim3(256), 0, st,
+                       L->ptime, C, NEVER);
+    bool done = false, split = false;
+    for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
+      a.keep_decls = pass > 0;
+      int r = 0;
+      const int rc = xcg_launch_encode_stream(&a, &r, st);
+      rounds += r;
+      if (rc) return rc;
+      if (lru_analyze(a, L, st)) return -5;
+      if (lru_debug())
+        fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u\n", i0,
+                m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
+                L->h_tot[T_OVF]);
+      if (L->h_tot[T_OVF]) return -75;
+      if (L->h_tot[T_E] > C) split = true;
+      else if (L->h_tot[T_BAD] == 0) done = true;
+    }
+    if (!done) {
+      if (m == 1) return split ? -95 : -75;
+      per = m / 2;                                   // redo this part in halves
+      continue;
+    }
+    if (lru_commit(a, L, st)) return -5;
+    i0 += m;
+  }
+  if (rounds_out) *rounds_out = rounds;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

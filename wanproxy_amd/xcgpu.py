@@ -66,6 +66,8 @@ def lib():
     L.xcg_ctx_create.restype = C.c_int
     L.xcg_ctx_create_ex.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_ex.restype = C.c_int
+    L.xcg_ctx_create_bounded.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_bounded.restype = C.c_int
     L.xcg_cache_size.argtypes = [vp]
     L.xcg_cache_size.restype = C.c_uint64
     L.xcg_cache_clear.argtypes = [vp]
@@ -134,14 +136,20 @@ class Context:
     """An XCodecEncoder + cache configuration bound to one GPU."""
 
     def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
-                 cache_segments: int = 1 << 19):
+                 cache_segments: int = 1 << 19, memory_cache_limit: int = 0):
+        """memory_cache_limit (bytes): the bounded, LRU-evicting cache
+        XCodecMemoryCache(uuid, memory_cache_limit) (xcodec/xcodec_cache.h:277)
+        instead of an unbounded one of cache_segments capacity."""
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        _check(lib().xcg_ctx_create_ex(device, self.flags, int(cache_segments), C.byref(h)))
+        if memory_cache_limit:
+            _check(lib().xcg_ctx_create_bounded(device, self.flags, int(memory_cache_limit), C.byref(h)))
+        else:
+            _check(lib().xcg_ctx_create_ex(device, self.flags, int(cache_segments), C.byref(h)))
         self.h = h
 
     # The persistent cache (XCG_SEM_STREAM): XCodecMemoryCache of the encoder.
