@@ -13,6 +13,8 @@ a GPU decode round trip.
   c4   131072 x 4 KiB packets (one GPU's shard of 1 M), seed 0xC4, dup 4
   c5   1 GiB (one GPU's shard of 8 GiB) in 128 KiB chunks, seed 0xC5, dup 20,
        cold unbounded cache, batches of --batch-mib
+  c5lru  c5 with a bounded --lru-mib (128) MiB LRU cache (wanproxy.conf's
+       memory cache), checked against the oracle's bounded cache
 
 Prints one JSON line per config.  --scale shrinks the inputs (tests).
 """
@@ -268,6 +270,41 @@ def run_c5(args):
             'rounds': B.rounds, 'checked': f'first {k} chunks vs oracle; full decode round trip'}
 
 
+def run_c5lru(args):
+    """C5 with wanproxy.conf's primary cache: a bounded 128 MiB
+    XCodecMemoryCache (LRU eviction) instead of an unbounded one."""
+    from oracle.lib import Oracle
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
+    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    limit = args.lru_mib * MiB
+    ctx = Context(0, memory_cache_limit=limit)
+    per = max(1, args.batch_mib * MiB // (128 * KiB))
+    B = Batches(ctx, data, offs, lens, per=per)
+    wall = timed_encode(B, args.reps)
+    got = B.outputs()
+    k = min(len(got), max(64, int(args.lru_check * len(got))))
+    o = Oracle()
+    c = o.cache_new(limit)
+    exp = o.encode_batch(data, offs[:k], lens[:k], mode=1, cache=c)
+    o.cache_free(c)
+    if got[:k] != exp:
+        bad = next(i for i in range(k) if got[i] != exp[i])
+        raise SystemExit(f'PARITY FAILURE (c5lru) at chunk {bad}')
+    dctx = Context(0, cache_segments=nbytes // 2048 + 4096)
+    dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c5lru)')
+    inb = data.size
+    return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, bounded %d MiB LRU cache' % (nbytes >> 20,
+                                                                                                 args.lru_mib),
+            'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds,
+            'checked': f'first {k} chunks vs the oracle with the same bounded cache; decoded back (unbounded decoder)'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('configs', nargs='*', default=['c2s', 'c3', 'c4', 'c5'])
@@ -275,10 +312,12 @@ def main():
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--batch-mib', type=int, default=512)
     ap.add_argument('--c4-batch', type=int, default=16384)
+    ap.add_argument('--lru-mib', type=int, default=128)
+    ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5}
+    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5, 'c5lru': run_c5lru}
     for c in args.configs:
         t0 = time.perf_counter()
         r = fns[c](args)

@@ -88,6 +88,20 @@ def test_lru_split_batches(oracle):
     assert got == exp
 
 
+def test_lru_cache_clear_restarts(oracle):
+    # Clearing the bounded cache starts a fresh LRU (the same stream encodes the same).
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = mlg.recency_stream(99, 2 << 20, 60, 300)
+    offs, lens = chunks_of(d, 65536)
+    exp, _ = oracle_stream(oracle, d, offs, lens, 150 * SEG)
+    ctx = Context(0, memory_cache_limit=150 * SEG)
+    for _ in range(3):
+        ctx.cache_clear()
+        assert ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM) == exp
+    ctx.close()
+
+
 def test_lru_uniform_and_magic(oracle, stream_seed):
     from wanproxy_amd import synth
     for seed, dup, magic, limit in ((11, 50, 0, 128), (12, 70, 3, 257), (13, 90, 0, 700)):

@@ -144,6 +144,8 @@ struct BatchScratch {
   uint32_t maxe = 0;
   uint32_t* ev_base = nullptr;     // n_cap + 1
   uint32_t* enter_base = nullptr;  // n_cap + 1
+  uint32_t* ev_slot = nullptr;     // n_cap * maxe: each reference's pool slot / LRU time
+  uint64_t* ev_time = nullptr;
 };
 
 struct DecodeScratch {
@@ -222,7 +224,7 @@ void free_cache(GpuCache& g) {
 void free_lru(XcgLruState& L) {
   (void)hipFree(L.skey); (void)hipFree(L.lastref); (void)hipFree(L.queue); (void)hipFree(L.queue2);
   (void)hipFree(L.ptime); (void)hipFree(L.hmin); (void)hipFree(L.wpop); (void)hipFree(L.tau);
-  (void)hipFree(L.alive); (void)hipFree(L.freel); (void)hipFree(L.evslot); (void)hipFree(L.evtime);
+  (void)hipFree(L.alive); (void)hipFree(L.freel);
   (void)hipFree(L.tot);
   if (L.h_tot) (void)hipHostFree(L.h_tot);
   const uint32_t C = L.C;
@@ -237,7 +239,6 @@ int alloc_lru(XcgLruState& L) {
       hipMalloc(&L.ptime, 8 * C) != hipSuccess || hipMalloc(&L.hmin, 8 * C) != hipSuccess ||
       hipMalloc(&L.wpop, 8 * C) != hipSuccess || hipMalloc(&L.tau, 8 * C) != hipSuccess ||
       hipMalloc(&L.alive, 4 * C) != hipSuccess || hipMalloc(&L.freel, 4 * C) != hipSuccess ||
-      hipMalloc(&L.evslot, 4 * C) != hipSuccess || hipMalloc(&L.evtime, 8 * C) != hipSuccess ||
       hipMalloc(&L.tot, 64) != hipSuccess || hipHostMalloc(&L.h_tot, 64) != hipSuccess ||
       hipMemset(L.lastref, 0, 8 * C) != hipSuccess) {
     free_lru(L);
@@ -256,6 +257,7 @@ void free_scratch(BatchScratch& b) {
   if (b.h_vflags) (void)hipHostFree(b.h_vflags);
   if (b.h_changed) (void)hipHostFree(b.h_changed);
   (void)hipFree(b.ev); (void)hipFree(b.nev); (void)hipFree(b.ev_base); (void)hipFree(b.enter_base);
+  (void)hipFree(b.ev_slot); (void)hipFree(b.ev_time);
   b = BatchScratch{};
 }
 
@@ -325,7 +327,8 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
   if (c->bounded) {
     b.maxe = 2 * maxd + 64;        // declarations + REFs + collision lookups of one chunk
     if (hipMalloc(&b.ev, 16ull * n * b.maxe) != hipSuccess || hipMalloc(&b.nev, 4ull * n) != hipSuccess ||
-        hipMalloc(&b.ev_base, 4ull * (n + 1)) != hipSuccess || hipMalloc(&b.enter_base, 4ull * (n + 1)) != hipSuccess) {
+        hipMalloc(&b.ev_base, 4ull * (n + 1)) != hipSuccess || hipMalloc(&b.enter_base, 4ull * (n + 1)) != hipSuccess ||
+        hipMalloc(&b.ev_slot, 4ull * n * b.maxe) != hipSuccess || hipMalloc(&b.ev_time, 8ull * n * b.maxe) != hipSuccess) {
       free_scratch(b);
       return XCG_ENOMEM;
     }
@@ -482,7 +485,8 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
   if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
-  c->lru.clock = 1;
+  // (the LRU clock keeps running: slots keep their last-reference times, which
+  // must stay below every later batch's)
   return clear_cache(c->g);
 }
 
@@ -608,7 +612,7 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
                     c->bs.r_filt, c->bs.r_ftab, c->bs.decl, c->bs.ndecl, maxd, c->bs.changed, c->bs.h_changed,
                     c->g.gfilt, c->bs.r_gfilt, c->g.gmask, c->bs.bcount, c->bs.b2_keys, c->bs.b2_vals,
                     c->bs.r_keys, c->bs.r_vals, c->bs.r_mask, c->bs.hits, c->bs.nhits, c->bs.maxh, c->bs.need,
-                    c->bs.vflags, c->bs.h_vflags, 0, nullptr, nullptr, nullptr, nullptr, 0u, 0, 0};
+                    c->bs.vflags, c->bs.h_vflags, 0, nullptr, nullptr, nullptr, nullptr, 0u, 0, 0, 0};
     // Seed the rounds with the chunks' 2048-byte tilings instead of a parse
     // round 0 when the last batch declared segments (cold / growing caches);
     // a warm cache's all-REF batches keep round 0, which then is all they need.
@@ -623,6 +627,8 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
       a.maxe = c->bs.maxe;
       c->lru.ev_base = c->bs.ev_base;
       c->lru.enter_base = c->bs.enter_base;
+      c->lru.evslot = c->bs.ev_slot;
+      c->lru.evtime = c->bs.ev_time;
       rc = xcg_lru_encode_stream(&a, &c->lru, &rounds, (hipStream_t)stream);
       c->last_rounds = rounds;
       return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : (rc == -95 ? XCG_ENOTSUP : XCG_EHIP));

@@ -63,6 +63,8 @@ struct XcgStreamArgs {
   uint32_t maxe;
   int no_commit;
   int keep_decls;        // start from the declaration lists already in decl/ndecl
+  int need_given;        // (keep_decls) round 1 parses only the chunks flagged in need[]
 };
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);
+extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream);

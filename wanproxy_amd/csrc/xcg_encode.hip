@@ -27,9 +27,11 @@
 // (ESCAPE / EXTRACT / REF, xcodec_encoder.cc:276-372) are written by the whole
 // wave as they are resolved, into the chunk's output slot.
 #include <stddef.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "xcg_cache.h"
 #include "xcg_args.h"
@@ -982,9 +984,15 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
 template __global__ void encode_independent_kernel<10, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
 template __global__ void encode_stream_kernel<8, 72, 16, false>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 8, false>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 4, false>(EncParams);
 template __global__ void encode_stream_kernel<10, 264, 6, false>(EncParams);
+template __global__ void encode_stream_kernel<10, 264, 2, false>(EncParams);
 template __global__ void encode_stream_kernel<8, 72, 16, true>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 8, true>(EncParams);
+template __global__ void encode_stream_kernel<8, 72, 4, true>(EncParams);
 template __global__ void encode_stream_kernel<10, 264, 6, true>(EncParams);
+template __global__ void encode_stream_kernel<10, 264, 2, true>(EncParams);
 
 }  // namespace xcg
 
@@ -1292,6 +1300,21 @@ extern "C" uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys) {
   return __atomic_exchange_n(&g_lds_filter_keys, keys, __ATOMIC_RELAXED);
 }
 
+// The tiling seed alone (decl / ndecl / nhits / changed), for a caller that
+// looks at it before the rounds (the bounded cache's first eviction guess);
+// then xcg_launch_encode_stream with keep_decls.
+extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream) {
+  if (a->n == 0) return 0;
+  hipLaunchKernelGGL(xcg::seed_tiling_kernel, dim3((a->n + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
+                     a->chunk_len, a->n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+static bool stream_debug() {
+  static const bool on = getenv("XCG_STREAM_DEBUG") != nullptr;
+  return on;
+}
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
   using namespace xcg;
   const uint32_t n = a->n;
@@ -1315,20 +1338,45 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   const size_t tbytes = ((size_t)a->fmask + 1) * 16;
   const size_t gbytes = ((size_t)a->gmask + 1) * 4;
   int dev = 0;
-  hipDeviceProp_t props;
-  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&props, dev) != hipSuccess) return -5;
-  const uint32_t wgs = (uint32_t)props.multiProcessorCount;
+  int cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -5;
+  const uint32_t wgs = (uint32_t)cus;
   const bool big = a->maxd > 72;                     // chunks > 128 KiB (<= 512 KiB frames): 264 records
-  const uint32_t SW = big ? 6 : 16;               // one workgroup per CU (LDS)
+  // One workgroup per CU (LDS): SW chunk-waves each.  A batch too small to
+  // give every CU a full workgroup spreads over more CUs with fewer waves
+  // (a wave alone on its SIMD parses faster than four sharing it).
+  const uint32_t SW = big ? (n <= 2 * wgs ? 2u : 6u) : (n <= 4 * wgs ? 4u : (n <= 8 * wgs ? 8u : 16u));
   const dim3 sgrid(min(wgs, (n + SW - 1) / SW)), sblock(64 * SW);
-  auto launch = [&]() {
-    if (prm.ev) {   // bounded cache: record the chunks' cache references (xcg_lru.hip)
-      if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6, true>), sgrid, sblock, 0, stream, prm);
-      else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, true>), sgrid, sblock, 0, stream, prm);
+  auto launch_sw = [&](auto lru) {
+    constexpr bool R = decltype(lru)::value;
+    if (big) {
+      if (SW == 2) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 2, R>), sgrid, sblock, 0, stream, prm);
+      else hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6, R>), sgrid, sblock, 0, stream, prm);
+    } else if (SW == 4) {
+      hipLaunchKernelGGL((encode_stream_kernel<8, 72, 4, R>), sgrid, sblock, 0, stream, prm);
+    } else if (SW == 8) {
+      hipLaunchKernelGGL((encode_stream_kernel<8, 72, 8, R>), sgrid, sblock, 0, stream, prm);
     } else {
-      if (big) hipLaunchKernelGGL((encode_stream_kernel<10, 264, 6, false>), sgrid, sblock, 0, stream, prm);
-      else hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, false>), sgrid, sblock, 0, stream, prm);
+      hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, R>), sgrid, sblock, 0, stream, prm);
     }
+  };
+  // bounded cache: the variant that records the chunks' cache references (xcg_lru.hip)
+  auto launch = [&]() {
+    if (stream_debug()) {
+      uint32_t cnt = n;
+      if (prm.need) {
+        std::vector<uint32_t> h(n);
+        (void)hipMemcpyAsync(h.data(), prm.need, 4ull * n, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        cnt = 0;
+        for (uint32_t v : h) cnt += v != 0;
+      }
+      fprintf(stderr, "stream: launch over %u of %u chunks (skip below %u)\n", cnt, n, prm.skip_below);
+    }
+    if (prm.ev) launch_sw(std::integral_constant<bool, true>{});
+    else launch_sw(std::integral_constant<bool, false>{});
   };
   // lowest chunk whose declaration list changed in the round just run (~0u: none)
   auto changed_after = [&](uint32_t& fc) -> bool {
@@ -1410,6 +1458,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     prm.b = tabs[cur];
     prm.skip_below = seeded ? 0 : fc + 1;            // (seeded: round 1 parses every chunk)
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
+    if (keep && a->need_given) prm.need = a->need;   // the rest stand under the kept lists
     launch();
     ++rounds;
     prm.skip_below = 0;
@@ -1435,6 +1484,9 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       commit(a->vflags + 1);                           // runs while the host waits, if nothing was flagged
       if (hipStreamSynchronize(stream) != hipSuccess) return -5;
       if (a->decls_out) *a->decls_out = a->h_vflags[2];
+      if (stream_debug())
+        fprintf(stderr, "stream: n %u round %u first (a)-flag %d any %u\n", n, r, (int)a->h_vflags[0],
+                a->h_vflags[1]);
       if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point (already committed)
         converged = true;
         committed = true;

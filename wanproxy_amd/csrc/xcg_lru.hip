@@ -11,11 +11,12 @@
 //               for an enter)) -- the order XCodecLRU's counters give
 //   queue[A]    the A live slots, least recently used first
 //
-// Within one batch (at most C references, so nothing the batch itself
-// references can be evicted before the batch ends -- that takes C newer
-// distinct references), the entries evicted are persistent ones: enter number
-// C - A + j (in stream order) evicts the j-th least recently used persistent
-// entry not looked up in the batch before that point.  For a persistent entry
+// Within one batch whose enters N plus persistent entries looked up H stay
+// within C, the entries evicted are persistent ones that the batch does not
+// look up: enter number C - A + j (in stream order) evicts the j-th least
+// recently used persistent entry not looked up before that point, and the
+// N + A - C <= A - H evictions never reach an entry the batch itself made or
+// refreshed (those sit above every persistent entry in the LRU order).  For a persistent entry
 // of LRU rank r, with S(r) entries below it that the batch looks up, that is
 // eviction j = r - S(r) at tau[j], unless the batch looks it up first.  The
 // parse takes these eviction times (ptime) as given; the pass below recomputes
@@ -36,7 +37,7 @@
 namespace xcg {
 
 constexpr uint64_t NEVER = ~0ull;
-enum : uint32_t { T_E = 0, T_N, T_P, T_A, T_BAD, T_OVF, T_A2, T_NFREE, T_WORDS = 16 };
+enum : uint32_t { T_E = 0, T_N, T_P, T_A, T_BAD, T_OVF, T_A2, T_NFREE, T_H, T_WORDS = 16 };
 
 // Ordered scan by one 1024-thread workgroup over i in [0, n): emit(i, p, v)
 // with p = carry + sum of val(j) for j < i.  Returns carry + the total.
@@ -85,8 +86,10 @@ __global__ __launch_bounds__(256) void lru_fill32_kernel(uint32_t* p, uint32_t n
 // Per-chunk reference / enter bases, batch totals, the eviction count.
 __global__ __launch_bounds__(1024) void lru_prep_kernel(uint32_t n, const uint32_t* nev, const uint32_t* ndecl,
                                                         uint32_t maxe, uint32_t C, const uint32_t* nseg,
-                                                        uint32_t* ev_base, uint32_t* enter_base, uint32_t* tot) {
+                                                        uint32_t* ev_base, uint32_t* enter_base, uint32_t* need,
+                                                        uint32_t* tot) {
   if (threadIdx.x == 0) tot[T_OVF] = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) need[i] = 0u;
   __syncthreads();
   const uint32_t e = wg_scan(
       n, 0u,
@@ -129,14 +132,31 @@ __global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, uint32_t ma
   }
 }
 
+// First guess of a sub-batch's evictions, before any parse: every chunk
+// declares its 2048-byte tiling (the seed; the cold parse) and looks nothing
+// up.  Enter times as the sequential encoder makes them: tile p is declared
+// while examining window p + 2048, or after the last window.
+__global__ __launch_bounds__(256) void lru_seed_tau_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                           uint32_t maxd, const uint32_t* chunk_len,
+                                                           const uint32_t* enter_base, const uint32_t* tot,
+                                                           uint32_t C, uint64_t* tau) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxd), d = (uint32_t)(i % maxd);
+  if (c >= n || d >= ndecl[c]) return;
+  const uint32_t pos = decl[i].z, last = chunk_len[c] - SEG;
+  const uint32_t t = pos + SEG <= last ? 2u * (pos + SEG) : 2u * (last + 1u);
+  const uint32_t ge = enter_base[c] + d, thr = C - tot[T_A];
+  if (ge >= thr) tau[ge - thr] = ((uint64_t)c << 21) | t;
+}
+
 // Walk the persistent entries in LRU order: wpop[s] = when the batch's
 // evictions reach slot s (tau[r - S(r)]), ptime[s] = that, unless the batch
 // looks s up before then (then never).
-__global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, const uint32_t* tot,
+__global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, uint32_t* tot,
                                                         const uint64_t* hmin, const uint64_t* tau, uint64_t* wpop,
                                                         uint64_t* ptime) {
   const uint32_t A = tot[T_A], P = tot[T_P];
-  wg_scan(
+  const uint32_t H = wg_scan(
       A, 0u, [&](uint32_t r) { return hmin[queue[r]] != NEVER ? 1u : 0u; },
       [&](uint32_t r, uint32_t S, uint32_t h) {
         const uint32_t s = queue[r], j = r - S;
@@ -144,12 +164,13 @@ __global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, c
         wpop[s] = w;
         ptime[s] = h && hmin[s] < w ? NEVER : w;   // (a hit after the eviction did not happen)
       });
+  if (threadIdx.x == 0) tot[T_H] = H;
 }
 
 // Every recorded lookup of a persistent entry against the recomputed times.
 __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
                                                         const uint32_t* nev, const uint64_t* hmin,
-                                                        const uint64_t* wpop, uint32_t* tot) {
+                                                        const uint64_t* wpop, uint32_t* need, uint32_t* tot) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
   bool bad = false;
@@ -160,6 +181,7 @@ __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, uint32_t max
     if (kind == EV_GHIT) bad = t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
     else if (kind == EV_GMISS) bad = !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
   }
+  if (bad) need[c] = 1u;                              // the next pass re-parses chunk c
   if (ballot(bad) != 0 && lane_id() == 0) atomicAdd(&tot[T_BAD], 1u);
 }
 
@@ -327,7 +349,7 @@ int lru_analyze(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   const uint4* ev = (const uint4*)a.ev;
   hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev,
                      (const uint32_t*)a.ndecl, maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base,
-                     L->tot);
+                     a.need, L->tot);
   hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
                      L->hmin, L->C, NEVER);
   hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
@@ -335,14 +357,31 @@ int lru_analyze(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   const uint64_t ne = (uint64_t)n * maxe;
   hipLaunchKernelGGL(lru_events_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
                      (const uint32_t*)L->enter_base, (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
-  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue,
-                     (const uint32_t*)L->tot, (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
+  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
+                     (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
   hipLaunchKernelGGL(lru_check_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
-                     (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->tot);
+                     (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, a.need, L->tot);
   if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return -5;
   return 0;
+}
+
+// ptime from the tiling seed (lru_seed_tau_kernel).  Asynchronous.
+void lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+  using namespace xcg;
+  const uint32_t n = a.n;
+  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev,
+                     (const uint32_t*)a.ndecl, a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base,
+                     a.need, L->tot);
+  const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
+  hipLaunchKernelGGL(lru_seed_tau_kernel, dim3(grid_for((uint64_t)n * a.maxd)), dim3(256), 0, st, n,
+                     (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, a.chunk_len,
+                     (const uint32_t*)L->enter_base, (const uint32_t*)L->tot, L->C, L->tau);
+  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
+                     (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
 }
 
 int lru_commit(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
@@ -381,17 +420,19 @@ int lru_commit(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
 }  // namespace
 
 // Stream-semantics encode of a batch on a bounded cache.  The batch is cut
-// into sub-batches of at most C references (the bound the eviction rule above
-// needs; a sub-batch whose references exceed it is halved); each is parsed
+// into sub-batches with N + H <= C (the bound the eviction rule above needs; a
+// sub-batch that exceeds it is halved); each is parsed
 // (xcg_launch_encode_stream, commit off) until its eviction times are
 // consistent, then committed.  Returns 0, -75 (no fixed point / reference
-// list overflow), -95 (one chunk alone makes more than C references), -5.
+// list overflow), -95 (one chunk alone exceeds the bound), -5.
 extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, int* rounds_out, hipStream_t st) {
   using namespace xcg;
   const uint32_t n = a0->n, C = L->C;
   int rounds = 0;
-  const uint32_t per_chunk = 2 * a0->maxd;         // declarations + REFs a chunk can make (+ collisions)
-  uint32_t per = C / per_chunk ? C / per_chunk : 1u;
+  // chunks per sub-batch: from the bound (a chunk declares or REFs each
+  // 2048 bytes at most once; collision lookups aside), then from what the last
+  // sub-batch used
+  uint32_t per = C / a0->maxd ? C / a0->maxd : 1u;
   constexpr int MAX_PASSES = 12;
   uint32_t i0 = 0;
   while (i0 < n) {
@@ -405,11 +446,13 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     if (a.stats) a.stats += 4ull * i0;
     a.ptime = L->ptime;
     a.no_commit = 1;
-    hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(C) < 1024 ? grid_for(C) : 1024), dim3(256), 0, st,
-                       L->ptime, C, NEVER);
+    // Pass 0 starts from the tiling seed, with the evictions it implies.
+    if (xcg_launch_seed_tiling(&a, st)) return -5;
+    lru_seed_guess(a, L, st);
     bool done = false, split = false;
     for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
-      a.keep_decls = pass > 0;
+      a.keep_decls = 1;
+      a.need_given = pass > 0;                       // re-parse the chunks with an inconsistent lookup
       int r = 0;
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
@@ -420,7 +463,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
                 m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
                 L->h_tot[T_OVF]);
       if (L->h_tot[T_OVF]) return -75;
-      if (L->h_tot[T_E] > C) split = true;
+      if ((uint64_t)L->h_tot[T_N] + L->h_tot[T_H] > C) split = true;
       else if (L->h_tot[T_BAD] == 0) done = true;
     }
     if (!done) {
@@ -430,6 +473,9 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     }
     if (lru_commit(a, L, st)) return -5;
     i0 += m;
+    const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
+    const uint64_t want = used ? (uint64_t)C * 9 / 10 * m / used : (uint64_t)n;
+    per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
   }
   if (rounds_out) *rounds_out = rounds;
   return hipGetLastError() == hipSuccess ? 0 : -5;
