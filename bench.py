@@ -209,9 +209,11 @@ def other_configs():
     spec = importlib.util.spec_from_file_location('configs_bench', os.path.join(ROOT, 'scripts', 'configs_bench.py'))
     cb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(cb)
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384)
+    # C5-LRU: C5 on wanproxy.conf's bounded 128 MiB memory cache (LRU
+    # eviction), the first 25 % checked against the oracle's bounded cache
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, lru_mib=128, lru_check=0.25)
     out = {}
-    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5)):
+    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru)):
         try:
             out[name] = fn(a)
         except BaseException as e:          # SystemExit from a parity check included

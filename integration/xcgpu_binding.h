@@ -50,6 +50,22 @@ inline void forget(XCodecCache *cache)
 	ctx_map().erase(it);
 }
 
+/* Bounded memory caches: XCodecMemoryCache keeps memory_cache_limit_
+ * private (xcodec/xcodec_cache.h:272-288), so the code that makes one with a
+ * size (programs/wanproxy/wanproxy_config_class_cache.cc:66) tells the binding:
+ * its GPU mirror is then created with xcg_ctx_create_bounded (LRU eviction). */
+inline std::map<XCodecCache *, uint64_t>& limit_map()
+{
+	static std::map<XCodecCache *, uint64_t> limits;
+	return limits;
+}
+
+inline void set_cache_limit(XCodecCache *cache, uint64_t memory_cache_limit_bytes)
+{
+	if (memory_cache_limit_bytes != 0)
+		limit_map()[cache] = memory_cache_limit_bytes;
+}
+
 inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 {
 	std::map<XCodecCache *, xcg_ctx *>& ctxs = ctx_map();
@@ -64,7 +80,9 @@ inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 	const char *dev = getenv("XCGPU_DEVICE");
 	if (dev != NULL)
 		device = atoi(dev);
-	if (xcg_ctx_create(device, flags, &ctx) != XCG_OK)
+	std::map<XCodecCache *, uint64_t>::const_iterator lim = limit_map().find(cache);
+	if (lim != limit_map().end() ? xcg_ctx_create_bounded(device, flags, lim->second, &ctx) != XCG_OK
+	                             : xcg_ctx_create(device, flags, &ctx) != XCG_OK)
 		return NULL;
 	ctxs[cache] = ctx;
 	return ctx;
