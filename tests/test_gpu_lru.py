@@ -127,10 +127,172 @@ def test_lru_no_eviction_equals_unbounded(oracle):
 def test_lru_unsupported_paths():
     from wanproxy_amd.xcgpu import Context, XCGError
     ctx = Context(0, memory_cache_limit=64 * SEG)
-    with pytest.raises(XCGError):
-        ctx.decode_chunks([b'\xf1\x00'])
     # independent chunks of more than limit * 2048 bytes could evict
     x = np.random.default_rng(1).integers(0, 256, 65 * SEG, dtype=np.uint8).tobytes()
     with pytest.raises(XCGError):
         ctx.encode_chunks(x, [0], [len(x)])
     ctx.close()
+
+
+def decode_calls(ctx, encs):
+    """One decode() call per encoded chunk on ctx (a persistent decoder), as
+    the reference harness made tests/golden/lru.json's 'dec' entries."""
+    calls = []
+    for e in encs:
+        outs, st, cons, unk = ctx.decode_chunks([e])
+        calls.append({'ok': int(st[0]) != -1, 'consumed': int(cons[0]), 'nunknown': len(unk),
+                      'out_len': len(outs[0]), 'out_sha256': sha(outs[0])})
+        if int(st[0]) == -1 or unk:
+            break
+    return calls
+
+
+def test_lru_decode_golden_gpu(lru_golden, oracle):  # noqa: F811
+    # The reference XCodecDecoder on a bounded cache, call by call (incl. the
+    # collision case where the decoder's LRU falls out of step and blocks).
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import Context, XCGError
+    ran = 0
+    for case in lru_golden['cases']:
+        d = lru_inputs(case['input'])
+        offs, lens = chunks_of(d, case['chunk'])
+        encs, _ = oracle_stream(oracle, d, offs, lens, case['limit'])
+        ctx = Context(0, memory_cache_limit=case['limit'])
+        key = (case['input'], case['chunk'], case['limit'])
+        try:
+            got = decode_calls(ctx, encs)
+        except XCGError:
+            assert max(1, case['limit'] // SEG) < 2 * (case['chunk'] // SEG + 1), key
+            continue
+        finally:
+            ctx.close()
+        assert got == case['dec'], key
+        ran += 1
+    assert ran >= 6
+
+
+def test_lru_decode_batch_vs_oracle(oracle):
+    # A whole stream in one decode batch on a bounded cache, then more calls.
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import Context
+    d = mlg.recency_stream(515, 3 << 20, 60, 600)
+    offs, lens = chunks_of(d, 65536)
+    limit = 1500 * SEG
+    encs, _ = oracle_stream(oracle, d, offs, lens, limit)
+    ctx = Context(0, memory_cache_limit=limit)
+    half = len(encs) // 2
+    outs, st, cons, unk = ctx.decode_chunks(encs[:half])
+    assert (st == 0).all() and not unk
+    outs2, st2, _, unk2 = ctx.decode_chunks(encs[half:])
+    assert (st2 == 0).all() and not unk2
+    assert b''.join(outs + outs2) == d
+    # cache state: the oracle decoder's cache after the same calls
+    dc = oracle.cache_new(limit)
+    dec = oracle.decoder_new(dc)
+    for e in encs:
+        oracle.decode(e, dc, decoder=dec)
+    assert ctx.cache_size() == oracle.lib.xco_cache_size(dc)
+    oracle.decoder_free(dec)
+    oracle.cache_free(dc)
+    ctx.close()
+
+
+def test_lru_round_trip_gpu(oracle):
+    # GPU bounded encode -> GPU bounded decode (same limit) gives the input back.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    d = synth.stream(0x1A9, 4 << 20, 40, 1)
+    offs, lens = synth.chunks_of(d, 65536)
+    got, _ = gpu_stream(d, offs, lens, 400 * SEG)
+    ctx = Context(0, memory_cache_limit=400 * SEG)
+    out = []
+    for i in range(0, len(got), 8):
+        o, st, _, unk = ctx.decode_chunks(got[i:i + 8])
+        assert (st == 0).all() and not unk
+        out += o
+    ctx.close()
+    assert b''.join(out) == d
+
+
+@pytest.mark.parametrize('batch', [1, 4])
+def test_lru_decode_blocks_like_reference(oracle, batch):
+    # Frames from an UNBOUNDED encoder reference segments a bounded decoder has
+    # evicted: decode() blocks there with the skim's unknown set (ASK), exactly
+    # where the oracle's bounded XCodecDecoder does.
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import Context
+    d = mlg.recency_stream(808, 2 << 20, 60, 2000)
+    offs, lens = chunks_of(d, 32768)
+    c = oracle.cache_new()
+    encs = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    oracle.cache_free(c)
+    limit = 120 * SEG
+    dc = oracle.cache_new(limit)
+    dec = oracle.decoder_new(dc)
+    ctx = Context(0, memory_cache_limit=limit)
+    blocked = False
+    for i in range(0, len(encs), batch):
+        part = encs[i:i + batch]
+        outs, st, cons, unk = ctx.decode_chunks(part)
+        exp_out, exp_unk = [], []
+        for j, e in enumerate(part):
+            ok, o, cn, u = oracle.decode(e, dc, decoder=dec)
+            exp_out.append(o)
+            if u:
+                # (the batch decoder's skim also covers the frames after this one in its batch)
+                exp_unk = u
+                assert int(st[j]) == 1 and int(cons[j]) == cn, (i, j)
+                assert outs[j] == o
+                blocked = True
+                break
+            assert int(st[j]) == 0 and outs[j] == o and int(cons[j]) == cn, (i, j)
+        if blocked:
+            assert set(exp_unk) <= set(unk)
+            break
+    assert blocked
+    oracle.decoder_free(dec)
+    oracle.cache_free(dc)
+    ctx.close()
+
+
+def test_lru_host_ops_vs_oracle(oracle):
+    # Single-segment lookups / enters (XCodecPipePair's <LEARN>: lookup, then
+    # replace or enter) on a bounded cache, against the oracle's LRU.
+    import ctypes as C
+    from wanproxy_amd.xcgpu import Context
+    rng = np.random.default_rng(21)
+    L = oracle.lib
+    L.xco_cache_lookup.restype = C.c_void_p
+    L.xco_cache_lookup.argtypes = [C.c_void_p, C.c_uint64]
+    L.xco_cache_replace.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint8)]
+    u8 = lambda b: (C.c_uint8 * 2048).from_buffer_copy(b)
+    keys = [int(rng.integers(0, 1 << 62)) & ~(0xF << 32) for _ in range(40)]
+    segs = {k: rng.integers(0, 256, 2048, dtype=np.uint8).tobytes() for k in keys}
+    limit = 9
+    oc = oracle.cache_new(limit * SEG)
+    ctx = Context(0, memory_cache_limit=limit * SEG)
+
+    def o_lookup(k):
+        p = L.xco_cache_lookup(oc, k)
+        return None if p is None else C.string_at(p, 2048)
+
+    def o_learn(k, b):
+        old = o_lookup(k)
+        if old is None:
+            assert L.xco_cache_enter(oc, k, u8(b)) == 0
+        elif old != b:
+            L.xco_cache_replace(oc, k, u8(b))
+
+    for step in range(300):
+        k = keys[int(rng.integers(0, 20 if step < 150 else 40))]
+        if rng.random() < 0.5:
+            b = segs[k] if rng.random() < 0.8 else rng.integers(0, 256, 2048, dtype=np.uint8).tobytes()
+            o_learn(k, b)
+            ctx.cache_enter(k, b)
+        else:
+            assert ctx.cache_lookup(k) == o_lookup(k), step
+        assert ctx.cache_size() == L.xco_cache_size(oc), step
+    for k in keys:                                   # final contents (lookups refresh both alike)
+        assert ctx.cache_lookup(k) == o_lookup(k)
+    ctx.close()
+    oracle.cache_free(oc)

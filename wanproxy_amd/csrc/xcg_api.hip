@@ -22,28 +22,6 @@ extern "C" int xcg_launch_encode_independent(const uint8_t*, const uint64_t*, co
 extern "C" int xcg_launch_window_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
 
 
-// Bounded cache (xcg_lru.hip).
-struct XcgLruState {
-  uint32_t C;
-  uint64_t* skey;
-  uint64_t* lastref;
-  uint32_t* queue;
-  uint32_t* queue2;
-  uint64_t* ptime;
-  uint64_t* hmin;
-  uint64_t* wpop;
-  uint64_t* tau;
-  uint32_t* alive;
-  uint32_t* freel;
-  uint32_t* evslot;
-  uint64_t* evtime;
-  uint32_t* ev_base;
-  uint32_t* enter_base;
-  uint32_t* tot;
-  uint32_t* h_tot;
-  uint64_t clock;
-};
-extern "C" int xcg_lru_encode_stream(const XcgStreamArgs*, XcgLruState*, int*, hipStream_t);
 extern "C" int xcg_launch_segment_hashes(const uint8_t*, uint64_t, uint64_t*, hipStream_t);
 
 struct XcgDecodeArgs {
@@ -84,6 +62,8 @@ struct XcgDecodeArgs {
   uint64_t* win_hash;
   uint8_t* win_seg;
   uint64_t win_count;
+  XcgLruState* lru;      // bounded cache (null: unbounded)
+  uint32_t maxd;         // EXTRACTs a chunk can hold (bounded: declaration rows per chunk)
 };
 extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*, uint32_t, uint8_t*, uint64_t*,
                                uint64_t*, hipStream_t);
@@ -386,7 +366,7 @@ int ensure_dscratch(xcg_ctx* c, uint64_t max_extracts) {
   if (hipMalloc(&d.x_keys, 8ull * cap) != hipSuccess || hipMalloc(&d.x_vals, 8ull * cap) != hipSuccess ||
       hipMalloc(&d.x_latest, 8ull * cap) != hipSuccess || hipMalloc(&d.unknown, 8ull * UNKNOWN_CAP) != hipSuccess ||
       hipMalloc(&d.unknown_pos, 8ull * UNKNOWN_CAP) != hipSuccess || hipMalloc(&d.nunknown, 16) != hipSuccess ||
-      hipMalloc(&d.scratch, 64) != hipSuccess || hipHostMalloc(&d.h_scratch, 64) != hipSuccess) {
+      hipMalloc(&d.scratch, 64) != hipSuccess || hipHostMalloc(&d.h_scratch, 128) != hipSuccess) {
     free_dscratch(d);
     return XCG_ENOMEM;
   }
@@ -524,9 +504,94 @@ int host_seg_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
 }
 }  // namespace
 
+namespace {
+// Single-segment host calls on a bounded cache: lookup (a hit refreshes the
+// entry, xcodec_cache.h:348-364) and enter (XCodecPipePair's <LEARN>:
+// lookup, then replace if the bytes differ or enter, evicting at the limit,
+// xcodec_pipe_pair.cc:311-327) -- as a one-reference batch through the LRU
+// pass and commit (xcg_lru.hip).
+int lru_host_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out_seg, int enter, int32_t* found) {
+  DeviceGuard g(c->device);
+  int rc = ensure_cache(c);
+  if (rc != XCG_OK) return rc;
+  // device scratch: [0, 2048) new bytes, [2048, 4096) old bytes, then the batch
+  uint8_t* m = nullptr;
+  if (hipMalloc(&m, 8192) != hipSuccess) return XCG_ENOMEM;
+  uint8_t* d_new = m;
+  uint8_t* d_old = m + 2048;
+  int32_t* d_res = (int32_t*)(m + 4096);
+  rc = XCG_OK;
+  do {
+    if (xcg_launch_cache_lookup(c->g.keys, c->g.vals, c->g.mask, c->g.pool, hash, d_old, d_res, nullptr) != 0 ||
+        hipMemcpy(found, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = XCG_EHIP;
+      break;
+    }
+    if (*found && out_seg && hipMemcpy(out_seg, d_old, XCG_SEGMENT_LENGTH, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = XCG_EHIP;
+      break;
+    }
+    if (!*found && !enter) break;                   // a miss changes nothing
+    if (enter && hipMemcpy(d_new, in_seg, XCG_SEGMENT_LENGTH, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = XCG_EHIP;
+      break;
+    }
+    int32_t res = 0;
+    if (enter && *found &&                          // replace (the table entry stays)
+        (xcg_launch_cache_enter(c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap, c->g.filt,
+                                c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, hash, d_new, 1, d_res, nullptr) != 0 ||
+         hipMemcpy(&res, d_res, 4, hipMemcpyDeviceToHost) != hipSuccess)) {
+      rc = XCG_EHIP;
+      break;
+    }
+    // the one-reference batch: chunk 0 = the new bytes; an ENTER (declaration
+    // row 0) or a HIT at time 1
+    struct {
+      uint64_t chunk_off;
+      uint32_t ev[4], decl[4];
+      uint32_t nev, ndecl, need, pad;
+      uint32_t ev_base[2], enter_base[2];
+      uint32_t evslot[2];
+      uint64_t evtime[2];
+    } h{};
+    const uint32_t lo = (uint32_t)hash, hi = (uint32_t)(hash >> 32);
+    h.ev[0] = lo; h.ev[1] = hi;
+    h.ev[2] = *found ? 1u : 0u;
+    h.ev[3] = *found ? (1u << 30) : 0u;             // EV_HIT / EV_ENTER d = 0
+    h.decl[0] = lo; h.decl[1] = hi;
+    h.nev = 1;
+    h.ndecl = *found ? 0u : 1u;
+    uint8_t* d_h = m + 4608;
+    if (hipMemcpy(d_h, &h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = XCG_EHIP;
+      break;
+    }
+    auto at = [&](const void* field) { return d_h + ((const uint8_t*)field - (const uint8_t*)&h); };
+    XcgLruState& L = c->lru;
+    L.ev_base = (uint32_t*)at(h.ev_base);
+    L.enter_base = (uint32_t*)at(h.enter_base);
+    L.evslot = (uint32_t*)at(h.evslot);
+    L.evtime = (uint64_t*)at(h.evtime);
+    const LruBatch b{1u, d_new, (const uint64_t*)at(&h.chunk_off), at(h.decl), (const uint32_t*)at(&h.ndecl), 1u,
+                     at(h.ev), (const uint32_t*)at(&h.nev), 1u, 0, (uint32_t*)at(&h.need), c->g.keys, c->g.vals,
+                     c->g.mask, c->g.pool, c->g.nseg, c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask,
+                     c->d_status};
+    if (xcg_lru_times(&b, &L, nullptr) != 0 || xcg_lru_commit(&b, &L, nullptr) != 0 ||
+        hipStreamSynchronize(nullptr) != hipSuccess)
+      rc = XCG_EHIP;
+  } while (0);
+  (void)hipFree(m);
+  return rc;
+}
+}  // namespace
+
 int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
   if (!c || !seg_out) return XCG_EINVAL;
-  if (c->bounded) return XCG_ENOTSUP;
+  if (c->bounded) {
+    int32_t found = 0;
+    const int rc = lru_host_call(c, hash, nullptr, seg_out, 0, &found);
+    return rc != XCG_OK ? rc : (found ? XCG_OK : XCG_ENOENT);
+  }
   int32_t found = 0;
   const int rc = host_seg_call(c, hash, nullptr, seg_out, 0, &found);
   if (rc != XCG_OK) return rc;
@@ -535,7 +600,10 @@ int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
 
 int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
   if (!c || !seg) return XCG_EINVAL;
-  if (c->bounded) return XCG_ENOTSUP;
+  if (c->bounded) {
+    int32_t found = 0;
+    return lru_host_call(c, hash, seg, nullptr, 1, &found);
+  }
   int32_t res = 0;
   const int rc = host_seg_call(c, hash, seg, nullptr, 1, &res);
   if (rc != XCG_OK) return rc;
@@ -723,7 +791,6 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   if (h_nunknown) *h_nunknown = 0;
   if (h_total_out) *h_total_out = 0;
   if (n == 0) return XCG_OK;
-  if (c->bounded) return XCG_ENOTSUP;
   DeviceGuard g(c->device);
   int rc = ensure_cache(c);
   if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));
@@ -738,12 +805,14 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
                   d_consumed, c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                   c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
                   c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
-                  c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count};
+                  c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count, c->bounded ? &c->lru : nullptr,
+                  max_chunk_len / 2050 + 1};
   uint64_t total = 0, blockp = 0, berr = 0;
   uint32_t nunk = 0;
   const int lrc = xcg_launch_decode(&a, &total, &blockp, &berr, &nunk, (hipStream_t)stream);
   if (h_total_out) *h_total_out = total;
   if (lrc == -75) return XCG_EOVERFLOW;
+  if (lrc == -95) return XCG_ENOTSUP;
   if (lrc != 0) return XCG_EHIP;
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return XCG_EHIP;
   // status word and the declare count, by async copies into pinned memory

@@ -66,5 +66,59 @@ struct XcgStreamArgs {
   int need_given;        // (keep_decls) round 1 parses only the chunks flagged in need[]
 };
 
+// Bounded cache (xcg_lru.hip): device LRU state of a context.
+struct XcgLruState {
+  uint32_t C;             // memory_cache_limit_ in segments (= pool slots)
+  uint64_t* skey;         // [C] key of the entry in pool slot s
+  uint64_t* lastref;      // [C] LRU time of its last enter / lookup
+  uint32_t* queue;        // [C] live slots, least recently used first
+  uint32_t* queue2;
+  uint64_t* ptime;        // [C] batch time from which slot s is evicted (~0: never)
+  uint64_t* hmin;
+  uint64_t* wpop;
+  uint64_t* tau;
+  uint32_t* alive;
+  uint32_t* freel;
+  uint32_t* evslot;       // per reference of the batch (scratch)
+  uint64_t* evtime;
+  uint32_t* ev_base;      // [n + 1]
+  uint32_t* enter_base;   // [n + 1]
+  uint32_t* tot;          // [16]
+  uint32_t* h_tot;        // pinned [16]
+  uint64_t clock;         // LRU time base of the next batch (host)
+};
+
+// A batch's cache references for the LRU pass: enters as declaration rows
+// decl[c * maxd + d] = (lo, hi, position, -), d < ndecl[c]; references as
+// ev[row(c) + k], k < nev[c] (row = c * maxe, or packed when dense).
+struct LruBatch {
+  uint32_t n;
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const void* decl;
+  const uint32_t* ndecl;
+  uint32_t maxd;
+  const void* ev;
+  const uint32_t* nev;
+  uint32_t maxe;
+  int dense;
+  uint32_t* need;         // (encoder) chunks with an inconsistent lookup; may be scratch
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  uint32_t* g_gfilt;
+  uint32_t gmask;
+  int32_t* status;
+};
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);
+extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a, XcgLruState* L, int* rounds_out, hipStream_t st);
+extern "C" int xcg_lru_times(const LruBatch* b, XcgLruState* L, hipStream_t st);
+extern "C" int xcg_lru_commit(const LruBatch* b, XcgLruState* L, hipStream_t st);
+extern "C" int xcg_lru_reset_times(XcgLruState* L, hipStream_t st);
 extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream);

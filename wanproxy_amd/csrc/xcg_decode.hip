@@ -29,7 +29,11 @@
 // window update can reach; an invalid BACKREF stops the stream like an unknown
 // REF (decode() returns false there, :172-176); `window_update` carries the
 // 256 slots (hash + an owned copy of the bytes) into the next batch.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "xcg_cache.h"
+#include "xcg_args.h"
 
 namespace xcg {
 
@@ -66,7 +70,17 @@ struct DecParams {
   uint64_t* win_hash;          // the decoder's window: 256 hashes (0 = empty slot)
   uint8_t* win_seg;            //   and the bytes of each slot
   uint64_t win_count;          // declares made before this batch
+  // ---- bounded cache (xcg_lru.hip): a persistent entry serves a lookup at
+  // stream time (chunk << 21 | op offset) only before ptime[slot]
+  const uint64_t* ptime;
 };
+
+// Is persistent slot gv live for a lookup at stream position `here`?
+__device__ __forceinline__ bool g_live(const DecParams& prm, uint64_t gv, uint64_t here) {
+  if (gv == ~0ull) return false;
+  if (!prm.ptime) return true;
+  return ((here >> 32 << 21) | (uint32_t)here) < prm.ptime[gv];
+}
 
 __device__ __forceinline__ uint64_t spos(uint32_t chunk, uint32_t off) { return ((uint64_t)chunk << 32) | off; }
 
@@ -252,7 +266,7 @@ __device__ __forceinline__ const uint8_t* ref_source(const DecParams& prm, uint3
   const uint64_t e = tab_lookup(prm.x, lo, hi);
   if (e != ~0ull && e < here) return prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
   const uint64_t gv = tab_lookup(prm.g, lo, hi);
-  if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+  if (g_live(prm, gv, here)) return prm.pool + gv * (uint64_t)SEG;
   return nullptr;
 }
 
@@ -261,7 +275,7 @@ __device__ __forceinline__ const uint8_t* ref_source_t(const DecParams& prm, uin
   const uint64_t e = tab_lookup_t(prm.x, lo, hi);
   if (e != ~0ull && e < here) return prm.in + prm.chunk_off[e >> 32] + (uint32_t)e;
   const uint64_t gv = tab_lookup_t(prm.g, lo, hi);
-  if (gv != ~0ull) return prm.pool + gv * (uint64_t)SEG;
+  if (g_live(prm, gv, here)) return prm.pool + gv * (uint64_t)SEG;
   return nullptr;
 }
 
@@ -559,7 +573,7 @@ __global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
         const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
         const uint64_t e = tab_lookup_t(prm.x, lo, hi);
         bool ok = e != ~0ull && e < here;
-        if (!ok) ok = tab_lookup_t(prm.g, lo, hi) != ~0ull;
+        if (!ok) ok = g_live(prm, tab_lookup_t(prm.g, lo, hi), here);
         if (!ok) {
           atomicMin((unsigned long long*)prm.block_pos, (unsigned long long)here);
           const uint32_t k = atomicAdd(prm.nunknown, 1u);
@@ -673,6 +687,148 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
     }
     uint8_t* dst = pool + (uint64_t)dseg * SEG;
     if (jkind == 1 || !readfirst((uint32_t)dec_equal2048(dst, src))) wave_copy2048(dst, src);   // enter / replace (:130)
+  }
+}
+
+// ------------------------------------------------ bounded cache (xcg_lru.hip)
+
+// Every EXTRACT / REF op of the batch as (lo, hi, op offset, op), packed by
+// chunk at decl_base[c] (the scan's declare numbering).  One wave per chunk.
+__global__ __launch_bounds__(256) void dec_ops_kernel(DecParams prm, uint4* raw) {
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  if (chunk >= prm.n) return;
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const uint32_t len = prm.chunk_len[chunk];
+  uint64_t t = prm.decl_base[chunk];
+  uint32_t i = 0;
+  while (i < len) {
+    uint32_t nesc = 0;
+    i = next_op(x, i, len, nesc);
+    if (i + 1 >= len) break;
+    const uint32_t op = x[i + 1];
+    if (op == OP_EXTRACT) {
+      if (len - i < 2u + SEG) break;
+      const uint2 h = dec_window_hash(x + i + 2);
+      if (lane_id() == 0) raw[t] = make_uint4(readfirst(h.x), readfirst(h.y), i, OP_EXTRACT);
+      ++t;
+      i += 2 + SEG;
+    } else if (op == OP_REF) {
+      if (len - i < 10u) break;
+      uint64_t h, here;
+      const uint32_t r = ref_run(x, i, len, chunk, ~0ull, h, here);
+      if ((uint32_t)lane_id() < r) raw[t + lane_id()] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)here, OP_REF);
+      t += r;
+      i += 10u * r;
+    } else if (op == OP_BACKREF) {
+      if (len - i < 3u) break;
+      i += 3;
+    } else {
+      break;
+    }
+  }
+}
+
+// What each op does to the bounded cache, given the eviction times (ptime)
+// and the stop point of the last pass (blockp): an EXTRACT looks its hash up
+// (xcodec_decoder.cc:106-136): an earlier EXTRACT of the batch (HIT), a live
+// persistent entry (GHIT: use, replace if the bytes differ) or an ENTER; a
+// REF (:141-163) hits likewise or is unknown -- the stream stops at the first
+// one.  After the stop point decode_skim (:196-272) still looks up every REF
+// (a hit refreshes the entry) against the cache as it stands there.
+// ev[decl_base[c] + k]: (lo, hi, op offset, kind << 30 | ref) with GMISS =
+// no cache effect; ENTERs also as declaration rows.  One wave per chunk.
+__global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const uint4* raw, uint4* ev, uint32_t* nev,
+                                                           uint4* drow, uint32_t* ndecl, uint32_t maxd,
+                                                           uint64_t blockp, uint64_t* block_new, uint32_t* changes,
+                                                           int first) {
+  const uint32_t c = blockIdx.x * 4u + (uint32_t)readfirst(threadIdx.x >> 6);
+  if (c >= prm.n) return;
+  const uint32_t cnt = (uint32_t)prm.n_decl[c];
+  const uint64_t base = prm.decl_base[c];
+  const uint64_t tb = blockp == ~0ull ? ~0ull : ((blockp >> 32 << 21) | (uint32_t)blockp);
+  uint32_t nd = 0;
+  bool chg = false;
+  for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+    const uint32_t k = k0 + (uint32_t)lane_id();
+    const bool valid = k < cnt;
+    uint4 r = valid ? raw[base + k] : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t here = spos(c, r.z), t = ((uint64_t)c << 21) | r.z;
+    uint32_t kind = EV_GMISS, ref = 0;
+    bool enter = false;
+    if (valid) {
+      const uint64_t e = tab_lookup_t(prm.x, r.x, r.y);
+      if (here <= blockp) {                           // (the op at the stop point is looked at again)
+        if (e != ~0ull && e < here) {
+          kind = EV_HIT;
+        } else {
+          const uint64_t gv = tab_lookup_t(prm.g, r.x, r.y);
+          if (gv != ~0ull && t < prm.ptime[gv]) {
+            kind = EV_GHIT;
+            ref = (uint32_t)gv;
+          } else if (r.w == OP_EXTRACT) {
+            enter = true;
+          } else {
+            atomicMin((unsigned long long*)block_new, (unsigned long long)here);   // unknown REF
+          }
+        }
+      } else if (r.w == OP_REF) {                     // decode_skim's lookup, cache as at the stop
+        if (e != ~0ull && e < blockp) {
+          kind = EV_HIT;
+        } else {
+          const uint64_t gv = tab_lookup_t(prm.g, r.x, r.y);
+          if (gv != ~0ull && tb < prm.ptime[gv]) {
+            kind = EV_GHIT;
+            ref = (uint32_t)gv;
+          }
+        }
+      }
+    }
+    const uint64_t m = ballot(enter);
+    if (enter) {
+      const uint32_t d = nd + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      kind = EV_ENTER;
+      ref = d;
+      if (d < maxd) drow[(uint64_t)c * maxd + d] = make_uint4(r.x, r.y, r.z + 2u, 0u);
+    }
+    nd += (uint32_t)__builtin_popcountll(m);
+    if (valid) {
+      const uint32_t w = (kind << 30) | ref;
+      chg |= first || ev[base + k].w != w;
+      ev[base + k] = make_uint4(r.x, r.y, r.z, w);
+    }
+  }
+  if (ballot(chg) != 0 && lane_id() == 0) atomicAdd(changes, 1u);
+  if (lane_id() == 0) {
+    nev[c] = cnt;
+    ndecl[c] = nd;
+    if (nd > maxd) atomicOr(prm.status, 1 << 11);
+  }
+}
+
+// EXTRACTs that looked up a live entry: replace its bytes if they differ
+// (XCodecMemoryCache::replace, :130); a second EXTRACT of a hash in the batch
+// with other bytes is the name reuse the batch decoder does not model (bit 9).
+__global__ __launch_bounds__(256) void dec_replace_kernel(DecParams prm, const uint4* raw, const uint4* ev,
+                                                          uint8_t* pool) {
+  const uint32_t c = blockIdx.x * 4u + (uint32_t)readfirst(threadIdx.x >> 6);
+  if (c >= prm.n) return;
+  const uint32_t cnt = (uint32_t)prm.n_decl[c];
+  const uint64_t base = prm.decl_base[c];
+  const uint8_t* x = prm.in + prm.chunk_off[c];
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint4 e = ev[base + k];
+    const uint32_t kind = readfirst(e.w) >> 30;
+    if (readfirst(raw[base + k].w) != OP_EXTRACT || (kind != EV_GHIT && kind != EV_HIT)) continue;
+    const uint8_t* src = x + readfirst(e.z) + 2;
+    if (kind == EV_GHIT) {
+      uint8_t* dst = pool + (uint64_t)(readfirst(e.w) & EV_REF_MASK) * SEG;
+      if (!dec_equal2048(dst, src)) wave_copy2048(dst, src);
+    } else {
+      const uint64_t first = tab_lookup(prm.x, readfirst(e.x), readfirst(e.y));
+      const uint8_t* s0 = prm.in + prm.chunk_off[first >> 32] + (uint32_t)first;
+      if (!dec_equal2048(s0, src) && lane_id() == 0) atomicOr(prm.status, 1 << 9);
+    }
   }
 }
 
@@ -801,6 +957,8 @@ struct XcgDecodeArgs {
   uint64_t* win_hash;    // the decoder's BACKREF window
   uint8_t* win_seg;
   uint64_t win_count;
+  XcgLruState* lru;      // bounded cache (null: unbounded)
+  uint32_t maxd;         // EXTRACTs a chunk can hold (bounded: declaration rows per chunk)
 };
 
 // Returns 0, -75 (output too small) or -5.  Outputs: total decoded bytes, the
@@ -855,6 +1013,64 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
       hipStreamSynchronize(stream) != hipSuccess)
     return -5;
   const uint64_t ndecl = a->h_scratch[3], nbref = a->h_scratch[4];
+  // Bounded cache: classify every op against the eviction times until they
+  // agree (xcg_lru.hip); the passes below then see the cache as it evolves.
+  uint8_t* lru_mem = nullptr;
+  LruBatch lb{};
+  uint4 *raw = nullptr, *evs = nullptr;
+  if (a->lru) {
+    if (nbref > 0) return -95;                       // (BACKREF stop points are not modelled on a bounded cache)
+    XcgLruState* L = a->lru;
+    const uint64_t m = ndecl ? ndecl : 1;
+    // raw ops, classified ops, declaration rows | evtime | evslot, per-chunk
+    // counts, bases, flags
+    const uint64_t bytes = 32 * m + 16ull * n * a->maxd + 8 * m + 4 * m + 20ull * (n + 1) + 64;
+    if (hipMallocAsync((void**)&lru_mem, bytes, stream) != hipSuccess) return -5;
+    raw = (uint4*)lru_mem;
+    evs = raw + m;
+    uint4* drow = evs + m;
+    L->evtime = (uint64_t*)(drow + (uint64_t)n * a->maxd);
+    L->evslot = (uint32_t*)(L->evtime + m);
+    uint32_t* nev32 = L->evslot + m;
+    uint32_t* nd32 = nev32 + (n + 1);
+    uint32_t* need = nd32 + (n + 1);
+    L->ev_base = need + (n + 1);
+    L->enter_base = L->ev_base + (n + 1);
+    uint64_t* blk = (uint64_t*)(((uintptr_t)(L->enter_base + n + 1) + 15) & ~(uintptr_t)15);
+    uint32_t* changes = (uint32_t*)(blk + 1);
+    lb = LruBatch{n, a->in, a->chunk_off, drow, nd32, a->maxd, evs, nev32, 0xFFFFFFFFu, 1, need,
+                  a->g_keys, a->g_vals, a->g_mask, a->pool, a->nseg, a->g_filt, a->g_ftab, a->fmask,
+                  a->g_gfilt, a->gmask, a->status};
+    auto fail = [&](int rc) {
+      (void)hipFreeAsync(lru_mem, stream);
+      return rc;
+    };
+    hipLaunchKernelGGL(dec_ops_kernel, grid, block, 0, stream, p, raw);
+    if (xcg_lru_reset_times(L, stream)) return fail(-5);
+    p.ptime = L->ptime;
+    uint64_t blockp = ~0ull;
+    bool agreed = false;
+    for (int pass = 0; pass < 64 && !agreed; ++pass) {
+      if (hipMemsetAsync(blk, 0xFF, 8, stream) != hipSuccess || hipMemsetAsync(changes, 0, 4, stream) != hipSuccess)
+        return fail(-5);
+      hipLaunchKernelGGL(dec_classify_kernel, grid, block, 0, stream, p, (const uint4*)raw, evs, nev32, drow, nd32,
+                         a->maxd, blockp, blk, changes, pass == 0 ? 1 : 0);
+      if (xcg_lru_times(&lb, L, stream)) return fail(-5);   // (synchronises)
+      if (hipMemcpyAsync(a->h_scratch + 8, blk, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess)
+        return fail(-5);
+      const uint64_t nb = a->h_scratch[8];
+      const uint32_t nchg = (uint32_t)a->h_scratch[9];
+      if ((uint64_t)L->h_tot[1] + L->h_tot[8] > L->C) return fail(-95);   // enters + persistent lookups > limit
+      if (getenv("XCG_LRU_DEBUG"))
+        fprintf(stderr, "lru-dec: n %u pass %d enters %u evict %u live %u hits %u changes %u block %llx -> %llx\n", n,
+                pass, L->h_tot[1], L->h_tot[2], L->h_tot[3], L->h_tot[8], nchg, (unsigned long long)blockp,
+                (unsigned long long)nb);
+      agreed = nchg == 0 && nb == blockp;
+      blockp = nb;
+    }
+    if (!agreed) return fail(-75);
+  }
   uint4* dfull = nullptr;
   if (nbref > 0 && ndecl > 0) {
     // BACKREFs present: records of every declare (rare; never made by XCodecEncoder)
@@ -880,6 +1096,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   *nunknown_out = (uint32_t)(a->h_scratch[6] & 0xFFFFFFFFu);
   if (*total_out > a->out_cap) {
     if (dfull) (void)hipFreeAsync(dfull, stream);
+    if (lru_mem) (void)hipFreeAsync(lru_mem, stream);
     return -75;
   }
   hipLaunchKernelGGL(decode_kernel<true>, grid, block, 0, stream, p);
@@ -890,9 +1107,16 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
   }
   hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
-  const uint64_t slots = (uint64_t)a->x_mask + 1;
-  hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, p,
-                     a->pool, a->nseg, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask});
+  if (a->lru) {
+    hipLaunchKernelGGL(dec_replace_kernel, grid, block, 0, stream, p, (const uint4*)raw, (const uint4*)evs, a->pool);
+    const int crc = xcg_lru_commit(&lb, a->lru, stream);
+    (void)hipFreeAsync(lru_mem, stream);
+    if (crc) return crc;
+  } else {
+    const uint64_t slots = (uint64_t)a->x_mask + 1;
+    hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, p,
+                       a->pool, a->nseg, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask});
+  }
   if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

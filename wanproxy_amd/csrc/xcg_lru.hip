@@ -115,20 +115,36 @@ __global__ __launch_bounds__(1024) void lru_prep_kernel(uint32_t n, const uint32
 
 // tau[j] = time of the enter that makes eviction j; hmin[s] = first lookup hit
 // of persistent slot s.
-__global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
-                                                         const uint32_t* nev, const uint32_t* enter_base,
+// Reference lists: chunk c's k-th reference is ev[row(c) + k], k < nev[c]
+// (capped at maxe); row(c) = c * maxe (the encoder's fixed rows) or, dense,
+// ev_base[c] (the decoder's, packed by op).  One wave per chunk.
+struct EvRows {
+  const uint4* ev;
+  const uint32_t* nev;
+  const uint32_t* ev_base;
+  uint32_t maxe;
+  bool dense;
+  __device__ uint64_t row(uint32_t c) const { return dense ? (uint64_t)ev_base[c] : (uint64_t)c * maxe; }
+  __device__ uint32_t count(uint32_t c) const { return min(nev[c], maxe); }
+};
+__device__ __forceinline__ uint32_t wave_chunk() { return blockIdx.x * 4u + readfirst(threadIdx.x >> 6); }
+
+__global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, EvRows R, const uint32_t* enter_base,
                                                          const uint32_t* tot, uint32_t C, uint64_t* hmin,
                                                          uint64_t* tau) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
-  if (c >= n || k >= min(nev[c], maxe)) return;
-  const uint4 e = ev[i];
-  const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
-  if (kind == EV_ENTER) {
-    const uint32_t ge = enter_base[c] + ref, thr = C - tot[T_A];
-    if (ge >= thr) tau[ge - thr] = ev_time(c, e);
-  } else if (kind == EV_GHIT) {
-    atomicMin((unsigned long long*)&hmin[ref], (unsigned long long)ev_time(c, e));
+  const uint32_t c = wave_chunk();
+  if (c >= n) return;
+  const uint64_t r0 = R.row(c);
+  const uint32_t cnt = R.count(c);
+  for (uint32_t k = lane_id(); k < cnt; k += 64) {
+    const uint4 e = R.ev[r0 + k];
+    const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+    if (kind == EV_ENTER) {
+      const uint32_t ge = enter_base[c] + ref, thr = C - tot[T_A];
+      if (ge >= thr) tau[ge - thr] = ev_time(c, e);
+    } else if (kind == EV_GHIT) {
+      atomicMin((unsigned long long*)&hmin[ref], (unsigned long long)ev_time(c, e));
+    }
   }
 }
 
@@ -168,21 +184,24 @@ __global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, u
 }
 
 // Every recorded lookup of a persistent entry against the recomputed times.
-__global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
-                                                        const uint32_t* nev, const uint64_t* hmin,
+__global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, const uint64_t* hmin,
                                                         const uint64_t* wpop, uint32_t* need, uint32_t* tot) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
+  const uint32_t c = wave_chunk();
+  if (c >= n) return;
+  const uint64_t r0 = R.row(c);
+  const uint32_t cnt = R.count(c);
   bool bad = false;
-  if (c < n && k < min(nev[c], maxe)) {
-    const uint4 e = ev[i];
+  for (uint32_t k = lane_id(); k < cnt; k += 64) {
+    const uint4 e = R.ev[r0 + k];
     const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
     const uint64_t t = ev_time(c, e);
-    if (kind == EV_GHIT) bad = t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
-    else if (kind == EV_GMISS) bad = !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
+    if (kind == EV_GHIT) bad |= t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
+    else if (kind == EV_GMISS) bad |= !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
   }
-  if (bad) need[c] = 1u;                              // the next pass re-parses chunk c
-  if (ballot(bad) != 0 && lane_id() == 0) atomicAdd(&tot[T_BAD], 1u);
+  if (ballot(bad) != 0 && lane_id() == 0) {
+    need[c] = 1u;                                     // the next pass re-parses chunk c
+    atomicAdd(&tot[T_BAD], 1u);
+  }
 }
 
 // ---- commit
@@ -257,25 +276,26 @@ __global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const u
 
 // Every reference's slot (evslot, in stream order) and time; lastref = the
 // latest reference of each slot.
-__global__ __launch_bounds__(256) void lru_lastref_kernel(uint32_t n, uint32_t maxe, const uint4* ev,
-                                                          const uint32_t* nev, const uint32_t* ev_base,
-                                                          const uint32_t* enter_base, const uint32_t* freel,
-                                                          HashTab g, uint64_t clock, uint64_t* lastref,
-                                                          uint32_t* evslot, uint64_t* evtime) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = (uint32_t)(i / maxe), k = (uint32_t)(i % maxe);
-  if (c >= n || k >= min(nev[c], maxe)) return;
-  const uint4 e = ev[i];
-  const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
-  uint32_t s = ~0u;
-  if (kind == EV_ENTER) s = freel[enter_base[c] + ref];
-  else if (kind == EV_GHIT) s = ref;
-  else if (kind == EV_HIT) s = (uint32_t)tab_lookup_t(g, e.x, e.y);
-  const uint64_t t = clock + ev_time(c, e);
-  const uint32_t gi = ev_base[c] + k;
-  evslot[gi] = s;
-  evtime[gi] = t;
-  if (s != ~0u) atomicMax((unsigned long long*)&lastref[s], (unsigned long long)t);
+__global__ __launch_bounds__(256) void lru_lastref_kernel(uint32_t n, EvRows R, const uint32_t* enter_base,
+                                                          const uint32_t* freel, HashTab g, uint64_t clock,
+                                                          uint64_t* lastref, uint32_t* evslot, uint64_t* evtime) {
+  const uint32_t c = wave_chunk();
+  if (c >= n) return;
+  const uint64_t r0 = R.row(c);
+  const uint32_t cnt = R.count(c);
+  for (uint32_t k = lane_id(); k < cnt; k += 64) {
+    const uint4 e = R.ev[r0 + k];
+    const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+    uint32_t s = ~0u;
+    if (kind == EV_ENTER) s = freel[enter_base[c] + ref];
+    else if (kind == EV_GHIT) s = ref;
+    else if (kind == EV_HIT) s = (uint32_t)tab_lookup_t(g, e.x, e.y);
+    const uint64_t t = clock + ev_time(c, e);
+    const uint32_t gi = R.ev_base[c] + k;
+    evslot[gi] = s;
+    evtime[gi] = t;
+    if (s != ~0u) atomicMax((unsigned long long*)&lastref[s], (unsigned long long)t);
+  }
 }
 
 // The new LRU order: persistent entries the batch left alone, in their old
@@ -311,27 +331,6 @@ __global__ __launch_bounds__(1024) void lru_queue_kernel(uint32_t* tot, const ui
 
 }  // namespace xcg
 
-struct XcgLruState {
-  uint32_t C;
-  uint64_t* skey;
-  uint64_t* lastref;
-  uint32_t* queue;
-  uint32_t* queue2;
-  uint64_t* ptime;
-  uint64_t* hmin;
-  uint64_t* wpop;
-  uint64_t* tau;
-  uint32_t* alive;
-  uint32_t* freel;
-  uint32_t* evslot;
-  uint64_t* evtime;
-  uint32_t* ev_base;      // [n_cap + 1]
-  uint32_t* enter_base;   // [n_cap + 1]
-  uint32_t* tot;          // [16]
-  uint32_t* h_tot;        // pinned [16]
-  uint64_t clock;
-};
-
 namespace {
 
 bool lru_debug() {
@@ -341,26 +340,32 @@ bool lru_debug() {
 
 unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
 
-// Recompute eviction times from the parse's references; h_tot gets the totals
-// (T_BAD = inconsistent lookups).  Synchronises `st`.
-int lru_analyze(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+LruBatch batch_of(const XcgStreamArgs& a) {
+  return LruBatch{a.n, a.in, a.chunk_off, a.decl, a.ndecl, a.maxd, a.ev, a.nev, a.maxe, 0, a.need,
+                  a.g_keys, a.g_vals, a.g_mask, a.pool, a.nseg, a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask,
+                  a.status};
+}
+
+// Eviction times from a batch's references: tau, first hits, the LRU-order
+// scan (ptime, wpop), and -- check != 0 -- every recorded persistent lookup
+// against them.  h_tot gets the totals.  Synchronises `st`.
+int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   using namespace xcg;
-  const uint32_t n = a.n, maxe = a.maxe;
-  const uint4* ev = (const uint4*)a.ev;
-  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev,
-                     (const uint32_t*)a.ndecl, maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base,
-                     a.need, L->tot);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
-                     L->hmin, L->C, NEVER);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(grid_for(L->C) < 1024 ? grid_for(L->C) : 1024), dim3(256), 0, st,
-                     L->tau, L->C, NEVER);
-  const uint64_t ne = (uint64_t)n * maxe;
-  hipLaunchKernelGGL(lru_events_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
-                     (const uint32_t*)L->enter_base, (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
+  const uint32_t n = b.n;
+  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, b.nev, b.ndecl, b.maxe, L->C,
+                     (const uint32_t*)b.nseg, L->ev_base, L->enter_base, b.need, L->tot);
+  const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
+  const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
+  const dim3 wgrid((n + 3) / 4);
+  hipLaunchKernelGGL(lru_events_kernel, wgrid, dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
   hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
                      (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
-  hipLaunchKernelGGL(lru_check_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, ev, (const uint32_t*)a.nev,
-                     (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, a.need, L->tot);
+  if (check)
+    hipLaunchKernelGGL(lru_check_kernel, wgrid, dim3(256), 0, st, n, R, (const uint64_t*)L->hmin,
+                       (const uint64_t*)L->wpop, b.need, L->tot);
   if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return -5;
@@ -384,31 +389,36 @@ void lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
                      (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
 }
 
-int lru_commit(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+}  // namespace
+
+// Commit a consistent batch (its references as lru_times last saw them):
+// evict, number the new entries, rebuild table + probe structures, new LRU
+// order.  Asynchronous.
+extern "C" int xcg_lru_commit(const LruBatch* bp, XcgLruState* L, hipStream_t st) {
   using namespace xcg;
-  const uint32_t n = a.n, maxe = a.maxe, C = L->C;
+  const LruBatch& b = *bp;
+  const uint32_t n = b.n, C = L->C;
   const unsigned cg = grid_for(C) < 1024 ? grid_for(C) : 1024;
   hipLaunchKernelGGL(lru_fill32_kernel, dim3(cg), dim3(256), 0, st, L->alive, C, 0u);
   hipLaunchKernelGGL(lru_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, (const uint32_t*)L->tot,
                      (const uint32_t*)L->queue, (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->alive);
   hipLaunchKernelGGL(lru_free_kernel, dim3(1), dim3(1024), 0, st, C, (const uint32_t*)L->alive, L->freel, L->tot);
-  const HashTab g{a.g_keys, a.g_vals, a.g_mask};
-  const FiltSet fs{a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask};
-  Wipe w{g, a.g_filt, (u32x4*)a.g_ftab, a.fmask + 1, a.g_gfilt, a.gmask + 1};
+  const HashTab g{b.g_keys, b.g_vals, b.g_mask};
+  const FiltSet fs{b.g_filt, b.g_ftab, b.fmask, b.g_gfilt, b.gmask};
+  Wipe w{g, b.g_filt, (u32x4*)b.g_ftab, b.fmask + 1, b.g_gfilt, b.gmask + 1};
   hipLaunchKernelGGL(lru_wipe_kernel, dim3(1024), dim3(256), 0, st, w);
   hipLaunchKernelGGL(lru_insert_alive_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, (const uint32_t*)L->alive,
-                     (const uint64_t*)L->skey, g, fs, a.status);
-  const uint64_t waves = (uint64_t)n * a.maxd;
+                     (const uint64_t*)L->skey, g, fs, b.status);
+  const uint64_t waves = (uint64_t)n * b.maxd;
   hipLaunchKernelGGL(lru_insert_new_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, n,
-                     (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->freel, a.in, a.chunk_off, L->skey, L->alive, g, a.pool, fs, a.status);
-  const uint64_t ne = (uint64_t)n * maxe;
-  hipLaunchKernelGGL(lru_lastref_kernel, dim3(grid_for(ne)), dim3(256), 0, st, n, maxe, (const uint4*)a.ev,
-                     (const uint32_t*)a.nev, (const uint32_t*)L->ev_base, (const uint32_t*)L->enter_base,
+                     (const uint4*)b.decl, b.ndecl, b.maxd, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->freel, b.in, b.chunk_off, L->skey, L->alive, g, b.pool, fs, b.status);
+  const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
+  hipLaunchKernelGGL(lru_lastref_kernel, dim3((n + 3) / 4), dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
                      (const uint32_t*)L->freel, g, L->clock, L->lastref, L->evslot, L->evtime);
   hipLaunchKernelGGL(lru_queue_kernel, dim3(1), dim3(1024), 0, st, L->tot, (const uint32_t*)L->queue,
                      (const uint32_t*)L->alive, (const uint64_t*)L->lastref, L->clock, (const uint32_t*)L->evslot,
-                     (const uint64_t*)L->evtime, L->queue2, a.nseg);
+                     (const uint64_t*)L->evtime, L->queue2, b.nseg);
   if (hipGetLastError() != hipSuccess) return -5;
   uint32_t* q = L->queue;
   L->queue = L->queue2;
@@ -417,7 +427,16 @@ int lru_commit(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   return 0;
 }
 
-}  // namespace
+// Eviction times of a batch whose references are already classified (the
+// decoder's: fixed by the stream).  h_tot: totals.  Synchronises.
+extern "C" int xcg_lru_times(const LruBatch* b, XcgLruState* L, hipStream_t st) { return lru_times(*b, L, false, st); }
+
+extern "C" int xcg_lru_reset_times(XcgLruState* L, hipStream_t st) {
+  using namespace xcg;
+  const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->ptime, L->C, NEVER);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 // Stream-semantics encode of a batch on a bounded cache.  The batch is cut
 // into sub-batches with N + H <= C (the bound the eviction rule above needs; a
@@ -457,7 +476,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
       if (rc) return rc;
-      if (lru_analyze(a, L, st)) return -5;
+      if (lru_times(batch_of(a), L, true, st)) return -5;
       if (lru_debug())
         fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u\n", i0,
                 m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
@@ -471,7 +490,8 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       per = m / 2;                                   // redo this part in halves
       continue;
     }
-    if (lru_commit(a, L, st)) return -5;
+    const LruBatch b = batch_of(a);
+    if (xcg_lru_commit(&b, L, st)) return -5;
     i0 += m;
     const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
     const uint64_t want = used ? (uint64_t)C * 9 / 10 * m / used : (uint64_t)n;

@@ -32,6 +32,9 @@ XCG_EOVERFLOW = -75
 _lib = None
 
 
+XCG_ENOENT = -2
+
+
 class XCGError(RuntimeError):
     pass
 
@@ -155,6 +158,21 @@ class Context:
     # The persistent cache (XCG_SEM_STREAM): XCodecMemoryCache of the encoder.
     def cache_size(self) -> int:
         return int(lib().xcg_cache_size(self.h))
+
+    def cache_lookup(self, h: int):
+        """XCodecCache::lookup of one hash: its 2048 bytes, or None (a hit
+        refreshes a bounded cache's LRU order)."""
+        buf = (C.c_uint8 * 2048)()
+        rc = lib().xcg_cache_lookup_host(self.h, C.c_uint64(h), buf)
+        if rc == XCG_ENOENT:
+            return None
+        _check(rc)
+        return bytes(buf)
+
+    def cache_enter(self, h: int, seg: bytes):
+        """enter (or replace the bytes of) one segment -- XCodecPipePair's <LEARN>."""
+        assert len(seg) == 2048
+        _check(lib().xcg_cache_enter_host(self.h, C.c_uint64(h), (C.c_uint8 * 2048).from_buffer_copy(seg)))
 
     def cache_clear(self):
         _check(lib().xcg_cache_clear(self.h))
