@@ -145,3 +145,36 @@ def test_partial_ops_wait_for_more(ctxs):
         _, local, _, _ = b.decoder_consume(wire[i:i + 777])
         got += local
     assert got == m
+
+
+def test_bounded_caches_like_wanproxy_conf(oracle):
+    """wanproxy.conf's sized memory caches (LRU eviction) on both sides: the
+    frames equal the oracle's with the same bounded cache, and the peer's
+    bounded decoder cache stays in step (no <ASK>)."""
+    from oracle.pipe import encoder_stream
+    from wanproxy_amd.xcgpu import Context, PipePair
+    limit = 600 * 2048
+    enc, adec = Context(0, memory_cache_limit=limit), Context(0, memory_cache_limit=limit)
+    benc, bdec = Context(0, memory_cache_limit=limit), Context(0, memory_cache_limit=limit)
+    a = PipePair(enc, adec, UUID_A)
+    b = PipePair(benc, bdec, UUID_B)
+    # one frame per read (a decode call on a bounded cache holds at most its
+    # limit in references); later messages repeat earlier ones, some of whose
+    # segments the LRU has evicted by then
+    msgs = [payload(40 + i % 7, 400_000 + 9_000 * i) for i in range(14)]
+    wires = []
+    for m in msgs:
+        w = a.encoder_consume(m)
+        wires.append(w)
+        to_a, local, _, _ = b.decoder_consume(w)
+        assert local == m and b'\xf0' not in to_a
+        a.decoder_consume(to_a)
+    cache = oracle.cache_new(limit)
+    try:
+        exp = encoder_stream(oracle, cache, UUID_A, msgs)
+    finally:
+        oracle.cache_free(cache)
+    assert b''.join(wires) == exp
+    assert enc.cache_size() == bdec.cache_size() <= 600
+    for c in (enc, adec, benc, bdec):
+        c.close()

@@ -46,11 +46,16 @@ namespace xcg {
 // there -- plus the exact records the slots point to.  The key tables of a
 // block's waves sit first in LDS, 8 << LOGNB bytes each, so a lane's probe
 // address is a single and-or of K.
+// Overflow keys a chunk's table holds: 8, or 32 for frames of up to 512 KiB
+// (~256 declarations in 1024 buckets: a tail of 9+ three-key buckets happens).
+template <int MAXD>
+constexpr int ovf_cap() { return MAXD > 72 ? 32 : 8; }
+
 template <int LOGNB, int MAXD>
 struct WaveRecs {
   static constexpr int NB = 1 << LOGNB;
   uint32_t rlo[MAXD], rhi[MAXD], rc[MAXD];  // exact hash + chunk position
-  uint32_t ovf_k[8];          // keys whose bucket was full
+  uint32_t ovf_k[ovf_cap<MAXD>()];          // keys whose bucket was full
 };
 
 template <int LOGNB>
@@ -357,7 +362,7 @@ __device__ __forceinline__ void glb_flush(GlbQ& gq) {
 // at q0 (RollingHash::roll, xcodec_hash.h:57-70, negated), so K = -lo costs one
 // instruction.  C0: the pending candidate (key c0k) is not in the table yet and
 // becomes visible at piece offset rvis (position p + rvis).  OVF: also compare the (rare) overflow
-// keys ovk[8].  FM: also run pass 1 of the persistent cache / batch probe (gq)
+// keys ovk[NOVF].  FM: also run pass 1 of the persistent cache / batch probe (gq)
 // through the LDS lane filter (1) or the global one (2); 0: no such probe.
 template <int LOGNB, bool C0, int NOVF, int FM>
 __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
@@ -369,9 +374,9 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
   const uint32_t KM = (uint32_t)opaque((int)(((1u << LOGNB) - 1u) << 3));
   const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
   const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
-  uint32_t o[8];
+  uint32_t o[NOVF > 0 ? NOVF : 1];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = k < NOVF ? ovk[k] : 0u;
+  for (int k = 0; k < NOVF; ++k) o[k] = ovk[k];
   // C0 visibility: lanes l with 32 l + j >= rvis.  With rvis = 32 A + B that is
   // l >= A + 1 for j < B and l >= A for j >= B -- two masks per piece.
   uint64_t vis_hi = 0, vis_lo = 0;
@@ -554,10 +559,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
       if (s0 == ke) keyt[2 * b] = k;
       else if (s1 == ke) keyt[2 * b + 1] = k;
-      else if (novf < 8) T.ovf_k[novf] = k;
+      else if (novf < (uint32_t)ovf_cap<MAXD>()) T.ovf_k[novf] = k;
     }
     if (s0 != ke && s1 != ke) {
-      if (novf < 8) ++novf;
+      if (novf < (uint32_t)ovf_cap<MAXD>()) ++novf;
       else if (l == 0 && prm.status) atomicOr(prm.status, 1);
     }
     __builtin_amdgcn_wave_barrier();
@@ -762,10 +767,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         const int rvis = vis - p;
         const uint32_t c0k = probe_key(cand_lo);
         // Bucket overflows are rare (three of a chunk's keys in one 2-slot
-        // bucket); one overflow key costs one compare, more cost eight.
-        uint32_t ovk[8];
+        // bucket); one overflow key costs one compare, more cost eight (32
+        // beyond eight, in frames of up to 512 KiB).
+        constexpr int OC = ovf_cap<MAXD>();
+        uint32_t ovk[OC];
   #pragma unroll
-        for (int k = 0; k < 8; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
+        for (int k = 0; k < OC; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
         const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
         GlbQ gq{gs.lds, gs.lfo, prm.lf.gfilt, prm.lf.gmask, prm.lf.ftab, prm.lf.fmask, sa0, sa0, sa0 + 256u * GSLOTS,
                 0u, 0u};
@@ -779,11 +786,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         using N0 = std::integral_constant<int, 0>;
         using N1 = std::integral_constant<int, 1>;
         using N8 = std::integral_constant<int, 8>;
+        using NC = std::integral_constant<int, OC>;
         auto by_novf = [&](auto glbt) {
           if (novf == 0) return c0 ? roll(T1{}, N0{}, glbt) : roll(T0{}, N0{}, glbt);
           if (novf == 1) return c0 ? roll(T1{}, N1{}, glbt) : roll(T0{}, N1{}, glbt);
           // duplicates of a real overflow key pad the unused slots
-          return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
+          if (OC == 8 || novf <= 8) return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
+          return c0 ? roll(T1{}, NC{}, glbt) : roll(T0{}, NC{}, glbt);
         };
         if (STREAM && gs.fmode == 1) {
           ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});

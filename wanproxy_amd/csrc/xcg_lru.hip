@@ -477,10 +477,13 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       rounds += r;
       if (rc) return rc;
       if (lru_times(batch_of(a), L, true, st)) return -5;
-      if (lru_debug())
-        fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u\n", i0,
-                m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
-                L->h_tot[T_OVF]);
+      if (lru_debug()) {
+        int32_t stw = 0;
+        (void)hipMemcpy(&stw, a.status, 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u status %x\n",
+                i0, m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
+                L->h_tot[T_OVF], stw);
+      }
       if (L->h_tot[T_OVF]) return -75;
       if ((uint64_t)L->h_tot[T_N] + L->h_tot[T_H] > C) split = true;
       else if (L->h_tot[T_BAD] == 0) done = true;
