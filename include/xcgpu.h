@@ -89,11 +89,12 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
  * `set <cache>.size`, programs/wanproxy/wanproxy_config_class_cache.cc:66):
  * limit = bytes / 2048 segments (at least 1); entering at the limit evicts the
  * least recently entered-or-looked-up segment (XCodecLRU, xcodec/xcodec_lru.h).
- * XCG_SEM_STREAM batches stay bit-exact with the sequential encoder; a chunk
- * whose own cache references (declarations + REFs + collision lookups) exceed
- * the limit is XCG_ENOTSUP, as is XCG_SEM_INDEPENDENT with chunks of more than
- * limit * 2048 bytes, and (this version) decoding and the single-segment host
- * calls on a bounded context. */
+ * XCG_SEM_STREAM batches, decode batches and the single-segment host calls
+ * stay bit-exact with the sequential XCodecEncoder / XCodecDecoder on such a
+ * cache.  XCG_ENOTSUP (never a different result): an encode chunk, or a decode
+ * call, whose own enters + persistent-entry lookups exceed the limit (encode
+ * batches are cut into sub-batches that fit); XCG_SEM_INDEPENDENT with chunks of
+ * more than limit * 2048 bytes; BACKREF ops in a decode on a bounded cache. */
 int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_ctx **out);
 void xcg_ctx_destroy(xcg_ctx *ctx);
 
