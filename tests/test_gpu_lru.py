@@ -296,3 +296,20 @@ def test_lru_host_ops_vs_oracle(oracle):
         assert ctx.cache_lookup(k) == o_lookup(k)
     ctx.close()
     oracle.cache_free(oc)
+
+
+def test_lru_out_of_band(oracle):
+    # Out-of-band declarations (F1 02 BE64, XCodecCache::out_of_band()) on a
+    # bounded cache: the eviction order is the same, only the output form differs.
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = mlg.recency_stream(616, 2 << 20, 60, 400)
+    offs, lens = chunks_of(d, 65536)
+    limit = 180 * SEG
+    c = oracle.cache_new(limit)
+    exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, oob=True, cache=c)
+    oracle.cache_free(c)
+    ctx = Context(0, out_of_band=True, memory_cache_limit=limit)
+    got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+    ctx.close()
+    assert got == exp
