@@ -149,20 +149,55 @@ __global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, EvRows R, c
 }
 
 // First guess of a sub-batch's evictions, before any parse: every chunk
-// declares its 2048-byte tiling (the seed; the cold parse) and looks nothing
-// up.  Enter times as the sequential encoder makes them: tile p is declared
-// while examining window p + 2048, or after the last window.
-__global__ __launch_bounds__(256) void lru_seed_tau_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
-                                                           uint32_t maxd, const uint32_t* chunk_len,
-                                                           const uint32_t* enter_base, const uint32_t* tot,
-                                                           uint32_t C, uint64_t* tau) {
+// parses as its 2048-byte tiling (the seed), a tile found in the persistent
+// cache being a REF there (a lookup hit), a tile equal to an earlier tile of
+// the batch a REF too, and every other tile a declaration.  Enter times as
+// the sequential encoder makes them: tile p is declared while examining window
+// p + 2048, or after the last window.  One wave per chunk; pass 0 counts the
+// chunk's enters (cnt) and records the hits, pass 1 places the enters in tau.
+__global__ __launch_bounds__(256) void lru_seed_classify_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                                uint32_t maxd, const uint32_t* chunk_len, HashTab g,
+                                                                HashTab b, uint32_t* cnt, const uint32_t* enter_base,
+                                                                const uint32_t* tot, uint32_t C, uint64_t* hmin,
+                                                                uint64_t* tau, int pass) {
+  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (c >= n) return;
+  const uint32_t nd = ndecl[c], last = chunk_len[c] - SEG;
+  uint32_t ne = 0;
+  for (uint32_t d0 = 0; d0 < nd; d0 += 64) {
+    const uint32_t d = d0 + (uint32_t)lane_id();
+    bool enter = false;
+    uint4 dd = make_uint4(0u, 0u, 0u, 0u);
+    if (d < nd) {
+      dd = decl[(uint64_t)c * maxd + d];
+      const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
+      if (gv != ~0ull) {
+        if (pass == 0)
+          atomicMin((unsigned long long*)&hmin[gv], (unsigned long long)(((uint64_t)c << 21) | (2u * dd.z + 1u)));
+      } else {
+        enter = tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z);   // the earliest tile with this hash
+      }
+    }
+    const uint64_t m = ballot(enter);
+    if (pass == 1 && enter) {
+      const uint32_t o = ne + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const uint32_t t = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
+      const uint32_t ge = enter_base[c] + o, thr = C - tot[T_A];
+      if (ge >= thr) tau[ge - thr] = ((uint64_t)c << 21) | t;
+    }
+    ne += (uint32_t)__builtin_popcountll(m);
+  }
+  if (pass == 0 && lane_id() == 0) cnt[c] = ne;
+}
+
+// The batch's tiles in a scratch table: hash -> earliest (chunk << 32 | position).
+__global__ __launch_bounds__(256) void lru_seed_table_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                             uint32_t maxd, HashTab b, int32_t* status) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = (uint32_t)(i / maxd), d = (uint32_t)(i % maxd);
   if (c >= n || d >= ndecl[c]) return;
-  const uint32_t pos = decl[i].z, last = chunk_len[c] - SEG;
-  const uint32_t t = pos + SEG <= last ? 2u * (pos + SEG) : 2u * (last + 1u);
-  const uint32_t ge = enter_base[c] + d, thr = C - tot[T_A];
-  if (ge >= thr) tau[ge - thr] = ((uint64_t)c << 21) | t;
+  const uint4 dd = decl[i];
+  if (!tab_insert_min(b, dd.x, dd.y, ((uint64_t)c << 32) | dd.z)) atomicOr(status, 2);
 }
 
 // Walk the persistent entries in LRU order: wpop[s] = when the batch's
@@ -372,19 +407,28 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   return 0;
 }
 
-// ptime from the tiling seed (lru_seed_tau_kernel).  Asynchronous.
+// ptime from the tiling seed (lru_seed_classify_kernel).  Asynchronous.
 void lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   using namespace xcg;
   const uint32_t n = a.n;
-  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev,
-                     (const uint32_t*)a.ndecl, a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base,
-                     a.need, L->tot);
   const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
+  const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};   // (b: the rounds rebuild it)
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, b.mask + 1, EMPTY_KEY);
+  hipLaunchKernelGGL(lru_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, b.mask + 1, ~0ull);
+  hipLaunchKernelGGL(lru_seed_table_kernel, dim3(grid_for((uint64_t)n * a.maxd)), dim3(256), 0, st, n,
+                     (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
   hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
   hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
-  hipLaunchKernelGGL(lru_seed_tau_kernel, dim3(grid_for((uint64_t)n * a.maxd)), dim3(256), 0, st, n,
-                     (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, a.chunk_len,
-                     (const uint32_t*)L->enter_base, (const uint32_t*)L->tot, L->C, L->tau);
+  uint32_t* cnt = a.nhits;                         // (scratch until the rounds: round 1 rewrites it)
+  const dim3 wgrid((n + 3) / 4);
+  hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
+                     (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 0);
+  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev, (const uint32_t*)cnt,
+                     a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base, a.need, L->tot);
+  hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
+                     (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
+                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1);
   hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
                      (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
 }
