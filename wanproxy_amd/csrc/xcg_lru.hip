@@ -1,8 +1,9 @@
 // Bounded persistent cache: XCodecMemoryCache with memory_cache_limit_ != 0
 // (xcodec/xcodec_cache.h:277-364) -- at the limit, enter() first evicts the
 // least recently used entry; lookup() and replace() refresh an entry
-// (XCodecLRU, xcodec/xcodec_lru.h:30-104).  Stream-semantics batches stay
-// bit-exact with the sequential encoder.
+// (XCodecLRU, xcodec/xcodec_lru.h:30-104).  Stream-semantics encode batches,
+// decode batches and single-segment host calls stay bit-exact with the
+// sequential XCodecEncoder / XCodecDecoder on such a cache.
 //
 // LRU state in HBM (C = limit in segments = pool slots):
 //   skey[C]     key of the entry in pool slot s
@@ -16,16 +17,19 @@
 // look up: enter number C - A + j (in stream order) evicts the j-th least
 // recently used persistent entry not looked up before that point, and the
 // N + A - C <= A - H evictions never reach an entry the batch itself made or
-// refreshed (those sit above every persistent entry in the LRU order).  For a persistent entry
-// of LRU rank r, with S(r) entries below it that the batch looks up, that is
-// eviction j = r - S(r) at tau[j], unless the batch looks it up first.  The
-// parse takes these eviction times (ptime) as given; the pass below recomputes
+// refreshed (those sit above every persistent entry in the LRU order).  For
+// a persistent entry of LRU rank r, with S(r) entries below it that the batch
+// looks up, that is eviction j = r - S(r) at tau[j], unless the batch looks it
+// up first.  The parse takes these eviction times (ptime) as given; the pass
+// below recomputes
 // them from the references the parse made and checks every recorded lookup of
 // a persistent entry against them -- a hit must come before the entry's
 // eviction, a miss (GMISS) after it.  All checks passing means the parse is
 // the sequential one (by induction over stream time: every lookup result then
 // equals the LRU state the sequential encoder has at that point); otherwise
-// the batch is parsed again with the new times.
+// the chunks with an inconsistent lookup are parsed again with the new times.
+// (The decoder's references follow from the stream, so xcg_decode.hip only
+// alternates classification and these times; see dec_classify_kernel.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
