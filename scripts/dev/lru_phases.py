@@ -1,0 +1,39 @@
+"""Per-chunk phase times of stream parses (diagnostics, GPU box; XCG_PHASES
+build via XCGPU_LIB): vector phase, REF-chaining probes, the rest (resolve
+phase: exact lookups, declarations, output).  Unbounded C5 batch (full
+occupancy) vs the same data on a bounded cache (one wave per SIMD)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..'))
+import numpy as np
+import torch
+
+from wanproxy_amd import synth
+from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+
+CH = 131072
+N = int(os.environ.get('CHUNKS', 4096))
+dev = torch.device('cuda', 0)
+data = np.frombuffer(synth.stream(0xC5, 2 * N * CH, 20, 0), dtype=np.uint8)
+d_in = torch.from_numpy(data.copy()).to(dev)
+d_len = torch.full((N,), CH, dtype=torch.int32, device=dev)
+bound = 2 * CH + 16
+d_oo = torch.arange(N, dtype=torch.int64, device=dev) * bound
+d_out = torch.empty(N * bound, dtype=torch.uint8, device=dev)
+d_ol = torch.zeros(N, dtype=torch.int64, device=dev)
+d_st = torch.zeros(4 * N, dtype=torch.int32, device=dev)
+for name, kw in (('unbounded', dict(cache_segments=1 << 20)), ('bounded', dict(memory_cache_limit=128 << 20))):
+    ctx = Context(0, **kw)
+    for half in range(2):
+        d_off = (torch.arange(N, dtype=torch.int64, device=dev) + half * N) * CH
+        ctx.encode_batch_device(d_in, d_off, d_len, N, CH, d_out, d_oo, d_ol, d_st, semantics=XCG_SEM_STREAM)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy().view(np.uint32).reshape(N, 4).astype(np.float64)
+    w3 = st[:, 3].astype(np.int64)
+    vec, evt, tot, pcs, nev = st[:, 0] / 100, st[:, 1] / 100, st[:, 2] / 100, w3 & 0xFFFF, w3 >> 16
+    rest = tot - vec - evt
+    print(f'{name}: per chunk (us, median) total {np.median(tot):.0f} vector {np.median(vec):.0f} '
+          f'exact events {np.median(evt):.0f} ({np.median(nev):.0f} events, {np.median(evt / np.maximum(nev, 1)):.1f} us each) '
+          f'rest {np.median(rest):.0f}; pieces {np.median(pcs):.0f}')
+    ctx.close()

@@ -263,9 +263,14 @@ int ensure_cache(xcg_ctx* c) {
   g.seg_cap = (uint32_t)segs;
   const uint32_t cap = pow2_at_least(2 * segs + 1024);
   g.mask = cap - 1;
-  const uint32_t fb = pow2_at_least(segs < 65536 ? 32768 : segs / 2);   // ~2 keys per bucket at capacity
+  // ~2 keys per bucket at capacity.  A bounded cache is always full and a
+  // batch's declarations (up to the limit again) share the round's copy, so
+  // it gets ~1 bucket per key (a bucket past 7 fingerprints sends every probe
+  // into an exact check).
+  const uint64_t fkeys = c->bounded ? 4 * segs : segs;
+  const uint32_t fb = pow2_at_least(fkeys < 65536 ? 32768 : fkeys / 2);
   g.fmask = fb - 1;
-  const uint32_t gw = pow2_at_least(segs < 131072 ? 65536 : segs / 2);
+  const uint32_t gw = pow2_at_least(fkeys < 131072 ? 65536 : fkeys / 2);
   g.gmask = gw - 1;
   if (hipMalloc(&g.keys, 8ull * cap) != hipSuccess || hipMalloc(&g.vals, 8ull * cap) != hipSuccess ||
       hipMalloc(&g.pool, segs * (uint64_t)XCG_SEGMENT_LENGTH + 16) != hipSuccess ||

@@ -497,8 +497,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   uint32_t olen = 0;
   uint32_t n_extract = 0, n_ref = 0, n_coll = 0, n_pieces = 0;
 
-#ifdef XCG_TIMING
+#if defined(XCG_TIMING) || defined(XCG_PHASES)
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef XCG_PHASES
+  // diagnostics build: time in the vector phase and in REF-chaining probes
+  uint64_t ph_vec = 0, ph_chain = 0, ph_ev = 0;
+  uint32_t ph_nev = 0;
 #endif
   // A chunk longer than the launch's bound would overrun the records sized
   // for it: refuse it loudly (status bit 3) instead.
@@ -721,6 +726,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // through the filters only, and a miss or a collision falls through to
     // the ordinary vector phase, which decides position s itself.
     if (STREAM && chain && !nullcache) {
+#ifdef XCG_PHASES
+      const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+#endif
       chain = false;
       uint32_t lo, hi;
       if (s == p) {
@@ -742,11 +750,20 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         s = base;
         chain = true;
         totXA = totXB; totTA = totTB;               // (as at the end of a piece)
+#ifdef XCG_PHASES
+        ph_chain += __builtin_amdgcn_s_memrealtime() - tc0;
+#endif
         continue;
       }
+#ifdef XCG_PHASES
+      ph_chain += __builtin_amdgcn_s_memrealtime() - tc0;
+#endif
     }
 
     // ---- vector phase
+#ifdef XCG_PHASES
+    const uint64_t tv0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint32_t ev = 0;
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
     if (!nullcache) {
@@ -811,6 +828,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // resolve phase issues this piece's stores.
     vuse(nb0); vuse(nb1);                          // (unconditional: so the compiler sees them waited)
 
+#ifdef XCG_PHASES
+    ph_vec += __builtin_amdgcn_s_memrealtime() - tv0;
+#endif
     // ---- resolve phase (wave-uniform)
     auto next_event = [&](int from) -> int {
       const int rel = from - p;
@@ -837,6 +857,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       if (have_cand && cand + SEG <= s) declare(s);           // :183-190
       const int e = nullcache ? INT32_MAX : next_event(s);
       if (e == s) {
+#ifdef XCG_PHASES
+        const uint64_t te0 = __builtin_amdgcn_s_memrealtime();
+        ++ph_nev;
+        struct PhEv {
+          uint64_t t0; uint64_t& acc;
+          __device__ ~PhEv() { acc += __builtin_amdgcn_s_memrealtime() - t0; }
+        } ph_guard{te0, ph_ev};
+#endif
         // Exact re-check of the probe (find_reference, :374-416).  A record
         // still missing its hi gets it from the same (single) hash call site,
         // then the window is hashed again.
@@ -934,7 +962,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   if (l == 0) {
     prm.out_len[chunk] = olen;
     if (prm.stats) {
-#ifdef XCG_TIMING
+#if defined(XCG_PHASES)
+      // diagnostics build: {vector phase, REF-chaining probes, whole chunk} (100 MHz ticks), pieces
+      prm.stats[4 * chunk + 0] = (uint32_t)ph_vec;
+      prm.stats[4 * chunk + 1] = (uint32_t)ph_ev;
+      prm.stats[4 * chunk + 2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+      prm.stats[4 * chunk + 3] = (ph_nev << 16) | n_pieces;
+      (void)ph_chain;
+      (void)n_extract; (void)n_ref; (void)n_coll;
+#elif defined(XCG_TIMING)
       // diagnostics build: {start, end} (100 MHz realtime, low words), HW_ID, XCC_ID
       const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
       prm.stats[4 * chunk + 0] = (uint32_t)t_start;
