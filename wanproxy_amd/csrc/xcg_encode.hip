@@ -501,8 +501,11 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifdef XCG_PHASES
+#ifndef XCG_PHASES_SLOT1
+#define XCG_PHASES_SLOT1 0   // 1: stats word 1 = piece setup time instead of exact-event time
+#endif
   // diagnostics build: time in the vector phase and in REF-chaining probes
-  uint64_t ph_vec = 0, ph_chain = 0, ph_ev = 0;
+  uint64_t ph_vec = 0, ph_chain = 0, ph_ev = 0, ph_setup = 0;
   uint32_t ph_nev = 0;
 #endif
   // A chunk longer than the launch's bound would overrun the records sized
@@ -665,6 +668,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   };
 
   while (s <= last) {
+#ifdef XCG_PHASES
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // ---- piece geometry: q0 = p + 32 lane, loads 16-byte aligned in memory
     const int p = s - (int)(((uint32_t)mis + (uint32_t)s) & 15u);
     const int l = opaque(lane_id());
@@ -763,6 +769,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // ---- vector phase
 #ifdef XCG_PHASES
     const uint64_t tv0 = __builtin_amdgcn_s_memrealtime();
+    ph_setup += tv0 - tp0;
 #endif
     uint32_t ev = 0;
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
@@ -965,10 +972,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #if defined(XCG_PHASES)
       // diagnostics build: {vector phase, REF-chaining probes, whole chunk} (100 MHz ticks), pieces
       prm.stats[4 * chunk + 0] = (uint32_t)ph_vec;
-      prm.stats[4 * chunk + 1] = (uint32_t)ph_ev;
+      prm.stats[4 * chunk + 1] = (uint32_t)(XCG_PHASES_SLOT1 ? ph_setup : ph_ev);
       prm.stats[4 * chunk + 2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
       prm.stats[4 * chunk + 3] = (ph_nev << 16) | n_pieces;
-      (void)ph_chain;
+      (void)ph_chain; (void)ph_setup; (void)ph_ev;
       (void)n_extract; (void)n_ref; (void)n_coll;
 #elif defined(XCG_TIMING)
       // diagnostics build: {start, end} (100 MHz realtime, low words), HW_ID, XCC_ID
