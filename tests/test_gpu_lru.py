@@ -313,3 +313,104 @@ def test_lru_out_of_band(oracle):
     got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
     ctx.close()
     assert got == exp
+
+
+def test_lru_fuzz(oracle):
+    # Random limits, chunkings, data shapes and call splits against the oracle.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    rng = np.random.default_rng(2024)
+    for case in range(16):
+        kind = case % 3
+        nbytes = int(rng.integers(1 << 19, 3 << 20))
+        if kind == 0:
+            d = mlg.recency_stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(30, 90)),
+                                   int(rng.integers(50, 3000)))
+        elif kind == 1:
+            d = synth.stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(10, 90)), int(rng.integers(0, 4)))
+        else:   # runs and repeats of a short period: many collisions between nearby windows
+            pat = rng.integers(0, 256, int(rng.integers(100, 5000)), dtype=np.uint8).tobytes()
+            d = (pat * (nbytes // len(pat) + 1))[:nbytes]
+            d = bytearray(d)
+            for _ in range(200):
+                d[int(rng.integers(0, nbytes))] = int(rng.integers(0, 256))
+            d = bytes(d)
+        chunk = int(rng.choice([4096, 20000, 65536, 131072]))
+        offs, lens = synth.chunks_of(d, chunk)
+        limit = int(rng.integers(2 * (chunk // SEG + 1) + 8, 3000)) * SEG
+        exp, esize = oracle_stream(oracle, d, offs, lens, limit)
+        ctx = Context(0, memory_cache_limit=limit)
+        got, i = [], 0
+        while i < len(offs):
+            m = int(rng.integers(1, 40))
+            got += ctx.encode_chunks(d, offs[i:i + m], lens[i:i + m], semantics=XCG_SEM_STREAM)
+            i += m
+        gsize = ctx.cache_size()
+        ctx.close()
+        bad = [k for k in range(len(exp)) if got[k] != exp[k]]
+        assert not bad and gsize == esize, (case, kind, chunk, limit // SEG, bad[:5])
+
+
+def test_lru_short_chunks_between_calls(oracle):
+    # A chunk shorter than one segment makes no cache reference; its (scratch)
+    # reference list must not keep an earlier call's entries.
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = mlg.recency_stream(77, 600_000, 50, 300)
+    offs, lens = chunks_of(d, 4096)
+    offs, lens = list(offs), list(lens)
+    # splice in short chunks: every 5th chunk cut to 100 bytes + remainder
+    o2, l2 = [], []
+    for k, (a, n) in enumerate(zip(offs, lens)):
+        if k % 5 == 3 and n > 100:
+            o2 += [a, a + 100]
+            l2 += [100, n - 100]
+        else:
+            o2.append(a)
+            l2.append(n)
+    o2, l2 = np.array(o2, np.uint64), np.array(l2, np.uint32)
+    limit = 400 * SEG
+    exp, esize = oracle_stream(oracle, d, o2, l2, limit)
+    ctx = Context(0, memory_cache_limit=limit)
+    got, i = [], 0
+    for m in [7, 3, 11, 2, 9] * 200:
+        if i >= len(o2):
+            break
+        got += ctx.encode_chunks(d, o2[i:i + m], l2[i:i + m], semantics=XCG_SEM_STREAM)
+        i += m
+    assert got == exp and ctx.cache_size() == esize
+    ctx.close()
+
+
+def test_lru_decode_fuzz(oracle):
+    # Bounded decoders (GPU and oracle, same limit as the encoder) over random
+    # call splits: same output, same cache size after every call.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    rng = np.random.default_rng(77)
+    for case in range(8):
+        nbytes = int(rng.integers(1 << 19, 2 << 20))
+        if case % 2:
+            d = mlg.recency_stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(30, 90)),
+                                   int(rng.integers(50, 2000)))
+        else:
+            d = synth.stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(10, 90)), int(rng.integers(0, 3)))
+        chunk = int(rng.choice([4096, 30000, 65536]))
+        offs, lens = synth.chunks_of(d, chunk)
+        limit = int(rng.integers(2 * (chunk // SEG + 1) + 8, 1500)) * SEG
+        encs, _ = oracle_stream(oracle, d, offs, lens, limit)
+        dc = oracle.cache_new(limit)
+        dec = oracle.decoder_new(dc)
+        ctx = Context(0, memory_cache_limit=limit)
+        i = 0
+        while i < len(encs):
+            m = int(rng.integers(1, 12))
+            part = encs[i:i + m]
+            outs, st, _, unk = ctx.decode_chunks(part)
+            exp = [oracle.decode(e, dc, decoder=dec)[1] for e in part]
+            assert (st == 0).all() and not unk and outs == exp, (case, i)
+            assert ctx.cache_size() == oracle.lib.xco_cache_size(dc), (case, i)
+            i += m
+        ctx.close()
+        oracle.decoder_free(dec)
+        oracle.cache_free(dc)

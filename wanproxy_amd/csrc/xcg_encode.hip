@@ -514,12 +514,16 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     if (l == 0) {
       prm.out_len[chunk] = 0;
       if (prm.status) atomicOr(prm.status, 8);
+      if (LRU) prm.nev[chunk] = 0;
     }
     return;
   }
   if (L < SEG) {                                   // xcodec_encoder.cc:77-83
     if (L > 0) olen = escape_u(out, x, 0, (uint32_t)L);
-    if (l == 0) prm.out_len[chunk] = olen;
+    if (l == 0) {
+      prm.out_len[chunk] = olen;
+      if (LRU) prm.nev[chunk] = 0;                 // (no cache reference; the list is scratch)
+    }
     return;
   }
 
