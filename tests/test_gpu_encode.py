@@ -144,3 +144,38 @@ def test_overlong_chunk_is_refused():
         with pytest.raises(XCGError):
             ctx.status()
         ctx.close()
+
+
+def test_independent_fuzz(oracle):
+    # Random chunk lengths up to 512 KiB (both kernel variants), in-band,
+    # out-of-band and null-cache declarations, three data shapes.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    rng = np.random.default_rng(4242)
+    for case in range(9):
+        nbytes = int(rng.integers(1 << 19, 4 << 20))
+        kind = case % 3
+        if kind == 0:
+            d = synth.stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(0, 95)), int(rng.integers(0, 5)))
+        elif kind == 1:
+            pat = rng.integers(0, 256, int(rng.integers(1, 5000)), dtype=np.uint8).tobytes()
+            d = (pat * (nbytes // len(pat) + 1))[:nbytes]
+        else:
+            d = bytes(rng.choice([0, 0xF1, 9], size=nbytes, p=[0.4, 0.4, 0.2]).astype(np.uint8))
+        lens, tot = [], 0
+        big = case >= 6
+        while tot < nbytes:
+            n = int(rng.integers(0, 524288 if big else 131072))
+            n = min(n, nbytes - tot)
+            lens.append(n)
+            tot += n
+        lens = np.array(lens, np.uint32)
+        offs = np.zeros(lens.size, np.uint64)
+        offs[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        mode = case % 3                   # 0 in-band, 1 out-of-band, 2 null cache
+        ctx = Context(0, out_of_band=mode != 0, null_cache=mode == 2)   # (TackNullCache is out-of-band)
+        got = ctx.encode_chunks(d, offs, lens)
+        ctx.close()
+        exp = oracle.encode_batch(d, offs, lens, mode=2 if mode == 2 else 0, oob=mode != 0)
+        bad = [k for k in range(len(exp)) if got[k] != exp[k]]
+        assert not bad, (case, kind, mode, bad[:5])

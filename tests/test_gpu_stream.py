@@ -100,3 +100,41 @@ def test_encoder_mirror_tack_loop(oracle):
     out = b''.join(enc.encode(d[i:i + 65536]) for i in range(0, len(d), 65536))
     ctx.close()
     assert out == oracle.encode_stream(d)
+
+
+def test_stream_fuzz_ragged_calls(oracle):
+    # Random chunk lengths (0 .. 70000, segments cut anywhere), random call
+    # splits, three data shapes: one persistent cache, against the oracle.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    rng = np.random.default_rng(909)
+    for case in range(10):
+        nbytes = int(rng.integers(1 << 18, 3 << 20))
+        kind = case % 3
+        if kind == 0:
+            d = synth.stream(int(rng.integers(1 << 30)), nbytes, int(rng.integers(0, 95)), int(rng.integers(0, 5)))
+        elif kind == 1:
+            pat = rng.integers(0, 256, int(rng.integers(1, 3000)), dtype=np.uint8).tobytes()
+            d = (pat * (nbytes // len(pat) + 1))[:nbytes]
+        else:
+            d = bytes(rng.choice([0, 0xF1, 7], size=nbytes, p=[0.5, 0.3, 0.2]).astype(np.uint8))
+        lens = []
+        tot = 0
+        while tot < nbytes:
+            n = int(rng.choice([0, 1, 2047, 2048, 2049, int(rng.integers(0, 70000))]))
+            n = min(n, nbytes - tot)
+            lens.append(n)
+            tot += n
+        lens = np.array(lens, np.uint32)
+        offs = np.zeros(lens.size, np.uint64)
+        offs[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        exp = oracle.encode_batch(d, offs, lens, mode=1)
+        ctx = Context(0, cache_segments=1 << 16)
+        got, i = [], 0
+        while i < len(offs):
+            m = int(rng.integers(1, 60))
+            got += enc_stream(ctx, d, offs[i:i + m], lens[i:i + m])
+            i += m
+        ctx.close()
+        bad = [k for k in range(len(exp)) if got[k] != exp[k]]
+        assert not bad, (case, kind, bad[:5])
