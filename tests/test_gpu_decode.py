@@ -113,3 +113,41 @@ def test_gpu_encode_gpu_decode_stream(dctx):
     dctx.cache_clear()
     outs, st, cons, unk = dctx.decode_chunks(enc)
     assert b''.join(outs) == d and not unk
+
+
+@pytest.mark.parametrize('limit', [0, 900 * 2048])
+def test_decode_fuzz_byte_splits(oracle, limit):
+    # The reference's caller pattern: input arrives in pieces cut anywhere
+    # (ops split across calls); each decode() consumes whole ops and leaves the
+    # rest, which is prepended to the next piece.  GPU XCodecDecoder vs the
+    # oracle's, on an unbounded and on a bounded cache.
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context, XCodecDecoder
+    rng = np.random.default_rng(31 + limit)
+    d = synth.stream(0xDEC, 3 << 20, 60, 3)
+    offs, lens = synth.chunks_of(d, 65536)
+    enc = b''.join(oracle.encode_batch(d, offs, lens, mode=1))
+    ctx = Context(0, memory_cache_limit=limit) if limit else Context(0, cache_segments=1 << 16)
+    gdec = XCodecDecoder(ctx)
+    oc = oracle.cache_new(limit)
+    odec = oracle.decoder_new(oc)
+    gbuf = obuf = b''
+    gout, oout = [], []
+    i = 0
+    while i < len(enc):
+        n = int(rng.choice([1, 2, 9, 10, 11, 2049, 2050, 2051, int(rng.integers(1, 200000))]))
+        piece = enc[i:i + n]
+        i += n
+        gbuf += piece
+        obuf += piece
+        ok, out, cons, unk = gdec.decode(gbuf)
+        ook, oo, ocons, ounk = oracle.decode(obuf, oc, decoder=odec)
+        assert (ok, cons, unk) == (ook, ocons, ounk) and out == oo, i
+        gbuf, obuf = gbuf[cons:], obuf[ocons:]
+        gout.append(out)
+        oout.append(oo)
+    assert b''.join(gout) == d and gbuf == b''
+    assert ctx.cache_size() == oracle.lib.xco_cache_size(oc)
+    ctx.close()
+    oracle.decoder_free(odec)
+    oracle.cache_free(oc)
