@@ -83,7 +83,10 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 
 	if (refmap == NULL)
 		return;
-	/* REF ops of the output (out-of-band declarations look the same; skip them). */
+	/* REF ops of the output.  An out-of-band declaration looks like a REF and
+	 * comes first in the output for its hash (a REF to it can only follow);
+	 * encode_declaration passes no refmap (xcodec_encoder.cc:288-295), so that
+	 * first occurrence is skipped, later ones are REFs. */
 	uint64_t i = 0;
 	while (i < olen) {
 		if (out[i] != XCODEC_MAGIC) {
@@ -100,8 +103,13 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 			memcpy(&behash, &out[i + 2], sizeof behash);
 			const uint64_t hash = BigEndian::decode(behash);
 			i += 10;
-			if (!stream_ && declared.find(hash) != declared.end())
-				continue;
+			if (!stream_) {
+				std::map<uint64_t, unsigned>::iterator dit = declared.find(hash);
+				if (dit != declared.end()) {
+					declared.erase(dit);
+					continue;
+				}
+			}
 			if (refmap->find(hash) != refmap->end())
 				continue;
 			BufferSegment *seg = cache_->lookup(hash);

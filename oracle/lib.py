@@ -48,6 +48,7 @@ class Oracle:
             raise FileNotFoundError(path)
         L = self.lib = C.CDLL(path)
         pre = ('xdi_' if dropin else 'xcr_') if ref else 'xco_'
+        self._pre = pre
         self._hash = getattr(L, pre + 'hash')
         self._hash.restype = C.c_uint64
         self._hash.argtypes = [_u8p]
@@ -144,6 +145,37 @@ class Oracle:
         from wanproxy_amd.synth import chunks_of
         offs, lens = chunks_of(data, chunk)
         return b''.join(self.encode_batch(data, offs, lens, mode=mode, oob=oob, cache=cache))
+
+    # ------------------------------------------------- encode with a refmap
+    def encoder_new(self, cache):
+        """A persistent XCodecEncoder on `cache` (reference / drop-in builds)."""
+        f = getattr(self.lib, self._pre + 'encoder_new')
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_void_p]
+        return f(cache)
+
+    def encoder_free(self, enc):
+        f = getattr(self.lib, self._pre + 'encoder_free')
+        f.argtypes = [C.c_void_p]
+        f(enc)
+
+    def encode_refmap(self, enc, data: bytes):
+        """One encode(output, input, &refmap) call: (output, {hash: segment})."""
+        f = getattr(self.lib, self._pre + 'encode_refmap')
+        f.argtypes = [C.c_void_p, _u8p, C.c_uint64, _u8p, C.c_uint64, _u64p, _u64p, _u8p, C.c_uint64, _u64p]
+        f.restype = C.c_int
+        a = np.frombuffer(data, dtype=np.uint8)
+        out = np.zeros(2 * a.size + 16, dtype=np.uint8)
+        ol = np.zeros(1, dtype=np.uint64)
+        mx = a.size // SEG + 1
+        hs = np.zeros(mx, dtype=np.uint64)
+        segs = np.zeros(mx * SEG, dtype=np.uint8)
+        nref = np.zeros(1, dtype=np.uint64)
+        if f(enc, _p(a, _u8p), a.size, _p(out, _u8p), out.size, _p(ol, _u64p), _p(hs, _u64p), _p(segs, _u8p), mx,
+             _p(nref, _u64p)) != 0:
+            raise RuntimeError('encode overflow')
+        refs = {int(hs[k]): segs[k * SEG:(k + 1) * SEG].tobytes() for k in range(int(nref[0]))}
+        return out[:int(ol[0])].tobytes(), refs
 
     # ---------------------------------------------------------------- decode
     def decoder_new(self, cache):

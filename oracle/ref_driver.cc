@@ -135,6 +135,36 @@ int xcr_encode_batch(void *cache, const uint8_t *in, const uint64_t *off, const 
 	return rc;
 }
 
+/* One XCodecEncoder::encode call with a refmap (the XCodecPipePair caller,
+ * xcodec/xcodec_pipe_pair.cc:610-618), on a persistent encoder made by
+ * xcr_encoder_new.  Returns the output and the refmap: hashes in map order and
+ * their segments.  Returns 0, or -1 on overflow. */
+void *xcr_encoder_new(void *cache) { return new XCodecEncoder((XCodecCache *)cache); }
+void xcr_encoder_free(void *enc) { delete (XCodecEncoder *)enc; }
+
+int xcr_encode_refmap(void *enc, const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                      uint64_t *hashes, uint8_t *segs, uint64_t max, uint64_t *nref)
+{
+	Buffer input, output;
+	input.append(in, len);
+	std::map<uint64_t, BufferSegment *> refmap;
+	((XCodecEncoder *)enc)->encode(&output, &input, &refmap);
+	uint64_t r = drain(&output, out, cap);
+	*nref = 0;
+	for (std::map<uint64_t, BufferSegment *>::iterator it = refmap.begin(); it != refmap.end(); ++it) {
+		if (*nref < max) {
+			hashes[*nref] = it->first;
+			it->second->copyout(segs + *nref * XCODEC_SEGMENT_LENGTH, 0, XCODEC_SEGMENT_LENGTH);
+			(*nref)++;
+		}
+		it->second->unref();
+	}
+	if (r == ~(uint64_t)0)
+		return -1;
+	*out_len = r;
+	return 0;
+}
+
 /* One XCodecDecoder::decode over a whole buffer with cache `cache`
  * (tack -d, programs/tack/tack.cc:329-359).  Returns 1/0 like decode(),
  * -1 on overflow; *consumed = bytes parsed; *nunk = unknown hashes. */

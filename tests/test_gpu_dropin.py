@@ -61,3 +61,24 @@ def test_dropin_decode_unknown_like_reference(dropin, ref_oracle):
         o.cache_free(c)
         res.append((ok, out, consumed, sorted(unk)))
     assert res[0] == res[1]
+
+
+def test_dropin_refmap_like_reference(dropin, ref_oracle):
+    # encode(output, input, &refmap) as XCodecPipePair calls it
+    # (xcodec/xcodec_pipe_pair.cc:610-618): the drop-in's output and refmap
+    # (hash -> segment of every REF made) equal the reference's, call by call
+    # on one persistent encoder + cache.
+    from wanproxy_amd import synth
+    d = synth.stream(0x7EF, 3 << 20, 60, 2)
+    pieces = [d[a:a + 524288] for a in range(0, len(d), 524288)] + [d[:70000], d[100:2200], b'x' * 3000]
+    encs = []
+    for o in (ref_oracle, dropin):
+        c = o.cache_new()
+        e = o.encoder_new(c)
+        encs.append([o.encode_refmap(e, p) for p in pieces])
+        o.encoder_free(e)
+        o.cache_free(c)
+    for k, (r, g) in enumerate(zip(*encs)):
+        assert r[0] == g[0], k
+        assert r[1] == g[1], (k, len(r[1]), len(g[1]))
+    assert sum(len(r[1]) for r in encs[0]) > 100
