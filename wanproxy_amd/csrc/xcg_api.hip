@@ -204,7 +204,7 @@ void free_cache(GpuCache& g) {
 void free_lru(XcgLruState& L) {
   (void)hipFree(L.skey); (void)hipFree(L.lastref); (void)hipFree(L.queue); (void)hipFree(L.queue2);
   (void)hipFree(L.ptime); (void)hipFree(L.hmin); (void)hipFree(L.wpop); (void)hipFree(L.tau);
-  (void)hipFree(L.alive); (void)hipFree(L.freel);
+  (void)hipFree(L.alive); (void)hipFree(L.freel); (void)hipFree(L.part);
   (void)hipFree(L.tot);
   if (L.h_tot) (void)hipHostFree(L.h_tot);
   const uint32_t C = L.C;
@@ -580,7 +580,7 @@ int lru_host_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
     const LruBatch b{1u, d_new, (const uint64_t*)at(&h.chunk_off), at(h.decl), (const uint32_t*)at(&h.ndecl), 1u,
                      at(h.ev), (const uint32_t*)at(&h.nev), 1u, 0, (uint32_t*)at(&h.need), c->g.keys, c->g.vals,
                      c->g.mask, c->g.pool, c->g.nseg, c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask,
-                     c->d_status};
+                     c->d_status, 1u};
     if (xcg_lru_times(&b, &L, nullptr) != 0 || xcg_lru_commit(&b, &L, nullptr) != 0 ||
         hipStreamSynchronize(nullptr) != hipSuccess)
       rc = XCG_EHIP;

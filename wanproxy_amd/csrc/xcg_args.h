@@ -86,6 +86,8 @@ struct XcgLruState {
   uint32_t* tot;          // [16]
   uint32_t* h_tot;        // pinned [16]
   uint64_t clock;         // LRU time base of the next batch (host)
+  uint32_t* part;         // per-tile counts of the multi-workgroup scans (grown on demand)
+  uint32_t part_cap;
 };
 
 // A batch's cache references for the LRU pass: enters as declaration rows
@@ -114,6 +116,7 @@ struct LruBatch {
   uint32_t* g_gfilt;
   uint32_t gmask;
   int32_t* status;
+  uint64_t ev_bound;      // upper bound of the batch's references (sizes the scans)
 };
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);

@@ -1040,7 +1040,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     uint32_t* changes = (uint32_t*)(blk + 1);
     lb = LruBatch{n, a->in, a->chunk_off, drow, nd32, a->maxd, evs, nev32, 0xFFFFFFFFu, 1, need,
                   a->g_keys, a->g_vals, a->g_mask, a->pool, a->nseg, a->g_filt, a->g_ftab, a->fmask,
-                  a->g_gfilt, a->gmask, a->status};
+                  a->g_gfilt, a->gmask, a->status, m};
     auto fail = [&](int rc) {
       (void)hipFreeAsync(lru_mem, stream);
       return rc;

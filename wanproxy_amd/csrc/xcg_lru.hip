@@ -204,23 +204,6 @@ __global__ __launch_bounds__(256) void lru_seed_table_kernel(uint32_t n, const u
   if (!tab_insert_min(b, dd.x, dd.y, ((uint64_t)c << 32) | dd.z)) atomicOr(status, 2);
 }
 
-// Walk the persistent entries in LRU order: wpop[s] = when the batch's
-// evictions reach slot s (tau[r - S(r)]), ptime[s] = that, unless the batch
-// looks s up before then (then never).
-__global__ __launch_bounds__(1024) void lru_rank_kernel(const uint32_t* queue, uint32_t* tot,
-                                                        const uint64_t* hmin, const uint64_t* tau, uint64_t* wpop,
-                                                        uint64_t* ptime) {
-  const uint32_t A = tot[T_A], P = tot[T_P];
-  const uint32_t H = wg_scan(
-      A, 0u, [&](uint32_t r) { return hmin[queue[r]] != NEVER ? 1u : 0u; },
-      [&](uint32_t r, uint32_t S, uint32_t h) {
-        const uint32_t s = queue[r], j = r - S;
-        const uint64_t w = j < P ? tau[j] : NEVER;
-        wpop[s] = w;
-        ptime[s] = h && hmin[s] < w ? NEVER : w;   // (a hit after the eviction did not happen)
-      });
-  if (threadIdx.x == 0) tot[T_H] = H;
-}
 
 // Every recorded lookup of a persistent entry against the recomputed times.
 __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, const uint64_t* hmin,
@@ -243,6 +226,135 @@ __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, co
   }
 }
 
+// ---- ordered scans over many workgroups (rank walk, free list, new LRU order)
+//
+// Two launches instead of one workgroup walking everything (whose dependent
+// random loads per 4096-element tile made it ~100 us at C = 65536): pass 0
+// counts each 1024-element tile's flags into part[tile]; pass 1 adds the counts
+// of the tiles before it and emits.
+enum : int { SK_RANK = 0, SK_QUEUE = 1, SK_FREE = 2 };
+struct ScanArgs {
+  uint32_t* tot;
+  const uint32_t* queue;
+  const uint64_t* hmin;
+  const uint64_t* tau;
+  uint64_t* wpop;
+  uint64_t* ptime;
+  const uint32_t* alive;
+  const uint64_t* lastref;
+  uint64_t clock;
+  const uint32_t* evslot;
+  const uint64_t* evtime;
+  uint32_t* queue2;
+  uint32_t* nseg;
+  uint32_t C;
+  uint32_t* freel;
+  uint32_t* part;
+};
+
+template <int K>
+__device__ __forceinline__ uint32_t scan_n(const ScanArgs& a) {
+  if (K == SK_RANK) return a.tot[T_A];
+  if (K == SK_QUEUE) return a.tot[T_A] + a.tot[T_E];
+  return a.C;
+}
+
+// flag of element i (and the value a compaction writes)
+template <int K>
+__device__ __forceinline__ uint32_t scan_flag(const ScanArgs& a, uint32_t i, uint32_t& v) {
+  if (K == SK_RANK) {
+    v = a.queue[i];
+    return a.hmin[v] != NEVER ? 1u : 0u;
+  }
+  if (K == SK_QUEUE) {
+    const uint32_t A = a.tot[T_A];
+    if (i < A) {                                   // persistent entries the batch left alone, old order
+      v = a.queue[i];
+      return a.alive[v] && a.lastref[v] < a.clock ? 1u : 0u;
+    }
+    v = a.evslot[i - A];                           // then each entry's last reference, in stream order
+    return v != ~0u && a.lastref[v] == a.evtime[i - A] ? 1u : 0u;
+  }
+  v = i;
+  return a.alive[i] ? 0u : 1u;
+}
+
+template <int K>
+__device__ __forceinline__ void scan_emit(const ScanArgs& a, uint32_t i, uint32_t p, uint32_t f, uint32_t v) {
+  if (K == SK_RANK) {                              // p = S(r): looked-up entries below rank i
+    const uint32_t j = i - p, P = a.tot[T_P];
+    const uint64_t w = j < P ? a.tau[j] : NEVER;
+    a.wpop[v] = w;
+    a.ptime[v] = f && a.hmin[v] < w ? NEVER : w;   // (a hit after the eviction did not happen)
+  } else if (K == SK_QUEUE) {
+    if (f) a.queue2[p] = v;
+  } else {
+    if (f) a.freel[p] = v;
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void scan_total(const ScanArgs& a, uint32_t total) {
+  if (K == SK_RANK) a.tot[T_H] = total;
+  else if (K == SK_QUEUE) { *a.nseg = total; a.tot[T_A2] = total; }
+  else a.tot[T_NFREE] = total;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void scan_count_kernel(ScanArgs a) {
+  __shared__ uint32_t ws[4];
+  const uint32_t n = scan_n<K>(a), i0 = blockIdx.x * 1024u + 4u * threadIdx.x;
+  if (blockIdx.x * 1024u >= n && blockIdx.x != 0) return;
+  uint32_t c = 0, v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (i0 + k < n) c += scan_flag<K>(a, i0 + k, v);
+  c = wave_sum(c);
+  if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) a.part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void scan_emit_kernel(ScanArgs a) {
+  __shared__ uint32_t ws[4], s_base;
+  const uint32_t n = scan_n<K>(a), ntiles = (n + 1023u) / 1024u, tile = blockIdx.x;
+  if (tile >= ntiles && !(tile == 0 && n == 0)) return;
+  // base = counts of the tiles before this one
+  uint32_t b = 0;
+  for (uint32_t t = threadIdx.x; t < tile; t += 256) b += a.part[t];
+  b = wave_sum(b);
+  if (lane_id() == 0) ws[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = ws[0] + ws[1] + ws[2] + ws[3];
+  __syncthreads();
+  const uint32_t base = s_base;
+  __syncthreads();
+  const uint32_t i0 = tile * 1024u + 4u * threadIdx.x;
+  uint32_t f[4], v[4], c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[k] = i0 + k < n ? scan_flag<K>(a, i0 + k, v[k]) : 0u;
+    c += f[k];
+  }
+  const uint32_t inc = wave_incl_scan(c);
+  if (lane_id() == 63) ws[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t wpre = 0, tt = 0;
+  for (uint32_t w = 0; w < 4; ++w) {
+    const uint32_t x = ws[w];
+    if (w < (threadIdx.x >> 6)) wpre += x;
+    tt += x;
+  }
+  uint32_t run = base + wpre + inc - c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (i0 + k < n) scan_emit<K>(a, i0 + k, run, f[k], v[k]);
+    run += f[k];
+  }
+  if (threadIdx.x == 0 && (tile + 1 >= ntiles)) scan_total<K>(a, base + tt);
+}
+
 // ---- commit
 
 __global__ __launch_bounds__(256) void lru_mark_kernel(const uint32_t* tot, const uint32_t* queue,
@@ -253,14 +365,6 @@ __global__ __launch_bounds__(256) void lru_mark_kernel(const uint32_t* tot, cons
   alive[s] = (hmin[s] == NEVER && wpop[s] != NEVER) ? 0u : 1u;   // evicted in the batch
 }
 
-__global__ __launch_bounds__(1024) void lru_free_kernel(uint32_t C, const uint32_t* alive, uint32_t* freel,
-                                                        uint32_t* tot) {
-  const uint32_t nf = wg_scan(C, 0u, [&](uint32_t s) { return alive[s] ? 0u : 1u; },
-                              [&](uint32_t s, uint32_t p, uint32_t v) {
-                                if (v) freel[p] = s;
-                              });
-  if (threadIdx.x == 0) tot[T_NFREE] = nf;
-}
 
 struct Wipe {
   HashTab g;
@@ -337,36 +441,6 @@ __global__ __launch_bounds__(256) void lru_lastref_kernel(uint32_t n, EvRows R, 
   }
 }
 
-// The new LRU order: persistent entries the batch left alone, in their old
-// order, then every entry the batch referenced, by its last reference.
-__global__ __launch_bounds__(1024) void lru_queue_kernel(uint32_t* tot, const uint32_t* queue, const uint32_t* alive,
-                                                         const uint64_t* lastref, uint64_t clock,
-                                                         const uint32_t* evslot, const uint64_t* evtime,
-                                                         uint32_t* queue2, uint32_t* nseg) {
-  const uint32_t A = tot[T_A], E = tot[T_E];
-  const uint32_t p1 = wg_scan(
-      A, 0u,
-      [&](uint32_t r) {
-        const uint32_t s = queue[r];
-        return alive[s] && lastref[s] < clock ? 1u : 0u;
-      },
-      [&](uint32_t r, uint32_t p, uint32_t v) {
-        if (v) queue2[p] = queue[r];
-      });
-  const uint32_t p2 = wg_scan(
-      E, p1,
-      [&](uint32_t i) {
-        const uint32_t s = evslot[i];
-        return s != ~0u && lastref[s] == evtime[i] ? 1u : 0u;
-      },
-      [&](uint32_t i, uint32_t p, uint32_t v) {
-        if (v) queue2[p] = evslot[i];
-      });
-  if (threadIdx.x == 0) {
-    *nseg = p2;
-    tot[T_A2] = p2;
-  }
-}
 
 }  // namespace xcg
 
@@ -379,10 +453,47 @@ bool lru_debug() {
 
 unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
 
+// One multi-workgroup ordered scan over at most max_n elements.
+template <int K>
+int run_scan(XcgLruState* L, xcg::ScanArgs a, uint64_t max_n, hipStream_t st) {
+  const uint32_t tiles = (uint32_t)((max_n + 1023) / 1024) + 1;
+  if (tiles > L->part_cap) {
+    (void)hipFree(L->part);
+    L->part = nullptr;
+    L->part_cap = 0;
+    if (hipMalloc(&L->part, 4ull * tiles * 2) != hipSuccess) return -5;
+    L->part_cap = tiles * 2;
+  }
+  a.part = L->part;
+  hipLaunchKernelGGL(xcg::scan_count_kernel<K>, dim3(tiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(xcg::scan_emit_kernel<K>, dim3(tiles), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+xcg::ScanArgs scan_args(XcgLruState* L, uint32_t* nseg) {
+  xcg::ScanArgs a{};
+  a.tot = L->tot;
+  a.queue = L->queue;
+  a.hmin = L->hmin;
+  a.tau = L->tau;
+  a.wpop = L->wpop;
+  a.ptime = L->ptime;
+  a.alive = L->alive;
+  a.lastref = L->lastref;
+  a.clock = L->clock;
+  a.evslot = L->evslot;
+  a.evtime = L->evtime;
+  a.queue2 = L->queue2;
+  a.nseg = nseg;
+  a.C = L->C;
+  a.freel = L->freel;
+  return a;
+}
+
 LruBatch batch_of(const XcgStreamArgs& a) {
   return LruBatch{a.n, a.in, a.chunk_off, a.decl, a.ndecl, a.maxd, a.ev, a.nev, a.maxe, 0, a.need,
                   a.g_keys, a.g_vals, a.g_mask, a.pool, a.nseg, a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask,
-                  a.status};
+                  a.status, (uint64_t)a.n * a.maxe};
 }
 
 // Eviction times from a batch's references: tau, first hits, the LRU-order
@@ -400,8 +511,7 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   const dim3 wgrid((n + 3) / 4);
   hipLaunchKernelGGL(lru_events_kernel, wgrid, dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
                      (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
-  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
-                     (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
+  if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
   if (check)
     hipLaunchKernelGGL(lru_check_kernel, wgrid, dim3(256), 0, st, n, R, (const uint64_t*)L->hmin,
                        (const uint64_t*)L->wpop, b.need, L->tot);
@@ -412,7 +522,7 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
 }
 
 // ptime from the tiling seed (lru_seed_classify_kernel).  Asynchronous.
-void lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
+int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   using namespace xcg;
   const uint32_t n = a.n;
   const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
@@ -433,8 +543,8 @@ void lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
                      (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
                      (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1);
-  hipLaunchKernelGGL(lru_rank_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)L->queue, L->tot,
-                     (const uint64_t*)L->hmin, (const uint64_t*)L->tau, L->wpop, L->ptime);
+  if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
+  return 0;
 }
 
 }  // namespace
@@ -450,7 +560,7 @@ extern "C" int xcg_lru_commit(const LruBatch* bp, XcgLruState* L, hipStream_t st
   hipLaunchKernelGGL(lru_fill32_kernel, dim3(cg), dim3(256), 0, st, L->alive, C, 0u);
   hipLaunchKernelGGL(lru_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, (const uint32_t*)L->tot,
                      (const uint32_t*)L->queue, (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->alive);
-  hipLaunchKernelGGL(lru_free_kernel, dim3(1), dim3(1024), 0, st, C, (const uint32_t*)L->alive, L->freel, L->tot);
+  if (run_scan<SK_FREE>(L, scan_args(L, nullptr), C, st)) return -5;
   const HashTab g{b.g_keys, b.g_vals, b.g_mask};
   const FiltSet fs{b.g_filt, b.g_ftab, b.fmask, b.g_gfilt, b.gmask};
   Wipe w{g, b.g_filt, (u32x4*)b.g_ftab, b.fmask + 1, b.g_gfilt, b.gmask + 1};
@@ -464,9 +574,9 @@ extern "C" int xcg_lru_commit(const LruBatch* bp, XcgLruState* L, hipStream_t st
   const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
   hipLaunchKernelGGL(lru_lastref_kernel, dim3((n + 3) / 4), dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
                      (const uint32_t*)L->freel, g, L->clock, L->lastref, L->evslot, L->evtime);
-  hipLaunchKernelGGL(lru_queue_kernel, dim3(1), dim3(1024), 0, st, L->tot, (const uint32_t*)L->queue,
-                     (const uint32_t*)L->alive, (const uint64_t*)L->lastref, L->clock, (const uint32_t*)L->evslot,
-                     (const uint64_t*)L->evtime, L->queue2, b.nseg);
+  {
+    if (run_scan<SK_QUEUE>(L, scan_args(L, b.nseg), (uint64_t)C + b.ev_bound, st)) return -5;
+  }
   if (hipGetLastError() != hipSuccess) return -5;
   uint32_t* q = L->queue;
   L->queue = L->queue2;
@@ -515,7 +625,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     a.no_commit = 1;
     // Pass 0 starts from the tiling seed, with the evictions it implies.
     if (xcg_launch_seed_tiling(&a, st)) return -5;
-    lru_seed_guess(a, L, st);
+    if (lru_seed_guess(a, L, st)) return -5;
     bool done = false, split = false;
     for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
       a.keep_decls = 1;
