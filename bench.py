@@ -210,8 +210,9 @@ def other_configs():
     cb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(cb)
     # C5-LRU: C5 on wanproxy.conf's bounded 128 MiB memory cache (LRU
-    # eviction), the first 25 % checked against the oracle's bounded cache
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, lru_mib=128, lru_check=0.25)
+    # eviction), every chunk checked against the oracle's bounded cache
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, lru_mib=128, lru_check=1.0,
+                           no_decode=False)
     out = {}
     for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru)):
         try:

@@ -97,6 +97,8 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
  * more than limit * 2048 bytes; BACKREF ops in a decode on a bounded cache. */
 int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_ctx **out);
 void xcg_ctx_destroy(xcg_ctx *ctx);
+/* The XCG_FLAG_* the context was created with. */
+int xcg_ctx_flags(const xcg_ctx *ctx, uint32_t *flags);
 
 /* Persistent cache: number of segments held / drop everything. */
 uint64_t xcg_cache_size(xcg_ctx *ctx);
@@ -111,7 +113,9 @@ int xcg_cache_lookup_host(xcg_ctx *ctx, uint64_t hash, uint8_t *seg_out);
 int xcg_cache_enter_host(xcg_ctx *ctx, uint64_t hash, const uint8_t *seg);
 /* Declarations (hash, position in the chunk) chunk `chunk` of the last
  * XCG_SEM_STREAM batch made, in order: what XCodecEncoder::encode_declaration
- * entered into the cache (xcodec/xcodec_encoder.cc:276-313). */
+ * entered into the cache (xcodec/xcodec_encoder.cc:276-313).  On a bounded
+ * cache only the chunks of the batch's last sub-batch are kept (XCG_ENOTSUP
+ * for earlier ones; a single-chunk batch is always one sub-batch). */
 int xcg_last_declarations(xcg_ctx *ctx, uint32_t chunk, uint64_t *h_hash, uint32_t *h_pos, uint32_t cap,
                           uint32_t *h_count);
 /* Diagnostics: copy the persistent cache's lane filters to host memory

@@ -66,6 +66,33 @@ inline void set_cache_limit(XCodecCache *cache, uint64_t memory_cache_limit_byte
 		limit_map()[cache] = memory_cache_limit_bytes;
 }
 
+/* wanproxy.conf's cache pair (XCodecCachePair of a bounded XCodecMemoryCache
+ * and the local XCodecDiskCache, programs/wanproxy/wanproxy.conf:8-26): the
+ * pair keeps its levels private (xcodec/xcodec_cache.h:140-153), so the code
+ * that builds it (wanproxy_config_class_cache.cc) tells the binding the two
+ * sizes; the GPU mirror is then an xcg_ctx_create_pair context. */
+struct PairGeometry {
+	uint64_t memory_limit_bytes;
+	uint64_t disk_bytes;
+};
+
+inline std::map<XCodecCache *, PairGeometry>& pair_map()
+{
+	static std::map<XCodecCache *, PairGeometry> pairs;
+	return pairs;
+}
+
+inline void set_pair_geometry(XCodecCache *cache, uint64_t memory_limit_bytes, uint64_t disk_bytes)
+{
+	PairGeometry g = { memory_limit_bytes, disk_bytes };
+	pair_map()[cache] = g;
+}
+
+inline bool is_pair(XCodecCache *cache)
+{
+	return pair_map().find(cache) != pair_map().end();
+}
+
 inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 {
 	std::map<XCodecCache *, xcg_ctx *>& ctxs = ctx_map();

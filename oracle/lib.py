@@ -114,6 +114,31 @@ class Oracle:
         XCodecMemoryCache(uuid, limit_bytes) (xcodec/xcodec_cache.h:277-288)."""
         return self._cnewl(limit_bytes) if limit_bytes else self._cnew()
 
+    def cache_new_pair(self, memory_limit_bytes: int, disk_bytes: int):
+        """XCodecCachePair(XCodecMemoryCache(uuid, memory_limit_bytes), disk of
+        disk_bytes) -- wanproxy.conf's cache (xcodec/xcodec_cache.h:140-237,
+        xcodec/xcodec_cache_disk.cc).  The reference build runs the real pair
+        over a restated disk level (oracle/ref_driver.cc RefDiskCache)."""
+        f = getattr(self.lib, self._pre + 'cache_new_pair')
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_uint64, C.c_uint64]
+        c = f(memory_limit_bytes, disk_bytes)
+        if not c:
+            raise ValueError('disk too small for one index block')
+        return c
+
+    def pair_stats(self, c):
+        """(disk index entries, disk entries written) of a pair cache."""
+        st = np.zeros(4, np.uint64)
+        if self.ref:
+            f = getattr(self.lib, self._pre + 'pair_stats')
+            f.argtypes = [C.c_void_p, _u64p]
+            f(c, _p(st, _u64p))
+            return int(st[0]), int(st[1])
+        self.lib.xco_pair_stats.argtypes = [C.c_void_p, _u64p]
+        self.lib.xco_pair_stats(c, _p(st, _u64p))
+        return int(st[1]), int(st[2])
+
     def cache_free(self, c):
         self._cfree(c)
 

@@ -19,6 +19,9 @@
 
 #include <string.h>
 
+#include <map>
+#include <vector>
+
 #ifdef XCGPU_DROPIN
 #include "../integration/xcgpu_binding.h"
 #define RELEASE_CACHE(c) xcgpu_binding::forget(c)
@@ -37,6 +40,108 @@ public:
 	BufferSegment *lookup(const uint64_t&) { return NULL; }
 	bool out_of_band(void) const { return true; }
 };
+
+/*
+ * The disk secondary of wanproxy.conf's cache pair.  XCodecDisk /
+ * XCodecDiskCache (xcodec/xcodec_cache_disk.{h,cc}) cannot be compiled here:
+ * it needs UUID::generate / UUID::decode from common/uuid/uuid_libuuid.cc,
+ * whose libuuid header the image lacks (no stand-in is written).  This class
+ * RESTATES its in-memory behaviour for the local namespace, so the REAL
+ * XCodecCachePair (xcodec/xcodec_cache.h:140-237) and the real encoder /
+ * decoder run over it: FIFO data blocks in index blocks of 204 entries
+ * (:72-101, :694-741), the next index block's entries leave the index when the
+ * write head reaches it (:327-382), lookup re-hashes (:743-771), touch
+ * re-enters a lost hash (:813-823), replace = remove + enter
+ * (xcodec_cache_disk.h:130-134).  The bytes live in memory, not in a file.
+ */
+class RefDiskCache : public XCodecCache {
+	uint64_t nb_, slots_, clock_;
+	std::vector<uint64_t> key_;
+	std::vector<uint8_t> alive_;
+	std::vector<uint8_t> data_;
+	std::map<uint64_t, uint64_t> index_;
+public:
+	RefDiskCache(const UUID& uuid, uint64_t disk_bytes)
+	: XCodecCache(uuid),
+	  nb_(((disk_bytes / XCODEC_SEGMENT_LENGTH) - 18) / 205),
+	  slots_(nb_ * 204),
+	  clock_(0),
+	  key_(slots_),
+	  alive_(slots_),
+	  data_(slots_ * XCODEC_SEGMENT_LENGTH),
+	  index_()
+	{ }
+
+	XCodecCache *connect(const UUID&) { return NULL; }
+
+	void enter(const uint64_t& hash, BufferSegment *seg)
+	{
+		ASSERT("/ref/disk", index_.find(hash) == index_.end());
+		uint64_t slot = clock_ % slots_;
+		seg->copyout(&data_[slot * XCODEC_SEGMENT_LENGTH], 0, XCODEC_SEGMENT_LENGTH);
+		key_[slot] = hash;
+		alive_[slot] = 1;
+		index_[hash] = slot;
+		if (++clock_ % 204 == 0) {
+			uint64_t b = (clock_ / 204) % nb_;
+			for (uint64_t i = b * 204; i < (b + 1) * 204; i++) {
+				if (!alive_[i])
+					continue;
+				index_.erase(key_[i]);
+				alive_[i] = 0;
+			}
+		}
+	}
+
+	void remove(const uint64_t& hash)
+	{
+		std::map<uint64_t, uint64_t>::iterator it = index_.find(hash);
+		if (it == index_.end())
+			return;
+		alive_[it->second] = 0;
+		index_.erase(it);
+	}
+
+	void replace(const uint64_t& hash, BufferSegment *seg)
+	{
+		remove(hash);
+		enter(hash, seg);
+	}
+
+	BufferSegment *lookup(const uint64_t& hash)
+	{
+		std::map<uint64_t, uint64_t>::iterator it = index_.find(hash);
+		if (it == index_.end())
+			return NULL;
+		BufferSegment *seg = BufferSegment::create();
+		memcpy(seg->head(), &data_[it->second * XCODEC_SEGMENT_LENGTH], XCODEC_SEGMENT_LENGTH);
+		seg->set_length(XCODEC_SEGMENT_LENGTH);
+		if (XCodecHash::hash(seg->data()) != hash) {
+			seg->unref();
+			alive_[it->second] = 0;
+			index_.erase(it);
+			return NULL;
+		}
+		return seg;
+	}
+
+	void touch(const uint64_t& hash, BufferSegment *seg)
+	{
+		if (index_.find(hash) == index_.end())
+			enter(hash, seg);
+	}
+
+	bool out_of_band(void) const { return false; }
+
+	uint64_t entries(void) const { return index_.size(); }
+	uint64_t written(void) const { return clock_; }
+};
+
+static std::map<void *, std::pair<XCodecCache *, XCodecCache *> >& pair_levels()
+{
+	static std::map<void *, std::pair<XCodecCache *, XCodecCache *> > m;
+	return m;
+}
 
 static uint64_t drain(Buffer *b, uint8_t *out, uint64_t cap)
 {
@@ -86,10 +191,41 @@ void *xcr_cache_new_limited(uint64_t limit_bytes)
 	return new XCodecMemoryCache(uuid, (size_t)limit_bytes);
 }
 
+/* XCodecCachePair(XCodecMemoryCache(uuid, memory_limit_bytes), disk of
+ * disk_bytes): wanproxy.conf's memory + disk pair
+ * (programs/wanproxy/wanproxy.conf:8-26, wanproxy_config_class_cache.cc). */
+void *xcr_cache_new_pair(uint64_t memory_limit_bytes, uint64_t disk_bytes)
+{
+	UUID uuid;
+	XCodecCache *primary = new XCodecMemoryCache(uuid, (size_t)memory_limit_bytes);
+	XCodecCache *secondary = new RefDiskCache(uuid, disk_bytes);
+	XCodecCache *pair = new XCodecCachePair(primary, secondary);
+	pair_levels()[pair] = std::make_pair(primary, secondary);
+#ifdef XCGPU_DROPIN
+	xcgpu_binding::set_pair_geometry(pair, memory_limit_bytes, disk_bytes);
+#endif
+	return pair;
+}
+
 void xcr_cache_free(void *c)
 {
 	RELEASE_CACHE((XCodecCache *)c);
+	std::map<void *, std::pair<XCodecCache *, XCodecCache *> >::iterator it = pair_levels().find(c);
+	if (it != pair_levels().end()) {       /* the pair does not own its levels */
+		delete it->second.first;
+		delete it->second.second;
+		pair_levels().erase(it);
+	}
 	delete (XCodecCache *)c;
+}
+
+/* Diagnostics of a pair made by xcr_cache_new_pair: [0] disk index entries,
+ * [1] disk entries written. */
+void xcr_pair_stats(void *c, uint64_t *st)
+{
+	RefDiskCache *d = (RefDiskCache *)pair_levels()[c].second;
+	st[0] = d->entries();
+	st[1] = d->written();
 }
 
 /* mode 0: fresh XCodecMemoryCache per chunk; mode 1: one cache + one encoder

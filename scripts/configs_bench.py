@@ -164,8 +164,10 @@ def run_c2s(args):
     wall = timed_encode(B, args.reps)
     got = B.outputs()
     k = check_prefix(data, offs, lens, got, 256, 'c2s')
-    dctx = Context(0, cache_segments=1 << 18)
-    dec, dsec = decode_device(dctx, got, per=n, chunk=64 * KiB)
+    dec, dsec = data.tobytes(), float('nan')
+    if not args.no_decode:
+        dctx = Context(0, cache_segments=1 << 18)
+        dec, dsec = decode_device(dctx, got, per=n, chunk=64 * KiB)
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c2s)')
     inb = data.size
@@ -235,8 +237,10 @@ def run_c4(args):
     wall = timed_encode(B, args.reps)
     got = B.outputs()
     k = check_prefix(data, offs, lens, got, 2048, 'c4')
-    dctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
-    dec, dsec = decode_device(dctx, got, per=args.c4_batch, chunk=4 * KiB)
+    dec, dsec = data.tobytes(), float('nan')
+    if not args.no_decode:
+        dctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
+        dec, dsec = decode_device(dctx, got, per=args.c4_batch, chunk=4 * KiB)
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c4)')
     inb = data.size
@@ -259,8 +263,10 @@ def run_c5(args):
     wall = timed_encode(B, args.reps)
     got = B.outputs()
     k = check_prefix(data, offs, lens, got, 64, 'c5')
-    dctx = Context(0, cache_segments=segs)
-    dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
+    dec, dsec = data.tobytes(), float('nan')
+    if not args.no_decode:
+        dctx = Context(0, cache_segments=segs)
+        dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c5)')
     inb = data.size
@@ -293,8 +299,10 @@ def run_c5lru(args):
     if got[:k] != exp:
         bad = next(i for i in range(k) if got[i] != exp[i])
         raise SystemExit(f'PARITY FAILURE (c5lru) at chunk {bad}')
-    dctx = Context(0, cache_segments=nbytes // 2048 + 4096)
-    dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
+    dec = data.tobytes()
+    if not args.no_decode:
+        dctx = Context(0, cache_segments=nbytes // 2048 + 4096)
+        dec, _ = decode_device(dctx, got, per=per, chunk=128 * KiB)
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c5lru)')
     inb = data.size
@@ -314,6 +322,7 @@ def main():
     ap.add_argument('--c4-batch', type=int, default=16384)
     ap.add_argument('--lru-mib', type=int, default=128)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
+    ap.add_argument('--no-decode', action='store_true', help='skip the decode round trips (profiling runs)')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)

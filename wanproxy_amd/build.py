@@ -1,15 +1,25 @@
 """Build libxcgpu.so in-tree for gfx950 (hipcc; no JIT cache, so the .so
-travels with the repository snapshot to the GPU box)."""
+travels with the repository snapshot to the GPU box).
+
+Each source compiles to its own object in parallel (objects are reused while
+they are newer than the source and every header), then one link."""
 from __future__ import annotations
 
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/xcg_hash.hip', 'csrc/xcg_lru.hip',
         'csrc/xcg_pipe.cpp']
+HDRS = ['csrc/xcg_device.h', 'csrc/xcg_cache.h', 'csrc/xcg_args.h', '../include/xcgpu.h']
 OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Wall']
+
+
+def _newer(out: str, deps) -> bool:
+    return os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)
 
 
 def build_lib(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
@@ -17,12 +27,28 @@ def build_lib(force: bool = False, verbose: bool = False, out: str = OUT, define
     -D `defines`, e.g. XCG_TIMING: per-wave timestamps in the stats words)."""
     out = os.path.abspath(out)
     srcs = [os.path.join(HERE, s) for s in SRCS]
-    deps = srcs + [os.path.join(HERE, 'csrc/xcg_device.h'), os.path.join(HERE, 'csrc/xcg_cache.h'),
-            os.path.join(HERE, 'csrc/xcg_args.h'), os.path.join(HERE, '..', 'include', 'xcgpu.h')]
-    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+    hdrs = [os.path.join(HERE, h) for h in HDRS]
+    if not force and _newer(out, srcs + hdrs):
         return out
-    cmd = [HIPCC, '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
-           '-o', out + '.tmp'] + ['-D' + d for d in defines] + srcs
+    tag = '' if not defines else '.' + '_'.join(defines)
+    objdir = os.path.join(HERE, 'build')
+    os.makedirs(objdir, exist_ok=True)
+    dflags = ['-D' + d for d in defines]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + tag + '.o')
+        if not force and _newer(obj, [src] + hdrs):
+            return obj
+        cmd = [HIPCC] + FLAGS + dflags + ['-c', '-o', obj + '.tmp', src]
+        if verbose:
+            print(' '.join(cmd))
+        subprocess.run(cmd, check=True, cwd=HERE)
+        os.replace(obj + '.tmp', obj)
+        return obj
+
+    with ThreadPoolExecutor(min(len(srcs), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', out + '.tmp'] + objs
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True, cwd=HERE)

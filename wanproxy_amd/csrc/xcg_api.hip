@@ -51,6 +51,7 @@ struct XcgDecodeArgs {
   uint64_t* x_vals;
   uint64_t* x_latest;
   uint32_t x_mask;
+  uint64_t* u_keys;
   uint64_t* unknown;
   uint64_t* unknown_pos;
   uint32_t* nunknown;
@@ -133,6 +134,7 @@ struct DecodeScratch {
   uint64_t* x_keys = nullptr;
   uint64_t* x_vals = nullptr;
   uint64_t* x_latest = nullptr;
+  uint64_t* u_keys = nullptr;      // unknown-hash set (2 * UNKNOWN_CAP)
   uint64_t* unknown = nullptr;
   uint64_t* unknown_pos = nullptr;
   uint32_t* nunknown = nullptr;
@@ -169,6 +171,10 @@ struct xcg_ctx {
   bool seed_next = false;          // the last stream batch declared something: seed the next one
   bool bounded = false;            // XCodecMemoryCache with a limit: LRU eviction (xcg_lru.hip)
   XcgLruState lru{};
+  // Completion of the context's last enqueued work (recorded on the caller's
+  // stream): the cache-inspection calls wait for this event only, never for
+  // the whole device, so other contexts and streams keep running.
+  hipEvent_t done_ev = nullptr;
 };
 
 namespace {
@@ -188,6 +194,15 @@ struct DeviceGuard {
 };
 
 constexpr uint32_t FILT_WORDS = (1u << 19) / 32;   // xcg_cache.h FILT_LOG2
+
+// The context's work so far is complete (its last call's stream reached the
+// event) -- the per-context replacement for a device-wide synchronise.
+int ctx_wait(xcg_ctx* c) {
+  return c->done_ev && hipEventSynchronize(c->done_ev) != hipSuccess ? XCG_EHIP : XCG_OK;
+}
+void ctx_mark(xcg_ctx* c, hipStream_t st) {
+  if (c->done_ev) (void)hipEventRecord(c->done_ev, st);
+}
 
 uint32_t pow2_at_least(uint64_t v) {
   uint64_t p = 1;
@@ -323,6 +338,7 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
 
 void free_dscratch(DecodeScratch& d) {
   (void)hipFree(d.x_keys); (void)hipFree(d.x_vals); (void)hipFree(d.x_latest); (void)hipFree(d.unknown);
+  (void)hipFree(d.u_keys);
   (void)hipFree(d.unknown_pos); (void)hipFree(d.nunknown); (void)hipFree(d.scratch);
   (void)hipFree(d.chunk_tmp); (void)hipFree(d.d_tail);
   if (d.h_scratch) (void)hipHostFree(d.h_scratch);
@@ -370,6 +386,7 @@ int ensure_dscratch(xcg_ctx* c, uint64_t max_extracts) {
   d.x_cap = cap;
   if (hipMalloc(&d.x_keys, 8ull * cap) != hipSuccess || hipMalloc(&d.x_vals, 8ull * cap) != hipSuccess ||
       hipMalloc(&d.x_latest, 8ull * cap) != hipSuccess || hipMalloc(&d.unknown, 8ull * UNKNOWN_CAP) != hipSuccess ||
+      hipMalloc(&d.u_keys, 16ull * UNKNOWN_CAP) != hipSuccess ||
       hipMalloc(&d.unknown_pos, 8ull * UNKNOWN_CAP) != hipSuccess || hipMalloc(&d.nunknown, 16) != hipSuccess ||
       hipMalloc(&d.scratch, 64) != hipSuccess || hipHostMalloc(&d.h_scratch, 128) != hipSuccess) {
     free_dscratch(d);
@@ -434,7 +451,8 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
     delete c;
     return XCG_ENOMEM;
   }
-  if (hipMemset(c->d_status, 0, 16) != hipSuccess) {
+  if (hipMemset(c->d_status, 0, 16) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(c->d_status);
     delete c;
     return XCG_EHIP;
@@ -453,6 +471,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   free_scratch(c->bs);
   free_dscratch(c->ds);
   window_free(c->own_win);
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   delete c;
 }
 
@@ -460,7 +479,7 @@ uint64_t xcg_cache_size(xcg_ctx* c) {
   if (!c || !c->g.keys) return 0;
   DeviceGuard g(c->device);
   uint32_t n = 0;
-  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&n, c->g.nseg, 4, hipMemcpyDeviceToHost) != hipSuccess)
+  if (ctx_wait(c) != XCG_OK || hipMemcpy(&n, c->g.nseg, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return 0;
   return n < c->g.seg_cap ? n : c->g.seg_cap;
 }
@@ -469,13 +488,19 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c) return XCG_EINVAL;
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
-  if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
+  if (ctx_wait(c) != XCG_OK) return XCG_EHIP;
   // (the LRU clock keeps running: slots keep their last-reference times, which
   // must stay below every later batch's)
   return clear_cache(c->g);
 }
 
 int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
+
+int xcg_ctx_flags(const xcg_ctx* c, uint32_t* flags) {
+  if (!c || !flags) return XCG_EINVAL;
+  *flags = c->flags;
+  return XCG_OK;
+}
 
 namespace {
 // A small pinned + device staging area for single-segment host calls.
@@ -617,10 +642,15 @@ int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
 
 int xcg_last_declarations(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t* h_pos, uint32_t cap,
                           uint32_t* h_count) {
-  if (!c || !h_count || !c->bs.decl || chunk >= c->bs.n_cap) return XCG_EINVAL;
+  if (!c || !h_count || !c->bs.decl) return XCG_EINVAL;
+  if (c->bounded) {                                    // rows of the last sub-batch only
+    if (chunk < c->lru.last_base) return XCG_ENOTSUP;
+    chunk -= c->lru.last_base;
+  }
+  if (chunk >= c->bs.n_cap) return XCG_EINVAL;
   DeviceGuard g(c->device);
   uint32_t nd = 0;
-  if (hipDeviceSynchronize() != hipSuccess ||
+  if (ctx_wait(c) != XCG_OK ||
       hipMemcpy(&nd, c->bs.ndecl + chunk, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return XCG_EHIP;
   *h_count = nd;
@@ -641,7 +671,7 @@ int xcg_debug_cache_dump(xcg_ctx* c, uint32_t* h_filt, uint32_t* h_ftab, uint64_
   if (!c || !c->g.keys) return XCG_EINVAL;
   DeviceGuard g(c->device);
   *h_fmask = c->g.fmask;
-  if (hipDeviceSynchronize() != hipSuccess) return XCG_EHIP;
+  if (ctx_wait(c) != XCG_OK) return XCG_EHIP;
   if (h_filt && hipMemcpy(h_filt, c->g.filt, 4ull * FILT_WORDS, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
   const uint64_t tw = 4ull * (c->g.fmask + 1);
   if (h_ftab && hipMemcpy(h_ftab, c->g.ftab, 4ull * (ftab_words < tw ? ftab_words : tw), hipMemcpyDeviceToHost) !=
@@ -654,7 +684,7 @@ int xcg_ctx_status(xcg_ctx* c) {
   if (!c) return XCG_EINVAL;
   DeviceGuard g(c->device);
   int32_t st = 0;
-  if (hipDeviceSynchronize() != hipSuccess ||
+  if (ctx_wait(c) != XCG_OK ||
       hipMemcpyAsync(c->h_status, c->d_status, sizeof st, hipMemcpyDeviceToHost, nullptr) != hipSuccess ||
       hipStreamSynchronize(nullptr) != hipSuccess)
     return XCG_EHIP;
@@ -662,9 +692,12 @@ int xcg_ctx_status(xcg_ctx* c) {
   return st ? XCG_EOVERFLOW : XCG_OK;
 }
 
-int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint64_t* d_chunk_off,
-                     const uint32_t* d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t* d_out,
-                     const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_stats, void* stream) {
+}  // extern "C"
+
+namespace {
+int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint64_t* d_chunk_off,
+                      const uint32_t* d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t* d_out,
+                      const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_stats, void* stream) {
   if (!c) return XCG_EINVAL;
   if (n == 0) return XCG_OK;
   if (!d_in || !d_chunk_off || !d_chunk_len || !d_out || !d_out_off || !d_out_len) return XCG_EINVAL;
@@ -717,6 +750,21 @@ int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint6
   int rc = xcg_launch_encode_independent(d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, c->flags, d_out,
                                          d_out_off, d_out_len, d_stats, c->d_status, (hipStream_t)stream);
   return rc == 0 ? XCG_OK : (rc == -22 ? XCG_EINVAL : XCG_EHIP);
+}
+}  // namespace
+
+extern "C" {
+
+int xcg_encode_batch(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint64_t* d_chunk_off,
+                     const uint32_t* d_chunk_len, uint32_t n, uint32_t max_chunk_len, uint8_t* d_out,
+                     const uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_stats, void* stream) {
+  const int rc = encode_batch_impl(c, semantics, d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, d_out, d_out_off,
+                                   d_out_len, d_stats, stream);
+  if (c) {
+    DeviceGuard g(c->device);
+    ctx_mark(c, (hipStream_t)stream);
+  }
+  return rc;
 }
 
 int xcg_encode_host(xcg_ctx* c, int semantics, const uint8_t* h_in, uint64_t in_len, const uint64_t* h_chunk_off,
@@ -786,10 +834,13 @@ int xcg_encode_host(xcg_ctx* c, int semantics, const uint8_t* h_in, uint64_t in_
   return rc;
 }
 
-int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_off, const uint32_t* d_chunk_len,
-                     uint32_t n, uint32_t max_chunk_len, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
-                     uint64_t* d_out_len, int32_t* d_chunk_status, uint64_t* d_consumed, uint64_t* h_unknown,
-                     uint32_t unknown_cap, uint32_t* h_nunknown, uint64_t* h_total_out, void* stream) {
+}  // extern "C"
+
+namespace {
+int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_off, const uint32_t* d_chunk_len,
+                      uint32_t n, uint32_t max_chunk_len, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                      uint64_t* d_out_len, int32_t* d_chunk_status, uint64_t* d_consumed, uint64_t* h_unknown,
+                      uint32_t unknown_cap, uint32_t* h_nunknown, uint64_t* h_total_out, void* stream) {
   if (!c || (n && (!d_enc || !d_chunk_off || !d_chunk_len || !d_out_off || !d_out_len || !d_chunk_status ||
                    !d_consumed)))
     return XCG_EINVAL;
@@ -809,7 +860,7 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
   XcgDecodeArgs a{d_enc, d_chunk_off, d_chunk_len, n, d_out, out_cap, d_out_off, d_out_len, d_chunk_status,
                   d_consumed, c->d_status, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                   c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
-                  c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
+                  c->ds.u_keys, c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
                   c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count, c->bounded ? &c->lru : nullptr,
                   max_chunk_len / 2050 + 1};
   uint64_t total = 0, blockp = 0, berr = 0;
@@ -834,6 +885,7 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
     (void)hipMemsetAsync(c->d_status, 0, 4, (hipStream_t)stream);
     return XCG_ENOTSUP;
   }
+  if (nunk > UNKNOWN_CAP) return XCG_EOVERFLOW;     // more distinct unknown hashes than the set holds
   if (nunk && blockp < berr) {
     // XCodecDecoder::decode_skim (xcodec/xcodec_decoder.cc:196-272): every REF
     // from the blocking point on that cannot resolve, as a sorted set.  The
@@ -853,6 +905,23 @@ int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_o
     if (h_nunknown) *h_nunknown = k;
   }
   return XCG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int xcg_decode_batch(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_off, const uint32_t* d_chunk_len,
+                     uint32_t n, uint32_t max_chunk_len, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                     uint64_t* d_out_len, int32_t* d_chunk_status, uint64_t* d_consumed, uint64_t* h_unknown,
+                     uint32_t unknown_cap, uint32_t* h_nunknown, uint64_t* h_total_out, void* stream) {
+  const int rc = decode_batch_impl(c, d_enc, d_chunk_off, d_chunk_len, n, max_chunk_len, d_out, out_cap, d_out_off,
+                                   d_out_len, d_chunk_status, d_consumed, h_unknown, unknown_cap, h_nunknown,
+                                   h_total_out, stream);
+  if (c) {
+    DeviceGuard g(c->device);
+    ctx_mark(c, (hipStream_t)stream);
+  }
+  return rc;
 }
 
 int xcg_window_create(xcg_ctx* c, xcg_window** out) {
@@ -930,9 +999,9 @@ int xcg_pack_outputs(xcg_ctx* c, const uint8_t* d_out, const uint64_t* d_out_off
                      uint32_t n, uint8_t* d_packed, uint64_t* d_packed_off, uint64_t* d_total, void* stream) {
   if (!c || (n && (!d_out || !d_out_off || !d_out_len || !d_packed || !d_packed_off || !d_total))) return XCG_EINVAL;
   DeviceGuard g(c->device);
-  return xcg_launch_pack(d_out, d_out_off, d_out_len, n, d_packed, d_packed_off, d_total, (hipStream_t)stream) == 0
-             ? XCG_OK
-             : XCG_EHIP;
+  const int rc = xcg_launch_pack(d_out, d_out_off, d_out_len, n, d_packed, d_packed_off, d_total, (hipStream_t)stream);
+  ctx_mark(c, (hipStream_t)stream);
+  return rc == 0 ? XCG_OK : XCG_EHIP;
 }
 
 int xcg_window_hashes(xcg_ctx* c, const uint8_t* d_x, uint64_t len, uint64_t* d_hash, void* stream) {

@@ -88,6 +88,7 @@ struct XcgLruState {
   uint64_t clock;         // LRU time base of the next batch (host)
   uint32_t* part;         // per-tile counts of the multi-workgroup scans (grown on demand)
   uint32_t part_cap;
+  uint32_t last_base;     // first chunk of the last committed sub-batch (its rows stay in the scratch)
 };
 
 // A batch's cache references for the LRU pass: enters as declaration rows

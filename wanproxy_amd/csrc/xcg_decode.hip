@@ -73,7 +73,23 @@ struct DecParams {
   // ---- bounded cache (xcg_lru.hip): a persistent entry serves a lookup at
   // stream time (chunk << 21 | op offset) only before ptime[slot]
   const uint64_t* ptime;
+  uint64_t* u_keys;            // unknown-hash set (EMPTY_KEY = free)
+  uint32_t u_mask;
 };
+
+// Insert h into an open-addressed set; true if it was not there.  A full set
+// reports every hash as new (the caller then overflows its cap).
+__device__ __forceinline__ bool uset_insert(uint64_t* keys, uint32_t mask, uint64_t h) {
+  uint32_t i = tab_slot((uint32_t)h, (uint32_t)(h >> 32), mask);
+  for (uint32_t n = 0; n <= mask; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&keys[i], (unsigned long long)EMPTY_KEY,
+                                    (unsigned long long)h);
+    if (prev == EMPTY_KEY) return true;
+    if (prev == h) return false;
+    i = (i + 1) & mask;
+  }
+  return true;
+}
 
 // Is persistent slot gv live for a lookup at stream position `here`?
 __device__ __forceinline__ bool g_live(const DecParams& prm, uint64_t gv, uint64_t here) {
@@ -576,10 +592,15 @@ __global__ __launch_bounds__(256) void decode_refcheck_kernel(DecParams prm) {
         if (!ok) ok = g_live(prm, tab_lookup_t(prm.g, lo, hi), here);
         if (!ok) {
           atomicMin((unsigned long long*)prm.block_pos, (unsigned long long)here);
-          const uint32_t k = atomicAdd(prm.nunknown, 1u);
-          if (k < prm.unknown_cap) {
-            prm.unknown[k] = h;
-            prm.unknown_pos[k] = here;
+          // decode_skim's set (xcodec_decoder.cc:196-272): each unknown hash once
+          // (u: open-addressed set of 2 * unknown_cap slots); past the cap the
+          // count keeps growing and xcg_decode_batch reports XCG_EOVERFLOW.
+          if (uset_insert(prm.u_keys, prm.u_mask, h)) {
+            const uint32_t k = atomicAdd(prm.nunknown, 1u);
+            if (k < prm.unknown_cap) {
+              prm.unknown[k] = h;
+              prm.unknown_pos[k] = here;
+            }
           }
         }
       }
@@ -832,6 +853,29 @@ __global__ __launch_bounds__(256) void dec_replace_kernel(DecParams prm, const u
   }
 }
 
+// Before anything is emitted or committed: batch EXTRACTs of one hash that
+// the batch decoder cannot model -- a second EXTRACT with other bytes (name
+// reuse; REFs between them would need the latest bytes, the emit pass uses the
+// earliest), or EXTRACTs on both sides of the stop point.  Status bit 9 makes
+// xcg_decode_batch refuse the batch (XCG_ENOTSUP) with the cache, window and
+// outputs untouched.  One thread per batch-table slot; the byte compare is rare.
+__global__ __launch_bounds__(256) void dec_precheck_kernel(DecParams prm) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (w > prm.x.mask) return;
+  const uint64_t key = prm.x.keys[w];
+  if (key == EMPTY_KEY) return;
+  const uint64_t first = prm.x.vals[w], last = prm.x_latest[w];
+  const uint64_t blockp = min(*prm.block_pos, *prm.berr_pos);
+  if (first >= blockp || last == first) return;
+  bool bad = last >= blockp;
+  if (!bad) {
+    const uint8_t* a = prm.in + prm.chunk_off[first >> 32] + (uint32_t)first;
+    const uint8_t* b = prm.in + prm.chunk_off[last >> 32] + (uint32_t)last;
+    for (uint32_t k = 0; k < SEG && !bad; ++k) bad = a[k] != b[k];
+  }
+  if (bad) atomicOr(prm.status, 1 << 9);
+}
+
 // Pack per-chunk output slots into one contiguous buffer (one wave per chunk).
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
                                                    const uint64_t* dst_off, uint8_t* dst, uint32_t n) {
@@ -946,6 +990,7 @@ struct XcgDecodeArgs {
   uint64_t* x_vals;
   uint64_t* x_latest;
   uint32_t x_mask;
+  uint64_t* u_keys;      // unknown-hash set, 2 * unknown_cap slots
   uint64_t* unknown;
   uint64_t* unknown_pos;
   uint32_t* nunknown;
@@ -985,6 +1030,8 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   p.unknown_pos = a->unknown_pos;
   p.nunknown = a->nunknown;
   p.unknown_cap = a->unknown_cap;
+  p.u_keys = a->u_keys;
+  p.u_mask = 2 * a->unknown_cap - 1;
   p.block_pos = a->scratch + 1;
   p.berr_pos = a->scratch + 2;
   p.t_end = a->scratch + 5;
@@ -1001,7 +1048,8 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
       hipMemsetAsync(a->x_vals, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->x_latest, 0, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->scratch + 1, 0xFF, 16, stream) != hipSuccess ||
-      hipMemsetAsync(a->nunknown, 0, 4, stream) != hipSuccess)
+      hipMemsetAsync(a->nunknown, 0, 4, stream) != hipSuccess ||
+      hipMemsetAsync(a->u_keys, 0xFF, 16ull * a->unknown_cap, stream) != hipSuccess)
     return -5;
   // scan, then number the declares
   hipLaunchKernelGGL(decode_kernel<false>, grid, block, 0, stream, p);
@@ -1084,11 +1132,24 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   if (nbref > 0) hipLaunchKernelGGL(decode_brefcheck_kernel, grid, block, 0, stream, p);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)a->out_len, a->out_off,
                      n, a->scratch);
+  hipLaunchKernelGGL(dec_precheck_kernel, dim3((unsigned)(((uint64_t)a->x_mask + 256) / 256)), dim3(256), 0, stream,
+                     p);
+  a->h_scratch[10] = 0;
   if (hipMemcpyAsync(a->h_scratch, a->scratch, 24, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipMemcpyAsync(a->h_scratch + 6, a->nunknown, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipMemcpyAsync(a->h_scratch + 10, a->status, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess) {
     if (dfull) (void)hipFreeAsync(dfull, stream);
     return -5;
+  }
+  if (a->h_scratch[10] & (1u << 9)) {
+    // refused before any output, cache or window change (dec_precheck_kernel)
+    a->h_scratch[11] = a->h_scratch[10] & ~(uint64_t)(1u << 9);
+    (void)hipMemcpyAsync(a->status, a->h_scratch + 11, 4, hipMemcpyHostToDevice, stream);
+    (void)hipStreamSynchronize(stream);
+    if (dfull) (void)hipFreeAsync(dfull, stream);
+    if (lru_mem) (void)hipFreeAsync(lru_mem, stream);
+    return -95;
   }
   *total_out = a->h_scratch[0];
   *block_pos_out = a->h_scratch[1];

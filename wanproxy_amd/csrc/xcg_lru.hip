@@ -653,6 +653,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     }
     const LruBatch b = batch_of(a);
     if (xcg_lru_commit(&b, L, st)) return -5;
+    L->last_base = i0;
     i0 += m;
     const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
     const uint64_t want = used ? (uint64_t)C * 9 / 10 * m / used : (uint64_t)n;

@@ -76,7 +76,12 @@ bool uuid_ok(const uint8_t* u) {   // the string form UUID::decode accepts (8-4-
 // there equals the segment the REF names (find_reference only emits a REF on
 // byte equality, xcodec_encoder.cc:382-390), so the refmap's segments come
 // from the frame's own input.
+// An out-of-band declaration is written as F1 02 BE64 too (xcodec_encoder.cc:
+// 288-295), but encode_declaration passes no refmap: those (hash, input offset)
+// pairs -- `decl`, sorted -- are skipped, so an <ASK> for such a hash is a
+// protocol error as in the reference (xcodec_pipe_pair.cc:265-267).
 void frame_refs(const uint8_t* enc, uint64_t n, const uint8_t* in,
+                const std::vector<std::pair<uint64_t, uint64_t>>& decl,
                 std::unordered_map<uint64_t, std::vector<uint8_t>>& refmap) {
   uint64_t i = 0, pos = 0;
   while (i < n) {
@@ -84,9 +89,10 @@ void frame_refs(const uint8_t* enc, uint64_t n, const uint8_t* in,
     const uint8_t op = enc[i + 1];
     if (op == 0x00) { i += 2; ++pos; }                      // escaped 0xF1
     else if (op == 0x01) { i += 2 + SEG; pos += SEG; }      // EXTRACT
-    else {                                                  // REF
+    else {                                                  // REF (or out-of-band declaration)
       const uint64_t h = get_be(enc + i + 2, 8);
-      if (!refmap.count(h)) refmap.emplace(h, std::vector<uint8_t>(in + pos, in + pos + SEG));
+      const bool is_decl = std::binary_search(decl.begin(), decl.end(), std::make_pair(pos, h));
+      if (!is_decl && !refmap.count(h)) refmap.emplace(h, std::vector<uint8_t>(in + pos, in + pos + SEG));
       i += 10;
       pos += SEG;
     }
@@ -349,6 +355,9 @@ int xcg_pipe_encoder_consume_many(xcg_pipe* const* pipes, const uint8_t* const* 
     if (rc != XCG_OK) return rc;
   }
   for (uint32_t k = 0; k < n; ++k) pipes[k]->begin();
+  uint32_t eflags = 0;
+  if (xcg_ctx_flags(enc, &eflags) != XCG_OK) return XCG_EINVAL;
+  const bool oob = (eflags & XCG_FLAG_OOB) != 0, nullc = (eflags & XCG_FLAG_NULLCACHE) != 0;
   uint32_t f = 0;
   for (uint32_t k = 0; k < n; ++k) {
     xcg_pipe* p = pipes[k];
@@ -364,7 +373,19 @@ int xcg_pipe_encoder_consume_many(xcg_pipe* const* pipes, const uint8_t* const* 
     }
     for (; f < nf && frames[f].pipe == k; ++f) {
       std::unordered_map<uint64_t, std::vector<uint8_t>> rm;
-      frame_refs(enc_out.data() + oo[f], ol[f], in.data() + off[f], rm);
+      std::vector<std::pair<uint64_t, uint64_t>> decl;   // (input offset, hash) of out-of-band declarations
+      if (nullc) {
+        // TackNullCache: every F1 02 is a declaration (lookups always miss)
+      } else if (oob) {
+        std::vector<uint64_t> dh(fl[f] / SEG + 1);
+        std::vector<uint32_t> dp(dh.size());
+        uint32_t nd = 0;
+        const int rc = xcg_last_declarations(enc, f, dh.data(), dp.data(), (uint32_t)dh.size(), &nd);
+        if (rc != XCG_OK) return rc;
+        for (uint32_t d = 0; d < nd && d < dh.size(); ++d) decl.emplace_back(dp[d], dh[d]);
+        std::sort(decl.begin(), decl.end());
+      }
+      if (!nullc) frame_refs(enc_out.data() + oo[f], ol[f], in.data() + off[f], decl, rm);
       p->ref_frames.push_back(std::move(rm));
       p->to_peer.push_back(OP_FRAME);                    // (:620-628)
       put_be32(p->to_peer, (uint32_t)ol[f]);
