@@ -1,0 +1,105 @@
+"""The oracle's XCodecCachePair (xcodec/xcodec_cache.h:140-237) of a bounded
+XCodecMemoryCache primary and a disk FIFO secondary (XCodecDisk,
+xcodec/xcodec_cache_disk.cc:694-823) pinned against the reference: fixtures
+made by tests/golden/make_pair_golden.py from the real pair, encoder and
+decoder over a restated disk level (oracle/ref_driver.cc RefDiskCache; the
+reference's XCodecDisk needs libuuid's header, absent here), and a direct
+comparison with oracle/_ref when it is built."""
+import hashlib
+import importlib.util
+import json
+import os
+
+import pytest
+
+from oracle.lib import MODE_STREAM
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_spec = importlib.util.spec_from_file_location('make_pair_golden', os.path.join(HERE, 'golden/make_pair_golden.py'))
+mpg = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(mpg)
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope='module')
+def pair_golden():
+    with open(os.path.join(HERE, 'golden/pair.json')) as f:
+        return json.load(f)
+
+
+def pair_inputs(name, _memo={}):
+    if name not in _memo:
+        _memo[name] = mpg.inputs(name)
+    return _memo[name]
+
+
+def test_pair_inputs_pinned(pair_golden):
+    for name, meta in pair_golden['inputs'].items():
+        d = pair_inputs(name)
+        assert (len(d), sha(d)) == (meta['len'], meta['sha256']), name
+
+
+def test_pair_geometry():
+    # XCodecDisk(fd, size): (size / 2048 - 18) / 205 index blocks of 204 entries
+    assert mpg.disk_bytes(1) == (18 + 205) * 2048
+    from oracle.lib import Oracle
+    o = Oracle()
+    with pytest.raises(ValueError):
+        o.cache_new_pair(1 << 20, 222 * 2048)            # one block short of an index block
+    c = o.cache_new_pair(1 << 20, mpg.disk_bytes(3))
+    o.cache_free(c)
+
+
+def test_pair_encode_golden(pair_golden, oracle):
+    from wanproxy_amd.synth import chunks_of
+    for case in pair_golden['cases']:
+        d = pair_inputs(case['input'])
+        offs, lens = chunks_of(d, case['chunk'])
+        c = oracle.cache_new_pair(case['limit'], case['disk'])
+        outs = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+        entries, written = oracle.pair_stats(c)
+        oracle.cache_free(c)
+        key = (case['input'], case['chunk'], case['limit'], case['disk'])
+        assert [len(o) for o in outs] == case['lens'], key
+        assert [sha(o)[:32] for o in outs] == case['chunk_sha256'], key
+        assert (entries, written) == (case['disk_entries'], case['disk_written']), key
+
+
+def test_pair_decode_golden(pair_golden, oracle):
+    from wanproxy_amd.synth import chunks_of
+    for case in pair_golden['cases']:
+        d = pair_inputs(case['input'])
+        offs, lens = chunks_of(d, case['chunk'])
+        c = oracle.cache_new_pair(case['limit'], case['disk'])
+        encs = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+        oracle.cache_free(c)
+        dc = oracle.cache_new_pair(case['limit'], case['disk'])
+        dec = oracle.decoder_new(dc)
+        for e, want in zip(encs, case['dec']):
+            ok, out, cons, unk = oracle.decode(e, dc, decoder=dec)
+            got = {'ok': ok, 'consumed': cons, 'nunknown': len(unk), 'out_len': len(out), 'out_sha256': sha(out)}
+            assert got == want, (case['input'], case['chunk'], case['limit'])
+        oracle.decoder_free(dec)
+        oracle.cache_free(dc)
+
+
+def test_pair_vs_reference_live(ref_oracle, oracle):
+    """Random geometries, both libraries on the same stream."""
+    import numpy as np
+    from wanproxy_amd import synth
+    rng = np.random.default_rng(7)
+    for t in range(6):
+        d = synth.stream(int(rng.integers(1 << 30)), int(rng.integers(1, 5)) << 20, int(rng.integers(10, 70)), 0)
+        chunk = int(rng.choice([4096, 16384, 65536, 131072]))
+        limit = int(rng.integers(1, 600)) * 2048
+        disk = mpg.disk_bytes(int(rng.integers(1, 8)))
+        offs, lens = synth.chunks_of(d, chunk)
+        res = []
+        for lib in (oracle, ref_oracle):
+            c = lib.cache_new_pair(limit, disk)
+            res.append((lib.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c), lib.pair_stats(c)))
+            lib.cache_free(c)
+        assert res[0] == res[1], (t, chunk, limit, disk)
