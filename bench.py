@@ -211,10 +211,13 @@ def other_configs():
     spec.loader.exec_module(cb)
     # C5-LRU: C5 on wanproxy.conf's bounded 128 MiB memory cache (LRU
     # eviction), every chunk checked against the oracle's bounded cache
+    # C5-PAIR: C5 on wanproxy.conf's whole cache, the 128 MiB memory cache over
+    # a 1 GiB disk (XCodecCachePair), every chunk checked against the oracle's pair
     a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, lru_mib=128, lru_check=1.0,
-                           no_decode=False)
+                           disk_mib=1024, no_decode=False)
     out = {}
-    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru)):
+    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru),
+                     ('C5-PAIR', cb.run_c5pair)):
         try:
             out[name] = fn(a)
         except BaseException as e:          # SystemExit from a parity check included

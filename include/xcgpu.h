@@ -96,6 +96,24 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
  * batches are cut into sub-batches that fit); XCG_SEM_INDEPENDENT with chunks of
  * more than limit * 2048 bytes; BACKREF ops in a decode on a bounded cache. */
 int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_ctx **out);
+/* A context whose persistent cache is wanproxy.conf's XCodecCachePair
+ * (xcodec/xcodec_cache.h:140-237, programs/wanproxy/wanproxy.conf:8-26): a
+ * bounded XCodecMemoryCache(uuid, memory_cache_limit_bytes) primary (LRU, as
+ * xcg_ctx_create_bounded) over the local XCodecDiskCache of a fresh volume of
+ * disk_bytes (xcodec/xcodec_cache_disk.cc: FIFO data blocks in index blocks
+ * of 204 entries, (disk_bytes / 2048 - 18) / 205 index blocks).  A lookup
+ * that misses the primary and hits the disk enters the hash into the primary;
+ * a primary hit re-enters a hash the disk index lost.  XCG_SEM_STREAM batches
+ * are bit-exact with the sequential XCodecEncoder on such a pair; the disk
+ * level lives in HBM (its bytes, and the index as a GPU table).  In-band only
+ * (XCG_EINVAL with XCG_FLAG_OOB / XCG_FLAG_NULLCACHE, or a volume without one
+ * index block).  Decode batches and the single-segment host calls return
+ * XCG_ENOTSUP on a pair context. */
+int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
+                        xcg_ctx **out);
+/* Pair context counters: st[0] primary entries, st[1] disk index entries,
+ * st[2] disk entries written so far, st[3] disk index blocks. */
+int xcg_pair_stats(xcg_ctx *ctx, uint64_t *st);
 void xcg_ctx_destroy(xcg_ctx *ctx);
 /* The XCG_FLAG_* the context was created with. */
 int xcg_ctx_flags(const xcg_ctx *ctx, uint32_t *flags);
@@ -118,6 +136,20 @@ int xcg_cache_enter_host(xcg_ctx *ctx, uint64_t hash, const uint8_t *seg);
  * for earlier ones; a single-chunk batch is always one sub-batch). */
 int xcg_last_declarations(xcg_ctx *ctx, uint32_t chunk, uint64_t *h_hash, uint32_t *h_pos, uint32_t cap,
                           uint32_t *h_count);
+/* The cache references chunk `chunk` of the last XCG_SEM_STREAM batch made on
+ * a bounded or pair cache, in stream order: every lookup that found the hash
+ * in a level at some point of the batch (XCodecCache::lookup refreshes an LRU
+ * entry, and a pair promotes or re-enters it, xcodec/xcodec_cache.h:208-230,
+ * :348-364 -- whether or not the bytes then match) and every declaration's
+ * enter (xcodec/xcodec_encoder.cc:284-286).  h_kind[i]: 0 enter (h_ref[i] =
+ * declaration index, as xcg_last_declarations numbers them), 1 lookup of a
+ * hash this batch declared, 2 lookup of a cached hash, 3 lookup of a cached
+ * hash already gone (a miss).  A host mirror of the cache that replays them
+ * in order -- lookup for kinds 1-3, enter for 0 -- holds what the engine's
+ * cache holds.  XCG_ENOTSUP on an unbounded cache (its lookups change
+ * nothing) and for chunks before the last sub-batch. */
+int xcg_last_references(xcg_ctx *ctx, uint32_t chunk, uint64_t *h_hash, uint32_t *h_kind, uint32_t *h_ref,
+                        uint32_t cap, uint32_t *h_count);
 /* Diagnostics: copy the persistent cache's lane filters to host memory
  * (h_filt: 2^19 bits; h_ftab: up to ftab_words u32; *h_fmask = buckets - 1). */
 int xcg_debug_cache_dump(xcg_ctx *ctx, uint32_t *h_filt, uint32_t *h_ftab, uint64_t ftab_words, uint32_t *h_fmask);

@@ -21,12 +21,19 @@
 
 #include "../include/xcgpu.h"
 
+/* Largest input of one encode() call (XCodecPipePair frames are at most
+ * XCODEC_PIPE_MAX_FRAME / 2 = 512 KiB, xcodec/xcodec_pipe_pair.cc:596-604;
+ * tack reads 64 KiB, programs/tack/tack.cc:419). */
+#define XCGPU_MAX_ENCODE (512u * 1024u)
+
 class XCodecCache;
 
 namespace xcgpu_binding {
 
-/* Cache kinds the engine can mirror exactly: XCodecMemoryCache (unbounded) and
- * tack's TackNullCache (lookups miss).  Anything else is rejected loudly. */
+/* Cache kinds the engine mirrors exactly: XCodecMemoryCache (unbounded, or
+ * bounded via set_cache_limit), XCodecCachePair of a bounded memory cache and
+ * the local disk cache (via set_pair_geometry), and tack's TackNullCache
+ * (lookups miss). */
 inline bool is_null_cache(XCodecCache *cache)
 {
 	return strstr(typeid(*cache).name(), "NullCache") != NULL;
@@ -38,6 +45,10 @@ inline std::map<XCodecCache *, xcg_ctx *>& ctx_map()
 	return ctxs;
 }
 
+inline std::map<XCodecCache *, uint64_t>& limit_map();
+struct PairGeometry;
+inline std::map<XCodecCache *, PairGeometry>& pair_map();
+
 /* The GPU mirror lives as long as the cache object.  wanproxy and tack keep
  * their caches for the life of the process; a caller that deletes a cache
  * must call forget() first (the reference caches have no hook for it). */
@@ -48,6 +59,8 @@ inline void forget(XCodecCache *cache)
 		return;
 	xcg_ctx_destroy(it->second);
 	ctx_map().erase(it);
+	limit_map().erase(cache);
+	pair_map().erase(cache);
 }
 
 /* Bounded memory caches: XCodecMemoryCache keeps memory_cache_limit_
@@ -99,6 +112,10 @@ inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctxs.find(cache);
 	if (it != ctxs.end())
 		return it->second;
+	/* a pair the binding was not told about (e.g. made by XCodecCachePair::
+	 * connect) cannot be mirrored: refuse rather than diverge */
+	if (strstr(typeid(*cache).name(), "XCodecCachePair") != NULL && !is_pair(cache))
+		return NULL;
 	uint32_t flags = out_of_band ? XCG_FLAG_OOB : 0;
 	if (is_null_cache(cache))
 		flags |= XCG_FLAG_NULLCACHE;
@@ -108,8 +125,15 @@ inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 	if (dev != NULL)
 		device = atoi(dev);
 	std::map<XCodecCache *, uint64_t>::const_iterator lim = limit_map().find(cache);
-	if (lim != limit_map().end() ? xcg_ctx_create_bounded(device, flags, lim->second, &ctx) != XCG_OK
-	                             : xcg_ctx_create(device, flags, &ctx) != XCG_OK)
+	std::map<XCodecCache *, PairGeometry>::const_iterator pg = pair_map().find(cache);
+	int rc;
+	if (pg != pair_map().end())
+		rc = xcg_ctx_create_pair(device, flags, pg->second.memory_limit_bytes, pg->second.disk_bytes, &ctx);
+	else if (lim != limit_map().end())
+		rc = xcg_ctx_create_bounded(device, flags, lim->second, &ctx);
+	else
+		rc = xcg_ctx_create(device, flags, &ctx);
+	if (rc != XCG_OK)
 		return NULL;
 	ctxs[cache] = ctx;
 	return ctx;

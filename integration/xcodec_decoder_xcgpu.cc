@@ -7,8 +7,14 @@
  * does not know but the host cache does (entered by ASK/LEARN,
  * xcodec/xcodec_pipe_pair.cc:274-333) are pushed to the GPU and the call is
  * retried; what remains unknown is returned like decode_skim (:196-272).
- * EXTRACTs are mirrored into the host cache (enter / replace, :106-136).
+ * The call's cache references are mirrored into the host cache in stream
+ * order: EXTRACT lookup + enter / replace (:106-136), REF lookups (:151-162)
+ * and, when blocked, decode_skim's lookups (:196-272) -- on a bounded cache
+ * each lookup that finds its hash refreshes it, so the host cache then holds
+ * what the engine's does.
  */
+#include <string.h>
+
 #include <set>
 #include <vector>
 
@@ -61,6 +67,12 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 			seg->unref();
 			i += 2 + XCODEC_SEGMENT_LENGTH;
 		} else if (op == XCODEC_OP_REF) {
+			/* :151-162: the REF's lookup refreshes a bounded cache's entry */
+			uint64_t behash;
+			memcpy(&behash, &in[i + 2], sizeof behash);
+			BufferSegment *oseg = cache->lookup(BigEndian::decode(behash));
+			if (oseg != NULL)
+				oseg->unref();
 			i += 10;
 		} else if (op == XCODEC_OP_BACKREF) {
 			i += 3;
@@ -68,6 +80,79 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 			i += 2;
 		}
 	}
+}
+
+/* decode_skim's lookups (:196-272) of the REFs from the blocking point on. */
+static void
+mirror_skim(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a)
+{
+	uint64_t i = a;
+	const uint64_t b = in.size();
+	while (i + 1 < b) {
+		if (in[i] != XCODEC_MAGIC) {
+			i++;
+			continue;
+		}
+		const uint8_t op = in[i + 1];
+		if (op == XCODEC_OP_ESCAPE) {
+			i += 2;
+		} else if (op == XCODEC_OP_EXTRACT) {
+			if (b - i < 2 + XCODEC_SEGMENT_LENGTH)
+				return;
+			i += 2 + XCODEC_SEGMENT_LENGTH;
+		} else if (op == XCODEC_OP_REF) {
+			if (b - i < 10)
+				return;
+			uint64_t behash;
+			memcpy(&behash, &in[i + 2], sizeof behash);
+			BufferSegment *oseg = cache->lookup(BigEndian::decode(behash));
+			if (oseg != NULL)
+				oseg->unref();
+			i += 10;
+		} else if (op == XCODEC_OP_BACKREF) {
+			if (b - i < 3)
+				return;
+			i += 3;
+		} else {
+			return;
+		}
+	}
+}
+
+/* Decoded size of in[a..) if every op resolves: literal and escaped bytes one
+ * each, EXTRACT / REF / BACKREF one segment each (:73-185). */
+static uint64_t
+decoded_bound(const std::vector<uint8_t>& in, uint64_t a)
+{
+	uint64_t i = a, n = 0;
+	const uint64_t b = in.size();
+	while (i < b) {
+		const uint8_t *m = (const uint8_t *)memchr(&in[i], XCODEC_MAGIC, b - i);
+		if (m == NULL)
+			return n + (b - i);
+		const uint64_t at = (uint64_t)(m - &in[0]);
+		n += at - i;
+		i = at;
+		if (i + 1 >= b)
+			return n;
+		const uint8_t op = in[i + 1];
+		if (op == XCODEC_OP_ESCAPE) {
+			n += 1;
+			i += 2;
+		} else if (op == XCODEC_OP_EXTRACT) {
+			n += XCODEC_SEGMENT_LENGTH;
+			i += 2 + XCODEC_SEGMENT_LENGTH;
+		} else if (op == XCODEC_OP_REF) {
+			n += XCODEC_SEGMENT_LENGTH;
+			i += 10;
+		} else if (op == XCODEC_OP_BACKREF) {
+			n += XCODEC_SEGMENT_LENGTH;
+			i += 3;
+		} else {
+			return n;
+		}
+	}
+	return n;
 }
 
 bool
@@ -85,7 +170,7 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	const uint32_t len = input->length();
 	std::vector<uint8_t> in(len);
 	input->copyout(&in[0], len);
-	std::vector<uint8_t> out((uint64_t)len * 205 + 4096);
+	std::vector<uint8_t> out;
 	std::vector<uint64_t> unk(1u << 16);
 	uint64_t pos = 0;
 	int32_t status = 0;
@@ -103,14 +188,9 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		const uint64_t off = 0;
 		const uint32_t rest = (uint32_t)(len - pos);
 		uint64_t ooff = 0, olen = 0, consumed = 0;
+		out.resize(decoded_bound(in, pos) + 1);
 		int rc = xcg_decode_host(ctx, &in[pos], rest, &off, &rest, 1, &out[0], out.size(), &ooff, &olen, &status,
 		                         &consumed, &unk[0], unk.size(), &nunk);
-		if (rc == XCG_EOVERFLOW) {
-			/* BACKREF-dense input: 3 bytes can decode to 2048 (nothing was committed). */
-			out.resize((uint64_t)rest / 3 * XCODEC_SEGMENT_LENGTH + rest + 4096);
-			rc = xcg_decode_host(ctx, &in[pos], rest, &off, &rest, 1, &out[0], out.size(), &ooff, &olen,
-			                     &status, &consumed, &unk[0], unk.size(), &nunk);
-		}
 		if (rc != XCG_OK) {
 			xcg_decode_set_window(ctx, NULL);
 			HALT(log_) << "xcgpu decode failed: " << xcg_strerror(rc);
@@ -136,6 +216,7 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 
 	input->skip(pos);
 	if (status == 1) {
+		mirror_skim(cache_, in, pos);
 		for (uint32_t k = 0; k < nunk; k++) {
 			BufferSegment *seg = cache_->lookup(unk[k]);
 			if (seg != NULL) {

@@ -6,10 +6,14 @@
  *
  * encode() flattens the input Buffer, runs one XCG_SEM_STREAM encode() on the
  * GPU against the cache's GPU mirror, appends the bytes, then reproduces the
- * reference's side effects on the host objects: the declarations enter the
- * XCodecCache (encode_declaration, :284-286) and every REF target enters the
- * refmap once (encode_reference, :364-371).
+ * reference's side effects on the host objects: the call's cache references
+ * are replayed into the XCodecCache in stream order (enters,
+ * encode_declaration :284-286, and -- on a bounded or pair cache, where they
+ * change the cache -- lookups, find_reference :374-416), and every REF target
+ * enters the refmap once, its segment taken from the input at the REF
+ * (encode_reference, :364-371).
  */
+#include <set>
 #include <vector>
 
 #include <common/buffer.h>
@@ -52,6 +56,9 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 		HALT(log_) << "No MI355X device for the XCodec engine.";
 
 	const uint32_t len = input->length();
+	if (len > XCGPU_MAX_ENCODE)
+		HALT(log_) << "xcgpu encode: " << len << " bytes in one encode() call; the engine takes at most "
+		           << XCGPU_MAX_ENCODE << " (XCodecPipePair frames are <= 512 KiB, tack reads 64 KiB).";
 	std::vector<uint8_t> in(len);
 	input->moveout(&in[0], len);
 
@@ -64,7 +71,7 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 		HALT(log_) << "xcgpu encode failed: " << xcg_strerror(rc);
 	output->append(&out[0], olen);
 
-	/* Declarations made by this call, mirrored into the host cache. */
+	/* Declarations made by this call, in order (encode_declaration, :276-313). */
 	uint32_t ndecl = 0;
 	std::vector<uint64_t> dh(len / XCODEC_SEGMENT_LENGTH + 1);
 	std::vector<uint32_t> dp(dh.size());
@@ -73,49 +80,85 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 		if (rc != XCG_OK)
 			HALT(log_) << "xcgpu declarations: " << xcg_strerror(rc);
 	}
-	std::map<uint64_t, unsigned> declared;
-	for (uint32_t i = 0; i < ndecl; i++) {
-		BufferSegment *seg = segment_of(&in[dp[i]]);
-		cache_->enter(dh[i], seg);
-		seg->unref();
-		declared[dh[i]] = dp[i];
+
+	/*
+	 * The host cache mirror.  On a bounded or pair cache every lookup that
+	 * found its hash changed the cache (LRU refresh, promotion, disk
+	 * re-enter, xcodec/xcodec_cache.h:208-230, :348-364), so the call's cache
+	 * references are replayed in stream order; on an unbounded memory cache
+	 * only the enters matter.
+	 */
+	uint32_t nref = 0;
+	std::vector<uint64_t> rh(2 * dh.size() + 64);
+	std::vector<uint32_t> rk(rh.size()), rr(rh.size());
+	rc = xcgpu_binding::is_null_cache(cache_) ? XCG_ENOTSUP
+	     : xcg_last_references(ctx, 0, &rh[0], &rk[0], &rr[0], rh.size(), &nref);
+	if (rc == XCG_OK) {
+		if (nref > rh.size())
+			HALT(log_) << "xcgpu references: list overflow.";
+		for (uint32_t i = 0; i < nref; i++) {
+			if (rk[i] == 0) {
+				if (rr[i] >= ndecl)
+					HALT(log_) << "xcgpu references: unknown declaration.";
+				BufferSegment *seg = segment_of(&in[dp[rr[i]]]);
+				cache_->enter(dh[rr[i]], seg);
+				seg->unref();
+			} else {
+				BufferSegment *seg = cache_->lookup(rh[i]);
+				if (seg != NULL)
+					seg->unref();
+			}
+		}
+	} else if (rc == XCG_ENOTSUP) {
+		for (uint32_t i = 0; i < ndecl; i++) {
+			BufferSegment *seg = segment_of(&in[dp[i]]);
+			cache_->enter(dh[i], seg);
+			seg->unref();
+		}
+	} else {
+		HALT(log_) << "xcgpu references: " << xcg_strerror(rc);
 	}
 
 	if (refmap == NULL)
 		return;
-	/* REF ops of the output.  An out-of-band declaration looks like a REF and
-	 * comes first in the output for its hash (a REF to it can only follow);
-	 * encode_declaration passes no refmap (xcodec_encoder.cc:288-295), so that
-	 * first occurrence is skipped, later ones are REFs. */
-	uint64_t i = 0;
+	/*
+	 * REF ops of the output, each with the input offset it stands for: the
+	 * refmap segment is the input there (a REF is only emitted on byte
+	 * equality, xcodec_encoder.cc:382-390), entered once per hash
+	 * (encode_reference, :364-371).  An out-of-band declaration is written as
+	 * F1 02 too, but encode_declaration passes no refmap (:288-295): those
+	 * (offset, hash) pairs are skipped.
+	 */
+	std::set<std::pair<uint64_t, uint64_t> > declared;
+	if (!stream_)
+		for (uint32_t i = 0; i < ndecl; i++)
+			declared.insert(std::make_pair((uint64_t)dp[i], dh[i]));
+	uint64_t i = 0, pos = 0;
 	while (i < olen) {
 		if (out[i] != XCODEC_MAGIC) {
 			i++;
+			pos++;
 			continue;
 		}
 		const uint8_t op = out[i + 1];
 		if (op == XCODEC_OP_ESCAPE) {
 			i += 2;
+			pos++;
 		} else if (op == XCODEC_OP_EXTRACT) {
 			i += 2 + XCODEC_SEGMENT_LENGTH;
+			pos += XCODEC_SEGMENT_LENGTH;
 		} else {
 			uint64_t behash;
 			memcpy(&behash, &out[i + 2], sizeof behash);
 			const uint64_t hash = BigEndian::decode(behash);
+			const uint64_t at = pos;
 			i += 10;
-			if (!stream_) {
-				std::map<uint64_t, unsigned>::iterator dit = declared.find(hash);
-				if (dit != declared.end()) {
-					declared.erase(dit);
-					continue;
-				}
-			}
+			pos += XCODEC_SEGMENT_LENGTH;
+			if (declared.count(std::make_pair(at, hash)) != 0)
+				continue;
 			if (refmap->find(hash) != refmap->end())
 				continue;
-			BufferSegment *seg = cache_->lookup(hash);
-			if (seg == NULL)
-				HALT(log_) << "REF target missing from the cache mirror.";
-			refmap->insert(std::map<uint64_t, BufferSegment *>::value_type(hash, seg));
+			refmap->insert(std::map<uint64_t, BufferSegment *>::value_type(hash, segment_of(&in[at])));
 		}
 	}
 }

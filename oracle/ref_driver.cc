@@ -188,7 +188,11 @@ void *xcr_cache_new(void)
 void *xcr_cache_new_limited(uint64_t limit_bytes)
 {
 	UUID uuid;
-	return new XCodecMemoryCache(uuid, (size_t)limit_bytes);
+	XCodecCache *c = new XCodecMemoryCache(uuid, (size_t)limit_bytes);
+#ifdef XCGPU_DROPIN
+	xcgpu_binding::set_cache_limit(c, limit_bytes);   /* as wanproxy_config_class_cache.cc would */
+#endif
+	return c;
 }
 
 /* XCodecCachePair(XCodecMemoryCache(uuid, memory_limit_bytes), disk of

@@ -15,6 +15,8 @@ a GPU decode round trip.
        cold unbounded cache, batches of --batch-mib
   c5lru  c5 with a bounded --lru-mib (128) MiB LRU cache (wanproxy.conf's
        memory cache), checked against the oracle's bounded cache
+  c5pair c5 with wanproxy.conf's XCodecCachePair: the --lru-mib memory cache
+       over a --disk-mib (1024) MiB disk, checked against the oracle's pair
 
 Prints one JSON line per config.  --scale shrinks the inputs (tests).
 """
@@ -313,6 +315,53 @@ def run_c5lru(args):
             'checked': f'first {k} chunks vs the oracle with the same bounded cache; decoded back (unbounded decoder)'}
 
 
+def run_c5pair(args):
+    """C5 with wanproxy.conf's whole cache: XCodecCachePair of a bounded
+    --lru-mib memory primary and a --disk-mib disk secondary
+    (programs/wanproxy/wanproxy.conf:8-26; xcodec/xcodec_cache.h:140-237,
+    xcodec/xcodec_cache_disk.cc), every chunk checked against the oracle's pair."""
+    from oracle.lib import Oracle
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
+    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    limit = max(2048, int(args.lru_mib * MiB * min(1.0, args.scale * 8)))
+    disk = max(1 << 20, int(args.disk_mib * MiB * min(1.0, args.scale * 8)))
+    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    per = max(1, args.batch_mib * MiB // (128 * KiB))
+    B = Batches(ctx, data, offs, lens, per=per)
+    wall = timed_encode(B, args.reps)
+    got = B.outputs()
+    st = ctx.pair_stats()
+    k = min(len(got), max(64, int(args.lru_check * len(got))))
+    o = Oracle()
+    c = o.cache_new_pair(limit, disk)
+    exp = o.encode_batch(data, offs[:k], lens[:k], mode=1, cache=c)
+    ost = o.pair_stats(c) if k == len(got) else None
+    o.cache_free(c)
+    if got[:k] != exp:
+        bad = next(i for i in range(k) if got[i] != exp[i])
+        raise SystemExit(f'PARITY FAILURE (c5pair) at chunk {bad}')
+    if ost is not None and ost != (st[1], st[2]):
+        raise SystemExit(f'PARITY FAILURE (c5pair disk counters {st} vs {ost})')
+    dec = data.tobytes()
+    if not args.no_decode:
+        dctx = Context(0, cache_segments=nbytes // 2048 + 4096)
+        dec, _ = decode_device(dctx, got, per=per, chunk=128 * KiB)
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c5pair)')
+    inb = data.size
+    return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, XCodecCachePair(%d MiB LRU memory, %d MiB disk)'
+                      % (nbytes >> 20, limit >> 20, disk >> 20),
+            'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds,
+            'pair_stats': {'primary_entries': st[0], 'disk_entries': st[1], 'disk_written': st[2],
+                           'disk_index_blocks': st[3]},
+            'checked': f'first {k} chunks (and the disk counters) vs the oracle with the same pair; '
+                       'decoded back (unbounded decoder)'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('configs', nargs='*', default=['c2s', 'c3', 'c4', 'c5'])
@@ -321,12 +370,13 @@ def main():
     ap.add_argument('--batch-mib', type=int, default=512)
     ap.add_argument('--c4-batch', type=int, default=16384)
     ap.add_argument('--lru-mib', type=int, default=128)
+    ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
     ap.add_argument('--no-decode', action='store_true', help='skip the decode round trips (profiling runs)')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5, 'c5lru': run_c5lru}
+    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5, 'c5lru': run_c5lru, 'c5pair': run_c5pair}
     for c in args.configs:
         t0 = time.perf_counter()
         r = fns[c](args)

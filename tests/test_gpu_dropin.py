@@ -82,3 +82,48 @@ def test_dropin_refmap_like_reference(dropin, ref_oracle):
         assert r[0] == g[0], k
         assert r[1] == g[1], (k, len(r[1]), len(g[1]))
     assert sum(len(r[1]) for r in encs[0]) > 100
+
+
+@pytest.mark.parametrize('kind', ['bounded', 'pair'])
+def test_dropin_refmap_bounded_and_pair_like_reference(dropin, ref_oracle, kind):
+    """The same calls on a bounded XCodecMemoryCache and on wanproxy.conf's
+    XCodecCachePair: output and refmap call by call equal the reference's, and
+    the host cache the adapter keeps in step (by replaying the engine's cache
+    references in stream order, xcg_last_references) keeps agreeing with the
+    engine -- later calls depend on its LRU order and disk contents."""
+    import importlib.util
+    from wanproxy_amd import synth
+    spec = importlib.util.spec_from_file_location('mpg', os.path.join(ROOT, 'tests/golden/make_pair_golden.py'))
+    mpg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mpg)
+    d = mpg.inputs('pair_far') + mpg.inputs('pair_hot')[:1 << 20]
+    pieces = [d[a:a + 65536] for a in range(0, len(d), 65536)] + [d[:70000], d[100:2200], b'x' * 3000]
+    res = []
+    for o in (ref_oracle, dropin):
+        c = o.cache_new(120 * 2048) if kind == 'bounded' else o.cache_new_pair(120 * 2048, mpg.disk_bytes(2))
+        e = o.encoder_new(c)
+        res.append([o.encode_refmap(e, p) for p in pieces])
+        o.encoder_free(e)
+        o.cache_free(c)
+    for k, (a, b) in enumerate(zip(*res)):
+        assert a == b, (kind, k)
+
+
+def test_dropin_decode_bounded_like_reference(dropin, ref_oracle):
+    """One persistent decoder on a bounded cache, frame by frame (the REF
+    lookups refresh its LRU: the adapter replays them into the host cache)."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    d = synth.stream(0xDEC, 3 << 20, 60, 0)
+    offs, lens = synth.chunks_of(d, 65536)
+    c = ref_oracle.cache_new(300 * 2048)
+    encs = ref_oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    ref_oracle.cache_free(c)
+    res = []
+    for o in (ref_oracle, dropin):
+        dc = o.cache_new(300 * 2048)
+        dec = o.decoder_new(dc)
+        res.append([o.decode(e, dc, decoder=dec) for e in encs])
+        o.decoder_free(dec)
+        o.cache_free(dc)
+    assert res[0] == res[1]

@@ -1,0 +1,131 @@
+"""XCodecCachePair (xcodec/xcodec_cache.h:140-237) of a bounded memory primary
+and a disk FIFO secondary (xcodec/xcodec_cache_disk.cc:694-823) on the GPU
+(xcg_ctx_create_pair, wanproxy_amd/csrc/xcg_pair.hip): stream-semantics
+encodes bit-exact against the reference-made fixtures (tests/golden/pair.json,
+the real pair over a restated disk level), against the oracle's pair on random
+geometries, in both seed modes and split batches, and decoded back."""
+import hashlib
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_spec = importlib.util.spec_from_file_location('make_pair_golden', os.path.join(HERE, 'golden/make_pair_golden.py'))
+mpg = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(mpg)
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope='module')
+def pair_golden():
+    with open(os.path.join(HERE, 'golden/pair.json')) as f:
+        return json.load(f)
+
+
+def _inputs(name, _memo={}):
+    if name not in _memo:
+        _memo[name] = mpg.inputs(name)
+    return _memo[name]
+
+
+def test_pair_golden(pair_golden, stream_seed):
+    from wanproxy_amd.synth import chunks_of
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    for case in pair_golden['cases']:
+        d = _inputs(case['input'])
+        offs, lens = chunks_of(d, case['chunk'])
+        key = (case['input'], case['chunk'], case['limit'], case['disk'])
+        print('case', key, flush=True)
+        ctx = Context(0, memory_cache_limit=case['limit'], disk_bytes=case['disk'])
+        got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+        st = ctx.pair_stats()
+        ctx.close()
+        assert [len(o) for o in got] == case['lens'], key
+        assert [sha(o)[:32] for o in got] == case['chunk_sha256'], key
+        assert (st[1], st[2]) == (case['disk_entries'], case['disk_written']), key
+
+
+@pytest.mark.parametrize('split', [1, 3, 17])
+def test_pair_split_batches_vs_oracle(oracle, split):
+    """The same stream in calls of `split` chunks: one encoder across calls."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = mpg.inputs('pair_far')
+    offs, lens = synth.chunks_of(d, 65536)
+    limit, disk = 150 * 2048, mpg.disk_bytes(3)
+    c = oracle.cache_new_pair(limit, disk)
+    exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    est = oracle.pair_stats(c)
+    oracle.cache_free(c)
+    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    got = []
+    for a in range(0, offs.size, split):
+        got += ctx.encode_chunks(d, offs[a:a + split], lens[a:a + split], semantics=XCG_SEM_STREAM)
+    st = ctx.pair_stats()
+    ctx.close()
+    assert got == exp
+    assert (st[1], st[2]) == est
+
+
+def test_pair_random_vs_oracle(oracle):
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    rng = np.random.default_rng(11)
+    for t in range(8):
+        d = synth.stream(int(rng.integers(1 << 30)), int(rng.integers(1, 6)) << 20, int(rng.integers(10, 80)), 0)
+        chunk = int(rng.choice([4096, 16384, 65536, 131072]))
+        limit = int(rng.integers(chunk // 2048 + 1, 800)) * 2048
+        disk = mpg.disk_bytes(int(rng.integers(1, 10)))
+        offs, lens = synth.chunks_of(d, chunk)
+        c = oracle.cache_new_pair(limit, disk)
+        exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+        est = oracle.pair_stats(c)
+        oracle.cache_free(c)
+        ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+        got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+        st = ctx.pair_stats()
+        ctx.close()
+        bad = [i for i in range(len(got)) if got[i] != exp[i]]
+        assert not bad, (t, chunk, limit, disk, bad[:5])
+        assert (st[1], st[2]) == est, (t, chunk, limit, disk)
+
+
+def test_pair_scaled_c5_decodes(oracle):
+    """A scaled C5-PAIR (16 MiB stream, 128 KiB chunks, 1 MiB primary, 8 MiB
+    disk): oracle parity and a GPU decode round trip (unbounded decoder)."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = synth.stream(0xC5, 16 << 20, 20, 0)
+    offs, lens = synth.chunks_of(d, 131072)
+    limit, disk = 1 << 20, 8 << 20
+    c = oracle.cache_new_pair(limit, disk)
+    exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    oracle.cache_free(c)
+    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+    ctx.close()
+    assert got == exp
+    dctx = Context(0, cache_segments=(16 << 20) // 2048 + 1024)
+    outs, st, _, unk = dctx.decode_chunks(got)
+    dctx.close()
+    assert not (st != 0).any() and not unk
+    assert b''.join(outs) == d
+
+
+def test_pair_create_rejects():
+    from wanproxy_amd.xcgpu import XCGError, Context
+    with pytest.raises(XCGError):
+        Context(0, memory_cache_limit=1 << 20, disk_bytes=222 * 2048)     # no index block
+    with pytest.raises(XCGError):
+        Context(0, out_of_band=True, memory_cache_limit=1 << 20, disk_bytes=1 << 20)

@@ -175,6 +175,8 @@ struct xcg_ctx {
   // stream): the cache-inspection calls wait for this event only, never for
   // the whole device, so other contexts and streams keep running.
   hipEvent_t done_ev = nullptr;
+  XcgPairState* pair = nullptr;    // XCodecCachePair(memory, disk) (xcg_pair.hip)
+  uint32_t pair_C = 0;             // its primary limit in segments
 };
 
 namespace {
@@ -282,7 +284,7 @@ int ensure_cache(xcg_ctx* c) {
   // batch's declarations (up to the limit again) share the round's copy, so
   // it gets ~1 bucket per key (a bucket past 7 fingerprints sends every probe
   // into an exact check).
-  const uint64_t fkeys = c->bounded ? 4 * segs : segs;
+  const uint64_t fkeys = c->bounded ? 4 * segs : (c->pair ? segs + 2ull * c->pair_C : segs);
   const uint32_t fb = pow2_at_least(fkeys < 65536 ? 32768 : fkeys / 2);
   g.fmask = fb - 1;
   const uint32_t gw = pow2_at_least(fkeys < 131072 ? 65536 : fkeys / 2);
@@ -324,7 +326,7 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
-  if (c->bounded) {
+  if (c->bounded || c->pair) {
     b.maxe = 2 * maxd + 64;        // declarations + REFs + collision lookups of one chunk
     if (hipMalloc(&b.ev, 16ull * n * b.maxe) != hipSuccess || hipMalloc(&b.nev, 4ull * n) != hipSuccess ||
         hipMalloc(&b.ev_base, 4ull * (n + 1)) != hipSuccess || hipMalloc(&b.enter_base, 4ull * (n + 1)) != hipSuccess ||
@@ -438,6 +440,40 @@ int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_lim
   return XCG_OK;
 }
 
+int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
+                        xcg_ctx** out) {
+  if (!out || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE))) return XCG_EINVAL;
+  uint64_t C = memory_cache_limit_bytes / XCG_SEGMENT_LENGTH;   // xcodec_cache.h:283-287
+  if (C == 0) C = 1;
+  if (C > (1ull << 28)) return XCG_EINVAL;
+  XcgPairState* P = nullptr;
+  {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
+    DeviceGuard g(device);
+    const int prc = xcg_pair_state_create((uint32_t)C, disk_bytes, &P);
+    if (prc == -22) return XCG_EINVAL;
+    if (prc) return XCG_ENOMEM;
+  }
+  uint64_t st[4];
+  xcg_pair_state_stats(P, st);
+  const int rc = xcg_ctx_create_ex(device, flags, C + st[3] * 204, out);
+  if (rc != XCG_OK) {
+    DeviceGuard g(device);
+    xcg_pair_state_destroy(P);
+    return rc;
+  }
+  (*out)->pair = P;
+  (*out)->pair_C = (uint32_t)C;
+  return XCG_OK;
+}
+
+int xcg_pair_stats(xcg_ctx* c, uint64_t* st) {
+  if (!c || !c->pair || !st) return XCG_EINVAL;
+  xcg_pair_state_stats(c->pair, st);
+  return XCG_OK;
+}
+
 int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_ctx** out) {
   if (!out || cache_segments == 0 || cache_segments > (1ull << 30)) return XCG_EINVAL;
   *out = nullptr;
@@ -472,6 +508,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   free_dscratch(c->ds);
   window_free(c->own_win);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+  xcg_pair_state_destroy(c->pair);
   delete c;
 }
 
@@ -491,6 +528,7 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (ctx_wait(c) != XCG_OK) return XCG_EHIP;
   // (the LRU clock keeps running: slots keep their last-reference times, which
   // must stay below every later batch's)
+  if (c->pair && xcg_pair_state_clear(c->pair) != 0) return XCG_EHIP;
   return clear_cache(c->g);
 }
 
@@ -617,6 +655,7 @@ int lru_host_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
 
 int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
   if (!c || !seg_out) return XCG_EINVAL;
+  if (c->pair) return XCG_ENOTSUP;
   if (c->bounded) {
     int32_t found = 0;
     const int rc = lru_host_call(c, hash, nullptr, seg_out, 0, &found);
@@ -630,6 +669,7 @@ int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
 
 int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
   if (!c || !seg) return XCG_EINVAL;
+  if (c->pair) return XCG_ENOTSUP;
   if (c->bounded) {
     int32_t found = 0;
     return lru_host_call(c, hash, seg, nullptr, 1, &found);
@@ -643,9 +683,10 @@ int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
 int xcg_last_declarations(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t* h_pos, uint32_t cap,
                           uint32_t* h_count) {
   if (!c || !h_count || !c->bs.decl) return XCG_EINVAL;
-  if (c->bounded) {                                    // rows of the last sub-batch only
-    if (chunk < c->lru.last_base) return XCG_ENOTSUP;
-    chunk -= c->lru.last_base;
+  if (c->bounded || c->pair) {                         // rows of the last sub-batch only
+    const uint32_t base = c->pair ? xcg_pair_state_last_base(c->pair) : c->lru.last_base;
+    if (chunk < base) return XCG_ENOTSUP;
+    chunk -= base;
   }
   if (chunk >= c->bs.n_cap) return XCG_EINVAL;
   DeviceGuard g(c->device);
@@ -663,6 +704,37 @@ int xcg_last_declarations(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t
   for (uint32_t i = 0; i < k; ++i) {
     if (h_hash) h_hash[i] = ((uint64_t)buf[4 * i + 1] << 32) | buf[4 * i];
     if (h_pos) h_pos[i] = buf[4 * i + 2];
+  }
+  return XCG_OK;
+}
+
+int xcg_last_references(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t* h_kind, uint32_t* h_ref,
+                        uint32_t cap, uint32_t* h_count) {
+  if (!c || !h_count) return XCG_EINVAL;
+  if (!(c->bounded || c->pair) || !c->bs.ev) return XCG_ENOTSUP;
+  const uint32_t base = c->pair ? xcg_pair_state_last_base(c->pair) : c->lru.last_base;
+  if (chunk < base) return XCG_ENOTSUP;
+  chunk -= base;
+  if (chunk >= c->bs.n_cap) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  uint32_t ne = 0;
+  if (ctx_wait(c) != XCG_OK || hipMemcpy(&ne, c->bs.nev + chunk, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return XCG_EHIP;
+  if (ne > c->bs.maxe) return XCG_EOVERFLOW;
+  *h_count = ne;
+  std::vector<uint32_t> buf(4ull * ne);
+  if (ne && hipMemcpy(buf.data(), (const uint8_t*)c->bs.ev + 16ull * chunk * c->bs.maxe, 16ull * ne,
+                      hipMemcpyDeviceToHost) != hipSuccess)
+    return XCG_EHIP;
+  std::vector<uint32_t> order(ne);
+  for (uint32_t i = 0; i < ne; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return buf[4 * a + 2] < buf[4 * b + 2]; });
+  const uint32_t k = ne < cap ? ne : cap;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint32_t* e = &buf[4ull * order[j]];
+    if (h_hash) h_hash[j] = ((uint64_t)e[1] << 32) | e[0];
+    if (h_kind) h_kind[j] = e[3] >> 30;          // EV_ENTER 0, EV_HIT 1, EV_GHIT 2, EV_GMISS 3 (xcg_cache.h)
+    if (h_ref) h_ref[j] = e[3] & ((1u << 30) - 1u);
   }
   return XCG_OK;
 }
@@ -727,6 +799,14 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     uint32_t decls = ~0u;
     a.decls_out = &decls;
     int rounds = 0;
+    if (c->pair) {
+      a.ev = c->bs.ev;
+      a.nev = c->bs.nev;
+      a.maxe = c->bs.maxe;
+      rc = xcg_pair_encode_stream(&a, c->pair, &rounds, (hipStream_t)stream);
+      c->last_rounds = rounds;
+      return rc == 0 ? XCG_OK : (rc == -75 ? XCG_EOVERFLOW : (rc == -95 ? XCG_ENOTSUP : XCG_EHIP));
+    }
     if (c->bounded) {
       a.ev = c->bs.ev;
       a.nev = c->bs.nev;
@@ -747,6 +827,7 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
   // A fresh bounded cache per chunk evicts nothing while the chunk's
   // declarations fit the limit (at most max_chunk_len / 2048 of them).
   if (c->bounded && max_chunk_len / XCG_SEGMENT_LENGTH > c->lru.C) return XCG_ENOTSUP;
+  if (c->pair && max_chunk_len / XCG_SEGMENT_LENGTH > c->pair_C) return XCG_ENOTSUP;
   int rc = xcg_launch_encode_independent(d_in, d_chunk_off, d_chunk_len, n, max_chunk_len, c->flags, d_out,
                                          d_out_off, d_out_len, d_stats, c->d_status, (hipStream_t)stream);
   return rc == 0 ? XCG_OK : (rc == -22 ? XCG_EINVAL : XCG_EHIP);
@@ -847,6 +928,7 @@ int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_
   if (h_nunknown) *h_nunknown = 0;
   if (h_total_out) *h_total_out = 0;
   if (n == 0) return XCG_OK;
+  if (c->pair) return XCG_ENOTSUP;
   DeviceGuard g(c->device);
   int rc = ensure_cache(c);
   if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));

@@ -120,6 +120,15 @@ struct LruBatch {
   uint64_t ev_bound;      // upper bound of the batch's references (sizes the scans)
 };
 
+// XCodecCachePair of a bounded memory primary and a disk secondary (xcg_pair.hip).
+struct XcgPairState;
+extern "C" int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out);
+extern "C" void xcg_pair_state_destroy(XcgPairState* P);
+extern "C" int xcg_pair_state_clear(XcgPairState* P);
+extern "C" void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st);
+extern "C" uint32_t xcg_pair_state_last_base(const XcgPairState* P);
+extern "C" int xcg_pair_encode_stream(const XcgStreamArgs* a, XcgPairState* P, int* rounds_out, hipStream_t st);
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);
 extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a, XcgLruState* L, int* rounds_out, hipStream_t st);
 extern "C" int xcg_lru_times(const LruBatch* b, XcgLruState* L, hipStream_t st);

@@ -1,0 +1,860 @@
+// XCodecCachePair (xcodec/xcodec_cache.h:140-237) of a bounded
+// XCodecMemoryCache primary (:245-365, XCodecLRU xcodec/xcodec_lru.h) and an
+// XCodecDisk secondary (xcodec/xcodec_cache_disk.{h,cc}): wanproxy.conf's
+// cache, `memory` + `disk` under a `pair` (programs/wanproxy/wanproxy.conf:
+// 8-26).  Stream-semantics encode batches stay bit-exact with the sequential
+// XCodecEncoder on such a pair.
+//
+// Semantics (restated from the reference):
+//   lookup(h)  primary hit: LRU use, then the disk's touch -- re-enter h if
+//              the disk index lost it (:217-221, xcodec_cache_disk.cc:813-823);
+//              else disk hit: enter h into the primary, evicting its LRU entry
+//              at the limit (:223-227); else miss.
+//   enter(h)   primary enter (may evict) and disk enter (:163-185).
+//   disk       FIFO: entry number e goes to data block e mod nb*204; when an
+//              index block of 204 entries fills, the write head moves to the
+//              next one and the entries written there one lap earlier leave the
+//              index (xcodec_cache_disk.cc:694-741, :327-382).
+// A hash is visible while it is in either level.
+//
+// Division of work.  The GPU parses (encode_stream_kernel, the same rounds as
+// every stream batch) against G = one table over the union of both levels:
+// id s < C = primary slot s, id C + i = disk data block i (a hash in both maps
+// to its primary slot); the pool holds C + nb*204 segments, so `pool + id *
+// 2048` is the hash's bytes either way.  The parse takes, per id, the batch
+// time from which the hash is gone from both levels (ptime) as given and
+// records every cache reference it makes, in order (ENTER / HIT / GHIT /
+// GMISS, xcg_cache.h).  The host replays those references through the pair's
+// exact policy over metadata only (XcgPairState below: the primary's LRU list, the
+// disk ring, the links between them) -- a sequential walk over a few tens of
+// thousands of references -- and checks every recorded lookup against it.
+// All consistent = the sequential encoder's result (by induction over stream
+// time); otherwise the inconsistent chunks are parsed again under the replay's
+// ptime.  An entry a sub-batch made must not leave both levels and then be
+// looked up within it (the parse sees the batch's declarations to its end);
+// the replay detects that and the sub-batch is halved.  The commit then moves bytes on the GPU (input ->
+// new primary / disk slots, disk -> promoted primary slots, primary -> touched
+// disk slots, through a staging copy) and rebuilds G and its probe filters.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "xcg_cache.h"
+#include "xcg_args.h"
+
+namespace xcg {
+
+constexpr uint32_t DISK_ENTRIES = 204;   // XCDFS_ENTRIES_PER_INDEX_BLOCK, xcodec_cache_disk.cc:87
+
+__global__ __launch_bounds__(256) void pair_fill64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// dst[kv[2j]] = kv[2j + 1]
+__global__ __launch_bounds__(256) void pair_scatter64_kernel(uint64_t* dst, const uint64_t* kv, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) dst[kv[2 * j]] = kv[2 * j + 1];
+}
+
+// Seed tiles in a batch table: hash -> earliest (chunk << 32 | position).
+__global__ __launch_bounds__(256) void pair_seed_table_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                              uint32_t maxd, HashTab b, int32_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxd), d = (uint32_t)(i % maxd);
+  if (c >= n || d >= ndecl[c]) return;
+  const uint4 dd = decl[i];
+  if (!tab_insert_min(b, dd.x, dd.y, ((uint64_t)c << 32) | dd.z)) atomicOr(status, 2);
+}
+
+// First guess of a sub-batch's references, before any parse: every chunk
+// parses as its 2048-byte tiling (its cold parse), a tile found in G being a
+// lookup hit, a repeat of an earlier tile of the batch a hit on that
+// declaration, and every other tile a declaration, entered while the window
+// 2048 bytes on (or after the last window) is examined.  One event per tile,
+// in the same row format the parse records.
+__global__ __launch_bounds__(256) void pair_seed_events_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                               uint32_t maxd, const uint32_t* chunk_len, HashTab g,
+                                                               HashTab b, uint4* ev, uint32_t* nev, uint32_t maxe) {
+  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (c >= n) return;
+  const uint32_t nd = min(ndecl[c], maxe), last = chunk_len[c] - SEG;
+  for (uint32_t d = (uint32_t)lane_id(); d < nd; d += 64) {
+    const uint4 dd = decl[(uint64_t)c * maxd + d];
+    const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
+    uint4 e;
+    if (gv != ~0ull) {
+      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, (EV_GHIT << 30) | (uint32_t)gv);
+    } else if (tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z)) {
+      const uint32_t t = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
+      e = make_uint4(dd.x, dd.y, t, (EV_ENTER << 30) | d);
+    } else {
+      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, EV_HIT << 30);
+    }
+    ev[(uint64_t)c * maxe + d] = e;
+  }
+  if (lane_id() == 0) nev[c] = nd;
+}
+
+// Commit moves: w = (destination pool index, kind, a, b); kind 0: the bytes of
+// declaration b of chunk a (input), kind 1: the pre-batch bytes of pool index a
+// (staged first into staging slot b, so no move reads what another overwrote).
+__global__ __launch_bounds__(256) void pair_stage_kernel(const uint4* w, uint32_t nw, const uint8_t* pool,
+                                                         uint8_t* staging) {
+  const uint32_t j = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (j >= nw) return;
+  const uint4 m = w[j];
+  if (m.y != 1u) return;
+  const uint8_t* src = pool + (uint64_t)m.z * SEG;
+  uint8_t* dst = staging + (uint64_t)m.w * SEG;
+  const int l = lane_id();
+  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+}
+
+__global__ __launch_bounds__(256) void pair_move_kernel(const uint4* w, uint32_t nw, const uint8_t* in,
+                                                        const uint64_t* chunk_off, const uint4* decl, uint32_t maxd,
+                                                        const uint8_t* staging, uint8_t* pool) {
+  const uint32_t j = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (j >= nw) return;
+  const uint4 m = w[j];
+  const uint8_t* src = m.y == 0u ? in + chunk_off[m.z] + decl[(uint64_t)m.z * maxd + m.w].z
+                                 : staging + (uint64_t)m.w * SEG;
+  uint8_t* dst = pool + (uint64_t)m.x * SEG;
+  const int l = lane_id();
+  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
+  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+}
+
+struct PairWipe {
+  HashTab g;
+  uint32_t* filt;
+  u32x4* ftab; uint32_t ftab_n;
+  uint32_t* gfilt; uint32_t gfilt_n;
+  uint32_t* nseg;
+};
+__global__ __launch_bounds__(256) void pair_wipe_kernel(PairWipe w) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i <= w.g.mask; i += stride) { w.g.keys[i] = EMPTY_KEY; w.g.vals[i] = ~0ull; }
+  for (uint64_t i = i0; i < FILT_WORDS; i += stride) w.filt[i] = 0u;
+  for (uint64_t i = i0; i < w.ftab_n; i += stride) w.ftab[i] = u32x4{0u, 0u, 0u, 0u};
+  for (uint64_t i = i0; i < w.gfilt_n; i += stride) w.gfilt[i] = 0u;
+  if (i0 == 0) *w.nseg = 0u;
+}
+
+// G from the per-id keys (EMPTY_KEY: no hash there, or a disk block whose hash
+// also sits in the primary), plus the probe filters and the key count.
+__global__ __launch_bounds__(256) void pair_rebuild_kernel(const uint64_t* keyg, uint32_t n, HashTab g, FiltSet fs,
+                                                           uint32_t* nseg, int32_t* status) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t k = id < n ? keyg[id] : EMPTY_KEY;
+  const bool have = k != EMPTY_KEY;
+  if (have) {
+    if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), id)) atomicOr(status, 2);
+    filt_insert(fs, (uint32_t)k, (uint32_t)(k >> 32));
+  }
+  const uint64_t m = ballot(have);
+  if (lane_id() == 0 && m) atomicAdd(nseg, (uint32_t)__builtin_popcountll(m));
+}
+
+}  // namespace xcg
+
+namespace {
+
+using namespace xcg;
+constexpr uint32_t NIL = 0xFFFFFFFFu;
+constexpr uint64_t NEVER = ~0ull;
+constexpr uint64_t NOKEY = ~0ull;
+
+bool pair_debug() {
+  static const bool on = getenv("XCG_PAIR_DEBUG") != nullptr;
+  return on;
+}
+
+// Open-addressed u64 -> u32 map whose slots are tagged with an epoch, so a
+// new pass clears it in O(1).
+struct EpochMap {
+  std::vector<uint64_t> key;
+  std::vector<uint32_t> val, tag;
+  uint64_t mask = 0;
+  uint32_t epoch = 0;
+  void reset(uint64_t want) {
+    uint64_t cap = 1024;
+    while (cap < 2 * want + 16) cap <<= 1;
+    if (cap > key.size()) {
+      key.assign(cap, 0);
+      val.assign(cap, 0);
+      tag.assign(cap, 0);
+      epoch = 0;
+    }
+    mask = key.size() - 1;
+    if (++epoch == 0) {
+      std::fill(tag.begin(), tag.end(), 0u);
+      epoch = 1;
+    }
+  }
+  static uint64_t mixk(uint64_t k) {
+    k ^= k >> 31;
+    k *= 0x9E3779B97F4A7C15ull;
+    return k ^ (k >> 29);
+  }
+  uint32_t find(uint64_t k) const {
+    for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
+      if (tag[i] != epoch) return NIL;
+      if (key[i] == k) return val[i];
+    }
+  }
+  void put(uint64_t k, uint32_t v) {
+    for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
+      if (tag[i] != epoch || key[i] == k) {
+        tag[i] = epoch;
+        key[i] = k;
+        val[i] = v;
+        return;
+      }
+    }
+  }
+};
+
+}  // namespace
+
+// The pair's metadata (host, authoritative) and one replay pass over a
+// sub-batch's references.  Slots: primary s in [0, C), disk data block i in
+// [0, D).  Entities: the hash in primary slot s at the sub-batch start is
+// entity s, a hash only on disk at the start is entity C + i, the pass's own
+// declarations are C + D + k.  A pass never writes the committed arrays: it
+// works on epoch-tagged copies of the slots it touches, which the commit
+// copies back (so an inconsistent pass is dropped for free).
+struct XcgPairState {
+  uint32_t C = 0;                  // primary limit in segments
+  uint64_t nb = 0;                 // disk index blocks
+  uint32_t D = 0;                  // nb * 204 disk data blocks
+  // committed
+  std::vector<uint64_t> pkey;      // hash in primary slot s (NOKEY: free)
+  std::vector<uint32_t> pprev, pnext, pd;   // LRU links; the hash's disk block (NIL: not on disk)
+  uint32_t head = NIL, tail = NIL, pcount = 0, ftop = 0;
+  std::vector<uint32_t> pfree;     // free primary slots, pfree[0 .. ftop)
+  std::vector<uint64_t> dkey;      // hash in disk block i
+  std::vector<uint8_t> dlive;      // block i is the disk index's entry for its hash
+  std::vector<uint32_t> dp;        // the hash's primary slot (NIL: disk only)
+  uint64_t dclock = 0;             // disk entries written
+  uint64_t dcount = 0;             // live disk index entries
+  // pass overlay
+  uint32_t epoch = 0;
+  std::vector<uint32_t> ps_ep, ds_ep;
+  std::vector<uint64_t> o_pkey, o_dkey;
+  std::vector<uint32_t> o_pprev, o_pnext, o_pd, o_powner, o_dp, o_downer;
+  std::vector<uint8_t> o_dlive, o_dapp;
+  std::vector<uint32_t> touchedP, touchedD;
+  uint32_t s_head, s_tail, s_pcount, s_ftop;
+  uint64_t s_dclock, s_dcount;
+  // entities
+  std::vector<uint32_t> e_ep, e_p, e_d;
+  std::vector<uint8_t> e_ref;
+  std::vector<uint64_t> e_leave;
+  std::vector<uint32_t> touchedE;
+  std::vector<uint64_t> n_key;     // the pass's declarations
+  std::vector<uint32_t> n_p, n_d, n_chunk, n_decl;
+  EpochMap bmap;                   // hash -> the pass's declaration
+  // pass results
+  bool split = false;
+  std::vector<uint8_t> bad;        // per chunk: a recorded lookup the replay contradicts
+  std::vector<uint4> writes;       // commit moves (dest, kind, a, b)
+  uint32_t nstaged = 0;
+  uint64_t enters = 0, refs = 0, appends = 0;
+  // device
+  uint64_t* d_keyg = nullptr;      // [C + D]
+  uint64_t* d_ptime = nullptr;     // [C + D]
+  uint8_t* d_staging = nullptr;
+  uint64_t staging_cap = 0;
+  uint8_t* d_xfer = nullptr;       // upload area (moves, key updates, ptime list)
+  uint64_t xfer_cap = 0;
+  uint8_t* h_xfer = nullptr;       // pinned
+  uint64_t h_xfer_cap = 0;
+  uint4* h_ev = nullptr;           // pinned copy of the reference rows
+  uint64_t h_ev_cap = 0;
+  uint32_t* h_nev = nullptr;
+  uint32_t h_nev_cap = 0;
+  uint32_t* h_need = nullptr;
+  uint32_t last_base = 0;
+
+  uint32_t ids() const { return C + D; }
+
+  // ---- overlay access
+  void ptouch(uint32_t s) {
+    if (ps_ep[s] == epoch) return;
+    ps_ep[s] = epoch;
+    o_pkey[s] = pkey[s];
+    o_pprev[s] = pprev[s];
+    o_pnext[s] = pnext[s];
+    o_pd[s] = pd[s];
+    o_powner[s] = pkey[s] != NOKEY ? s : NIL;
+    touchedP.push_back(s);
+  }
+  void dtouch(uint32_t i) {
+    if (ds_ep[i] == epoch) return;
+    ds_ep[i] = epoch;
+    o_dkey[i] = dkey[i];
+    o_dlive[i] = dlive[i];
+    o_dp[i] = dp[i];
+    o_dapp[i] = 0;
+    o_downer[i] = dlive[i] ? (dp[i] != NIL ? dp[i] : C + i) : NIL;
+    touchedD.push_back(i);
+  }
+  void etouch(uint32_t x) {
+    if (e_ep[x] == epoch) return;
+    e_ep[x] = epoch;
+    if (x < C) {
+      e_p[x] = pkey[x] != NOKEY ? x : NIL;
+      e_d[x] = e_p[x] != NIL ? pd[x] : NIL;
+    } else {
+      const uint32_t i = x - C;
+      e_p[x] = NIL;
+      e_d[x] = dlive[i] && dp[i] == NIL ? i : NIL;
+    }
+    e_ref[x] = 0;
+    e_leave[x] = NEVER;
+    touchedE.push_back(x);
+  }
+  bool is_new(uint32_t x) const { return x >= C + D; }
+  // an entity's current primary slot / disk block (a persistent one's record
+  // is initialised from the sub-batch start on first use)
+  uint32_t& ep(uint32_t x) {
+    if (is_new(x)) return n_p[x - C - D];
+    etouch(x);
+    return e_p[x];
+  }
+  uint32_t& ed(uint32_t x) {
+    if (is_new(x)) return n_d[x - C - D];
+    etouch(x);
+    return e_d[x];
+  }
+  uint64_t ekey(uint32_t x) const { return is_new(x) ? n_key[x - C - D] : (x < C ? pkey[x] : dkey[x - C]); }
+  // commit move of entity x's bytes to pool index `dest`
+  void move_to(uint32_t dest, uint32_t x) {
+    if (is_new(x)) writes.push_back(make_uint4(dest, 0u, n_chunk[x - C - D], n_decl[x - C - D]));
+    else writes.push_back(make_uint4(dest, 1u, x, nstaged++));
+  }
+  // x is in neither level from time t on.  A cached entry's departure becomes
+  // its ptime; one this sub-batch made has no ptime (the parse sees the batch's
+  // declarations to its end), so a later lookup of it splits the sub-batch.
+  void left(uint32_t x, uint64_t t) {
+    if (is_new(x)) return;
+    etouch(x);
+    e_leave[x] = t;
+  }
+
+  // ---- the primary's LRU list (xcodec_lru.h: enter / use move to the tail, evict takes the head)
+  void unlink(uint32_t s) {
+    const uint32_t p = o_pprev[s], q = o_pnext[s];
+    if (p != NIL) { ptouch(p); o_pnext[p] = q; } else s_head = q;
+    if (q != NIL) { ptouch(q); o_pprev[q] = p; } else s_tail = p;
+  }
+  void append(uint32_t s) {
+    o_pprev[s] = s_tail;
+    o_pnext[s] = NIL;
+    if (s_tail != NIL) { ptouch(s_tail); o_pnext[s_tail] = s; } else s_head = s;
+    s_tail = s;
+  }
+
+  // XCodecMemoryCache::enter (xcodec_cache.h:303-325)
+  void p_enter(uint32_t x, uint64_t t) {
+    uint32_t s;
+    if (s_pcount == C) {
+      s = s_head;
+      ptouch(s);
+      const uint32_t y = o_powner[s];
+      unlink(s);
+      --s_pcount;
+      ep(y) = NIL;
+      const uint32_t dj = o_pd[s];
+      if (dj != NIL) { dtouch(dj); o_dp[dj] = NIL; }    // now on disk only
+      else left(y, t);
+    } else {
+      s = pfree[--s_ftop];
+      ptouch(s);
+    }
+    o_pkey[s] = ekey(x);
+    o_powner[s] = x;
+    ep(x) = s;
+    append(s);
+    ++s_pcount;
+    const uint32_t dj = ed(x);
+    o_pd[s] = dj;
+    if (dj != NIL) { dtouch(dj); o_dp[dj] = s; }
+    move_to(s, x);
+    ++enters;
+  }
+
+  // XCodecDisk::enter (xcodec_cache_disk.cc:694-741)
+  void d_append(uint32_t x, uint64_t t) {
+    const uint32_t i = (uint32_t)(s_dclock % D);
+    dtouch(i);
+    o_dkey[i] = ekey(x);
+    o_dlive[i] = 1;
+    o_dapp[i] = 1;
+    o_downer[i] = x;
+    const uint32_t p = ep(x);
+    o_dp[i] = p;
+    if (p != NIL) { ptouch(p); o_pd[p] = i; }
+    ed(x) = i;
+    move_to(C + i, x);
+    ++s_dcount;
+    ++appends;
+    if (++s_dclock % DISK_ENTRIES == 0) {          // the write head moves on: index_invalidate_entries
+      const uint64_t b = (s_dclock / DISK_ENTRIES) % nb;
+      for (uint32_t j = (uint32_t)(b * DISK_ENTRIES); j < (uint32_t)((b + 1) * DISK_ENTRIES); ++j) {
+        dtouch(j);
+        if (!o_dlive[j]) continue;
+        const uint32_t y = o_downer[j];
+        o_dlive[j] = 0;
+        o_downer[j] = NIL;
+        --s_dcount;
+        ed(y) = NIL;
+        const uint32_t q = o_dp[j];
+        if (q != NIL) { ptouch(q); o_pd[q] = NIL; }  // now in the primary only
+        else left(y, t);
+      }
+    }
+  }
+
+  // XCodecCachePair::lookup on a hash present in a level (:208-230)
+  void lookup(uint32_t x, uint64_t t) {
+    if (!is_new(x) && !e_ref[x]) {
+      e_ref[x] = 1;
+      ++refs;                                      // distinct persistent entries referenced
+    }
+    const uint32_t p = ep(x);
+    if (p != NIL) {
+      ptouch(p);
+      if (s_tail != p) { unlink(p); append(p); }   // XCodecLRU::use
+      if (ed(x) == NIL) d_append(x, t);            // XCodecDisk::touch
+    } else {
+      p_enter(x, t);                               // promotion
+    }
+  }
+
+  // One replay pass over chunks [0, n) of the sub-batch: rows ev[c * maxe ..],
+  // nev[c].  Returns false if the pass is not the sequential one (bad[] and
+  // split tell why).
+  bool replay(uint32_t n, const uint4* ev, const uint32_t* nev, uint32_t maxe, uint32_t maxd) {
+    if (++epoch == 0) {
+      std::fill(ps_ep.begin(), ps_ep.end(), 0u);
+      std::fill(ds_ep.begin(), ds_ep.end(), 0u);
+      std::fill(e_ep.begin(), e_ep.end(), 0u);
+      epoch = 1;
+    }
+    touchedP.clear();
+    touchedD.clear();
+    touchedE.clear();
+    n_key.clear(); n_p.clear(); n_d.clear(); n_chunk.clear(); n_decl.clear();
+    bmap.reset((uint64_t)n * maxd);
+    writes.clear();
+    nstaged = 0;
+    enters = refs = appends = 0;
+    split = false;
+    bad.assign(n, 0);
+    s_head = head; s_tail = tail; s_pcount = pcount; s_ftop = ftop; s_dclock = dclock; s_dcount = dcount;
+    std::vector<uint32_t> order;
+    bool ok = true;
+    for (uint32_t c = 0; c < n && !split; ++c) {
+      const uint32_t cnt = nev[c];
+      if (cnt > maxe) { split = true; break; }     // (reference list overflow: a smaller sub-batch)
+      const uint4* r = ev + (uint64_t)c * maxe;
+      // rows are in stream order; a stable sort by time guards it
+      order.resize(cnt);
+      for (uint32_t k = 0; k < cnt; ++k) order[k] = k;
+      bool sorted = true;
+      for (uint32_t k = 1; k < cnt; ++k) sorted &= r[k - 1].z <= r[k].z;
+      if (!sorted) std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return r[a].z < r[b].z; });
+      for (uint32_t k = 0; k < cnt && !split; ++k) {
+        const uint4 e = r[order[k]];
+        const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+        const uint64_t t = ((uint64_t)c << 21) | e.z;
+        const uint64_t h = ((uint64_t)e.y << 32) | e.x;
+        if (kind == EV_GHIT || kind == EV_GMISS) {
+          if (ref >= C + D) { bad[c] = 1; ok = false; continue; }
+          etouch(ref);
+          const bool present = e_p[ref] != NIL || e_d[ref] != NIL;
+          if (present != (kind == EV_GHIT)) { bad[c] = 1; ok = false; }
+          if (present) lookup(ref, t);
+        } else if (kind == EV_HIT) {
+          const uint32_t x = bmap.find(h);
+          if (x == NIL) { bad[c] = 1; ok = false; continue; }
+          if (ep(x) == NIL && ed(x) == NIL) { split = true; break; }   // made here, gone already
+          lookup(x, t);
+        } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
+          const uint32_t x0 = bmap.find(h);
+          if (x0 != NIL && (ep(x0) != NIL || ed(x0) != NIL)) { bad[c] = 1; ok = false; continue; }
+          const uint32_t x = C + D + (uint32_t)n_key.size();
+          n_key.push_back(h); n_p.push_back(NIL); n_d.push_back(NIL); n_chunk.push_back(c); n_decl.push_back(ref);
+          bmap.put(h, x);
+          p_enter(x, t);
+          d_append(x, t);
+        }
+      }
+    }
+    return ok && !split;
+  }
+
+  // Keep the pass: overlay -> committed.
+  void keep() {
+    for (uint32_t s : touchedP) {
+      pkey[s] = o_pkey[s]; pprev[s] = o_pprev[s]; pnext[s] = o_pnext[s]; pd[s] = o_pd[s];
+    }
+    for (uint32_t i : touchedD) {
+      dkey[i] = o_dkey[i]; dlive[i] = o_dlive[i]; dp[i] = o_dp[i];
+    }
+    head = s_head; tail = s_tail; pcount = s_pcount; ftop = s_ftop; dclock = s_dclock; dcount = s_dcount;
+  }
+};
+
+namespace {
+
+unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
+
+int ensure_dev(uint8_t** p, uint64_t* cap, uint64_t want) {
+  if (*cap >= want) return 0;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, want) != hipSuccess) return -5;
+  *cap = want;
+  return 0;
+}
+int ensure_pinned(uint8_t** p, uint64_t* cap, uint64_t want) {
+  if (*cap >= want) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipHostMalloc(p, want) != hipSuccess) return -5;
+  *cap = want;
+  return 0;
+}
+
+// Upload `bytes` from the pinned transfer area to the device one (offset o).
+int upload(XcgPairState* P, uint64_t o, uint64_t bytes, hipStream_t st) {
+  if (!bytes) return 0;
+  return hipMemcpyAsync(P->d_xfer + o, P->h_xfer + o, bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -5;
+}
+
+// ptime for the next parse: NEVER everywhere, then the replay's departures.
+int upload_ptime(XcgPairState* P, hipStream_t st) {
+  const uint32_t ids = P->ids();
+  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)ids, NEVER);
+  uint64_t* kv = (uint64_t*)P->h_xfer;
+  uint32_t m = 0;
+  for (uint32_t x : P->touchedE)
+    if (P->e_leave[x] != NEVER) {
+      kv[2 * m] = x;
+      kv[2 * m + 1] = P->e_leave[x];
+      ++m;
+    }
+  if (m) {
+    if (upload(P, 0, 16ull * m, st)) return -5;
+    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_ptime,
+                       (const uint64_t*)P->d_xfer, m);
+  }
+  // (the pinned area is reused by the next upload only after a stream sync)
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -5;
+}
+
+// The reference rows of a sub-batch, to the host.
+int download_refs(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
+  const uint64_t rows = (uint64_t)a.n * a.maxe;
+  if (P->h_ev_cap < rows) {
+    if (P->h_ev) (void)hipHostFree(P->h_ev);
+    P->h_ev = nullptr;
+    P->h_ev_cap = 0;
+    if (hipHostMalloc(&P->h_ev, 16 * rows) != hipSuccess) return -5;
+    P->h_ev_cap = rows;
+  }
+  if (P->h_nev_cap < a.n) {
+    if (P->h_nev) (void)hipHostFree(P->h_nev);
+    if (P->h_need) (void)hipHostFree(P->h_need);
+    P->h_nev = P->h_need = nullptr;
+    P->h_nev_cap = 0;
+    if (hipHostMalloc(&P->h_nev, 4ull * a.n) != hipSuccess || hipHostMalloc(&P->h_need, 4ull * a.n) != hipSuccess)
+      return -5;
+    P->h_nev_cap = a.n;
+  }
+  if (hipMemcpyAsync(P->h_nev, a.nev, 4ull * a.n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(P->h_ev, a.ev, 16 * rows, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return -5;
+  return 0;
+}
+
+// XCodecHash::hash of one segment (xcodec/xcodec_hash.h:166-174), host side,
+// for the XCG_PAIR_VERIFY diagnostics.
+uint64_t host_hash(const uint8_t* w) {
+  uint32_t s1 = 0, s2 = 0, b1 = 0, b2 = 0;
+  for (int k = 0; k < SEG; ++k) {
+    s1 += (uint32_t)w[k] + 1u;
+    s2 += s1;
+    b1 += w[k] ? (uint32_t)__builtin_ctz(w[k]) + 1u : 0u;
+    b2 += b1;
+  }
+  const uint32_t bits = (b1 << 16) + b2, bytes = (s1 << 20) + s2;
+  return ((uint64_t)bits << 36) + (uint64_t)bytes;
+}
+
+// Diagnostics (XCG_PAIR_VERIFY): every primary slot and live disk block holds
+// bytes of its hash, and G finds every level entry.
+void pair_verify(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
+  const uint64_t ids = P->ids();
+  std::vector<uint8_t> pool(ids * SEG);
+  std::vector<uint64_t> keyg(ids);
+  (void)hipStreamSynchronize(st);
+  (void)hipMemcpy(pool.data(), a.pool, ids * SEG, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(keyg.data(), P->d_keyg, 8 * ids, hipMemcpyDeviceToHost);
+  uint32_t bad = 0;
+  for (uint32_t s = 0; s < P->C; ++s) {
+    if (P->pkey[s] == NOKEY) continue;
+    if (host_hash(&pool[(uint64_t)s * SEG]) != P->pkey[s] && bad++ < 5)
+      fprintf(stderr, "pair verify: primary slot %u bytes do not hash to its key\n", s);
+    if (keyg[s] != P->pkey[s] && bad++ < 5) fprintf(stderr, "pair verify: keyg[%u] stale\n", s);
+  }
+  for (uint32_t i = 0; i < P->D; ++i) {
+    if (!P->dlive[i]) continue;
+    if (host_hash(&pool[((uint64_t)P->C + i) * SEG]) != P->dkey[i] && bad++ < 5)
+      fprintf(stderr, "pair verify: disk block %u bytes do not hash to its key\n", i);
+    const uint64_t want = P->dp[i] == NIL ? P->dkey[i] : NOKEY;
+    if (keyg[P->C + i] != want && bad++ < 5) fprintf(stderr, "pair verify: keyg[C+%u] stale\n", i);
+    if (P->dp[i] != NIL && P->pkey[P->dp[i]] != P->dkey[i] && bad++ < 5)
+      fprintf(stderr, "pair verify: disk block %u links slot %u of another hash\n", i, P->dp[i]);
+  }
+  for (uint32_t s = 0; s < P->C; ++s)
+    if (P->pkey[s] != NOKEY && P->pd[s] != NIL && (P->dkey[P->pd[s]] != P->pkey[s] || !P->dlive[P->pd[s]]) &&
+        bad++ < 5)
+      fprintf(stderr, "pair verify: slot %u links disk block %u of another hash\n", s, P->pd[s]);
+  fprintf(stderr, "pair verify: %u problems (primary %u, disk live %llu)\n", bad, P->pcount,
+          (unsigned long long)P->dcount);
+}
+
+// Commit a kept pass on the GPU: bytes, per-id keys, G and its filters.
+int pair_commit(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
+  // A primary slot can change hands more than once in a sub-batch (an entry
+  // evicted to disk frees it again), and a small disk can lap within one:
+  // only the last move into each destination stays.  (Sources are the input or
+  // pre-sub-batch bytes, staged before any move.)
+  {
+    std::vector<uint4>& w = P->writes;
+    std::vector<uint8_t> seen(P->ids(), 0);
+    size_t k = w.size();
+    for (size_t j = w.size(); j-- > 0;) {
+      if (seen[w[j].x]) continue;
+      seen[w[j].x] = 1;
+      w[--k] = w[j];
+    }
+    w.erase(w.begin(), w.begin() + (ptrdiff_t)k);
+  }
+  const uint32_t nw = (uint32_t)P->writes.size();
+  // per-id key updates for every slot the pass touched
+  std::vector<uint64_t> kv;
+  kv.reserve(2 * (P->touchedP.size() + P->touchedD.size()));
+  for (uint32_t s : P->touchedP) {
+    kv.push_back(s);
+    kv.push_back(P->pkey[s]);
+  }
+  for (uint32_t i : P->touchedD) {
+    kv.push_back((uint64_t)P->C + i);
+    kv.push_back(P->dlive[i] && P->dp[i] == NIL ? P->dkey[i] : NOKEY);
+  }
+  const uint32_t nk = (uint32_t)(kv.size() / 2);
+  const uint64_t wbytes = 16ull * nw, kbytes = 8ull * kv.size();
+  if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, wbytes + kbytes + 16) ||
+      ensure_dev(&P->d_xfer, &P->xfer_cap, wbytes + kbytes + 16) ||
+      ensure_dev(&P->d_staging, &P->staging_cap, (uint64_t)(P->nstaged ? P->nstaged : 1) * SEG))
+    return -5;
+  memcpy(P->h_xfer, P->writes.data(), wbytes);
+  memcpy(P->h_xfer + wbytes, kv.data(), kbytes);
+  if (upload(P, 0, wbytes + kbytes, st)) return -5;
+  const uint4* w = (const uint4*)P->d_xfer;
+  if (nw) {
+    hipLaunchKernelGGL(pair_stage_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, (const uint8_t*)a.pool,
+                       P->d_staging);
+    hipLaunchKernelGGL(pair_move_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, a.in, a.chunk_off,
+                       (const uint4*)a.decl, a.maxd, (const uint8_t*)P->d_staging, a.pool);
+  }
+  if (nk)
+    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(nk)), dim3(256), 0, st, P->d_keyg,
+                       (const uint64_t*)(P->d_xfer + wbytes), nk);
+  const HashTab g{a.g_keys, a.g_vals, a.g_mask};
+  PairWipe wp{g, a.g_filt, (u32x4*)a.g_ftab, a.fmask + 1, a.g_gfilt, a.gmask + 1, a.nseg};
+  hipLaunchKernelGGL(pair_wipe_kernel, dim3(1024), dim3(256), 0, st, wp);
+  const uint32_t ids = P->ids();
+  hipLaunchKernelGGL(pair_rebuild_kernel, dim3(grid_for(ids)), dim3(256), 0, st, (const uint64_t*)P->d_keyg, ids, g,
+                     FiltSet{a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask}, a.nseg, a.status);
+  // (the pinned transfer area is free again once the stream passes here)
+  return hipStreamSynchronize(st) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out) {
+  const uint64_t blocks = disk_bytes / SEG;
+  if (C == 0 || blocks <= 18) return -22;
+  const uint64_t nb = (blocks - 18) / (1 + DISK_ENTRIES);   // xcodec_cache_disk.cc:110-111
+  if (nb == 0 || nb * DISK_ENTRIES + C >= (1ull << 30)) return -22;
+  XcgPairState* P = new XcgPairState;
+  P->C = C;
+  P->nb = nb;
+  P->D = (uint32_t)(nb * DISK_ENTRIES);
+  const uint32_t D = P->D, ids = C + D;
+  P->pkey.assign(C, NOKEY);
+  P->pprev.assign(C, NIL);
+  P->pnext.assign(C, NIL);
+  P->pd.assign(C, NIL);
+  P->pfree.resize(C);
+  for (uint32_t s = 0; s < C; ++s) P->pfree[s] = C - 1 - s;   // slot 0 first
+  P->ftop = C;
+  P->dkey.assign(D, NOKEY);
+  P->dlive.assign(D, 0);
+  P->dp.assign(D, NIL);
+  P->ps_ep.assign(C, 0);
+  P->ds_ep.assign(D, 0);
+  P->o_pkey.resize(C); P->o_pprev.resize(C); P->o_pnext.resize(C); P->o_pd.resize(C); P->o_powner.resize(C);
+  P->o_dkey.resize(D); P->o_dlive.resize(D); P->o_dapp.resize(D); P->o_dp.resize(D); P->o_downer.resize(D);
+  P->e_ep.assign(ids, 0);
+  P->e_p.resize(ids); P->e_d.resize(ids); P->e_ref.resize(ids); P->e_leave.resize(ids);
+  if (hipMalloc(&P->d_keyg, 8ull * ids) != hipSuccess || hipMalloc(&P->d_ptime, 8ull * ids) != hipSuccess ||
+      hipMemset(P->d_keyg, 0xFF, 8ull * ids) != hipSuccess || hipMemset(P->d_ptime, 0xFF, 8ull * ids) != hipSuccess) {
+    (void)hipFree(P->d_keyg);
+    (void)hipFree(P->d_ptime);
+    delete P;
+    return -12;
+  }
+  *out = P;
+  return 0;
+}
+
+void xcg_pair_state_destroy(XcgPairState* P) {
+  if (!P) return;
+  (void)hipFree(P->d_keyg); (void)hipFree(P->d_ptime); (void)hipFree(P->d_staging); (void)hipFree(P->d_xfer);
+  if (P->h_xfer) (void)hipHostFree(P->h_xfer);
+  if (P->h_ev) (void)hipHostFree(P->h_ev);
+  if (P->h_nev) (void)hipHostFree(P->h_nev);
+  if (P->h_need) (void)hipHostFree(P->h_need);
+  delete P;
+}
+
+// Drop everything (XCodecCache objects have no clear; this is a fresh pair on
+// an empty volume).  The caller wipes G itself.
+int xcg_pair_state_clear(XcgPairState* P) {
+  std::fill(P->pkey.begin(), P->pkey.end(), NOKEY);
+  std::fill(P->pprev.begin(), P->pprev.end(), NIL);
+  std::fill(P->pnext.begin(), P->pnext.end(), NIL);
+  std::fill(P->pd.begin(), P->pd.end(), NIL);
+  for (uint32_t s = 0; s < P->C; ++s) P->pfree[s] = P->C - 1 - s;
+  P->ftop = P->C;
+  P->head = P->tail = NIL;
+  P->pcount = 0;
+  std::fill(P->dkey.begin(), P->dkey.end(), NOKEY);
+  std::fill(P->dlive.begin(), P->dlive.end(), 0);
+  std::fill(P->dp.begin(), P->dp.end(), NIL);
+  P->dclock = P->dcount = 0;
+  return hipMemset(P->d_keyg, 0xFF, 8ull * P->ids()) == hipSuccess ? 0 : -5;
+}
+
+void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st) {
+  st[0] = P->pcount;
+  st[1] = P->dcount;
+  st[2] = P->dclock;
+  st[3] = P->nb;
+}
+
+uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; }
+
+// Stream-semantics encode of a batch on the pair, in sub-batches (see the top
+// of this file).  Returns 0, -75 (no consistent pass / overflow), -95 (one
+// chunk alone exceeds what a sub-batch may hold), -5.
+int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds_out, hipStream_t st) {
+  const uint32_t n = a0->n;
+  int rounds = 0;
+  uint32_t per = P->C / a0->maxd ? P->C / a0->maxd : 1u;
+  constexpr int MAX_PASSES = 12;
+  uint32_t i0 = 0;
+  while (i0 < n) {
+    const uint32_t m = per < n - i0 ? per : n - i0;
+    XcgStreamArgs a = *a0;
+    a.n = m;
+    a.chunk_off += i0;
+    a.chunk_len += i0;
+    a.out_off += i0;
+    a.out_len += i0;
+    if (a.stats) a.stats += 4ull * i0;
+    a.ptime = P->d_ptime;
+    a.no_commit = 1;
+    // first guess: the tiling seed's references, replayed
+    if (xcg_launch_seed_tiling(&a, st)) return -5;
+    const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};
+    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, (uint64_t)b.mask + 1, NOKEY);
+    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
+    hipLaunchKernelGGL(pair_seed_table_kernel, dim3(grid_for((uint64_t)m * a.maxd)), dim3(256), 0, st, m,
+                       (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
+    hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
+                       (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe);
+    if (download_refs(P, a, st)) return -5;
+    (void)P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
+    if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
+        ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
+      return -5;
+    bool done = false, split = false;
+    for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
+      a.keep_decls = 1;
+      a.need_given = pass > 0;
+      int r = 0;
+      const int rc = xcg_launch_encode_stream(&a, &r, st);
+      rounds += r;
+      if (rc) return rc;
+      if (download_refs(P, a, st)) return -5;
+      const bool ok = P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
+      uint32_t nbad = 0;
+      for (uint32_t c = 0; c < m; ++c) nbad += P->bad[c];
+      if (pair_debug())
+        fprintf(stderr, "pair: chunks %u+%u pass %d rounds %d enters %llu refs %llu appends %llu bad %u split %d\n",
+                i0, m, pass, r, (unsigned long long)P->enters, (unsigned long long)P->refs,
+                (unsigned long long)P->appends, nbad, (int)P->split);
+      if (P->split) split = true;
+      else if (ok) done = true;
+      else {
+        for (uint32_t c = 0; c < m; ++c) P->h_need[c] = P->bad[c];
+        if (hipMemcpyAsync(a.need, P->h_need, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess) return -5;
+        if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
+            ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
+          return -5;
+      }
+    }
+    if (!done) {
+      if (m == 1) return split ? -95 : -75;
+      per = m / 2;                                 // redo this part in halves
+      continue;
+    }
+    P->keep();
+    if (pair_commit(P, a, st)) return -5;
+    if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, a, st);
+    // the next sub-batch starts with every hash visible to its end
+    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+    P->last_base = i0;
+    i0 += m;
+    // size the next sub-batch from what this one used of each level
+    const uint64_t useP = P->enters + P->refs, useD = P->appends;
+    uint64_t want = (uint64_t)n;
+    if (useP) want = std::min<uint64_t>(want, (uint64_t)P->C * 9 / 10 * m / useP);
+    if (useD && P->D > 2 * DISK_ENTRIES) want = std::min<uint64_t>(want, (uint64_t)(P->D - 2 * DISK_ENTRIES) * 9 / 10 * m / useD);
+    per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
+  }
+  if (rounds_out) *rounds_out = rounds;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // extern "C"

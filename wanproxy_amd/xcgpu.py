@@ -71,6 +71,12 @@ def lib():
     L.xcg_ctx_create_ex.restype = C.c_int
     L.xcg_ctx_create_bounded.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_bounded.restype = C.c_int
+    L.xcg_ctx_create_pair.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_pair.restype = C.c_int
+    L.xcg_pair_stats.argtypes = [vp, vp]
+    L.xcg_pair_stats.restype = C.c_int
+    L.xcg_ctx_flags.argtypes = [vp, vp]
+    L.xcg_ctx_flags.restype = C.c_int
     L.xcg_cache_size.argtypes = [vp]
     L.xcg_cache_size.restype = C.c_uint64
     L.xcg_cache_clear.argtypes = [vp]
@@ -139,17 +145,21 @@ class Context:
     """An XCodecEncoder + cache configuration bound to one GPU."""
 
     def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
-                 cache_segments: int = 1 << 19, memory_cache_limit: int = 0):
+                 cache_segments: int = 1 << 19, memory_cache_limit: int = 0, disk_bytes: int = 0):
         """memory_cache_limit (bytes): the bounded, LRU-evicting cache
         XCodecMemoryCache(uuid, memory_cache_limit) (xcodec/xcodec_cache.h:277)
-        instead of an unbounded one of cache_segments capacity."""
+        instead of an unbounded one of cache_segments capacity.  With
+        disk_bytes too: wanproxy.conf's XCodecCachePair of that memory cache
+        and a disk of disk_bytes (xcodec/xcodec_cache.h:140-237)."""
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        if memory_cache_limit:
+        if disk_bytes:
+            _check(lib().xcg_ctx_create_pair(device, self.flags, int(memory_cache_limit), int(disk_bytes), C.byref(h)))
+        elif memory_cache_limit:
             _check(lib().xcg_ctx_create_bounded(device, self.flags, int(memory_cache_limit), C.byref(h)))
         else:
             _check(lib().xcg_ctx_create_ex(device, self.flags, int(cache_segments), C.byref(h)))
@@ -173,6 +183,13 @@ class Context:
         """enter (or replace the bytes of) one segment -- XCodecPipePair's <LEARN>."""
         assert len(seg) == 2048
         _check(lib().xcg_cache_enter_host(self.h, C.c_uint64(h), (C.c_uint8 * 2048).from_buffer_copy(seg)))
+
+    def pair_stats(self):
+        """(primary entries, disk index entries, disk entries written, disk
+        index blocks) of a pair context."""
+        st = (C.c_uint64 * 4)()
+        _check(lib().xcg_pair_stats(self.h, st))
+        return tuple(int(v) for v in st)
 
     def cache_clear(self):
         _check(lib().xcg_cache_clear(self.h))
