@@ -42,6 +42,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "xcg_cache.h"
@@ -178,24 +179,25 @@ bool pair_debug() {
 }
 
 // Open-addressed u64 -> u32 map whose slots are tagged with an epoch, so a
-// new pass clears it in O(1).
+// new pass clears it in O(1); one 16-byte slot per probe.
 struct EpochMap {
-  std::vector<uint64_t> key;
-  std::vector<uint32_t> val, tag;
+  struct Slot {
+    uint64_t key;
+    uint32_t val, tag;
+  };
+  std::vector<Slot> t;
   uint64_t mask = 0;
   uint32_t epoch = 0;
   void reset(uint64_t want) {
     uint64_t cap = 1024;
     while (cap < 2 * want + 16) cap <<= 1;
-    if (cap > key.size()) {
-      key.assign(cap, 0);
-      val.assign(cap, 0);
-      tag.assign(cap, 0);
+    if (cap > t.size()) {
+      t.assign(cap, Slot{0, 0, 0});
       epoch = 0;
     }
-    mask = key.size() - 1;
+    mask = t.size() - 1;
     if (++epoch == 0) {
-      std::fill(tag.begin(), tag.end(), 0u);
+      for (Slot& q : t) q.tag = 0;
       epoch = 1;
     }
   }
@@ -204,18 +206,21 @@ struct EpochMap {
     k *= 0x9E3779B97F4A7C15ull;
     return k ^ (k >> 29);
   }
+  void prefetch(uint64_t k) const { __builtin_prefetch(&t[mixk(k) & mask]); }
   uint32_t find(uint64_t k) const {
     for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
-      if (tag[i] != epoch) return NIL;
-      if (key[i] == k) return val[i];
+      const Slot& q = t[i];
+      if (q.tag != epoch) return NIL;
+      if (q.key == k) return q.val;
     }
   }
   void put(uint64_t k, uint32_t v) {
     for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
-      if (tag[i] != epoch || key[i] == k) {
-        tag[i] = epoch;
-        key[i] = k;
-        val[i] = v;
+      Slot& q = t[i];
+      if (q.tag != epoch || q.key == k) {
+        q.tag = epoch;
+        q.key = k;
+        q.val = v;
         return;
       }
     }
@@ -231,36 +236,49 @@ struct EpochMap {
 // declarations are C + D + k.  A pass never writes the committed arrays: it
 // works on epoch-tagged copies of the slots it touches, which the commit
 // copies back (so an inconsistent pass is dropped for free).
+// One primary slot / disk block / entity record each in one cache line:
+// the committed fields, then the pass's copy (valid while ep == the pass's
+// epoch).
+struct PSlot {
+  uint64_t key, okey;              // hash (NOKEY: free)
+  uint32_t prev, next, pd;         // LRU links; the hash's disk block (NIL: not on disk)
+  uint32_t oprev, onext, opd, owner, ep;
+};
+struct DSlot {
+  uint64_t key, okey;
+  uint32_t dp, odp;                // the hash's primary slot (NIL: disk only)
+  uint32_t owner, ep;
+  uint8_t live, olive;             // the disk index's entry for its hash
+};
+struct Ent {                       // a hash cached at the sub-batch start
+  uint64_t leave;                  // time it left both levels (NEVER)
+  uint32_t ep, p, d;
+  uint8_t ref;
+};
+struct NewEnt {                    // a declaration of the pass
+  uint64_t key;
+  uint32_t p, d, chunk, decl;
+};
+
 struct XcgPairState {
   uint32_t C = 0;                  // primary limit in segments
   uint64_t nb = 0;                 // disk index blocks
   uint32_t D = 0;                  // nb * 204 disk data blocks
-  // committed
-  std::vector<uint64_t> pkey;      // hash in primary slot s (NOKEY: free)
-  std::vector<uint32_t> pprev, pnext, pd;   // LRU links; the hash's disk block (NIL: not on disk)
+  // committed scalars
   uint32_t head = NIL, tail = NIL, pcount = 0, ftop = 0;
   std::vector<uint32_t> pfree;     // free primary slots, pfree[0 .. ftop)
-  std::vector<uint64_t> dkey;      // hash in disk block i
-  std::vector<uint8_t> dlive;      // block i is the disk index's entry for its hash
-  std::vector<uint32_t> dp;        // the hash's primary slot (NIL: disk only)
   uint64_t dclock = 0;             // disk entries written
   uint64_t dcount = 0;             // live disk index entries
-  // pass overlay
+  std::vector<PSlot> ps;
+  std::vector<DSlot> ds;
+  // pass state
   uint32_t epoch = 0;
-  std::vector<uint32_t> ps_ep, ds_ep;
-  std::vector<uint64_t> o_pkey, o_dkey;
-  std::vector<uint32_t> o_pprev, o_pnext, o_pd, o_powner, o_dp, o_downer;
-  std::vector<uint8_t> o_dlive, o_dapp;
   std::vector<uint32_t> touchedP, touchedD;
   uint32_t s_head, s_tail, s_pcount, s_ftop;
   uint64_t s_dclock, s_dcount;
-  // entities
-  std::vector<uint32_t> e_ep, e_p, e_d;
-  std::vector<uint8_t> e_ref;
-  std::vector<uint64_t> e_leave;
+  std::vector<Ent> es;
   std::vector<uint32_t> touchedE;
-  std::vector<uint64_t> n_key;     // the pass's declarations
-  std::vector<uint32_t> n_p, n_d, n_chunk, n_decl;
+  std::vector<NewEnt> ns;
   EpochMap bmap;                   // hash -> the pass's declaration
   // pass results
   bool split = false;
@@ -283,83 +301,77 @@ struct XcgPairState {
   uint32_t h_nev_cap = 0;
   uint32_t* h_need = nullptr;
   uint32_t last_base = 0;
+  int prev_passes = 1;             // passes the last sub-batch needed
 
   uint32_t ids() const { return C + D; }
 
-  // ---- overlay access
-  void ptouch(uint32_t s) {
-    if (ps_ep[s] == epoch) return;
-    ps_ep[s] = epoch;
-    o_pkey[s] = pkey[s];
-    o_pprev[s] = pprev[s];
-    o_pnext[s] = pnext[s];
-    o_pd[s] = pd[s];
-    o_powner[s] = pkey[s] != NOKEY ? s : NIL;
-    touchedP.push_back(s);
-  }
-  void dtouch(uint32_t i) {
-    if (ds_ep[i] == epoch) return;
-    ds_ep[i] = epoch;
-    o_dkey[i] = dkey[i];
-    o_dlive[i] = dlive[i];
-    o_dp[i] = dp[i];
-    o_dapp[i] = 0;
-    o_downer[i] = dlive[i] ? (dp[i] != NIL ? dp[i] : C + i) : NIL;
-    touchedD.push_back(i);
-  }
-  void etouch(uint32_t x) {
-    if (e_ep[x] == epoch) return;
-    e_ep[x] = epoch;
-    if (x < C) {
-      e_p[x] = pkey[x] != NOKEY ? x : NIL;
-      e_d[x] = e_p[x] != NIL ? pd[x] : NIL;
-    } else {
-      const uint32_t i = x - C;
-      e_p[x] = NIL;
-      e_d[x] = dlive[i] && dp[i] == NIL ? i : NIL;
+  // ---- the pass's view of a slot / block / entity (copied on first use)
+  PSlot& P(uint32_t s) {
+    PSlot& q = ps[s];
+    if (q.ep != epoch) {
+      q.ep = epoch;
+      q.okey = q.key; q.oprev = q.prev; q.onext = q.next; q.opd = q.pd;
+      q.owner = q.key != NOKEY ? s : NIL;
+      touchedP.push_back(s);
     }
-    e_ref[x] = 0;
-    e_leave[x] = NEVER;
-    touchedE.push_back(x);
+    return q;
+  }
+  DSlot& Dk(uint32_t i) {
+    DSlot& q = ds[i];
+    if (q.ep != epoch) {
+      q.ep = epoch;
+      q.okey = q.key; q.olive = q.live; q.odp = q.dp;
+      q.owner = q.live ? (q.dp != NIL ? q.dp : C + i) : NIL;
+      touchedD.push_back(i);
+    }
+    return q;
+  }
+  Ent& E(uint32_t x) {
+    Ent& e = es[x];
+    if (e.ep != epoch) {
+      e.ep = epoch;
+      if (x < C) {
+        const PSlot& q = ps[x];              // committed fields: the sub-batch start
+        e.p = q.key != NOKEY ? x : NIL;
+        e.d = e.p != NIL ? q.pd : NIL;
+      } else {
+        const DSlot& q = ds[x - C];
+        e.p = NIL;
+        e.d = q.live && q.dp == NIL ? x - C : NIL;
+      }
+      e.ref = 0;
+      e.leave = NEVER;
+      touchedE.push_back(x);
+    }
+    return e;
   }
   bool is_new(uint32_t x) const { return x >= C + D; }
-  // an entity's current primary slot / disk block (a persistent one's record
-  // is initialised from the sub-batch start on first use)
-  uint32_t& ep(uint32_t x) {
-    if (is_new(x)) return n_p[x - C - D];
-    etouch(x);
-    return e_p[x];
-  }
-  uint32_t& ed(uint32_t x) {
-    if (is_new(x)) return n_d[x - C - D];
-    etouch(x);
-    return e_d[x];
-  }
-  uint64_t ekey(uint32_t x) const { return is_new(x) ? n_key[x - C - D] : (x < C ? pkey[x] : dkey[x - C]); }
+  // an entity's current primary slot / disk block
+  uint32_t& ep(uint32_t x) { return is_new(x) ? ns[x - C - D].p : E(x).p; }
+  uint32_t& ed(uint32_t x) { return is_new(x) ? ns[x - C - D].d : E(x).d; }
+  uint64_t ekey(uint32_t x) const { return is_new(x) ? ns[x - C - D].key : (x < C ? ps[x].key : ds[x - C].key); }
   // commit move of entity x's bytes to pool index `dest`
   void move_to(uint32_t dest, uint32_t x) {
-    if (is_new(x)) writes.push_back(make_uint4(dest, 0u, n_chunk[x - C - D], n_decl[x - C - D]));
+    if (is_new(x)) writes.push_back(make_uint4(dest, 0u, ns[x - C - D].chunk, ns[x - C - D].decl));
     else writes.push_back(make_uint4(dest, 1u, x, nstaged++));
   }
   // x is in neither level from time t on.  A cached entry's departure becomes
   // its ptime; one this sub-batch made has no ptime (the parse sees the batch's
   // declarations to its end), so a later lookup of it splits the sub-batch.
   void left(uint32_t x, uint64_t t) {
-    if (is_new(x)) return;
-    etouch(x);
-    e_leave[x] = t;
+    if (!is_new(x)) E(x).leave = t;
   }
 
   // ---- the primary's LRU list (xcodec_lru.h: enter / use move to the tail, evict takes the head)
-  void unlink(uint32_t s) {
-    const uint32_t p = o_pprev[s], q = o_pnext[s];
-    if (p != NIL) { ptouch(p); o_pnext[p] = q; } else s_head = q;
-    if (q != NIL) { ptouch(q); o_pprev[q] = p; } else s_tail = p;
+  void unlink(PSlot& q) {
+    const uint32_t p = q.oprev, n = q.onext;
+    if (p != NIL) P(p).onext = n; else s_head = n;
+    if (n != NIL) P(n).oprev = p; else s_tail = p;
   }
-  void append(uint32_t s) {
-    o_pprev[s] = s_tail;
-    o_pnext[s] = NIL;
-    if (s_tail != NIL) { ptouch(s_tail); o_pnext[s_tail] = s; } else s_head = s;
+  void append(uint32_t s, PSlot& q) {
+    q.oprev = s_tail;
+    q.onext = NIL;
+    if (s_tail != NIL) P(s_tail).onext = s; else s_head = s;
     s_tail = s;
   }
 
@@ -368,26 +380,33 @@ struct XcgPairState {
     uint32_t s;
     if (s_pcount == C) {
       s = s_head;
-      ptouch(s);
-      const uint32_t y = o_powner[s];
-      unlink(s);
+      PSlot& q = P(s);
+      const uint32_t y = q.owner;
+      unlink(q);
       --s_pcount;
       ep(y) = NIL;
-      const uint32_t dj = o_pd[s];
-      if (dj != NIL) { dtouch(dj); o_dp[dj] = NIL; }    // now on disk only
+      if (q.opd != NIL) Dk(q.opd).odp = NIL;      // now on disk only
       else left(y, t);
     } else {
       s = pfree[--s_ftop];
-      ptouch(s);
     }
-    o_pkey[s] = ekey(x);
-    o_powner[s] = x;
+    PSlot& q = P(s);
+    if (s_head != NIL) {                           // the next victim and what it links to
+      const PSlot& h = ps[s_head];
+      __builtin_prefetch(&es[s_head < C ? s_head : 0]);
+      if (h.onext != NIL && h.ep == epoch) __builtin_prefetch(&ps[h.onext]);
+      else if (h.next != NIL) __builtin_prefetch(&ps[h.next]);
+      const uint32_t hd = h.ep == epoch ? h.opd : h.pd;
+      if (hd != NIL) __builtin_prefetch(&ds[hd]);
+    }
+    q.okey = ekey(x);
+    q.owner = x;
     ep(x) = s;
-    append(s);
+    append(s, q);
     ++s_pcount;
     const uint32_t dj = ed(x);
-    o_pd[s] = dj;
-    if (dj != NIL) { dtouch(dj); o_dp[dj] = s; }
+    q.opd = dj;
+    if (dj != NIL) Dk(dj).odp = s;
     move_to(s, x);
     ++enters;
   }
@@ -395,14 +414,13 @@ struct XcgPairState {
   // XCodecDisk::enter (xcodec_cache_disk.cc:694-741)
   void d_append(uint32_t x, uint64_t t) {
     const uint32_t i = (uint32_t)(s_dclock % D);
-    dtouch(i);
-    o_dkey[i] = ekey(x);
-    o_dlive[i] = 1;
-    o_dapp[i] = 1;
-    o_downer[i] = x;
+    DSlot& q = Dk(i);
+    q.okey = ekey(x);
+    q.olive = 1;
+    q.owner = x;
     const uint32_t p = ep(x);
-    o_dp[i] = p;
-    if (p != NIL) { ptouch(p); o_pd[p] = i; }
+    q.odp = p;
+    if (p != NIL) P(p).opd = i;
     ed(x) = i;
     move_to(C + i, x);
     ++s_dcount;
@@ -410,15 +428,14 @@ struct XcgPairState {
     if (++s_dclock % DISK_ENTRIES == 0) {          // the write head moves on: index_invalidate_entries
       const uint64_t b = (s_dclock / DISK_ENTRIES) % nb;
       for (uint32_t j = (uint32_t)(b * DISK_ENTRIES); j < (uint32_t)((b + 1) * DISK_ENTRIES); ++j) {
-        dtouch(j);
-        if (!o_dlive[j]) continue;
-        const uint32_t y = o_downer[j];
-        o_dlive[j] = 0;
-        o_downer[j] = NIL;
+        DSlot& r = Dk(j);
+        if (!r.olive) continue;
+        const uint32_t y = r.owner;
+        r.olive = 0;
+        r.owner = NIL;
         --s_dcount;
         ed(y) = NIL;
-        const uint32_t q = o_dp[j];
-        if (q != NIL) { ptouch(q); o_pd[q] = NIL; }  // now in the primary only
+        if (r.odp != NIL) P(r.odp).opd = NIL;      // now in the primary only
         else left(y, t);
       }
     }
@@ -426,14 +443,20 @@ struct XcgPairState {
 
   // XCodecCachePair::lookup on a hash present in a level (:208-230)
   void lookup(uint32_t x, uint64_t t) {
-    if (!is_new(x) && !e_ref[x]) {
-      e_ref[x] = 1;
-      ++refs;                                      // distinct persistent entries referenced
+    if (!is_new(x)) {
+      Ent& e = E(x);
+      if (!e.ref) {
+        e.ref = 1;
+        ++refs;                                    // distinct cached entries referenced
+      }
     }
     const uint32_t p = ep(x);
     if (p != NIL) {
-      ptouch(p);
-      if (s_tail != p) { unlink(p); append(p); }   // XCodecLRU::use
+      PSlot& q = P(p);
+      if (s_tail != p) {                           // XCodecLRU::use
+        unlink(q);
+        append(p, q);
+      }
       if (ed(x) == NIL) d_append(x, t);            // XCodecDisk::touch
     } else {
       p_enter(x, t);                               // promotion
@@ -445,17 +468,19 @@ struct XcgPairState {
   // split tell why).
   bool replay(uint32_t n, const uint4* ev, const uint32_t* nev, uint32_t maxe, uint32_t maxd) {
     if (++epoch == 0) {
-      std::fill(ps_ep.begin(), ps_ep.end(), 0u);
-      std::fill(ds_ep.begin(), ds_ep.end(), 0u);
-      std::fill(e_ep.begin(), e_ep.end(), 0u);
+      for (PSlot& q : ps) q.ep = 0;
+      for (DSlot& q : ds) q.ep = 0;
+      for (Ent& e : es) e.ep = 0;
       epoch = 1;
     }
     touchedP.clear();
     touchedD.clear();
     touchedE.clear();
-    n_key.clear(); n_p.clear(); n_d.clear(); n_chunk.clear(); n_decl.clear();
+    ns.clear();
     bmap.reset((uint64_t)n * maxd);
     writes.clear();
+    writes.reserve((size_t)n * maxd * 2);
+    ns.reserve((size_t)n * maxd);
     nstaged = 0;
     enters = refs = appends = 0;
     split = false;
@@ -468,20 +493,35 @@ struct XcgPairState {
       if (cnt > maxe) { split = true; break; }     // (reference list overflow: a smaller sub-batch)
       const uint4* r = ev + (uint64_t)c * maxe;
       // rows are in stream order; a stable sort by time guards it
-      order.resize(cnt);
-      for (uint32_t k = 0; k < cnt; ++k) order[k] = k;
       bool sorted = true;
       for (uint32_t k = 1; k < cnt; ++k) sorted &= r[k - 1].z <= r[k].z;
-      if (!sorted) std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return r[a].z < r[b].z; });
+      if (!sorted) {
+        order.resize(cnt);
+        for (uint32_t k = 0; k < cnt; ++k) order[k] = k;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return r[a].z < r[b].z; });
+      }
       for (uint32_t k = 0; k < cnt && !split; ++k) {
-        const uint4 e = r[order[k]];
+        if (k + 8 < cnt) {                         // memory-level parallelism: touch ahead
+          const uint4 f = r[sorted ? k + 8 : order[k + 8]];
+          const uint32_t fk = f.w >> 30, fr = f.w & EV_REF_MASK;
+          if (fk == EV_GHIT || fk == EV_GMISS) {
+            if (fr < C + D) {
+              __builtin_prefetch(&es[fr]);
+              if (fr < C) __builtin_prefetch(&ps[fr]);
+              else __builtin_prefetch(&ds[fr - C]);
+            }
+          } else {
+            bmap.prefetch(((uint64_t)f.y << 32) | f.x);
+          }
+        }
+        const uint4 e = r[sorted ? k : order[k]];
         const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
         const uint64_t t = ((uint64_t)c << 21) | e.z;
         const uint64_t h = ((uint64_t)e.y << 32) | e.x;
         if (kind == EV_GHIT || kind == EV_GMISS) {
           if (ref >= C + D) { bad[c] = 1; ok = false; continue; }
-          etouch(ref);
-          const bool present = e_p[ref] != NIL || e_d[ref] != NIL;
+          const Ent& en = E(ref);
+          const bool present = en.p != NIL || en.d != NIL;
           if (present != (kind == EV_GHIT)) { bad[c] = 1; ok = false; }
           if (present) lookup(ref, t);
         } else if (kind == EV_HIT) {
@@ -492,8 +532,8 @@ struct XcgPairState {
         } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
           const uint32_t x0 = bmap.find(h);
           if (x0 != NIL && (ep(x0) != NIL || ed(x0) != NIL)) { bad[c] = 1; ok = false; continue; }
-          const uint32_t x = C + D + (uint32_t)n_key.size();
-          n_key.push_back(h); n_p.push_back(NIL); n_d.push_back(NIL); n_chunk.push_back(c); n_decl.push_back(ref);
+          const uint32_t x = C + D + (uint32_t)ns.size();
+          ns.push_back(NewEnt{h, NIL, NIL, c, ref});
           bmap.put(h, x);
           p_enter(x, t);
           d_append(x, t);
@@ -503,13 +543,15 @@ struct XcgPairState {
     return ok && !split;
   }
 
-  // Keep the pass: overlay -> committed.
+  // Keep the pass: its copies -> committed.
   void keep() {
     for (uint32_t s : touchedP) {
-      pkey[s] = o_pkey[s]; pprev[s] = o_pprev[s]; pnext[s] = o_pnext[s]; pd[s] = o_pd[s];
+      PSlot& q = ps[s];
+      q.key = q.okey; q.prev = q.oprev; q.next = q.onext; q.pd = q.opd;
     }
     for (uint32_t i : touchedD) {
-      dkey[i] = o_dkey[i]; dlive[i] = o_dlive[i]; dp[i] = o_dp[i];
+      DSlot& q = ds[i];
+      q.key = q.okey; q.live = q.olive; q.dp = q.odp;
     }
     head = s_head; tail = s_tail; pcount = s_pcount; ftop = s_ftop; dclock = s_dclock; dcount = s_dcount;
   }
@@ -551,9 +593,9 @@ int upload_ptime(XcgPairState* P, hipStream_t st) {
   uint64_t* kv = (uint64_t*)P->h_xfer;
   uint32_t m = 0;
   for (uint32_t x : P->touchedE)
-    if (P->e_leave[x] != NEVER) {
+    if (P->es[x].leave != NEVER) {
       kv[2 * m] = x;
-      kv[2 * m + 1] = P->e_leave[x];
+      kv[2 * m + 1] = P->es[x].leave;
       ++m;
     }
   if (m) {
@@ -616,24 +658,24 @@ void pair_verify(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
   (void)hipMemcpy(keyg.data(), P->d_keyg, 8 * ids, hipMemcpyDeviceToHost);
   uint32_t bad = 0;
   for (uint32_t s = 0; s < P->C; ++s) {
-    if (P->pkey[s] == NOKEY) continue;
-    if (host_hash(&pool[(uint64_t)s * SEG]) != P->pkey[s] && bad++ < 5)
+    const PSlot& q = P->ps[s];
+    if (q.key == NOKEY) continue;
+    if (host_hash(&pool[(uint64_t)s * SEG]) != q.key && bad++ < 5)
       fprintf(stderr, "pair verify: primary slot %u bytes do not hash to its key\n", s);
-    if (keyg[s] != P->pkey[s] && bad++ < 5) fprintf(stderr, "pair verify: keyg[%u] stale\n", s);
+    if (keyg[s] != q.key && bad++ < 5) fprintf(stderr, "pair verify: keyg[%u] stale\n", s);
+    if (q.pd != NIL && (P->ds[q.pd].key != q.key || !P->ds[q.pd].live) && bad++ < 5)
+      fprintf(stderr, "pair verify: slot %u links disk block %u of another hash\n", s, q.pd);
   }
   for (uint32_t i = 0; i < P->D; ++i) {
-    if (!P->dlive[i]) continue;
-    if (host_hash(&pool[((uint64_t)P->C + i) * SEG]) != P->dkey[i] && bad++ < 5)
+    const DSlot& q = P->ds[i];
+    if (!q.live) continue;
+    if (host_hash(&pool[((uint64_t)P->C + i) * SEG]) != q.key && bad++ < 5)
       fprintf(stderr, "pair verify: disk block %u bytes do not hash to its key\n", i);
-    const uint64_t want = P->dp[i] == NIL ? P->dkey[i] : NOKEY;
+    const uint64_t want = q.dp == NIL ? q.key : NOKEY;
     if (keyg[P->C + i] != want && bad++ < 5) fprintf(stderr, "pair verify: keyg[C+%u] stale\n", i);
-    if (P->dp[i] != NIL && P->pkey[P->dp[i]] != P->dkey[i] && bad++ < 5)
-      fprintf(stderr, "pair verify: disk block %u links slot %u of another hash\n", i, P->dp[i]);
+    if (q.dp != NIL && P->ps[q.dp].key != q.key && bad++ < 5)
+      fprintf(stderr, "pair verify: disk block %u links slot %u of another hash\n", i, q.dp);
   }
-  for (uint32_t s = 0; s < P->C; ++s)
-    if (P->pkey[s] != NOKEY && P->pd[s] != NIL && (P->dkey[P->pd[s]] != P->pkey[s] || !P->dlive[P->pd[s]]) &&
-        bad++ < 5)
-      fprintf(stderr, "pair verify: slot %u links disk block %u of another hash\n", s, P->pd[s]);
   fprintf(stderr, "pair verify: %u problems (primary %u, disk live %llu)\n", bad, P->pcount,
           (unsigned long long)P->dcount);
 }
@@ -661,11 +703,12 @@ int pair_commit(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
   kv.reserve(2 * (P->touchedP.size() + P->touchedD.size()));
   for (uint32_t s : P->touchedP) {
     kv.push_back(s);
-    kv.push_back(P->pkey[s]);
+    kv.push_back(P->ps[s].key);
   }
   for (uint32_t i : P->touchedD) {
+    const DSlot& q = P->ds[i];
     kv.push_back((uint64_t)P->C + i);
-    kv.push_back(P->dlive[i] && P->dp[i] == NIL ? P->dkey[i] : NOKEY);
+    kv.push_back(q.live && q.dp == NIL ? q.key : NOKEY);
   }
   const uint32_t nk = (uint32_t)(kv.size() / 2);
   const uint64_t wbytes = 16ull * nw, kbytes = 8ull * kv.size();
@@ -710,22 +753,12 @@ int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out) {
   P->nb = nb;
   P->D = (uint32_t)(nb * DISK_ENTRIES);
   const uint32_t D = P->D, ids = C + D;
-  P->pkey.assign(C, NOKEY);
-  P->pprev.assign(C, NIL);
-  P->pnext.assign(C, NIL);
-  P->pd.assign(C, NIL);
+  P->ps.assign(C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
+  P->ds.assign(D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0});
+  P->es.assign(ids, Ent{NEVER, 0, NIL, NIL, 0});
   P->pfree.resize(C);
   for (uint32_t s = 0; s < C; ++s) P->pfree[s] = C - 1 - s;   // slot 0 first
   P->ftop = C;
-  P->dkey.assign(D, NOKEY);
-  P->dlive.assign(D, 0);
-  P->dp.assign(D, NIL);
-  P->ps_ep.assign(C, 0);
-  P->ds_ep.assign(D, 0);
-  P->o_pkey.resize(C); P->o_pprev.resize(C); P->o_pnext.resize(C); P->o_pd.resize(C); P->o_powner.resize(C);
-  P->o_dkey.resize(D); P->o_dlive.resize(D); P->o_dapp.resize(D); P->o_dp.resize(D); P->o_downer.resize(D);
-  P->e_ep.assign(ids, 0);
-  P->e_p.resize(ids); P->e_d.resize(ids); P->e_ref.resize(ids); P->e_leave.resize(ids);
   if (hipMalloc(&P->d_keyg, 8ull * ids) != hipSuccess || hipMalloc(&P->d_ptime, 8ull * ids) != hipSuccess ||
       hipMemset(P->d_keyg, 0xFF, 8ull * ids) != hipSuccess || hipMemset(P->d_ptime, 0xFF, 8ull * ids) != hipSuccess) {
     (void)hipFree(P->d_keyg);
@@ -750,17 +783,14 @@ void xcg_pair_state_destroy(XcgPairState* P) {
 // Drop everything (XCodecCache objects have no clear; this is a fresh pair on
 // an empty volume).  The caller wipes G itself.
 int xcg_pair_state_clear(XcgPairState* P) {
-  std::fill(P->pkey.begin(), P->pkey.end(), NOKEY);
-  std::fill(P->pprev.begin(), P->pprev.end(), NIL);
-  std::fill(P->pnext.begin(), P->pnext.end(), NIL);
-  std::fill(P->pd.begin(), P->pd.end(), NIL);
+  P->ps.assign(P->C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
+  P->ds.assign(P->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0});
+  for (Ent& e : P->es) e.ep = 0;
+  P->epoch = 0;
   for (uint32_t s = 0; s < P->C; ++s) P->pfree[s] = P->C - 1 - s;
   P->ftop = P->C;
   P->head = P->tail = NIL;
   P->pcount = 0;
-  std::fill(P->dkey.begin(), P->dkey.end(), NOKEY);
-  std::fill(P->dlive.begin(), P->dlive.end(), 0);
-  std::fill(P->dp.begin(), P->dp.end(), NIL);
   P->dclock = P->dcount = 0;
   return hipMemset(P->d_keyg, 0xFF, 8ull * P->ids()) == hipSuccess ? 0 : -5;
 }
@@ -780,10 +810,17 @@ uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; 
 int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds_out, hipStream_t st) {
   const uint32_t n = a0->n;
   int rounds = 0;
-  uint32_t per = P->C / a0->maxd ? P->C / a0->maxd : 1u;
+  // A sub-batch is bounded by the disk only: while it writes fewer than a lap
+  // of disk blocks, nothing it declared can leave both levels within it (a
+  // chunk writes at most maxd declarations plus its touches).
+  const uint64_t lap = P->D > 2 * DISK_ENTRIES ? P->D - 2 * DISK_ENTRIES : 1;
+  uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, lap / a0->maxd));
   constexpr int MAX_PASSES = 12;
   uint32_t i0 = 0;
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   while (i0 < n) {
+    const clk::time_point t0 = clk::now();
     const uint32_t m = per < n - i0 ? per : n - i0;
     XcgStreamArgs a = *a0;
     a.n = m;
@@ -794,30 +831,49 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     if (a.stats) a.stats += 4ull * i0;
     a.ptime = P->d_ptime;
     a.no_commit = 1;
-    // first guess: the tiling seed's references, replayed
+    // The rounds start from each chunk's tiling (its cold parse).  ptime is
+    // NEVER (no cached entry leaves) unless the last sub-batch needed more than
+    // one pass: then the first guess is the tiling seed's own references,
+    // replayed (a cached tile is a lookup hit, a repeat of an earlier tile a hit
+    // on its declaration, every other tile a declaration).
     if (xcg_launch_seed_tiling(&a, st)) return -5;
-    const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};
-    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, (uint64_t)b.mask + 1, NOKEY);
-    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
-    hipLaunchKernelGGL(pair_seed_table_kernel, dim3(grid_for((uint64_t)m * a.maxd)), dim3(256), 0, st, m,
-                       (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
-    hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
-                       (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe);
-    if (download_refs(P, a, st)) return -5;
-    (void)P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
-    if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
-        ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
-      return -5;
+    const clk::time_point t1 = clk::now();
+    if (P->prev_passes > 1) {
+      const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};
+      hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, (uint64_t)b.mask + 1, NOKEY);
+      hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
+      hipLaunchKernelGGL(pair_seed_table_kernel, dim3(grid_for((uint64_t)m * a.maxd)), dim3(256), 0, st, m,
+                         (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
+      hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
+                         (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe);
+      if (download_refs(P, a, st)) return -5;
+      (void)P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
+      if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
+          ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
+        return -5;
+    }
+    const clk::time_point t2 = clk::now();
+    double t_parse = 0, t_dl = 0, t_replay = 0;
     bool done = false, split = false;
+    int passes = 0;
     for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
+      ++passes;
       a.keep_decls = 1;
       a.need_given = pass > 0;
       int r = 0;
+      const clk::time_point q0 = clk::now();
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
       if (rc) return rc;
+      if (pair_debug()) (void)hipStreamSynchronize(st);
+      const clk::time_point q1 = clk::now();
       if (download_refs(P, a, st)) return -5;
+      const clk::time_point q2 = clk::now();
       const bool ok = P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
+      const clk::time_point q3 = clk::now();
+      t_parse += ms(q0, q1);
+      t_dl += ms(q1, q2);
+      t_replay += ms(q2, q3);
       uint32_t nbad = 0;
       for (uint32_t c = 0; c < m; ++c) nbad += P->bad[c];
       if (pair_debug())
@@ -837,20 +893,25 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     if (!done) {
       if (m == 1) return split ? -95 : -75;
       per = m / 2;                                 // redo this part in halves
+      P->prev_passes = MAX_PASSES;
       continue;
     }
+    const clk::time_point t3 = clk::now();
     P->keep();
     if (pair_commit(P, a, st)) return -5;
+    if (pair_debug())
+      fprintf(stderr, "pair: ms seed %.2f seed-replay %.2f parse %.2f download %.2f replay %.2f commit %.2f\n",
+              ms(t0, t1), ms(t1, t2), t_parse, t_dl, t_replay, ms(t3, clk::now()));
     if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, a, st);
     // the next sub-batch starts with every hash visible to its end
     hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
     P->last_base = i0;
+    P->prev_passes = passes;
     i0 += m;
-    // size the next sub-batch from what this one used of each level
-    const uint64_t useP = P->enters + P->refs, useD = P->appends;
+    // size the next sub-batch from the disk blocks this one wrote
+    const uint64_t useD = P->appends;
     uint64_t want = (uint64_t)n;
-    if (useP) want = std::min<uint64_t>(want, (uint64_t)P->C * 9 / 10 * m / useP);
-    if (useD && P->D > 2 * DISK_ENTRIES) want = std::min<uint64_t>(want, (uint64_t)(P->D - 2 * DISK_ENTRIES) * 9 / 10 * m / useD);
+    if (useD) want = std::min<uint64_t>(want, lap * 9 / 10 * m / useD);
     per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
   }
   if (rounds_out) *rounds_out = rounds;
