@@ -6,11 +6,16 @@ the survey generator (seed 0xC2, 50 % duplicate 2 KiB segments), each chunk
 one independent XCodecEncoder::encode call with its own fresh
 XCodecMemoryCache (XCG_SEM_INDEPENDENT).  A step = one batched encode launch
 over all chunks; inputs, offsets and output slots are resident in HBM before
-the timed region.  Output is bit-exact with the reference encoder (checked
-against the CPU oracle on a sample every run).
+the timed region.  Output is bit-exact with the reference encoder: every run
+checks ALL 4096 chunks against the CPU oracle (and the stream-semantics side
+figure all 4096 too).
 
 Multi-GPU (torchrun, one rank per GPU): every rank encodes its own 4096-chunk
 shard (seed 0xC2 + rank) with no collective in the timed loop -> weak scaling.
+With N > 1 the line also carries `sharded_configs`: BASELINE configs C4 (1 M x
+4 KiB packets) and C5 (8 GiB in 128 KiB calls), ONE stream each cut into
+contiguous per-rank ranges (wanproxy_amd/shard.py config_shard), each rank with
+a private cache, checked per shard against the oracle run on that shard alone.
 
 rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
 """
@@ -39,43 +44,141 @@ def parse():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--chunks', type=int, default=NCHUNKS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-passes', type=int, default=8)
+    ap.add_argument('--cpu-seconds', type=float, default=10.0,
+                    help='minimum wall of the headline CPU baseline (the reference on T threads)')
     ap.add_argument('--no-extras', action='store_true', help='skip the stream / decode / PCIe side measurements')
     ap.add_argument('--no-configs', action='store_true',
                     help='skip the C3 / C4 / C5 stream-configuration figures (scripts/configs_bench.py)')
     return ap.parse_args()
 
 
-def cpu_baseline(data: np.ndarray, offs, lens, passes: int):
-    """Reference XCodecEncoder (oracle/_ref, compiled from the reference
-    sources) on this host's cores: contiguous chunk shards, one thread each,
-    independent-chunk semantics (same output as the GPU run)."""
+def host_cpus():
+    """This host's CPUs: nproc, the affinity set, the cgroup quota, the model,
+    and the threads the CPU baselines use -- the share of the machine this
+    process may use (affinity, cgroup quota and OMP_NUM_THREADS, the GPU box's
+    per-GPU CPU share), not the whole machine's nproc."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()
+        if q != 'max':
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = ''
+    try:
+        for ln in open('/proc/cpuinfo'):
+            if ln.startswith('model name'):
+                model = ln.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    t = aff
+    if quota:
+        t = min(t, max(1, int(quota)))
+    if os.environ.get('OMP_NUM_THREADS', '').isdigit():
+        t = min(t, int(os.environ['OMP_NUM_THREADS']))
+    return {'nproc': nproc, 'affinity': aff, 'cgroup_cpus': quota, 'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
+            'model': model, 'threads': max(1, t)}
+
+
+def _threads_rate(o, jobs, threads, min_s):
+    """Run `jobs` (callables returning bytes encoded) on `threads` threads,
+    repeating the whole set until min_s have passed; GiB/s over the wall."""
     from concurrent.futures import ThreadPoolExecutor
+    total, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while True:
+            total += sum(ex.map(lambda f: f(), jobs))
+            dt = time.perf_counter() - t0
+            if dt >= min_s:
+                break
+    return total / 2**30 / dt, total, dt
+
+
+def cpu_baseline(data: np.ndarray, offs, lens, min_s: float = 10.0):
+    """The reference XCodecEncoder (oracle/_ref, compiled from the reference
+    sources; the C restatement if that is absent) on this host's cores, same
+    semantics and inputs as the GPU figures.  Headline: independent chunks
+    (S1) on T threads x contiguous shards, repeated over the batch for >=
+    min_s.  `extra`: S1 on one thread, the S2 tack loop (one encoder + cache,
+    programs/tack/tack.cc:298-321 -- inherently one thread), and bounded
+    samples of C3 / C4 / C5 on one thread and (C4 / C5, a private cache per
+    thread as per GPU) on T threads."""
     from oracle.lib import Oracle
     kind = 'reference'
     try:
         o = Oracle(ref=True)
     except FileNotFoundError:
         o, kind = Oracle(), 'port'
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hc = host_cpus()
+    T = hc['threads']
     n = offs.size
-    shards = np.array_split(np.arange(n), threads)
+    shards = [idx for idx in np.array_split(np.arange(n), T) if idx.size]
 
-    def run(idx):
-        if idx.size:
-            o.encode_batch(data, offs[idx], lens[idx], mode=0)
-
-    total = 0
+    def s1_job(idx):
+        return lambda: (o.encode_batch(data, offs[idx], lens[idx], mode=0), int(lens[idx].astype(np.int64).sum()))[1]
+    v, tot, dt = _threads_rate(o, [s1_job(i) for i in shards], T, min_s)
+    res = {'value': round(v, 4), 'unit': 'GiB/s', 'cores': T, 'kind': kind,
+           'sample': f'S1 (independent chunks): the full {n} x 64 KiB C2 batch repeated to {tot / 2**30:.1f} GiB, '
+                     f'{T} threads x contiguous shards, fresh XCodecMemoryCache per chunk; {dt:.1f} s wall',
+           'host': hc}
+    extra = {}
+    first = np.arange(min(n, 256))
+    v1, tot, dt = _threads_rate(o, [s1_job(first)], 1, 3.0)
+    extra['S1_1thread'] = {'value': round(v1, 4), 'unit': 'GiB/s', 'sample': f'{tot >> 20} MiB, {dt:.1f} s'}
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        for _ in range(passes):
-            list(ex.map(run, shards))
-            total += int(lens.astype(np.int64).sum())
+    o.encode_batch(data, offs, lens, mode=1)
     dt = time.perf_counter() - t0
-    gib = total / 2**30
-    return {'value': round(gib / dt, 4), 'unit': 'GiB/s', 'cores': threads, 'kind': kind,
-            'sample': f'{passes} passes over the full {n} x 64 KiB batch ({total / 2**20:.0f} MiB), '
-                      f'{threads} threads x contiguous shards, fresh XCodecMemoryCache per chunk; {dt:.1f} s wall'}
+    extra['S2_1thread'] = {'value': round(int(lens.astype(np.int64).sum()) / 2**30 / dt, 4), 'unit': 'GiB/s',
+                           'sample': f'the full C2 batch as one tack loop (one encoder + cache), {dt:.1f} s'}
+    extra.update(cpu_configs(o, T))
+    res['extra'] = extra
+    return res
+
+
+def cpu_configs(o, T):
+    """C3 / C4 / C5 on the CPU reference, bounded samples of the GPU figures'
+    workloads (scripts/configs_bench.py)."""
+    from wanproxy_amd import synth
+    from wanproxy_amd.shard import shard_data
+    out = {}
+    # C3: 16 of the 64 streams x 16 MiB (seeds 100..115, dup 5), round-robin
+    # 64 KiB calls, warm-up encode then the timed re-encode on the warm cache
+    ns, per = 16, 16 << 20
+    streams = [np.frombuffer(synth.stream(100 + i, per, 5, 0), np.uint8) for i in range(ns)]
+    data = np.stack([st.reshape(-1, 65536) for st in streams], 1).reshape(-1).copy()
+    offs = np.arange(0, data.size, 65536, dtype=np.uint64)
+    lens = np.full(data.size // 65536, 65536, np.uint32)
+    c = o.cache_new()
+    o.encode_batch(data, offs, lens, mode=1, cache=c)
+    t0 = time.perf_counter()
+    o.encode_batch(data, offs, lens, mode=1, cache=c)
+    dt = time.perf_counter() - t0
+    o.cache_free(c)
+    out['C3_1thread'] = {'value': round(data.size / 2**30 / dt, 4), 'unit': 'GiB/s',
+                         'sample': f'{ns} streams x 16 MiB round-robin, warm shared cache, {dt:.1f} s'}
+    for name, k1 in (('C4', 8192), ('C5', 512)):
+        d, offs, lens, _ = shard_data(name, 8, 0)
+        unit = int(lens[0])
+        t0 = time.perf_counter()
+        o.encode_batch(d, offs[:k1], lens[:k1], mode=1)
+        dt = time.perf_counter() - t0
+        out[f'{name}_1thread'] = {'value': round(k1 * unit / 2**30 / dt, 4), 'unit': 'GiB/s',
+                                  'sample': f'first {k1} calls of the rank-0 shard ({k1 * unit >> 20} MiB), cold '
+                                            f'cache, {dt:.1f} s'}
+        kt = max(1, min(offs.size // T, k1 // 2))
+        jobs = [(lambda a: (lambda: (o.encode_batch(d, offs[a:a + kt], lens[a:a + kt], mode=1), kt * unit)[1]))(
+            t * kt) for t in range(T)]
+        v, tot, dt = _threads_rate(o, jobs, T, 0.0)
+        out[f'{name}_{T}threads'] = {'value': round(v, 4), 'unit': 'GiB/s',
+                                     'sample': f'{T} threads x {kt} calls ({kt * unit >> 20} MiB) each, a private '
+                                               f'cold cache per thread (as per GPU), {dt:.1f} s'}
+    return out
 
 
 def pmc_traffic(n):
@@ -92,11 +195,17 @@ def pmc_traffic(n):
     return int(s['hbm_traffic_bytes_per_launch']), 'profiles/r01_c2_independent_summary.json (rocprofv3 --pmc)'
 
 
-def timed(fn, steps, stream):
+def timed(fn, steps, stream, kernel_time=False):
+    """(wall s / step, HIP-event s / step on `stream`, stream-parse kernel ms /
+    step, its launches / step) over `steps` calls after 2 untimed ones."""
     import torch
+    from wanproxy_amd.xcgpu import lib, stream_kernel_time
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
+    if kernel_time:
+        lib().xcg_debug_stream_kernel_timing(1)
+        stream_kernel_time()                       # (drop anything earlier)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -105,14 +214,33 @@ def timed(fn, steps, stream):
         fn()
     ev1.record(stream)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps, ev0.elapsed_time(ev1) / steps * 1e-3
+    wall = (time.perf_counter() - t0) / steps
+    kms, kl = 0.0, 0
+    if kernel_time:
+        lib().xcg_debug_stream_kernel_timing(0)
+        kms, kl = stream_kernel_time()
+    return wall, ev0.elapsed_time(ev1) / steps * 1e-3, kms / steps, kl / steps
+
+
+def oracle_all(data, offs, lens, mode, threads=None):
+    """The CPU oracle over every chunk (independent chunks split over threads;
+    a stream is one sequential walk)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.lib import Oracle
+    o = Oracle()
+    if mode == 1:
+        return o.encode_batch(data, offs, lens, mode=1)
+    parts = [p for p in np.array_split(np.arange(offs.size), threads or host_cpus()['threads']) if p.size]
+    with ThreadPoolExecutor(len(parts)) as ex:
+        res = list(ex.map(lambda idx: o.encode_batch(data, offs[idx], lens[idx], mode=0), parts))
+    return [e for r in res for e in r]
 
 
 def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, d_st, n, stream, dev, rank):
     """Same C2 batch under stream semantics (one cache, chunk order), its GPU
-    decode, and the host-inclusive (PCIe) encode rate.  Each is checked."""
+    decode, the host-inclusive (PCIe) encode rate, and the drop-in's per-call
+    tack loop.  Each is checked."""
     import torch
-    from oracle.lib import Oracle
     from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
     in_bytes = int(lens.astype(np.int64).sum())
     res = {}
@@ -123,20 +251,31 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
         sctx.cache_clear()
         sctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream,
                                  semantics=XCG_SEM_STREAM)
-    wall, _ = timed(s2, 5, stream)
+    wall, _, kms, kl = timed(s2, 5, stream, kernel_time=True)
     sctx.status()
     ol = d_ol.cpu().numpy()
     outh = d_out.cpu().numpy()
     oo = d_oo.cpu().numpy()
     enc = [outh[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)]
-    k = min(n, 256)                       # sequential oracle on a prefix (same stream order)
-    exp = Oracle().encode_batch(data, offs[:k], lens[:k], mode=1)
-    if enc[:k] != exp:
-        raise SystemExit('PARITY FAILURE (stream semantics)')
-    res['stream_semantics'] = {'metric': 'XCodec encode GiB/s, one cache across the batch (tack loop order)',
-                               'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
-                               'rounds': sctx.last_rounds(), 'out_in_ratio': round(int(ol.sum()) / in_bytes, 5),
-                               'includes': 'cache clear + Jacobi rounds + commit'}
+    exp = oracle_all(data, offs, lens, mode=1)        # every chunk, sequential oracle (same stream order)
+    if enc != exp:
+        bad = next(i for i in range(n) if enc[i] != exp[i])
+        raise SystemExit(f'PARITY FAILURE (stream semantics) at chunk {bad}')
+    out_bytes = int(ol.sum())
+    ach = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9
+    res['stream_semantics'] = {
+        'metric': 'XCodec encode GiB/s, one cache across the batch (tack loop order)',
+        'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
+        'rounds': sctx.last_rounds(), 'out_in_ratio': round(out_bytes / in_bytes, 5),
+        'includes': 'cache clear + tiling seed + Jacobi rounds + verification + commit',
+        'checked': f'all {n} chunks vs the sequential oracle',
+        'roofline': {'bound': 'hbm', 'achieved': round(ach, 2), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                     'frac': round(ach / PEAK_HBM_GBS, 5),
+                     'frac_read': round(in_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5),
+                     'kernel': 'encode_stream_kernel', 'kernel_ms_per_step': round(kms, 4),
+                     'launches_per_step': kl, 'algorithmic_bytes_per_step': in_bytes + out_bytes,
+                     'traffic': None,
+                     'traffic_note': 'PMC HBM bytes of this kernel: profiles/r02_stream_pmc_summary.json'}}
     # -- decode of that stream with a fresh decoder cache
     dctx = Context(dev.index, cache_segments=1 << 18)
     elens = ol.astype(np.uint32)
@@ -165,7 +304,7 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
                                       C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
                                       C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
                                       tot.ctypes.data, C.c_void_p(stream.cuda_stream)))
-    wall, _ = timed(dec, 5, stream)
+    wall, _, _, _ = timed(dec, 5, stream)
     if int(tot[0]) != in_bytes or d_dout[:in_bytes].cpu().numpy().tobytes() != data.tobytes():
         raise SystemExit('PARITY FAILURE (decode round trip)')
     res['decode'] = {'metric': 'XCodec decode GiB/s of decoded bytes (that stream, fresh decoder cache)',
@@ -173,30 +312,112 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
                      'includes': 'cache clear + scan + size + emit + commit, one host sync'}
     sctx.close()
     dctx.close()
-    # -- host-inclusive independent encode: pinned H2D of the input, encode,
-    #    pack the slots, D2H of exactly the encoded bytes
-    ctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream)
-    torch.cuda.synchronize()
-    enc_bytes = int(d_ol.sum().item())
-    h_in = torch.from_numpy(data.copy()).pin_memory()
-    h_out = torch.empty(enc_bytes, dtype=torch.uint8).pin_memory()
-    d_packed = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
-    d_poff = torch.zeros(n, dtype=torch.int64, device=dev)
-    d_ptot = torch.zeros(1, dtype=torch.int64, device=dev)
+    del d_enc, d_dout
+    res['host_inclusive'] = host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, n, dev)
+    res['tack_loop'] = tack_loop(data, offs, lens)
+    return res
 
-    def pcie():
-        d_in.copy_(h_in, non_blocking=True)
-        ctx.encode_batch_device(d_in, d_off, d_len, n, CHUNK, d_out, d_oo, d_ol, d_st, stream=stream)
-        _check(lib().xcg_pack_outputs(ctx.h, C.c_void_p(d_out.data_ptr()), C.c_void_p(d_oo.data_ptr()),
-                                      C.c_void_p(d_ol.data_ptr()), n, C.c_void_p(d_packed.data_ptr()),
-                                      C.c_void_p(d_poff.data_ptr()), C.c_void_p(d_ptot.data_ptr()),
-                                      C.c_void_p(stream.cuda_stream)))
-        h_out.copy_(d_packed[:enc_bytes], non_blocking=True)
-    wall, _ = timed(pcie, 5, stream)
-    if int(d_ptot.item()) != enc_bytes:
-        raise SystemExit('pack size mismatch')
-    res['host_inclusive'] = {'metric': 'independent-chunk encode GiB/s incl. pinned H2D of input and D2H of output',
-                             'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3)}
+
+def host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, n, dev, nsub=16):
+    """Independent-chunk encode from pinned host memory to pinned host memory:
+    H2D of the input, encode, pack, D2H of exactly the encoded bytes -- cut
+    into `nsub` sub-batches pipelined over three HIP streams (copy in /
+    compute / copy out), so the two PCIe directions and the kernels overlap.
+    The host learns each sub-batch's packed size from a 8-byte readback and
+    issues its D2H then; checked byte for byte against the device result."""
+    import ctypes as C
+    import torch
+    from wanproxy_amd.xcgpu import _check, lib
+    per = (n + nsub - 1) // nsub
+    subs = [(a, min(n, a + per)) for a in range(0, n, per)]
+    bnd = [(int(offs[a]), int(offs[b - 1]) + int(lens[b - 1])) for a, b in subs]
+    h_in = torch.from_numpy(data.copy()).pin_memory()
+    slot = [(int(d_oo[a].item()), int(d_oo[b - 1].item()) + 2 * CHUNK + 16) for a, b in subs]
+    d_packed = torch.empty(int(d_out.numel()) + 16, dtype=torch.uint8, device=dev)
+    d_poff = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_ptot = torch.zeros(len(subs), dtype=torch.int64, device=dev)
+    h_tot = torch.zeros(len(subs), dtype=torch.int64).pin_memory()
+    h_out = torch.empty(int(d_out.numel()), dtype=torch.uint8).pin_memory()
+    s_in, s_cmp, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev_in = [torch.cuda.Event() for _ in subs]
+    ev_c = [torch.cuda.Event() for _ in subs]
+    L = lib()
+    sizes = [0] * len(subs)
+
+    def run():
+        for i, (a, b) in enumerate(subs):
+            x0, x1 = bnd[i]
+            with torch.cuda.stream(s_in):
+                d_in[x0:x1].copy_(h_in[x0:x1], non_blocking=True)
+                ev_in[i].record(s_in)
+            s_cmp.wait_event(ev_in[i])
+            ctx.encode_batch_device(d_in, d_off[a:b], d_len[a:b], b - a, CHUNK, d_out, d_oo[a:b], d_ol[a:b],
+                                    stream=s_cmp)
+            p0 = slot[i][0]
+            _check(L.xcg_pack_outputs(ctx.h, C.c_void_p(d_out.data_ptr()), C.c_void_p(d_oo[a:].data_ptr()),
+                                      C.c_void_p(d_ol[a:].data_ptr()), b - a, C.c_void_p(d_packed.data_ptr() + p0),
+                                      C.c_void_p(d_poff[a:].data_ptr()), C.c_void_p(d_ptot[i:].data_ptr()),
+                                      C.c_void_p(s_cmp.cuda_stream)))
+            with torch.cuda.stream(s_cmp):
+                h_tot[i:i + 1].copy_(d_ptot[i:i + 1], non_blocking=True)
+                ev_c[i].record(s_cmp)
+        o = 0
+        for i in range(len(subs)):
+            ev_c[i].synchronize()
+            sz = int(h_tot[i])
+            sizes[i] = sz
+            s_out.wait_event(ev_c[i])
+            with torch.cuda.stream(s_out):
+                h_out[o:o + sz].copy_(d_packed[slot[i][0]:slot[i][0] + sz], non_blocking=True)
+            o += sz
+        s_out.synchronize()
+        return o
+
+    run()
+    torch.cuda.synchronize(dev)
+    walls = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        tot = run()
+        walls.append(time.perf_counter() - t0)
+    wall = sorted(walls)[len(walls) // 2]
+    ol = d_ol.cpu().numpy()
+    oo = d_oo.cpu().numpy()
+    dout = d_out.cpu().numpy()
+    want = b''.join(dout[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n))
+    if tot != len(want) or h_out[:tot].numpy().tobytes() != want:
+        raise SystemExit('host-inclusive output differs from the device-resident encode')
+    in_bytes = int(lens.astype(np.int64).sum())
+    return {'metric': 'independent-chunk encode GiB/s incl. pinned H2D of input and D2H of the packed output',
+            'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
+            'pcie_GBps': round((in_bytes + tot) / wall / 1e9, 2), 'sub_batches': len(subs),
+            'includes': 'H2D + encode + pack + size readback + D2H, 3 streams (median of 5)'}
+
+
+def tack_loop(data, offs, lens, ncalls=1024):
+    """The drop-in path as tack calls it (programs/tack/tack.cc:298-321): one
+    XCodecEncoder::encode per 64 KiB read on one encoder + cache, through the
+    reference's own driver and Buffer classes with integration/'s encoder over
+    the GPU engine (oracle/_ref/libxcdropin.so), beside the compiled reference
+    (libxcref.so) on the same calls; outputs must be identical."""
+    from oracle.lib import Oracle
+    try:
+        gpu, ref = Oracle(dropin=True), Oracle(ref=True)
+    except FileNotFoundError as e:
+        return {'error': f'not built: {e}'}
+    k = min(ncalls, offs.size)
+    res, outs = {}, {}
+    for name, o in (('gpu_dropin', gpu), ('reference_cpu', ref)):
+        o.encode_batch(data, offs[:8], lens[:8], mode=1)       # (warm: HIP init, allocations)
+        t0 = time.perf_counter()
+        outs[name] = o.encode_batch(data, offs[:k], lens[:k], mode=1)
+        dt = time.perf_counter() - t0
+        b = int(lens[:k].astype(np.int64).sum())
+        res[name] = {'us_per_call': round(dt / k * 1e6, 1), 'GiBps': round(b / 2**30 / dt, 3)}
+    if outs['gpu_dropin'] != outs['reference_cpu']:
+        raise SystemExit('PARITY FAILURE (drop-in tack loop vs the reference)')
+    res.update({'calls': k, 'call_bytes': int(lens[0]), 'checked': 'drop-in output == reference output, every call',
+                'includes': 'per call: Buffer -> H2D, one stream-semantics launch, D2H, host cache mirror'})
     return res
 
 
@@ -222,6 +443,52 @@ def other_configs():
             out[name] = fn(a)
         except BaseException as e:          # SystemExit from a parity check included
             out[name] = {'error': f'{type(e).__name__}: {e}'}
+    return out
+
+
+def sharded_configs(world, rank, dev):
+    """N > 1: BASELINE configs C4 and C5 as ONE dataset each, split into
+    contiguous per-rank ranges (wanproxy_amd/shard.py config_shard: C4 2^20/N
+    packets, C5 8 GiB/N), every rank encoding its range with a private cache
+    (wanproxy's one encoder + cache per codec,
+    programs/wanproxy/wanproxy_config_class_codec.cc:39-80).  Timed between
+    barriers, max wall over ranks; each rank checks a prefix of its range
+    against the oracle run on that range alone and decodes all of it back.
+    Returns aggregate GiB/s (strong scaling: the dataset is fixed)."""
+    import importlib.util
+    import torch
+    import torch.distributed as dist
+    spec = importlib.util.spec_from_file_location('configs_bench', os.path.join(ROOT, 'scripts', 'configs_bench.py'))
+    cb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cb)
+
+    def reduce(w):
+        if w is None:
+            dist.barrier()
+            return None
+        t = torch.tensor([w], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, world=world, rank=rank, reduce=reduce,
+                           no_decode=False, check_c4=16384, check_c5=512)
+    out = {}
+    for name, fn in (('C4', cb.run_c4), ('C5', cb.run_c5)):
+        err = ''
+        try:
+            r = fn(a)
+        except BaseException as e:          # SystemExit from a parity check included
+            r, err = None, f'{type(e).__name__}: {e}'
+        t = torch.tensor([0.0 if r is None else float(r['in_bytes']), 1.0 if err else 0.0, 0.0 if r is None else
+                          float(r['encode_wall_s'])], dtype=torch.float64, device=dev)
+        dist.all_reduce(t[:2], op=dist.ReduceOp.SUM)
+        tot, fails = float(t[0]), int(t[1])
+        if fails:
+            out[name] = {'error': f'{fails} rank(s) failed; rank {rank}: {err or "ok"}'}
+            continue
+        wall = r['encode_wall_s']           # already the max over ranks (reduce)
+        out[name] = {'value': round(tot / 2**30 / wall, 2), 'unit': 'GiB/s', 'scaling': 'strong',
+                     'dataset_bytes': int(tot), 'ms': round(wall * 1e3, 2), 'ranks': world,
+                     'rank0': {k: r[k] for k in ('config', 'shard', 'out_in', 'decode_GiBps', 'checked')}}
     return out
 
 
@@ -267,16 +534,14 @@ def main():
     torch.cuda.synchronize(dev)
     ctx.status()
 
-    # Parity check of this run's output against the CPU oracle (sampled chunks).
-    from oracle.lib import Oracle
+    # Parity of this run's output: every chunk against the CPU oracle.
     ol = d_ol.cpu().numpy()
-    sample = np.unique(np.linspace(0, n - 1, 16).astype(np.int64))
-    exp = Oracle().encode_batch(data, offs[sample], lens[sample], mode=0)
     outh = d_out.cpu().numpy()
-    for k, i in enumerate(sample):
-        got = outh[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()
-        if got != exp[k]:
+    exp = oracle_all(data, offs, lens, mode=0)
+    for i in range(n):
+        if outh[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() != exp[i]:
             raise SystemExit(f'PARITY FAILURE on chunk {i}')
+    del exp
     out_bytes = int(ol.sum())
     in_bytes = int(lens.astype(np.int64).sum())
 
@@ -297,8 +562,11 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP events on the launch stream
     ctx.status()
 
-    extras = {} if args.no_extras else side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol,
-                                                          d_st, n, stream, dev, rank)
+    extras = {}
+    if world == 1 and not args.no_extras:
+        extras = side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, d_st, n, stream, dev,
+                                   rank)
+    sharded = sharded_configs(world, rank, dev) if world > 1 and not args.no_configs else None
 
     from wanproxy_amd.shard import reduce_run
     wall, job_bytes = reduce_run(wall, in_bytes, device=dev)   # max wall, total bytes over ranks
@@ -307,6 +575,7 @@ def main():
 
     if rank == 0:
         achieved = (in_bytes + out_bytes) / (kern_ms * 1e-3) / 1e9
+        read = in_bytes / (kern_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(n)
         line = {
             'metric': 'XCodec encode GiB/s device-resident, batched 64 KiB chunks, 1/2/4/8 GPU',
@@ -326,15 +595,21 @@ def main():
                        'chunks_per_gpu': n, 'chunk_bytes': CHUNK, 'out_in_ratio': round(out_bytes / in_bytes, 5),
                        'parallelism': f'dp{world} (shard per GPU, no collective)'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / PEAK_HBM_GBS, 5), 'traffic': traffic, 'traffic_source': tsrc,
+                         'frac': round(achieved / PEAK_HBM_GBS, 5),
+                         'frac_read': round(read / PEAK_HBM_GBS, 5),
+                         'frac_note': 'frac: (input + output bytes) / kernel time / peak; frac_read: input bytes '
+                                      'only (the north star\'s HBM-read roofline)',
+                         'traffic': traffic, 'traffic_source': tsrc,
                          'kernel': 'encode_independent_kernel', 'kernel_ms': round(kern_ms, 4),
                          'algorithmic_bytes_per_launch': in_bytes + out_bytes},
         }
         line.update(extras)
+        if sharded is not None:
+            line['sharded_configs'] = sharded
         if world == 1 and not args.no_extras and not args.no_configs:
             line['configs'] = other_configs()
         if world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_passes)
+            line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

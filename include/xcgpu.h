@@ -272,6 +272,12 @@ uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
  * corrected by the verification.  Same output either way.  mode: -1
  * automatic (default), 0 never seed, 1 always seed.  Returns the previous mode. */
 int xcg_debug_set_stream_seed(int mode);
+/* Diagnostics / bench: while on, every stream-parse kernel launch
+ * (encode_stream_kernel) is bracketed by HIP events on its launch stream;
+ * xcg_debug_stream_kernel_time returns (and resets) the summed milliseconds
+ * and the launch count.  Process-wide.  Returns the previous setting. */
+int xcg_debug_stream_kernel_timing(int on);
+int xcg_debug_stream_kernel_time(double *ms, uint32_t *launches);
 
 /* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for
  * s in [0, len - 2048]. */

@@ -140,17 +140,27 @@ def check_prefix(data, offs, lens, got, k, what):
     return k
 
 
-def timed_encode(B: 'Batches', reps: int, clear_ctx=True):
+def torch_dev(args) -> int:
+    import torch
+    return torch.cuda.current_device()
+
+
+def timed_encode(B: 'Batches', reps: int, clear_ctx=True, reduce=None):
+    """Best of `reps` cold-cache encodes of the whole shard.  reduce: the
+    multi-GPU run's max-over-ranks (a barrier precedes every rep)."""
     import torch
     walls = []
     for _ in range(reps):
         if clear_ctx:
             B.ctx.cache_clear()
         torch.cuda.synchronize(B.dev)
+        if reduce is not None:
+            reduce(None)
         t0 = time.perf_counter()
         B.encode_all()
         torch.cuda.synchronize(B.dev)
-        walls.append(time.perf_counter() - t0)
+        w = time.perf_counter() - t0
+        walls.append(reduce(w) if reduce is not None else w)
     B.ctx.status()
     return min(walls)
 
@@ -228,65 +238,80 @@ def run_c3(args):
             'checked': f'warm-up first {k} chunks vs oracle; both passes decoded back to the input'}
 
 
+def _shard(name, args):
+    """This GPU's shard of dataset `name` (wanproxy_amd/shard.py): by default
+    one GPU's share of the 8-GPU split (rank 0 of 8), or --world / --rank."""
+    from wanproxy_amd.shard import shard_data
+    return shard_data(name, getattr(args, 'world', 8), getattr(args, 'rank', 0), args.scale)
+
+
+def _shard_desc(args, rng):
+    return 'rank %d of %d: stream bytes [%d, %d)' % (getattr(args, 'rank', 0), getattr(args, 'world', 8), *rng)
+
+
 def run_c4(args):
-    from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
-    n = max(64, int(131072 * args.scale))
-    data = np.frombuffer(synth.stream(0xC4, n * 4 * KiB, 4, 0), np.uint8).copy()
-    offs, lens = synth.chunks_of(data.tobytes(), 4 * KiB)
-    ctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
+    data, offs, lens, rng = _shard('C4', args)
+    n = offs.size
+    dev = torch_dev(args)
+    ctx = Context(dev, cache_segments=int(n * 2 * 1.05) + 4096)
     B = Batches(ctx, data, offs, lens, per=args.c4_batch)
-    wall = timed_encode(B, args.reps)
+    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None))
     got = B.outputs()
-    k = check_prefix(data, offs, lens, got, 2048, 'c4')
+    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c4', 2048), 'c4')
     dec, dsec = data.tobytes(), float('nan')
     if not args.no_decode:
-        dctx = Context(0, cache_segments=int(n * 2 * 1.05) + 4096)
+        dctx = Context(dev, cache_segments=int(n * 2 * 1.05) + 4096)
         dec, dsec = decode_device(dctx, got, per=args.c4_batch, chunk=4 * KiB)
+        dctx.close()
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c4)')
     inb = data.size
-    return {'config': 'C4 shard: %d x 4 KiB packets, dup 4, one cache' % n, 'batch_chunks': args.c4_batch,
-            'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
-            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
-            'rounds': B.rounds[:8], 'checked': f'first {k} packets vs oracle; full decode round trip'}
+    r = {'config': 'C4 shard: %d x 4 KiB packets, dup 4, one cache' % n, 'shard': _shard_desc(args, rng),
+         'batch_chunks': args.c4_batch, 'in_bytes': inb, 'encode_wall_s': wall,
+         'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+         'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+         'rounds': B.rounds[:8], 'checked': f'first {k} packets of the shard vs oracle; full decode round trip'}
+    ctx.close()
+    return r
 
 
 def run_c5(args):
-    from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
-    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
-    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
-    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    data, offs, lens, rng = _shard('C5', args)
+    nbytes = data.size
     segs = nbytes // 2048 + 4096
-    ctx = Context(0, cache_segments=segs)
+    dev = torch_dev(args)
+    ctx = Context(dev, cache_segments=segs)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
     B = Batches(ctx, data, offs, lens, per=per)
-    wall = timed_encode(B, args.reps)
+    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None))
     got = B.outputs()
-    k = check_prefix(data, offs, lens, got, 64, 'c5')
+    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c5', 512), 'c5')
     dec, dsec = data.tobytes(), float('nan')
     if not args.no_decode:
-        dctx = Context(0, cache_segments=segs)
+        dctx = Context(dev, cache_segments=segs)
         dec, dsec = decode_device(dctx, got, per=per, chunk=128 * KiB)
+        dctx.close()
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c5)')
     inb = data.size
-    return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, cold unbounded cache' % (nbytes >> 20),
-            'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
-            'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
-            'rounds': B.rounds, 'checked': f'first {k} chunks vs oracle; full decode round trip'}
+    r = {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, cold unbounded cache' % (nbytes >> 20),
+         'shard': _shard_desc(args, rng), 'in_bytes': inb, 'encode_wall_s': wall,
+         'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+         'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
+         'rounds': B.rounds, 'checked': f'first {k} chunks of the shard vs oracle; full decode round trip'}
+    ctx.close()
+    return r
 
 
 def run_c5lru(args):
     """C5 with wanproxy.conf's primary cache: a bounded 128 MiB
     XCodecMemoryCache (LRU eviction) instead of an unbounded one."""
     from oracle.lib import Oracle
-    from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
-    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
-    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
-    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    data, offs, lens, rng = _shard('C5', args)
+    nbytes = data.size
     limit = args.lru_mib * MiB
     ctx = Context(0, memory_cache_limit=limit)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
@@ -321,11 +346,9 @@ def run_c5pair(args):
     (programs/wanproxy/wanproxy.conf:8-26; xcodec/xcodec_cache.h:140-237,
     xcodec/xcodec_cache_disk.cc), every chunk checked against the oracle's pair."""
     from oracle.lib import Oracle
-    from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
-    nbytes = max(4 * MiB, int(1024 * MiB * args.scale) // (128 * KiB) * 128 * KiB)
-    data = np.frombuffer(synth.stream(0xC5, nbytes, 20, 0), np.uint8).copy()
-    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    data, offs, lens, rng = _shard('C5', args)
+    nbytes = data.size
     limit = max(2048, int(args.lru_mib * MiB * min(1.0, args.scale * 8)))
     disk = max(1 << 20, int(args.disk_mib * MiB * min(1.0, args.scale * 8)))
     ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU box: parity tests, then the C2 bench line without the CPU baseline / configs.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest.log; exit 1; }
+tail -2 gpurun_out/pytest.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-configs ${BENCH_ARGS} > gpurun_out/bench_q.json 2> gpurun_out/bench_q.err || { echo "bench failed"; tail -30 gpurun_out/bench_q.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/bench_q.json')); print(json.dumps({k: d[k] for k in ('value','stream_semantics','host_inclusive','tack_loop') if k in d}))"
+${EXTRA:-true}

@@ -28,22 +28,26 @@ def _free_port():
     return p
 
 
+SCALE = 64 / (1 << 20)          # C4 at 64 packets; C5 at 8 chunks of 128 KiB
+
+
 def _worker(rank, world, port, q):
     import torch.distributed as dist
     from oracle.lib import Oracle
-    from wanproxy_amd import synth
-    from wanproxy_amd.shard import reduce_run, shard_range
+    from wanproxy_amd.shard import reduce_run, shard_data
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    d = synth.stream(0xC4, 64 * 4096, 4, 0)
-    offs, lens = synth.chunks_of(d, 4096)
-    lo, hi = shard_range(offs.size, world, rank)
-    dist.barrier()
-    out = Oracle().encode_batch(d, offs[lo:hi], lens[lo:hi], mode=1)   # private cache per shard
-    dist.barrier()
-    wall, nbytes = reduce_run(0.1 * (rank + 1), int(lens[lo:hi].sum()))
-    q.put((rank, lo, hi, [len(o) for o in out], wall, nbytes))
+    res = {}
+    for name, scale in (('C4', SCALE), ('C5', 8 / 65536)):
+        # the partition bench.py --gpus N uses (sharded_configs -> configs_bench -> shard_data)
+        d, offs, lens, (lo, hi) = shard_data(name, world, rank, scale)
+        dist.barrier()
+        out = Oracle().encode_batch(d, offs, lens, mode=1)   # a private cache per shard
+        dist.barrier()
+        wall, nbytes = reduce_run(0.1 * (rank + 1), int(lens.astype(np.int64).sum()))
+        res[name] = (lo, hi, d.tobytes(), [len(o) for o in out], wall, nbytes)
+    q.put((rank, res))
     dist.destroy_process_group()
 
 
@@ -55,17 +59,20 @@ def test_two_rank_gloo_shards():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in procs)
+    res = dict(q.get(timeout=100) for _ in procs)
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    (r0, lo0, hi0, l0, w0, b0), (r1, lo1, hi1, l1, w1, b1) = res
-    assert (lo0, hi0, lo1, hi1) == (0, 32, 32, 64)
-    assert w0 == w1 == pytest.approx(0.2) and b0 == b1 == 64 * 4096
-    # each shard is an independent stream: rank 1's first packet sees an empty cache
     from oracle.lib import Oracle
     from wanproxy_amd import synth
-    d = synth.stream(0xC4, 64 * 4096, 4, 0)
-    offs, lens = synth.chunks_of(d, 4096)
-    exp1 = Oracle().encode_batch(d, offs[32:], lens[32:], mode=1)
-    assert l1 == [len(e) for e in exp1]
+    for name, unit, seed, dup, units in (('C4', 4096, 0xC4, 4, 64), ('C5', 128 << 10, 0xC5, 20, 8)):
+        (lo0, hi0, d0, l0, w0, b0), (lo1, hi1, d1, l1, w1, b1) = res[0][name], res[1][name]
+        # contiguous ranges of ONE stream that tile it
+        assert (lo0, hi0, lo1, hi1) == (0, units // 2 * unit, units // 2 * unit, units * unit)
+        full = synth.stream(seed, units * unit, dup, 0)
+        assert d0 + d1 == full
+        assert w0 == w1 == pytest.approx(0.2) and b0 == b1 == units * unit
+        # each shard is an independent stream: rank 1's first call sees an empty cache
+        offs, lens = synth.chunks_of(full, unit)
+        exp1 = Oracle().encode_batch(full, offs[units // 2:], lens[units // 2:], mode=1)
+        assert l1 == [len(e) for e in exp1]

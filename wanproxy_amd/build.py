@@ -56,5 +56,18 @@ def build_lib(force: bool = False, verbose: bool = False, out: str = OUT, define
     return out
 
 
+SYNTH_SRC = os.path.join(HERE, 'csrc/xcg_synth.c')
+SYNTH_OUT = os.path.join(HERE, 'libxcsynth.so')
+
+
+def build_synth(force: bool = False) -> str:
+    """The workload generator (csrc/xcg_synth.c: bench / test inputs, no GPU)."""
+    if force or not _newer(SYNTH_OUT, [SYNTH_SRC]):
+        subprocess.run(['gcc', '-O2', '-shared', '-fPIC', '-o', SYNTH_OUT + '.tmp', SYNTH_SRC], check=True)
+        os.replace(SYNTH_OUT + '.tmp', SYNTH_OUT)
+    return SYNTH_OUT
+
+
 if __name__ == '__main__':
     print(build_lib(force=True, verbose=True))
+    print(build_synth(force=True))

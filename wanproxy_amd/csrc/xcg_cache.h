@@ -124,6 +124,28 @@ __device__ __forceinline__ uint64_t tab_lookup(const HashTab& t, uint32_t lo, ui
   return ~0ull;
 }
 
+// Uniform lookup of one key in two tables at once: the first probe slot of
+// each (key and value words) is loaded together, so the common case (found
+// there, or an empty slot) costs one memory round trip instead of four.
+__device__ __forceinline__ uint64_t tab_probe_rest(const HashTab& t, uint64_t key, uint32_t i) {
+  for (uint32_t n = 1; n <= t.mask; ++n) {
+    i = (i + 1) & t.mask;
+    const uint64_t k = readfirst64(t.keys[i]);
+    if (k == key) return readfirst64(t.vals[i]);
+    if (k == EMPTY_KEY) break;
+  }
+  return ~0ull;
+}
+__device__ __forceinline__ void tab_lookup2(const HashTab& a, const HashTab& b, uint32_t lo, uint32_t hi,
+                                            uint64_t& va, uint64_t& vb) {
+  const uint64_t key = ((uint64_t)hi << 32) | lo;
+  const uint32_t ia = tab_slot(lo, hi, a.mask), ib = tab_slot(lo, hi, b.mask);
+  const uint64_t ka = a.keys[ia], xa = a.vals[ia], kb = b.keys[ib], xb = b.vals[ib];
+  const uint64_t ua = readfirst64(ka), ub = readfirst64(kb);
+  va = ua == key ? readfirst64(xa) : (ua == EMPTY_KEY ? ~0ull : tab_probe_rest(a, key, ia));
+  vb = ub == key ? readfirst64(xb) : (ub == EMPTY_KEY ? ~0ull : tab_probe_rest(b, key, ib));
+}
+
 // Per-thread exact lookup (each lane its own key): value or ~0 when absent.
 __device__ __forceinline__ uint64_t tab_lookup_t(const HashTab& t, uint32_t lo, uint32_t hi) {
   const uint64_t key = ((uint64_t)hi << 32) | lo;

@@ -30,7 +30,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "xcg_cache.h"
@@ -618,7 +620,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     ++ne;
   };
   auto cache_src = [&](uint32_t lo, uint32_t hi, int at) -> const uint8_t* {
-    const uint64_t gv = tab_lookup(prm.g, lo, hi);
+    uint64_t gv, bv;                               // (both tables probed in one round trip)
+    tab_lookup2(prm.g, prm.use_b ? prm.b : prm.g, lo, hi, gv, bv);
     if (gv != ~0ull) {
       if (!LRU) return prm.pool + gv * (uint64_t)SEG;
       const uint32_t t = 2u * (uint32_t)at + 1u;
@@ -629,7 +632,6 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       record(lo, hi, t, EV_GMISS, (uint32_t)gv);   // evicted earlier in the batch
     }
     if (prm.use_b) {
-      const uint64_t bv = tab_lookup(prm.b, lo, hi);
       if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) {
         if (nh < prm.maxh && l == 0) prm.hits[(uint64_t)chunk * prm.maxh + nh] = ((uint64_t)hi << 32) | lo;
         ++nh;
@@ -639,15 +641,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     }
     return nullptr;
   };
-  // Could the cache or the batch hold probe key k?  (lane filter, then the
-  // fingerprint bucket; no false negatives)
-  auto glb_maybe = [&](uint32_t k) -> bool {
+  // Could the cache or the batch hold probe key k?  (the LDS lane filter, no
+  // false negatives; the global-filter mode goes to the exact tables)
+  auto glb_pass = [&](uint32_t k) -> bool {
     if (gs.fmode == 0) return false;
-    uint32_t pass;
-    if (gs.fmode == 1) pass = filt_test(*(const uint32_t*)(gs.lds + gs.lfo + filt_word_ofs(k)), k);
-    else pass = gfilt_test(prm.lf.gfilt[gfilt_word(k, prm.lf.gmask)], k);
-    if (readfirst(pass) == 0u) return false;
-    return readfirst((uint32_t)ftab_match(prm.lf.ftab[fbucket(k, prm.lf.fmask)], k)) != 0u;
+    if (gs.fmode == 2) return true;
+    return readfirst(filt_test(*(const uint32_t*)(gs.lds + gs.lfo + filt_word_ofs(k)), k)) != 0u;
   };
   bool chain = false;                              // the last op was a REF
 
@@ -735,6 +734,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // xcodec_encoder.cc:374-416) before rolling 2048 positions; a miss goes
     // through the filters only, and a miss or a collision falls through to
     // the ordinary vector phase, which decides position s itself.
+    // The same holds right after a declaration: a candidate that survived its
+    // 2048 windows is declared here, at window s = cand + 2048, before that
+    // window's lookup (:183-196) -- and when the data repeats in 2 KiB blocks
+    // the window at the end of a new block is often the next REF.
+    int chain_miss = -1;
+    if (STREAM && !nullcache && !chain && have_cand && cand + SEG == s) {
+      declare(s);
+      chain = true;
+    }
     if (STREAM && chain && !nullcache) {
 #ifdef XCG_PHASES
       const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
@@ -751,7 +759,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const int d = lookup(lo, hi);                 // stream records carry their hi
       const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
       if (LRU && d >= 0) record(lo, hi, 2u * (uint32_t)s + 1u, EV_HIT, 0u);
-      if (src == nullptr && glb_maybe(probe_key(lo))) src = cache_src(lo, hi, s);
+      // (straight to the exact tables after the LDS lane filter: a chain probe
+      // hits often, and both tables cost one round trip together)
+      if (src == nullptr && glb_pass(probe_key(lo))) src = cache_src(lo, hi, s);
       if (src != nullptr && equal2048_u(src, x + s)) {
         wave_put_ref(out + olen, lo, hi);           // encode_reference :342-372
         olen += 10;
@@ -765,6 +775,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #endif
         continue;
       }
+      if (src == nullptr) chain_miss = s;          // an exact miss: the vector phase's event at s is moot
 #ifdef XCG_PHASES
       ph_chain += __builtin_amdgcn_s_memrealtime() - tc0;
 #endif
@@ -833,6 +844,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         const int nvalid = pe - q0;
         const uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
         ev &= vm;
+        if (STREAM && chain_miss >= 0) {         // (chain_miss == s: decided by the chain probe)
+          const int rel = chain_miss - p;
+          if (lane_id() == (rel >> 5)) ev &= ~(1u << (rel & 31));
+        }
       }
     }
     // The prefetch has had the vector phase to land; take it before the
@@ -882,7 +897,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         uint32_t lo = 0, hi = 0;
         int d = -1, fill = -1;
         for (;;) {
-          const uint2 hh = window_hash_u(fill >= 0 ? x + readfirst(T.rc[fill]) : x + s);
+          uint2 hh;
+          if (fill < 0 && ((s - p) & 31) == 0) {   // a lane's first window: the hash from registers
+            hh.x = 0u - readlane(k0, (s - p) >> 5);
+            hh.y = readfirst(lane_window_hi(P, (s - p) >> 5));
+          } else {
+            hh = window_hash_u(fill >= 0 ? x + readfirst(T.rc[fill]) : x + s);
+          }
           if (fill >= 0) {
             if (l == 0) T.rhi[fill] = hh.y;
             __builtin_amdgcn_wave_barrier();
@@ -1371,6 +1392,53 @@ static bool stream_debug() {
   return on;
 }
 
+// Live timing of the stream-parse kernel for bench.py's roofline: while on,
+// every encode_stream_kernel launch is bracketed by HIP events on its own
+// launch stream; xcg_debug_stream_kernel_time sums them (process-wide).
+namespace {
+std::mutex g_ktime_mu;
+bool g_ktime_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ktime_ev;
+}  // namespace
+extern "C" int xcg_debug_stream_kernel_timing(int on) {
+  std::lock_guard<std::mutex> g(g_ktime_mu);
+  const int old = g_ktime_on;
+  g_ktime_on = on != 0;
+  return old;
+}
+extern "C" int xcg_debug_stream_kernel_time(double* ms, uint32_t* launches) {
+  std::lock_guard<std::mutex> g(g_ktime_mu);
+  double tot = 0;
+  int rc = 0;
+  for (auto& e : g_ktime_ev) {
+    float t = 0;
+    if (hipEventSynchronize(e.second) != hipSuccess || hipEventElapsedTime(&t, e.first, e.second) != hipSuccess)
+      rc = -5;
+    tot += t;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (ms) *ms = tot;
+  if (launches) *launches = (uint32_t)g_ktime_ev.size();
+  g_ktime_ev.clear();
+  return rc;
+}
+static hipEvent_t ktime_begin(hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_ktime_mu);
+  hipEvent_t e = nullptr;
+  if (!g_ktime_on || hipEventCreate(&e) != hipSuccess) return nullptr;
+  (void)hipEventRecord(e, s);
+  return e;
+}
+static void ktime_end(hipEvent_t e0, hipStream_t s) {
+  if (!e0) return;
+  std::lock_guard<std::mutex> g(g_ktime_mu);
+  hipEvent_t e1 = nullptr;
+  if (hipEventCreate(&e1) != hipSuccess) return;
+  (void)hipEventRecord(e1, s);
+  g_ktime_ev.emplace_back(e0, e1);
+}
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
   using namespace xcg;
   const uint32_t n = a->n;
@@ -1431,8 +1499,10 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       }
       fprintf(stderr, "stream: launch over %u of %u chunks (skip below %u)\n", cnt, n, prm.skip_below);
     }
+    hipEvent_t e0 = ktime_begin(stream);
     if (prm.ev) launch_sw(std::integral_constant<bool, true>{});
     else launch_sw(std::integral_constant<bool, false>{});
+    ktime_end(e0, stream);
   };
   // lowest chunk whose declaration list changed in the round just run (~0u: none)
   auto changed_after = [&](uint32_t& fc) -> bool {

@@ -20,6 +20,39 @@ def shard_range(n_units: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + q + (1 if rank < r else 0)
 
 
+# BASELINE.json's partitioned datasets: ONE synthetic stream
+# per configuration, cut into contiguous unit ranges, one per rank.
+#   C4: 1 M x 4 KiB packets (seed 0xC4, dup 4), each packet one encode() call
+#   C5: 8 GiB (seed 0xC5, dup 20) in 128 KiB encode() calls
+DATASETS = {
+    'C4': {'seed': 0xC4, 'dup': 4, 'unit': 4096, 'units': 1 << 20},
+    'C5': {'seed': 0xC5, 'dup': 20, 'unit': 128 << 10, 'units': 65536},
+}
+
+
+def config_shard(name: str, world: int, rank: int, scale: float = 1.0):
+    """Rank `rank`'s share of dataset `name` split over `world` ranks:
+    (seed, dup, unit bytes, first byte, end byte) of the one stream.  bench.py
+    (--gpus N), scripts/configs_bench.py (N=1 runs one GPU's shard of 8) and
+    tests/test_shard_gloo.py all cut the data through here."""
+    d = DATASETS[name]
+    units = max(world, int(d['units'] * scale))
+    lo, hi = shard_range(units, world, rank)
+    return d['seed'], d['dup'], d['unit'], lo * d['unit'], hi * d['unit']
+
+
+def shard_data(name: str, world: int, rank: int, scale: float = 1.0):
+    """The shard's bytes and its encode() calls (offsets relative to the
+    shard): (data, offsets, lengths, (first byte, end byte) in the stream)."""
+    import numpy as np
+    from wanproxy_amd import synth
+    seed, dup, unit, lo, hi = config_shard(name, world, rank, scale)
+    data = synth.stream_range(seed, dup, 0, lo, hi)
+    offs = np.arange(0, hi - lo, unit, dtype=np.uint64)
+    lens = np.minimum(unit, (hi - lo) - offs.astype(np.int64)).astype(np.uint32)
+    return data, offs, lens, (lo, hi)
+
+
 def reduce_run(wall_s: float, bytes_done: int, device=None):
     """Whole-job (max wall over ranks, total bytes) -- identity without a
     process group."""

@@ -37,45 +37,97 @@ def _draw1(seed: int, i: int) -> int:
     return int(_draw(seed, np.array([i], dtype=np.uint64))[0])
 
 
+_CTL = {}
+
+
+def _control(seed: int, nblocks: int, dup_pct: int, magic_pct: int):
+    """The generator's sequential control walk over the first `nblocks` blocks:
+    (draw index of the first body draw of each fresh block, fresh-block id of
+    each block).  Cached per (seed, dup, magic) and extended on demand."""
+    key = (seed, dup_pct, magic_pct)
+    st = _CTL.get(key)
+    if st is None:
+        st = _CTL[key] = {'pos': 0, 'fresh': [], 'order': []}
+    fresh_starts, order = st['fresh'], st['order']
+    if len(order) < nblocks:
+        per_fresh = 256 + (SEG if magic_pct else 0)
+        pos = st['pos']
+        cache_base, cache = -1, None
+
+        def ctl(i: int) -> int:
+            nonlocal cache_base, cache
+            if cache is None or not (cache_base <= i < cache_base + len(cache)):
+                cache_base = i
+                cache = _draw(seed, np.arange(i, i + 4096, dtype=np.uint64)).tolist()
+            return cache[i - cache_base]
+
+        for _ in range(nblocks - len(order)):
+            if fresh_starts and dup_pct > 0:
+                r = ctl(pos); pos += 1
+                if r % 100 < dup_pct:
+                    order.append(ctl(pos) % len(fresh_starts)); pos += 1
+                    continue
+            elif fresh_starts:
+                pos += 1          # `r.next() % 100 < 0` still consumes a draw
+            fresh_starts.append(pos)
+            order.append(len(fresh_starts) - 1)
+            pos += per_fresh
+        st['pos'] = pos
+    return fresh_starts, order
+
+
+_SYNTH = None
+
+
+def _csynth():
+    """csrc/xcg_synth.c (built by build.py / __graft_entry__.build()), or None."""
+    global _SYNTH
+    if _SYNTH is None:
+        import ctypes as C
+        import os
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libxcsynth.so')
+        _SYNTH = False
+        if os.path.exists(p):
+            L = C.CDLL(p)
+            L.xcs_stream_range.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p]
+            L.xcs_stream_range.restype = C.c_int
+            _SYNTH = L
+    return _SYNTH or None
+
+
+def stream_range(seed: int, dup_pct: int, magic_pct: int, lo: int, hi: int, use_c: bool = True) -> np.ndarray:
+    """Bytes [lo, hi) of the generator's stream (any stream of >= hi bytes has
+    this prefix), built so memory stays ~ (hi - lo): a rank's shard of a long
+    stream without materialising the rest.  Uses the C build of
+    the same generator when present (8 GiB streams), else numpy."""
+    if hi <= lo:
+        return np.zeros(0, np.uint8)
+    L = _csynth() if use_c else None
+    if L is not None:
+        out = np.empty(hi - lo, np.uint8)
+        if L.xcs_stream_range(seed & M64, dup_pct, magic_pct, lo, hi, out.ctypes.data) != 0:
+            raise MemoryError('xcs_stream_range')
+        return out
+    b0, b1 = lo // SEG, (hi + SEG - 1) // SEG
+    fresh_starts, order = _control(seed, b1, dup_pct, magic_pct)
+    starts = np.asarray(fresh_starts, dtype=np.uint64)
+    ords = np.asarray(order[b0:b1], dtype=np.int64)
+    out = np.empty((b1 - b0) * SEG, np.uint8)
+    PIECE = 16384
+    for a in range(0, b1 - b0, PIECE):
+        st = starts[ords[a:a + PIECE]]
+        body_idx = st[:, None] + np.arange(256, dtype=np.uint64)[None, :]
+        blk = _draw(seed, body_idx).astype('<u8').view(np.uint8).reshape(st.size, SEG)
+        if magic_pct:
+            midx = st[:, None] + np.uint64(256) + np.arange(SEG, dtype=np.uint64)[None, :]
+            blk[(_draw(seed, midx) % np.uint64(100)) < np.uint64(magic_pct)] = 0xF1
+        out[a * SEG:(a + st.size) * SEG] = blk.reshape(-1)
+    return out[lo - b0 * SEG:hi - b0 * SEG]
+
+
 def stream(seed: int, nbytes: int, dup_pct: int, magic_pct: int = 0) -> bytes:
     """Bit-exact port of BASELINE.md's `stream(seed, nbytes, dup, magic)`."""
-    nblocks = (nbytes + SEG - 1) // SEG
-    # Walk the control draws sequentially (2 per dup, 1 + 256 [+2048] per fresh).
-    per_fresh = 256 + (SEG if magic_pct else 0)
-    pos = 0
-    fresh_starts = []      # draw index of the first body draw of each fresh block
-    order = np.empty(nblocks, dtype=np.int64)   # fresh-block id of each block
-    # Control draws are needed one at a time; batch them lazily.
-    cache_base, cache = -1, None
-
-    def ctl(i: int) -> int:
-        nonlocal cache_base, cache
-        if cache is None or not (cache_base <= i < cache_base + len(cache)):
-            cache_base = i
-            cache = _draw(seed, np.arange(i, i + 4096, dtype=np.uint64))
-        return int(cache[i - cache_base])
-
-    for b in range(nblocks):
-        if fresh_starts and dup_pct > 0:
-            r = ctl(pos); pos += 1
-            if r % 100 < dup_pct:
-                k = ctl(pos) % len(fresh_starts); pos += 1
-                order[b] = k
-                continue
-        elif fresh_starts:
-            pos += 1          # `r.next() % 100 < 0` still consumes a draw
-        fresh_starts.append(pos)
-        order[b] = len(fresh_starts) - 1
-        pos += per_fresh
-    starts = np.array(fresh_starts, dtype=np.uint64)
-    body_idx = starts[:, None] + np.arange(256, dtype=np.uint64)[None, :]
-    blocks = _draw(seed, body_idx).astype('<u8').view(np.uint8).reshape(len(starts), SEG).copy()
-    if magic_pct:
-        midx = starts[:, None] + np.uint64(256) + np.arange(SEG, dtype=np.uint64)[None, :]
-        m = (_draw(seed, midx) % np.uint64(100)) < np.uint64(magic_pct)
-        blocks[m] = 0xF1
-    out = blocks[order].reshape(-1)[:nbytes]
-    return out.tobytes()
+    return stream_range(seed, dup_pct, magic_pct, 0, nbytes).tobytes()
 
 
 def stream_ref(seed: int, nbytes: int, dup_pct: int, magic_pct: int = 0) -> bytes:

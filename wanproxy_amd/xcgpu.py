@@ -120,6 +120,10 @@ def lib():
     L.xcg_pipe_pending_frames.restype = C.c_uint32
     L.xcg_debug_set_stream_seed.argtypes = [C.c_int]
     L.xcg_debug_set_stream_seed.restype = C.c_int
+    L.xcg_debug_stream_kernel_timing.argtypes = [C.c_int]
+    L.xcg_debug_stream_kernel_timing.restype = C.c_int
+    L.xcg_debug_stream_kernel_time.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+    L.xcg_debug_stream_kernel_time.restype = C.c_int
     L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     _lib = L
@@ -135,6 +139,15 @@ def _stream_ptr(stream):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return C.c_void_p(s.cuda_stream)
+
+
+def stream_kernel_time():
+    """(milliseconds, launches) of the stream-parse kernel since the last call,
+    timed by HIP events on its launch stream while xcg_debug_stream_kernel_timing
+    is on (bench.py's roofline for stream semantics)."""
+    ms, k = C.c_double(), C.c_uint32()
+    _check(lib().xcg_debug_stream_kernel_time(C.byref(ms), C.byref(k)))
+    return float(ms.value), int(k.value)
 
 
 def encode_bound(n: int) -> int:
