@@ -175,6 +175,29 @@ int xcg_encode_host(xcg_ctx *ctx, int semantics, const uint8_t *h_in, uint64_t i
                     const uint64_t *h_chunk_off, const uint32_t *h_chunk_len, uint32_t n, uint8_t *h_out,
                     uint64_t out_cap, const uint64_t *h_out_off, uint64_t *h_out_len);
 
+/* *h_nref of xcg_encode_call on a cache whose lookups change nothing (an
+ * unbounded memory cache, the null cache): no reference list is kept. */
+#define XCG_NO_REFERENCES 0xFFFFFFFFu
+
+/* One XCodecEncoder::encode(output, input) call from host memory, the way tack
+ * (programs/tack/tack.cc:308-321, one call per <= 64 KiB read) and
+ * XCodecPipePair (xcodec/xcodec_pipe_pair.cc:596-618, per <= 512 KiB frame)
+ * make it -- stream semantics on the context's persistent cache.  h_in[0 .. len)
+ * is encoded into h_out (out_cap >= xcg_encode_bound(len)); the call's
+ * declarations come back in order (hash and input offset, encode_declaration
+ * xcodec_encoder.cc:276-313) and, on a bounded or pair cache, its cache
+ * references in stream order (kind: 0 enter, 1 hit on a declaration of the
+ * call, 2 hit on a cached entry, 3 lookup of an entry evicted earlier in the
+ * call; idx: the declaration number of an enter), else *h_nref =
+ * XCG_NO_REFERENCES.  The reference-class adapters (integration/) replay these
+ * into the host XCodecCache.  The context keeps its staging buffers and stream,
+ * so a call allocates nothing and synchronises once (unbounded caches).
+ * *h_ndecl / *h_nref may exceed the caps (then only the first cap are written). */
+int xcg_encode_call(xcg_ctx *ctx, const uint8_t *h_in, uint32_t len, uint8_t *h_out, uint64_t out_cap,
+                    uint64_t *h_out_len, uint64_t *h_decl_hash, uint32_t *h_decl_pos, uint32_t decl_cap,
+                    uint32_t *h_ndecl, uint64_t *h_ref_hash, uint32_t *h_ref_kind, uint32_t *h_ref_idx,
+                    uint32_t ref_cap, uint32_t *h_nref);
+
 /*
  * Decode n encoded chunks that form ONE stream (successive
  * XCodecDecoder::decode calls on one decoder whose cache is the context's

@@ -62,24 +62,25 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 	std::vector<uint8_t> in(len);
 	input->moveout(&in[0], len);
 
-	const uint64_t off = 0;
-	const uint64_t ooff = 0;
+	/*
+	 * One engine call: the output, the call's declarations in order
+	 * (encode_declaration, :276-313) and, on a bounded or pair cache, its
+	 * cache references in stream order -- one host synchronisation.
+	 */
 	uint64_t olen = 0;
 	std::vector<uint8_t> out(xcg_encode_bound(len));
-	int rc = xcg_encode_host(ctx, XCG_SEM_STREAM, &in[0], len, &off, &len, 1, &out[0], out.size(), &ooff, &olen);
-	if (rc != XCG_OK)
-		HALT(log_) << "xcgpu encode failed: " << xcg_strerror(rc);
-	output->append(&out[0], olen);
-
-	/* Declarations made by this call, in order (encode_declaration, :276-313). */
-	uint32_t ndecl = 0;
+	uint32_t ndecl = 0, nref = 0;
 	std::vector<uint64_t> dh(len / XCODEC_SEGMENT_LENGTH + 1);
 	std::vector<uint32_t> dp(dh.size());
-	if (!xcgpu_binding::is_null_cache(cache_)) {
-		rc = xcg_last_declarations(ctx, 0, &dh[0], &dp[0], dh.size(), &ndecl);
-		if (rc != XCG_OK)
-			HALT(log_) << "xcgpu declarations: " << xcg_strerror(rc);
-	}
+	std::vector<uint64_t> rh(2 * dh.size() + 64);
+	std::vector<uint32_t> rk(rh.size()), rr(rh.size());
+	int rc = xcg_encode_call(ctx, &in[0], len, &out[0], out.size(), &olen, &dh[0], &dp[0], dh.size(), &ndecl,
+	                         &rh[0], &rk[0], &rr[0], rh.size(), &nref);
+	if (rc != XCG_OK)
+		HALT(log_) << "xcgpu encode failed: " << xcg_strerror(rc);
+	if (ndecl > dh.size())
+		HALT(log_) << "xcgpu declarations: list overflow.";
+	output->append(&out[0], olen);
 
 	/*
 	 * The host cache mirror.  On a bounded or pair cache every lookup that
@@ -88,12 +89,9 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 	 * references are replayed in stream order; on an unbounded memory cache
 	 * only the enters matter.
 	 */
-	uint32_t nref = 0;
-	std::vector<uint64_t> rh(2 * dh.size() + 64);
-	std::vector<uint32_t> rk(rh.size()), rr(rh.size());
-	rc = xcgpu_binding::is_null_cache(cache_) ? XCG_ENOTSUP
-	     : xcg_last_references(ctx, 0, &rh[0], &rk[0], &rr[0], rh.size(), &nref);
-	if (rc == XCG_OK) {
+	if (xcgpu_binding::is_null_cache(cache_)) {
+		/* TackNullCache: nothing to keep. */
+	} else if (nref != XCG_NO_REFERENCES) {
 		if (nref > rh.size())
 			HALT(log_) << "xcgpu references: list overflow.";
 		for (uint32_t i = 0; i < nref; i++) {
@@ -109,14 +107,12 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 					seg->unref();
 			}
 		}
-	} else if (rc == XCG_ENOTSUP) {
+	} else {
 		for (uint32_t i = 0; i < ndecl; i++) {
 			BufferSegment *seg = segment_of(&in[dp[i]]);
 			cache_->enter(dh[i], seg);
 			seg->unref();
 		}
-	} else {
-		HALT(log_) << "xcgpu references: " << xcg_strerror(rc);
 	}
 
 	if (refmap == NULL)

@@ -177,6 +177,12 @@ struct xcg_ctx {
   hipEvent_t done_ev = nullptr;
   XcgPairState* pair = nullptr;    // XCodecCachePair(memory, disk) (xcg_pair.hip)
   uint32_t pair_C = 0;             // its primary limit in segments
+  // Host-call staging (xcg_encode_call / xcg_encode_host): kept across calls,
+  // so a per-call encode() allocates nothing and synchronises once.
+  uint8_t* stage_h = nullptr;      // pinned
+  uint8_t* stage_d = nullptr;
+  size_t stage_h_cap = 0, stage_d_cap = 0;
+  hipStream_t call_st = nullptr;
 };
 
 namespace {
@@ -258,17 +264,55 @@ void free_scratch(BatchScratch& b) {
   b = BatchScratch{};
 }
 
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// The context's host-call staging: pinned host and device blocks of at least
+// the given sizes, and its own stream.
+int ensure_stage(xcg_ctx* c, size_t dbytes, size_t hbytes) {
+  if (!c->call_st && hipStreamCreateWithFlags(&c->call_st, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
+  if (dbytes > c->stage_d_cap) {
+    if (c->stage_d) { (void)hipStreamSynchronize(c->call_st); (void)hipFree(c->stage_d); }
+    c->stage_d = nullptr;
+    c->stage_d_cap = 0;
+    const size_t want = dbytes < (1u << 20) ? (1u << 20) : dbytes;
+    if (hipMalloc(&c->stage_d, want) != hipSuccess) return XCG_ENOMEM;
+    c->stage_d_cap = want;
+  }
+  if (hbytes > c->stage_h_cap) {
+    if (c->stage_h) { (void)hipStreamSynchronize(c->call_st); (void)hipHostFree(c->stage_h); }
+    c->stage_h = nullptr;
+    c->stage_h_cap = 0;
+    const size_t want = hbytes < (1u << 20) ? (1u << 20) : hbytes;
+    if (hipHostMalloc(&c->stage_h, want, hipHostMallocDefault) != hipSuccess) return XCG_ENOMEM;
+    c->stage_h_cap = want;
+  }
+  return XCG_OK;
+}
+
+// Every array of an empty cache in one launch: the table (all ones), the
+// segment count and the three probe filters (zero).
+__global__ __launch_bounds__(256) void cache_wipe_kernel(uint4* kv, uint64_t kv_n, uint32_t* nseg, uint4* filt,
+                                                         uint32_t filt_n, uint4* ftab, uint64_t ftab_n, uint4* gfilt,
+                                                         uint64_t gfilt_n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t i = i0; i < kv_n; i += stride) kv[i] = ones;
+  for (uint64_t i = i0; i < filt_n; i += stride) filt[i] = zero;
+  for (uint64_t i = i0; i < ftab_n; i += stride) ftab[i] = zero;
+  for (uint64_t i = i0; i < gfilt_n; i += stride) gfilt[i] = zero;
+  if (i0 == 0) *nseg = 0u;
+}
+
 int clear_cache(GpuCache& g) {
-  // (asynchronous fills + one sync: a synchronous hipMemset of a fresh
-  // buffer costs milliseconds)
-  if (hipMemsetAsync(g.keys, 0xFF, 8ull * (g.mask + 1), nullptr) != hipSuccess ||
-      hipMemsetAsync(g.vals, 0xFF, 8ull * (g.mask + 1), nullptr) != hipSuccess ||
-      hipMemsetAsync(g.nseg, 0, 4, nullptr) != hipSuccess ||
-      hipMemsetAsync(g.filt, 0, 4ull * FILT_WORDS, nullptr) != hipSuccess ||
-      hipMemsetAsync(g.ftab, 0, 16ull * (g.fmask + 1), nullptr) != hipSuccess ||
-      hipMemsetAsync(g.gfilt, 0, 4ull * (g.gmask + 1), nullptr) != hipSuccess ||
-      hipStreamSynchronize(nullptr) != hipSuccess)
-    return XCG_EHIP;
+  // keys and vals are separate allocations of (mask + 1) u64 each (>= 1024)
+  const uint64_t half = (uint64_t)(g.mask + 1) / 2;   // uint4 per array
+  hipLaunchKernelGGL(cache_wipe_kernel, dim3(1024), dim3(256), 0, nullptr, (uint4*)g.keys, half, g.nseg,
+                     (uint4*)g.filt, FILT_WORDS / 4, (uint4*)g.ftab, (uint64_t)g.fmask + 1, (uint4*)g.gfilt,
+                     ((uint64_t)g.gmask + 1) / 4);
+  hipLaunchKernelGGL(cache_wipe_kernel, dim3(256), dim3(256), 0, nullptr, (uint4*)g.vals, half, g.nseg,
+                     (uint4*)nullptr, 0u, (uint4*)nullptr, 0ull, (uint4*)nullptr, 0ull);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) return XCG_EHIP;
   return XCG_OK;
 }
 
@@ -509,6 +553,9 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   window_free(c->own_win);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   xcg_pair_state_destroy(c->pair);
+  if (c->stage_h) (void)hipHostFree(c->stage_h);
+  (void)hipFree(c->stage_d);
+  if (c->call_st) (void)hipStreamDestroy(c->call_st);
   delete c;
 }
 
@@ -860,59 +907,136 @@ int xcg_encode_host(xcg_ctx* c, int semantics, const uint8_t* h_in, uint64_t in_
     if (h_chunk_len[i] > maxlen) maxlen = h_chunk_len[i];
   }
   DeviceGuard g(c->device);
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  uint64_t *d_off = nullptr, *d_oo = nullptr, *d_ol = nullptr;
-  uint32_t* d_len = nullptr;
-  int rc = XCG_OK;
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
-  do {
-    if (hipMalloc(&d_in, in_len ? in_len : 1) != hipSuccess || hipMalloc(&d_out, out_cap ? out_cap : 1) != hipSuccess ||
-        hipMalloc(&d_off, 8ull * n) != hipSuccess || hipMalloc(&d_oo, 8ull * n) != hipSuccess ||
-        hipMalloc(&d_ol, 8ull * n) != hipSuccess || hipMalloc(&d_len, 4ull * n) != hipSuccess) {
-      rc = XCG_ENOMEM;
-      break;
+  // staging (kept by the context): [off n][oo n][ol n][len n] | input | output slots
+  const size_t meta = align256(28ull * n), inb = align256(in_len ? in_len : 1), outb = align256(out_cap ? out_cap : 1);
+  int rc = ensure_stage(c, meta + inb + outb, meta + inb + outb);
+  if (rc != XCG_OK) return rc;
+  uint8_t* hm = c->stage_h;
+  uint8_t* dm = c->stage_d;
+  memcpy(hm, h_chunk_off, 8ull * n);
+  memcpy(hm + 8ull * n, h_out_off, 8ull * n);
+  memcpy(hm + 24ull * n, h_chunk_len, 4ull * n);
+  memcpy(hm + meta, h_in, in_len);
+  const hipStream_t st = c->call_st;
+  const uint64_t* d_off = (const uint64_t*)dm;
+  const uint64_t* d_oo = (const uint64_t*)(dm + 8ull * n);
+  uint64_t* d_ol = (uint64_t*)(dm + 16ull * n);
+  const uint32_t* d_len = (const uint32_t*)(dm + 24ull * n);
+  uint8_t* d_out = dm + meta + inb;
+  if (hipMemcpyAsync(dm, hm, meta + in_len, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
+  rc = xcg_encode_batch(c, semantics, dm + meta, d_off, d_len, n, maxlen, d_out, d_oo, d_ol, nullptr, st);
+  if (rc != XCG_OK) return rc;
+  uint64_t* ol = (uint64_t*)(hm + 16ull * n);
+  if (hipMemcpyAsync(ol, d_ol, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return XCG_EHIP;
+  if (*c->h_status) return XCG_EOVERFLOW;
+  // only the bytes each slot holds come back
+  uint8_t* ho = hm + meta + inb;
+  for (uint32_t i = 0; i < n; ++i) {
+    h_out_len[i] = ol[i];
+    if (ol[i] && hipMemcpyAsync(ho + h_out_off[i], d_out + h_out_off[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
+      return XCG_EHIP;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
+  for (uint32_t i = 0; i < n; ++i)
+    if (ol[i]) memcpy(h_out + h_out_off[i], ho + h_out_off[i], ol[i]);
+  return XCG_OK;
+}
+
+int xcg_encode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_out, uint64_t out_cap,
+                    uint64_t* h_out_len, uint64_t* h_decl_hash, uint32_t* h_decl_pos, uint32_t decl_cap,
+                    uint32_t* h_ndecl, uint64_t* h_ref_hash, uint32_t* h_ref_kind, uint32_t* h_ref_idx, uint32_t ref_cap,
+                    uint32_t* h_nref) {
+  if (!c || !h_out_len || !h_ndecl || !h_nref || (len && (!h_in || !h_out))) return XCG_EINVAL;
+  *h_out_len = 0;
+  *h_ndecl = 0;
+  *h_nref = (c->bounded || c->pair) ? 0u : XCG_NO_REFERENCES;
+  if (len == 0) return XCG_OK;
+  if (out_cap < xcg_encode_bound(len) || len > (1u << 19)) return XCG_EINVAL;
+  DeviceGuard g(c->device);
+  const bool nullc = (c->flags & XCG_FLAG_NULLCACHE) != 0;
+  const bool refs = (c->bounded || c->pair) && !nullc;
+  const uint32_t maxd = len / XCG_SEGMENT_LENGTH + 1;
+  // staging: device [off 8][oo 8][ol 8][len 4] | input | output slot;
+  //          host   the same head, then [ndecl 4][nev 4] | decl rows | event rows | output
+  const uint64_t bound = xcg_encode_bound(len);
+  const size_t inb = align256(len), outb = align256(bound);
+  const size_t rows_d = align256(16ull * maxd);
+  size_t rows_e = 0;
+  if (refs) {
+    int rc0 = ensure_cache(c);
+    if (rc0 == XCG_OK) rc0 = ensure_scratch(c, 1, maxd);
+    if (rc0 != XCG_OK) return rc0;
+    rows_e = align256(16ull * c->bs.maxe);
+  }
+  int rc = ensure_stage(c, 256 + inb + outb, 256 + inb + 256 + rows_d + rows_e + outb);
+  if (rc != XCG_OK) return rc;
+  uint8_t* hm = c->stage_h;
+  uint8_t* dm = c->stage_d;
+  uint64_t* hmeta = (uint64_t*)hm;
+  hmeta[0] = 0;                                      // chunk offset
+  hmeta[1] = 0;                                      // output slot offset
+  hmeta[2] = 0;
+  *(uint32_t*)(hm + 24) = len;
+  memcpy(hm + 256, h_in, len);
+  const hipStream_t st = c->call_st;
+  uint8_t* d_out = dm + 256 + inb;
+  if (hipMemcpyAsync(dm, hm, 256 + len, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
+  rc = xcg_encode_batch(c, XCG_SEM_STREAM, dm + 256, (const uint64_t*)dm, (const uint32_t*)(dm + 24), 1, len, d_out,
+                        (const uint64_t*)(dm + 8), (uint64_t*)(dm + 16), nullptr, st);
+  if (rc != XCG_OK) return rc;
+  // everything the call produced, back in one synchronisation
+  uint8_t* hres = hm + 256 + inb;
+  uint32_t* hcnt = (uint32_t*)hres;                  // [0] ndecl, [1] nev
+  uint8_t* hdecl = hres + 256;
+  uint8_t* hev = hdecl + rows_d;
+  uint8_t* hout = hev + rows_e;
+  const bool stream_rows = !nullc;                   // (a null cache parses without declaration rows)
+  if (hipMemcpyAsync(hm + 16, dm + 16, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(hout, d_out, bound, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return XCG_EHIP;
+  if (stream_rows && (hipMemcpyAsync(hcnt, c->bs.ndecl, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                      hipMemcpyAsync(hdecl, c->bs.decl, 16ull * maxd, hipMemcpyDeviceToHost, st) != hipSuccess))
+    return XCG_EHIP;
+  if (refs && (hipMemcpyAsync(hcnt + 1, c->bs.nev, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(hev, c->bs.ev, 16ull * c->bs.maxe, hipMemcpyDeviceToHost, st) != hipSuccess))
+    return XCG_EHIP;
+  if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
+  if (*c->h_status) return XCG_EOVERFLOW;
+  const uint64_t olen = hmeta[2];
+  if (olen > bound) return XCG_EHIP;
+  memcpy(h_out, hout, olen);
+  *h_out_len = olen;
+  if (stream_rows) {
+    const uint32_t nd = hcnt[0];
+    *h_ndecl = nd;
+    const uint32_t k = nd < decl_cap ? nd : decl_cap;
+    const uint32_t* r = (const uint32_t*)hdecl;
+    for (uint32_t i = 0; i < k; ++i) {
+      if (h_decl_hash) h_decl_hash[i] = ((uint64_t)r[4 * i + 1] << 32) | r[4 * i];
+      if (h_decl_pos) h_decl_pos[i] = r[4 * i + 2];
     }
-    if (hipMemcpyAsync(d_in, h_in, in_len, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_off, h_chunk_off, 8ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_oo, h_out_off, 8ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_len, h_chunk_len, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess) {
-      rc = XCG_EHIP;
-      break;
+  }
+  if (refs) {
+    const uint32_t ne = hcnt[1];
+    if (ne > c->bs.maxe) return XCG_EOVERFLOW;
+    *h_nref = ne;
+    const uint32_t* e = (const uint32_t*)hev;
+    std::vector<uint32_t> order(ne);
+    for (uint32_t i = 0; i < ne; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return e[4 * a + 2] < e[4 * b + 2]; });
+    const uint32_t k = ne < ref_cap ? ne : ref_cap;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t* v = e + 4ull * order[j];
+      if (h_ref_hash) h_ref_hash[j] = ((uint64_t)v[1] << 32) | v[0];
+      if (h_ref_kind) h_ref_kind[j] = v[3] >> 30;
+      if (h_ref_idx) h_ref_idx[j] = v[3] & ((1u << 30) - 1u);
     }
-    rc = xcg_encode_batch(c, semantics, d_in, d_off, d_len, n, maxlen, d_out, d_oo, d_ol, nullptr, st);
-    if (rc != XCG_OK) break;
-    std::vector<uint64_t> ol(n);
-    if (hipMemcpyAsync(ol.data(), d_ol, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-      rc = XCG_EHIP;
-      break;
-    }
-    // Copy back only the bytes each slot actually holds.
-    for (uint32_t i = 0; i < n; ++i) {
-      h_out_len[i] = ol[i];
-      if (ol[i] && hipMemcpyAsync(h_out + h_out_off[i], d_out + h_out_off[i], ol[i], hipMemcpyDeviceToHost, st) !=
-                       hipSuccess) {
-        rc = XCG_EHIP;
-        break;
-      }
-    }
-    if (rc == XCG_OK && hipStreamSynchronize(st) != hipSuccess) rc = XCG_EHIP;
-    int32_t status = 0;
-    if (rc == XCG_OK && (hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                         hipStreamSynchronize(st) != hipSuccess))
-      rc = XCG_EHIP;
-    status = *c->h_status;
-    if (rc == XCG_OK && status) rc = XCG_EOVERFLOW;
-  } while (0);
-  (void)hipFree(d_in);
-  (void)hipFree(d_out);
-  (void)hipFree(d_off);
-  (void)hipFree(d_oo);
-  (void)hipFree(d_ol);
-  (void)hipFree(d_len);
-  (void)hipStreamDestroy(st);
-  return rc;
+  }
+  return XCG_OK;
 }
 
 }  // extern "C"

@@ -1538,8 +1538,9 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   } else {
     launch();
     rounds = 1;
-    if (!changed_after(fc)) return -5;
-    if (fc == ~0u && a->decls_out) *a->decls_out = 0;   // round 0 declared nothing
+    // (one chunk: no round follows, so no need to learn what it declared)
+    if (n > 1 && !changed_after(fc)) return -5;
+    if (n > 1 && fc == ~0u && a->decls_out) *a->decls_out = 0;   // round 0 declared nothing
   }
   // Jacobi rounds: chunk k re-parses against the declarations chunks < k made
   // in the previous round.  Chunk 0 is exact after round 0 and, inductively,
