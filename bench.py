@@ -416,7 +416,30 @@ def tack_loop(data, offs, lens, ncalls=1024):
         res[name] = {'us_per_call': round(dt / k * 1e6, 1), 'GiBps': round(b / 2**30 / dt, 3)}
     if outs['gpu_dropin'] != outs['reference_cpu']:
         raise SystemExit('PARITY FAILURE (drop-in tack loop vs the reference)')
-    res.update({'calls': k, 'call_bytes': int(lens[0]), 'checked': 'drop-in output == reference output, every call',
+    # tack -d: one XCodecDecoder::decode per encoded call output, one decoder + cache
+    encs = outs['reference_cpu']
+    decs = {}
+    for name, o in (('gpu_dropin', gpu), ('reference_cpu', ref)):
+        c = o.cache_new()
+        dec = o.decoder_new(c)
+        o.decode(encs[0], c, decoder=dec)                        # (warm)
+        o.decoder_free(dec)
+        o.cache_free(c)
+        c = o.cache_new()
+        dec = o.decoder_new(c)
+        t0 = time.perf_counter()
+        got = [o.decode(e, c, decoder=dec, out_cap=2 * CHUNK) for e in encs]
+        dt = time.perf_counter() - t0
+        o.decoder_free(dec)
+        o.cache_free(c)
+        decs[name] = got
+        b = int(lens[:k].astype(np.int64).sum())
+        res[name].update({'decode_us_per_call': round(dt / k * 1e6, 1), 'decode_GiBps': round(b / 2**30 / dt, 3)})
+    if decs['gpu_dropin'] != decs['reference_cpu'] or b''.join(r[1] for r in decs['gpu_dropin']) != \
+            data[:int(lens[:k].astype(np.int64).sum())].tobytes():
+        raise SystemExit('PARITY FAILURE (drop-in tack decode loop vs the reference)')
+    res.update({'calls': k, 'call_bytes': int(lens[0]),
+                'checked': 'drop-in output == reference output, every encode and decode call; decode == input',
                 'includes': 'per call: Buffer -> H2D, one stream-semantics launch, D2H, host cache mirror'})
     return res
 

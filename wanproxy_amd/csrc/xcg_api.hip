@@ -1162,43 +1162,39 @@ int xcg_decode_host(xcg_ctx* c, const uint8_t* h_enc, uint64_t enc_len, const ui
     if (h_chunk_len[i] > maxlen) maxlen = h_chunk_len[i];
   }
   DeviceGuard g(c->device);
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  uint64_t *d_off = nullptr, *d_oo = nullptr, *d_ol = nullptr, *d_cons = nullptr;
-  uint32_t* d_len = nullptr;
-  int32_t* d_st = nullptr;
-  hipStream_t st = nullptr;
-  int rc = XCG_OK;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
-  do {
-    if (hipMalloc(&d_in, enc_len ? enc_len : 1) != hipSuccess || hipMalloc(&d_out, out_cap ? out_cap : 1) != hipSuccess ||
-        hipMalloc(&d_off, 8ull * n) != hipSuccess || hipMalloc(&d_oo, 8ull * n) != hipSuccess ||
-        hipMalloc(&d_ol, 8ull * n) != hipSuccess || hipMalloc(&d_cons, 8ull * n) != hipSuccess ||
-        hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_st, 4ull * n) != hipSuccess) {
-      rc = XCG_ENOMEM;
-      break;
-    }
-    if (hipMemcpyAsync(d_in, h_enc, enc_len, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_off, h_chunk_off, 8ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_len, h_chunk_len, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess) {
-      rc = XCG_EHIP;
-      break;
-    }
-    uint64_t total = 0;
-    rc = xcg_decode_batch(c, d_in, d_off, d_len, n, maxlen, d_out, out_cap, d_oo, d_ol, d_st, d_cons, h_unknown,
-                          unknown_cap, h_nunknown, &total, st);
-    if (rc != XCG_OK) break;
-    if (hipMemcpyAsync(h_out_off, d_oo, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_out_len, d_ol, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_chunk_status, d_st, 4ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_consumed, d_cons, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_out, d_out, total < out_cap ? total : out_cap, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      rc = XCG_EHIP;
-  } while (0);
-  (void)hipFree(d_in); (void)hipFree(d_out); (void)hipFree(d_off); (void)hipFree(d_oo); (void)hipFree(d_ol);
-  (void)hipFree(d_cons); (void)hipFree(d_len); (void)hipFree(d_st);
-  (void)hipStreamDestroy(st);
-  return rc;
+  // staging (kept by the context): [off n][oo n][ol n][cons n][len n][status n] | input | output
+  const size_t meta = align256(40ull * n), inb = align256(enc_len ? enc_len : 1), outb = align256(out_cap ? out_cap : 1);
+  int rc = ensure_stage(c, meta + inb + outb, meta + inb + outb);
+  if (rc != XCG_OK) return rc;
+  uint8_t* hm = c->stage_h;
+  uint8_t* dm = c->stage_d;
+  memcpy(hm, h_chunk_off, 8ull * n);
+  memcpy(hm + 32ull * n, h_chunk_len, 4ull * n);
+  memcpy(hm + meta, h_enc, enc_len);
+  const hipStream_t st = c->call_st;
+  uint64_t* d_oo = (uint64_t*)(dm + 8ull * n);
+  uint64_t* d_ol = (uint64_t*)(dm + 16ull * n);
+  uint64_t* d_cons = (uint64_t*)(dm + 24ull * n);
+  int32_t* d_st = (int32_t*)(dm + 36ull * n);
+  uint8_t* d_out = dm + meta + inb;
+  if (hipMemcpyAsync(dm, hm, meta + enc_len, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
+  uint64_t total = 0;
+  rc = xcg_decode_batch(c, dm + meta, (const uint64_t*)dm, (const uint32_t*)(dm + 32ull * n), n, maxlen, d_out,
+                        out_cap, d_oo, d_ol, d_st, d_cons, h_unknown, unknown_cap, h_nunknown, &total, st);
+  if (rc != XCG_OK) return rc;
+  uint8_t* ho = hm + meta + inb;
+  const uint64_t nout = total < out_cap ? total : out_cap;
+  if (hipMemcpyAsync(hm + 8ull * n, dm + 8ull * n, 24ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(hm + 36ull * n, d_st, 4ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      (nout && hipMemcpyAsync(ho, d_out, nout, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return XCG_EHIP;
+  memcpy(h_out_off, hm + 8ull * n, 8ull * n);
+  memcpy(h_out_len, hm + 16ull * n, 8ull * n);
+  memcpy(h_consumed, hm + 24ull * n, 8ull * n);
+  memcpy(h_chunk_status, hm + 36ull * n, 4ull * n);
+  if (nout) memcpy(h_out, ho, nout);
+  return XCG_OK;
 }
 
 int xcg_pack_outputs(xcg_ctx* c, const uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
