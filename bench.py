@@ -318,13 +318,15 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
     return res
 
 
-def host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, n, dev, nsub=16):
+def host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, n, dev, nsub=8, zero_copy=True):
     """Independent-chunk encode from pinned host memory to pinned host memory:
     H2D of the input, encode, pack, D2H of exactly the encoded bytes -- cut
     into `nsub` sub-batches pipelined over three HIP streams (copy in /
     compute / copy out), so the two PCIe directions and the kernels overlap.
-    The host learns each sub-batch's packed size from a 8-byte readback and
-    issues its D2H then; checked byte for byte against the device result."""
+    The host learns each sub-batch's packed size (zero_copy: the pack kernel
+    writes it straight into pinned host memory; else an 8-byte readback on the
+    compute stream) and issues its D2H then; checked byte for byte against the
+    device result."""
     import ctypes as C
     import torch
     from wanproxy_amd.xcgpu import _check, lib
@@ -354,12 +356,14 @@ def host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol,
             ctx.encode_batch_device(d_in, d_off[a:b], d_len[a:b], b - a, CHUNK, d_out, d_oo[a:b], d_ol[a:b],
                                     stream=s_cmp)
             p0 = slot[i][0]
+            tot_ptr = h_tot[i:].data_ptr() if zero_copy else d_ptot[i:].data_ptr()
             _check(L.xcg_pack_outputs(ctx.h, C.c_void_p(d_out.data_ptr()), C.c_void_p(d_oo[a:].data_ptr()),
                                       C.c_void_p(d_ol[a:].data_ptr()), b - a, C.c_void_p(d_packed.data_ptr() + p0),
-                                      C.c_void_p(d_poff[a:].data_ptr()), C.c_void_p(d_ptot[i:].data_ptr()),
+                                      C.c_void_p(d_poff[a:].data_ptr()), C.c_void_p(tot_ptr),
                                       C.c_void_p(s_cmp.cuda_stream)))
             with torch.cuda.stream(s_cmp):
-                h_tot[i:i + 1].copy_(d_ptot[i:i + 1], non_blocking=True)
+                if not zero_copy:
+                    h_tot[i:i + 1].copy_(d_ptot[i:i + 1], non_blocking=True)
                 ev_c[i].record(s_cmp)
         o = 0
         for i in range(len(subs)):
@@ -388,10 +392,28 @@ def host_inclusive(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol,
     if tot != len(want) or h_out[:tot].numpy().tobytes() != want:
         raise SystemExit('host-inclusive output differs from the device-resident encode')
     in_bytes = int(lens.astype(np.int64).sum())
+    # the link's own ceiling on this box: plain pinned copies of the same sizes,
+    # each direction alone and both at once (two streams)
+    def copy_rate(h2d, d2h):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            if h2d:
+                with torch.cuda.stream(s_in):
+                    d_in.copy_(h_in, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s_out):
+                    h_out[:tot].copy_(d_packed[:tot], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        return ((in_bytes if h2d else 0) + (tot if d2h else 0)) * 3 / (time.perf_counter() - t0) / 1e9
+    link = {'h2d_GBps': round(copy_rate(True, False), 1), 'd2h_GBps': round(copy_rate(False, True), 1),
+            'both_GBps': round(copy_rate(True, True), 1)}
     return {'metric': 'independent-chunk encode GiB/s incl. pinned H2D of input and D2H of the packed output',
             'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
             'pcie_GBps': round((in_bytes + tot) / wall / 1e9, 2), 'sub_batches': len(subs),
-            'includes': 'H2D + encode + pack + size readback + D2H, 3 streams (median of 5)'}
+            'link_copies_only': link,
+            'includes': 'H2D + encode + pack + size readback + D2H, 3 streams (median of 5)',
+            'size_readback': 'pack kernel writes pinned host memory' if zero_copy else '8-byte D2H per sub-batch'}
 
 
 def tack_loop(data, offs, lens, ncalls=1024):
