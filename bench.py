@@ -186,13 +186,26 @@ def pmc_traffic(n):
     summary (scripts/profile.sh + scripts/prof_summary.py: FETCH_SIZE doubled
     per MI355X_MICROARCH.md "HBM", plus WRITE_SIZE), when it was taken on this
     same workload; PMC counters cannot be read from inside the timed run."""
-    p = os.path.join(ROOT, 'profiles', 'r01_c2_independent_summary.json')
-    if n != NCHUNKS or not os.path.exists(p):
+    for name in ('r02_c2_independent_summary.json', 'r01_c2_independent_summary.json'):
+        p = os.path.join(ROOT, 'profiles', name)
+        if n != NCHUNKS or not os.path.exists(p):
+            continue
+        s = json.load(open(p))
+        if 'hbm_traffic_bytes_per_launch' in s:
+            return int(s['hbm_traffic_bytes_per_launch']), f'profiles/{name} (rocprofv3 --pmc)'
+    return None, None
+
+
+def pmc_stream_traffic():
+    """HBM bytes of the seeded C2-S2 stream-parse launch (the bench's S2 step)
+    from the committed scripts/profile_stream.sh summary."""
+    p = os.path.join(ROOT, 'profiles', 'r02_stream_pmc_summary.json')
+    if not os.path.exists(p):
         return None, None
-    s = json.load(open(p))
-    if 'hbm_traffic_bytes_per_launch' not in s:
+    g = json.load(open(p)).get('c2s_seeded', {})
+    if 'hbm_bytes' not in g:
         return None, None
-    return int(s['hbm_traffic_bytes_per_launch']), 'profiles/r01_c2_independent_summary.json (rocprofv3 --pmc)'
+    return int(g['hbm_bytes'] / max(1, g['dispatches'])), 'profiles/r02_stream_pmc_summary.json c2s_seeded (rocprofv3 --pmc)'
 
 
 def timed(fn, steps, stream, kernel_time=False):
@@ -274,8 +287,7 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
                      'frac_read': round(in_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5),
                      'kernel': 'encode_stream_kernel', 'kernel_ms_per_step': round(kms, 4),
                      'launches_per_step': kl, 'algorithmic_bytes_per_step': in_bytes + out_bytes,
-                     'traffic': None,
-                     'traffic_note': 'PMC HBM bytes of this kernel: profiles/r02_stream_pmc_summary.json'}}
+                     'traffic': pmc_stream_traffic()[0], 'traffic_source': pmc_stream_traffic()[1]}}
     # -- decode of that stream with a fresh decoder cache
     dctx = Context(dev.index, cache_segments=1 << 18)
     elens = ol.astype(np.uint32)

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/profs
 rm -rf $OUT; mkdir -p $OUT
-CMD="python3 scripts/configs_bench.py ${CFGS:-c2s c4 c5} --reps 1 --no-decode"
+CMD="python3 scripts/configs_bench.py ${CFGS:-c2s c4 c5} --reps ${REPS:-2} --no-decode"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $CMD > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $CMD > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $CMD > $OUT/write.log 2>&1 || exit $?

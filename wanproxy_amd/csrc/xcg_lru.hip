@@ -35,6 +35,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <chrono>
+
 #include "xcg_cache.h"
 #include "xcg_args.h"
 
@@ -623,24 +625,33 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     if (a.stats) a.stats += 4ull * i0;
     a.ptime = L->ptime;
     a.no_commit = 1;
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    auto dsync = [&]() { if (lru_debug()) (void)hipStreamSynchronize(st); return clk::now(); };
+    const clk::time_point t0 = dsync();
     // Pass 0 starts from the tiling seed, with the evictions it implies.
     if (xcg_launch_seed_tiling(&a, st)) return -5;
     if (lru_seed_guess(a, L, st)) return -5;
+    const clk::time_point t1 = dsync();
     bool done = false, split = false;
     for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
       a.keep_decls = 1;
       a.need_given = pass > 0;                       // re-parse the chunks with an inconsistent lookup
       int r = 0;
+      const clk::time_point q0 = dsync();
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
       if (rc) return rc;
+      const clk::time_point q1 = dsync();
       if (lru_times(batch_of(a), L, true, st)) return -5;
+      const clk::time_point q2 = dsync();
       if (lru_debug()) {
         int32_t stw = 0;
         (void)hipMemcpy(&stw, a.status, 4, hipMemcpyDeviceToHost);
-        fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u status %x\n",
+        fprintf(stderr, "lru: chunks %u+%u pass %d rounds %d refs %u enters %u evict %u live %u bad %u ovf %u status %x"
+                " | ms seed %.3f parse %.3f times %.3f\n",
                 i0, m, pass, r, L->h_tot[T_E], L->h_tot[T_N], L->h_tot[T_P], L->h_tot[T_A], L->h_tot[T_BAD],
-                L->h_tot[T_OVF], stw);
+                L->h_tot[T_OVF], stw, pass == 0 ? ms(t0, t1) : 0.0, ms(q0, q1), ms(q1, q2));
       }
       if (L->h_tot[T_OVF]) return -75;
       if ((uint64_t)L->h_tot[T_N] + L->h_tot[T_H] > C) split = true;
@@ -652,7 +663,9 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       continue;
     }
     const LruBatch b = batch_of(a);
+    const clk::time_point c0 = dsync();
     if (xcg_lru_commit(&b, L, st)) return -5;
+    if (lru_debug()) fprintf(stderr, "lru: commit %.3f ms\n", ms(c0, dsync()));
     L->last_base = i0;
     i0 += m;
     const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
