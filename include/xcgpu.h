@@ -300,6 +300,11 @@ int xcg_debug_set_stream_seed(int mode);
  * xcg_debug_stream_kernel_time returns (and resets) the summed milliseconds
  * and the launch count.  Process-wide.  Returns the previous setting. */
 int xcg_debug_stream_kernel_timing(int on);
+/* Diagnostics / tests: on a bounded or pair context, how many re-parsed chunks
+ * so far resumed from their previous pass's rows, and how many of those rejoined
+ * their old parse (DESIGN.md 3.6 "Re-parse restart"); env XCG_NO_RESTART turns
+ * resuming off (same output). */
+int xcg_debug_restart_counts(xcg_ctx *ctx, uint64_t *resumed, uint64_t *spliced);
 int xcg_debug_stream_kernel_time(double *ms, uint32_t *launches);
 
 /* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for

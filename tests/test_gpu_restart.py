@@ -1,0 +1,50 @@
+"""Re-parse restart on bounded (LRU) and pair caches: a chunk
+whose recorded lookups the eviction analysis contradicts is re-parsed from its
+last clean point before the first such lookup and rejoins its previous parse
+after the last one.  The output must equal the sequential oracle -- and the
+same run with resuming turned off (XCG_NO_RESTART) -- while resumes and
+splices really happen."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+def _encode(kind, d, offs, lens, per, restart):
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    if restart:
+        os.environ.pop('XCG_NO_RESTART', None)
+    else:
+        os.environ['XCG_NO_RESTART'] = '1'
+    try:
+        kw = dict(memory_cache_limit=2 * MiB) if kind == 'bounded' else dict(memory_cache_limit=1 * MiB,
+                                                                            disk_bytes=8 * MiB)
+        ctx = Context(0, **kw)
+        got = []
+        for a in range(0, offs.size, per):
+            got += ctx.encode_chunks(d, offs[a:a + per], lens[a:a + per], semantics=XCG_SEM_STREAM)
+        counts = ctx.restart_counts()
+        ctx.close()
+    finally:
+        os.environ.pop('XCG_NO_RESTART', None)
+    return got, counts
+
+
+@pytest.mark.parametrize('kind', ['bounded', 'pair'])
+def test_restart_equals_oracle_and_full_reparse(oracle, kind):
+    from wanproxy_amd import synth
+    d = np.frombuffer(synth.stream(0xC5, 24 * MiB, 20, 0), np.uint8).copy()
+    offs, lens = synth.chunks_of(d.tobytes(), 128 * 1024)
+    c = oracle.cache_new(2 * MiB) if kind == 'bounded' else oracle.cache_new_pair(1 * MiB, 8 * MiB)
+    exp = oracle.encode_batch(d, offs, lens, mode=1, cache=c)
+    oracle.cache_free(c)
+    got, (resumed, spliced) = _encode(kind, d, offs, lens, 64, True)
+    bad = [i for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, (kind, bad[:8])
+    plain, (r0, s0) = _encode(kind, d, offs, lens, 64, False)
+    assert plain == got and r0 == 0 and s0 == 0
+    if kind == 'bounded':
+        assert resumed > 0 and spliced > 0, (resumed, spliced)

@@ -7,6 +7,7 @@
 // caller may capture it into a hipGraph.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -127,6 +128,21 @@ struct BatchScratch {
   uint32_t* enter_base = nullptr;  // n_cap + 1
   uint32_t* ev_slot = nullptr;     // n_cap * maxe: each reference's pool slot / LRU time
   uint64_t* ev_time = nullptr;
+  // re-parse restart (xcg_encode.hip RestartArgs): REF output lengths, the
+  // contradicted-lookup times, and a backup of the flagged chunks' rows
+  uint32_t* eo = nullptr;          // n_cap * maxe
+  uint32_t* bad_t = nullptr;       // n_cap
+  uint32_t* bad_hi = nullptr;      // n_cap
+  uint32_t* bslot = nullptr;       // n_cap
+  uint32_t* b_count = nullptr;
+  uint32_t b_slots = 0;
+  void* b_ev = nullptr;            // b_slots * maxe uint4
+  uint32_t* b_eo = nullptr;
+  uint64_t* b_hits = nullptr;      // b_slots * maxh
+  uint32_t* b_cnt = nullptr;       // b_slots * 4
+  uint8_t* b_out = nullptr;        // b_slots * b_stride
+  uint64_t b_stride = 0;
+  void* splice = nullptr;          // n_cap uint4
 };
 
 struct DecodeScratch {
@@ -261,6 +277,9 @@ void free_scratch(BatchScratch& b) {
   if (b.h_changed) (void)hipHostFree(b.h_changed);
   (void)hipFree(b.ev); (void)hipFree(b.nev); (void)hipFree(b.ev_base); (void)hipFree(b.enter_base);
   (void)hipFree(b.ev_slot); (void)hipFree(b.ev_time);
+  (void)hipFree(b.eo); (void)hipFree(b.bad_t); (void)hipFree(b.bad_hi); (void)hipFree(b.bslot);
+  (void)hipFree(b.b_count); (void)hipFree(b.b_ev); (void)hipFree(b.b_eo); (void)hipFree(b.b_hits);
+  (void)hipFree(b.b_cnt); (void)hipFree(b.b_out); (void)hipFree(b.splice);
   b = BatchScratch{};
 }
 
@@ -375,6 +394,21 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
     if (hipMalloc(&b.ev, 16ull * n * b.maxe) != hipSuccess || hipMalloc(&b.nev, 4ull * n) != hipSuccess ||
         hipMalloc(&b.ev_base, 4ull * (n + 1)) != hipSuccess || hipMalloc(&b.enter_base, 4ull * (n + 1)) != hipSuccess ||
         hipMalloc(&b.ev_slot, 4ull * n * b.maxe) != hipSuccess || hipMalloc(&b.ev_time, 8ull * n * b.maxe) != hipSuccess) {
+      free_scratch(b);
+      return XCG_ENOMEM;
+    }
+    // restart backups for up to b_slots flagged chunks per pass (more re-parse from the start)
+    b.b_slots = n < 256 ? n : 256;
+    b.b_stride = (2ull * maxd * XCG_SEGMENT_LENGTH + 16 + 255) & ~255ull;   // >= xcg_encode_bound(max chunk)
+    if (hipMalloc(&b.eo, 4ull * n * b.maxe) != hipSuccess || hipMalloc(&b.bad_t, 4ull * n) != hipSuccess ||
+        hipMalloc(&b.bad_hi, 4ull * n) != hipSuccess || hipMalloc(&b.bslot, 4ull * n) != hipSuccess ||
+        hipMalloc(&b.b_count, 16) != hipSuccess || hipMalloc(&b.b_ev, 16ull * b.b_slots * b.maxe) != hipSuccess ||
+        hipMalloc(&b.b_eo, 4ull * b.b_slots * b.maxe) != hipSuccess ||
+        hipMalloc(&b.b_hits, 8ull * b.b_slots * b.maxh) != hipSuccess ||
+        hipMalloc(&b.b_cnt, 16ull * b.b_slots) != hipSuccess ||
+        hipMalloc(&b.b_out, b.b_stride * b.b_slots) != hipSuccess || hipMalloc(&b.splice, 16ull * n) != hipSuccess ||
+        hipMemset(b.splice, 0, 16ull * n) != hipSuccess || hipMemset(b.bad_t, 0xFF, 4ull * n) != hipSuccess ||
+        hipMemset(b.bad_hi, 0, 4ull * n) != hipSuccess || hipMemset(b.b_count, 0, 16) != hipSuccess) {
       free_scratch(b);
       return XCG_ENOMEM;
     }
@@ -786,6 +820,18 @@ int xcg_last_references(xcg_ctx* c, uint32_t chunk, uint64_t* h_hash, uint32_t* 
   return XCG_OK;
 }
 
+int xcg_debug_restart_counts(xcg_ctx* c, uint64_t* resumed, uint64_t* spliced) {
+  if (!c || !resumed || !spliced) return XCG_EINVAL;
+  *resumed = *spliced = 0;
+  if (!c->bs.b_count) return XCG_OK;
+  DeviceGuard g(c->device);
+  uint32_t v[4] = {0, 0, 0, 0};
+  if (ctx_wait(c) != XCG_OK || hipMemcpy(v, c->bs.b_count, 16, hipMemcpyDeviceToHost) != hipSuccess) return XCG_EHIP;
+  *resumed = v[2];
+  *spliced = v[3];
+  return XCG_OK;
+}
+
 int xcg_debug_cache_dump(xcg_ctx* c, uint32_t* h_filt, uint32_t* h_ftab, uint64_t ftab_words, uint32_t* h_fmask) {
   if (!c || !c->g.keys) return XCG_EINVAL;
   DeviceGuard g(c->device);
@@ -846,6 +892,13 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     uint32_t decls = ~0u;
     a.decls_out = &decls;
     int rounds = 0;
+    if (c->pair || c->bounded) {
+      BatchScratch& b = c->bs;
+      a.eo = b.eo; a.bad_t = b.bad_t; a.bad_hi = b.bad_hi; a.bslot = b.bslot; a.b_count = b.b_count;
+      a.b_slots = b.b_slots; a.b_ev = b.b_ev; a.b_eo = b.b_eo; a.b_hits = b.b_hits; a.b_cnt = b.b_cnt;
+      a.b_out = b.b_out; a.b_stride = b.b_stride; a.splice = b.splice;
+      a.restart = getenv("XCG_NO_RESTART") ? 0 : 1;
+    }
     if (c->pair) {
       a.ev = c->bs.ev;
       a.nev = c->bs.nev;

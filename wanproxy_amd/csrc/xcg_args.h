@@ -64,6 +64,23 @@ struct XcgStreamArgs {
   int no_commit;
   int keep_decls;        // start from the declaration lists already in decl/ndecl
   int need_given;        // (keep_decls) round 1 parses only the chunks flagged in need[]
+  // re-parse restart (bounded / pair): output length after each REF-making
+  // lookup, per chunk the earliest / latest contradicted lookup time, and the
+  // backup of the previous pass's rows of the flagged chunks
+  uint32_t* eo;          // [n * maxe]
+  uint32_t* bad_t;       // [n] (~0: none)
+  uint32_t* bad_hi;      // [n]
+  int restart;           // (need_given) round 1 resumes flagged chunks from their rows
+  uint32_t* bslot;       // [n]
+  uint32_t* b_count;     // [1]
+  uint32_t b_slots;
+  void* b_ev;            // [b_slots * maxe] uint4
+  uint32_t* b_eo;        // [b_slots * maxe]
+  uint64_t* b_hits;      // [b_slots * maxh]
+  uint32_t* b_cnt;       // [b_slots * 4]
+  uint8_t* b_out;        // [b_slots * b_stride]
+  uint64_t b_stride;
+  void* splice;          // [n] uint4
 };
 
 // Bounded cache (xcg_lru.hip): device LRU state of a context.
@@ -118,6 +135,8 @@ struct LruBatch {
   uint32_t gmask;
   int32_t* status;
   uint64_t ev_bound;      // upper bound of the batch's references (sizes the scans)
+  uint32_t* bad_t;        // (encoder, optional) per chunk earliest / latest contradicted lookup time
+  uint32_t* bad_hi;
 };
 
 // XCodecCachePair of a bounded memory primary and a disk secondary (xcg_pair.hip).

@@ -77,6 +77,21 @@ struct StreamLDS {
   uint32_t lfilt[FILT_WORDS];                // the lane filter (64 KiB)
   uint32_t scr[W][GSLOTS_DECL + 1][64];      // pass-1 queues (+ a garbage slot)
   WaveRecs<LOGNB, MAXD> rec[W];
+  uint32_t ro[W][MAXD];                      // output length after each declaration's op (restart points)
+  uint32_t rsv[W][8];                        // restart state (kept out of registers)
+};
+
+// Re-parse restart (bounded / pair passes after the first; the driver backs up
+// the previous pass's rows of each flagged chunk, xcg_restart_backup_kernel).
+struct RestartArgs {
+  const uint32_t* bad_t;   // [n] in-chunk time of the chunk's earliest contradicted lookup (~0: none)
+  const uint32_t* bad_hi;  // [n] ... and of its latest
+  const uint32_t* bslot;   // [n] backup slot of the chunk's previous pass (~0: none)
+  const uint4* b_ev;       // [slots * maxe] its reference rows
+  const uint32_t* b_eo;    // [slots * maxe] their REF output lengths
+  const uint64_t* b_hits;  // [slots * maxh] its batch hits
+  const uint32_t* b_cnt;   // [slots * 4] its nev, nhits, output length, ndecl
+  uint4* splice;           // [n] {new offset, old offset, old end, 1}: the old tail to append
 };
 
 struct EncParams {
@@ -114,6 +129,8 @@ struct EncParams {
   uint4* ev;           // [n * maxe] the chunk's cache references in order (lo, hi, time, kind << 30 | ref)
   uint32_t* nev;       // [n] (> maxe: overflowed)
   uint32_t maxe;
+  uint32_t* eo;        // [n * maxe] output length after the REF a lookup made (~0: it made none)
+  RestartArgs rs;      // re-parse from the previous pass's rows (bslot null: off)
 };
 
 // ------------------------------------------------------------------ emission
@@ -483,6 +500,8 @@ struct GlbView {
   uint32_t lfo;
   uint32_t sofs;
   int fmode;   // 0: no probe, 1: LDS lane filter, 2: global lane filter
+  uint32_t* ro;   // (stream) the wave's per-declaration output lengths, LDS
+  uint32_t* rsv;  // (stream) the wave's restart state, LDS: slot, old nev, nhits, olen, ndecl, restart ndecl
 };
 
 template <int LOGNB, int MAXD, bool STREAM, bool LRU = false>
@@ -616,8 +635,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   // LRU pass (xcg_lru.hip) derives the eviction times from these.
   uint32_t ne = 0;
   auto record = [&](uint32_t lo, uint32_t hi, uint32_t t, uint32_t kind, uint32_t ref) {
-    if (ne < prm.maxe && l == 0) prm.ev[(uint64_t)chunk * prm.maxe + ne] = make_uint4(lo, hi, t, (kind << 30) | ref);
+    if (ne < prm.maxe && l == 0) {
+      prm.ev[(uint64_t)chunk * prm.maxe + ne] = make_uint4(lo, hi, t, (kind << 30) | ref);
+      if (prm.eo) prm.eo[(uint64_t)chunk * prm.maxe + ne] = ~0u;
+    }
     ++ne;
+  };
+  // (after a REF: the output length, at the lookup that made it)
+  auto ref_made = [&]() {
+    if (LRU && prm.eo && l == 0 && ne > 0 && ne - 1 < prm.maxe) prm.eo[(uint64_t)chunk * prm.maxe + ne - 1] = olen;
   };
   auto cache_src = [&](uint32_t lo, uint32_t hi, int at) -> const uint8_t* {
     uint64_t gv, bv;                               // (both tables probed in one round trip)
@@ -635,7 +661,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       if (bv != ~0ull && (uint32_t)(bv >> 32) < chunk) {
         if (nh < prm.maxh && l == 0) prm.hits[(uint64_t)chunk * prm.maxh + nh] = ((uint64_t)hi << 32) | lo;
         ++nh;
-        if (LRU) record(lo, hi, 2u * (uint32_t)at + 1u, EV_HIT, 0u);
+        if (LRU) record(lo, hi, 2u * (uint32_t)at + 1u, EV_HIT, 1u);   // (ref 1: a batch hit, listed in hits)
         return prm.in + prm.chunk_off[bv >> 32] + (uint32_t)bv;
       }
     }
@@ -665,9 +691,218 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       olen += 2 + SEG;
     }
     ++n_extract;
+    if (STREAM && gs.ro && !nullcache && l == 0 && ndecl > 0) gs.ro[ndecl - 1] = olen;   // (the candidate's record)
     base = cand + SEG;
     have_cand = false;
     c0_in_table = true;
+  };
+
+  // ---- Re-parse restart (bounded / pair passes after the first, xcg_lru.hip /
+  // xcg_pair.hip).  The previous pass's parse of this chunk stands up to its
+  // first lookup the new eviction times contradict (in-chunk time bad_t).
+  // Resume at its last clean point before that -- right after a declaration or
+  // a REF: parse point = base, nothing pending, about to look that window up
+  // (xcodec_encoder.cc:183-208) -- from the state its rows give, and stop as
+  // soon as the new parse reaches a clean point the old one also passed
+  // through, with the same own declarations as far as the old remainder looks
+  // them up: the old remainder is then appended (rows here, output bytes by
+  // xcg_splice_kernel after the launch).  The rows of a chunk are in time
+  // order, so everything before the restart point is still in place.
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  int rs_q = -1;
+  uint32_t rs_hi = 0;                              // in-chunk time of the latest contradicted lookup
+  bool spliced = false;
+  if (LRU && STREAM && prm.rs.bslot && prm.eo && gs.ro && gs.rsv && !nullcache) {
+    const uint32_t rs_slot = readfirst(prm.rs.bslot[chunk]);
+    const uint32_t tb = readfirst(prm.rs.bad_t[chunk]);
+    rs_hi = readfirst(prm.rs.bad_hi[chunk]);
+    if (rs_slot != NONE && tb != NONE) {
+      const uint4* const odl = prm.decl + (uint64_t)chunk * prm.maxd;   // old rows (in place until the end)
+      const uint4* oev = prm.rs.b_ev + (uint64_t)rs_slot * prm.maxe;
+      const uint32_t* oeo = prm.rs.b_eo + (uint64_t)rs_slot * prm.maxe;
+      const uint32_t o_nev = min(readfirst(prm.rs.b_cnt[4 * rs_slot]), prm.maxe);
+      const uint32_t o_nd = readfirst(prm.rs.b_cnt[4 * rs_slot + 3]);
+      // the latest clean point q (a window, <= last) with 2q + 1 <= tb
+      int best = -1;
+      uint32_t best_olen = 0;
+      for (uint32_t i0 = 0; i0 < o_nev; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)l;
+        int q = -1;
+        uint32_t ol = 0;
+        if (i < o_nev) {
+          const uint4 e = oev[i];
+          if ((e.w >> 30) == EV_ENTER) {               // declared while examining window e.z / 2
+            const uint32_t d = e.w & EV_REF_MASK;
+            if (d < o_nd) { q = (int)(e.z >> 1); ol = odl[d].w; }
+          } else if (oeo[i] != NONE) {                  // a REF at window (e.z - 1) / 2
+            q = (int)((e.z - 1u) >> 1) + SEG;
+            ol = oeo[i];
+          }
+          if (q > last || (q >= 0 && 2u * (uint32_t)q + 1u > tb)) q = -1;
+        }
+        int mq = q;
+        for (int off = 32; off >= 1; off >>= 1) mq = max(mq, __shfl_xor(mq, off));
+        mq = readfirst(mq);
+        if (mq > best) {
+          const uint64_t bl = ballot(q == mq);
+          best = mq;
+          best_olen = readlane(ol, (int)__builtin_ctzll(bl));
+        }
+      }
+      if (best >= 0) {
+        rs_q = best;
+        uint32_t ne_r = 0, nd_r = 0, nh_r = 0, nref_r = 0;
+        for (uint32_t i0 = 0; i0 < o_nev; i0 += 64) {
+          const uint32_t i = i0 + (uint32_t)l;
+          bool in = false, ent = false, bh = false, rf = false;
+          if (i < o_nev) {
+            const uint4 e = oev[i];
+            in = e.z < 2u * (uint32_t)best + 1u;
+            ent = in && (e.w >> 30) == EV_ENTER;
+            bh = in && (e.w >> 30) == EV_HIT && (e.w & EV_REF_MASK) == 1u;
+            rf = in && oeo[i] != NONE;
+          }
+          ne_r += (uint32_t)__builtin_popcountll(ballot(in));
+          nd_r += (uint32_t)__builtin_popcountll(ballot(ent));
+          nh_r += (uint32_t)__builtin_popcountll(ballot(bh));
+          nref_r += (uint32_t)__builtin_popcountll(ballot(rf));
+        }
+        for (uint32_t d = 0; d < nd_r; ++d) {           // the own records and key table so far
+          const uint4 r = odl[d];
+          insert(readfirst(r.x), readfirst(r.y), readfirst(r.z));
+          if (l == 0) gs.ro[d] = r.w;
+        }
+        if (l == 0) {
+          gs.rsv[0] = rs_slot;
+          gs.rsv[1] = o_nev;
+          gs.rsv[2] = readfirst(prm.rs.b_cnt[4 * rs_slot + 1]);
+          gs.rsv[3] = readfirst(prm.rs.b_cnt[4 * rs_slot + 2]);
+          gs.rsv[4] = o_nd;
+          gs.rsv[5] = nd_r;
+        }
+        __builtin_amdgcn_wave_barrier();
+        ne = ne_r;
+        nh = nh_r;
+        olen = best_olen;
+        n_extract = nd_r;
+        n_ref = nref_r;
+        s = base = best;
+        chain = true;
+      }
+    }
+  }
+  // Splice at clean point s (the new parse is about to look window s up, with
+  // nothing pending): true when the old parse had the same state there.
+  auto try_splice = [&]() -> bool {
+    const uint32_t rs_slot = readfirst(gs.rsv[0]), o_nev = readfirst(gs.rsv[1]), o_nh = readfirst(gs.rsv[2]);
+    const uint32_t o_olen = readfirst(gs.rsv[3]), o_nd = readfirst(gs.rsv[4]), rs_nd = readfirst(gs.rsv[5]);
+    const uint4* const odl = prm.decl + (uint64_t)chunk * prm.maxd;
+    const uint4* const oev = prm.rs.b_ev + (uint64_t)rs_slot * prm.maxe;
+    const uint32_t* const oeo = prm.rs.b_eo + (uint64_t)rs_slot * prm.maxe;
+    // the old clean point at s: a declaration made at window s, or a REF at s - 2048
+    int it = -1, dt = -1;
+    uint32_t ol_old = 0;
+    for (uint32_t i0 = 0; i0 < o_nev && it < 0; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)l;
+      bool hit = false;
+      if (i < o_nev) {
+        const uint4 e = oev[i];
+        hit = ((e.w >> 30) == EV_ENTER && e.z == 2u * (uint32_t)s) ||
+              (oeo[i] != NONE && s >= SEG && e.z == 2u * (uint32_t)(s - SEG) + 1u);
+      }
+      const uint64_t bl = ballot(hit);
+      if (bl) it = (int)(i0 + (uint32_t)__builtin_ctzll(bl));
+    }
+    if (it < 0) return false;
+    {
+      const uint4 e = oev[it];
+      if ((e.w >> 30) == EV_ENTER) {
+        dt = (int)(e.w & EV_REF_MASK) + 1;
+        ol_old = readfirst(odl[dt - 1].w);
+      } else {
+        ol_old = readfirst(oeo[it]);
+        uint32_t c = 0;                                  // declarations before the REF
+        for (uint32_t i0 = 0; i0 < (uint32_t)it; i0 += 64) {
+          const uint32_t i = i0 + (uint32_t)l;
+          c += (uint32_t)__builtin_popcountll(ballot(i < (uint32_t)it && (oev[i].w >> 30) == EV_ENTER));
+        }
+        dt = (int)c;
+      }
+    }
+    ++it;                                                // the old remainder's first reference
+    if ((uint32_t)dt < rs_nd || (uint32_t)dt > o_nd) return false;
+    // own declarations that differ: the new ones since the restart vs the old ones
+    const uint32_t nn = ndecl - rs_nd, no = (uint32_t)dt - rs_nd;
+    if (nn > 32 || no > 32) return false;
+    uint32_t hlo = 0, hhi = 0;
+    if ((uint32_t)l < nn) { hlo = T.rlo[rs_nd + l]; hhi = T.rhi[rs_nd + l]; }
+    else if ((uint32_t)l >= 32 && (uint32_t)l - 32 < no) { const uint4 r = odl[rs_nd + l - 32]; hlo = r.x; hhi = r.y; }
+    const bool is_new = (uint32_t)l < nn, is_old = (uint32_t)l >= 32 && (uint32_t)l - 32 < no;
+    bool inD = is_new || is_old;
+    for (uint32_t j = 0; j < (nn > no ? nn : no); ++j) {   // (uniform: readlane of lanes j and 32 + j)
+      const uint32_t nlo = readlane(hlo, (int)j), nhi = readlane(hhi, (int)j);
+      const uint32_t olo = readlane(hlo, (int)(32 + j)), ohi = readlane(hhi, (int)(32 + j));
+      if (is_old && j < nn && hlo == nlo && hhi == nhi) inD = false;
+      if (is_new && j < no && hlo == olo && hhi == ohi) inD = false;
+    }
+    const uint64_t dm = ballot(inD);
+    // the old remainder must not look any of them up (or declare one)
+    for (uint32_t i0 = (uint32_t)it; i0 < o_nev; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)l;
+      const uint4 e = i < o_nev ? oev[i] : make_uint4(0u, 0u, 0u, 0u);
+      bool clash = false;
+      uint64_t m = dm;
+      while (m) {
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        clash |= i < o_nev && e.x == (uint32_t)readlane(hlo, j) && e.y == (uint32_t)readlane(hhi, j);
+      }
+      if (ballot(clash)) return false;
+    }
+    // splice: the old remainder's declarations, references and batch hits follow
+    const uint32_t delta = olen - ol_old;                // (mod 2^32: offsets shift by it)
+    const uint32_t nd0 = ndecl;
+    for (uint32_t d = (uint32_t)dt; d < o_nd && ndecl < (uint32_t)MAXD; ++d) {
+      const uint4 r = odl[d];
+      if (l == 0) {
+        T.rlo[ndecl] = r.x; T.rhi[ndecl] = r.y; T.rc[ndecl] = r.z;
+        gs.ro[ndecl] = r.w + delta;
+      }
+      ++ndecl;
+    }
+    uint32_t hb = 0;                                     // batch hits before the old remainder
+    for (uint32_t i0 = 0; i0 < (uint32_t)it; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)l;
+      hb += (uint32_t)__builtin_popcountll(
+          ballot(i < (uint32_t)it && (oev[i].w >> 30) == EV_HIT && (oev[i].w & EV_REF_MASK) == 1u));
+    }
+    uint32_t nref_t = 0;
+    for (uint32_t i0 = (uint32_t)it; i0 < o_nev; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)l;
+      if (i < o_nev) {
+        uint4 e = oev[i];
+        if ((e.w >> 30) == EV_ENTER) e.w = (EV_ENTER << 30) | ((e.w & EV_REF_MASK) - (uint32_t)dt + nd0);
+        const uint32_t o = oeo[i];
+        const uint32_t k = ne + (i - (uint32_t)it);
+        if (k < prm.maxe) {
+          prm.ev[(uint64_t)chunk * prm.maxe + k] = e;
+          prm.eo[(uint64_t)chunk * prm.maxe + k] = o == NONE ? NONE : o + delta;
+        }
+      }
+      nref_t += (uint32_t)__builtin_popcountll(ballot(i < o_nev && oeo[i] != NONE));
+    }
+    ne += o_nev - (uint32_t)it;
+    const uint64_t* oh = prm.rs.b_hits + (uint64_t)rs_slot * prm.maxh;
+    for (uint32_t j = hb + (uint32_t)l; j < o_nh && j < prm.maxh; j += 64) {
+      const uint32_t k = nh + (j - hb);
+      if (k < prm.maxh) prm.hits[(uint64_t)chunk * prm.maxh + k] = oh[j];
+    }
+    nh += o_nh > hb ? o_nh - hb : 0u;
+    n_ref += nref_t;
+    n_extract += o_nd - (uint32_t)dt;
+    if (l == 0) prm.rs.splice[chunk] = make_uint4(olen, ol_old, o_olen, 1u);
+    olen += o_olen - ol_old;
+    return true;
   };
 
   while (s <= last) {
@@ -743,6 +978,11 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       declare(s);
       chain = true;
     }
+    // a clean point past every contradicted lookup: rejoin the old parse?
+    if (LRU && rs_q >= 0 && chain && s > rs_q && 2u * (uint32_t)s + 1u > rs_hi && try_splice()) {
+      spliced = true;
+      break;
+    }
     if (STREAM && chain && !nullcache) {
 #ifdef XCG_PHASES
       const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
@@ -765,6 +1005,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       if (src != nullptr && equal2048_u(src, x + s)) {
         wave_put_ref(out + olen, lo, hi);           // encode_reference :342-372
         olen += 10;
+        ref_made();
         ++n_ref;
         base = s + SEG;
         s = base;
@@ -926,6 +1167,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
             if (s > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)s);
             wave_put_ref(out + olen, lo, hi);                 // encode_reference :342-372
             olen += 10;
+            ref_made();
             ++n_ref;
             base = s + SEG;
             s = base;
@@ -969,15 +1211,17 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     totXA = totXB; totTA = totTB;
   }
 
-  if (have_cand) declare(last + 1);                           // :257-261 (after every lookup)
-  if (base < L) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
+  if (!spliced) {
+    if (have_cand) declare(last + 1);                         // :257-261 (after every lookup)
+    if (base < L) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)L);   // :267-269
+  }
   if (STREAM) {
     // This round's declarations; flag a change against the previous round's.
     const uint32_t nold = prm.ndecl[chunk];
     bool diff = nold != ndecl;
     uint4* dl = prm.decl + (uint64_t)chunk * prm.maxd;
     for (uint32_t k = l; k < ndecl; k += 64) {
-      const uint4 nv = make_uint4(T.rlo[k], T.rhi[k], T.rc[k], 0u);
+      const uint4 nv = make_uint4(T.rlo[k], T.rhi[k], T.rc[k], gs.ro ? gs.ro[k] : 0u);
       if (k < nold) {
         const uint4 ov = dl[k];
         diff |= ov.x != nv.x || ov.y != nv.y || ov.z != nv.z;
@@ -1028,7 +1272,7 @@ __global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams pr
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
   if (chunk >= prm.n) return;
   encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk,
-                                   GlbView{nullptr, 0u, 0u, 0});
+                                   GlbView{nullptr, 0u, 0u, 0, nullptr, nullptr});
 }
 
 // Stream semantics: persistent workgroups of SW waves share one LDS copy of
@@ -1049,7 +1293,7 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
   const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
-                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode};
+                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode, S.ro[wv], S.rsv[wv]};
   const uint32_t stride = gridDim.x * SW;
   for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
@@ -1111,6 +1355,79 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   const uint4 d = decl[i];
   if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
   filt_insert(fs, d.x, d.y);
+}
+
+// Restart backup (before a re-parse round that may resume chunks from their
+// rows): every flagged chunk with a contradicted-lookup time gets a backup
+// slot (while slots last) holding its previous pass's reference rows, REF
+// output lengths, batch hits, counts and output bytes.  One workgroup per chunk.
+__global__ __launch_bounds__(256) void restart_backup_kernel(uint32_t n, const uint32_t* need, const uint32_t* bad_t,
+                                                             uint32_t* bslot, uint32_t* b_count, uint32_t slots,
+                                                             const uint8_t* out, const uint64_t* out_off,
+                                                             const uint64_t* out_len, uint8_t* b_out, uint64_t stride,
+                                                             const uint4* ev, const uint32_t* eo, const uint32_t* nev,
+                                                             uint32_t maxe, const uint64_t* hits, const uint32_t* nhits,
+                                                             uint32_t maxh, const uint32_t* ndecl, uint4* b_ev,
+                                                             uint32_t* b_eo, uint64_t* b_hits, uint32_t* b_cnt) {
+  __shared__ uint32_t sk;
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  if (c >= n) return;
+  if (t == 0) {
+    uint32_t k = ~0u;
+    // (overflowed rows are incomplete: such a chunk re-parses from the start)
+    if (need[c] && bad_t[c] != ~0u && nev[c] <= maxe && nhits[c] <= maxh) {
+      const uint32_t j = atomicAdd(b_count, 1u);
+      if (j < slots) {
+        k = j;
+        atomicAdd(b_count + 2, 1u);                  // (cumulative: chunks resumed from their rows)
+      }
+    }
+    bslot[c] = k;
+    sk = k;
+  }
+  __syncthreads();
+  const uint32_t k = sk;
+  if (k == ~0u) return;
+  const uint32_t ne = nev[c], nh = nhits[c];
+  const uint64_t ol = out_len[c];
+  if (t == 0) {
+    b_cnt[4 * k] = ne;
+    b_cnt[4 * k + 1] = nh;
+    b_cnt[4 * k + 2] = (uint32_t)ol;
+    b_cnt[4 * k + 3] = ndecl[c];
+  }
+  for (uint32_t i = t; i < ne; i += 256) {
+    b_ev[(uint64_t)k * maxe + i] = ev[(uint64_t)c * maxe + i];
+    b_eo[(uint64_t)k * maxe + i] = eo[(uint64_t)c * maxe + i];
+  }
+  for (uint32_t i = t; i < nh; i += 256) b_hits[(uint64_t)k * maxh + i] = hits[(uint64_t)c * maxh + i];
+  const uint8_t* src = out + out_off[c];
+  uint8_t* dst = b_out + (uint64_t)k * stride;
+  for (uint64_t i = 16ull * t; i < ol; i += 16ull * 256) {
+    if (i + 16 <= ol) *(u32x4_u*)(dst + i) = *(const u32x4_u*)(src + i);
+    else for (uint64_t j = i; j < ol; ++j) dst[j] = src[j];
+  }
+}
+
+// After that round: the old output tail of every spliced chunk (its previous
+// pass's bytes from the rejoin point on) to its place behind the new part.
+__global__ __launch_bounds__(256) void restart_splice_kernel(uint32_t n, uint4* splice, const uint32_t* bslot,
+                                                             const uint8_t* b_out, uint64_t stride, uint8_t* out,
+                                                             const uint64_t* out_off, uint32_t* b_count) {
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  if (c >= n) return;
+  const uint4 sp = splice[c];
+  if (sp.w == 0u) return;
+  if (t == 0) atomicAdd(b_count + 3, 1u);          // (cumulative: chunks that rejoined their old parse)
+  const uint8_t* src = b_out + (uint64_t)bslot[c] * stride + sp.y;
+  uint8_t* dst = out + out_off[c] + sp.x;
+  const uint64_t len = sp.z - sp.y;
+  for (uint64_t i = 16ull * t; i < len; i += 16ull * 256) {
+    if (i + 16 <= len) *(u32x4_u*)(dst + i) = *(const u32x4_u*)(src + i);
+    else for (uint64_t j = i; j < len; ++j) dst[j] = src[j];
+  }
+  __syncthreads();
+  if (t == 0) splice[c].w = 0u;
 }
 
 // Seed for the rounds instead of round 0: a chunk's cold parse (nothing
@@ -1459,6 +1776,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.ev = (uint4*)a->ev;
   prm.nev = a->nev;
   prm.maxe = a->maxe;
+  prm.eo = a->ev ? a->eo : nullptr;
+  prm.rs = RestartArgs{};
   const size_t tbytes = ((size_t)a->fmask + 1) * 16;
   const size_t gbytes = ((size_t)a->gmask + 1) * 4;
   int dev = 0;
@@ -1586,8 +1905,27 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     prm.skip_below = seeded ? 0 : fc + 1;            // (seeded: round 1 parses every chunk)
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     if (keep && a->need_given) prm.need = a->need;   // the rest stand under the kept lists
+    const bool rs = keep && a->need_given && a->restart && a->bslot && prm.eo;
+    if (rs) {
+      // flagged chunks resume from their rows (encode_chunk, "Re-parse restart")
+      if (hipMemsetAsync(a->b_count, 0, 4, stream) != hipSuccess) return -5;
+      hipLaunchKernelGGL(restart_backup_kernel, dim3(n), dim3(256), 0, stream, n, (const uint32_t*)a->need,
+                         (const uint32_t*)a->bad_t, a->bslot, a->b_count, a->b_slots, (const uint8_t*)a->out,
+                         a->out_off, (const uint64_t*)a->out_len, a->b_out, a->b_stride, (const uint4*)a->ev,
+                         (const uint32_t*)a->eo, (const uint32_t*)a->nev, a->maxe, (const uint64_t*)a->hits,
+                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)a->ndecl, (uint4*)a->b_ev, a->b_eo,
+                         a->b_hits, a->b_cnt);
+      prm.rs = RestartArgs{a->bad_t, a->bad_hi, a->bslot, (const uint4*)a->b_ev, a->b_eo, a->b_hits, a->b_cnt,
+                           (uint4*)a->splice};
+    }
     launch();
     ++rounds;
+    if (rs) {
+      hipLaunchKernelGGL(restart_splice_kernel, dim3(n), dim3(256), 0, stream, n, (uint4*)a->splice,
+                         (const uint32_t*)a->bslot, (const uint8_t*)a->b_out, a->b_stride, a->out, a->out_off,
+                         a->b_count);
+      prm.rs = RestartArgs{};                        // (later rounds re-parse from the start)
+    }
     prm.skip_below = 0;
     // (no host sync here: the verification's own sync tells whether round 1
     // changed anything that matters)

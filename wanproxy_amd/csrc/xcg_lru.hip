@@ -208,23 +208,36 @@ __global__ __launch_bounds__(256) void lru_seed_table_kernel(uint32_t n, const u
 
 
 // Every recorded lookup of a persistent entry against the recomputed times.
+// The in-chunk times of the first and last inconsistent lookup go to bad_t /
+// bad_hi (the re-parse resumes before the first and may rejoin its old parse
+// after the last, encode_chunk "Re-parse restart").
 __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, const uint64_t* hmin,
-                                                        const uint64_t* wpop, uint32_t* need, uint32_t* tot) {
+                                                        const uint64_t* wpop, uint32_t* need, uint32_t* tot,
+                                                        uint32_t* bad_t, uint32_t* bad_hi) {
   const uint32_t c = wave_chunk();
   if (c >= n) return;
   const uint64_t r0 = R.row(c);
   const uint32_t cnt = R.count(c);
-  bool bad = false;
+  uint32_t lo = ~0u, hi = 0u;
   for (uint32_t k = lane_id(); k < cnt; k += 64) {
     const uint4 e = R.ev[r0 + k];
     const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
     const uint64_t t = ev_time(c, e);
-    if (kind == EV_GHIT) bad |= t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
-    else if (kind == EV_GMISS) bad |= !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
+    bool bad = false;
+    if (kind == EV_GHIT) bad = t == hmin[ref] && !(t < wpop[ref]);        // hit after its eviction
+    else if (kind == EV_GMISS) bad = !(hmin[ref] == NEVER && t >= wpop[ref]);   // missed a live entry
+    if (bad) { lo = min(lo, e.z); hi = max(hi, e.z); }
   }
-  if (ballot(bad) != 0 && lane_id() == 0) {
-    need[c] = 1u;                                     // the next pass re-parses chunk c
-    atomicAdd(&tot[T_BAD], 1u);
+  for (int off = 32; off >= 1; off >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, off));
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, off));
+  }
+  if (lane_id() == 0) {
+    if (bad_t) { bad_t[c] = lo; bad_hi[c] = hi; }
+    if (lo != ~0u) {
+      need[c] = 1u;                                   // the next pass re-parses chunk c
+      atomicAdd(&tot[T_BAD], 1u);
+    }
   }
 }
 
@@ -495,7 +508,7 @@ xcg::ScanArgs scan_args(XcgLruState* L, uint32_t* nseg) {
 LruBatch batch_of(const XcgStreamArgs& a) {
   return LruBatch{a.n, a.in, a.chunk_off, a.decl, a.ndecl, a.maxd, a.ev, a.nev, a.maxe, 0, a.need,
                   a.g_keys, a.g_vals, a.g_mask, a.pool, a.nseg, a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask,
-                  a.status, (uint64_t)a.n * a.maxe};
+                  a.status, (uint64_t)a.n * a.maxe, a.bad_t, a.bad_hi};
 }
 
 // Eviction times from a batch's references: tau, first hits, the LRU-order
@@ -516,7 +529,7 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
   if (check)
     hipLaunchKernelGGL(lru_check_kernel, wgrid, dim3(256), 0, st, n, R, (const uint64_t*)L->hmin,
-                       (const uint64_t*)L->wpop, b.need, L->tot);
+                       (const uint64_t*)L->wpop, b.need, L->tot, b.bad_t, b.bad_hi);
   if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return -5;
@@ -668,8 +681,11 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     if (lru_debug()) fprintf(stderr, "lru: commit %.3f ms\n", ms(c0, dsync()));
     L->last_base = i0;
     i0 += m;
+    // (a sub-batch that started below the limit saw fewer cached entries to
+    // look up than the next will: size the next one more cautiously)
     const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
-    const uint64_t want = used ? (uint64_t)C * 9 / 10 * m / used : (uint64_t)n;
+    const uint64_t pct = L->h_tot[T_A] < C ? 75 : 88;
+    const uint64_t want = used ? (uint64_t)C * pct / 100 * m / used : (uint64_t)n;
     per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
   }
   if (rounds_out) *rounds_out = rounds;

@@ -283,6 +283,7 @@ struct XcgPairState {
   // pass results
   bool split = false;
   std::vector<uint8_t> bad;        // per chunk: a recorded lookup the replay contradicts
+  std::vector<uint32_t> blo, bhi;  // ... the in-chunk times of the first and last such lookup
   std::vector<uint4> writes;       // commit moves (dest, kind, a, b)
   uint32_t nstaged = 0;
   uint64_t enters = 0, refs = 0, appends = 0;
@@ -346,6 +347,11 @@ struct XcgPairState {
     return e;
   }
   bool is_new(uint32_t x) const { return x >= C + D; }
+  void mark_bad(uint32_t c, uint32_t t) {
+    bad[c] = 1;
+    blo[c] = t < blo[c] ? t : blo[c];
+    bhi[c] = t > bhi[c] ? t : bhi[c];
+  }
   // an entity's current primary slot / disk block
   uint32_t& ep(uint32_t x) { return is_new(x) ? ns[x - C - D].p : E(x).p; }
   uint32_t& ed(uint32_t x) { return is_new(x) ? ns[x - C - D].d : E(x).d; }
@@ -485,6 +491,8 @@ struct XcgPairState {
     enters = refs = appends = 0;
     split = false;
     bad.assign(n, 0);
+    blo.assign(n, ~0u);
+    bhi.assign(n, 0u);
     s_head = head; s_tail = tail; s_pcount = pcount; s_ftop = ftop; s_dclock = dclock; s_dcount = dcount;
     std::vector<uint32_t> order;
     bool ok = true;
@@ -519,19 +527,19 @@ struct XcgPairState {
         const uint64_t t = ((uint64_t)c << 21) | e.z;
         const uint64_t h = ((uint64_t)e.y << 32) | e.x;
         if (kind == EV_GHIT || kind == EV_GMISS) {
-          if (ref >= C + D) { bad[c] = 1; ok = false; continue; }
+          if (ref >= C + D) { mark_bad(c, e.z); ok = false; continue; }
           const Ent& en = E(ref);
           const bool present = en.p != NIL || en.d != NIL;
-          if (present != (kind == EV_GHIT)) { bad[c] = 1; ok = false; }
+          if (present != (kind == EV_GHIT)) { mark_bad(c, e.z); ok = false; }
           if (present) lookup(ref, t);
         } else if (kind == EV_HIT) {
           const uint32_t x = bmap.find(h);
-          if (x == NIL) { bad[c] = 1; ok = false; continue; }
+          if (x == NIL) { mark_bad(c, e.z); ok = false; continue; }
           if (ep(x) == NIL && ed(x) == NIL) { split = true; break; }   // made here, gone already
           lookup(x, t);
         } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
           const uint32_t x0 = bmap.find(h);
-          if (x0 != NIL && (ep(x0) != NIL || ed(x0) != NIL)) { bad[c] = 1; ok = false; continue; }
+          if (x0 != NIL && (ep(x0) != NIL || ed(x0) != NIL)) { mark_bad(c, e.z); ok = false; continue; }
           const uint32_t x = C + D + (uint32_t)ns.size();
           ns.push_back(NewEnt{h, NIL, NIL, c, ref});
           bmap.put(h, x);
@@ -622,7 +630,7 @@ int download_refs(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
     if (P->h_need) (void)hipHostFree(P->h_need);
     P->h_nev = P->h_need = nullptr;
     P->h_nev_cap = 0;
-    if (hipHostMalloc(&P->h_nev, 4ull * a.n) != hipSuccess || hipHostMalloc(&P->h_need, 4ull * a.n) != hipSuccess)
+    if (hipHostMalloc(&P->h_nev, 4ull * a.n) != hipSuccess || hipHostMalloc(&P->h_need, 12ull * a.n) != hipSuccess)
       return -5;
     P->h_nev_cap = a.n;
   }
@@ -883,8 +891,15 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
       if (P->split) split = true;
       else if (ok) done = true;
       else {
-        for (uint32_t c = 0; c < m; ++c) P->h_need[c] = P->bad[c];
+        for (uint32_t c = 0; c < m; ++c) {
+          P->h_need[c] = P->bad[c];
+          P->h_need[m + c] = P->blo[c];
+          P->h_need[2 * m + c] = P->bhi[c];
+        }
         if (hipMemcpyAsync(a.need, P->h_need, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess) return -5;
+        if (a.bad_t && (hipMemcpyAsync(a.bad_t, P->h_need + m, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(a.bad_hi, P->h_need + 2 * m, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess))
+          return -5;
         if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
             ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
           return -5;

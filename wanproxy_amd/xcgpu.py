@@ -124,6 +124,8 @@ def lib():
     L.xcg_debug_stream_kernel_timing.restype = C.c_int
     L.xcg_debug_stream_kernel_time.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
     L.xcg_debug_stream_kernel_time.restype = C.c_int
+    L.xcg_debug_restart_counts.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.xcg_debug_restart_counts.restype = C.c_int
     L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     _lib = L
@@ -203,6 +205,13 @@ class Context:
         st = (C.c_uint64 * 4)()
         _check(lib().xcg_pair_stats(self.h, st))
         return tuple(int(v) for v in st)
+
+    def restart_counts(self):
+        """(chunks resumed from their rows, chunks that rejoined their old parse)
+        in this context's bounded / pair re-parse passes so far."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(lib().xcg_debug_restart_counts(self.h, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
 
     def cache_clear(self):
         _check(lib().xcg_cache_clear(self.h))
