@@ -1555,13 +1555,13 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
   if (vt == vv) return;
   const uint32_t INF = 0xFFFFFFFFu;
   const uint32_t ct = vt == ~0ull ? INF : (uint32_t)(vt >> 32), cv = vv == ~0ull ? INF : (uint32_t)(vv >> 32);
+  uint32_t rlo = INF, rhi = 0;
   if (ct < cv) atomicMin(a_first, ct + 1);                                   // (a)
   bool same = false;
   if (vt != ~0ull && vv != ~0ull)
     same = seg_equal_t(in + chunk_off[ct] + (uint32_t)vt, in + chunk_off[cv] + (uint32_t)vv);
   // (b): chunks in (cv, ct] lose h; with other bytes, every chunk > min(cv, ct) that found h
-  uint32_t rlo = INF, rhi = 0;
-  if (cv < ct) { rlo = cv + 1; rhi = ct == INF ? INF - 1 : ct; }
+  if (cv < ct) { rlo = min(rlo, cv + 1); rhi = max(rhi, ct == INF ? INF - 1 : ct); }
   if (!same && ct != INF && cv != INF) { rlo = min(rlo, min(ct, cv) + 1); rhi = INF - 1; }
   if (rlo <= rhi && !tab_insert_min(rt, (uint32_t)h, (uint32_t)(h >> 32), ((uint64_t)rlo << 32) | rhi))
     atomicOr(status, 2);
@@ -1898,6 +1898,25 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
                        FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
     return hipGetLastError() == hipSuccess;
   };
+  // A re-parse round whose flagged chunks (their first contradicted lookup in
+  // bad_t) resume from their rows (encode_chunk, "Re-parse restart"): back
+  // the rows up, parse, splice the rejoined tails' bytes.
+  auto run_restarted = [&]() {
+    (void)hipMemsetAsync(a->b_count, 0, 4, stream);
+    hipLaunchKernelGGL(restart_backup_kernel, dim3(n), dim3(256), 0, stream, n, (const uint32_t*)a->need,
+                       (const uint32_t*)a->bad_t, a->bslot, a->b_count, a->b_slots, (const uint8_t*)a->out,
+                       a->out_off, (const uint64_t*)a->out_len, a->b_out, a->b_stride, (const uint4*)a->ev,
+                       (const uint32_t*)a->eo, (const uint32_t*)a->nev, a->maxe, (const uint64_t*)a->hits,
+                       (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)a->ndecl, (uint4*)a->b_ev, a->b_eo,
+                       a->b_hits, a->b_cnt);
+    prm.rs = RestartArgs{a->bad_t, a->bad_hi, a->bslot, (const uint4*)a->b_ev, a->b_eo, a->b_hits, a->b_cnt,
+                         (uint4*)a->splice};
+    launch();
+    hipLaunchKernelGGL(restart_splice_kernel, dim3(n), dim3(256), 0, stream, n, (uint4*)a->splice,
+                       (const uint32_t*)a->bslot, (const uint8_t*)a->b_out, a->b_stride, a->out, a->out_off,
+                       a->b_count);
+    prm.rs = RestartArgs{};
+  };
   if (n > 1 && fc != ~0u) {
     if (!build(cur, false)) return -5;
     prm.use_b = true;
@@ -1906,26 +1925,9 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
     if (keep && a->need_given) prm.need = a->need;   // the rest stand under the kept lists
     const bool rs = keep && a->need_given && a->restart && a->bslot && prm.eo;
-    if (rs) {
-      // flagged chunks resume from their rows (encode_chunk, "Re-parse restart")
-      if (hipMemsetAsync(a->b_count, 0, 4, stream) != hipSuccess) return -5;
-      hipLaunchKernelGGL(restart_backup_kernel, dim3(n), dim3(256), 0, stream, n, (const uint32_t*)a->need,
-                         (const uint32_t*)a->bad_t, a->bslot, a->b_count, a->b_slots, (const uint8_t*)a->out,
-                         a->out_off, (const uint64_t*)a->out_len, a->b_out, a->b_stride, (const uint4*)a->ev,
-                         (const uint32_t*)a->eo, (const uint32_t*)a->nev, a->maxe, (const uint64_t*)a->hits,
-                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)a->ndecl, (uint4*)a->b_ev, a->b_eo,
-                         a->b_hits, a->b_cnt);
-      prm.rs = RestartArgs{a->bad_t, a->bad_hi, a->bslot, (const uint4*)a->b_ev, a->b_eo, a->b_hits, a->b_cnt,
-                           (uint4*)a->splice};
-    }
-    launch();
+    if (rs) run_restarted();
+    else launch();
     ++rounds;
-    if (rs) {
-      hipLaunchKernelGGL(restart_splice_kernel, dim3(n), dim3(256), 0, stream, n, (uint4*)a->splice,
-                         (const uint32_t*)a->bslot, (const uint8_t*)a->b_out, a->b_stride, a->out, a->out_off,
-                         a->b_count);
-      prm.rs = RestartArgs{};                        // (later rounds re-parse from the start)
-    }
     prm.skip_below = 0;
     // (no host sync here: the verification's own sync tells whether round 1
     // changed anything that matters)
@@ -1961,7 +1963,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       cur = nxt;
       prm.b = tabs[cur];
       prm.need = a->need;
-      launch();
+      launch();                                      // (flagged by the verification: from the start)
       ++rounds;
     }
     if (!converged) return -75;
