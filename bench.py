@@ -49,6 +49,9 @@ def parse():
     ap.add_argument('--no-extras', action='store_true', help='skip the stream / decode / PCIe side measurements')
     ap.add_argument('--no-configs', action='store_true',
                     help='skip the C3 / C4 / C5 stream-configuration figures (scripts/configs_bench.py)')
+    ap.add_argument('--dist-backend', default='nccl',
+                    help='torch.distributed backend for N > 1 (nccl = RCCL; gloo rehearses the N > 1 path with '
+                         'several ranks sharing one GPU: device = LOCAL_RANK mod the visible GPUs)')
     return ap.parse_args()
 
 
@@ -503,7 +506,7 @@ def other_configs():
     return out
 
 
-def sharded_configs(world, rank, dev):
+def sharded_configs(world, rank, dev, backend='nccl'):
     """N > 1: BASELINE configs C4 and C5 as ONE dataset each, split into
     contiguous per-rank ranges (wanproxy_amd/shard.py config_shard: C4 2^20/N
     packets, C5 8 GiB/N), every rank encoding its range with a private cache
@@ -523,7 +526,7 @@ def sharded_configs(world, rank, dev):
         if w is None:
             dist.barrier()
             return None
-        t = torch.tensor([w], dtype=torch.float64, device=dev)
+        t = torch.tensor([w], dtype=torch.float64, device=dev if backend == 'nccl' else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
     a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, world=world, rank=rank, reduce=reduce,
@@ -536,7 +539,8 @@ def sharded_configs(world, rank, dev):
         except BaseException as e:          # SystemExit from a parity check included
             r, err = None, f'{type(e).__name__}: {e}'
         t = torch.tensor([0.0 if r is None else float(r['in_bytes']), 1.0 if err else 0.0, 0.0 if r is None else
-                          float(r['encode_wall_s'])], dtype=torch.float64, device=dev)
+                          float(r['encode_wall_s'])], dtype=torch.float64,
+                         device=dev if backend == 'nccl' else None)
         dist.all_reduce(t[:2], op=dist.ReduceOp.SUM)
         tot, fails = float(t[0]), int(t[1])
         if fails:
@@ -557,8 +561,12 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
+        local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device('cuda', torch.cuda.current_device())
@@ -623,10 +631,11 @@ def main():
     if world == 1 and not args.no_extras:
         extras = side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_ol, d_st, n, stream, dev,
                                    rank)
-    sharded = sharded_configs(world, rank, dev) if world > 1 and not args.no_configs else None
+    sharded = sharded_configs(world, rank, dev, args.dist_backend) if world > 1 and not args.no_configs else None
 
     from wanproxy_amd.shard import reduce_run
-    wall, job_bytes = reduce_run(wall, in_bytes, device=dev)   # max wall, total bytes over ranks
+    red_dev = dev if args.dist_backend == 'nccl' else None
+    wall, job_bytes = reduce_run(wall, in_bytes, device=red_dev)   # max wall, total bytes over ranks
     total_bytes = float(job_bytes) * args.steps
     value = total_bytes / 2**30 / wall
 
