@@ -227,6 +227,12 @@ int ctx_wait(xcg_ctx* c) {
 void ctx_mark(xcg_ctx* c, hipStream_t st) {
   if (c->done_ev) (void)hipEventRecord(c->done_ev, st);
 }
+// Work enqueued on `st` starts after the context's last enqueued work (a cache
+// clear on another stream, the previous call of another stream): the
+// reference's calls on one cache are serialised, and so are these.
+void ctx_order(xcg_ctx* c, hipStream_t st) {
+  if (c->done_ev) (void)hipStreamWaitEvent(st, c->done_ev, 0);
+}
 
 uint32_t pow2_at_least(uint64_t v) {
   uint64_t p = 1;
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(256) void cache_wipe_kernel(uint4* kv, uint64_t kv_
   if (i0 == 0) *nseg = 0u;
 }
 
-int clear_cache(GpuCache& g) {
+int clear_cache(GpuCache& g, bool sync = true) {
   // keys and vals are separate allocations of (mask + 1) u64 each (>= 1024)
   const uint64_t half = (uint64_t)(g.mask + 1) / 2;   // uint4 per array
   hipLaunchKernelGGL(cache_wipe_kernel, dim3(1024), dim3(256), 0, nullptr, (uint4*)g.keys, half, g.nseg,
@@ -331,7 +337,7 @@ int clear_cache(GpuCache& g) {
                      ((uint64_t)g.gmask + 1) / 4);
   hipLaunchKernelGGL(cache_wipe_kernel, dim3(256), dim3(256), 0, nullptr, (uint4*)g.vals, half, g.nseg,
                      (uint4*)nullptr, 0u, (uint4*)nullptr, 0ull, (uint4*)nullptr, 0ull);
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) return XCG_EHIP;
+  if (hipGetLastError() != hipSuccess || (sync && hipStreamSynchronize(nullptr) != hipSuccess)) return XCG_EHIP;
   return XCG_OK;
 }
 
@@ -610,7 +616,11 @@ int xcg_cache_clear(xcg_ctx* c) {
   // (the LRU clock keeps running: slots keep their last-reference times, which
   // must stay below every later batch's)
   if (c->pair && xcg_pair_state_clear(c->pair) != 0) return XCG_EHIP;
-  return clear_cache(c->g);
+  // asynchronous: the context's later work waits for the wipe on the device
+  // (ctx_order), host inspection calls wait for it (ctx_wait)
+  const int rc = clear_cache(c->g, c->done_ev == nullptr);
+  ctx_mark(c, nullptr);
+  return rc;
 }
 
 int xcg_last_rounds(xcg_ctx* c) { return c ? c->last_rounds : -1; }
@@ -869,6 +879,7 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
   if (semantics != XCG_SEM_INDEPENDENT && semantics != XCG_SEM_STREAM) return XCG_EINVAL;
   if (max_chunk_len > (1u << 19)) return XCG_EINVAL;
   DeviceGuard g(c->device);
+  ctx_order(c, (hipStream_t)stream);
   // A null cache has no state to carry: both semantics are the same pass.
   if (semantics == XCG_SEM_STREAM && !(c->flags & XCG_FLAG_NULLCACHE)) {
     // declaration slots per chunk: a chunk of L bytes declares at most L / 2048
@@ -1107,6 +1118,7 @@ int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_
   if (n == 0) return XCG_OK;
   if (c->pair) return XCG_ENOTSUP;
   DeviceGuard g(c->device);
+  ctx_order(c, (hipStream_t)stream);
   int rc = ensure_cache(c);
   if (rc == XCG_OK) rc = ensure_dscratch(c, (uint64_t)n * (max_chunk_len / 2050 + 1));
   if (rc == XCG_OK) rc = ensure_dchunks(c, n);

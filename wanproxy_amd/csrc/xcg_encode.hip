@@ -1437,48 +1437,68 @@ __global__ __launch_bounds__(256) void restart_splice_kernel(uint32_t n, uint4* 
 // tiling of the chunks before it; the verification flags every chunk the
 // guess misled, so the result is exact whatever the data.  One wave per
 // (chunk, tile): a hash pass over the batch instead of a full parse.
+// SEED_TILES tiles per wave (several waves per chunk): all of a wave's loads
+// are in flight together, and the batch's ~32 k waves hide HBM latency (one
+// wave per chunk walking its tiles four at a time left each wave waiting).
+constexpr uint32_t SEED_TILES = 8;
 __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, const uint64_t* chunk_off,
                                                           const uint32_t* chunk_len, uint32_t n, uint32_t maxd,
                                                           uint4* decl, uint32_t* ndecl, uint32_t* nhits,
                                                           uint32_t* changed) {
-  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);   // one wave per chunk
-  if (c == 0 && threadIdx.x == 0) *changed = ~0u;
+  const uint32_t wpc = (maxd + SEED_TILES - 1) / SEED_TILES;       // waves per chunk
+  const uint32_t w = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  const uint32_t c = w / wpc, k0 = (w % wpc) * SEED_TILES;
+  if (w == 0 && threadIdx.x == 0) *changed = ~0u;
   if (c >= n) return;
   const int l = lane_id();
   const uint32_t m = min(chunk_len[c] / SEG, maxd);    // (an over-long chunk is refused by the round)
   const uint8_t* x = in + chunk_off[c];
-  if (l == 0) {
+  if (l == 0 && k0 == 0) {
     ndecl[c] = m;
     nhits[c] = 0u;
   }
-  // four tiles per step: lane l sums bytes [16 l, 16 l + 16) and [1024 + 16 l, ...) of each
-  for (uint32_t k0 = 0; k0 < m; k0 += 4) {
-    u32x4 v[4][2];
+  if (k0 >= m) return;
+  // lane l sums bytes [16 l, 16 l + 16) and [1024 + 16 l, ...) of each tile
+  u32x4 v[SEED_TILES][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+  for (uint32_t t = 0; t < SEED_TILES; ++t)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-        v[t][h] = k0 + t < m ? *(const u32x4_u*)(x + (uint64_t)(k0 + t) * SEG + 1024u * h + 16u * l)
-                             : u32x4{0u, 0u, 0u, 0u};
+    for (int h = 0; h < 2; ++h)
+      v[t][h] = k0 + t < m ? *(const u32x4_u*)(x + (uint64_t)(k0 + t) * SEG + 1024u * h + 16u * l)
+                           : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (k0 + t >= m) break;
-      uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
+  for (uint32_t t = 0; t < SEED_TILES; ++t) {
+    if (k0 + t >= m) break;
+    // Per 16-byte group h (offset q0 = 1024 h + 16 l in the tile): plain and
+    // k-weighted sums of the bytes (v_dot4) and of ffs = ffbl + 1 (ffbl of a
+    // zero byte is -1, so ffs sums are the ffbl sums + 16 and + 0 + ... + 15);
+    // then X2 = sum (2048 - q0) S - W per group, and the same for F.
+    uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t q0 = 1024u * h + 16u * l;
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t q0 = 1024u * h + 16u * l;
+      uint32_t sx = 0, wx = 0, sf = 0, wf = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const uint32_t xb = byte_of(v[t][h][k >> 2], k & 3);
-          const uint32_t f = ffbl(xb) + 1u;
-          const uint32_t wt = 2048u - (q0 + k);
-          X1 += xb; X2 += wt * xb; F1 += f; F2 += wt * f;
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const uint32_t d = v[t][h][w4];
+        const uint32_t wts = (4u * w4) | ((4u * w4 + 1) << 8) | ((4u * w4 + 2) << 16) | ((4u * w4 + 3) << 24);
+        sx = __builtin_amdgcn_udot4(d, 0x01010101u, sx, false);
+        wx = __builtin_amdgcn_udot4(d, wts, wx, false);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t f = ffbl(byte_of(d, b));
+          sf += f;
+          wf += (uint32_t)(4 * w4 + b) * f;
         }
       }
-      X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
-      if (l == 0) decl[(uint64_t)c * maxd + k0 + t] = make_uint4((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4,
-                                                                  (k0 + t) * SEG, 0u);
+      sf += 16u;
+      wf += 120u;
+      X1 += sx; X2 += (2048u - q0) * sx - wx;
+      F1 += sf; F2 += (2048u - q0) * sf - wf;
     }
+    X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
+    if (l == 0) decl[(uint64_t)c * maxd + k0 + t] = make_uint4((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4,
+                                                                (k0 + t) * SEG, 0u);
   }
 }
 
@@ -1699,7 +1719,8 @@ extern "C" uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys) {
 // then xcg_launch_encode_stream with keep_decls.
 extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream) {
   if (a->n == 0) return 0;
-  hipLaunchKernelGGL(xcg::seed_tiling_kernel, dim3((a->n + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
+  const uint32_t seed_waves = a->n * ((a->maxd + xcg::SEED_TILES - 1) / xcg::SEED_TILES);
+  hipLaunchKernelGGL(xcg::seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
                      a->chunk_len, a->n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -1852,7 +1873,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     // the previous pass's declaration lists seed round 1 (a bounded cache's
     // eviction times changed under them)
   } else if (seeded) {
-    hipLaunchKernelGGL(seed_tiling_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
+    const uint32_t seed_waves = n * ((a->maxd + SEED_TILES - 1) / SEED_TILES);
+    hipLaunchKernelGGL(seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
                        a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
   } else {
     launch();
