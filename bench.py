@@ -494,7 +494,7 @@ def other_configs():
     # eviction), every chunk checked against the oracle's bounded cache
     # C5-PAIR: C5 on wanproxy.conf's whole cache, the 128 MiB memory cache over
     # a 1 GiB disk (XCodecCachePair), every chunk checked against the oracle's pair
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, lru_mib=128, lru_check=1.0,
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, lru_mib=128, lru_check=1.0,
                            disk_mib=1024, no_decode=False)
     out = {}
     for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru),
@@ -529,7 +529,7 @@ def sharded_configs(world, rank, dev, backend='nccl'):
         t = torch.tensor([w], dtype=torch.float64, device=dev if backend == 'nccl' else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=16384, world=world, rank=rank, reduce=reduce,
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, world=world, rank=rank, reduce=reduce,
                            no_decode=False, check_c4=16384, check_c5=512)
     out = {}
     for name, fn in (('C4', cb.run_c4), ('C5', cb.run_c5)):

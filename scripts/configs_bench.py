@@ -391,7 +391,7 @@ def main():
     ap.add_argument('--scale', type=float, default=1.0)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--batch-mib', type=int, default=512)
-    ap.add_argument('--c4-batch', type=int, default=16384)
+    ap.add_argument('--c4-batch', type=int, default=65536)
     ap.add_argument('--lru-mib', type=int, default=128)
     ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')

@@ -119,6 +119,9 @@ struct BatchScratch {
   uint32_t* need = nullptr;
   uint32_t* vflags = nullptr;
   uint32_t* h_vflags = nullptr;    // pinned
+  uint64_t* a_keys = nullptr;      // newly visible hashes -> chunk range (verification (a))
+  uint64_t* a_vals = nullptr;
+  uint32_t* a_bits = nullptr;
   uint32_t last_maxd = 0;          // declaration stride of the last stream batch
   // bounded cache: every chunk's cache references (xcg_lru.hip)
   void* ev = nullptr;              // n_cap * maxe uint4
@@ -286,6 +289,7 @@ void free_scratch(BatchScratch& b) {
   (void)hipFree(b.eo); (void)hipFree(b.bad_t); (void)hipFree(b.bad_hi); (void)hipFree(b.bslot);
   (void)hipFree(b.b_count); (void)hipFree(b.b_ev); (void)hipFree(b.b_eo); (void)hipFree(b.b_hits);
   (void)hipFree(b.b_cnt); (void)hipFree(b.b_out); (void)hipFree(b.splice);
+  (void)hipFree(b.a_keys); (void)hipFree(b.a_vals); (void)hipFree(b.a_bits);
   b = BatchScratch{};
 }
 
@@ -391,7 +395,9 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipMalloc(&b.r_keys, 16ull * cap) != hipSuccess || hipMalloc(&b.r_vals, 16ull * cap) != hipSuccess ||
       hipMalloc(&b.hits, 8ull * n * (maxd + 8)) != hipSuccess || hipMalloc(&b.nhits, 4ull * n) != hipSuccess ||
       hipMalloc(&b.need, 4ull * n) != hipSuccess || hipMalloc(&b.vflags, 16) != hipSuccess ||
-      hipHostMalloc(&b.h_vflags, 16) != hipSuccess) {
+      hipHostMalloc(&b.h_vflags, 16) != hipSuccess || hipMalloc(&b.a_keys, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
+      hipMalloc(&b.a_vals, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
+      hipMalloc(&b.a_bits, 4ull * XCG_VERIFY_A_WORDS) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
@@ -903,6 +909,9 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     uint32_t decls = ~0u;
     a.decls_out = &decls;
     int rounds = 0;
+    a.a_keys = c->bs.a_keys;
+    a.a_vals = c->bs.a_vals;
+    a.a_bits = getenv("XCG_NO_APROBE") ? nullptr : c->bs.a_bits;
     if (c->pair || c->bounded) {
       BatchScratch& b = c->bs;
       a.eo = b.eo; a.bad_t = b.bad_t; a.bad_hi = b.bad_hi; a.bslot = b.bslot; a.b_count = b.b_count;

@@ -81,7 +81,16 @@ struct XcgStreamArgs {
   uint8_t* b_out;        // [b_slots * b_stride]
   uint64_t b_stride;
   void* splice;          // [n] uint4
+  // verification (a), exactly (verify_probe_kernel): the hashes that became
+  // visible to more chunks -> that chunk range, and their Bloom words
+  uint64_t* a_keys;      // [XCG_VERIFY_A_CAP]
+  uint64_t* a_vals;
+  uint32_t* a_bits;      // [XCG_VERIFY_A_WORDS]
 };
+
+// (a)-probe sizes: at most A_LIMIT newly visible hashes per verification (more:
+// the conservative flag), a table of twice that, a 32 KiB blocked Bloom filter.
+constexpr uint32_t XCG_VERIFY_A_LIMIT = 8192, XCG_VERIFY_A_CAP = 16384, XCG_VERIFY_A_WORDS = 8192;
 
 // Bounded cache (xcg_lru.hip): device LRU state of a context.
 struct XcgLruState {

@@ -846,6 +846,21 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       if (is_new && j < no && hlo == olo && hhi == ohi) inD = false;
     }
     const uint64_t dm = ballot(inD);
+    // The old remainder's lookups of these are in its rows only where the old
+    // parse found the hash: as its own record (the old ones), in the
+    // persistent table, or in the batch table visible to this chunk.  A new
+    // declaration found nowhere else may have been missed there unrecorded
+    // (an in-chunk repeat): no splice then.
+    bool unknown = false;
+    if (is_new && inD) {
+      bool known = tab_lookup_t(prm.g, hlo, hhi) != ~0ull;
+      if (!known && prm.use_b) {
+        const uint64_t bv = tab_lookup_t(prm.b, hlo, hhi);
+        known = bv != ~0ull && (uint32_t)(bv >> 32) < chunk;
+      }
+      unknown = !known;
+    }
+    if (ballot(unknown)) return false;
     // the old remainder must not look any of them up (or declare one)
     for (uint32_t i0 = (uint32_t)it; i0 < o_nev; i0 += 64) {
       const uint32_t i = i0 + (uint32_t)l;
@@ -1374,8 +1389,9 @@ __global__ __launch_bounds__(256) void restart_backup_kernel(uint32_t n, const u
   if (c >= n) return;
   if (t == 0) {
     uint32_t k = ~0u;
-    // (overflowed rows are incomplete: such a chunk re-parses from the start)
-    if (need[c] && bad_t[c] != ~0u && nev[c] <= maxe && nhits[c] <= maxh) {
+    // (overflowed rows are incomplete: such a chunk re-parses from the start,
+    // like one flagged with bad_t 0 or ~0)
+    if (need[c] && bad_t[c] != ~0u && bad_t[c] != 0u && nev[c] <= maxe && nhits[c] <= maxh) {
       const uint32_t j = atomicAdd(b_count, 1u);
       if (j < slots) {
         k = j;
@@ -1517,6 +1533,8 @@ struct RoundPrep {
   uint32_t* changed;
   HashTab rt;           // keys == nullptr: not a verification round
   uint32_t* vflags;
+  HashTab at;           // (keys == nullptr: no (a)-probe) newly visible hashes
+  uint32_t* abits;
 };
 __global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1525,13 +1543,17 @@ __global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
   for (uint64_t i = i0; i <= a.tab.mask; i += stride) { a.tab.keys[i] = EMPTY_KEY; a.tab.vals[i] = ~0ull; }
   if (a.rt.keys)
     for (uint64_t i = i0; i <= a.rt.mask; i += stride) { a.rt.keys[i] = EMPTY_KEY; a.rt.vals[i] = ~0ull; }
+  if (a.rt.keys && a.at.keys) {
+    for (uint64_t i = i0; i <= a.at.mask; i += stride) { a.at.keys[i] = EMPTY_KEY; a.at.vals[i] = ~0ull; }
+    for (uint64_t i = i0; i < XCG_VERIFY_A_WORDS; i += stride) a.abits[i] = 0u;
+  }
   for (uint64_t i = i0; i < FILT_WORDS; i += stride) a.r_filt[i] = g_empty ? 0u : a.g_filt[i];
   for (uint64_t i = i0; i < a.ftab_n; i += stride) a.r_ftab[i] = g_empty ? u32x4{0u, 0u, 0u, 0u} : a.g_ftab[i];
   for (uint64_t i = i0; i < a.gfilt_n; i += stride) a.r_gfilt[i] = g_empty ? 0u : a.g_gfilt[i];
   if (i0 < 64) a.bcount[i0] = 0u;
   if (i0 == 0) {
     *a.changed = ~0u;
-    if (a.rt.keys) { a.vflags[0] = ~0u; a.vflags[1] = 0u; }
+    if (a.rt.keys) { a.vflags[0] = ~0u; a.vflags[1] = 0u; a.vflags[3] = 0u; }
   }
 }
 
@@ -1541,7 +1563,9 @@ __global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
 // declarations; T = the table of round r's.  k's parse depends on the batch
 // only through its lookups, so it stands under T unless, for some hash h,
 // (a) h becomes visible to k (earliest declaring chunk c_T < k <= c_V: a miss
-//     may turn into a hit) -- flagged conservatively for every k > c_T; or
+//     may turn into a hit) and one of k's windows has hash h
+//     (verify_probe_kernel; with more than XCG_VERIFY_A_LIMIT such hashes,
+//     conservatively every k > c_T); or
 // (b) k found h in V (a recorded hit) and under T h is invisible to k, or its
 //     earliest declaration has other bytes.
 // The fixed point is reached when no chunk is flagged.
@@ -1552,9 +1576,17 @@ __device__ __forceinline__ bool seg_equal_t(const uint8_t* a, const uint8_t* b) 
   return true;
 }
 
+// The newly visible hashes' blocked Bloom filter: one word, two bits.
+__device__ __forceinline__ uint32_t abits_word(uint32_t lo, uint32_t hi) {
+  return (lo ^ (hi >> 4)) & (XCG_VERIFY_A_WORDS - 1u);
+}
+__device__ __forceinline__ uint32_t abits_mask(uint32_t lo, uint32_t hi) {
+  return (1u << ((lo >> 13) & 31u)) | (1u << ((hi >> 21) & 31u));
+}
+
 __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt, const uint8_t* in,
                                                           const uint64_t* chunk_off, HashTab rt, uint32_t* a_first,
-                                                          int32_t* status) {
+                                                          HashTab at, uint32_t* abits, int32_t* status) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nt = (uint64_t)tt.mask + 1, nv = (uint64_t)tv.mask + 1;
   uint64_t h, vt, vv;
@@ -1576,7 +1608,18 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
   const uint32_t INF = 0xFFFFFFFFu;
   const uint32_t ct = vt == ~0ull ? INF : (uint32_t)(vt >> 32), cv = vv == ~0ull ? INF : (uint32_t)(vv >> 32);
   uint32_t rlo = INF, rhi = 0;
-  if (ct < cv) atomicMin(a_first, ct + 1);                                   // (a)
+  if (ct < cv) {                                                             // (a)
+    atomicMin(a_first, ct + 1);
+    if (at.keys) {                  // chunks (ct, cv] newly see h (a_first[3]: how many such h)
+      const uint32_t j = atomicAdd(a_first + 3, 1u);
+      if (j < XCG_VERIFY_A_LIMIT) {
+        const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+        if (!tab_insert_min(at, lo, hi, ((uint64_t)(ct + 1) << 32) | (cv == INF ? INF - 1 : cv)))
+          atomicOr(a_first + 3, 0x80000000u);                                 // (conservative then)
+        atomicOr(abits + abits_word(lo, hi), abits_mask(lo, hi));
+      }
+    }
+  }
   bool same = false;
   if (vt != ~0ull && vv != ~0ull)
     same = seg_equal_t(in + chunk_off[ct] + (uint32_t)vt, in + chunk_off[cv] + (uint32_t)vv);
@@ -1587,15 +1630,131 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
     atomicOr(status, 2);
 }
 
-// need[k] for every chunk: (a) or an overflowed hit list; then (b), one
-// thread per recorded hit (verify_hits_kernel).
+// need[k] for every chunk: the conservative (a) (no probe, or too many newly
+// visible hashes) or overflowed hit / reference lists -- such a chunk re-parses
+// from its start (bad_t 0); then (a) by the probe and (b), which also give
+// the times of the first and last affected lookup (bad_t / bad_hi, for the
+// re-parse restart; ~0 / 0 until then).
 __global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uint32_t* nhits, uint32_t maxh,
-                                                           const uint32_t* a_first, uint32_t* need, uint32_t* any) {
+                                                           const uint32_t* nev, uint32_t maxe, bool probe,
+                                                           const uint32_t* vflags, uint32_t* need, uint32_t* any,
+                                                           uint32_t* bad_t, uint32_t* bad_hi) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const bool f = k >= *a_first || nhits[k] > maxh;
+  const bool conservative = !probe || vflags[3] > XCG_VERIFY_A_LIMIT;
+  const bool f = (k >= vflags[0] && conservative) || nhits[k] > maxh || (nev && nev[k] > maxe);
   need[k] = f ? 1u : 0u;
+  if (bad_t) {
+    bad_t[k] = f ? 0u : ~0u;
+    bad_hi[k] = f ? ~1u : 0u;
+  }
   if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
+}
+
+// Flag chunk k with the in-chunk times [lo, hi] of affected lookups.
+__device__ __forceinline__ void flag_chunk(uint32_t k, uint32_t lo, uint32_t hi, uint32_t* need, uint32_t* any,
+                                           uint32_t* bad_t, uint32_t* bad_hi) {
+  for (int off = 32; off >= 1; off >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, off));
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, off));
+  }
+  if (lane_id() == 0 && lo != ~0u) {
+    need[k] = 1u;
+    atomicOr(any, 1u);
+    if (bad_t) {
+      atomicMin(bad_t + k, lo);
+      atomicMax(bad_hi + k, hi);
+    }
+  }
+}
+
+// (a) exactly: every window of every chunk >= a_first, hashed like
+// window_hashes_kernel (one wave per 2048 positions, 32 per lane), tested
+// against the newly visible hashes' Bloom filter in LDS, then exactly; a
+// window of chunk k whose hash became visible to k flags k at that window's
+// lookup time 2 s + 1.  Blocks loop over the (chunk, span) items.
+__global__ __launch_bounds__(256) void verify_probe_kernel(const uint8_t* in, const uint64_t* chunk_off,
+                                                           const uint32_t* chunk_len, uint32_t n, uint32_t spc,
+                                                           const uint32_t* vflags, HashTab at, const uint32_t* abits,
+                                                           uint32_t* need, uint32_t* any, uint32_t* bad_t,
+                                                           uint32_t* bad_hi) {
+  __shared__ uint32_t sb[XCG_VERIFY_A_WORDS];
+  const uint32_t a_first = vflags[0], acount = vflags[3];
+  if (acount == 0u || acount > XCG_VERIFY_A_LIMIT || a_first >= n) return;
+  for (uint32_t i = threadIdx.x; i < XCG_VERIFY_A_WORDS / 4; i += blockDim.x)
+    ((u32x4*)sb)[i] = ((const u32x4*)abits)[i];
+  __syncthreads();
+  const int l = lane_id();
+  const uint64_t items = (uint64_t)(n - a_first) * spc, nw = (uint64_t)gridDim.x * 4u;
+  for (uint64_t it = (uint64_t)blockIdx.x * 4u + readfirst(threadIdx.x >> 6); it < items; it += nw) {
+    const uint32_t k = a_first + (uint32_t)(it / spc);
+    const int64_t len = chunk_len[k], npos = len - SEG + 1, p = (int64_t)(it % spc) * SEG;
+    if (p >= npos) continue;
+    const uint8_t* x = in + chunk_off[k];
+    const int64_t q0 = p + 32 * l;
+    const u32x4 a0 = load16_guarded(x, q0, len), a1 = load16_guarded(x, q0 + 16, len);
+    const u32x4 b0 = load16_guarded(x, q0 + SEG, len), b1 = load16_guarded(x, q0 + SEG + 16, len);
+    const uint32_t xa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const uint32_t xb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    uint32_t sxa = 0, sqxa = 0, sfa = 0, sqfa = 0, sxb = 0, sqxb = 0, sfb = 0, sqfb = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const uint32_t va = byte_of(xa[j >> 2], j & 3), vb = byte_of(xb[j >> 2], j & 3);
+      const uint32_t fa = ffbl(va) + 1u, fb = ffbl(vb) + 1u;
+      sxa += va; sqxa += j * va; sfa += fa; sqfa += j * fa;
+      sxb += vb; sqxb += j * vb; sfb += fb; sqfb += j * fb;
+    }
+    const uint32_t qa = 32u * l, qb = 2048u + 32u * l;
+    const uint32_t ta = qa * sxa + sqxa, tb = qb * sxb + sqxb;
+    const uint32_t tfa = qa * sfa + sqfa, tfb = qb * sfb + sqfb;
+    const uint32_t dx = sxb - sxa, dt = tb - ta, df = sfb - sfa, dtf = tfb - tfa;
+    uint32_t X1 = wave_sum(sxa) + wave_incl_scan(dx) - dx;
+    const uint32_t TT = wave_sum(ta) + wave_incl_scan(dt) - dt;
+    uint32_t F1 = wave_sum(sfa) + wave_incl_scan(df) - df;
+    const uint32_t TF = wave_sum(tfa) + wave_incl_scan(dtf) - dtf;
+    uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
+    uint32_t F2 = (2048u + qa) * F1 - TF;
+    uint32_t tlo = ~0u, thi = 0u;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int64_t s = q0 + j;
+      const uint32_t lo = (X1 << 20) + X2c, hi = ((F1 << 16) + F2) << 4;
+      const uint32_t w = sb[abits_word(lo, hi)], m = abits_mask(lo, hi);
+      if (s < npos && (w & m) == m) {
+        const uint64_t v = tab_lookup_t(at, lo, hi);
+        if (v != ~0ull && k >= (uint32_t)(v >> 32) && k <= (uint32_t)v) {
+          tlo = min(tlo, 2u * (uint32_t)s + 1u);
+          thi = max(thi, 2u * (uint32_t)s + 1u);
+        }
+      }
+      const uint32_t xo = byte_of(xa[j >> 2], j & 3), xn = byte_of(xb[j >> 2], j & 3);
+      const uint32_t ro = ffbl(xo), rn = ffbl(xn);
+      X1 = X1 + xn - xo;
+      X2c = X2c + X1 - (xo << 11);
+      F1 = F1 + rn - ro;
+      F2 = F2 + F1 - (ro << 11) - 2048u;
+    }
+    flag_chunk(k, tlo, thi, need, any, bad_t, bad_hi);
+  }
+}
+
+// (b) from the reference rows (bounded caches: batch hits carry their lookup
+// times), one wave per chunk; the hit lists' verify_hits_kernel otherwise.
+__global__ __launch_bounds__(256) void verify_hit_events_kernel(uint32_t n, const uint4* ev, const uint32_t* nev,
+                                                                uint32_t maxe, HashTab rt, uint32_t* need,
+                                                                uint32_t* any, uint32_t* bad_t, uint32_t* bad_hi) {
+  const uint32_t k = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (k >= n) return;
+  const uint32_t cnt = min(nev[k], maxe);
+  uint32_t lo = ~0u, hi = 0u;
+  for (uint32_t i = lane_id(); i < cnt; i += 64) {
+    const uint4 e = ev[(uint64_t)k * maxe + i];
+    if ((e.w >> 30) == EV_HIT && (e.w & EV_REF_MASK) == 1u) {
+      const uint64_t r = tab_lookup_t(rt, e.x, e.y);
+      if (r != ~0ull && k >= (uint32_t)(r >> 32) && k <= (uint32_t)r) { lo = min(lo, e.z); hi = max(hi, e.z); }
+    }
+  }
+  flag_chunk(k, lo, hi, need, any, bad_t, bad_hi);
 }
 __global__ __launch_bounds__(256) void verify_hits_kernel(uint32_t n, const uint64_t* hits, const uint32_t* nhits,
                                                           uint32_t maxh, HashTab rt, uint32_t* need, uint32_t* any) {
@@ -1893,6 +2052,12 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   // the fixed point, which is the sequential result.
   HashTab tabs[2] = {HashTab{a->b_keys, a->b_vals, a->b_mask}, HashTab{a->b2_keys, a->b2_vals, a->b_mask}};
   const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
+  // (a) by probing the windows (a_bits null: the conservative flag)
+  const bool probe = a->a_bits && a->a_keys;
+  const HashTab at = probe ? HashTab{a->a_keys, a->a_vals, XCG_VERIFY_A_CAP - 1} : HashTab{nullptr, nullptr, 0u};
+  // later rounds resume flagged chunks too (bounded / pair: the verification
+  // gives the affected lookups' times)
+  const bool rs_rounds = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;
   int cur = 0;
   int dev_cus = (int)wgs;
   // Commit the declaration lists into the persistent cache; with a gate, only
@@ -1912,7 +2077,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   auto build = [&](int t, bool verify) -> bool {
     RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
                  a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
-                 verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags};
+                 verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags, at, a->a_bits};
     hipLaunchKernelGGL(round_prep_kernel, dim3(4 * dev_cus), dim3(256), 0, stream, rp);
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
@@ -1938,6 +2103,12 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
                        (const uint32_t*)a->bslot, (const uint8_t*)a->b_out, a->b_stride, a->out, a->out_off,
                        a->b_count);
     prm.rs = RestartArgs{};
+    if (stream_debug()) {
+      uint32_t bc[4] = {0, 0, 0, 0};
+      (void)hipMemcpyAsync(bc, a->b_count, 16, hipMemcpyDeviceToHost, stream);
+      (void)hipStreamSynchronize(stream);
+      fprintf(stderr, "stream: restart slots %u, cumulative resumed %u rejoined %u\n", bc[0], bc[2], bc[3]);
+    }
   };
   if (n > 1 && fc != ~0u) {
     if (!build(cur, false)) return -5;
@@ -1962,20 +2133,35 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       if (!build(nxt, true)) return -5;
       const uint64_t slots = 2ull * (a->b_mask + 1);
       hipLaunchKernelGGL(verify_diff_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, tabs[cur],
-                         tabs[nxt], a->in, a->chunk_off, rt, a->vflags, a->status);
+                         tabs[nxt], a->in, a->chunk_off, rt, a->vflags, at, a->a_bits, a->status);
+      uint32_t* vbad_t = rs_rounds ? a->bad_t : nullptr;
+      uint32_t* vbad_hi = rs_rounds ? a->bad_hi : nullptr;
       hipLaunchKernelGGL(verify_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n,
-                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)a->vflags, a->need, a->vflags + 1);
-      const uint64_t nh = (uint64_t)n * a->maxh;
-      hipLaunchKernelGGL(verify_hits_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, n,
-                         (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt, a->need, a->vflags + 1);
+                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)(a->ev ? a->nev : nullptr), a->maxe,
+                         probe, (const uint32_t*)a->vflags, a->need, a->vflags + 1, vbad_t, vbad_hi);
+      if (probe) {
+        const uint64_t items = (uint64_t)n * a->maxd;   // (chunk, 2048-position span) pairs, maxd per chunk
+        const uint64_t blocks = (items + 3) / 4, cap = 5ull * (uint64_t)dev_cus;   // (32 KiB of LDS each)
+        hipLaunchKernelGGL(verify_probe_kernel, dim3((unsigned)(blocks < cap ? blocks : cap)), dim3(256), 0, stream,
+                           a->in, a->chunk_off, a->chunk_len, n, a->maxd, (const uint32_t*)a->vflags, at,
+                           (const uint32_t*)a->a_bits, a->need, a->vflags + 1, vbad_t, vbad_hi);
+      }
+      if (a->ev) {
+        hipLaunchKernelGGL(verify_hit_events_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, n, (const uint4*)a->ev,
+                           (const uint32_t*)a->nev, a->maxe, rt, a->need, a->vflags + 1, vbad_t, vbad_hi);
+      } else {
+        const uint64_t nh = (uint64_t)n * a->maxh;
+        hipLaunchKernelGGL(verify_hits_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, n,
+                           (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt, a->need, a->vflags + 1);
+      }
       hipLaunchKernelGGL(count_decls_kernel, dim3(1), dim3(64), 0, stream, (const uint32_t*)a->bcount, a->vflags + 2);
-      if (hipMemcpyAsync(a->h_vflags, a->vflags, 12, hipMemcpyDeviceToHost, stream) != hipSuccess) return -5;
+      if (hipMemcpyAsync(a->h_vflags, a->vflags, 16, hipMemcpyDeviceToHost, stream) != hipSuccess) return -5;
       commit(a->vflags + 1);                           // runs while the host waits, if nothing was flagged
       if (hipStreamSynchronize(stream) != hipSuccess) return -5;
       if (a->decls_out) *a->decls_out = a->h_vflags[2];
       if (stream_debug())
-        fprintf(stderr, "stream: n %u round %u first (a)-flag %d any %u\n", n, r, (int)a->h_vflags[0],
-                a->h_vflags[1]);
+        fprintf(stderr, "stream: n %u round %u first (a)-flag %d any %u newly visible %u\n", n, r,
+                (int)a->h_vflags[0], a->h_vflags[1], a->h_vflags[3]);
       if (a->h_vflags[1] == 0) {                       // nothing flagged: fixed point (already committed)
         converged = true;
         committed = true;
@@ -1985,7 +2171,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       cur = nxt;
       prm.b = tabs[cur];
       prm.need = a->need;
-      launch();                                      // (flagged by the verification: from the start)
+      if (rs_rounds) run_restarted();                // (resumed before the first affected lookup)
+      else launch();                                 // (flagged by the verification: from the start)
       ++rounds;
     }
     if (!converged) return -75;
