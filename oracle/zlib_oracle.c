@@ -1,0 +1,577 @@
+/*
+ * zlib stage oracle -- TEST INFRASTRUCTURE ONLY (tests/, smoke() and bench.py's
+ * cpu_baseline may use it; nothing in wanproxy_amd/ links it).
+ *
+ * What it restates.  wanproxy chains a DeflatePipe after the XCodec encoder
+ * (programs/wanproxy/wanproxy_codec_pipe_pair.cc:97-106,148-157).  Its
+ * consume() (zlib/deflate_pipe.cc:57-115) feeds every input segment to
+ * deflate(Z_NO_FLUSH) and then calls deflate(Z_SYNC_FLUSH) -- or deflate(
+ * Z_FINISH) when the consumed buffer is empty (EOS).  The compressor itself is
+ * zlib, a third-party dependency that /root/reference does not vendor; this
+ * image (and the GPU box) carries zlib 1.2.11, the pinned version checked
+ * here.  This file restates zlib 1.2.11's deflate for windowBits 15, memLevel
+ * 8, Z_DEFAULT_STRATEGY, levels 4-9 (deflateInit(level), deflate_pipe.cc:45;
+ * levels 1-3 run deflate_fast, whose hash insertion depends on the parse, and
+ * level 0 deflate_stored -- neither is restated):
+ *   - deflate.c: configuration_table, deflate() header / flush / trailer,
+ *     fill_window() (window slide + high-water zeroing), longest_match(),
+ *     deflate_slow() (levels 4-9: lazy matching; wanproxy.conf sets 6)
+ *   - trees.c: _tr_tally, _tr_flush_block (stored / static / dynamic choice),
+ *     build_tree / gen_bitlen / gen_codes, scan_tree / send_tree,
+ *     build_bl_tree, send_all_trees, compress_block, _tr_stored_block.
+ * It is written in the formulation the GPU kernels use (wanproxy_amd/csrc/
+ * xcg_deflate.hip): a call's bytes are hashed at every position, every
+ * position's hash chain is walked up front ("match table": best length and
+ * first position reaching it, for the full and the quartered chain budget),
+ * and a sequential scan then replays deflate_slow's decisions
+ * over that table; only the last 257 positions of a call (whose
+ * longest_match reads past the data, into the stale window) are searched
+ * during the scan, against a literal 64 KiB zlib window.  Why the input's
+ * segmentation into deflate(Z_NO_FLUSH) calls cannot change the output: every
+ * position deflate processes under Z_NO_FLUSH has >= MIN_LOOKAHEAD bytes of
+ * lookahead and the window slides at the first loop top past strstart 65274
+ * whatever the segment sizes (checked against zlib with random segmentations
+ * in tests/test_zlib_oracle.py).
+ *
+ * Pinning: tests/test_zlib_oracle.py compares every call's output with the
+ * system zlib 1.2.11 driven in DeflatePipe's call pattern
+ * (oracle/zlib_pipe.py), and with fixtures it produced (tests/golden/zlib.json).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define WSIZE 32768u
+#define WINSZ 65536u
+#define MIN_MATCH 3
+#define MAX_MATCH 258
+#define MIN_LOOKAHEAD (MAX_MATCH + MIN_MATCH + 1)   /* deflate.h */
+#define MAX_DIST (WSIZE - MIN_LOOKAHEAD)             /* 32506 */
+#define TOO_FAR 4096
+#define LIT_BUFSIZE 16384u                           /* 1 << (memLevel + 6) */
+#define WIN_INIT MAX_MATCH
+#define NONE UINT64_MAX
+
+#define L_CODES 286
+#define D_CODES 30
+#define BL_CODES 19
+#define HEAP_SIZE (2 * L_CODES + 1)
+#define MAX_BITS 15
+#define END_BLOCK 256
+
+/* configuration_table (deflate.c): good, lazy, nice, chain */
+static const int CFG[10][4] = {
+    {0, 0, 0, 0},        {4, 4, 8, 4},         {4, 5, 16, 8},       {4, 6, 32, 32},
+    {4, 4, 16, 16},      {8, 16, 32, 32},      {8, 16, 128, 128},   {8, 32, 128, 256},
+    {32, 128, 258, 1024}, {32, 258, 258, 4096}};
+
+static const int XLB[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+static const int XDB[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+static const int XBB[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+static const uint8_t BL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+static uint8_t len_code[256], dist_code[512];
+static int base_len[29], base_dist[30];
+static uint16_t st_lcode[288], st_llen[288], st_dcode[30];
+static int tables_ready;
+
+static unsigned bitrev(unsigned c, int n) {
+    unsigned r = 0;
+    while (n-- > 0) { r = (r << 1) | (c & 1); c >>= 1; }
+    return r;
+}
+
+/* trees.c tr_static_init: length / distance code maps and the fixed trees */
+static void init_tables(void) {
+    if (tables_ready) return;
+    int l = 0, code;
+    for (code = 0; code < 28; code++) {
+        base_len[code] = l;
+        for (int n = 0; n < (1 << XLB[code]); n++) len_code[l++] = (uint8_t)code;
+    }
+    len_code[255] = 28;              /* length 258: code 285, no extra bits */
+    base_len[28] = 0;
+    int d = 0;
+    for (code = 0; code < 16; code++) {
+        base_dist[code] = d;
+        for (int n = 0; n < (1 << XDB[code]); n++) dist_code[d++] = (uint8_t)code;
+    }
+    d >>= 7;
+    for (; code < D_CODES; code++) {
+        base_dist[code] = d << 7;
+        for (int n = 0; n < (1 << (XDB[code] - 7)); n++) dist_code[256 + d++] = (uint8_t)code;
+    }
+    int cnt[MAX_BITS + 1] = {0};
+    for (int n = 0; n < 288; n++) {
+        st_llen[n] = n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8;
+        cnt[st_llen[n]]++;
+    }
+    unsigned next[MAX_BITS + 1], c = 0;
+    for (int b = 1; b <= MAX_BITS; b++) { c = (c + cnt[b - 1]) << 1; next[b] = c; }
+    for (int n = 0; n < 288; n++) st_lcode[n] = (uint16_t)bitrev(next[st_llen[n]]++, st_llen[n]);
+    for (int n = 0; n < D_CODES; n++) st_dcode[n] = (uint16_t)bitrev(n, 5);
+    tables_ready = 1;
+}
+
+static int d_code(unsigned dist) { return dist < 256 ? dist_code[dist] : dist_code[256 + (dist >> 7)]; }
+
+/* ------------------------------------------------------------------ bits */
+typedef struct { uint8_t *p; uint64_t n, cap; uint64_t acc; int nb; int err; } Bits;
+
+static void put_byte(Bits *b, uint8_t v) {
+    if (b->n < b->cap) b->p[b->n] = v; else b->err = 1;
+    b->n++;
+}
+static void put_bits(Bits *b, unsigned v, int n) {      /* LSB first, as send_bits */
+    b->acc |= (uint64_t)v << b->nb;
+    b->nb += n;
+    while (b->nb >= 8) { put_byte(b, (uint8_t)b->acc); b->acc >>= 8; b->nb -= 8; }
+}
+static void windup(Bits *b) {                           /* bi_windup */
+    if (b->nb > 0) put_byte(b, (uint8_t)b->acc);
+    b->acc = 0; b->nb = 0;
+}
+
+/* ------------------------------------------------------------------ trees */
+typedef struct { uint16_t fc; uint16_t dl; } ct;         /* Freq|Code, Dad|Len */
+
+typedef struct {
+    ct lt[HEAP_SIZE], dt[2 * D_CODES + 1], bt[2 * BL_CODES + 1];
+    int heap[2 * L_CODES + 1], heap_len, heap_max;
+    uint8_t depth[2 * L_CODES + 1];
+    int bl_count[MAX_BITS + 1];
+    uint64_t opt_len, static_len;
+    int lmax, dmax;
+} Trees;
+
+#define SMALLER(t, n, m, dep) ((t)[n].fc < (t)[m].fc || ((t)[n].fc == (t)[m].fc && (dep)[n] <= (dep)[m]))
+
+static void downheap(Trees *s, ct *t, int k) {
+    int v = s->heap[k], j = k << 1;
+    while (j <= s->heap_len) {
+        if (j < s->heap_len && SMALLER(t, s->heap[j + 1], s->heap[j], s->depth)) j++;
+        if (SMALLER(t, v, s->heap[j], s->depth)) break;
+        s->heap[k] = s->heap[j]; k = j; j <<= 1;
+    }
+    s->heap[k] = v;
+}
+
+/* build_tree + gen_bitlen + gen_codes (trees.c).  stl: static lengths or NULL. */
+static int build_tree(Trees *s, ct *t, int elems, const uint16_t *stl, const int *extra, int xbase, int maxlen) {
+    int n, m, max_code = -1, node;
+    s->heap_len = 0; s->heap_max = HEAP_SIZE;
+    for (n = 0; n < elems; n++) {
+        if (t[n].fc) { s->heap[++s->heap_len] = max_code = n; s->depth[n] = 0; }
+        else t[n].dl = 0;
+    }
+    while (s->heap_len < 2) {
+        node = s->heap[++s->heap_len] = (max_code < 2 ? ++max_code : 0);
+        t[node].fc = 1; s->depth[node] = 0;
+        s->opt_len--; if (stl) s->static_len -= stl[node];
+    }
+    for (n = s->heap_len / 2; n >= 1; n--) downheap(s, t, n);
+    node = elems;
+    do {
+        n = s->heap[1]; s->heap[1] = s->heap[s->heap_len--]; downheap(s, t, 1);
+        m = s->heap[1];
+        s->heap[--s->heap_max] = n; s->heap[--s->heap_max] = m;
+        t[node].fc = (uint16_t)(t[n].fc + t[m].fc);
+        s->depth[node] = (uint8_t)((s->depth[n] >= s->depth[m] ? s->depth[n] : s->depth[m]) + 1);
+        t[n].dl = t[m].dl = (uint16_t)node;
+        s->heap[1] = node++;
+        downheap(s, t, 1);
+    } while (s->heap_len >= 2);
+    s->heap[--s->heap_max] = s->heap[1];
+
+    /* gen_bitlen */
+    int h, bits, overflow = 0;
+    for (bits = 0; bits <= MAX_BITS; bits++) s->bl_count[bits] = 0;
+    t[s->heap[s->heap_max]].dl = 0;
+    for (h = s->heap_max + 1; h < HEAP_SIZE; h++) {
+        n = s->heap[h];
+        bits = t[t[n].dl].dl + 1;
+        if (bits > maxlen) { bits = maxlen; overflow++; }
+        t[n].dl = (uint16_t)bits;
+        if (n > max_code) continue;
+        s->bl_count[bits]++;
+        int xb = n >= xbase ? extra[n - xbase] : 0;
+        s->opt_len += (uint64_t)t[n].fc * (unsigned)(bits + xb);
+        if (stl) s->static_len += (uint64_t)t[n].fc * (unsigned)(stl[n] + xb);
+    }
+    if (overflow) {
+        do {
+            bits = maxlen - 1;
+            while (s->bl_count[bits] == 0) bits--;
+            s->bl_count[bits]--; s->bl_count[bits + 1] += 2; s->bl_count[maxlen]--;
+            overflow -= 2;
+        } while (overflow > 0);
+        for (bits = maxlen; bits != 0; bits--) {
+            n = s->bl_count[bits];
+            while (n != 0) {
+                m = s->heap[--h];
+                if (m > max_code) continue;
+                if (t[m].dl != (unsigned)bits) {
+                    s->opt_len += ((uint64_t)bits - t[m].dl) * t[m].fc;
+                    t[m].dl = (uint16_t)bits;
+                }
+                n--;
+            }
+        }
+    }
+    /* gen_codes */
+    unsigned next[MAX_BITS + 1], code = 0;
+    for (bits = 1; bits <= MAX_BITS; bits++) { code = (code + s->bl_count[bits - 1]) << 1; next[bits] = code; }
+    for (n = 0; n <= max_code; n++) {
+        int len = t[n].dl;
+        if (len) t[n].fc = (uint16_t)bitrev(next[len]++, len);
+    }
+    return max_code;
+}
+
+/* scan_tree (count) when b == NULL, send_tree (emit) otherwise */
+static void scan_send_tree(Trees *s, ct *t, int max_code, Bits *b) {
+    int prevlen = -1, curlen, nextlen = t[0].dl, count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    if (!b) t[max_code + 1].dl = 0xffff;                  /* guard */
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen; nextlen = t[n + 1].dl;
+        if (++count < max_count && curlen == nextlen) continue;
+        else if (count < min_count) {
+            if (!b) s->bt[curlen].fc += count;
+            else do { put_bits(b, s->bt[curlen].fc, s->bt[curlen].dl); } while (--count != 0);
+        } else if (curlen != 0) {
+            if (!b) { if (curlen != prevlen) s->bt[curlen].fc++; s->bt[16].fc++; }
+            else {
+                if (curlen != prevlen) { put_bits(b, s->bt[curlen].fc, s->bt[curlen].dl); count--; }
+                put_bits(b, s->bt[16].fc, s->bt[16].dl); put_bits(b, count - 3, 2);
+            }
+        } else if (count <= 10) {
+            if (!b) s->bt[17].fc++;
+            else { put_bits(b, s->bt[17].fc, s->bt[17].dl); put_bits(b, count - 3, 3); }
+        } else {
+            if (!b) s->bt[18].fc++;
+            else { put_bits(b, s->bt[18].fc, s->bt[18].dl); put_bits(b, count - 11, 7); }
+        }
+        count = 0; prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+/* one block's symbols: lit[i] = literal or length-3, dist[i] = 0 or distance */
+typedef struct { uint8_t lit[LIT_BUFSIZE]; uint16_t dist[LIT_BUFSIZE]; uint32_t n; } Syms;
+
+static void compress_block(Bits *b, const Syms *sy, const ct *lt, const ct *dt) {
+    for (uint32_t i = 0; i < sy->n; i++) {
+        unsigned lc = sy->lit[i], dist = sy->dist[i];
+        if (dist == 0) { put_bits(b, lt[lc].fc, lt[lc].dl); continue; }
+        int code = len_code[lc];
+        put_bits(b, lt[code + 257].fc, lt[code + 257].dl);
+        if (XLB[code]) put_bits(b, lc - base_len[code], XLB[code]);
+        dist--;
+        code = d_code(dist);
+        put_bits(b, dt[code].fc, dt[code].dl);
+        if (XDB[code]) put_bits(b, dist - base_dist[code], XDB[code]);
+    }
+    put_bits(b, lt[END_BLOCK].fc, lt[END_BLOCK].dl);
+}
+
+static void stored_block(Bits *b, const uint8_t *buf, uint32_t len, int last) {   /* _tr_stored_block */
+    put_bits(b, (0 << 1) + last, 3);
+    windup(b);
+    put_byte(b, len & 0xff); put_byte(b, (len >> 8) & 0xff);
+    put_byte(b, ~len & 0xff); put_byte(b, (~len >> 8) & 0xff);
+    for (uint32_t i = 0; i < len; i++) put_byte(b, buf[i]);
+}
+
+/* _tr_flush_block: buf == NULL when the block's bytes left the window */
+static void flush_block(Bits *b, const Syms *sy, const uint8_t *buf, uint64_t stored_len, int last) {
+    static ct slt[288], sdt[30];
+    Trees *s = calloc(1, sizeof(Trees));
+    for (uint32_t i = 0; i < sy->n; i++) {
+        if (sy->dist[i] == 0) s->lt[sy->lit[i]].fc++;
+        else { s->lt[len_code[sy->lit[i]] + 257].fc++; s->dt[d_code(sy->dist[i] - 1u)].fc++; }
+    }
+    s->lt[END_BLOCK].fc = 1;
+    s->lmax = build_tree(s, s->lt, L_CODES, st_llen, XLB, 257, MAX_BITS);
+    static uint16_t st_dlen[30];
+    for (int i = 0; i < 30; i++) st_dlen[i] = 5;
+    s->dmax = build_tree(s, s->dt, D_CODES, st_dlen, XDB, 0, MAX_BITS);
+    scan_send_tree(s, s->lt, s->lmax, NULL);
+    scan_send_tree(s, s->dt, s->dmax, NULL);
+    build_tree(s, s->bt, BL_CODES, NULL, XBB, 0, 7);
+    int max_blindex;
+    for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+        if (s->bt[BL_ORDER[max_blindex]].dl != 0) break;
+    s->opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
+    uint64_t opt_lenb = (s->opt_len + 3 + 7) >> 3, static_lenb = (s->static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    if (stored_len + 4 <= opt_lenb && buf) {
+        stored_block(b, buf, (uint32_t)stored_len, last);
+    } else if (static_lenb == opt_lenb) {
+        for (int i = 0; i < 288; i++) { slt[i].fc = st_lcode[i]; slt[i].dl = st_llen[i]; }
+        for (int i = 0; i < 30; i++) { sdt[i].fc = st_dcode[i]; sdt[i].dl = 5; }
+        put_bits(b, (1 << 1) + last, 3);
+        compress_block(b, sy, slt, sdt);
+    } else {
+        put_bits(b, (2 << 1) + last, 3);
+        int lcodes = s->lmax + 1, dcodes = s->dmax + 1, blcodes = max_blindex + 1;
+        put_bits(b, lcodes - 257, 5); put_bits(b, dcodes - 1, 5); put_bits(b, blcodes - 4, 4);
+        for (int r = 0; r < blcodes; r++) put_bits(b, s->bt[BL_ORDER[r]].dl, 3);
+        scan_send_tree(s, s->lt, lcodes - 1, b);
+        scan_send_tree(s, s->dt, dcodes - 1, b);
+        compress_block(b, sy, s->lt, s->dt);
+    }
+    if (last) windup(b);
+    free(s);
+}
+
+/* ------------------------------------------------------------------ stream */
+typedef struct zr_stream {
+    int level, good, lazy, nice, chain;
+    uint8_t win[WINSZ];           /* zlib's window, coords 0..65535 */
+    uint64_t base;                /* stream position of window coord 0 */
+    uint64_t total;               /* bytes consumed so far (= data end) */
+    uint32_t high_water;
+    int started, finished;
+    uint32_t adler;
+    uint64_t match_start;
+    uint64_t block_start;         /* stream position */
+    Syms sy;
+    /* per-call scratch */
+    uint64_t lo;                  /* stream position of x[0] */
+    uint8_t *x; uint32_t *prv;    /* bytes [lo, end) and their hash-chain links (index or UINT32_MAX) */
+    uint16_t *mfull, *mquar; uint32_t *sfull, *squar;
+} zr_stream;
+
+zr_stream *zr_create(int level) {
+    if (level < 4 || level > 9) return NULL;   /* deflate_slow levels (wanproxy.conf: 6) */
+    init_tables();
+    zr_stream *s = calloc(1, sizeof(zr_stream));
+    s->level = level;
+    s->good = CFG[level][0]; s->lazy = CFG[level][1]; s->nice = CFG[level][2]; s->chain = CFG[level][3];
+    s->adler = 1;
+    return s;
+}
+
+void zr_free(zr_stream *s) { free(s); }
+
+static uint32_t adler32(uint32_t a, const uint8_t *p, uint64_t n) {
+    uint32_t s1 = a & 0xffff, s2 = a >> 16;
+    for (uint64_t i = 0; i < n; i++) { s1 = (s1 + p[i]) % 65521; s2 = (s2 + s1) % 65521; }
+    return (s2 << 16) | s1;
+}
+
+static inline uint8_t X(const zr_stream *s, uint64_t pos) { return s->x[pos - s->lo]; }
+static inline uint32_t hash3(const zr_stream *s, uint64_t q) {   /* UPDATE_HASH x3, hash_shift 5, 15 bits */
+    return (((uint32_t)X(s, q) << 10) ^ ((uint32_t)X(s, q + 1) << 5) ^ X(s, q + 2)) & 0x7fff;
+}
+static inline uint64_t prevlink(const zr_stream *s, uint64_t q) {
+    uint32_t v = s->prv[q - s->lo];
+    return v == UINT32_MAX ? NONE : s->lo + v;
+}
+
+/* the data-only match length of longest_match's inner loop (bytes 0,1 then 3..) */
+static int lcp(const zr_stream *s, uint64_t p, uint64_t c) {
+    if (X(s, p) != X(s, c) || X(s, p + 1) != X(s, c + 1)) return 0;
+    int len = 3;
+    while (len < MAX_MATCH && X(s, p + len) == X(s, c + len)) len++;
+    return len;
+}
+
+/* match table entry for position p (lookahead >= MAX_MATCH): the walk from
+ * the chain head with `budget` candidates; M = best length (0: none >= 3),
+ * S = first candidate reaching it.  Independent of the threshold prev_length:
+ * longest_match keeps the first candidate of maximal length, and its nice
+ * break (first candidate with len >= nice) does not depend on it. */
+static void walk(const zr_stream *s, uint64_t p, int budget, int nice, uint16_t *M, uint32_t *S) {
+    uint64_t cur = prevlink(s, p), limit = p > MAX_DIST ? p - MAX_DIST : 0;
+    int best = 0; uint64_t bs = 0;
+    while (cur != NONE) {
+        int len = lcp(s, p, cur);
+        if (len > best) { best = len; bs = cur; if (len >= nice) break; }
+        cur = prevlink(s, cur);
+        if (cur == NONE || cur <= limit || --budget == 0) break;
+    }
+    *M = (uint16_t)best; *S = (uint32_t)(bs - s->lo);
+}
+
+/* longest_match against the literal window (a call's last positions) */
+static int longest_literal(zr_stream *s, uint64_t p, uint64_t head, int prev_length, uint32_t lookahead) {
+    unsigned chain = (unsigned)s->chain;
+    if (prev_length >= s->good) chain >>= 2;
+    int nice = s->nice; if ((uint32_t)nice > lookahead) nice = (int)lookahead;
+    int best = prev_length;
+    const uint8_t *scan = s->win + (p - s->base);
+    uint64_t limit = (p - s->base) > MAX_DIST ? p - MAX_DIST : s->base;
+    uint64_t cur = head;
+    do {
+        const uint8_t *m = s->win + (cur - s->base);
+        if (m[best] != scan[best] || m[best - 1] != scan[best - 1] || m[0] != scan[0] || m[1] != scan[1]) continue;
+        int len = 3;
+        while (len < MAX_MATCH && scan[len] == m[len]) len++;
+        if (len > best) { s->match_start = cur; best = len; if (len >= nice) break; }
+    } while ((cur = prevlink(s, cur)) != NONE && cur > limit && --chain != 0);
+    return (uint32_t)best <= lookahead ? best : (int)lookahead;
+}
+
+typedef struct { uint64_t rd, end; } Feed;   /* stream positions read into the window / available */
+
+/* fill_window: slide when strstart >= WSIZE + MAX_DIST, then read what fits */
+static void fill_window(zr_stream *s, uint64_t strstart, Feed *f) {
+    do {
+        uint32_t more = (uint32_t)(WINSZ - (f->rd - s->base));
+        if (strstart - s->base >= WSIZE + MAX_DIST) {
+            memcpy(s->win, s->win + WSIZE, WSIZE - more);
+            s->base += WSIZE;
+            more += WSIZE;
+        }
+        if (f->rd == f->end) break;
+        uint64_t n = f->end - f->rd; if (n > more) n = more;
+        memcpy(s->win + (f->rd - s->base), s->x + (f->rd - s->lo), n);
+        f->rd += n;
+    } while (f->rd - strstart < MIN_LOOKAHEAD && f->rd < f->end);
+    if (s->high_water < WINSZ) {
+        uint32_t curr = (uint32_t)(f->rd - s->base);
+        if (s->high_water < curr) {
+            uint32_t init = WINSZ - curr; if (init > WIN_INIT) init = WIN_INIT;
+            memset(s->win + curr, 0, init);
+            s->high_water = curr + init;
+        } else if (s->high_water < curr + WIN_INIT) {
+            uint32_t init = curr + WIN_INIT - s->high_water;
+            if (init > WINSZ - s->high_water) init = WINSZ - s->high_water;
+            memset(s->win + s->high_water, 0, init);
+            s->high_water += init;
+        }
+    }
+}
+
+static int tally(zr_stream *s, unsigned lc, unsigned dist) {
+    s->sy.lit[s->sy.n] = (uint8_t)lc; s->sy.dist[s->sy.n] = (uint16_t)dist; s->sy.n++;
+    return s->sy.n == LIT_BUFSIZE - 1;
+}
+
+static void flush(zr_stream *s, Bits *b, uint64_t strstart, int last) {   /* FLUSH_BLOCK_ONLY */
+    const uint8_t *buf = s->block_start >= s->base ? s->win + (s->block_start - s->base) : NULL;
+    flush_block(b, &s->sy, buf, strstart - s->block_start, last);
+    s->sy.n = 0;
+    s->block_start = strstart;
+}
+
+/* the eligible chain head at loop top p (hash_head != NIL && within MAX_DIST) */
+static uint64_t head_of(const zr_stream *s, uint64_t p, uint32_t lookahead) {
+    if (lookahead < MIN_MATCH) return NONE;
+    uint64_t h = prevlink(s, p);
+    if (h == NONE || h <= s->base || p - h > MAX_DIST) return NONE;   /* coord 0 is NIL */
+    return h;
+}
+
+/* One DeflatePipe::consume(): n > 0 bytes, then Z_SYNC_FLUSH; n == 0: Z_FINISH.
+ * Returns the bytes written to out (or -1 if cap was too small). */
+int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap) {
+    Bits b = {out, 0, cap, 0, 0, 0};
+    if (s->finished) return 0;
+    if (!s->started) {
+        unsigned lf = s->level < 2 ? 0 : s->level < 6 ? 1 : s->level == 6 ? 2 : 3;
+        unsigned header = ((8 + (7 << 4)) << 8) | (lf << 6);
+        header += 31 - (header % 31);
+        put_byte(&b, header >> 8); put_byte(&b, header & 0xff);
+        s->started = 1;
+    }
+    uint64_t p = s->total, end = s->total + n;
+    /* history the chains can reach + this call's bytes, by stream position */
+    uint64_t lo = s->total > WSIZE ? s->total - WSIZE : 0;
+    if (lo < s->base) lo = s->base;
+    s->lo = lo;
+    uint64_t span = end - lo;
+    s->x = malloc(span + MAX_MATCH + 8);
+    memcpy(s->x, s->win + (lo - s->base), s->total - lo);
+    memcpy(s->x + (s->total - lo), in, n);
+    memset(s->x + span, 0, MAX_MATCH + 8);
+    s->adler = adler32(s->adler, in, n);
+
+    /* phase A: hash chains (prev links) over [lo, end - 2) */
+    s->prv = malloc(sizeof(uint32_t) * (span + 1));
+    uint32_t *headt = malloc(sizeof(uint32_t) * 32768);
+    for (int i = 0; i < 32768; i++) headt[i] = UINT32_MAX;
+    for (uint64_t q = lo; q < end; q++) {
+        if (q + 2 < end) {
+            uint32_t h = hash3(s, q);
+            s->prv[q - lo] = headt[h];
+            headt[h] = (uint32_t)(q - lo);
+        } else s->prv[q - lo] = UINT32_MAX;
+    }
+    free(headt);
+    /* phase B: match table for every position with >= MAX_MATCH lookahead */
+    s->mfull = calloc(span, 2); s->mquar = calloc(span, 2);
+    s->sfull = calloc(span, 4); s->squar = calloc(span, 4);
+    for (uint64_t q = p; q + MAX_MATCH <= end; q++) {
+        uint64_t i = q - lo;
+        if (q + 2 >= end || prevlink(s, q) == NONE) continue;
+        walk(s, q, s->chain, s->nice, &s->mfull[i], &s->sfull[i]);
+        walk(s, q, s->chain >> 2, s->nice, &s->mquar[i], &s->squar[i]);
+    }
+
+    /* phase C: deflate_slow over the table */
+    Feed f = {s->total, end};
+    int flush_kind = n == 0 ? 2 : 1;              /* 1 = Z_SYNC_FLUSH, 2 = Z_FINISH */
+    {
+        int match_length = MIN_MATCH - 1, match_available = 0;
+        for (;;) {
+            if (f.rd - p < MIN_LOOKAHEAD) {
+                fill_window(s, p, &f);
+                if (f.rd - p == 0) break;
+            }
+            uint32_t lookahead = (uint32_t)(f.rd - p);
+            uint64_t head = head_of(s, p, lookahead);
+            int prev_length = match_length;
+            uint64_t prev_match = s->match_start;
+            match_length = MIN_MATCH - 1;
+            if (head != NONE && prev_length < s->lazy) {
+                if (p + MAX_MATCH <= end) {
+                    uint64_t i = p - lo;
+                    int quar = prev_length >= s->good;
+                    int M = quar ? s->mquar[i] : s->mfull[i];
+                    if (M > prev_length) {
+                        match_length = M;
+                        s->match_start = lo + (quar ? s->squar[i] : s->sfull[i]);
+                    } else match_length = prev_length;
+                } else {
+                    match_length = longest_literal(s, p, head, prev_length, lookahead);
+                }
+                if (match_length <= 5 && match_length == MIN_MATCH && p - s->match_start > TOO_FAR)
+                    match_length = MIN_MATCH - 1;
+            }
+            if (prev_length >= MIN_MATCH && match_length <= prev_length) {
+                int bf = tally(s, (unsigned)(prev_length - MIN_MATCH), (unsigned)(p - 1 - prev_match));
+                p += (uint64_t)prev_length - 1;
+                match_available = 0;
+                match_length = MIN_MATCH - 1;
+                if (bf) flush(s, &b, p, 0);
+            } else if (match_available) {
+                if (tally(s, X(s, p - 1), 0)) flush(s, &b, p, 0);
+                p++;
+            } else {
+                match_available = 1;
+                p++;
+            }
+        }
+        if (match_available) tally(s, X(s, p - 1), 0);
+    }
+    if (flush_kind == 2) {
+        flush(s, &b, p, 1);
+        put_byte(&b, s->adler >> 24); put_byte(&b, (s->adler >> 16) & 0xff);
+        put_byte(&b, (s->adler >> 8) & 0xff); put_byte(&b, s->adler & 0xff);
+        s->finished = 1;
+    } else {
+        if (s->sy.n) flush(s, &b, p, 0);
+        stored_block(&b, NULL, 0, 0);            /* Z_SYNC_FLUSH marker */
+    }
+    s->total = end;
+    free(s->x); free(s->prv); free(s->mfull); free(s->mquar); free(s->sfull); free(s->squar);
+    s->x = NULL;
+    return b.err ? -1 : (int64_t)b.n;
+}
+
+uint64_t zr_bound(uint64_t n) { return 2 * n + 1024; }
