@@ -14,7 +14,7 @@
  * levels 1-3 run deflate_fast, whose hash insertion depends on the parse, and
  * level 0 deflate_stored -- neither is restated):
  *   - deflate.c: configuration_table, deflate() header / flush / trailer,
- *     fill_window() (window slide + high-water zeroing), longest_match(),
+ *     fill_window() (window slides), longest_match(),
  *     deflate_slow() (levels 4-9: lazy matching; wanproxy.conf sets 6)
  *   - trees.c: _tr_tally, _tr_flush_block (stored / static / dynamic choice),
  *     build_tree / gen_bitlen / gen_codes, scan_tree / send_tree,
@@ -23,10 +23,11 @@
  * xcg_deflate.hip): a call's bytes are hashed at every position, every
  * position's hash chain is walked up front ("match table": best length and
  * first position reaching it, for the full and the quartered chain budget),
- * and a sequential scan then replays deflate_slow's decisions
- * over that table; only the last 257 positions of a call (whose
- * longest_match reads past the data, into the stale window) are searched
- * during the scan, against a literal 64 KiB zlib window.  Why the input's
+ * and a sequential scan then replays deflate_slow's decisions over that
+ * table.  zlib's 64 KiB window itself is never materialised: only its slides
+ * (which make coord 0 NIL and decide whether a block can still be stored) are
+ * tracked, and what longest_match reads past the data cannot change its
+ * result (walk()).  Per stream only the last 32 KiB of input persist.  Why the input's
  * segmentation into deflate(Z_NO_FLUSH) calls cannot change the output: every
  * position deflate processes under Z_NO_FLUSH has >= MIN_LOOKAHEAD bytes of
  * lookahead and the window slides at the first loop top past strstart 65274
@@ -49,7 +50,6 @@
 #define MAX_DIST (WSIZE - MIN_LOOKAHEAD)             /* 32506 */
 #define TOO_FAR 4096
 #define LIT_BUFSIZE 16384u                           /* 1 << (memLevel + 6) */
-#define WIN_INIT MAX_MATCH
 #define NONE UINT64_MAX
 
 #define L_CODES 286
@@ -330,10 +330,9 @@ static void flush_block(Bits *b, const Syms *sy, const uint8_t *buf, uint64_t st
 /* ------------------------------------------------------------------ stream */
 typedef struct zr_stream {
     int level, good, lazy, nice, chain;
-    uint8_t win[WINSZ];           /* zlib's window, coords 0..65535 */
-    uint64_t base;                /* stream position of window coord 0 */
-    uint64_t total;               /* bytes consumed so far (= data end) */
-    uint32_t high_water;
+    uint8_t hist[WSIZE];          /* hist[i] = byte at stream position total - WSIZE + i */
+    uint64_t base;                /* stream position of zlib's window coord 0 (moves by WSIZE per slide) */
+    uint64_t total;               /* bytes consumed so far */
     int started, finished;
     uint32_t adler;
     uint64_t match_start;
@@ -372,79 +371,54 @@ static inline uint64_t prevlink(const zr_stream *s, uint64_t q) {
     return v == UINT32_MAX ? NONE : s->lo + v;
 }
 
-/* the data-only match length of longest_match's inner loop (bytes 0,1 then 3..) */
-static int lcp(const zr_stream *s, uint64_t p, uint64_t c) {
+/* longest_match's inner compare over the data only: bytes 0, 1, then 3.. (2
+ * is equal by the hash), at most `cap` = min(MAX_MATCH, lookahead) bytes */
+static int lcp(const zr_stream *s, uint64_t p, uint64_t c, int cap) {
     if (X(s, p) != X(s, c) || X(s, p + 1) != X(s, c + 1)) return 0;
     int len = 3;
-    while (len < MAX_MATCH && X(s, p + len) == X(s, c + len)) len++;
+    while (len < cap && X(s, p + len) == X(s, c + len)) len++;
     return len;
 }
 
-/* match table entry for position p (lookahead >= MAX_MATCH): the walk from
- * the chain head with `budget` candidates; M = best length (0: none >= 3),
- * S = first candidate reaching it.  Independent of the threshold prev_length:
- * longest_match keeps the first candidate of maximal length, and its nice
- * break (first candidate with len >= nice) does not depend on it. */
-static void walk(const zr_stream *s, uint64_t p, int budget, int nice, uint16_t *M, uint32_t *S) {
+/* Match table entry for position p with lookahead la = end - p >= MIN_MATCH:
+ * longest_match's walk from the chain head with `budget` candidates, giving
+ * M = the best length (0: none reaches MIN_MATCH), S = the first candidate
+ * reaching it.  Independent of the threshold prev_length: longest_match keeps
+ * the first candidate of maximal length, and its nice break (the first
+ * candidate with len >= nice) does not depend on it.
+ * Bytes past the data: longest_match may compare into the stale window past
+ * the lookahead, but that never changes its result.  nice is clipped to the
+ * lookahead; if la <= nice, the first candidate matching all la data bytes is
+ * the break candidate (every earlier one mismatched inside the data), and if
+ * la > nice, len >= nice is decided inside the data.  So lengths are capped
+ * at la, and the scan clips the threshold to la as longest_match's return
+ * does. */
+static void walk(const zr_stream *s, uint64_t p, uint64_t end, int budget, int nice, uint16_t *M, uint32_t *S) {
+    int cap = end - p < MAX_MATCH ? (int)(end - p) : MAX_MATCH;
+    if (nice > cap) nice = cap;
     uint64_t cur = prevlink(s, p), limit = p > MAX_DIST ? p - MAX_DIST : 0;
     int best = 0; uint64_t bs = 0;
     while (cur != NONE) {
-        int len = lcp(s, p, cur);
+        int len = lcp(s, p, cur, cap);
         if (len > best) { best = len; bs = cur; if (len >= nice) break; }
         cur = prevlink(s, cur);
         if (cur == NONE || cur <= limit || --budget == 0) break;
     }
     *M = (uint16_t)best; *S = (uint32_t)(bs - s->lo);
 }
+typedef struct { uint64_t rd, end; } Feed;   /* stream positions read into zlib's window / available */
 
-/* longest_match against the literal window (a call's last positions) */
-static int longest_literal(zr_stream *s, uint64_t p, uint64_t head, int prev_length, uint32_t lookahead) {
-    unsigned chain = (unsigned)s->chain;
-    if (prev_length >= s->good) chain >>= 2;
-    int nice = s->nice; if ((uint32_t)nice > lookahead) nice = (int)lookahead;
-    int best = prev_length;
-    const uint8_t *scan = s->win + (p - s->base);
-    uint64_t limit = (p - s->base) > MAX_DIST ? p - MAX_DIST : s->base;
-    uint64_t cur = head;
-    do {
-        const uint8_t *m = s->win + (cur - s->base);
-        if (m[best] != scan[best] || m[best - 1] != scan[best - 1] || m[0] != scan[0] || m[1] != scan[1]) continue;
-        int len = 3;
-        while (len < MAX_MATCH && scan[len] == m[len]) len++;
-        if (len > best) { s->match_start = cur; best = len; if (len >= nice) break; }
-    } while ((cur = prevlink(s, cur)) != NONE && cur > limit && --chain != 0);
-    return (uint32_t)best <= lookahead ? best : (int)lookahead;
-}
-
-typedef struct { uint64_t rd, end; } Feed;   /* stream positions read into the window / available */
-
-/* fill_window: slide when strstart >= WSIZE + MAX_DIST, then read what fits */
+/* fill_window's effect on positions: slide (base += WSIZE) when strstart >=
+ * WSIZE + MAX_DIST, then read what fits.  The window's bytes themselves are
+ * not needed (see walk()). */
 static void fill_window(zr_stream *s, uint64_t strstart, Feed *f) {
     do {
-        uint32_t more = (uint32_t)(WINSZ - (f->rd - s->base));
-        if (strstart - s->base >= WSIZE + MAX_DIST) {
-            memcpy(s->win, s->win + WSIZE, WSIZE - more);
-            s->base += WSIZE;
-            more += WSIZE;
-        }
+        uint64_t more = WINSZ - (f->rd - s->base);
+        if (strstart - s->base >= WSIZE + MAX_DIST) { s->base += WSIZE; more += WSIZE; }
         if (f->rd == f->end) break;
         uint64_t n = f->end - f->rd; if (n > more) n = more;
-        memcpy(s->win + (f->rd - s->base), s->x + (f->rd - s->lo), n);
         f->rd += n;
     } while (f->rd - strstart < MIN_LOOKAHEAD && f->rd < f->end);
-    if (s->high_water < WINSZ) {
-        uint32_t curr = (uint32_t)(f->rd - s->base);
-        if (s->high_water < curr) {
-            uint32_t init = WINSZ - curr; if (init > WIN_INIT) init = WIN_INIT;
-            memset(s->win + curr, 0, init);
-            s->high_water = curr + init;
-        } else if (s->high_water < curr + WIN_INIT) {
-            uint32_t init = curr + WIN_INIT - s->high_water;
-            if (init > WINSZ - s->high_water) init = WINSZ - s->high_water;
-            memset(s->win + s->high_water, 0, init);
-            s->high_water += init;
-        }
-    }
 }
 
 static int tally(zr_stream *s, unsigned lc, unsigned dist) {
@@ -453,7 +427,8 @@ static int tally(zr_stream *s, unsigned lc, unsigned dist) {
 }
 
 static void flush(zr_stream *s, Bits *b, uint64_t strstart, int last) {   /* FLUSH_BLOCK_ONLY */
-    const uint8_t *buf = s->block_start >= s->base ? s->win + (s->block_start - s->base) : NULL;
+    /* the block's bytes are still in zlib's window unless a slide passed block_start */
+    const uint8_t *buf = s->block_start >= s->base ? s->x + (s->block_start - s->lo) : NULL;
     flush_block(b, &s->sy, buf, strstart - s->block_start, last);
     s->sy.n = 0;
     s->block_start = strstart;
@@ -486,7 +461,7 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
     s->lo = lo;
     uint64_t span = end - lo;
     s->x = malloc(span + MAX_MATCH + 8);
-    memcpy(s->x, s->win + (lo - s->base), s->total - lo);
+    memcpy(s->x, s->hist + (lo + WSIZE - s->total), s->total - lo);
     memcpy(s->x + (s->total - lo), in, n);
     memset(s->x + span, 0, MAX_MATCH + 8);
     s->adler = adler32(s->adler, in, n);
@@ -503,14 +478,14 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
         } else s->prv[q - lo] = UINT32_MAX;
     }
     free(headt);
-    /* phase B: match table for every position with >= MAX_MATCH lookahead */
+    /* phase B: match table for every position with >= MIN_MATCH lookahead */
     s->mfull = calloc(span, 2); s->mquar = calloc(span, 2);
     s->sfull = calloc(span, 4); s->squar = calloc(span, 4);
-    for (uint64_t q = p; q + MAX_MATCH <= end; q++) {
+    for (uint64_t q = p; q + 2 < end; q++) {
         uint64_t i = q - lo;
-        if (q + 2 >= end || prevlink(s, q) == NONE) continue;
-        walk(s, q, s->chain, s->nice, &s->mfull[i], &s->sfull[i]);
-        walk(s, q, s->chain >> 2, s->nice, &s->mquar[i], &s->squar[i]);
+        if (prevlink(s, q) == NONE) continue;
+        walk(s, q, end, s->chain, s->nice, &s->mfull[i], &s->sfull[i]);
+        walk(s, q, end, s->chain >> 2, s->nice, &s->mquar[i], &s->squar[i]);
     }
 
     /* phase C: deflate_slow over the table */
@@ -529,16 +504,14 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
             uint64_t prev_match = s->match_start;
             match_length = MIN_MATCH - 1;
             if (head != NONE && prev_length < s->lazy) {
-                if (p + MAX_MATCH <= end) {
-                    uint64_t i = p - lo;
-                    int quar = prev_length >= s->good;
-                    int M = quar ? s->mquar[i] : s->mfull[i];
-                    if (M > prev_length) {
-                        match_length = M;
-                        s->match_start = lo + (quar ? s->squar[i] : s->sfull[i]);
-                    } else match_length = prev_length;
+                uint64_t i = p - lo;
+                int quar = prev_length >= s->good;
+                int M = quar ? s->mquar[i] : s->mfull[i];
+                if (M > prev_length) {
+                    match_length = M;
+                    s->match_start = lo + (quar ? s->squar[i] : s->sfull[i]);
                 } else {
-                    match_length = longest_literal(s, p, head, prev_length, lookahead);
+                    match_length = (uint32_t)prev_length <= lookahead ? prev_length : (int)lookahead;
                 }
                 if (match_length <= 5 && match_length == MIN_MATCH && p - s->match_start > TOO_FAR)
                     match_length = MIN_MATCH - 1;
@@ -568,6 +541,9 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
         if (s->sy.n) flush(s, &b, p, 0);
         stored_block(&b, NULL, 0, 0);            /* Z_SYNC_FLUSH marker */
     }
+    /* keep the last WSIZE bytes: the next call's chains reach back MAX_DIST */
+    uint64_t keep = end - lo < WSIZE ? end - lo : WSIZE;
+    memcpy(s->hist + WSIZE - keep, s->x + (end - keep - lo), keep);
     s->total = end;
     free(s->x); free(s->prv); free(s->mfull); free(s->mquar); free(s->sfull); free(s->squar);
     s->x = NULL;
