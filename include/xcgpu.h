@@ -30,6 +30,10 @@
  *   xcg_segment_hashes
  *       XCodecHash::hash per 2048-byte segment          xcodec/xcodec_hash.h:166-174
  *       (tack -h, programs/tack/tack.cc:368-414)
+ *   xcg_zdeflate_*
+ *       DeflatePipe::DeflatePipe(int level) / consume(Buffer *)
+ *                                                      zlib/deflate_pipe.h:33-42,
+ *                                                      zlib/deflate_pipe.cc:36-115
  */
 #ifndef XCGPU_H
 #define XCGPU_H
@@ -283,6 +287,36 @@ int xcg_pipe_encoder_consume_many(xcg_pipe *const *pipes, const uint8_t *const *
 int xcg_pipe_decoder_consume(xcg_pipe *p, const uint8_t *data, uint64_t len, xcg_pipe_out *out);
 /* Frames whose REF segments the encoder still keeps for <ASK> (not yet <ADVANCE>d). */
 uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
+
+/* ------------------------------------------------------------------------
+ * zlib stage: wanproxy's DeflatePipe after the XCodec encoder
+ * (programs/wanproxy/wanproxy_codec_pipe_pair.cc:97-106,148-157; set
+ * codecN.compressor zlib / compressor_level N, wanproxy.conf:32-41).
+ * A context holds `nstreams` DeflatePipe(level) instances
+ * (zlib/deflate_pipe.cc:36-50: deflateInit(level), windowBits 15, memLevel 8)
+ * in HBM.  Output is bit-exact with zlib 1.2.11 for levels 4-9 (deflate_slow);
+ * levels 0-3 return XCG_ENOTSUP.
+ *   xcg_zdeflate_batch: one DeflatePipe::consume() per listed stream (a stream
+ *   at most once per batch; successive batches continue the streams):
+ *   h_len[i] > 0 bytes at d_in + h_in_off[i] = every segment through
+ *   deflate(Z_NO_FLUSH), then deflate(Z_SYNC_FLUSH) (deflate_pipe.cc:57-115);
+ *   h_len[i] == 0 = EOS: deflate(Z_FINISH) (zlib trailer; the stream is done).
+ *   The produced bytes go to d_out + h_out_off[i] (4-byte aligned, room for
+ *   xcg_zdeflate_bound(h_len[i])), their count to d_out_len[i].  Metadata
+ *   arrays are host memory; the call is asynchronous on `stream`.
+ *   xcg_zdeflate_reset: the slot becomes a fresh DeflatePipe.
+ */
+typedef struct xcg_zdeflate xcg_zdeflate;
+uint64_t xcg_zdeflate_bound(uint32_t len);
+int xcg_zdeflate_create(int device, int level, uint32_t nstreams, xcg_zdeflate **out);
+void xcg_zdeflate_destroy(xcg_zdeflate *z);
+int xcg_zdeflate_reset(xcg_zdeflate *z, uint32_t stream);
+int xcg_zdeflate_batch(xcg_zdeflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
+                       const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
+                       uint32_t *d_out_len, void *stream);
+int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
+                      const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
+                      uint32_t *h_out_len);
 
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,

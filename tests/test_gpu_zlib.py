@@ -1,0 +1,119 @@
+"""GPU parity of the zlib stage (DeflatePipe, zlib/deflate_pipe.cc:57-115):
+xcg_zdeflate_* against the system zlib 1.2.11 driven in DeflatePipe's call
+pattern (oracle/zlib_pipe.py) and against the committed fixtures.  Many
+streams per batch, successive batches continue them."""
+import hashlib
+import json
+import os
+import random
+import zlib
+
+import pytest
+
+from oracle.zlib_pipe import DeflatePipeRef
+from tests.zlib_cases import cases, gen_bytes, wan_stream
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_streams(streams_by_level):
+    """streams_by_level: {level: [[call bytes...], ...]} -> {level: [[outputs...]]},
+    every level's streams batched together, call k of every stream in batch k."""
+    from wanproxy_amd.zpipe import DeflatePipes
+    res = {}
+    for level, streams in streams_by_level.items():
+        ctx = DeflatePipes(level, len(streams))
+        outs = [[] for _ in streams]
+        for k in range(max(len(s) for s in streams)):
+            items = [(i, s[k]) for i, s in enumerate(streams) if k < len(s)]
+            got = ctx.consume_many(items)
+            for (i, _), g in zip(items, got):
+                outs[i].append(g)
+        ctx.close()
+        res[level] = outs
+    return res
+
+
+def check_vs_zlib(streams_by_level):
+    got = run_streams(streams_by_level)
+    for level, streams in streams_by_level.items():
+        for si, calls in enumerate(streams):
+            ref = DeflatePipeRef(level)
+            for k, c in enumerate(calls):
+                exp = ref.consume(c)
+                g = got[level][si][k]
+                if g != exp:
+                    i = next((i for i in range(min(len(g), len(exp))) if g[i] != exp[i]), min(len(g), len(exp)))
+                    raise AssertionError(f'level {level} stream {si} call {k} (len {len(c)}): '
+                                         f'got {len(g)} B, zlib {len(exp)} B, first difference at byte {i}')
+
+
+def test_golden_fixture_gpu():
+    with open(os.path.join(ROOT, 'tests/golden/zlib.json')) as f:
+        g = json.load(f)
+    by_level = {}
+    recs = {}
+    for (level, calls), rec in zip(cases(7, 24), g['streams']):
+        by_level.setdefault(level, []).append(calls)
+        recs.setdefault(level, []).append(rec)
+    got = run_streams(by_level)
+    for level in by_level:
+        for si, rec in enumerate(recs[level]):
+            for k, e in enumerate(rec['calls']):
+                out = got[level][si][k]
+                assert len(out) == e['out_len'] and hashlib.sha256(out).hexdigest() == e['out_sha256'], \
+                    (level, si, k)
+
+
+@pytest.mark.parametrize('seed', [21, 22])
+def test_random_streams_vs_zlib(seed):
+    by_level = {}
+    for level, calls in cases(seed, 14):
+        by_level.setdefault(level, []).append(calls)
+    check_vs_zlib(by_level)
+
+
+def test_tiny_calls_vs_zlib():
+    rng = random.Random(5)
+    streams = [[gen_bytes(rng, rng.randint(1, 6)) for _ in range(40)] + [b''] for _ in range(8)]
+    check_vs_zlib({6: streams, 9: streams[:3], 4: streams[3:5]})
+
+
+def test_many_streams_wan_traffic_round_trip():
+    """256 streams x 3 consumes of 64 KiB of XCodec-output-like bytes (level 6,
+    wanproxy.conf), each stream inflated back by zlib."""
+    streams = [wan_stream(1000 + i, 3, 65536) + [b''] for i in range(256)]
+    got = run_streams({6: streams})[6]
+    for i, calls in enumerate(streams[:64]):
+        ref = DeflatePipeRef(6)
+        for k, c in enumerate(calls):
+            assert got[i][k] == ref.consume(c), (i, k)
+    for i, calls in enumerate(streams):
+        assert zlib.decompress(b''.join(got[i])) == b''.join(calls)
+
+
+def test_long_matches_and_slides():
+    """Runs and far copies across several window slides in one call and
+    across calls (512 KiB calls, 258-byte matches, nice breaks)."""
+    rng = random.Random(77)
+    base = rng.randbytes(40000)
+    s1 = [base * 13, bytes(300000), base[::-1] * 3 + base] + [b'']
+    s2 = [gen_bytes(rng, 524288), gen_bytes(rng, 100000)] + [b'']
+    check_vs_zlib({6: [s1, s2], 9: [s1], 4: [s2]})
+
+
+def test_errors():
+    from wanproxy_amd.xcgpu import XCGError
+    from wanproxy_amd.zpipe import DeflatePipes
+    with pytest.raises(XCGError):
+        DeflatePipes(1, 1)
+    ctx = DeflatePipes(6, 2)
+    with pytest.raises(XCGError):
+        ctx.consume_many([(0, b'a'), (0, b'b')])
+    with pytest.raises(XCGError):
+        ctx.consume_many([(5, b'a')])
+    assert ctx.pipe(1).consume(b'') == DeflatePipeRef(6).consume(b'')
+    ctx.reset(1)
+    assert ctx.pipe(1).consume(b'hello') == DeflatePipeRef(6).consume(b'hello')
+    ctx.close()

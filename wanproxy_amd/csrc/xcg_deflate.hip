@@ -1,0 +1,1179 @@
+// wanproxy's zlib stage on the GPU: DeflatePipe (zlib/deflate_pipe.cc:57-115)
+// for many streams at once, bit-exact with zlib 1.2.11's deflate at levels 4-9
+// (deflate_slow; wanproxy.conf sets level 6).  gfx950, wave64.
+//
+// A DeflatePipe::consume() of n bytes is deflate(Z_NO_FLUSH) over its
+// segments then deflate(Z_SYNC_FLUSH); an empty consume is deflate(Z_FINISH).
+// The output does not depend on the segmentation (every position zlib
+// processes under Z_NO_FLUSH has >= MIN_LOOKAHEAD bytes of lookahead), so a
+// call is its bytes plus a flush.  Per call, in HBM:
+//
+//   X      the stream's last 32 KiB (history) ++ the call's bytes.  X index j
+//          is stream position total - 32768 + j.
+//   d16    hash-chain links: j - prev(j), prev(j) = the latest earlier position
+//          with the same 3-byte hash (zlib's head/prev, deflate.c INSERT_STRING:
+//          deflate_slow inserts every position once its 3 bytes exist, in
+//          order), 0 = none / farther than 32767.          zd_chain_kernel
+//   tf/tq  per position: longest_match's walk from the chain head with the full
+//          and the quartered (prev_length >= good_match) chain budget: best
+//          length and the distance of the first candidate reaching it.  The
+//          threshold prev_length cannot change which candidate wins (first of
+//          maximal length) nor where the nice-length break falls, so one walk
+//          serves every prev_length.  Bytes past the lookahead never change
+//          longest_match's result (nice is clipped to the lookahead), so lengths
+//          are capped there and zlib's 64 KiB window is never materialised.
+//                                                          zd_match_kernel
+//   sym    the lazy-matching scan (deflate_slow) over that table, one wave per
+//          call, sequential but cheap per position; runs of positions where no
+//          match can start are emitted 64 at a time.  Window slides are
+//          tracked (coord 0 is NIL; a block whose start slid out cannot be
+//          stored).  Blocks end every 16383 symbols (lit_bufsize - 1).
+//                                                          zd_scan_kernel
+//   trees  per block (one wave): symbol histogram, zlib's build_tree /
+//          gen_bitlen / gen_codes, bit-length tree, the stored / static /
+//          dynamic choice of _tr_flush_block.              zd_trees_kernel
+//   out    layout (block bit offsets, zeroed output), then every block's bits
+//          in parallel (atomicOr into the zeroed words).   zd_layout / zd_emit
+//
+// The reference interface replaced is DeflatePipe(level) / consume(Buffer*)
+// (zlib/deflate_pipe.h:33-42, deflate_pipe.cc:36-115).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/xcgpu.h"
+#include "xcg_device.h"
+
+namespace xcg {
+namespace zd {
+
+constexpr int WSIZE = 32768;
+constexpr int WINSZ = 65536;
+constexpr int MIN_MATCH = 3;
+constexpr int MAX_MATCH = 258;
+constexpr int MIN_LOOKAHEAD = MAX_MATCH + MIN_MATCH + 1;   // 262
+constexpr int MAX_DIST = WSIZE - MIN_LOOKAHEAD;            // 32506
+constexpr int TOO_FAR = 4096;
+constexpr uint32_t SYMS_PER_BLOCK = 16383;                 // lit_bufsize - 1
+constexpr int L_CODES = 286, D_CODES = 30, BL_CODES = 19, HEAP_SIZE = 2 * L_CODES + 1;
+constexpr int MAX_BITS = 15;
+constexpr int XPAD = 272;                                  // zeroed bytes after a call's data in X
+constexpr int TAB_WORDS = L_CODES + D_CODES + BL_CODES;    // per block: code | len << 16
+
+// configuration_table (deflate.c): good, lazy, nice, chain
+__constant__ int CFG[10][4] = {{0, 0, 0, 0},        {4, 4, 8, 4},     {4, 5, 16, 8},      {4, 6, 32, 32},
+                               {4, 4, 16, 16},      {8, 16, 32, 32},  {8, 16, 128, 128},  {8, 32, 128, 256},
+                               {32, 128, 258, 1024}, {32, 258, 258, 4096}};
+__constant__ uint8_t XLB[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint8_t XDB[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t XBB[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+__constant__ uint8_t BL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+__constant__ uint16_t BASE_LEN[29] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 0};
+__constant__ uint16_t BASE_DIST[30] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768,
+                                       1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384, 24576};
+
+// length - 3 (0..255) -> length code 0..28 (trees.c _length_code; 255 -> 28)
+__device__ __forceinline__ int len_code(uint32_t lc) {
+  if (lc >= 255) return 28;
+  if (lc < 8) return (int)lc;
+  int b = 31 - __clz(lc);                       // 3..7
+  return 4 * (b - 1) + (int)((lc >> (b - 2)) & 3);
+}
+// distance - 1 (0..32767) -> distance code 0..29 (trees.c d_code)
+__device__ __forceinline__ int dist_code(uint32_t d) {
+  if (d < 4) return (int)d;
+  int b = 31 - __clz(d);                        // 2..14
+  return 2 * b + (int)((d >> (b - 1)) & 1);
+}
+__device__ __forceinline__ uint32_t bitrev(uint32_t c, int n) { return __brev(c) >> (32 - n); }
+
+struct ZState {          // one DeflatePipe's z_stream, reduced to what the output depends on
+  uint64_t total;        // bytes consumed
+  uint64_t base;         // stream position of zlib's window coord 0 (slides by WSIZE)
+  uint32_t adler;        // adler32 of everything consumed (the Z_FINISH trailer)
+  uint32_t flags;        // 1: header written, 2: finished (Z_STREAM_END)
+};
+
+struct ZCall {           // host-built, one per consume()
+  uint64_t in_off, out_off;   // into d_in / d_out (out_off % 4 == 0)
+  uint64_t x_off;             // X (and d16 at 2 * x_off) in the scratch
+  uint64_t t_off;             // tf / tq / sym: call-relative position 0
+  uint32_t len, stream;
+  uint32_t blk_off, blk_cap;  // block records
+};
+
+struct ZBlock {
+  uint32_t sym_begin, sym_end;
+  uint32_t start;        // X index of block_start
+  uint32_t stored_len;
+  uint32_t flags;        // 1 storable (block_start not slid out), 2 last
+  uint32_t type;         // 0 stored, 1 static, 2 dynamic
+  uint32_t lcodes, dcodes, blcodes, pad;
+  uint64_t bits;         // Huffman blocks: 3 + trees + symbols + end-of-block
+  uint64_t bit_off;      // start of the block in the call's output
+};
+
+struct ZCallRes {
+  uint32_t nblocks;
+  uint32_t nsym;
+  uint64_t base_end;     // stream position of coord 0 after the call
+  uint32_t adler;        // adler32 after the call
+  uint32_t out_len;
+  uint64_t end_bit;      // bit offset after the last block
+};
+
+struct ZArgs {
+  const ZCall* calls;
+  ZState* st;
+  uint8_t* hist;         // nstreams x WSIZE
+  const uint8_t* in;
+  uint8_t* out;
+  uint8_t* X;
+  uint16_t* d16;
+  uint32_t* tf;
+  uint32_t* tq;
+  uint32_t* sym;
+  ZBlock* blk;
+  uint32_t* tabs;        // blk index * TAB_WORDS
+  ZCallRes* res;
+  uint32_t* out_len;     // caller's d_out_len
+  const uint32_t* tile_call;   // zd_match_kernel: call of each 256-position tile
+  const uint32_t* tile_pos;    // and its first call-relative position
+  int level;
+};
+
+// ------------------------------------------------------------------- prep
+// X = history ++ data ++ zero pad.  Grid: (tiles of 4 KiB, calls).
+__global__ __launch_bounds__(256) void zd_prep_kernel(ZArgs a) {
+  const ZCall c = a.calls[blockIdx.y];
+  uint64_t span = (uint64_t)WSIZE + c.len + XPAD;
+  uint8_t* X = a.X + c.x_off;
+  const uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
+  const uint8_t* d = a.in + c.in_off;
+  for (uint64_t j = (uint64_t)blockIdx.x * 4096 + threadIdx.x; j < span; j += (uint64_t)gridDim.x * 4096) {
+    for (int k = 0; k < 16; k++) {
+      uint64_t q = j + (uint64_t)k * 256;
+      if (q >= span) break;
+      uint8_t v = 0;
+      if (q < WSIZE) v = h[q];
+      else if (q < (uint64_t)WSIZE + c.len) v = d[q - WSIZE];
+      X[q] = v;
+    }
+  }
+}
+
+// adler32 of the call's bytes, combined with the stream's (one wave per call)
+__global__ __launch_bounds__(64) void zd_adler_kernel(ZArgs a) {
+  const ZCall c = a.calls[blockIdx.x];
+  const uint8_t* d = a.in + c.in_off;
+  const int lane = threadIdx.x;
+  uint64_t A = 0, B = 0;   // sum d_i, sum i * d_i (i < len <= 2^24: fits)
+  uint64_t chunk = (c.len + 63) / 64;
+  uint64_t s = (uint64_t)lane * chunk, e = std::min<uint64_t>(s + chunk, c.len);
+  for (uint64_t i = s; i < e; i++) {
+    uint32_t v = d[i];
+    A += v;
+    B += i * v;
+  }
+  A %= 65521u;
+  B %= 65521u;
+  for (int o = 32; o >= 1; o >>= 1) {
+    A += __shfl_xor(A, o);
+    B += __shfl_xor(B, o);
+  }
+  if (lane == 0) {
+    uint32_t old = a.st[c.stream].adler;
+    uint64_t s1 = old & 0xffff, s2 = old >> 16, n = c.len % 65521u;
+    A %= 65521u;
+    B %= 65521u;
+    uint64_t ns1 = (s1 + A) % 65521u;
+    uint64_t ns2 = (s2 + n * s1 + n * A + 65521u - B) % 65521u;
+    a.res[blockIdx.x].adler = (uint32_t)((ns2 << 16) | ns1);
+  }
+}
+
+// ------------------------------------------------------------------- chains
+__device__ __forceinline__ uint32_t hash3(const uint8_t* X, int64_t j) {
+  return (((uint32_t)X[j] << 10) ^ ((uint32_t)X[j + 1] << 5) ^ X[j + 2]) & 0x7fffu;
+}
+
+// One wave per call, positions in order in groups of 64: a lane's previous
+// occurrence is the nearest lower lane with its hash, else the LDS head table;
+// the last lane of each hash then becomes the head.
+__global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
+  __shared__ int32_t head[32768];
+  __shared__ uint32_t succ[2];
+  const ZCall c = a.calls[blockIdx.x];
+  const ZState s = a.st[c.stream];
+  const int lane = threadIdx.x;
+  const uint8_t* X = a.X + c.x_off;
+  uint16_t* d16 = a.d16 + c.x_off;
+  for (int i = lane; i < 32768; i += 64) head[i] = -1;
+  // first valid position: max(base, total - WSIZE) as an X index
+  int64_t jlo = (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
+  int64_t jend = (int64_t)WSIZE + c.len;     // positions q with q + 2 < jend get a hash
+  for (int64_t g = jlo; g < jend; g += 64) {
+    int64_t j = g + lane;
+    bool valid = j + 2 < jend;
+    uint32_t h = valid ? hash3(X, j) : 0x8000u + lane;   // invalid lanes never match
+    int pred = -1;
+#pragma unroll 8
+    for (int k = 63; k >= 1; k--) {
+      uint32_t o = __shfl(h, (lane - k) & 63);
+      if (lane >= k && o == h) pred = lane - k;
+    }
+    if (lane < 2) succ[lane] = 0;
+    __syncthreads();
+    if (pred >= 0) atomicOr(&succ[pred >> 5], 1u << (pred & 31));
+    __syncthreads();
+    bool last = !((succ[lane >> 5] >> (lane & 31)) & 1);
+    int32_t prev = -1;
+    if (valid) prev = pred >= 0 ? (int32_t)(g + pred) : head[h];
+    if (j < jend) {
+      int64_t dd = prev >= 0 ? j - prev : 0;
+      d16[j] = (dd > 0 && dd <= 32767) ? (uint16_t)dd : 0;
+    }
+    __syncthreads();
+    if (valid && last) head[h] = (int32_t)j;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------- match table
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *(const u32_u*)p; }
+
+// Entry: M (9 bits) | distance of the first candidate reaching M (15 bits) << 9
+// | ELIG << 31 (chain head exists, within MAX_DIST, lookahead >= 3).  The scan
+// also rejects a head at zlib's window coord 0 (NIL).
+__global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
+  const uint32_t ci = a.tile_call[blockIdx.x];
+  const ZCall c = a.calls[ci];
+  const uint32_t rel = a.tile_pos[blockIdx.x] + threadIdx.x;
+  if (rel >= c.len) return;
+  const ZState s = a.st[c.stream];
+  const uint8_t* X = a.X + c.x_off;
+  const uint16_t* d16 = a.d16 + c.x_off;
+  const int64_t j = (int64_t)WSIZE + rel;
+  const int64_t la = (int64_t)c.len - rel;
+  uint32_t ef = 0, eq = 0;
+  uint32_t d = la >= MIN_MATCH ? d16[j] : 0;
+  if (d != 0 && d <= (uint32_t)MAX_DIST) {
+    const int budget = CFG[a.level][3], qb = budget >> 2;
+    const int cap = la < MAX_MATCH ? (int)la : MAX_MATCH;
+    const int nice = CFG[a.level][2] < cap ? CFG[a.level][2] : cap;
+    // chain continues while cur > max(p - MAX_DIST, stream position 0)
+    int64_t limit = j - MAX_DIST;
+    int64_t zero = (int64_t)WSIZE - (int64_t)s.total;
+    if (zero > limit) limit = zero;
+    int64_t cur = j - d;
+    int best = 0, bq = -1;
+    int64_t bs = 0, bsq = 0;
+    const uint32_t x01 = X[j] | ((uint32_t)X[j + 1] << 8);
+    int count = 0;
+    for (;;) {
+      // longest_match: reject on bytes 0, 1 (and at best_len), then compare
+      if ((X[cur] | ((uint32_t)X[cur + 1] << 8)) == x01 && (best < 3 || X[cur + best] == X[j + best])) {
+        int len = 2;
+        while (len < cap) {
+          uint32_t w = ld32(X + cur + len) ^ ld32(X + j + len);
+          if (w) {
+            len += __builtin_ctz(w) >> 3;
+            break;
+          }
+          len += 4;
+        }
+        if (len > cap) len = cap;
+        if (len >= MIN_MATCH && len > best) {
+          best = len;
+          bs = cur;
+          if (len >= nice) break;
+        }
+      }
+      if (++count == qb) {
+        bq = best;
+        bsq = bs;
+      }
+      if (count >= budget) break;
+      uint32_t dd = d16[cur];
+      if (dd == 0) break;
+      cur -= dd;
+      if (cur <= limit) break;
+    }
+    if (bq < 0) {
+      bq = best;
+      bsq = bs;
+    }
+    ef = 0x80000000u | (uint32_t)best | (best ? (uint32_t)(j - bs) << 9 : 0);
+    eq = 0x80000000u | (uint32_t)bq | (bq ? (uint32_t)(j - bsq) << 9 : 0);
+  }
+  a.tf[c.t_off + rel] = ef;
+  a.tq[c.t_off + rel] = eq;
+}
+
+// ------------------------------------------------------------------- lazy scan
+struct ScanWin {
+  uint32_t tf, tq, x;   // lane l: entries of position w + l, X byte w - 1 + l
+  uint32_t d;
+};
+
+__device__ __forceinline__ void load_win(ScanWin& W, const ZArgs& a, const ZCall& c, int64_t w) {
+  const int lane = threadIdx.x;
+  int64_t rel = w - WSIZE + lane;
+  W.tf = 0;
+  W.tq = 0;
+  W.d = 0;
+  if (rel >= 0 && rel < (int64_t)c.len) {
+    W.tf = a.tf[c.t_off + rel];
+    W.tq = a.tq[c.t_off + rel];
+    W.d = a.d16[c.x_off + w + lane];
+  }
+  W.x = (rel - 1 < (int64_t)c.len) ? a.X[c.x_off + w - 1 + lane] : 0;
+}
+
+// deflate_slow (deflate.c) over the match table; one wave per call.
+__global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.x;
+  const ZCall c = a.calls[ci];
+  const ZState s = a.st[c.stream];
+  const int lane = threadIdx.x;
+  const int good = CFG[a.level][0], lazy = CFG[a.level][1];
+  uint32_t* sym = a.sym + c.t_off;
+  ZBlock* blk = a.blk + c.blk_off;
+  const bool finish = c.len == 0;
+  // positions are X indices; bidx = X index of zlib's window coord 0
+  int64_t bidx = (int64_t)s.base - (int64_t)s.total + WSIZE;
+  const int64_t end = (int64_t)WSIZE + c.len;
+  int64_t p = WSIZE, rd = WSIZE;
+  uint32_t nsym = 0, symbase = 0, nblk = 0;
+  int64_t block_start = p;
+  int ml = MIN_MATCH - 1, avail = 0;
+  int64_t ms = 0;
+  ScanWin W;
+  int64_t w = p;
+  load_win(W, a, c, w);
+
+  auto flush = [&](int64_t q, bool last) {
+    if (lane == 0) {
+      ZBlock b;
+      b.sym_begin = symbase;
+      b.sym_end = symbase + nsym;
+      b.start = (uint32_t)block_start;
+      b.stored_len = (uint32_t)(q - block_start);
+      b.flags = (block_start >= bidx ? 1u : 0u) | (last ? 2u : 0u);
+      b.type = 0;
+      b.lcodes = b.dcodes = b.blcodes = b.pad = 0;
+      b.bits = 0;
+      b.bit_off = 0;
+      blk[nblk] = b;
+    }
+    nblk++;
+    symbase += nsym;
+    nsym = 0;
+    block_start = q;
+  };
+  auto put = [&](uint32_t v) {
+    if (lane == 0) sym[symbase + nsym] = v;
+    nsym++;
+  };
+
+  for (;;) {
+    if (rd - p < MIN_LOOKAHEAD) {   // fill_window: slide, then read what fits
+      do {
+        int64_t more = WINSZ - (rd - bidx);
+        if (p - bidx >= WSIZE + MAX_DIST) {
+          bidx += WSIZE;
+          more += WSIZE;
+        }
+        if (rd == end) break;
+        int64_t nrd = end - rd;
+        if (nrd > more) nrd = more;
+        rd += nrd;
+      } while (rd - p < MIN_LOOKAHEAD && rd < end);
+      if (rd == p) break;
+    }
+    if (p >= w + 64 || p < w) {
+      w = p;
+      load_win(W, a, c, w);
+    }
+    const int li = (int)(p - w);
+    if (avail && ml == MIN_MATCH - 1) {
+      // literal run: positions where no match can start emit the previous byte
+      int64_t lim = w + 64;
+      if (rd - (MIN_LOOKAHEAD - 1) < lim) lim = rd - (MIN_LOOKAHEAD - 1);
+      int64_t room = SYMS_PER_BLOCK - nsym;
+      if (p + room < lim) lim = p + room;
+      if (lim > p) {
+        uint32_t M = W.tf & 511u, dist = (W.tf >> 9) & 0x7fffu;
+        int64_t pos = w + lane;
+        bool elig = (W.tf >> 31) && pos - (int64_t)W.d != bidx && M >= MIN_MATCH && !(M == MIN_MATCH && dist > TOO_FAR);
+        uint64_t m = ballot(elig && pos >= p && pos < lim);
+        int64_t stop = m ? w + (int64_t)__builtin_ctzll(m) : lim;
+        int64_t k = stop - p;
+        if (k > 0) {
+          if (lane >= li && lane < li + k) sym[symbase + nsym + (lane - li)] = W.x;
+          nsym += (uint32_t)k;
+          p = stop;
+          if (nsym == SYMS_PER_BLOCK) flush(p - 1, false);
+          continue;
+        }
+      }
+    }
+    // one loop top of deflate_slow at p
+    const uint32_t ef = readlane(W.tf, li), dd = readlane(W.d, li);
+    const int64_t la = rd - p;
+    int prev_length = ml;
+    int64_t prev_match = ms;
+    ml = MIN_MATCH - 1;
+    bool head_ok = la >= MIN_MATCH && (ef >> 31) && (p - (int64_t)dd != bidx);
+    if (head_ok && prev_length < lazy) {
+      uint32_t e = prev_length >= good ? readlane(W.tq, li) : ef;
+      int M = (int)(e & 511u);
+      if (M > prev_length) {
+        ml = M;
+        ms = p - (int64_t)((e >> 9) & 0x7fffu);
+      } else {
+        ml = (int64_t)prev_length <= la ? prev_length : (int)la;
+      }
+      if (ml == MIN_MATCH && p - ms > TOO_FAR) ml = MIN_MATCH - 1;
+    }
+    if (prev_length >= MIN_MATCH && ml <= prev_length) {
+      put((uint32_t)(prev_length - MIN_MATCH) | ((uint32_t)(p - 1 - prev_match) << 8));
+      p += prev_length - 1;
+      avail = 0;
+      ml = MIN_MATCH - 1;
+      if (nsym == SYMS_PER_BLOCK) flush(p, false);
+    } else if (avail) {
+      put(readlane(W.x, li));
+      if (nsym == SYMS_PER_BLOCK) flush(p, false);
+      p++;
+    } else {
+      avail = 1;
+      p++;
+    }
+  }
+  if (avail) put(a.X[c.x_off + p - 1]);
+  if (finish) flush(p, true);
+  else if (nsym) flush(p, false);
+  if (lane == 0) {
+    ZCallRes r = a.res[ci];
+    r.nblocks = nblk;
+    r.nsym = symbase;
+    r.base_end = (uint64_t)((int64_t)s.total - WSIZE + bidx);
+    a.res[ci] = r;
+  }
+}
+
+// ------------------------------------------------------------------- trees
+struct TreeLds {
+  uint16_t fc[HEAP_SIZE];    // Freq | Code
+  uint16_t dl[HEAP_SIZE];    // Dad | Len
+  uint16_t dfc[2 * D_CODES + 1], ddl[2 * D_CODES + 1];
+  uint16_t bfc[2 * BL_CODES + 1], bdl[2 * BL_CODES + 1];
+  uint32_t lfreq[L_CODES], dfreq[D_CODES], bfreq[BL_CODES];   // real counts (forced codes excluded)
+  int16_t heap[HEAP_SIZE];
+  uint8_t depth[HEAP_SIZE];
+  int bl_count[MAX_BITS + 1];
+  int heap_len, heap_max;
+  int64_t opt_len, static_len;
+};
+
+__device__ __forceinline__ bool smaller(const uint16_t* fc, const uint8_t* dep, int n, int m) {
+  return fc[n] < fc[m] || (fc[n] == fc[m] && dep[n] <= dep[m]);
+}
+__device__ void downheap(TreeLds& s, const uint16_t* fc, int k) {
+  int v = s.heap[k], j = k << 1;
+  while (j <= s.heap_len) {
+    if (j < s.heap_len && smaller(fc, s.depth, s.heap[j + 1], s.heap[j])) j++;
+    if (smaller(fc, s.depth, v, s.heap[j])) break;
+    s.heap[k] = s.heap[j];
+    k = j;
+    j <<= 1;
+  }
+  s.heap[k] = (int16_t)v;
+}
+__device__ __forceinline__ int static_llen(int n) { return n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8; }
+
+// trees.c build_tree + gen_bitlen + gen_codes.  kind: 0 literal/length, 1 distance, 2 bit length.
+__device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int kind) {
+  const int maxlen = kind == 2 ? 7 : MAX_BITS;
+  int n, m, max_code = -1, node;
+  s.heap_len = 0;
+  s.heap_max = HEAP_SIZE;
+  for (n = 0; n < elems; n++) {
+    if (fc[n]) {
+      s.heap[++s.heap_len] = (int16_t)(max_code = n);
+      s.depth[n] = 0;
+    } else {
+      dl[n] = 0;
+    }
+  }
+  while (s.heap_len < 2) {
+    node = max_code < 2 ? ++max_code : 0;
+    s.heap[++s.heap_len] = (int16_t)node;
+    fc[node] = 1;
+    s.depth[node] = 0;
+    s.opt_len--;
+    if (kind == 0) s.static_len -= static_llen(node);
+    else if (kind == 1) s.static_len -= 5;
+  }
+  for (n = s.heap_len / 2; n >= 1; n--) downheap(s, fc, n);
+  node = elems;
+  do {
+    n = s.heap[1];
+    s.heap[1] = s.heap[s.heap_len--];
+    downheap(s, fc, 1);
+    m = s.heap[1];
+    s.heap[--s.heap_max] = (int16_t)n;
+    s.heap[--s.heap_max] = (int16_t)m;
+    fc[node] = (uint16_t)(fc[n] + fc[m]);
+    s.depth[node] = (uint8_t)((s.depth[n] >= s.depth[m] ? s.depth[n] : s.depth[m]) + 1);
+    dl[n] = dl[m] = (uint16_t)node;
+    s.heap[1] = (int16_t)node++;
+    downheap(s, fc, 1);
+  } while (s.heap_len >= 2);
+  s.heap[--s.heap_max] = s.heap[1];
+
+  int h, bits, overflow = 0;
+  for (bits = 0; bits <= MAX_BITS; bits++) s.bl_count[bits] = 0;
+  dl[s.heap[s.heap_max]] = 0;
+  for (h = s.heap_max + 1; h < HEAP_SIZE; h++) {
+    n = s.heap[h];
+    bits = dl[dl[n]] + 1;
+    if (bits > maxlen) {
+      bits = maxlen;
+      overflow++;
+    }
+    dl[n] = (uint16_t)bits;
+    if (n > max_code) continue;
+    s.bl_count[bits]++;
+    int xb = 0;
+    if (kind == 0 && n >= 257) xb = XLB[n - 257];
+    else if (kind == 1) xb = XDB[n];
+    else if (kind == 2) xb = XBB[n];
+    s.opt_len += (int64_t)fc[n] * (bits + xb);
+    if (kind == 0) s.static_len += (int64_t)fc[n] * (static_llen(n) + xb);
+    else if (kind == 1) s.static_len += (int64_t)fc[n] * (5 + xb);
+  }
+  if (overflow) {
+    do {
+      bits = maxlen - 1;
+      while (s.bl_count[bits] == 0) bits--;
+      s.bl_count[bits]--;
+      s.bl_count[bits + 1] += 2;
+      s.bl_count[maxlen]--;
+      overflow -= 2;
+    } while (overflow > 0);
+    for (bits = maxlen; bits != 0; bits--) {
+      n = s.bl_count[bits];
+      while (n != 0) {
+        m = s.heap[--h];
+        if (m > max_code) continue;
+        if (dl[m] != (unsigned)bits) {
+          s.opt_len += ((int64_t)bits - dl[m]) * fc[m];
+          dl[m] = (uint16_t)bits;
+        }
+        n--;
+      }
+    }
+  }
+  uint32_t next[MAX_BITS + 1], code = 0;
+  for (bits = 1; bits <= MAX_BITS; bits++) {
+    code = (code + s.bl_count[bits - 1]) << 1;
+    next[bits] = code;
+  }
+  for (n = 0; n <= max_code; n++) {
+    int len = dl[n];
+    if (len) fc[n] = (uint16_t)bitrev(next[len]++, len);
+  }
+  return max_code;
+}
+
+// scan_tree: bit-length code frequencies of one tree's lengths (guard: 0xffff)
+__device__ void scan_tree(TreeLds& s, const uint16_t* dl, int max_code) {
+  int prevlen = -1, curlen, nextlen = dl[0], count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) {
+    max_count = 138;
+    min_count = 3;
+  }
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen;
+    nextlen = n + 1 <= max_code ? dl[n + 1] : 0xffff;
+    if (++count < max_count && curlen == nextlen) continue;
+    if (count < min_count) s.bfreq[curlen] += count;
+    else if (curlen != 0) {
+      if (curlen != prevlen) s.bfreq[curlen]++;
+      s.bfreq[16]++;
+    } else if (count <= 10) s.bfreq[17]++;
+    else s.bfreq[18]++;
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) {
+      max_count = 138;
+      min_count = 3;
+    } else if (curlen == nextlen) {
+      max_count = 6;
+      min_count = 3;
+    } else {
+      max_count = 7;
+      min_count = 4;
+    }
+  }
+}
+
+// One wave per block: histogram, trees, the _tr_flush_block decision and the
+// block's exact bit count; code tables to `tabs`.
+__global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a, const uint32_t* blk_call) {
+  __shared__ TreeLds s;
+  const uint32_t bi = blockIdx.x;
+  const uint32_t ci = blk_call[bi];
+  const ZCall c = a.calls[ci];
+  const uint32_t k = bi - c.blk_off;
+  if (k >= a.res[ci].nblocks) return;
+  ZBlock* B = a.blk + bi;
+  const int lane = threadIdx.x;
+  const uint32_t* sym = a.sym + c.t_off;
+  for (int i = lane; i < L_CODES; i += 64) s.lfreq[i] = 0;
+  if (lane < D_CODES) s.dfreq[lane] = 0;
+  if (lane < BL_CODES) s.bfreq[lane] = 0;
+  __syncthreads();
+  const uint32_t sb = B->sym_begin, se = B->sym_end;
+  for (uint32_t i = sb + lane; i < se; i += 64) {
+    uint32_t v = sym[i];
+    uint32_t dist = v >> 8;
+    if (dist == 0) atomicAdd(&s.lfreq[v & 255], 1u);
+    else {
+      atomicAdd(&s.lfreq[257 + len_code(v & 255)], 1u);
+      atomicAdd(&s.dfreq[dist_code(dist - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    s.lfreq[256] = 1;
+    for (int i = 0; i < L_CODES; i++) s.fc[i] = (uint16_t)s.lfreq[i];
+    for (int i = 0; i < D_CODES; i++) s.dfc[i] = (uint16_t)s.dfreq[i];
+    s.opt_len = s.static_len = 0;
+    int lmax = build_tree(s, s.fc, s.dl, L_CODES, 0);
+    int dmax = build_tree(s, s.dfc, s.ddl, D_CODES, 1);
+    scan_tree(s, s.dl, lmax);
+    scan_tree(s, s.ddl, dmax);
+    for (int i = 0; i < BL_CODES; i++) s.bfc[i] = (uint16_t)s.bfreq[i];
+    build_tree(s, s.bfc, s.bdl, BL_CODES, 2);
+    int max_blindex;
+    for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+      if (s.bdl[BL_ORDER[max_blindex]] != 0) break;
+    s.opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+    int64_t opt_lenb = (s.opt_len + 3 + 7) >> 3, static_lenb = (s.static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    uint32_t type;
+    if ((int64_t)B->stored_len + 4 <= opt_lenb && (B->flags & 1)) type = 0;
+    else if (static_lenb == opt_lenb) type = 1;
+    else type = 2;
+    // exact bits of a Huffman block (real symbol counts; forced codes emit nothing)
+    uint64_t bits = 3;
+    if (type == 1) {
+      for (int i = 0; i < L_CODES; i++)
+        bits += (uint64_t)s.lfreq[i] * (static_llen(i) + (i >= 257 ? XLB[i - 257] : 0));
+      for (int i = 0; i < D_CODES; i++) bits += (uint64_t)s.dfreq[i] * (5 + XDB[i]);
+    } else if (type == 2) {
+      bits += 14 + 3 * (uint64_t)(max_blindex + 1);
+      for (int i = 0; i < BL_CODES; i++) bits += (uint64_t)s.bfreq[i] * (s.bdl[i] + XBB[i]);
+      for (int i = 0; i < L_CODES; i++) bits += (uint64_t)s.lfreq[i] * (s.dl[i] + (i >= 257 ? XLB[i - 257] : 0));
+      for (int i = 0; i < D_CODES; i++) bits += (uint64_t)s.dfreq[i] * (s.ddl[i] + XDB[i]);
+    }
+    B->type = type;
+    B->bits = bits;
+    B->lcodes = lmax + 1;
+    B->dcodes = dmax + 1;
+    B->blcodes = max_blindex + 1;
+  }
+  __syncthreads();
+  uint32_t* tab = a.tabs + (uint64_t)bi * TAB_WORDS;
+  if (B->type == 2) {
+    for (int i = lane; i < L_CODES; i += 64) tab[i] = s.fc[i] | ((uint32_t)s.dl[i] << 16);
+    if (lane < D_CODES) tab[L_CODES + lane] = s.dfc[lane] | ((uint32_t)s.ddl[lane] << 16);
+    if (lane < BL_CODES) tab[L_CODES + D_CODES + lane] = s.bfc[lane] | ((uint32_t)s.bdl[lane] << 16);
+  }
+}
+
+// ------------------------------------------------------------------- layout
+// One wave per call: block bit offsets, the call's length, zeroed output.
+__global__ __launch_bounds__(64) void zd_layout_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.x;
+  const ZCall c = a.calls[ci];
+  const ZState s = a.st[c.stream];
+  const int lane = threadIdx.x;
+  __shared__ uint32_t total_bytes;
+  if (lane == 0) {
+    uint64_t off = (s.flags & 1) ? 0 : 16;   // zlib header on the first call
+    uint32_t nb = a.res[ci].nblocks;
+    bool last = false;
+    for (uint32_t k = 0; k < nb; k++) {
+      ZBlock* B = a.blk + c.blk_off + k;
+      B->bit_off = off;
+      if (B->type == 0) off = (((off + 3 + 7) >> 3) + 4 + B->stored_len) * 8;
+      else off += B->bits;
+      if (B->flags & 2) {
+        off = (off + 7) & ~7ull;   // bi_windup after the last block
+        last = true;
+      }
+    }
+    a.res[ci].end_bit = off;
+    uint64_t bytes;
+    if (last) bytes = off / 8 + 4;                      // adler32 trailer
+    else bytes = ((off + 3 + 7) >> 3) + 4;              // Z_SYNC_FLUSH: empty stored block
+    total_bytes = (uint32_t)bytes;
+    a.res[ci].out_len = (uint32_t)bytes;
+    a.out_len[ci] = (uint32_t)bytes;
+  }
+  __syncthreads();
+  uint32_t* o = (uint32_t*)(a.out + c.out_off);
+  uint32_t words = (total_bytes + 3) / 4;
+  for (uint32_t i = lane; i < words; i += 64) o[i] = 0;
+}
+
+// ------------------------------------------------------------------- emit
+// Output words of one call: writes past its computed length are dropped (they
+// cannot happen when the layout is right; the guard keeps a bug from touching
+// another call's output).
+struct OutW {
+  uint32_t* o;
+  uint64_t nwords;
+};
+__device__ __forceinline__ void or_word(OutW o, uint64_t wi, uint32_t v) {
+  if (v && wi < o.nwords) atomicOr(o.o + wi, v);
+}
+__device__ __forceinline__ void or_bits(OutW o, uint64_t pos, uint64_t v, int nb) {
+  // v < 2^nb, nb <= 48: spans at most three words
+  if (nb == 0) return;
+  uint64_t wi = pos >> 5;
+  int sh = (int)(pos & 31);
+  uint64_t lo = v << sh;                     // bits [sh, sh + nb) of a 96-bit window
+  or_word(o, wi, (uint32_t)lo);
+  or_word(o, wi + 1, (uint32_t)(lo >> 32));
+  if (sh) or_word(o, wi + 2, (uint32_t)(v >> (64 - sh)));
+}
+__device__ __forceinline__ void or_byte(OutW o, uint64_t byte, uint32_t v) {
+  or_word(o, byte >> 2, v << (8 * (byte & 3)));
+}
+
+struct BitW {           // lane-0 sequential writer (block header, tree description)
+  OutW o;
+  uint64_t pos;
+  __device__ void put(uint32_t v, int n) {
+    or_bits(o, pos, v, n);
+    pos += n;
+  }
+};
+
+__device__ void send_tree(BitW& bw, const uint32_t* tab, int max_code, const uint32_t* btab) {
+  int prevlen = -1, curlen, nextlen = tab[0] >> 16, count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) {
+    max_count = 138;
+    min_count = 3;
+  }
+  auto code = [&](int c) { bw.put(btab[c] & 0xffff, btab[c] >> 16); };
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen;
+    nextlen = n + 1 <= max_code ? (int)(tab[n + 1] >> 16) : 0xffff;
+    if (++count < max_count && curlen == nextlen) continue;
+    if (count < min_count) {
+      do code(curlen);
+      while (--count != 0);
+    } else if (curlen != 0) {
+      if (curlen != prevlen) {
+        code(curlen);
+        count--;
+      }
+      code(16);
+      bw.put(count - 3, 2);
+    } else if (count <= 10) {
+      code(17);
+      bw.put(count - 3, 3);
+    } else {
+      code(18);
+      bw.put(count - 11, 7);
+    }
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) {
+      max_count = 138;
+      min_count = 3;
+    } else if (curlen == nextlen) {
+      max_count = 6;
+      min_count = 3;
+    } else {
+      max_count = 7;
+      min_count = 4;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t static_lcode(int n) {   // fixed literal/length tree (code | len << 16)
+  uint32_t len, code;
+  if (n < 144) { len = 8; code = 0x30 + n; }
+  else if (n < 256) { len = 9; code = 0x190 + (n - 144); }
+  else if (n < 280) { len = 7; code = n - 256; }
+  else { len = 8; code = 0xc0 + (n - 280); }
+  return bitrev(code, len) | (len << 16);
+}
+
+__global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a, const uint32_t* blk_call) {
+  __shared__ uint32_t ltab[L_CODES], dtab[D_CODES];
+  const uint32_t bi = blockIdx.x;
+  const uint32_t ci = blk_call[bi];
+  const ZCall c = a.calls[ci];
+  const uint32_t k = bi - c.blk_off;
+  const ZCallRes r = a.res[ci];
+  if (k >= r.nblocks) return;
+  const ZBlock B = a.blk[bi];
+  const ZState s = a.st[c.stream];
+  const int lane = threadIdx.x;
+  const OutW o{(uint32_t*)(a.out + c.out_off), (r.out_len + 3ull) / 4};
+  const OutW ob = o;
+  const bool last = B.flags & 2;
+  if (k == 0 && lane == 0 && !(s.flags & 1)) {   // zlib header (deflate.c: 0x78, level flags)
+    int lf = a.level < 2 ? 0 : a.level < 6 ? 1 : a.level == 6 ? 2 : 3;
+    uint32_t hdr = ((8 + (7 << 4)) << 8) | (lf << 6);
+    hdr += 31 - (hdr % 31);
+    or_byte(ob, 0, hdr >> 8);
+    or_byte(ob, 1, hdr & 0xff);
+  }
+  if (B.type == 0) {   // _tr_stored_block
+    if (lane == 0) {
+      or_bits(o, B.bit_off, last ? 1 : 0, 3);
+      uint64_t db = (B.bit_off + 3 + 7) >> 3;
+      uint32_t L = B.stored_len;
+      or_byte(ob, db, L & 0xff);
+      or_byte(ob, db + 1, (L >> 8) & 0xff);
+      or_byte(ob, db + 2, ~L & 0xff);
+      or_byte(ob, db + 3, (~L >> 8) & 0xff);
+    }
+    const uint8_t* X = a.X + c.x_off + B.start;
+    uint64_t db = ((B.bit_off + 3 + 7) >> 3) + 4;
+    // whole words inside [db, db + L) by plain stores, the edge words by atomicOr
+    uint64_t w0 = (db + 3) >> 2, w1 = (db + B.stored_len) >> 2;
+    for (uint64_t wi = w0 + lane; wi < w1 && wi < o.nwords; wi += 64) {
+      uint64_t b = wi * 4 - db;
+      o.o[wi] = X[b] | ((uint32_t)X[b + 1] << 8) | ((uint32_t)X[b + 2] << 16) | ((uint32_t)X[b + 3] << 24);
+    }
+    for (uint64_t i = lane; i < B.stored_len; i += 64) {
+      uint64_t byte = db + i;
+      if ((byte >> 2) < w0 || (byte >> 2) >= w1) or_byte(ob, byte, X[i]);
+    }
+  } else {
+    const uint32_t* tab = a.tabs + (uint64_t)bi * TAB_WORDS;
+    for (int i = lane; i < L_CODES; i += 64) ltab[i] = B.type == 2 ? tab[i] : static_lcode(i);
+    if (lane < D_CODES) dtab[lane] = B.type == 2 ? tab[L_CODES + lane] : (bitrev(lane, 5) | (5u << 16));
+    __syncthreads();
+    uint64_t pos = B.bit_off;
+    if (lane == 0) {
+      BitW bw{o, pos};
+      bw.put((B.type << 1) | (last ? 1 : 0), 3);
+      if (B.type == 2) {
+        const uint32_t* btab = tab + L_CODES + D_CODES;
+        bw.put(B.lcodes - 257, 5);
+        bw.put(B.dcodes - 1, 5);
+        bw.put(B.blcodes - 4, 4);
+        for (uint32_t rk = 0; rk < B.blcodes; rk++) bw.put(btab[BL_ORDER[rk]] >> 16, 3);
+        send_tree(bw, tab, B.lcodes - 1, btab);
+        send_tree(bw, tab + L_CODES, B.dcodes - 1, btab);
+      }
+      pos = bw.pos;
+    }
+    pos = readlane64(pos, 0);
+    const uint32_t* sym = a.sym + c.t_off;
+    for (uint32_t i0 = B.sym_begin; i0 < B.sym_end; i0 += 64) {
+      uint32_t i = i0 + lane;
+      uint64_t v = 0;
+      int nb = 0;
+      if (i < B.sym_end) {
+        uint32_t e = sym[i], dist = e >> 8;
+        if (dist == 0) {
+          uint32_t t = ltab[e & 255];
+          v = t & 0xffff;
+          nb = t >> 16;
+        } else {
+          uint32_t lc = e & 255;
+          int code = len_code(lc);
+          uint32_t t = ltab[257 + code];
+          v = t & 0xffff;
+          nb = t >> 16;
+          int xl = XLB[code];   // code 28 (length 258) has no extra bits
+          if (xl) v |= (uint64_t)(lc - BASE_LEN[code]) << nb;
+          nb += xl;
+          uint32_t d = dist - 1;
+          int dc = dist_code(d);
+          uint32_t td = dtab[dc];
+          v |= (uint64_t)(td & 0xffff) << nb;
+          nb += td >> 16;
+          v |= (uint64_t)(d - BASE_DIST[dc]) << nb;
+          nb += XDB[dc];
+        }
+      }
+      uint32_t incl = wave_incl_scan((uint32_t)nb);
+      or_bits(o, pos + incl - nb, v, nb);
+      pos += readlane(incl, 63);
+    }
+    if (lane == 0) {
+      uint32_t t = ltab[256];
+      or_bits(o, pos, t & 0xffff, t >> 16);
+    }
+  }
+  if (k == r.nblocks - 1 && lane == 0) {
+    if (last) {   // Z_FINISH: adler32 trailer, big-endian (putShortMSB x2)
+      uint64_t b = r.end_bit >> 3;
+      uint32_t ad = s.adler;
+      or_byte(ob, b, ad >> 24);
+      or_byte(ob, b + 1, (ad >> 16) & 0xff);
+      or_byte(ob, b + 2, (ad >> 8) & 0xff);
+      or_byte(ob, b + 3, ad & 0xff);
+    } else {      // Z_SYNC_FLUSH: empty stored block, 000 + align + 00 00 FF FF
+      uint64_t b = (r.end_bit + 3 + 7) >> 3;
+      or_byte(ob, b + 2, 0xff);
+      or_byte(ob, b + 3, 0xff);
+    }
+  }
+}
+
+// ------------------------------------------------------------------- commit
+// Stream state after the call: history = the last 32 KiB of X, position,
+// window base, adler, flags.  Grid: (8 tiles, calls).
+__global__ __launch_bounds__(256) void zd_commit_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.y;
+  const ZCall c = a.calls[ci];
+  const uint8_t* X = a.X + c.x_off + c.len;   // X[len .. len + WSIZE) = the last WSIZE positions
+  uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < (uint32_t)WSIZE / 4; i += gridDim.x * 256) {
+    const uint8_t* q = X + 4 * i;
+    *(uint32_t*)(h + 4 * i) = q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ZState s = a.st[c.stream];
+    s.total += c.len;
+    s.base = a.res[ci].base_end;
+    s.adler = c.len ? a.res[ci].adler : s.adler;
+    s.flags |= 1u;
+    if (c.len == 0) s.flags |= 2u;
+    a.st[c.stream] = s;
+  }
+}
+
+}  // namespace zd
+}  // namespace xcg
+
+using namespace xcg::zd;
+
+struct xcg_zdeflate {
+  int device = 0, level = 6;
+  uint32_t nstreams = 0;
+  ZState* st = nullptr;
+  uint8_t* hist = nullptr;
+  std::vector<ZState> h_init;
+  // scratch (grow-only)
+  uint8_t* scratch = nullptr;
+  size_t scratch_cap = 0;
+  void* meta = nullptr;       // ZCall[] + tile maps + block maps (device)
+  size_t meta_cap = 0;
+  void* h_meta = nullptr;     // pinned staging for meta
+  size_t h_meta_cap = 0;
+  hipEvent_t done = nullptr;
+};
+
+namespace {
+int grow(void** p, size_t* cap, size_t want, bool pinned) {
+  if (*cap >= want) return XCG_OK;
+  size_t n = std::max(want, *cap * 3 / 2);
+  if (*p) {
+    if (pinned) (void)hipHostFree(*p);
+    else (void)hipFree(*p);
+    *p = nullptr;
+  }
+  hipError_t e = pinned ? hipHostMalloc(p, n) : hipMalloc(p, n);
+  if (e != hipSuccess) {
+    *cap = 0;
+    *p = nullptr;
+    return XCG_ENOMEM;
+  }
+  *cap = n;
+  return XCG_OK;
+}
+inline size_t al(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+extern "C" {
+
+uint64_t xcg_zdeflate_bound(uint32_t len) { return (uint64_t)len + (len >> 1) + 128; }
+
+int xcg_zdeflate_create(int device, int level, uint32_t nstreams, xcg_zdeflate** out) {
+  if (!out || level < 4 || level > 9 || nstreams == 0) return level >= 0 && level < 4 ? XCG_ENOTSUP : XCG_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return XCG_EHIP;
+  xcg_zdeflate* z = new xcg_zdeflate();
+  z->device = device;
+  z->level = level;
+  z->nstreams = nstreams;
+  if (hipMalloc(&z->st, sizeof(ZState) * nstreams) != hipSuccess ||
+      hipMalloc(&z->hist, (size_t)WSIZE * nstreams) != hipSuccess || hipEventCreateWithFlags(&z->done, hipEventDisableTiming) != hipSuccess) {
+    delete z;
+    return XCG_ENOMEM;
+  }
+  z->h_init.assign(nstreams, ZState{0, 0, 1u, 0u});
+  if (hipMemcpy(z->st, z->h_init.data(), sizeof(ZState) * nstreams, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(z->hist, 0, (size_t)WSIZE * nstreams) != hipSuccess) {
+    delete z;
+    return XCG_EHIP;
+  }
+  *out = z;
+  return XCG_OK;
+}
+
+void xcg_zdeflate_destroy(xcg_zdeflate* z) {
+  if (!z) return;
+  (void)hipSetDevice(z->device);
+  if (z->done) (void)hipEventSynchronize(z->done);
+  (void)hipFree(z->st);
+  (void)hipFree(z->hist);
+  (void)hipFree(z->scratch);
+  (void)hipFree(z->meta);
+  if (z->h_meta) (void)hipHostFree(z->h_meta);
+  if (z->done) (void)hipEventDestroy(z->done);
+  delete z;
+}
+
+int xcg_zdeflate_reset(xcg_zdeflate* z, uint32_t stream) {
+  if (!z || stream >= z->nstreams) return XCG_EINVAL;
+  (void)hipSetDevice(z->device);
+  if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
+  ZState s0{0, 0, 1u, 0u};
+  if (hipMemcpy(z->st + stream, &s0, sizeof s0, hipMemcpyHostToDevice) != hipSuccess) return XCG_EHIP;
+  return XCG_OK;
+}
+
+int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                       const uint32_t* h_stream, uint32_t n, uint8_t* d_out, const uint64_t* h_out_off,
+                       uint32_t* d_out_len, void* stream) {
+  if (!z || n == 0 || !h_in_off || !h_len || !h_stream || !h_out_off || !d_out || !d_out_len) return XCG_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipSetDevice(z->device);
+  // host plan: scratch offsets, tiles, block maps
+  std::vector<ZCall> calls(n);
+  std::vector<uint32_t> tile_call, tile_pos, blk_call;
+  std::vector<uint8_t> seen(z->nstreams, 0);
+  size_t xo = 0, to = 0;
+  uint32_t bo = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (h_stream[i] >= z->nstreams || seen[h_stream[i]] || (h_out_off[i] & 3) || h_len[i] > (1u << 24))
+      return XCG_EINVAL;
+    seen[h_stream[i]] = 1;
+    ZCall& c = calls[i];
+    c.in_off = h_in_off[i];
+    c.out_off = h_out_off[i];
+    c.len = h_len[i];
+    c.stream = h_stream[i];
+    c.x_off = xo;
+    xo += al((size_t)WSIZE + c.len + XPAD, 256);
+    c.t_off = to;
+    to += al((size_t)c.len + 1, 64);
+    c.blk_off = bo;
+    c.blk_cap = c.len / SYMS_PER_BLOCK + 2;
+    bo += c.blk_cap;
+    for (uint32_t k = 0; k < c.blk_cap; k++) blk_call.push_back(i);
+    for (uint32_t p = 0; p < c.len; p += 256) {
+      tile_call.push_back(i);
+      tile_pos.push_back(p);
+    }
+  }
+  // scratch layout
+  size_t o_X = 0, o_d16 = al(o_X + xo, 256), o_tf = al(o_d16 + 2 * xo, 256), o_tq = al(o_tf + 4 * to, 256),
+         o_sym = al(o_tq + 4 * to, 256), o_blk = al(o_sym + 4 * to, 256),
+         o_tab = al(o_blk + sizeof(ZBlock) * bo, 256), o_res = al(o_tab + 4ull * TAB_WORDS * bo, 256),
+         o_end = al(o_res + sizeof(ZCallRes) * n, 256);
+  // the previous batch may still read the scratch
+  if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
+  if (grow((void**)&z->scratch, &z->scratch_cap, o_end, false)) return XCG_ENOMEM;
+  size_t m_calls = 0, m_tc = al(sizeof(ZCall) * n, 256), m_tp = al(m_tc + 4 * tile_call.size(), 256),
+         m_bc = al(m_tp + 4 * tile_pos.size(), 256), m_end = al(m_bc + 4 * blk_call.size(), 256);
+  if (grow(&z->meta, &z->meta_cap, m_end, false) || grow(&z->h_meta, &z->h_meta_cap, m_end, true)) return XCG_ENOMEM;
+  uint8_t* hm = (uint8_t*)z->h_meta;
+  memcpy(hm + m_calls, calls.data(), sizeof(ZCall) * n);
+  if (!tile_call.empty()) {
+    memcpy(hm + m_tc, tile_call.data(), 4 * tile_call.size());
+    memcpy(hm + m_tp, tile_pos.data(), 4 * tile_pos.size());
+  }
+  memcpy(hm + m_bc, blk_call.data(), 4 * blk_call.size());
+  if (hipMemcpyAsync(z->meta, hm, m_end, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
+  uint8_t* dm = (uint8_t*)z->meta;
+  ZArgs a;
+  a.calls = (const ZCall*)(dm + m_calls);
+  a.st = z->st;
+  a.hist = z->hist;
+  a.in = d_in;
+  a.out = d_out;
+  a.X = z->scratch + o_X;
+  a.d16 = (uint16_t*)(z->scratch + o_d16);
+  a.tf = (uint32_t*)(z->scratch + o_tf);
+  a.tq = (uint32_t*)(z->scratch + o_tq);
+  a.sym = (uint32_t*)(z->scratch + o_sym);
+  a.blk = (ZBlock*)(z->scratch + o_blk);
+  a.tabs = (uint32_t*)(z->scratch + o_tab);
+  a.res = (ZCallRes*)(z->scratch + o_res);
+  a.out_len = d_out_len;
+  a.tile_call = (const uint32_t*)(dm + m_tc);
+  a.tile_pos = (const uint32_t*)(dm + m_tp);
+  a.level = z->level;
+  const uint32_t* d_blk_call = (const uint32_t*)(dm + m_bc);
+  uint32_t maxlen = 0;
+  for (uint32_t i = 0; i < n; i++) maxlen = std::max(maxlen, h_len[i]);
+  uint32_t prep_tiles = std::min<uint32_t>(64, ((uint32_t)WSIZE + maxlen + XPAD + 4095) / 4096);
+  hipLaunchKernelGGL(zd_prep_kernel, dim3(prep_tiles, n), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
+  if (!tile_call.empty()) hipLaunchKernelGGL(zd_match_kernel, dim3((uint32_t)tile_call.size()), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(zd_scan_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_trees_kernel, dim3(bo), dim3(64), 0, st, a, d_blk_call);
+  hipLaunchKernelGGL(zd_layout_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a, d_blk_call);
+  hipLaunchKernelGGL(zd_commit_kernel, dim3(8, n), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) return XCG_EHIP;
+  if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
+  return XCG_OK;
+}
+
+// Host buffers: one consume() per listed stream, inputs concatenated in h_in
+// at h_in_off, outputs to h_out at h_out_off (room for xcg_zdeflate_bound);
+// lengths to h_out_len.  Synchronous.
+int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                      const uint32_t* h_stream, uint32_t n, uint8_t* h_out, const uint64_t* h_out_off,
+                      uint32_t* h_out_len) {
+  if (!z || n == 0) return XCG_EINVAL;
+  (void)hipSetDevice(z->device);
+  uint64_t in_end = 0, out_end = 0;
+  std::vector<uint64_t> doff(n);
+  for (uint32_t i = 0; i < n; i++) {
+    in_end = std::max(in_end, h_in_off[i] + h_len[i]);
+    doff[i] = out_end;
+    out_end += al(xcg_zdeflate_bound(h_len[i]), 4);
+  }
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  uint32_t* d_len = nullptr;
+  int rc = XCG_OK;
+  if (hipMalloc(&d_in, in_end + 1) != hipSuccess || hipMalloc(&d_out, out_end) != hipSuccess ||
+      hipMalloc(&d_len, 4ull * n) != hipSuccess) {
+    rc = XCG_ENOMEM;
+  }
+  if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
+  if (!rc) rc = xcg_zdeflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), d_len, nullptr);
+  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = XCG_EHIP;
+  if (!rc && hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
+  for (uint32_t i = 0; !rc && i < n; i++)
+    if (hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  (void)hipFree(d_len);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+"""Host-side mirror of wanproxy's zlib stage over libxcgpu.so's xcg_zdeflate_*.
+
+Reference interface (wanproxy tree):
+  DeflatePipe(int level) / consume(Buffer *in)      zlib/deflate_pipe.h:33-42,
+                                                    zlib/deflate_pipe.cc:36-115
+  chained after the XCodec pipe pair                programs/wanproxy/
+                                                    wanproxy_codec_pipe_pair.cc:97-106,148-157
+
+`DeflatePipes(level, nstreams)` is a GPU context holding `nstreams`
+DeflatePipe instances; `consume_many` runs one consume() per listed stream in
+one batch (what a proxy serving many connections issues per event-loop turn);
+`pipe(i).consume(data)` is the single-pipe form with DeflatePipe's exact
+signature semantics: non-empty input -> the bytes produced after
+deflate(Z_SYNC_FLUSH); b'' -> EOS, deflate(Z_FINISH).  Errors raise; there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .xcgpu import XCGError, _check, _stream_ptr, lib as _xlib
+
+XCG_ENOTSUP = -95
+
+
+def _lib():
+    L = _xlib()
+    if not getattr(L, '_zd_bound', False):
+        vp = C.c_void_p
+        L.xcg_zdeflate_bound.argtypes = [C.c_uint32]
+        L.xcg_zdeflate_bound.restype = C.c_uint64
+        L.xcg_zdeflate_create.argtypes = [C.c_int, C.c_int, C.c_uint32, C.POINTER(vp)]
+        L.xcg_zdeflate_create.restype = C.c_int
+        L.xcg_zdeflate_destroy.argtypes = [vp]
+        L.xcg_zdeflate_destroy.restype = None
+        L.xcg_zdeflate_reset.argtypes = [vp, C.c_uint32]
+        L.xcg_zdeflate_reset.restype = C.c_int
+        L.xcg_zdeflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
+        L.xcg_zdeflate_batch.restype = C.c_int
+        L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp]
+        L.xcg_zdeflate_host.restype = C.c_int
+        L._zd_bound = True
+    return L
+
+
+def bound(n: int) -> int:
+    return int(n) + (int(n) >> 1) + 128
+
+
+class DeflatePipes:
+    def __init__(self, level: int = 6, nstreams: int = 1, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise XCGError('DeflatePipes needs a GPU (no CPU fallback)')
+        self.level, self.nstreams, self.device = level, nstreams, device
+        h = C.c_void_p()
+        rc = _lib().xcg_zdeflate_create(device, level, nstreams, C.byref(h))
+        if rc == XCG_ENOTSUP:
+            raise XCGError(f'zlib level {level}: only levels 4-9 (deflate_slow) are implemented')
+        _check(rc)
+        self.h = h
+
+    def close(self):
+        if getattr(self, 'h', None):
+            _lib().xcg_zdeflate_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def reset(self, stream: int):
+        _check(_lib().xcg_zdeflate_reset(self.h, stream))
+
+    def pipe(self, stream: int) -> 'DeflatePipe':
+        return DeflatePipe(self, stream)
+
+    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, d_out_len, stream=None):
+        """Device-resident batch: d_in / d_out / d_out_len are torch CUDA
+        tensors; in_off / lens / streams / out_off host numpy arrays."""
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        streams = np.ascontiguousarray(streams, dtype=np.uint32)
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+        n = int(lens.size)
+        _check(_lib().xcg_zdeflate_batch(self.h, C.c_void_p(d_in.data_ptr()), in_off.ctypes.data, lens.ctypes.data,
+                                         streams.ctypes.data, n, C.c_void_p(d_out.data_ptr()), out_off.ctypes.data,
+                                         C.c_void_p(d_out_len.data_ptr()), _stream_ptr(stream)))
+
+    def consume_many(self, items):
+        """items: [(stream, bytes)] (each stream at most once).  Returns the
+        produced bytes per item, in order."""
+        import torch
+        dev = torch.device('cuda', self.device)
+        n = len(items)
+        if n == 0:
+            return []
+        lens = np.array([len(d) for _, d in items], dtype=np.uint32)
+        streams = np.array([s for s, _ in items], dtype=np.uint32)
+        in_off = np.zeros(n, dtype=np.uint64)
+        in_off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        bounds = np.array([(bound(x) + 3) & ~3 for x in lens], dtype=np.uint64)
+        out_off = np.zeros(n, dtype=np.uint64)
+        out_off[1:] = np.cumsum(bounds)[:-1]
+        blob = b''.join(d for _, d in items)
+        d_in = torch.frombuffer(bytearray(blob or b'\0'), dtype=torch.uint8).to(dev)
+        d_out = torch.empty(int(bounds.sum()), dtype=torch.uint8, device=dev)
+        d_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.batch_device(d_in, in_off, lens, streams, d_out, out_off, d_len)
+        torch.cuda.synchronize(dev)
+        ol = d_len.cpu().numpy().astype(np.uint64)
+        out = d_out.cpu().numpy()
+        return [out[int(out_off[i]):int(out_off[i] + ol[i])].tobytes() for i in range(n)]
+
+
+class DeflatePipe:
+    """One DeflatePipe(level) of a DeflatePipes context."""
+
+    def __init__(self, ctx: DeflatePipes, stream: int):
+        self.ctx, self.stream = ctx, stream
+
+    def consume(self, data: bytes) -> bytes:
+        return self.ctx.consume_many([(self.stream, data)])[0]
