@@ -34,6 +34,9 @@
  *       DeflatePipe::DeflatePipe(int level) / consume(Buffer *)
  *                                                      zlib/deflate_pipe.h:33-42,
  *                                                      zlib/deflate_pipe.cc:36-115
+ *   xcg_zinflate_*
+ *       InflatePipe::InflatePipe() / consume(Buffer *) zlib/inflate_pipe.h:33-42,
+ *                                                      zlib/inflate_pipe.cc:33-139
  */
 #ifndef XCGPU_H
 #define XCGPU_H
@@ -317,6 +320,23 @@ int xcg_zdeflate_batch(xcg_zdeflate *z, const uint8_t *d_in, const uint64_t *h_i
 int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
                       const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
                       uint32_t *h_out_len);
+
+/* Receiving side: `nstreams` InflatePipe instances (zlib/inflate_pipe.cc:33-46,
+ * inflateInit) in HBM.  xcg_zinflate_batch: one InflatePipe::consume() per
+ * listed stream (at most once per batch): h_len[i] bytes at d_in + h_in_off[i]
+ * are the next cut of the peer's zlib stream (any cut: inside a symbol or a
+ * block header is fine); every byte they let inflate() produce goes to
+ * d_out + h_out_off[i] (at most h_out_cap[i] bytes), its count to
+ * d_out_len[i].  d_status[i]: 0 ok, 1 the stream's end was reached (with
+ * h_len 0 = EOS: InflatePipe's produce_eos), -1 Z_DATA_ERROR (bad header,
+ * code, distance, adler32, or bytes after the end: produce_error), -2 h_out_cap
+ * too small (nothing committed: the call may be repeated with more room). */
+typedef struct xcg_zinflate xcg_zinflate;
+int xcg_zinflate_create(int device, uint32_t nstreams, xcg_zinflate **out);
+void xcg_zinflate_destroy(xcg_zinflate *z);
+int xcg_zinflate_batch(xcg_zinflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
+                       const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
+                       const uint32_t *h_out_cap, uint32_t *d_out_len, int32_t *d_status, void *stream);
 
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""zlib stage throughput (DeflatePipe, zlib/deflate_pipe.cc:57-115) on the GPU:
+S streams, each step = one consume() of B bytes per stream (Z_SYNC_FLUSH),
+inputs resident in HBM; every output checked against the system zlib 1.2.11
+driven in DeflatePipe's call pattern.  Prints one JSON object.
+
+Workloads: `xcodec` = the XCodec stream encoding of C2 (what wanproxy feeds its
+DeflatePipe: wanproxy_codec_pipe_pair.cc:97-106), cut into per-stream calls;
+`text` = compressible protocol-like traffic (tests/zlib_cases.wan_stream)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def workload(kind: str, streams: int, call_bytes: int, steps: int):
+    """list over steps of list over streams of bytes"""
+    if kind == 'text':
+        from tests.zlib_cases import wan_stream
+        per = [wan_stream(5000 + s, steps, call_bytes) for s in range(streams)]
+        return [[per[s][k] for s in range(streams)] for k in range(steps)]
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d = synth.stream(0xC2, 4096 * 65536, 50, 0)
+    offs, lens = synth.chunks_of(d, 65536)
+    ctx = Context(0, cache_segments=1 << 18)
+    enc = b''.join(ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM))
+    ctx.close()
+    need = streams * call_bytes * steps
+    while len(enc) < need:
+        enc += enc
+    out, o = [], 0
+    for _ in range(steps):
+        row = []
+        for _ in range(streams):
+            row.append(enc[o:o + call_bytes])
+            o += call_bytes
+        out.append(row)
+    return out
+
+
+def zlib_ref(streams_calls, level, threads):
+    """outputs of the reference call pattern, streams in parallel (zlib releases the GIL)"""
+    from oracle.zlib_pipe import DeflatePipeRef
+
+    def one(calls):
+        r = DeflatePipeRef(level)
+        return [r.consume(c) for c in calls]
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(one, streams_calls))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--kind', default='xcodec', choices=['xcodec', 'text'])
+    ap.add_argument('--streams', type=int, default=4096)
+    ap.add_argument('--call-bytes', type=int, default=65536)
+    ap.add_argument('--steps', type=int, default=4)
+    ap.add_argument('--level', type=int, default=6)
+    ap.add_argument('--check', type=float, default=1.0, help='fraction of streams checked against zlib')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    args = ap.parse_args()
+    import torch
+    from wanproxy_amd.zpipe import DeflatePipes, bound
+    dev = torch.device('cuda', 0)
+    S, B, K = args.streams, args.call_bytes, args.steps
+    data = workload(args.kind, S, B, K)
+    ctx = DeflatePipes(args.level, S)
+    lens = np.full(S, B, dtype=np.uint32)
+    sids = np.arange(S, dtype=np.uint32)
+    in_off = (np.arange(S, dtype=np.uint64) * B)
+    ob = (bound(B) + 255) & ~255
+    out_off = np.arange(S, dtype=np.uint64) * ob
+    d_ins = [torch.frombuffer(bytearray(b''.join(row)), dtype=torch.uint8).to(dev) for row in data]
+    d_out = [torch.empty(S * ob, dtype=torch.uint8, device=dev) for _ in range(K)]
+    d_len = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(K)]
+    torch.cuda.synchronize()
+    times = []
+    for k in range(K):
+        t0 = time.perf_counter()
+        ctx.batch_device(d_ins[k], in_off, lens, sids, d_out[k], out_off, d_len[k])
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    outs = []
+    for k in range(K):
+        ol = d_len[k].cpu().numpy()
+        o = d_out[k].cpu().numpy()
+        outs.append([o[s * ob:s * ob + int(ol[s])].tobytes() for s in range(S)])
+    nchk = max(1, int(S * args.check))
+    t0 = time.perf_counter()
+    ref = zlib_ref([[data[k][s] for k in range(K)] for s in range(nchk)], args.level, args.cpu_threads)
+    cpu_s = time.perf_counter() - t0
+    bad = sum(1 for s in range(nchk) for k in range(K) if ref[s][k] != outs[k][s])
+    # steady state: steps after the first (the first carries the zlib header)
+    steady = times[1:] if K > 1 else times
+    ms = 1e3 * float(np.median(steady))
+    in_bytes = S * B
+    out_bytes = sum(len(outs[K - 1][s]) for s in range(S))
+    res = {
+        'metric': 'DeflatePipe consume GiB/s (device-resident, one consume per stream per step)',
+        'kind': args.kind, 'level': args.level, 'streams': S, 'call_bytes': B, 'steps': K,
+        'value': round(in_bytes / (ms / 1e3) / 2**30, 3), 'ms_per_step': round(ms, 3),
+        'out_in': round(out_bytes / in_bytes, 5),
+        'checked': f'{nchk} of {S} streams x {K} calls vs zlib {zlib.ZLIB_RUNTIME_VERSION}, {bad} mismatches',
+        'cpu_zlib': {'GiBps': round(nchk * K * B / cpu_s / 2**30, 4), 'threads': args.cpu_threads,
+                     'sample': f'{nchk} streams x {K} calls'},
+    }
+    print(json.dumps(res))
+    ctx.close()
+    if bad:
+        sys.exit(1)
+
+
+if __name__ == '__main__':
+    main()

@@ -117,3 +117,90 @@ def test_errors():
     ctx.reset(1)
     assert ctx.pipe(1).consume(b'hello') == DeflatePipeRef(6).consume(b'hello')
     ctx.close()
+
+
+# ---------------------------------------------------------------- InflatePipe
+def inflate_streams(streams):
+    """streams: [[input cut bytes...]] -> [[(produced, status)...]], call k of
+    every stream in batch k (InflatePipe::consume per cut)."""
+    from wanproxy_amd.zpipe import InflatePipes
+    ctx = InflatePipes(len(streams))
+    outs = [[] for _ in streams]
+    for k in range(max(len(s) for s in streams)):
+        items = [(i, s[k]) for i, s in enumerate(streams) if k < len(s)]
+        for (i, _), g in zip(items, ctx.consume_many(items)):
+            outs[i].append(g)
+    ctx.close()
+    return outs
+
+
+def cuts(rng, z: bytes, mode: str):
+    if mode == 'bytes':
+        return [z[i:i + 1] for i in range(len(z))]
+    out, i = [], 0
+    while i < len(z):
+        n = rng.choice([1, 2, 3, 7, 100, 1500, 65536]) if mode == 'random' else 65536
+        out.append(z[i:i + n])
+        i += n
+    return out
+
+
+def test_inflate_zlib_streams_any_cut():
+    """zlib-made streams (stored, static, dynamic blocks; levels 1-9) cut at
+    random points; every call's output equals zlib's inflate on the same cuts."""
+    from oracle.zlib_pipe import InflatePipeRef
+    rng = random.Random(31)
+    srcs, streams = [], []
+    for level, calls in cases(41, 16):
+        level = rng.choice([1, 2, 3, level, 9])
+        ref = DeflatePipeRef(level)
+        z = b''.join(ref.consume(c) for c in calls if c) + ref.consume(b'')
+        srcs.append(b''.join(calls))
+        streams.append(cuts(rng, z, rng.choice(['random', 'random', 'frames'])) + [b''])
+    got = inflate_streams(streams)
+    for si, (src, cs) in enumerate(zip(srcs, streams)):
+        ref = InflatePipeRef()
+        for k, c in enumerate(cs[:-1]):
+            exp = ref.consume(c)
+            out, st = got[si][k]
+            assert out == exp, (si, k, len(out), len(exp))
+            assert st in (0, 1), (si, k, st)
+        assert b''.join(o for o, _ in got[si]) == src
+        assert got[si][-1] == (b'', 1)     # EOS after the end: produce_eos
+
+
+def test_inflate_byte_by_byte_and_small():
+    streams = []
+    srcs = []
+    for i, data in enumerate([b'', b'a', b'hello hello hello hello', bytes(1000), random.Random(3).randbytes(700)]):
+        z = zlib.compress(data, 6)
+        srcs.append(data)
+        streams.append([z[j:j + 1] for j in range(len(z))] + [b''])
+    got = inflate_streams(streams)
+    for si, src in enumerate(srcs):
+        assert b''.join(o for o, _ in got[si]) == src
+        assert got[si][-1][1] == 1
+
+
+def test_gpu_deflate_then_gpu_inflate():
+    """wanproxy's zlib stage both ways on the GPU: DeflatePipe output, cut
+    into frames, through InflatePipe, for 64 streams."""
+    rng = random.Random(8)
+    streams = [wan_stream(3000 + i, 3, 65536) + [b''] for i in range(64)]
+    z = run_streams({6: streams})[6]
+    cut = [cuts(rng, b''.join(zs), 'random') + [b''] for zs in z]
+    got = inflate_streams(cut)
+    for i in range(64):
+        assert b''.join(o for o, _ in got[i]) == b''.join(streams[i])
+
+
+def test_inflate_errors():
+    good = zlib.compress(b'payload ' * 100, 6)
+    bad_adler = good[:-1] + bytes([good[-1] ^ 1])
+    bad_header = bytes([0x78, 0x9d]) + good[2:]
+    trailing = good + b'x'
+    got = inflate_streams([[bad_adler], [bad_header], [trailing], [good, b'']])
+    assert got[0][0][1] == -1
+    assert got[1][0] == (b'', -1)
+    assert got[2][0][1] == -1
+    assert got[3][0] == (b'payload ' * 100, 1) and got[3][1] == (b'', 1)

@@ -11,7 +11,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/xcg_hash.hip', 'csrc/xcg_lru.hip',
-        'csrc/xcg_pair.hip', 'csrc/xcg_pipe.cpp', 'csrc/xcg_deflate.hip']
+        'csrc/xcg_pair.hip', 'csrc/xcg_pipe.cpp', 'csrc/xcg_deflate.hip', 'csrc/xcg_inflate.hip']
 HDRS = ['csrc/xcg_device.h', 'csrc/xcg_cache.h', 'csrc/xcg_args.h', '../include/xcgpu.h']
 OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

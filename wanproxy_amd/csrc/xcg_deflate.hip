@@ -197,54 +197,68 @@ __global__ __launch_bounds__(64) void zd_adler_kernel(ZArgs a) {
 }
 
 // ------------------------------------------------------------------- chains
-__device__ __forceinline__ uint32_t hash3(const uint8_t* X, int64_t j) {
-  return (((uint32_t)X[j] << 10) ^ ((uint32_t)X[j + 1] << 5) ^ X[j + 2]) & 0x7fffu;
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *(const u32_u*)p; }
+__device__ __forceinline__ uint32_t hash3(const uint8_t* X, int64_t j) {   // UPDATE_HASH x3 (hash_shift 5)
+  uint32_t w = ld32(X + j);
+  return (((w & 0xff) << 10) ^ (((w >> 8) & 0xff) << 5) ^ ((w >> 16) & 0xff)) & 0x7fffu;
 }
 
-// One wave per call, positions in order in groups of 64: a lane's previous
-// occurrence is the nearest lower lane with its hash, else the LDS head table;
-// the last lane of each hash then becomes the head.
+// One wave per call, positions in order in groups of 64.  A lane's previous
+// occurrence is the nearest lower lane with its hash (lanes with an equal hash
+// found by 15 ballots, one per hash bit), else the LDS head table; the last
+// lane of each hash then becomes the head.  The head table keeps the low 16
+// bits of positions (64 KiB: two waves per CU); an entry's age is
+// (j - v) mod 2^16, valid for 1..32767 (farther links are 0 anyway), and every
+// 16384 positions entries older than 32767 are expired, so no age ever wraps.
 __global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
-  __shared__ int32_t head[32768];
-  __shared__ uint32_t succ[2];
+  __shared__ uint16_t head[32768];
   const ZCall c = a.calls[blockIdx.x];
   const ZState s = a.st[c.stream];
   const int lane = threadIdx.x;
   const uint8_t* X = a.X + c.x_off;
   uint16_t* d16 = a.d16 + c.x_off;
-  for (int i = lane; i < 32768; i += 64) head[i] = -1;
   // first valid position: max(base, total - WSIZE) as an X index
   int64_t jlo = (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
+  const uint16_t empty = (uint16_t)(jlo + 32768);   // age >= 32768 until jlo + 32768
+  for (int i = lane; i < 32768; i += 64) head[i] = empty;
   int64_t jend = (int64_t)WSIZE + c.len;     // positions q with q + 2 < jend get a hash
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // X words for the next group are loaded one group ahead (X has XPAD bytes after the data)
+  uint32_t wcur = ld32(X + jlo + lane);
   for (int64_t g = jlo; g < jend; g += 64) {
+    const uint32_t wnext = g + 64 < jend ? ld32(X + g + 64 + lane) : 0u;
+    if (((g - jlo) & 16383) == 0 && g != jlo) {   // expire entries older than 32767
+      const uint16_t far = (uint16_t)(g + 32768);
+      for (int i = lane; i < 32768; i += 64) {
+        uint16_t v = head[i];
+        if ((uint16_t)(g - v) > 32767) head[i] = far;
+      }
+    }
     int64_t j = g + lane;
     bool valid = j + 2 < jend;
-    uint32_t h = valid ? hash3(X, j) : 0x8000u + lane;   // invalid lanes never match
-    int pred = -1;
-#pragma unroll 8
-    for (int k = 63; k >= 1; k--) {
-      uint32_t o = __shfl(h, (lane - k) & 63);
-      if (lane >= k && o == h) pred = lane - k;
+    // UPDATE_HASH x3 (hash_shift 5) over bytes j, j+1, j+2; invalid lanes form their own class
+    uint32_t h = valid ? (((wcur & 0xff) << 10) ^ (((wcur >> 8) & 0xff) << 5) ^ ((wcur >> 16) & 0xff)) & 0x7fffu : 0x8000u;
+    wcur = wnext;
+    uint64_t m = ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 15; b++) {
+      bool bit = (h >> b) & 1;
+      uint64_t bl = ballot(bit);
+      m &= bit ? bl : ~bl;
     }
-    if (lane < 2) succ[lane] = 0;
-    __syncthreads();
-    if (pred >= 0) atomicOr(&succ[pred >> 5], 1u << (pred & 31));
-    __syncthreads();
-    bool last = !((succ[lane >> 5] >> (lane & 31)) & 1);
-    int32_t prev = -1;
-    if (valid) prev = pred >= 0 ? (int32_t)(g + pred) : head[h];
-    if (j < jend) {
-      int64_t dd = prev >= 0 ? j - prev : 0;
-      d16[j] = (dd > 0 && dd <= 32767) ? (uint16_t)dd : 0;
+    uint64_t lower = m & below;
+    bool last = (m >> lane) == 1ull;
+    int32_t age = 0;
+    if (valid) {
+      if (lower) age = lane - (63 - __clzll(lower));
+      else age = (uint16_t)((uint16_t)j - head[h]);
     }
-    __syncthreads();
-    if (valid && last) head[h] = (int32_t)j;
-    __syncthreads();
+    if (j < jend) d16[j] = (age > 0 && age <= 32767) ? (uint16_t)age : 0;
+    if (valid && last) head[h] = (uint16_t)j;
   }
 }
 
 // ------------------------------------------------------------------- match table
-__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *(const u32_u*)p; }
 
 // Entry: M (9 bits) | distance of the first candidate reaching M (15 bits) << 9
 // | ELIG << 31 (chain head exists, within MAX_DIST, lookahead >= 3).  The scan
@@ -352,9 +366,10 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
   int64_t block_start = p;
   int ml = MIN_MATCH - 1, avail = 0;
   int64_t ms = 0;
-  ScanWin W;
+  ScanWin W, N;   // entries of [w, w + 64) and, loaded ahead, [w + 64, w + 128)
   int64_t w = p;
   load_win(W, a, c, w);
+  load_win(N, a, c, w + 64);
 
   auto flush = [&](int64_t q, bool last) {
     if (lane == 0) {
@@ -395,9 +410,15 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
       } while (rd - p < MIN_LOOKAHEAD && rd < end);
       if (rd == p) break;
     }
-    if (p >= w + 64 || p < w) {
-      w = p;
-      load_win(W, a, c, w);
+    if (p >= w + 64) {
+      if (p < w + 128) {
+        W = N;
+        w += 64;
+      } else {
+        w = p;
+        load_win(W, a, c, w);
+      }
+      load_win(N, a, c, w + 64);
     }
     const int li = (int)(p - w);
     if (avail && ml == MIN_MATCH - 1) {
@@ -858,7 +879,7 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a, const uint32_t* bl
     uint64_t w0 = (db + 3) >> 2, w1 = (db + B.stored_len) >> 2;
     for (uint64_t wi = w0 + lane; wi < w1 && wi < o.nwords; wi += 64) {
       uint64_t b = wi * 4 - db;
-      o.o[wi] = X[b] | ((uint32_t)X[b + 1] << 8) | ((uint32_t)X[b + 2] << 16) | ((uint32_t)X[b + 3] << 24);
+      o.o[wi] = ld32(X + b);
     }
     for (uint64_t i = lane; i < B.stored_len; i += 64) {
       uint64_t byte = db + i;
@@ -885,39 +906,73 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a, const uint32_t* bl
       pos = bw.pos;
     }
     pos = readlane64(pos, 0);
+    // Each lane packs a contiguous run of symbols: pass 1 sizes the runs, a
+    // wave scan places them, pass 2 writes whole words with plain stores and
+    // only each run's first and last (shared) words with atomicOr.
     const uint32_t* sym = a.sym + c.t_off;
-    for (uint32_t i0 = B.sym_begin; i0 < B.sym_end; i0 += 64) {
-      uint32_t i = i0 + lane;
-      uint64_t v = 0;
-      int nb = 0;
-      if (i < B.sym_end) {
-        uint32_t e = sym[i], dist = e >> 8;
-        if (dist == 0) {
-          uint32_t t = ltab[e & 255];
-          v = t & 0xffff;
-          nb = t >> 16;
-        } else {
-          uint32_t lc = e & 255;
-          int code = len_code(lc);
-          uint32_t t = ltab[257 + code];
-          v = t & 0xffff;
-          nb = t >> 16;
-          int xl = XLB[code];   // code 28 (length 258) has no extra bits
-          if (xl) v |= (uint64_t)(lc - BASE_LEN[code]) << nb;
-          nb += xl;
-          uint32_t d = dist - 1;
-          int dc = dist_code(d);
-          uint32_t td = dtab[dc];
-          v |= (uint64_t)(td & 0xffff) << nb;
-          nb += td >> 16;
-          v |= (uint64_t)(d - BASE_DIST[dc]) << nb;
-          nb += XDB[dc];
-        }
+    const uint32_t nsy = B.sym_end - B.sym_begin, per = (nsy + 63) / 64;
+    const uint32_t s0 = B.sym_begin + min(nsy, lane * per), s1 = B.sym_begin + min(nsy, (lane + 1) * per);
+    auto parts = [&](uint32_t e, uint32_t& v0, int& n0, uint32_t& v1, int& n1) {
+      uint32_t dist = e >> 8;
+      if (dist == 0) {
+        uint32_t t = ltab[e & 255];
+        v0 = t & 0xffff;
+        n0 = t >> 16;
+        v1 = 0;
+        n1 = 0;
+        return;
       }
-      uint32_t incl = wave_incl_scan((uint32_t)nb);
-      or_bits(o, pos + incl - nb, v, nb);
-      pos += readlane(incl, 63);
+      uint32_t lc = e & 255;
+      int code = len_code(lc);
+      uint32_t t = ltab[257 + code];
+      v0 = t & 0xffff;
+      n0 = t >> 16;
+      int xl = XLB[code];   // code 28 (length 258) has no extra bits
+      if (xl) v0 |= (lc - BASE_LEN[code]) << n0;
+      n0 += xl;
+      uint32_t d = dist - 1;
+      int dc = dist_code(d);
+      uint32_t td = dtab[dc];
+      v1 = (td & 0xffff) | ((d - BASE_DIST[dc]) << (td >> 16));
+      n1 = (td >> 16) + XDB[dc];
+    };
+    uint32_t mybits = 0;
+    for (uint32_t i = s0; i < s1; i++) {
+      uint32_t v0, v1;
+      int n0, n1;
+      parts(sym[i], v0, n0, v1, n1);
+      mybits += n0 + n1;
     }
+    uint32_t incl = wave_incl_scan(mybits);
+    uint64_t P = pos + incl - mybits;
+    if (s1 > s0) {
+      uint64_t wi = P >> 5;
+      uint64_t acc = 0;
+      int accn = (int)(P & 31);
+      bool first = true;
+      auto put = [&](uint32_t v, int n) {
+        acc |= (uint64_t)v << accn;
+        accn += n;
+        if (accn >= 32) {
+          uint32_t word = (uint32_t)acc;
+          if (first) or_word(o, wi, word);
+          else if (wi < o.nwords) o.o[wi] = word;
+          first = false;
+          wi++;
+          acc >>= 32;
+          accn -= 32;
+        }
+      };
+      for (uint32_t i = s0; i < s1; i++) {
+        uint32_t v0, v1;
+        int n0, n1;
+        parts(sym[i], v0, n0, v1, n1);
+        put(v0, n0);
+        if (n1) put(v1, n1);
+      }
+      if (accn > 0) or_word(o, wi, (uint32_t)acc);
+    }
+    pos += readlane(incl, 63);
     if (lane == 0) {
       uint32_t t = ltab[256];
       or_bits(o, pos, t & 0xffff, t >> 16);

@@ -9,6 +9,8 @@ Reference interface (wanproxy tree):
 `DeflatePipes(level, nstreams)` is a GPU context holding `nstreams`
 DeflatePipe instances; `consume_many` runs one consume() per listed stream in
 one batch (what a proxy serving many connections issues per event-loop turn);
+`InflatePipes(nstreams)` is the receiving side, InflatePipe
+(zlib/inflate_pipe.cc:54-139): consume() takes any cut of the peer's stream.
 `pipe(i).consume(data)` is the single-pipe form with DeflatePipe's exact
 signature semantics: non-empty input -> the bytes produced after
 deflate(Z_SYNC_FLUSH); b'' -> EOS, deflate(Z_FINISH).  Errors raise; there is
@@ -41,6 +43,12 @@ def _lib():
         L.xcg_zdeflate_batch.restype = C.c_int
         L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp]
         L.xcg_zdeflate_host.restype = C.c_int
+        L.xcg_zinflate_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(vp)]
+        L.xcg_zinflate_create.restype = C.c_int
+        L.xcg_zinflate_destroy.argtypes = [vp]
+        L.xcg_zinflate_destroy.restype = None
+        L.xcg_zinflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.xcg_zinflate_batch.restype = C.c_int
         L._zd_bound = True
     return L
 
@@ -122,3 +130,79 @@ class DeflatePipe:
 
     def consume(self, data: bytes) -> bytes:
         return self.ctx.consume_many([(self.stream, data)])[0]
+
+
+class InflateError(XCGError):
+    pass
+
+
+class InflatePipes:
+    """`nstreams` InflatePipe instances on one GPU."""
+
+    def __init__(self, nstreams: int = 1, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise XCGError('InflatePipes needs a GPU (no CPU fallback)')
+        self.nstreams, self.device = nstreams, device
+        h = C.c_void_p()
+        _check(_lib().xcg_zinflate_create(device, nstreams, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, 'h', None):
+            _lib().xcg_zinflate_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, out_cap, d_out_len, d_status, stream=None):
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        streams = np.ascontiguousarray(streams, dtype=np.uint32)
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+        out_cap = np.ascontiguousarray(out_cap, dtype=np.uint32)
+        _check(_lib().xcg_zinflate_batch(self.h, C.c_void_p(d_in.data_ptr()), in_off.ctypes.data, lens.ctypes.data,
+                                         streams.ctypes.data, int(lens.size), C.c_void_p(d_out.data_ptr()),
+                                         out_off.ctypes.data, out_cap.ctypes.data, C.c_void_p(d_out_len.data_ptr()),
+                                         C.c_void_p(d_status.data_ptr()), _stream_ptr(stream)))
+
+    def consume_many(self, items, out_cap: int = None):
+        """items: [(stream, bytes)] -> [(produced bytes, status)] with status
+        0 ok, 1 stream end (EOS for an empty consume), -1 data error.  A call
+        that needs more output room is repeated with more (-2 commits nothing)."""
+        import torch
+        dev = torch.device('cuda', self.device)
+        n = len(items)
+        if n == 0:
+            return []
+        lens = np.array([len(d) for _, d in items], dtype=np.uint32)
+        streams = np.array([s for s, _ in items], dtype=np.uint32)
+        in_off = np.zeros(n, dtype=np.uint64)
+        in_off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        cap = out_cap or max(1 << 20, 8 * int(lens.max()) + 65536)
+        blob = b''.join(d for _, d in items)
+        d_in = torch.frombuffer(bytearray(blob or b'\0'), dtype=torch.uint8).to(dev)
+        while True:
+            caps = np.full(n, cap, dtype=np.uint32)
+            out_off = np.arange(n, dtype=np.uint64) * cap
+            d_out = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+            d_len = torch.zeros(n, dtype=torch.int32, device=dev)
+            d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+            self.batch_device(d_in, in_off, lens, streams, d_out, out_off, caps, d_len, d_st)
+            torch.cuda.synchronize(dev)
+            st = d_st.cpu().numpy()
+            if (st == -2).any():
+                # calls with enough room committed; repeat only the others with more room
+                ol = d_len.cpu().numpy()
+                out = d_out.cpu().numpy()
+                done = {i: (out[int(out_off[i]):int(out_off[i]) + int(ol[i])].tobytes(), int(st[i]))
+                        for i in range(n) if st[i] != -2}
+                redo = [i for i in range(n) if st[i] == -2]
+                more = self.consume_many([items[i] for i in redo], out_cap=cap * 4)
+                for i, r in zip(redo, more):
+                    done[i] = r
+                return [done[i] for i in range(n)]
+            ol = d_len.cpu().numpy()
+            out = d_out.cpu().numpy()
+            return [(out[int(out_off[i]):int(out_off[i]) + int(ol[i])].tobytes(), int(st[i])) for i in range(n)]
