@@ -49,6 +49,7 @@ def parse():
     ap.add_argument('--no-extras', action='store_true', help='skip the stream / decode / PCIe side measurements')
     ap.add_argument('--no-configs', action='store_true',
                     help='skip the C3 / C4 / C5 stream-configuration figures (scripts/configs_bench.py)')
+    ap.add_argument('--no-zlib', action='store_true', help='skip the zlib stage figures (scripts/zlib_bench.py)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='torch.distributed backend for N > 1 (nccl = RCCL; gloo rehearses the N > 1 path with '
                          'several ranks sharing one GPU: device = LOCAL_RANK mod the visible GPUs)')
@@ -506,6 +507,28 @@ def other_configs():
     return out
 
 
+def zlib_stage(streams=2048, steps=3, check=0.25, threads=16):
+    """wanproxy's zlib stage after the codec (DeflatePipe / InflatePipe,
+    zlib/deflate_pipe.cc:57-115, inflate_pipe.cc:54-139) on the GPU, level 6
+    as wanproxy.conf: `streams` pipes, one consume() of 64 KiB per pipe per
+    step, on the XCodec output of C2 and on protocol-like text; every checked
+    output equal to the system zlib's in DeflatePipe's call pattern, every
+    stream inflated back (scripts/zlib_bench.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('zlib_bench', os.path.join(ROOT, 'scripts', 'zlib_bench.py'))
+    zb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(zb)
+    out = {}
+    for kind in ('xcodec', 'text'):
+        a = argparse.Namespace(kind=kind, streams=streams, call_bytes=65536, steps=steps, level=6, check=check,
+                               cpu_threads=threads)
+        try:
+            out[kind] = zb.run(a)
+        except BaseException as e:
+            out[kind] = {'error': f'{type(e).__name__}: {e}'}
+    return out
+
+
 def sharded_configs(world, rank, dev, backend='nccl'):
     """N > 1: BASELINE configs C4 and C5 as ONE dataset each, split into
     contiguous per-rank ranges (wanproxy_amd/shard.py config_shard: C4 2^20/N
@@ -674,6 +697,8 @@ def main():
             line['sharded_configs'] = sharded
         if world == 1 and not args.no_extras and not args.no_configs:
             line['configs'] = other_configs()
+        if world == 1 and not args.no_extras and not args.no_zlib:
+            line['zlib_stage'] = zlib_stage(threads=host_cpus()['threads'])
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_seconds)
         print(json.dumps(line), flush=True)

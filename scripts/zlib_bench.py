@@ -69,7 +69,13 @@ def main():
     ap.add_argument('--level', type=int, default=6)
     ap.add_argument('--check', type=float, default=1.0, help='fraction of streams checked against zlib')
     ap.add_argument('--cpu-threads', type=int, default=16)
-    args = ap.parse_args()
+    res = run(ap.parse_args())
+    print(json.dumps(res))
+    if res.get('mismatches') or 'MISMATCH' in res['inflate']['checked']:
+        sys.exit(1)
+
+
+def run(args) -> dict:
     import torch
     from wanproxy_amd.zpipe import DeflatePipes, bound
     dev = torch.device('cuda', 0)
@@ -96,7 +102,42 @@ def main():
         ol = d_len[k].cpu().numpy()
         o = d_out[k].cpu().numpy()
         outs.append([o[s * ob:s * ob + int(ol[s])].tobytes() for s in range(S)])
+    # InflatePipe on the GPU over the same streams: step k consumes deflate output k
+    from wanproxy_amd.zpipe import InflatePipes
+    ictx = InflatePipes(S)
+    icap = B + 4096
+    zi_times, zi_ok = [], True
+    for k in range(K):
+        zl = np.array([len(outs[k][s]) for s in range(S)], dtype=np.uint32)
+        zo = np.zeros(S, dtype=np.uint64)
+        zo[1:] = np.cumsum(zl.astype(np.uint64))[:-1]
+        d_z = torch.frombuffer(bytearray(b''.join(outs[k])), dtype=torch.uint8).to(dev)
+        d_o = torch.empty(S * icap, dtype=torch.uint8, device=dev)
+        d_ol = torch.zeros(S, dtype=torch.int32, device=dev)
+        d_st = torch.zeros(S, dtype=torch.int32, device=dev)
+        caps = np.full(S, icap, dtype=np.uint32)
+        ooff = np.arange(S, dtype=np.uint64) * icap
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ictx.batch_device(d_z, zo, zl, sids, d_o, ooff, caps, d_ol, d_st)
+        torch.cuda.synchronize()
+        zi_times.append(time.perf_counter() - t0)
+        st = d_st.cpu().numpy()
+        ol = d_ol.cpu().numpy()
+        o = d_o.cpu().numpy()
+        zi_ok = zi_ok and bool((st == 0).all()) and all(
+            o[s * icap:s * icap + int(ol[s])].tobytes() == data[k][s] for s in range(S))
+    ictx.close()
+    zi_ms = 1e3 * float(np.median(zi_times[1:] if K > 1 else zi_times))
     nchk = max(1, int(S * args.check))
+    t0 = time.perf_counter()
+
+    def inf_one(s):
+        d = zlib.decompressobj()
+        return [d.decompress(outs[k][s]) for k in range(K)]
+    with ThreadPoolExecutor(args.cpu_threads) as ex:
+        list(ex.map(inf_one, range(nchk)))
+    cpu_inf_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     ref = zlib_ref([[data[k][s] for k in range(K)] for s in range(nchk)], args.level, args.cpu_threads)
     cpu_s = time.perf_counter() - t0
@@ -112,13 +153,15 @@ def main():
         'value': round(in_bytes / (ms / 1e3) / 2**30, 3), 'ms_per_step': round(ms, 3),
         'out_in': round(out_bytes / in_bytes, 5),
         'checked': f'{nchk} of {S} streams x {K} calls vs zlib {zlib.ZLIB_RUNTIME_VERSION}, {bad} mismatches',
+        'mismatches': bad,
+        'inflate': {'GiBps': round(in_bytes / (zi_ms / 1e3) / 2**30, 3), 'ms_per_step': round(zi_ms, 3),
+                    'checked': 'every stream and step decoded back to its input' + ('' if zi_ok else ' -- MISMATCH')},
         'cpu_zlib': {'GiBps': round(nchk * K * B / cpu_s / 2**30, 4), 'threads': args.cpu_threads,
+                     'inflate_GiBps': round(nchk * K * B / cpu_inf_s / 2**30, 4),
                      'sample': f'{nchk} streams x {K} calls'},
     }
-    print(json.dumps(res))
     ctx.close()
-    if bad:
-        sys.exit(1)
+    return res
 
 
 if __name__ == '__main__':

@@ -5,12 +5,13 @@
 //
 // One wave per call; the decoder's control state is wave-uniform (every lane
 // runs it, values come from readlane), lanes split the byte copies.  The
-// stream's last 32 KiB of output and the call's new output live in a 64 KiB
-// LDS ring, so a match copies LDS -> LDS (the modular source index handles
-// overlapping copies) and the ring is flushed to the caller's buffer every
-// 32 KiB.  Input bits come from a 256-byte register window.  Huffman decoding:
-// a 1024-entry primary table per tree in LDS, codes longer than 10 bits by
-// canonical decoding.  Every field is read under a bounds check; when the
+// stream's last 32 KiB of output live in a 32 KiB LDS ring, so a match copies
+// LDS -> LDS (the modular source index handles overlapping copies); output is
+// flushed to the caller's buffer every 16 KiB, so a slot is rewritten only
+// after its byte was flushed and left the window (~39 KiB of LDS: four waves
+// per CU).  Input bits come from a 256-byte register window.  Huffman
+// decoding: a 512-entry primary table per tree in LDS, longer codes by
+// canonical decoding; the decoder's wave-uniform control runs on the SALU.  Every field is read under a bounds check; when the
 // input ends inside a symbol or a block header, the call stops at the symbol /
 // header start and carries the unread bytes (at most a dynamic block header)
 // into the next call.  The adler32 trailer is checked (inflate()'s
@@ -30,9 +31,9 @@ namespace xcg {
 namespace zi {
 
 constexpr int WSIZE = 32768;
-constexpr uint32_t RMASK = 65535;   // LDS ring of 64 KiB
+constexpr uint32_t RMASK = 32767;   // LDS ring of 32 KiB: the deflate window
 constexpr int PEND_CAP = 1024;
-constexpr int PRI = 10;             // primary table bits
+constexpr int PRI = 9;              // primary table bits
 constexpr int IPAD = 512;           // zero bytes after a call's input in the scratch
 
 enum Mode : uint32_t { M_HEADER = 0, M_BLOCK = 1, M_STORED = 2, M_HUFF = 3, M_TRAILER = 4, M_DONE = 5, M_ERROR = 6 };
@@ -172,19 +173,27 @@ struct Reader {
     uint32_t sh = q & 31;
     uint64_t lo = readlane(win, (int)k) | ((uint64_t)readlane(win, (int)k + 1) << 32);
     uint64_t hi = readlane(win, (int)k + 2);
-    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    uint64_t r = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    return ((uint64_t)readfirst((uint32_t)(r >> 32)) << 32) | readfirst((uint32_t)r);
   }
 };
 
+// A wave-uniform LDS value into a scalar register: the decoder's control runs
+// on the SALU instead of as 64-lane vector ops.
+__device__ __forceinline__ uint32_t su(uint32_t v) { return readfirst(v); }
+
+// the primary-table entry for the bits in v ((sym << 4) | len; len 0: longer code)
+__device__ __forceinline__ uint32_t decode_pri(const Tree& T, uint64_t v) { return su(T.pri[v & ((1u << PRI) - 1)]); }
+
 // Huffman decode of the bits in v: returns (sym << 4) | len, 0 if no code matches
 __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
-  uint32_t e = T.pri[v & ((1u << PRI) - 1)];
+  uint32_t e = su(T.pri[v & ((1u << PRI) - 1)]);
   if (e & 15) return e;
   int code = 0, first = 0, index = 0;
   for (int l = 1; l < 16; l++) {
     code |= (int)((v >> (l - 1)) & 1);
-    int count = T.cnt[l];
-    if (code - first < count) return ((uint32_t)T.sym[index + code - first] << 4) | (uint32_t)l;
+    int count = (int)su(T.cnt[l]);
+    if (code - first < count) return (su(T.sym[index + code - first]) << 4) | (uint32_t)l;
     index += count;
     first = (first + count) << 1;
     code <<= 1;
@@ -335,12 +344,12 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
       uint64_t done = 0;
       while (done < n) {
         uint64_t chunk = n - done;
-        if (chunk > 16384) chunk = 16384;
+        if (chunk > 8192) chunk = 8192;
         __syncthreads();
         for (uint64_t i = lane; i < chunk; i += 64) L.ring[(pos + i) & RMASK] = R.I[(q >> 3) + done + i];
         pos += chunk;
         done += chunk;
-        if (pos - flushed >= 32768) flush();
+        if (pos - flushed >= 16384) flush();
       }
       q += 8 * n;
       stored_left -= (uint32_t)n;
@@ -349,7 +358,49 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
       R.load(q >> 3);
     } else if (mode == M_HUFF) {
       for (;;) {
-        if (pos - flushed >= 32768) flush();
+        // fast path (as zlib's inflate_fast): while any symbol pair fits in the
+        // input, the output room and the ring before its next flush, decode
+        // without per-field checks, two literals per bit fetch
+        while (q + 128 <= qend && pos - flushed < 16000 && pos + 516 - total0 <= c.out_cap) {
+          uint64_t v = R.get(q);
+          uint32_t e = decode_pri(L.lt, v);
+          uint32_t l1 = e & 15, sym = e >> 4;
+          if (!l1) break;   // a long code: the careful path
+          if (sym < 256) {
+            uint32_t e2 = decode_pri(L.lt, v >> l1);
+            if (lane == 0) L.ring[pos & RMASK] = (uint8_t)sym;
+            pos++;
+            q += l1;
+            uint32_t l2 = e2 & 15;
+            if (l2 && (e2 >> 4) < 256) {
+              if (lane == 0) L.ring[pos & RMASK] = (uint8_t)(e2 >> 4);
+              pos++;
+              q += l2;
+            }
+            continue;
+          }
+          if (sym == 256 || sym > 285) break;
+          uint32_t li = sym - 257, xl = LEXT[li];
+          uint32_t length = LBASE[li] + ((uint32_t)(v >> l1) & ((1u << xl) - 1));
+          uint64_t qd = q + l1 + xl;
+          uint64_t vd = R.get(qd);
+          uint32_t ed = decode_pri(L.dt, vd);
+          uint32_t l2 = ed & 15, dsym = ed >> 4;
+          if (!l2 || dsym > 29) break;
+          uint32_t xd = DEXT[dsym];
+          uint32_t dist = DBASE[dsym] + ((uint32_t)(vd >> l2) & ((1u << xd) - 1));
+          if (dist > pos || dist > (uint32_t)WSIZE) break;
+          __syncthreads();
+          if (dist >= length) {
+            for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
+          } else {
+            for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + (i % dist)) & RMASK];
+          }
+          __syncthreads();
+          pos += length;
+          q = qd + l2 + xd;
+        }
+        if (pos - flushed >= 16384) flush();
         uint64_t v = R.get(q);
         uint32_t e = decode(L.lt, v);
         uint32_t l1 = e & 15, sym = e >> 4;
