@@ -337,6 +337,10 @@ void xcg_zinflate_destroy(xcg_zinflate *z);
 int xcg_zinflate_batch(xcg_zinflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
                        const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
                        const uint32_t *h_out_cap, uint32_t *d_out_len, int32_t *d_status, void *stream);
+/* The same on host buffers (synchronous); lengths / statuses to host arrays. */
+int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
+                      const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
+                      const uint32_t *h_out_cap, uint32_t *h_out_len, int32_t *h_status);
 
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,

@@ -1,0 +1,208 @@
+/*
+ * Drop-in bodies for wanproxy's zlib stage on the MI355X engine: DeflatePipe
+ * and InflatePipe with their reference headers unchanged (zlib/deflate_pipe.h,
+ * zlib/inflate_pipe.h); this file replaces zlib/deflate_pipe.cc and
+ * zlib/inflate_pipe.cc in zlib/lib.mk.  Every pipe is a slot
+ * of one process-wide GPU context per direction (and level): a
+ * DeflatePipe(level) consume() is one xcg_zdeflate call on its slot, an
+ * InflatePipe consume() one xcg_zinflate call.  Output bytes equal zlib
+ * 1.2.11's for levels 4-9 (wanproxy.conf uses 6); levels 0-3 HALT at
+ * construction.  The z_stream member the headers declare is left unused.
+ *
+ * Reference behaviour kept (zlib/deflate_pipe.cc:57-115,
+ * zlib/inflate_pipe.cc:54-139): a non-empty consume produces the bytes after
+ * Z_SYNC_FLUSH; an empty one is EOS (Z_FINISH -> produce_eos).  The inflate
+ * side produces what the input so far decodes to, produce_eos on EOS after the
+ * stream's end, produce_error on a data error or bytes after the end.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include <map>
+#include <vector>
+
+#include <common/buffer.h>
+#include <common/thread/mutex.h>
+#include <event/event_callback.h>
+#include <io/pipe/pipe.h>
+
+#include <zlib/deflate_pipe.h>
+#include <zlib/inflate_pipe.h>
+
+#include "../include/xcgpu.h"
+
+namespace {
+
+/* Slots: one per live pipe, handed back on destruction. */
+const uint32_t XCGPU_ZLIB_SLOTS = 4096;
+
+struct DeflatePool {
+	xcg_zdeflate *ctx;
+	std::vector<uint32_t> free_slots;
+	std::map<const void *, uint32_t> slot_of;
+};
+
+struct InflatePool {
+	xcg_zinflate *ctx;
+	std::vector<uint32_t> free_slots;
+	std::map<const void *, uint32_t> slot_of;
+};
+
+DeflatePool *deflate_pool(int level)
+{
+	static std::map<int, DeflatePool *> pools;
+	std::map<int, DeflatePool *>::iterator it = pools.find(level);
+	if (it != pools.end())
+		return it->second;
+	DeflatePool *p = new DeflatePool();
+	if (xcg_zdeflate_create(0, level, XCGPU_ZLIB_SLOTS, &p->ctx) != XCG_OK) {
+		delete p;
+		return NULL;
+	}
+	for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--)
+		p->free_slots.push_back(i - 1);
+	pools[level] = p;
+	return p;
+}
+
+InflatePool *inflate_pool(void)
+{
+	static InflatePool *p;
+	if (p != NULL)
+		return p;
+	InflatePool *q = new InflatePool();
+	if (xcg_zinflate_create(0, XCGPU_ZLIB_SLOTS, &q->ctx) != XCG_OK) {
+		delete q;
+		return NULL;
+	}
+	for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--)
+		q->free_slots.push_back(i - 1);
+	p = q;
+	return p;
+}
+
+std::map<const void *, int>& deflate_levels()
+{
+	static std::map<const void *, int> levels;
+	return levels;
+}
+
+void take_all(Buffer *in, std::vector<uint8_t>& bytes)
+{
+	bytes.resize(in->length());
+	if (!bytes.empty()) {
+		in->copyout(&bytes[0], bytes.size());
+		in->skip(bytes.size());
+	}
+}
+
+}  // namespace
+
+DeflatePipe::DeflatePipe(int level)
+: PipeProducer("/zlib/deflate_pipe", &mtx_),
+  mtx_("DeflatePipe"),
+  stream_()
+{
+	DeflatePool *p = deflate_pool(level);
+	if (p == NULL || p->free_slots.empty())
+		HALT(log_) << "Could not initialize deflate stream (MI355X engine: levels 4-9, "
+			   << XCGPU_ZLIB_SLOTS << " pipes).";
+	uint32_t slot = p->free_slots.back();
+	p->free_slots.pop_back();
+	if (xcg_zdeflate_reset(p->ctx, slot) != XCG_OK)
+		HALT(log_) << "Could not initialize deflate stream.";
+	p->slot_of[this] = slot;
+	deflate_levels()[this] = level;
+}
+
+DeflatePipe::~DeflatePipe()
+{
+	int level = deflate_levels()[this];
+	DeflatePool *p = deflate_pool(level);
+	p->free_slots.push_back(p->slot_of[this]);
+	p->slot_of.erase(this);
+	deflate_levels().erase(this);
+}
+
+void
+DeflatePipe::consume(Buffer *in)
+{
+	DeflatePool *p = deflate_pool(deflate_levels()[this]);
+	uint32_t slot = p->slot_of[this];
+	std::vector<uint8_t> bytes;
+	take_all(in, bytes);
+	uint32_t len = bytes.size();
+	uint64_t in_off = 0, out_off = 0;
+	uint32_t out_len = 0;
+	std::vector<uint8_t> obuf(xcg_zdeflate_bound(len));
+	int rc = xcg_zdeflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1, &obuf[0], &out_off,
+				   &out_len);
+	if (rc != XCG_OK)
+		HALT(log_) << "xcgpu deflate: " << xcg_strerror(rc);
+	Buffer out;
+	out.append(&obuf[0], out_len);
+	if (len == 0) {			/* Z_FINISH */
+		produce_eos(&out);
+		return;
+	}
+	if (!out.empty())
+		produce(&out);
+}
+
+InflatePipe::InflatePipe(void)
+: PipeProducer("/zlib/inflate_pipe", &mtx_),
+  mtx_("InflatePipe"),
+  stream_()
+{
+	InflatePool *p = inflate_pool();
+	if (p == NULL || p->free_slots.empty())
+		HALT(log_) << "Could not initialize inflate stream.";
+	uint32_t slot = p->free_slots.back();
+	p->free_slots.pop_back();
+	p->slot_of[this] = slot;
+}
+
+InflatePipe::~InflatePipe()
+{
+	InflatePool *p = inflate_pool();
+	p->free_slots.push_back(p->slot_of[this]);
+	p->slot_of.erase(this);
+}
+
+void
+InflatePipe::consume(Buffer *in)
+{
+	InflatePool *p = inflate_pool();
+	uint32_t slot = p->slot_of[this];
+	std::vector<uint8_t> bytes;
+	take_all(in, bytes);
+	uint32_t len = bytes.size();
+	uint64_t in_off = 0, out_off = 0;
+	uint32_t cap = 8 * len + 65536, out_len = 0;
+	int32_t status = 0;
+	std::vector<uint8_t> obuf;
+	for (;;) {		/* -2: more output room, nothing was committed */
+		obuf.resize(cap);
+		int rc = xcg_zinflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1, &obuf[0],
+					   &out_off, &cap, &out_len, &status);
+		if (rc != XCG_OK)
+			HALT(log_) << "xcgpu inflate: " << xcg_strerror(rc);
+		if (status != -2)
+			break;
+		cap *= 4;
+	}
+	if (status == -1) {
+		ERROR(log_) << "inflate(): data error";
+		produce_error();
+		return;
+	}
+	Buffer out;
+	if (out_len)
+		out.append(&obuf[0], out_len);
+	if (len == 0 && status == 1) {	/* Z_FINISH after the stream's end */
+		produce_eos(&out);
+		return;
+	}
+	if (!out.empty())
+		produce(&out);
+}

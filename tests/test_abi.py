@@ -48,3 +48,17 @@ def test_no_cpu_fallback_without_gpu():
     from wanproxy_amd.xcgpu import Context, XCGError
     with pytest.raises(XCGError):
         Context(0)
+
+
+def test_zlib_adapter_compiles_against_reference_headers():
+    """integration/zlib_pipes_xcgpu.cc defines DeflatePipe / InflatePipe with
+    the reference's headers unchanged (zlib/deflate_pipe.h, inflate_pipe.h)."""
+    import shutil
+    import subprocess
+    ref = '/root/reference'
+    if not os.path.exists(os.path.join(ref, 'zlib/deflate_pipe.h')) or not shutil.which('g++'):
+        pytest.skip('reference tree absent (GPU box)')
+    r = subprocess.run(['g++', '-std=c++11', '-fsyntax-only', '-Wall', '-Wno-deprecated', f'-I{ref}', '-include',
+                        'common/common.h', os.path.join(ROOT, 'integration/zlib_pipes_xcgpu.cc')],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -1221,7 +1221,7 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
   }
   if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
   if (!rc) rc = xcg_zdeflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), d_len, nullptr);
-  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = XCG_EHIP;
+  if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
   if (!rc && hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
   for (uint32_t i = 0; !rc && i < n; i++)
     if (hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;

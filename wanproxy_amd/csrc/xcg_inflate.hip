@@ -673,4 +673,41 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   return XCG_OK;
 }
 
+// Host buffers, synchronous: inputs at h_in + h_in_off[i], outputs to h_out +
+// h_out_off[i] (room h_out_cap[i]); lengths and statuses to host arrays.
+int xcg_zinflate_host(xcg_zinflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                      const uint32_t* h_stream, uint32_t n, uint8_t* h_out, const uint64_t* h_out_off,
+                      const uint32_t* h_out_cap, uint32_t* h_out_len, int32_t* h_status) {
+  if (!z || n == 0) return XCG_EINVAL;
+  (void)hipSetDevice(z->device);
+  uint64_t in_end = 0, out_end = 0;
+  std::vector<uint64_t> doff(n);
+  for (uint32_t i = 0; i < n; i++) {
+    in_end = std::max(in_end, h_in_off[i] + h_len[i]);
+    doff[i] = out_end;
+    out_end += ial(h_out_cap[i] ? h_out_cap[i] : 1, 4);
+  }
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  uint32_t* d_len = nullptr;
+  int32_t* d_st = nullptr;
+  int rc = XCG_OK;
+  if (hipMalloc(&d_in, in_end + 1) != hipSuccess || hipMalloc(&d_out, out_end) != hipSuccess ||
+      hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_st, 4ull * n) != hipSuccess)
+    rc = XCG_ENOMEM;
+  if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
+  if (!rc) rc = xcg_zinflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), h_out_cap, d_len, d_st, nullptr);
+  if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
+  if (!rc && (hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(h_status, d_st, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = XCG_EHIP;
+  for (uint32_t i = 0; !rc && i < n; i++)
+    if (h_out_len[i] && hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess)
+      rc = XCG_EHIP;
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  (void)hipFree(d_len);
+  (void)hipFree(d_st);
+  return rc;
+}
+
 }  // extern "C"
