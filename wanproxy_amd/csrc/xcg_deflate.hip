@@ -207,54 +207,78 @@ __device__ __forceinline__ uint32_t hash3(const uint8_t* X, int64_t j) {   // UP
 // occurrence is the nearest lower lane with its hash (lanes with an equal hash
 // found by 15 ballots, one per hash bit), else the LDS head table; the last
 // lane of each hash then becomes the head.  The head table keeps the low 16
-// bits of positions (64 KiB: two waves per CU); an entry's age is
-// (j - v) mod 2^16, valid for 1..32767 (farther links are 0 anyway), and every
-// 16384 positions entries older than 32767 are expired, so no age ever wraps.
+// bits of positions (64 KiB); an entry's age is (j - v) mod 2^16, valid for
+// 1..32767 (farther links are 0 anyway), and every 16384 positions entries
+// older than 32767 are expired, so no age ever wraps.  The call's bytes are
+// staged into LDS and the links collected there, 4096 positions at a time:
+// the group loop touches LDS only (on gfx9 a wait for a global load also
+// waits for every earlier global store, which otherwise stalls every group).
+constexpr int CTILE = 4096;
 __global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
   __shared__ uint16_t head[32768];
+  __shared__ uint32_t xs[CTILE / 4 + 2];     // X[t0 .. t0 + CTILE + 8)
+  __shared__ uint16_t ls[CTILE];              // links of the tile
   const ZCall c = a.calls[blockIdx.x];
   const ZState s = a.st[c.stream];
   const int lane = threadIdx.x;
   const uint8_t* X = a.X + c.x_off;
   uint16_t* d16 = a.d16 + c.x_off;
-  // first valid position: max(base, total - WSIZE) as an X index
-  int64_t jlo = (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
+  // first valid position: max(base, total - WSIZE) as an X index, rounded down to a word
+  const int64_t jlo = (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
   const uint16_t empty = (uint16_t)(jlo + 32768);   // age >= 32768 until jlo + 32768
   for (int i = lane; i < 32768; i += 64) head[i] = empty;
-  int64_t jend = (int64_t)WSIZE + c.len;     // positions q with q + 2 < jend get a hash
+  const int64_t jend = (int64_t)WSIZE + c.len;     // positions q with q + 2 < jend get a hash
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // X words for the next group are loaded one group ahead (X has XPAD bytes after the data)
-  uint32_t wcur = ld32(X + jlo + lane);
-  for (int64_t g = jlo; g < jend; g += 64) {
-    const uint32_t wnext = g + 64 < jend ? ld32(X + g + 64 + lane) : 0u;
-    if (((g - jlo) & 16383) == 0 && g != jlo) {   // expire entries older than 32767
-      const uint16_t far = (uint16_t)(g + 32768);
-      for (int i = lane; i < 32768; i += 64) {
-        uint16_t v = head[i];
-        if ((uint16_t)(g - v) > 32767) head[i] = far;
+  const int64_t t_first = jlo & ~3ll;
+  int64_t next_expiry = jlo + 16384;
+  for (int64_t t0 = t_first; t0 < jend; t0 += CTILE) {
+    // stage X[t0 .. t0 + CTILE + 8) (X has XPAD zero bytes past the data)
+    const uint32_t* xw = (const uint32_t*)(X + t0);
+    for (int i = lane; i < CTILE / 4 + 2; i += 64) xs[i] = xw[i];
+    __syncthreads();
+    const int64_t t1 = t0 + CTILE < jend ? t0 + CTILE : jend;
+    const int64_t gstart = t0 > jlo ? t0 : jlo;
+    for (int64_t g = gstart; g < t1; g += 64) {
+      if (g >= next_expiry) {   // every 16384 positions: expire entries older than 32767
+        next_expiry += 16384;
+        const uint16_t far = (uint16_t)(g + 32768);
+        for (int i = lane; i < 32768; i += 64) {
+          uint16_t v = head[i];
+          if ((uint16_t)(g - v) > 32767) head[i] = far;
+        }
       }
-    }
-    int64_t j = g + lane;
-    bool valid = j + 2 < jend;
-    // UPDATE_HASH x3 (hash_shift 5) over bytes j, j+1, j+2; invalid lanes form their own class
-    uint32_t h = valid ? (((wcur & 0xff) << 10) ^ (((wcur >> 8) & 0xff) << 5) ^ ((wcur >> 16) & 0xff)) & 0x7fffu : 0x8000u;
-    wcur = wnext;
-    uint64_t m = ballot(valid);
+      const int64_t j = g + lane;
+      const bool in_tile = j < t1;
+      const bool valid = in_tile && j + 2 < jend;
+      const uint32_t o = (uint32_t)(j - t0);           // byte offset in the stage
+      uint32_t h = 0x8000u;                            // invalid lanes form their own class
+      if (valid) {
+        uint32_t lo = xs[o >> 2], hi = xs[(o >> 2) + 1];
+        uint32_t w = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (o & 3)));
+        // UPDATE_HASH x3 (hash_shift 5) over bytes j, j+1, j+2
+        h = (((w & 0xff) << 10) ^ (((w >> 8) & 0xff) << 5) ^ ((w >> 16) & 0xff)) & 0x7fffu;
+      }
+      uint64_t m = ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 15; b++) {
-      bool bit = (h >> b) & 1;
-      uint64_t bl = ballot(bit);
-      m &= bit ? bl : ~bl;
+      for (int b = 0; b < 15; b++) {
+        bool bit = (h >> b) & 1;
+        uint64_t bl = ballot(bit);
+        m &= bit ? bl : ~bl;
+      }
+      const uint64_t lower = m & below;
+      const bool last = (m >> lane) == 1ull;
+      int32_t age = 0;
+      if (valid) {
+        if (lower) age = lane - (63 - __clzll(lower));
+        else age = (uint16_t)((uint16_t)j - head[h]);
+      }
+      if (in_tile) ls[j - t0] = (age > 0 && age <= 32767) ? (uint16_t)age : 0;
+      if (valid && last) head[h] = (uint16_t)j;
     }
-    uint64_t lower = m & below;
-    bool last = (m >> lane) == 1ull;
-    int32_t age = 0;
-    if (valid) {
-      if (lower) age = lane - (63 - __clzll(lower));
-      else age = (uint16_t)((uint16_t)j - head[h]);
-    }
-    if (j < jend) d16[j] = (age > 0 && age <= 32767) ? (uint16_t)age : 0;
-    if (valid && last) head[h] = (uint16_t)j;
+    __syncthreads();
+    // the tile's links to HBM (positions [gstart, t1))
+    for (int64_t q = gstart + lane; q < t1; q += 64) d16[q] = ls[q - t0];
+    __syncthreads();
   }
 }
 
