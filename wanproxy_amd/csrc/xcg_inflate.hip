@@ -96,15 +96,24 @@ __global__ __launch_bounds__(256) void zi_prep_kernel(IArgs a) {
   }
 }
 
-struct Tree {
-  uint16_t pri[1 << PRI];   // (sym << 4) | len; 0: a code longer than PRI bits
+template <int B, int NS>
+struct TreeT {
+  static constexpr int BITS = B;
+  uint16_t pri[1 << B];     // (sym << 4) | len; 0: a code longer than B bits
   uint16_t cnt[16];
-  uint16_t sym[320];        // symbols in canonical order (by length, then value)
+  uint16_t sym[NS];         // symbols in canonical order (by length, then value)
 };
+// literal/length codes of skewed blocks run to 10-12 bits: an 11-bit primary
+// table keeps them off the canonical path; ~39 KiB of LDS in all (4 waves/CU)
+typedef TreeT<11, 288> LTree;
+typedef TreeT<PRI, 32> DTree;
+typedef TreeT<7, 20> CTree;
 
 struct Lds {
   uint8_t ring[RMASK + 1];
-  Tree lt, dt, ct;          // literal/length, distance, code-length trees
+  LTree lt;
+  DTree dt;
+  CTree ct;                 // literal/length, distance, code-length trees
   uint8_t lens[320];        // fixed / code-length tree lengths
   uint8_t dlens[320];       // the dynamic block's literal/length + distance lengths
   uint16_t codes[320];
@@ -113,9 +122,11 @@ struct Lds {
 
 // Canonical decoder from code lengths (inflate_table's rules: over-subscribed
 // sets are errors, incomplete ones too unless the only code has length 1).
+template <class Tree>
 __device__ bool build(Lds& L, Tree& T, const uint8_t* lens, int n) {
+  constexpr int PB = Tree::BITS;
   const int lane = threadIdx.x;
-  for (int i = lane; i < (1 << PRI); i += 64) T.pri[i] = 0;
+  for (int i = lane; i < (1 << PB); i += 64) T.pri[i] = 0;
   if (lane == 0) {
     for (int l = 0; l < 16; l++) T.cnt[l] = 0;
     for (int i = 0; i < n; i++) T.cnt[lens[i]]++;
@@ -147,9 +158,9 @@ __device__ bool build(Lds& L, Tree& T, const uint8_t* lens, int n) {
   __syncthreads();
   for (int i = lane; i < n; i += 64) {
     int l = lens[i];
-    if (!l || l > PRI) continue;
+    if (!l || l > PB) continue;
     uint32_t r = __brev((uint32_t)L.codes[i]) >> (32 - l);
-    for (uint32_t k = r; k < (1u << PRI); k += 1u << l) T.pri[k] = (uint16_t)((i << 4) | l);
+    for (uint32_t k = r; k < (1u << PB); k += 1u << l) T.pri[k] = (uint16_t)((i << 4) | l);
   }
   __syncthreads();
   return L.ok;
@@ -183,11 +194,15 @@ struct Reader {
 __device__ __forceinline__ uint32_t su(uint32_t v) { return readfirst(v); }
 
 // the primary-table entry for the bits in v ((sym << 4) | len; len 0: longer code)
-__device__ __forceinline__ uint32_t decode_pri(const Tree& T, uint64_t v) { return su(T.pri[v & ((1u << PRI) - 1)]); }
+template <class Tree>
+__device__ __forceinline__ uint32_t decode_pri(const Tree& T, uint64_t v) {
+  return su(T.pri[v & ((1u << Tree::BITS) - 1)]);
+}
 
 // Huffman decode of the bits in v: returns (sym << 4) | len, 0 if no code matches
+template <class Tree>
 __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
-  uint32_t e = su(T.pri[v & ((1u << PRI) - 1)]);
+  uint32_t e = su(T.pri[v & ((1u << Tree::BITS) - 1)]);
   if (e & 15) return e;
   int code = 0, first = 0, index = 0;
   for (int l = 1; l < 16; l++) {
@@ -201,7 +216,27 @@ __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
   return 0;
 }
 
+#ifdef XCG_ZI_TIMING
+// diagnostics build: cycles per phase, summed over calls (setup, fast literals,
+// fast matches, careful path, flushes, stored copies, tail) and symbol counts
+__device__ unsigned long long g_zi_t[10];
+#define ZT_NOW() __builtin_readcyclecounter()
+#define ZT_ADD(i, t0)                                                         \
+  do {                                                                        \
+    uint64_t t1_ = ZT_NOW();                                                  \
+    if (threadIdx.x == 0) zt[i] += t1_ - (t0);                                \
+    t0 = t1_;                                                                 \
+  } while (0)
+#else
+#define ZT_NOW() 0ull
+#define ZT_ADD(i, t0) (void)(t0)
+#endif
+
 __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
+#ifdef XCG_ZI_TIMING
+  uint64_t zt[10] = {0};
+#endif
+  uint64_t tz = ZT_NOW();
   __shared__ Lds L;
   const uint32_t ci = blockIdx.x;
   const ICall c = a.calls[ci];
@@ -245,6 +280,7 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
     ok = build(L, L.dt, L.dlens + nlen, ndist) && ok;
     return ok;
   };
+  ZT_ADD(0, tz);
   if (mode == M_HUFF) {   // resume inside a block: rebuild its trees
     for (int i = lane; i < 320; i += 64) L.dlens[i] = sp->lens[i];
     __syncthreads();
@@ -352,55 +388,73 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
         if (pos - flushed >= 16384) flush();
       }
       q += 8 * n;
+      ZT_ADD(5, tz);
       stored_left -= (uint32_t)n;
       if (stored_left) { stall = true; break; }
       mode = last ? M_TRAILER : M_BLOCK;
       R.load(q >> 3);
     } else if (mode == M_HUFF) {
       for (;;) {
-        // fast path (as zlib's inflate_fast): while any symbol pair fits in the
-        // input, the output room and the ring before its next flush, decode
-        // without per-field checks, two literals per bit fetch
-        while (q + 128 <= qend && pos - flushed < 16000 && pos + 516 - total0 <= c.out_cap) {
-          uint64_t v = R.get(q);
-          uint32_t e = decode_pri(L.lt, v);
-          uint32_t l1 = e & 15, sym = e >> 4;
-          if (!l1) break;   // a long code: the careful path
-          if (sym < 256) {
-            uint32_t e2 = decode_pri(L.lt, v >> l1);
-            if (lane == 0) L.ring[pos & RMASK] = (uint8_t)sym;
-            pos++;
-            q += l1;
-            uint32_t l2 = e2 & 15;
-            if (l2 && (e2 >> 4) < 256) {
-              if (lane == 0) L.ring[pos & RMASK] = (uint8_t)(e2 >> 4);
+        // fast path (as zlib's inflate_fast): while 128 input bits, 516 bytes of
+        // output room and the ring before its next flush are guaranteed, decode
+        // without per-field checks; literals straight from a 64-bit bit buffer
+        // (one window fetch per run of literals)
+        {
+          const uint64_t qlim = qend > 128 ? qend - 128 : 0;
+          const uint64_t pcap = total0 + c.out_cap > 516 ? total0 + c.out_cap - 516 : 0;
+          while (q < qlim) {
+            const uint64_t plim = flushed + 16000 < pcap ? flushed + 16000 : pcap;
+            if (pos >= plim) break;
+            uint64_t v = R.get(q);
+            int vb = 64;
+            uint32_t e = 0;
+            ZT_ADD(3, tz);
+            for (;;) {   // literals while the buffer surely holds a primary code
+              e = decode_pri(L.lt, v);
+              if ((e & 15) == 0 || (e >> 4) >= 256 || vb < LTree::BITS || pos >= plim) break;
+              if (lane == 0) L.ring[pos & RMASK] = (uint8_t)(e >> 4);
+              const uint32_t l1 = e & 15;
               pos++;
-              q += l2;
+              v >>= l1;
+              vb -= (int)l1;
+              q += l1;
             }
-            continue;
+            ZT_ADD(1, tz);
+            if (pos >= plim) break;
+            if (vb < LTree::BITS) continue;                // refill
+            const uint32_t l1 = e & 15, sym = e >> 4;
+            if (!l1 || sym == 256 || sym > 285) break;     // long code / end of block: the careful path
+            const uint64_t vv = R.get(q);
+            const uint32_t li = sym - 257, xl = LEXT[li];
+            const uint32_t length = LBASE[li] + ((uint32_t)(vv >> l1) & ((1u << xl) - 1));
+            const uint64_t qd = q + l1 + xl;
+            const uint64_t vd = R.get(qd);
+            const uint32_t ed = decode_pri(L.dt, vd);
+            const uint32_t l2 = ed & 15, dsym = ed >> 4;
+            if (!l2 || dsym > 29) break;
+            const uint32_t xd = DEXT[dsym];
+            const uint32_t dist = DBASE[dsym] + ((uint32_t)(vd >> l2) & ((1u << xd) - 1));
+            if (dist > pos || dist > (uint32_t)WSIZE) break;
+            // One wave: its LDS accesses are ordered, and every byte read lies
+            // before pos, so no barrier is needed around the copy.
+            if (dist >= length) {
+              for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
+            } else {   // overlapping: byte i repeats source byte i mod dist
+              uint32_t r = lane % dist;
+              const uint32_t step = 64 % dist;
+              for (uint32_t i = lane; i < length; i += 64) {
+                L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + r) & RMASK];
+                r += step;
+                if (r >= dist) r -= dist;
+              }
+            }
+            pos += length;
+            q = qd + l2 + xd;
+            ZT_ADD(2, tz);
           }
-          if (sym == 256 || sym > 285) break;
-          uint32_t li = sym - 257, xl = LEXT[li];
-          uint32_t length = LBASE[li] + ((uint32_t)(v >> l1) & ((1u << xl) - 1));
-          uint64_t qd = q + l1 + xl;
-          uint64_t vd = R.get(qd);
-          uint32_t ed = decode_pri(L.dt, vd);
-          uint32_t l2 = ed & 15, dsym = ed >> 4;
-          if (!l2 || dsym > 29) break;
-          uint32_t xd = DEXT[dsym];
-          uint32_t dist = DBASE[dsym] + ((uint32_t)(vd >> l2) & ((1u << xd) - 1));
-          if (dist > pos || dist > (uint32_t)WSIZE) break;
-          __syncthreads();
-          if (dist >= length) {
-            for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
-          } else {
-            for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + (i % dist)) & RMASK];
-          }
-          __syncthreads();
-          pos += length;
-          q = qd + l2 + xd;
         }
-        if (pos - flushed >= 16384) flush();
+        ZT_ADD(3, tz);
+        if (pos - flushed >= 16000) { flush(); ZT_ADD(4, tz); }   // (the fast path's limit)
         uint64_t v = R.get(q);
         uint32_t e = decode(L.lt, v);
         uint32_t l1 = e & 15, sym = e >> 4;
@@ -455,6 +509,7 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
       mode = M_DONE;
     }
   }
+  ZT_ADD(3, tz);
   if (status == 0 && mode == M_ERROR) status = -1;
   // InflatePipe: bytes after the stream's end are an error ("Stream ended but more data follows")
   if (status == 0 && mode == M_DONE && q < qend && c.len) status = -1;
@@ -487,6 +542,11 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
       }
     }
   }
+  ZT_ADD(6, tz);
+#ifdef XCG_ZI_TIMING
+  if (lane == 0)
+    for (int i = 0; i < 7; i++) atomicAdd(&g_zi_t[i], (unsigned long long)zt[i]);
+#endif
   if (lane == 0) {
     IRes r;
     r.out_len = (uint32_t)(pos - total0);
@@ -709,5 +769,13 @@ int xcg_zinflate_host(xcg_zinflate* z, const uint8_t* h_in, const uint64_t* h_in
   (void)hipFree(d_st);
   return rc;
 }
+
+#ifdef XCG_ZI_TIMING
+int xcg_debug_zi_times(uint64_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zi_t), 8 * 10) != hipSuccess) return XCG_EHIP;
+  uint64_t z[10] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_zi_t), z, sizeof z) == hipSuccess ? XCG_OK : XCG_EHIP;
+}
+#endif
 
 }  // extern "C"
