@@ -198,10 +198,6 @@ __global__ __launch_bounds__(64) void zd_adler_kernel(ZArgs a) {
 
 // ------------------------------------------------------------------- chains
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *(const u32_u*)p; }
-__device__ __forceinline__ uint32_t hash3(const uint8_t* X, int64_t j) {   // UPDATE_HASH x3 (hash_shift 5)
-  uint32_t w = ld32(X + j);
-  return (((w & 0xff) << 10) ^ (((w >> 8) & 0xff) << 5) ^ ((w >> 16) & 0xff)) & 0x7fffu;
-}
 
 // One wave per call, positions in order in groups of 64.  A lane's previous
 // occurrence is the nearest lower lane with its hash (lanes with an equal hash
@@ -414,9 +410,21 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
     nsym = 0;
     block_start = q;
   };
+  // Symbols are staged in LDS and written out 2048 at a time (coalesced): a
+  // store per symbol would make every window load wait for all earlier
+  // stores (gfx9 counts both in vmcnt).
+  __shared__ uint32_t sbuf[2048 + 64];
+  uint32_t sb_n = 0, sb_base = 0;
+  auto sflush = [&]() {
+    for (uint32_t i = lane; i < sb_n; i += 64) sym[sb_base + i] = sbuf[i];
+    sb_base += sb_n;
+    sb_n = 0;
+  };
   auto put = [&](uint32_t v) {
-    if (lane == 0) sym[symbase + nsym] = v;
+    if (lane == 0) sbuf[sb_n] = v;
+    sb_n++;
     nsym++;
+    if (sb_n >= 2048) sflush();
   };
 
   for (;;) {
@@ -459,8 +467,10 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
         int64_t stop = m ? w + (int64_t)__builtin_ctzll(m) : lim;
         int64_t k = stop - p;
         if (k > 0) {
-          if (lane >= li && lane < li + k) sym[symbase + nsym + (lane - li)] = W.x;
+          if (lane >= li && lane < li + k) sbuf[sb_n + (lane - li)] = W.x;
+          sb_n += (uint32_t)k;
           nsym += (uint32_t)k;
+          if (sb_n >= 2048) sflush();
           p = stop;
           if (nsym == SYMS_PER_BLOCK) flush(p - 1, false);
           continue;
@@ -501,6 +511,7 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
     }
   }
   if (avail) put(a.X[c.x_off + p - 1]);
+  sflush();
   if (finish) flush(p, true);
   else if (nsym) flush(p, false);
   if (lane == 0) {
