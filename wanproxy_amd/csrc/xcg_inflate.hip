@@ -4,12 +4,13 @@
 // byte the input so far lets inflate() produce.  gfx950, wave64.
 //
 // One wave per call; the decoder's control state is wave-uniform (every lane
-// runs it, values come from readlane), lanes split the byte copies.  The
-// stream's last 32 KiB of output live in a 32 KiB LDS ring, so a match copies
-// LDS -> LDS (the modular source index handles overlapping copies); output is
-// flushed to the caller's buffer every 16 KiB, so a slot is rewritten only
-// after its byte was flushed and left the window (~39 KiB of LDS: four waves
-// per CU).  Input bits come from a 256-byte register window.  Huffman
+// runs it, values come from readlane), lanes split the byte copies.  The last
+// 8 KiB of output live in an LDS ring: a match up to 4 KiB back copies LDS ->
+// LDS (the modular source index handles overlapping copies); a farther one
+// reads HBM -- this call's output, flushed to the caller's buffer every 2 KiB
+// (a fence after each flush makes it readable), or the stream's 32 KiB history.
+// ~16 KiB of LDS per stream: ten streams per CU, where a 32 KiB window ring
+// allowed four, and the serial decode is latency-bound per stream.  Input bits come from a 256-byte register window.  Huffman
 // decoding: a 512-entry primary table per tree in LDS, longer codes by
 // canonical decoding; the decoder's wave-uniform control runs on the SALU.  Every field is read under a bounds check; when the
 // input ends inside a symbol or a block header, the call stops at the symbol /
@@ -31,7 +32,9 @@ namespace xcg {
 namespace zi {
 
 constexpr int WSIZE = 32768;
-constexpr uint32_t RMASK = 32767;   // LDS ring of 32 KiB: the deflate window
+constexpr uint32_t RMASK = 8191;    // LDS ring of the last 8 KiB of output
+constexpr uint32_t NEAR = 4096;     // matches up to this distance copy inside the ring
+constexpr uint32_t FLUSH_AT = 2048; // output is flushed to HBM every 2 KiB
 constexpr int PEND_CAP = 1024;
 constexpr int PRI = 9;              // primary table bits
 constexpr int IPAD = 512;           // zero bytes after a call's input in the scratch
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
   R.load(0);
   // history -> ring
   const uint8_t* hist = a.hist + (uint64_t)c.stream * WSIZE;
-  const uint64_t hn = total0 < (uint64_t)WSIZE ? total0 : (uint64_t)WSIZE;
+  const uint64_t hn = total0 < (uint64_t)(RMASK + 1) ? total0 : (uint64_t)(RMASK + 1);
   for (uint64_t i = lane; i < hn; i += 64) {
     uint64_t pos = total0 - hn + i;
     L.ring[pos & RMASK] = hist[WSIZE - hn + i];
@@ -265,6 +268,26 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
     __syncthreads();
     for (uint64_t p = flushed + lane; p < pos; p += 64) out[p - total0] = L.ring[p & RMASK];
     flushed = pos;
+    __threadfence();   // the flushed bytes are read back by far matches
+  };
+  // a match of `length` bytes from `dist` back, at pos
+  auto copy_match = [&](uint32_t dist, uint32_t length) {
+    if (dist >= length && dist <= NEAR) {
+      for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
+    } else if (dist <= NEAR) {   // overlapping: byte i repeats source byte i mod dist
+      uint32_t r = lane % dist;
+      const uint32_t step = 64 % dist;
+      for (uint32_t i = lane; i < length; i += 64) {
+        L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + r) & RMASK];
+        r += step;
+        if (r >= dist) r -= dist;
+      }
+    } else {                     // far: every source byte is in HBM already (pos - dist + 258 < flushed)
+      for (uint32_t i = lane; i < length; i += 64) {
+        const uint64_t x = pos - dist + i;
+        L.ring[(pos + i) & RMASK] = x >= total0 ? out[x - total0] : hist[WSIZE - (total0 - x)];
+      }
+    }
   };
   auto tables_for_block = [&]() -> bool {   // (re)build the block's trees
     if (btype == 1) {
@@ -376,17 +399,18 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
       uint64_t avail = (qend - q) >> 3;   // q is byte aligned here
       uint64_t n = stored_left < avail ? stored_left : avail;
       if (pos + n - total0 > c.out_cap) { status = -2; break; }
-      // through the ring (history for later matches), flushing as it fills
-      uint64_t done = 0;
-      while (done < n) {
-        uint64_t chunk = n - done;
-        if (chunk > 8192) chunk = 8192;
-        __syncthreads();
-        for (uint64_t i = lane; i < chunk; i += 64) L.ring[(pos + i) & RMASK] = R.I[(q >> 3) + done + i];
-        pos += chunk;
-        done += chunk;
-        if (pos - flushed >= 16384) flush();
-      }
+      // straight to the output (HBM), the ring's earlier bytes flushed first;
+      // then the last 8 KiB also into the ring for later near matches
+      flush();
+      const uint8_t* src = R.I + (q >> 3);
+      uint8_t* dst = out + (pos - total0);
+      for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+      const uint64_t keep = n < (uint64_t)(RMASK + 1) ? n : (uint64_t)(RMASK + 1);
+      for (uint64_t i = lane; i < keep; i += 64) L.ring[(pos + n - keep + i) & RMASK] = src[n - keep + i];
+      pos += n;
+      flushed = pos;
+      __threadfence();   // readable by far matches
+      __syncthreads();
       q += 8 * n;
       ZT_ADD(5, tz);
       stored_left -= (uint32_t)n;
@@ -403,7 +427,7 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
           const uint64_t qlim = qend > 128 ? qend - 128 : 0;
           const uint64_t pcap = total0 + c.out_cap > 516 ? total0 + c.out_cap - 516 : 0;
           while (q < qlim) {
-            const uint64_t plim = flushed + 16000 < pcap ? flushed + 16000 : pcap;
+            const uint64_t plim = flushed + FLUSH_AT < pcap ? flushed + FLUSH_AT : pcap;
             if (pos >= plim) break;
             uint64_t v = R.get(q);
             int vb = 64;
@@ -437,24 +461,14 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
             if (dist > pos || dist > (uint32_t)WSIZE) break;
             // One wave: its LDS accesses are ordered, and every byte read lies
             // before pos, so no barrier is needed around the copy.
-            if (dist >= length) {
-              for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
-            } else {   // overlapping: byte i repeats source byte i mod dist
-              uint32_t r = lane % dist;
-              const uint32_t step = 64 % dist;
-              for (uint32_t i = lane; i < length; i += 64) {
-                L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + r) & RMASK];
-                r += step;
-                if (r >= dist) r -= dist;
-              }
-            }
+            copy_match(dist, length);
             pos += length;
             q = qd + l2 + xd;
             ZT_ADD(2, tz);
           }
         }
         ZT_ADD(3, tz);
-        if (pos - flushed >= 16000) { flush(); ZT_ADD(4, tz); }   // (the fast path's limit)
+        if (pos - flushed >= FLUSH_AT) { flush(); ZT_ADD(4, tz); }   // (the fast path's limit)
         uint64_t v = R.get(q);
         uint32_t e = decode(L.lt, v);
         uint32_t l1 = e & 15, sym = e >> 4;
@@ -488,11 +502,7 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
         if (dist > pos || dist > (uint32_t)WSIZE) { mode = M_ERROR; break; }   // too far back
         if (pos + length - total0 > c.out_cap) { status = -2; break; }
         __syncthreads();
-        if (dist >= length) {
-          for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + i) & RMASK];
-        } else {   // overlapping: byte i repeats byte i mod dist of the source
-          for (uint32_t i = lane; i < length; i += 64) L.ring[(pos + i) & RMASK] = L.ring[(pos - dist + (i % dist)) & RMASK];
-        }
+        copy_match(dist, length);
         __syncthreads();
         pos += length;
         q = qd + l2 + xd;
@@ -525,10 +535,22 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
     if (np > PEND_CAP) status = -1;
     else {
       for (uint64_t i = lane; i < np; i += 64) sp->pend[i] = R.I[qb + i];
-      // history = the last 32 KiB of output
-      uint64_t hn2 = pos < (uint64_t)WSIZE ? pos : (uint64_t)WSIZE;
+      // history = the last 32 KiB of output: the old history moved down by this
+      // call's output length (ascending, so no lane reads what another wrote),
+      // then the output itself (flushed and fenced above)
+      const uint64_t ol = pos - total0;
       uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
-      for (uint64_t i = lane; i < hn2; i += 64) h[WSIZE - hn2 + i] = L.ring[(pos - hn2 + i) & RMASK];
+      if (ol < (uint64_t)WSIZE) {
+        for (uint64_t i0 = 0; ol && i0 < WSIZE - ol; i0 += 64) {
+          const uint64_t i = i0 + lane;
+          const uint8_t b = i < WSIZE - ol ? h[i + ol] : 0;
+          __syncthreads();
+          if (i < WSIZE - ol) h[i] = b;
+        }
+        for (uint64_t i = lane; i < ol; i += 64) h[WSIZE - ol + i] = out[i];
+      } else {
+        for (uint64_t i = lane; i < (uint64_t)WSIZE; i += 64) h[i] = out[ol - WSIZE + i];
+      }
       if (lane == 0) {
         sp->total_out = pos;
         sp->mode = mode;
