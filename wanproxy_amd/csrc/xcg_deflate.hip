@@ -134,6 +134,7 @@ struct ZArgs {
   uint8_t* out;
   uint8_t* X;
   uint16_t* d16;
+  uint32_t* pk;          // packed hashes (zd_hashes_kernel), indexed like X
   uint32_t* tf;
   uint32_t* tq;
   uint32_t* sym;
@@ -141,8 +142,10 @@ struct ZArgs {
   uint32_t* tabs;        // blk index * TAB_WORDS
   ZCallRes* res;
   uint32_t* out_len;     // caller's d_out_len
-  const uint32_t* tile_call;   // zd_match_kernel: call of each 256-position tile
-  const uint32_t* tile_pos;    // and its first call-relative position
+  uint32_t n;                  // calls
+  const uint32_t* mstart;      // first 256-position match tile of each call (n + 1, prefix)
+  const uint32_t* gstart;      // first 64-position hash group of each call (n + 1, prefix)
+  const uint32_t* bstart;      // first block record of each call (n + 1, prefix)
   int level;
 };
 
@@ -199,82 +202,156 @@ __global__ __launch_bounds__(64) void zd_adler_kernel(ZArgs a) {
 // ------------------------------------------------------------------- chains
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *(const u32_u*)p; }
 
-// One wave per call, positions in order in groups of 64.  A lane's previous
-// occurrence is the nearest lower lane with its hash (lanes with an equal hash
-// found by 15 ballots, one per hash bit), else the LDS head table; the last
-// lane of each hash then becomes the head.  The head table keeps the low 16
+// Hash-chain links in two passes.  Groups of 64 consecutive positions start at
+// the call's first valid position jlo (max(base, total - WSIZE) as an X index).
+//
+// zd_hashes_kernel (every group of every call in parallel): a position's 3-byte
+// hash (UPDATE_HASH x3, hash_shift 5) and its nearest lower lane with the same
+// hash inside the group (lanes with an equal hash found by 15 ballots, one per
+// hash bit), and whether it is the group's last with that hash; packed as
+// h | pred_delta << 15 | last << 21 | valid << 22.
+__device__ __forceinline__ uint32_t call_of(const uint32_t* starts, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;   // last call with starts[call] <= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (starts[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int64_t first_valid(const ZState& s) {
+  return (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
+}
+// call of x in a prefix array (starts[0] = 0), searched 64 entries per step by
+// the whole wave: two dependent loads for n <= 4096 instead of a 12-step chain
+__device__ __forceinline__ uint32_t call_of_wave(const uint32_t* starts, uint32_t n, uint32_t x, int lane) {
+  uint32_t lo = 0, span = n;   // answer in [lo, lo + span), starts[lo] <= x
+  while (span > 1) {
+    const uint32_t step = (span + 63) / 64;
+    const uint32_t idx = lo + (uint32_t)lane * step;
+    const uint64_t b = ballot(idx < lo + span && starts[idx] <= x);
+    const uint32_t nlo = lo + (uint32_t)(__popcll(b) - 1) * step;
+    span = std::min(step, lo + span - nlo);
+    lo = nlo;
+  }
+  return lo;
+}
+
+constexpr uint32_t HGROUPS = 16;   // hash groups per wave (a call has > 512 groups: at most two calls)
+__global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, const uint32_t* gstart) {
+  const uint32_t g0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * HGROUPS;   // this wave's first group
+  const uint32_t total = gstart[n];
+  if (g0 >= total) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t c0 = call_of_wave(gstart, n, g0, lane);
+  const uint32_t s0 = gstart[c0], split = gstart[c0 + 1];
+  const ZCall cA = a.calls[c0];
+  const ZCall cB = (split < g0 + HGROUPS && c0 + 1 < n) ? a.calls[c0 + 1] : cA;
+  const int64_t jloA = first_valid(a.st[cA.stream]), jloB = first_valid(a.st[cB.stream]);
+  uint32_t w[HGROUPS];
+  uint64_t xo[HGROUPS];
+  int64_t jv[HGROUPS], je[HGROUPS];
+#pragma unroll
+  for (uint32_t k = 0; k < HGROUPS; k++) {   // all loads first
+    const uint32_t gid = g0 + k;
+    const bool B = gid >= split;
+    xo[k] = B ? cB.x_off : cA.x_off;
+    jv[k] = (B ? jloB : jloA) + 64ll * (gid - (B ? split : s0)) + lane;
+    je[k] = gid < total ? (int64_t)WSIZE + (B ? cB.len : cA.len) : 0;
+    w[k] = jv[k] + 2 < je[k] ? *(const u32_u*)(a.X + xo[k] + jv[k]) : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < HGROUPS; k++) {
+    const int64_t j = jv[k];
+    const bool valid = j + 2 < je[k];
+    uint32_t h = 0x8000u;    // invalid lanes form their own class
+    if (valid) h = (((w[k] & 0xff) << 10) ^ (((w[k] >> 8) & 0xff) << 5) ^ ((w[k] >> 16) & 0xff)) & 0x7fffu;
+    uint64_t m = ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 15; b++) {
+      const bool bit = (h >> b) & 1;
+      const uint64_t bl = ballot(bit);
+      m &= bit ? bl : ~bl;
+    }
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t lower = m & below;
+    const uint32_t pd = lower ? (uint32_t)(lane - (63 - __clzll(lower))) : 0u;
+    const uint32_t last = (m >> lane) == 1ull ? 1u : 0u;
+    if (j < je[k]) a.pk[xo[k] + j] = (h & 0x7fffu) | (pd << 15) | (last << 21) | ((valid ? 1u : 0u) << 22);
+  }
+}
+
+// zd_chain_kernel (one wave per call, groups in order): a position's previous
+// occurrence is its in-group predecessor, else the LDS head table; the last of
+// each hash in the group becomes the head.  The head table keeps the low 16
 // bits of positions (64 KiB); an entry's age is (j - v) mod 2^16, valid for
-// 1..32767 (farther links are 0 anyway), and every 16384 positions entries
-// older than 32767 are expired, so no age ever wraps.  The call's bytes are
-// staged into LDS and the links collected there, 4096 positions at a time:
-// the group loop touches LDS only (on gfx9 a wait for a global load also
-// waits for every earlier global store, which otherwise stalls every group).
-constexpr int CTILE = 4096;
+// 1..32767 (farther links are 0 anyway).  Every 32768 positions entries aged
+// 0 or above 32767 are expired (set to age 32768), so between expiries every
+// live entry's true age stays below 65536 and its 16-bit age is exact.  The
+// packed hashes of the next 1024 positions are loaded into registers while
+// the current ones are linked, and the links leave from registers: the group
+// loop touches LDS only.
+constexpr int CG = 16;   // groups per tile
 __global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
   __shared__ uint16_t head[32768];
-  __shared__ uint32_t xs[CTILE / 4 + 2];     // X[t0 .. t0 + CTILE + 8)
-  __shared__ uint16_t ls[CTILE];              // links of the tile
   const ZCall c = a.calls[blockIdx.x];
   const ZState s = a.st[c.stream];
   const int lane = threadIdx.x;
-  const uint8_t* X = a.X + c.x_off;
   uint16_t* d16 = a.d16 + c.x_off;
-  // first valid position: max(base, total - WSIZE) as an X index, rounded down to a word
-  const int64_t jlo = (s.total - s.base >= (uint64_t)WSIZE) ? 0 : (int64_t)WSIZE - (int64_t)(s.total - s.base);
-  const uint16_t empty = (uint16_t)(jlo + 32768);   // age >= 32768 until jlo + 32768
+  const uint32_t* pk = a.pk + c.x_off;
+  const int64_t jlo = first_valid(s);
+  const uint16_t empty = (uint16_t)(jlo + 32768);   // age 32768 at jlo, expired again at jlo + 32768
   for (int i = lane; i < 32768; i += 64) head[i] = empty;
-  const int64_t jend = (int64_t)WSIZE + c.len;     // positions q with q + 2 < jend get a hash
-  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const int64_t t_first = jlo & ~3ll;
-  int64_t next_expiry = jlo + 16384;
-  for (int64_t t0 = t_first; t0 < jend; t0 += CTILE) {
-    // stage X[t0 .. t0 + CTILE + 8) (X has XPAD zero bytes past the data)
-    const uint32_t* xw = (const uint32_t*)(X + t0);
-    for (int i = lane; i < CTILE / 4 + 2; i += 64) xs[i] = xw[i];
-    __syncthreads();
-    const int64_t t1 = t0 + CTILE < jend ? t0 + CTILE : jend;
-    const int64_t gstart = t0 > jlo ? t0 : jlo;
-    for (int64_t g = gstart; g < t1; g += 64) {
-      if (g >= next_expiry) {   // every 16384 positions: expire entries older than 32767
-        next_expiry += 16384;
-        const uint16_t far = (uint16_t)(g + 32768);
-        for (int i = lane; i < 32768; i += 64) {
-          uint16_t v = head[i];
-          if ((uint16_t)(g - v) > 32767) head[i] = far;
-        }
-      }
-      const int64_t j = g + lane;
-      const bool in_tile = j < t1;
-      const bool valid = in_tile && j + 2 < jend;
-      const uint32_t o = (uint32_t)(j - t0);           // byte offset in the stage
-      uint32_t h = 0x8000u;                            // invalid lanes form their own class
-      if (valid) {
-        uint32_t lo = xs[o >> 2], hi = xs[(o >> 2) + 1];
-        uint32_t w = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (o & 3)));
-        // UPDATE_HASH x3 (hash_shift 5) over bytes j, j+1, j+2
-        h = (((w & 0xff) << 10) ^ (((w >> 8) & 0xff) << 5) ^ ((w >> 16) & 0xff)) & 0x7fffu;
-      }
-      uint64_t m = ballot(valid);
+  __syncthreads();
+  const int64_t jend = (int64_t)WSIZE + c.len;
+  int64_t next_expiry = jlo + 32768;   // tiles are 1024 positions from jlo: expiry falls on a tile start
+  uint32_t cur[CG], nxt[CG];
 #pragma unroll
-      for (int b = 0; b < 15; b++) {
-        bool bit = (h >> b) & 1;
-        uint64_t bl = ballot(bit);
-        m &= bit ? bl : ~bl;
-      }
-      const uint64_t lower = m & below;
-      const bool last = (m >> lane) == 1ull;
-      int32_t age = 0;
-      if (valid) {
-        if (lower) age = lane - (63 - __clzll(lower));
-        else age = (uint16_t)((uint16_t)j - head[h]);
-      }
-      if (in_tile) ls[j - t0] = (age > 0 && age <= 32767) ? (uint16_t)age : 0;
-      if (valid && last) head[h] = (uint16_t)j;
+  for (int k = 0; k < CG; k++) {
+    const int64_t q = jlo + 64 * k + lane;
+    cur[k] = q < jend ? pk[q] : 0u;
+  }
+  for (int64_t t0 = jlo; t0 < jend; t0 += 64 * CG) {
+#pragma unroll
+    for (int k = 0; k < CG; k++) {
+      const int64_t q = t0 + 64 * (CG + k) + lane;
+      nxt[k] = q < jend ? pk[q] : 0u;
     }
-    __syncthreads();
-    // the tile's links to HBM (positions [gstart, t1))
-    for (int64_t q = gstart + lane; q < t1; q += 64) d16[q] = ls[q - t0];
-    __syncthreads();
+    if (t0 == next_expiry) {
+      next_expiry += 32768;
+      const uint32_t far = (uint16_t)(t0 + 32768);
+      uint64_t* h64 = (uint64_t*)head;
+#pragma unroll 8
+      for (int i = lane; i < 8192; i += 64) {
+        const uint64_t v = h64[i];
+        uint64_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint16_t e = (uint16_t)(v >> (16 * b));
+          const uint16_t age = (uint16_t)((uint16_t)t0 - e);
+          r |= (uint64_t)((age == 0 || age > 32767) ? (uint16_t)far : e) << (16 * b);
+        }
+        if (r != v) h64[i] = r;
+      }
+      __syncthreads();
+    }
+    uint16_t lk[CG];
+#pragma unroll
+    for (int k = 0; k < CG; k++) {
+      const uint32_t e = cur[k];
+      const int64_t j = t0 + 64 * k + lane;
+      const uint32_t h = e & 0x7fffu, pd = (e >> 15) & 63u;
+      int32_t age = 0;
+      if (e >> 22) age = pd ? (int32_t)pd : (int32_t)(uint16_t)((uint16_t)j - head[h]);
+      lk[k] = (age > 0 && age <= 32767) ? (uint16_t)age : 0;
+      if ((e >> 22) && ((e >> 21) & 1)) head[h] = (uint16_t)j;
+    }
+#pragma unroll
+    for (int k = 0; k < CG; k++) {
+      const int64_t q = t0 + 64 * k + lane;
+      if (q < jend) d16[q] = lk[k];
+      cur[k] = nxt[k];
+    }
   }
 }
 
@@ -284,9 +361,9 @@ __global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
 // | ELIG << 31 (chain head exists, within MAX_DIST, lookahead >= 3).  The scan
 // also rejects a head at zlib's window coord 0 (NIL).
 __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
-  const uint32_t ci = a.tile_call[blockIdx.x];
+  const uint32_t ci = call_of(a.mstart, a.n, blockIdx.x);
   const ZCall c = a.calls[ci];
-  const uint32_t rel = a.tile_pos[blockIdx.x] + threadIdx.x;
+  const uint32_t rel = (blockIdx.x - a.mstart[ci]) * 256u + threadIdx.x;
   if (rel >= c.len) return;
   const ZState s = a.st[c.stream];
   const uint8_t* X = a.X + c.x_off;
@@ -682,10 +759,10 @@ __device__ void scan_tree(TreeLds& s, const uint16_t* dl, int max_code) {
 
 // One wave per block: histogram, trees, the _tr_flush_block decision and the
 // block's exact bit count; code tables to `tabs`.
-__global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a, const uint32_t* blk_call) {
+__global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
   __shared__ TreeLds s;
   const uint32_t bi = blockIdx.x;
-  const uint32_t ci = blk_call[bi];
+  const uint32_t ci = call_of(a.bstart, a.n, bi);
   const ZCall c = a.calls[ci];
   const uint32_t k = bi - c.blk_off;
   if (k >= a.res[ci].nblocks) return;
@@ -877,10 +954,10 @@ __device__ __forceinline__ uint32_t static_lcode(int n) {   // fixed literal/len
   return bitrev(code, len) | (len << 16);
 }
 
-__global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a, const uint32_t* blk_call) {
+__global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
   __shared__ uint32_t ltab[L_CODES], dtab[D_CODES];
   const uint32_t bi = blockIdx.x;
-  const uint32_t ci = blk_call[bi];
+  const uint32_t ci = call_of(a.bstart, a.n, bi);
   const ZCall c = a.calls[ci];
   const uint32_t k = bi - c.blk_off;
   const ZCallRes r = a.res[ci];
@@ -1150,7 +1227,7 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   (void)hipSetDevice(z->device);
   // host plan: scratch offsets, tiles, block maps
   std::vector<ZCall> calls(n);
-  std::vector<uint32_t> tile_call, tile_pos, blk_call;
+  std::vector<uint32_t> mstart(n + 1), gstart(n + 1), bstart(n + 1);
   std::vector<uint8_t> seen(z->nstreams, 0);
   size_t xo = 0, to = 0;
   uint32_t bo = 0;
@@ -1169,31 +1246,30 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
     to += al((size_t)c.len + 1, 64);
     c.blk_off = bo;
     c.blk_cap = c.len / SYMS_PER_BLOCK + 2;
+    bstart[i] = bo;
     bo += c.blk_cap;
-    for (uint32_t k = 0; k < c.blk_cap; k++) blk_call.push_back(i);
-    for (uint32_t p = 0; p < c.len; p += 256) {
-      tile_call.push_back(i);
-      tile_pos.push_back(p);
-    }
+    mstart[i + 1] = mstart[i] + (c.len + 255) / 256;
+    gstart[i + 1] = gstart[i] + ((uint32_t)WSIZE + c.len + 63) / 64 + 1;
   }
+  bstart[n] = bo;
+  const uint32_t mtiles = mstart[n], groups = gstart[n];
   // scratch layout
-  size_t o_X = 0, o_d16 = al(o_X + xo, 256), o_tf = al(o_d16 + 2 * xo, 256), o_tq = al(o_tf + 4 * to, 256),
+  size_t o_X = 0, o_d16 = al(o_X + xo, 256), o_pk = al(o_d16 + 2 * xo, 256), o_tf = al(o_pk + 4 * xo, 256),
+         o_tq = al(o_tf + 4 * to, 256),
          o_sym = al(o_tq + 4 * to, 256), o_blk = al(o_sym + 4 * to, 256),
          o_tab = al(o_blk + sizeof(ZBlock) * bo, 256), o_res = al(o_tab + 4ull * TAB_WORDS * bo, 256),
          o_end = al(o_res + sizeof(ZCallRes) * n, 256);
   // the previous batch may still read the scratch
   if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
   if (grow((void**)&z->scratch, &z->scratch_cap, o_end, false)) return XCG_ENOMEM;
-  size_t m_calls = 0, m_tc = al(sizeof(ZCall) * n, 256), m_tp = al(m_tc + 4 * tile_call.size(), 256),
-         m_bc = al(m_tp + 4 * tile_pos.size(), 256), m_end = al(m_bc + 4 * blk_call.size(), 256);
+  size_t m_calls = 0, m_ms = al(sizeof(ZCall) * n, 256), m_gs = al(m_ms + 4ull * (n + 1), 256),
+         m_bs = al(m_gs + 4ull * (n + 1), 256), m_end = al(m_bs + 4ull * (n + 1), 256);
   if (grow(&z->meta, &z->meta_cap, m_end, false) || grow(&z->h_meta, &z->h_meta_cap, m_end, true)) return XCG_ENOMEM;
   uint8_t* hm = (uint8_t*)z->h_meta;
   memcpy(hm + m_calls, calls.data(), sizeof(ZCall) * n);
-  if (!tile_call.empty()) {
-    memcpy(hm + m_tc, tile_call.data(), 4 * tile_call.size());
-    memcpy(hm + m_tp, tile_pos.data(), 4 * tile_pos.size());
-  }
-  memcpy(hm + m_bc, blk_call.data(), 4 * blk_call.size());
+  memcpy(hm + m_ms, mstart.data(), 4ull * (n + 1));
+  memcpy(hm + m_gs, gstart.data(), 4ull * (n + 1));
+  memcpy(hm + m_bs, bstart.data(), 4ull * (n + 1));
   if (hipMemcpyAsync(z->meta, hm, m_end, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
   uint8_t* dm = (uint8_t*)z->meta;
   ZArgs a;
@@ -1204,6 +1280,7 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.out = d_out;
   a.X = z->scratch + o_X;
   a.d16 = (uint16_t*)(z->scratch + o_d16);
+  a.pk = (uint32_t*)(z->scratch + o_pk);
   a.tf = (uint32_t*)(z->scratch + o_tf);
   a.tq = (uint32_t*)(z->scratch + o_tq);
   a.sym = (uint32_t*)(z->scratch + o_sym);
@@ -1211,21 +1288,24 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.tabs = (uint32_t*)(z->scratch + o_tab);
   a.res = (ZCallRes*)(z->scratch + o_res);
   a.out_len = d_out_len;
-  a.tile_call = (const uint32_t*)(dm + m_tc);
-  a.tile_pos = (const uint32_t*)(dm + m_tp);
+  a.n = n;
+  a.mstart = (const uint32_t*)(dm + m_ms);
+  a.gstart = (const uint32_t*)(dm + m_gs);
+  a.bstart = (const uint32_t*)(dm + m_bs);
   a.level = z->level;
-  const uint32_t* d_blk_call = (const uint32_t*)(dm + m_bc);
   uint32_t maxlen = 0;
   for (uint32_t i = 0; i < n; i++) maxlen = std::max(maxlen, h_len[i]);
   uint32_t prep_tiles = std::min<uint32_t>(64, ((uint32_t)WSIZE + maxlen + XPAD + 4095) / 4096);
   hipLaunchKernelGGL(zd_prep_kernel, dim3(prep_tiles, n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_hashes_kernel, dim3((groups + 4 * HGROUPS - 1) / (4 * HGROUPS)), dim3(256), 0, st, a, n,
+                     a.gstart);
   hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
-  if (!tile_call.empty()) hipLaunchKernelGGL(zd_match_kernel, dim3((uint32_t)tile_call.size()), dim3(256), 0, st, a);
+  if (mtiles) hipLaunchKernelGGL(zd_match_kernel, dim3(mtiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zd_scan_kernel, dim3(n), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(zd_trees_kernel, dim3(bo), dim3(64), 0, st, a, d_blk_call);
+  hipLaunchKernelGGL(zd_trees_kernel, dim3(bo), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_layout_kernel, dim3(n), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a, d_blk_call);
+  hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_commit_kernel, dim3(8, n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
