@@ -169,30 +169,43 @@ __global__ __launch_bounds__(256) void zd_prep_kernel(ZArgs a) {
   }
 }
 
-// adler32 of the call's bytes, combined with the stream's (one wave per call)
-__global__ __launch_bounds__(64) void zd_adler_kernel(ZArgs a) {
+// adler32 of the call's bytes, combined with the stream's.  Four waves per
+// call read consecutive 4-byte words (coalesced); per thread sum d_i and
+// sum i * d_i (i < len <= 2^24: both fit 64 bits), reduced through LDS.
+__global__ __launch_bounds__(256) void zd_adler_kernel(ZArgs a) {
+  __shared__ uint64_t red[2][4];
   const ZCall c = a.calls[blockIdx.x];
   const uint8_t* d = a.in + c.in_off;
-  const int lane = threadIdx.x;
-  uint64_t A = 0, B = 0;   // sum d_i, sum i * d_i (i < len <= 2^24: fits)
-  uint64_t chunk = (c.len + 63) / 64;
-  uint64_t s = (uint64_t)lane * chunk, e = std::min<uint64_t>(s + chunk, c.len);
-  for (uint64_t i = s; i < e; i++) {
-    uint32_t v = d[i];
-    A += v;
-    B += i * v;
+  const int t = threadIdx.x;
+  uint64_t A = 0, B = 0;
+  const uint32_t words = c.len / 4;
+#pragma unroll 4
+  for (uint32_t w = t; w < words; w += 256) {
+    const uint32_t v = *(const u32_u*)(d + 4ull * w);
+    const uint32_t s = (v & 0xff) + ((v >> 8) & 0xff) + ((v >> 16) & 0xff) + (v >> 24);
+    const uint32_t wsum = ((v >> 8) & 0xff) + 2 * ((v >> 16) & 0xff) + 3 * (v >> 24);   // in-word offsets
+    A += s;
+    B += (uint64_t)(4ull * w) * s + wsum;
   }
-  A %= 65521u;
-  B %= 65521u;
+  for (uint32_t i = 4 * words + t; i < c.len; i += 256) {
+    const uint32_t v = d[i];
+    A += v;
+    B += (uint64_t)i * v;
+  }
   for (int o = 32; o >= 1; o >>= 1) {
     A += __shfl_xor(A, o);
     B += __shfl_xor(B, o);
   }
-  if (lane == 0) {
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = A;
+    red[1][t >> 6] = B;
+  }
+  __syncthreads();
+  if (t == 0) {
+    A = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) % 65521u;
+    B = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) % 65521u;
     uint32_t old = a.st[c.stream].adler;
     uint64_t s1 = old & 0xffff, s2 = old >> 16, n = c.len % 65521u;
-    A %= 65521u;
-    B %= 65521u;
     uint64_t ns1 = (s1 + A) % 65521u;
     uint64_t ns2 = (s2 + n * s1 + n * A + 65521u - B) % 65521u;
     a.res[blockIdx.x].adler = (uint32_t)((ns2 << 16) | ns1);
@@ -601,32 +614,58 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
 }
 
 // ------------------------------------------------------------------- trees
+#ifdef XCG_ZD_TIMING
+// diagnostics build: wave cycles per phase summed over blocks (trees: histogram,
+// literal tree, distance + bit-length trees, bit count, tables; emit: tables and
+// header, sizing pass, packing pass) and block counts
+__device__ unsigned long long g_zd_t[16];
+#define ZD_NOW() __builtin_readcyclecounter()
+#define ZD_ADD(i, t0)                                                         \
+  do {                                                                        \
+    uint64_t t1_ = ZD_NOW();                                                  \
+    if (threadIdx.x == 0) atomicAdd(&g_zd_t[i], (unsigned long long)(t1_ - (t0))); \
+    t0 = t1_;                                                                 \
+  } while (0)
+#else
+#define ZD_NOW() 0ull
+#define ZD_ADD(i, t0) (void)(t0)
+#endif
+// Heap entries are freq << 15 | depth << 10 | node: trees.c's smaller(n, m)
+// (freq, then depth <=) is `key(n) <= key(m)` on key = entry >> 10, so a
+// downheap step is one 8-byte LDS read of both children.  A block holds at
+// most 16383 symbols + END_BLOCK (+2 forced), so freq < 2^17, and a Huffman
+// tree over that total weight is at most ~21 deep (Fibonacci bound): depth
+// fits 5 bits, nodes (< 573) 10.
 struct TreeLds {
-  uint16_t fc[HEAP_SIZE];    // Freq | Code
+  uint32_t heap[HEAP_SIZE + 1];
+  uint16_t fc[HEAP_SIZE];    // leaf Freq | Code
   uint16_t dl[HEAP_SIZE];    // Dad | Len
   uint16_t dfc[2 * D_CODES + 1], ddl[2 * D_CODES + 1];
   uint16_t bfc[2 * BL_CODES + 1], bdl[2 * BL_CODES + 1];
   uint32_t lfreq[L_CODES], dfreq[D_CODES], bfreq[BL_CODES];   // real counts (forced codes excluded)
-  int16_t heap[HEAP_SIZE];
-  uint8_t depth[HEAP_SIZE];
   int bl_count[MAX_BITS + 1];
   int heap_len, heap_max;
   int64_t opt_len, static_len;
 };
 
-__device__ __forceinline__ bool smaller(const uint16_t* fc, const uint8_t* dep, int n, int m) {
-  return fc[n] < fc[m] || (fc[n] == fc[m] && dep[n] <= dep[m]);
-}
-__device__ void downheap(TreeLds& s, const uint16_t* fc, int k) {
-  int v = s.heap[k], j = k << 1;
-  while (j <= s.heap_len) {
-    if (j < s.heap_len && smaller(fc, s.depth, s.heap[j + 1], s.heap[j])) j++;
-    if (smaller(fc, s.depth, v, s.heap[j])) break;
-    s.heap[k] = s.heap[j];
+__device__ __forceinline__ uint32_t hkey(uint32_t e) { return e >> 10; }
+__device__ void downheap(TreeLds& s, int k) {
+  const uint32_t v = s.heap[k];
+  const int len = s.heap_len;
+  int j = k << 1;
+  while (j <= len) {
+    const uint2 p = *(const uint2*)&s.heap[j];   // j even: heap[j], heap[j + 1]
+    uint32_t e = p.x;
+    if (j < len && hkey(p.y) <= hkey(p.x)) {
+      e = p.y;
+      j++;
+    }
+    if (hkey(v) <= hkey(e)) break;
+    s.heap[k] = e;
     k = j;
     j <<= 1;
   }
-  s.heap[k] = (int16_t)v;
+  s.heap[k] = v;
 }
 __device__ __forceinline__ int static_llen(int n) { return n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8; }
 
@@ -634,47 +673,46 @@ __device__ __forceinline__ int static_llen(int n) { return n < 144 ? 8 : n < 256
 __device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int kind) {
   const int maxlen = kind == 2 ? 7 : MAX_BITS;
   int n, m, max_code = -1, node;
-  s.heap_len = 0;
-  s.heap_max = HEAP_SIZE;
+  int len = 0, hmax = HEAP_SIZE;
   for (n = 0; n < elems; n++) {
     if (fc[n]) {
-      s.heap[++s.heap_len] = (int16_t)(max_code = n);
-      s.depth[n] = 0;
+      s.heap[++len] = ((uint32_t)fc[n] << 15) | (uint32_t)n;
+      max_code = n;
     } else {
       dl[n] = 0;
     }
   }
-  while (s.heap_len < 2) {
+  while (len < 2) {
     node = max_code < 2 ? ++max_code : 0;
-    s.heap[++s.heap_len] = (int16_t)node;
+    s.heap[++len] = (1u << 15) | (uint32_t)node;
     fc[node] = 1;
-    s.depth[node] = 0;
     s.opt_len--;
     if (kind == 0) s.static_len -= static_llen(node);
     else if (kind == 1) s.static_len -= 5;
   }
-  for (n = s.heap_len / 2; n >= 1; n--) downheap(s, fc, n);
+  s.heap_len = len;
+  for (n = len / 2; n >= 1; n--) downheap(s, n);
   node = elems;
   do {
-    n = s.heap[1];
+    const uint32_t en = s.heap[1];
     s.heap[1] = s.heap[s.heap_len--];
-    downheap(s, fc, 1);
-    m = s.heap[1];
-    s.heap[--s.heap_max] = (int16_t)n;
-    s.heap[--s.heap_max] = (int16_t)m;
-    fc[node] = (uint16_t)(fc[n] + fc[m]);
-    s.depth[node] = (uint8_t)((s.depth[n] >= s.depth[m] ? s.depth[n] : s.depth[m]) + 1);
-    dl[n] = dl[m] = (uint16_t)node;
-    s.heap[1] = (int16_t)node++;
-    downheap(s, fc, 1);
+    downheap(s, 1);
+    const uint32_t em = s.heap[1];
+    s.heap[--hmax] = en;
+    s.heap[--hmax] = em;
+    const uint32_t dn = (en >> 10) & 31, dm = (em >> 10) & 31;
+    const uint32_t f = (en >> 15) + (em >> 15), d = (dn >= dm ? dn : dm) + 1;
+    dl[en & 1023] = dl[em & 1023] = (uint16_t)node;
+    s.heap[1] = (f << 15) | (d << 10) | (uint32_t)node++;
+    downheap(s, 1);
   } while (s.heap_len >= 2);
-  s.heap[--s.heap_max] = s.heap[1];
+  s.heap[--hmax] = s.heap[1];
 
   int h, bits, overflow = 0;
   for (bits = 0; bits <= MAX_BITS; bits++) s.bl_count[bits] = 0;
-  dl[s.heap[s.heap_max]] = 0;
-  for (h = s.heap_max + 1; h < HEAP_SIZE; h++) {
-    n = s.heap[h];
+  dl[s.heap[hmax] & 1023] = 0;
+  for (h = hmax + 1; h < HEAP_SIZE; h++) {
+    n = s.heap[h] & 1023;
     bits = dl[dl[n]] + 1;
     if (bits > maxlen) {
       bits = maxlen;
@@ -703,7 +741,7 @@ __device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int
     for (bits = maxlen; bits != 0; bits--) {
       n = s.bl_count[bits];
       while (n != 0) {
-        m = s.heap[--h];
+        m = s.heap[--h] & 1023;
         if (m > max_code) continue;
         if (dl[m] != (unsigned)bits) {
           s.opt_len += ((int64_t)bits - dl[m]) * fc[m];
@@ -769,6 +807,7 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
   ZBlock* B = a.blk + bi;
   const int lane = threadIdx.x;
   const uint32_t* sym = a.sym + c.t_off;
+  uint64_t tz = ZD_NOW();
   for (int i = lane; i < L_CODES; i += 64) s.lfreq[i] = 0;
   if (lane < D_CODES) s.dfreq[lane] = 0;
   if (lane < BL_CODES) s.bfreq[lane] = 0;
@@ -789,7 +828,9 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     for (int i = 0; i < L_CODES; i++) s.fc[i] = (uint16_t)s.lfreq[i];
     for (int i = 0; i < D_CODES; i++) s.dfc[i] = (uint16_t)s.dfreq[i];
     s.opt_len = s.static_len = 0;
+    ZD_ADD(0, tz);
     int lmax = build_tree(s, s.fc, s.dl, L_CODES, 0);
+    ZD_ADD(1, tz);
     int dmax = build_tree(s, s.dfc, s.ddl, D_CODES, 1);
     scan_tree(s, s.dl, lmax);
     scan_tree(s, s.ddl, dmax);
@@ -799,6 +840,7 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
       if (s.bdl[BL_ORDER[max_blindex]] != 0) break;
     s.opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+    ZD_ADD(2, tz);
     int64_t opt_lenb = (s.opt_len + 3 + 7) >> 3, static_lenb = (s.static_len + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
     uint32_t type;
@@ -822,6 +864,7 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     B->lcodes = lmax + 1;
     B->dcodes = dmax + 1;
     B->blcodes = max_blindex + 1;
+    ZD_ADD(3, tz);
   }
   __syncthreads();
   uint32_t* tab = a.tabs + (uint64_t)bi * TAB_WORDS;
@@ -830,6 +873,10 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     if (lane < D_CODES) tab[L_CODES + lane] = s.dfc[lane] | ((uint32_t)s.ddl[lane] << 16);
     if (lane < BL_CODES) tab[L_CODES + D_CODES + lane] = s.bfc[lane] | ((uint32_t)s.bdl[lane] << 16);
   }
+  ZD_ADD(4, tz);
+#ifdef XCG_ZD_TIMING
+  if (lane == 0) atomicAdd(&g_zd_t[15], 1ull);
+#endif
 }
 
 // ------------------------------------------------------------------- layout
@@ -893,16 +940,22 @@ __device__ __forceinline__ void or_byte(OutW o, uint64_t byte, uint32_t v) {
   or_word(o, byte >> 2, v << (8 * (byte & 3)));
 }
 
-struct BitW {           // lane-0 sequential writer (block header, tree description)
-  OutW o;
+// Huffman blocks are packed through an LDS ring of output words: absolute
+// word w of the call's output lives in ring[w % RING] until it is complete.
+constexpr int RING = 512;
+struct RingW {          // lane-0 sequential writer (block header, tree description)
+  uint32_t* ring;
   uint64_t pos;
-  __device__ void put(uint32_t v, int n) {
-    or_bits(o, pos, v, n);
+  __device__ void put(uint32_t v, int n) {   // v < 2^n, n <= 16
+    const uint64_t x = (uint64_t)v << (pos & 31);
+    const uint64_t w = pos >> 5;
+    if ((uint32_t)x) atomicOr(&ring[w % RING], (uint32_t)x);
+    if (x >> 32) atomicOr(&ring[(w + 1) % RING], (uint32_t)(x >> 32));
     pos += n;
   }
 };
 
-__device__ void send_tree(BitW& bw, const uint32_t* tab, int max_code, const uint32_t* btab) {
+__device__ void send_tree(RingW& bw, const uint32_t* tab, int max_code, const uint32_t* btab) {
   int prevlen = -1, curlen, nextlen = tab[0] >> 16, count = 0, max_count = 7, min_count = 4;
   if (nextlen == 0) {
     max_count = 138;
@@ -954,8 +1007,17 @@ __device__ __forceinline__ uint32_t static_lcode(int n) {   // fixed literal/len
   return bitrev(code, len) | (len << 16);
 }
 
+// One wave per block.  Huffman blocks: per-block LDS tables give every symbol
+// its bits with the extra bits merged (literal: code; length: code + extra;
+// distance: code + extra), 64 symbols per step are loaded coalesced (prefetched
+// a step ahead), a wave scan places them, they are OR-ed into the LDS ring, and
+// completed words leave with coalesced stores -- the block's first and last
+// words (shared with its neighbours) with atomicOr.
+constexpr int EBATCH = 4;   // 64-symbol steps per prefetch
 __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
-  __shared__ uint32_t ltab[L_CODES], dtab[D_CODES];
+  __shared__ uint32_t litx[256], lenx[256], dtx[D_CODES];   // bits | nbits << 24 (dist: code | nbits << 16)
+  __shared__ uint32_t stab[TAB_WORDS];
+  __shared__ uint32_t ring[RING];
   const uint32_t bi = blockIdx.x;
   const uint32_t ci = call_of(a.bstart, a.n, bi);
   const ZCall c = a.calls[ci];
@@ -965,6 +1027,7 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
   const ZBlock B = a.blk[bi];
   const ZState s = a.st[c.stream];
   const int lane = threadIdx.x;
+  uint64_t tz = ZD_NOW();
   const OutW o{(uint32_t*)(a.out + c.out_off), (r.out_len + 3ull) / 4};
   const OutW ob = o;
   const bool last = B.flags & 2;
@@ -998,97 +1061,121 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
       if ((byte >> 2) < w0 || (byte >> 2) >= w1) or_byte(ob, byte, X[i]);
     }
   } else {
+    const bool dyn = B.type == 2;
     const uint32_t* tab = a.tabs + (uint64_t)bi * TAB_WORDS;
-    for (int i = lane; i < L_CODES; i += 64) ltab[i] = B.type == 2 ? tab[i] : static_lcode(i);
-    if (lane < D_CODES) dtab[lane] = B.type == 2 ? tab[L_CODES + lane] : (bitrev(lane, 5) | (5u << 16));
+    if (dyn)
+      for (int i = lane; i < TAB_WORDS; i += 64) stab[i] = tab[i];
+    for (int i = lane; i < RING; i += 64) ring[i] = 0;
     __syncthreads();
+    auto lcode = [&](int n) { return dyn ? stab[n] : static_lcode(n); };
+    for (int i = lane; i < 256; i += 64) {
+      const uint32_t t = lcode(i);
+      litx[i] = (t & 0xffff) | ((t >> 16) << 24);
+      const int code = len_code(i), xl = XLB[code];
+      const uint32_t u = lcode(257 + code), hl = u >> 16;
+      lenx[i] = ((u & 0xffff) | (xl ? (uint32_t)(i - BASE_LEN[code]) << hl : 0u)) | ((hl + xl) << 24);
+    }
+    if (lane < D_CODES) dtx[lane] = dyn ? stab[L_CODES + lane] : (bitrev(lane, 5) | (5u << 16));
+    const uint32_t eob = lcode(256);
     uint64_t pos = B.bit_off;
+    __syncthreads();
     if (lane == 0) {
-      BitW bw{o, pos};
+      RingW bw{ring, pos};
       bw.put((B.type << 1) | (last ? 1 : 0), 3);
-      if (B.type == 2) {
-        const uint32_t* btab = tab + L_CODES + D_CODES;
+      if (dyn) {
+        const uint32_t* btab = stab + L_CODES + D_CODES;
         bw.put(B.lcodes - 257, 5);
         bw.put(B.dcodes - 1, 5);
         bw.put(B.blcodes - 4, 4);
         for (uint32_t rk = 0; rk < B.blcodes; rk++) bw.put(btab[BL_ORDER[rk]] >> 16, 3);
-        send_tree(bw, tab, B.lcodes - 1, btab);
-        send_tree(bw, tab + L_CODES, B.dcodes - 1, btab);
+        send_tree(bw, stab, B.lcodes - 1, btab);
+        send_tree(bw, stab + L_CODES, B.dcodes - 1, btab);
       }
       pos = bw.pos;
     }
     pos = readlane64(pos, 0);
-    // Each lane packs a contiguous run of symbols: pass 1 sizes the runs, a
-    // wave scan places them, pass 2 writes whole words with plain stores and
-    // only each run's first and last (shared) words with atomicOr.
-    const uint32_t* sym = a.sym + c.t_off;
-    const uint32_t nsy = B.sym_end - B.sym_begin, per = (nsy + 63) / 64;
-    const uint32_t s0 = B.sym_begin + min(nsy, lane * per), s1 = B.sym_begin + min(nsy, (lane + 1) * per);
-    auto parts = [&](uint32_t e, uint32_t& v0, int& n0, uint32_t& v1, int& n1) {
-      uint32_t dist = e >> 8;
-      if (dist == 0) {
-        uint32_t t = ltab[e & 255];
-        v0 = t & 0xffff;
-        n0 = t >> 16;
-        v1 = 0;
-        n1 = 0;
-        return;
+    __syncthreads();
+    ZD_ADD(8, tz);
+    const uint64_t wfirst = B.bit_off >> 5;
+    uint64_t flushed = wfirst;
+    auto flush = [&](uint64_t upto) {   // words [flushed, upto) are complete
+      for (uint64_t w = flushed + lane; w < upto; w += 64) {
+        const uint32_t v = ring[w % RING];
+        ring[w % RING] = 0;
+        if (w == wfirst) or_word(o, w, v);
+        else if (w < o.nwords) o.o[w] = v;
       }
-      uint32_t lc = e & 255;
-      int code = len_code(lc);
-      uint32_t t = ltab[257 + code];
-      v0 = t & 0xffff;
-      n0 = t >> 16;
-      int xl = XLB[code];   // code 28 (length 258) has no extra bits
-      if (xl) v0 |= (lc - BASE_LEN[code]) << n0;
-      n0 += xl;
-      uint32_t d = dist - 1;
-      int dc = dist_code(d);
-      uint32_t td = dtab[dc];
-      v1 = (td & 0xffff) | ((d - BASE_DIST[dc]) << (td >> 16));
-      n1 = (td >> 16) + XDB[dc];
+      flushed = upto;
     };
-    uint32_t mybits = 0;
-    for (uint32_t i = s0; i < s1; i++) {
-      uint32_t v0, v1;
-      int n0, n1;
-      parts(sym[i], v0, n0, v1, n1);
-      mybits += n0 + n1;
+    const uint32_t* sym = a.sym + c.t_off;
+    const uint32_t sb = B.sym_begin, se = B.sym_end;
+    uint32_t cur[EBATCH], nxt[EBATCH];
+#pragma unroll
+    for (int q = 0; q < EBATCH; q++) {
+      const uint32_t i = sb + 64 * q + lane;
+      cur[q] = i < se ? sym[i] : 0xffffffffu;
     }
-    uint32_t incl = wave_incl_scan(mybits);
-    uint64_t P = pos + incl - mybits;
-    if (s1 > s0) {
-      uint64_t wi = P >> 5;
-      uint64_t acc = 0;
-      int accn = (int)(P & 31);
-      bool first = true;
-      auto put = [&](uint32_t v, int n) {
-        acc |= (uint64_t)v << accn;
-        accn += n;
-        if (accn >= 32) {
-          uint32_t word = (uint32_t)acc;
-          if (first) or_word(o, wi, word);
-          else if (wi < o.nwords) o.o[wi] = word;
-          first = false;
-          wi++;
-          acc >>= 32;
-          accn -= 32;
-        }
-      };
-      for (uint32_t i = s0; i < s1; i++) {
-        uint32_t v0, v1;
-        int n0, n1;
-        parts(sym[i], v0, n0, v1, n1);
-        put(v0, n0);
-        if (n1) put(v1, n1);
+    for (uint32_t b0 = sb; b0 < se; b0 += 64 * EBATCH) {
+#pragma unroll
+      for (int q = 0; q < EBATCH; q++) {
+        const uint32_t i = b0 + 64 * (EBATCH + q) + lane;
+        nxt[q] = i < se ? sym[i] : 0xffffffffu;
       }
-      if (accn > 0) or_word(o, wi, (uint32_t)acc);
+#pragma unroll
+      for (int q = 0; q < EBATCH; q++) {
+        if (b0 + 64 * q >= se) break;
+        const uint32_t e = cur[q];
+        uint64_t v = 0;
+        uint32_t nb = 0;
+        if (e != 0xffffffffu) {
+          const uint32_t dist = e >> 8;
+          if (dist == 0) {
+            const uint32_t t = litx[e & 255];
+            v = t & 0xffffff;
+            nb = t >> 24;
+          } else {
+            const uint32_t t = lenx[e & 255];
+            const uint32_t d = dist - 1;
+            const int dc = dist_code(d);
+            const uint32_t td = dtx[dc], hd = td >> 16;
+            const uint32_t xd = d < 4 ? 0u : (uint32_t)(31 - __clz(d)) - 1u;   // XDB[dc]
+            const uint32_t v1 = (td & 0xffff) | ((d & ((1u << xd) - 1u)) << hd);
+            const uint32_t n0 = t >> 24;
+            v = (uint64_t)(t & 0xffffff) | ((uint64_t)v1 << n0);
+            nb = n0 + hd + xd;
+          }
+        }
+        const uint32_t incl = wave_incl_scan(nb);
+        if (nb) {
+          const uint64_t P = pos + incl - nb;
+          const uint64_t w = P >> 5;
+          const uint32_t sh = (uint32_t)(P & 31);
+          const uint64_t lo = v << sh;
+          if ((uint32_t)lo) atomicOr(&ring[w % RING], (uint32_t)lo);
+          if (lo >> 32) atomicOr(&ring[(w + 1) % RING], (uint32_t)(lo >> 32));
+          if (sh && (v >> (64 - sh))) atomicOr(&ring[(w + 2) % RING], (uint32_t)(v >> (64 - sh)));
+        }
+        pos += readlane(incl, 63);
+        flush(pos >> 5);
+      }
+#pragma unroll
+      for (int q = 0; q < EBATCH; q++) cur[q] = nxt[q];
     }
-    pos += readlane(incl, 63);
+    ZD_ADD(9, tz);
     if (lane == 0) {
-      uint32_t t = ltab[256];
-      or_bits(o, pos, t & 0xffff, t >> 16);
+      RingW bw{ring, pos};
+      bw.put(eob & 0xffff, eob >> 16);
+      pos = bw.pos;
     }
+    pos = readlane64(pos, 0);
+    // the last (partial) word is shared with the next block
+    const uint64_t wend = (pos + 31) >> 5;
+    for (uint64_t w = flushed + lane; w < wend; w += 64) {
+      const uint32_t v = ring[w % RING];
+      if (w == wfirst || w == wend - 1) or_word(o, w, v);
+      else if (w < o.nwords) o.o[w] = v;
+    }
+    ZD_ADD(10, tz);
   }
   if (k == r.nblocks - 1 && lane == 0) {
     if (last) {   // Z_FINISH: adler32 trailer, big-endian (putShortMSB x2)
@@ -1297,7 +1384,7 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   for (uint32_t i = 0; i < n; i++) maxlen = std::max(maxlen, h_len[i]);
   uint32_t prep_tiles = std::min<uint32_t>(64, ((uint32_t)WSIZE + maxlen + XPAD + 4095) / 4096);
   hipLaunchKernelGGL(zd_prep_kernel, dim3(prep_tiles, n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zd_hashes_kernel, dim3((groups + 4 * HGROUPS - 1) / (4 * HGROUPS)), dim3(256), 0, st, a, n,
                      a.gstart);
   hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
@@ -1345,5 +1432,13 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
   (void)hipFree(d_len);
   return rc;
 }
+
+#ifdef XCG_ZD_TIMING
+int xcg_debug_zd_times(uint64_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zd_t), 8 * 16) != hipSuccess) return XCG_EHIP;
+  uint64_t z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_zd_t), z, sizeof z) == hipSuccess ? XCG_OK : XCG_EHIP;
+}
+#endif
 
 }  // extern "C"
