@@ -20,6 +20,6 @@ for k in range(2):
     ctx.consume_many([(s, calls[s][k]) for s in range(S)])
     dt = time.perf_counter() - t0
     L.xcg_debug_zd_times(t.ctypes.data)
-    nb = max(1, int(t[15]))
-    print(f'step {k}: wall {dt*1e3:.1f} ms, {nb} blocks; cycles per block:',
-          {n: int(t[i]) // nb for i, n in names.items()})
+    nb, nw = max(1, int(t[15])), max(1, int(t[14]))
+    print(f'step {k}: wall {dt*1e3:.1f} ms, {nb} blocks, {nw} tree waves; cycles per tree wave / emit block:',
+          {n: int(t[i]) // (nw if n.startswith('tr') else nb) for i, n in names.items()})

@@ -638,29 +638,48 @@ __device__ unsigned long long g_zd_t[16];
 // fits 5 bits, nodes (< 573) 10.
 struct TreeLds {
   uint32_t heap[HEAP_SIZE + 1];
-  uint16_t fc[HEAP_SIZE];    // leaf Freq | Code
-  uint16_t dl[HEAP_SIZE];    // Dad | Len
-  uint16_t dfc[2 * D_CODES + 1], ddl[2 * D_CODES + 1];
-  uint16_t bfc[2 * BL_CODES + 1], bdl[2 * BL_CODES + 1];
-  uint32_t lfreq[L_CODES], dfreq[D_CODES], bfreq[BL_CODES];   // real counts (forced codes excluded)
-  int bl_count[MAX_BITS + 1];
-  int heap_len, heap_max;
+  uint16_t dl[HEAP_SIZE + 1];  // Dad | Len
+  uint16_t fc[L_CODES];        // leaf Freq | Code
+  uint16_t dfc[D_CODES], ddl[2 * D_CODES + 1];
+  uint16_t bfc[BL_CODES], bdl[2 * BL_CODES + 1];
+  uint16_t lfreq[L_CODES], dfreq[D_CODES], bfreq[BL_CODES + 1];   // real counts (forced codes excluded)
+  uint16_t bl_count[MAX_BITS + 1];
+  uint32_t next_code[MAX_BITS + 1];
   int64_t opt_len, static_len;
 };
+// one TreeLds per lane-owned block, at a stride of 4 mod 64 words (16-byte aligned, no bank conflicts
+// between the TB lanes)
+constexpr int TB = 2;   // blocks per wave
+constexpr uint32_t TSTRIDE = ((sizeof(TreeLds) + 255) / 256) * 256 + 16;
 
 __device__ __forceinline__ uint32_t hkey(uint32_t e) { return e >> 10; }
-__device__ void downheap(TreeLds& s, int k) {
-  const uint32_t v = s.heap[k];
-  const int len = s.heap_len;
+// Two levels per LDS round trip: the children pair and the four grandchildren
+// are read together (stores along the path go to indices below both).
+__device__ void downheap(TreeLds& s, int k, int len) {
+  const uint32_t v = s.heap[k], kv = hkey(v);
   int j = k << 1;
   while (j <= len) {
-    const uint2 p = *(const uint2*)&s.heap[j];   // j even: heap[j], heap[j + 1]
+    const uint2 p = *(const uint2*)&s.heap[j];   // j even
+    uint4 g = make_uint4(0, 0, 0, 0);
+    if (2 * j <= len) g = *(const uint4*)&s.heap[2 * j];   // 2j % 4 == 0
     uint32_t e = p.x;
     if (j < len && hkey(p.y) <= hkey(p.x)) {
       e = p.y;
       j++;
     }
-    if (hkey(v) <= hkey(e)) break;
+    if (kv <= hkey(e)) break;
+    s.heap[k] = e;
+    k = j;
+    const bool right = j & 1;
+    j <<= 1;
+    if (j > len) break;
+    const uint32_t e0 = right ? g.z : g.x, e1 = right ? g.w : g.y;
+    e = e0;
+    if (j < len && hkey(e1) <= hkey(e0)) {
+      e = e1;
+      j++;
+    }
+    if (kv <= hkey(e)) break;
     s.heap[k] = e;
     k = j;
     j <<= 1;
@@ -690,13 +709,12 @@ __device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int
     if (kind == 0) s.static_len -= static_llen(node);
     else if (kind == 1) s.static_len -= 5;
   }
-  s.heap_len = len;
-  for (n = len / 2; n >= 1; n--) downheap(s, n);
+  for (n = len / 2; n >= 1; n--) downheap(s, n, len);
   node = elems;
   do {
     const uint32_t en = s.heap[1];
-    s.heap[1] = s.heap[s.heap_len--];
-    downheap(s, 1);
+    s.heap[1] = s.heap[len--];
+    downheap(s, 1, len);
     const uint32_t em = s.heap[1];
     s.heap[--hmax] = en;
     s.heap[--hmax] = em;
@@ -704,8 +722,8 @@ __device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int
     const uint32_t f = (en >> 15) + (em >> 15), d = (dn >= dm ? dn : dm) + 1;
     dl[en & 1023] = dl[em & 1023] = (uint16_t)node;
     s.heap[1] = (f << 15) | (d << 10) | (uint32_t)node++;
-    downheap(s, 1);
-  } while (s.heap_len >= 2);
+    downheap(s, 1, len);
+  } while (len >= 2);
   s.heap[--hmax] = s.heap[1];
 
   int h, bits, overflow = 0;
@@ -751,14 +769,14 @@ __device__ int build_tree(TreeLds& s, uint16_t* fc, uint16_t* dl, int elems, int
       }
     }
   }
-  uint32_t next[MAX_BITS + 1], code = 0;
+  uint32_t code = 0;
   for (bits = 1; bits <= MAX_BITS; bits++) {
     code = (code + s.bl_count[bits - 1]) << 1;
-    next[bits] = code;
+    s.next_code[bits] = code;
   }
   for (n = 0; n <= max_code; n++) {
-    int len = dl[n];
-    if (len) fc[n] = (uint16_t)bitrev(next[len]++, len);
+    const int l = dl[n];
+    if (l) fc[n] = (uint16_t)bitrev(s.next_code[l]++, l);
   }
   return max_code;
 }
@@ -797,44 +815,70 @@ __device__ void scan_tree(TreeLds& s, const uint16_t* dl, int max_code) {
 
 // One wave per block: histogram, trees, the _tr_flush_block decision and the
 // block's exact bit count; code tables to `tabs`.
+// TB blocks per wave: the wave builds each block's symbol histogram in turn,
+// then lane t runs block t's trees (the heap work is a serial chain per
+// block; one lane per block spends the wave's VALU issue slots on TB chains
+// instead of one), then the code tables leave with the whole wave.
 __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
-  __shared__ TreeLds s;
-  const uint32_t bi = blockIdx.x;
-  const uint32_t ci = call_of(a.bstart, a.n, bi);
-  const ZCall c = a.calls[ci];
-  const uint32_t k = bi - c.blk_off;
-  if (k >= a.res[ci].nblocks) return;
-  ZBlock* B = a.blk + bi;
+  __shared__ __attribute__((aligned(16))) uint8_t raw[TB * TSTRIDE];
+  __shared__ uint32_t hist[L_CODES + D_CODES];
+  __shared__ int ttype[TB];
   const int lane = threadIdx.x;
-  const uint32_t* sym = a.sym + c.t_off;
+  const uint32_t nrec = a.bstart[a.n];
   uint64_t tz = ZD_NOW();
-  for (int i = lane; i < L_CODES; i += 64) s.lfreq[i] = 0;
-  if (lane < D_CODES) s.dfreq[lane] = 0;
-  if (lane < BL_CODES) s.bfreq[lane] = 0;
-  __syncthreads();
-  const uint32_t sb = B->sym_begin, se = B->sym_end;
-  for (uint32_t i = sb + lane; i < se; i += 64) {
-    uint32_t v = sym[i];
-    uint32_t dist = v >> 8;
-    if (dist == 0) atomicAdd(&s.lfreq[v & 255], 1u);
-    else {
-      atomicAdd(&s.lfreq[257 + len_code(v & 255)], 1u);
-      atomicAdd(&s.dfreq[dist_code(dist - 1)], 1u);
+  for (int t = 0; t < TB; t++) {
+    const uint32_t bi = blockIdx.x * TB + t;
+    if (lane == 0) ttype[t] = -1;
+    if (bi >= nrec) continue;
+    const uint32_t ci = call_of(a.bstart, a.n, bi);
+    const ZCall c = a.calls[ci];
+    if (bi - c.blk_off >= a.res[ci].nblocks) continue;
+    TreeLds& s = *(TreeLds*)(raw + t * TSTRIDE);
+    for (int i = lane; i < L_CODES + D_CODES; i += 64) hist[i] = 0;
+    __syncthreads();
+    const ZBlock* B = a.blk + bi;
+    const uint32_t* sym = a.sym + c.t_off;
+    const uint32_t sb = B->sym_begin, se = B->sym_end;
+    for (uint32_t i0 = sb; i0 < se; i0 += 64 * 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t i = i0 + 64 * q + lane;
+        v[q] = i < se ? sym[i] : 0xffffffffu;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        if (v[q] == 0xffffffffu) continue;
+        const uint32_t dist = v[q] >> 8;
+        if (dist == 0) atomicAdd(&hist[v[q] & 255], 1u);
+        else {
+          atomicAdd(&hist[257 + len_code(v[q] & 255)], 1u);
+          atomicAdd(&hist[L_CODES + dist_code(dist - 1)], 1u);
+        }
+      }
     }
+    __syncthreads();
+    for (int i = lane; i < L_CODES; i += 64) {
+      const uint16_t f = i == 256 ? 1 : (uint16_t)hist[i];
+      s.lfreq[i] = f;
+      s.fc[i] = f;
+    }
+    if (lane < D_CODES) s.dfreq[lane] = s.dfc[lane] = (uint16_t)hist[L_CODES + lane];
+    if (lane <= BL_CODES) s.bfreq[lane] = 0;
+    if (lane == 0) ttype[t] = 0;
+    __syncthreads();
   }
-  __syncthreads();
-  if (lane == 0) {
-    s.lfreq[256] = 1;
-    for (int i = 0; i < L_CODES; i++) s.fc[i] = (uint16_t)s.lfreq[i];
-    for (int i = 0; i < D_CODES; i++) s.dfc[i] = (uint16_t)s.dfreq[i];
+  ZD_ADD(0, tz);
+  if (lane < TB && ttype[lane] >= 0) {
+    TreeLds& s = *(TreeLds*)(raw + lane * TSTRIDE);
+    ZBlock* B = a.blk + blockIdx.x * TB + lane;
     s.opt_len = s.static_len = 0;
-    ZD_ADD(0, tz);
     int lmax = build_tree(s, s.fc, s.dl, L_CODES, 0);
     ZD_ADD(1, tz);
     int dmax = build_tree(s, s.dfc, s.ddl, D_CODES, 1);
     scan_tree(s, s.dl, lmax);
     scan_tree(s, s.ddl, dmax);
-    for (int i = 0; i < BL_CODES; i++) s.bfc[i] = (uint16_t)s.bfreq[i];
+    for (int i = 0; i < BL_CODES; i++) s.bfc[i] = s.bfreq[i];
     build_tree(s, s.bfc, s.bdl, BL_CODES, 2);
     int max_blindex;
     for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
@@ -864,18 +908,21 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     B->lcodes = lmax + 1;
     B->dcodes = dmax + 1;
     B->blcodes = max_blindex + 1;
+    ttype[lane] = (int)type;
     ZD_ADD(3, tz);
   }
   __syncthreads();
-  uint32_t* tab = a.tabs + (uint64_t)bi * TAB_WORDS;
-  if (B->type == 2) {
+  for (int t = 0; t < TB; t++) {
+    if (ttype[t] != 2) continue;
+    const TreeLds& s = *(const TreeLds*)(raw + t * TSTRIDE);
+    uint32_t* tab = a.tabs + (uint64_t)(blockIdx.x * TB + t) * TAB_WORDS;
     for (int i = lane; i < L_CODES; i += 64) tab[i] = s.fc[i] | ((uint32_t)s.dl[i] << 16);
     if (lane < D_CODES) tab[L_CODES + lane] = s.dfc[lane] | ((uint32_t)s.ddl[lane] << 16);
     if (lane < BL_CODES) tab[L_CODES + D_CODES + lane] = s.bfc[lane] | ((uint32_t)s.bdl[lane] << 16);
   }
   ZD_ADD(4, tz);
 #ifdef XCG_ZD_TIMING
-  if (lane == 0) atomicAdd(&g_zd_t[15], 1ull);
+  if (lane == 0) atomicAdd(&g_zd_t[14], 1ull);
 #endif
 }
 
@@ -1177,6 +1224,9 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
     }
     ZD_ADD(10, tz);
   }
+#ifdef XCG_ZD_TIMING
+  if (lane == 0) atomicAdd(&g_zd_t[15], 1ull);
+#endif
   if (k == r.nblocks - 1 && lane == 0) {
     if (last) {   // Z_FINISH: adler32 trailer, big-endian (putShortMSB x2)
       uint64_t b = r.end_bit >> 3;
@@ -1390,7 +1440,7 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
   if (mtiles) hipLaunchKernelGGL(zd_match_kernel, dim3(mtiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zd_scan_kernel, dim3(n), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(zd_trees_kernel, dim3(bo), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zd_trees_kernel, dim3((bo + TB - 1) / TB), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_layout_kernel, dim3(n), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_commit_kernel, dim3(8, n), dim3(256), 0, st, a);
