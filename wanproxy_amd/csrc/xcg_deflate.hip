@@ -250,7 +250,7 @@ __device__ __forceinline__ uint32_t call_of_wave(const uint32_t* starts, uint32_
   return lo;
 }
 
-constexpr uint32_t HGROUPS = 16;   // hash groups per wave (a call has > 512 groups: at most two calls)
+constexpr uint32_t HGROUPS = 8;    // hash groups per wave (a call has > 512 groups: at most two calls)
 __global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, const uint32_t* gstart) {
   const uint32_t g0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * HGROUPS;   // this wave's first group
   const uint32_t total = gstart[n];
@@ -261,22 +261,31 @@ __global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, con
   const ZCall cA = a.calls[c0];
   const ZCall cB = (split < g0 + HGROUPS && c0 + 1 < n) ? a.calls[c0 + 1] : cA;
   const int64_t jloA = first_valid(a.st[cA.stream]), jloB = first_valid(a.st[cB.stream]);
-  uint32_t w[HGROUPS];
-  uint64_t xo[HGROUPS];
-  int64_t jv[HGROUPS], je[HGROUPS];
-#pragma unroll
-  for (uint32_t k = 0; k < HGROUPS; k++) {   // all loads first
+  // per group (wave-uniform): the call's X base, the group's first position, the call's end
+  auto group = [&](uint32_t k, const uint8_t*& x, int32_t& g, int32_t& jend) {
     const uint32_t gid = g0 + k;
     const bool B = gid >= split;
-    xo[k] = B ? cB.x_off : cA.x_off;
-    jv[k] = (B ? jloB : jloA) + 64ll * (gid - (B ? split : s0)) + lane;
-    je[k] = gid < total ? (int64_t)WSIZE + (B ? cB.len : cA.len) : 0;
-    w[k] = jv[k] + 2 < je[k] ? *(const u32_u*)(a.X + xo[k] + jv[k]) : 0u;
+    x = a.X + (B ? cB.x_off : cA.x_off);
+    g = (int32_t)((B ? jloB : jloA) + 64ll * (gid - (B ? split : s0)));
+    jend = gid < total ? WSIZE + (int32_t)(B ? cB.len : cA.len) : 0;
+  };
+  uint32_t w[HGROUPS];
+#pragma unroll
+  for (uint32_t k = 0; k < HGROUPS; k++) {   // all loads first
+    const uint8_t* x;
+    int32_t g, jend;
+    group(k, x, g, jend);
+    const int32_t j = g + lane;
+    w[k] = j + 2 < jend ? *(const u32_u*)(x + j) : 0u;
   }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
   for (uint32_t k = 0; k < HGROUPS; k++) {
-    const int64_t j = jv[k];
-    const bool valid = j + 2 < je[k];
+    const uint8_t* x;
+    int32_t g, jend;
+    group(k, x, g, jend);
+    const int32_t j = g + lane;
+    const bool valid = j + 2 < jend;
     uint32_t h = 0x8000u;    // invalid lanes form their own class
     if (valid) h = (((w[k] & 0xff) << 10) ^ (((w[k] >> 8) & 0xff) << 5) ^ ((w[k] >> 16) & 0xff)) & 0x7fffu;
     uint64_t m = ballot(valid);
@@ -286,11 +295,11 @@ __global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, con
       const uint64_t bl = ballot(bit);
       m &= bit ? bl : ~bl;
     }
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t lower = m & below;
     const uint32_t pd = lower ? (uint32_t)(lane - (63 - __clzll(lower))) : 0u;
     const uint32_t last = (m >> lane) == 1ull ? 1u : 0u;
-    if (j < je[k]) a.pk[xo[k] + j] = (h & 0x7fffu) | (pd << 15) | (last << 21) | ((valid ? 1u : 0u) << 22);
+    if (j < jend)
+      a.pk[(uint64_t)(x - a.X) + j] = (h & 0x7fffu) | (pd << 15) | (last << 21) | ((valid ? 1u : 0u) << 22);
   }
 }
 
