@@ -23,3 +23,5 @@ for k in range(2):
     nb, nw = max(1, int(t[15])), max(1, int(t[14]))
     print(f'step {k}: wall {dt*1e3:.1f} ms, {nb} blocks, {nw} tree waves; cycles per tree wave / emit block:',
           {n: int(t[i]) // (nw if n.startswith('tr') else nb) for i, n in names.items()})
+    nc = max(1, int(t[12]))
+    print(f'  scan per call: slow iterations {int(t[5]) // nc}, fast runs {int(t[6]) // nc} covering {int(t[7]) // nc} positions, cycles {int(t[11]) // nc}')

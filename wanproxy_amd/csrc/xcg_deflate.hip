@@ -447,6 +447,23 @@ __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
   a.tq[c.t_off + rel] = eq;
 }
 
+#ifdef XCG_ZD_TIMING
+// diagnostics build: wave cycles per phase summed over blocks (trees: histogram,
+// literal tree, distance + bit-length trees, bit count, tables; emit: tables and
+// header, sizing pass, packing pass; scan: loop tops, literal runs and their positions,
+// cycles) and block / call counts
+__device__ unsigned long long g_zd_t[16];
+#define ZD_NOW() __builtin_readcyclecounter()
+#define ZD_ADD(i, t0)                                                         \
+  do {                                                                        \
+    uint64_t t1_ = ZD_NOW();                                                  \
+    if (threadIdx.x == 0) atomicAdd(&g_zd_t[i], (unsigned long long)(t1_ - (t0))); \
+    t0 = t1_;                                                                 \
+  } while (0)
+#else
+#define ZD_NOW() 0ull
+#define ZD_ADD(i, t0) (void)(t0)
+#endif
 // ------------------------------------------------------------------- lazy scan
 struct ScanWin {
   uint32_t tf, tq, x;   // lane l: entries of position w + l, X byte w - 1 + l
@@ -489,6 +506,9 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
   int64_t w = p;
   load_win(W, a, c, w);
   load_win(N, a, c, w + 64);
+#ifdef XCG_ZD_TIMING
+  uint64_t n_fast = 0, n_slow = 0, n_fastpos = 0, t_scan = ZD_NOW();
+#endif
 
   auto flush = [&](int64_t q, bool last) {
     if (lane == 0) {
@@ -571,12 +591,19 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
           nsym += (uint32_t)k;
           if (sb_n >= 2048) sflush();
           p = stop;
+#ifdef XCG_ZD_TIMING
+          n_fast++;
+          n_fastpos += (uint64_t)k;
+#endif
           if (nsym == SYMS_PER_BLOCK) flush(p - 1, false);
           continue;
         }
       }
     }
     // one loop top of deflate_slow at p
+#ifdef XCG_ZD_TIMING
+    n_slow++;
+#endif
     const uint32_t ef = readlane(W.tf, li), dd = readlane(W.d, li);
     const int64_t la = rd - p;
     int prev_length = ml;
@@ -611,6 +638,15 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
   }
   if (avail) put(a.X[c.x_off + p - 1]);
   sflush();
+#ifdef XCG_ZD_TIMING
+  if (lane == 0) {
+    atomicAdd(&g_zd_t[5], (unsigned long long)n_slow);
+    atomicAdd(&g_zd_t[6], (unsigned long long)n_fast);
+    atomicAdd(&g_zd_t[7], (unsigned long long)n_fastpos);
+    atomicAdd(&g_zd_t[11], (unsigned long long)(ZD_NOW() - t_scan));
+    atomicAdd(&g_zd_t[12], 1ull);
+  }
+#endif
   if (finish) flush(p, true);
   else if (nsym) flush(p, false);
   if (lane == 0) {
@@ -623,22 +659,6 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
 }
 
 // ------------------------------------------------------------------- trees
-#ifdef XCG_ZD_TIMING
-// diagnostics build: wave cycles per phase summed over blocks (trees: histogram,
-// literal tree, distance + bit-length trees, bit count, tables; emit: tables and
-// header, sizing pass, packing pass) and block counts
-__device__ unsigned long long g_zd_t[16];
-#define ZD_NOW() __builtin_readcyclecounter()
-#define ZD_ADD(i, t0)                                                         \
-  do {                                                                        \
-    uint64_t t1_ = ZD_NOW();                                                  \
-    if (threadIdx.x == 0) atomicAdd(&g_zd_t[i], (unsigned long long)(t1_ - (t0))); \
-    t0 = t1_;                                                                 \
-  } while (0)
-#else
-#define ZD_NOW() 0ull
-#define ZD_ADD(i, t0) (void)(t0)
-#endif
 // Heap entries are freq << 15 | depth << 10 | node: trees.c's smaller(n, m)
 // (freq, then depth <=) is `key(n) <= key(m)` on key = entry >> 10, so a
 // downheap step is one 8-byte LDS read of both children.  A block holds at
