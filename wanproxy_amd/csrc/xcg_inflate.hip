@@ -581,20 +581,35 @@ __global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
 
 // adler32 of each call's output, combined into the stream's; the trailer
 // check (one wave per call)
-__global__ __launch_bounds__(64) void zi_adler_kernel(IArgs a) {
+// adler32 of the call's output (four waves per call, consecutive 4-byte words:
+// coalesced), combined with the stream's, checked against a trailer.
+__global__ __launch_bounds__(256) void zi_adler_kernel(IArgs a) {
+  __shared__ uint64_t red[2][4];
   const uint32_t ci = blockIdx.x;
   const ICall c = a.calls[ci];
   IRes r = a.res[ci];
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
   IState* sp = a.st + c.stream;
   if (r.status >= 0) {
     const uint8_t* d = a.out + c.out_off;
     const uint64_t n = r.out_len;
-    uint64_t A = 0, B = 0;
-    uint64_t chunk = (n + 63) / 64;
-    uint64_t s = (uint64_t)lane * chunk, e = s + chunk < n ? s + chunk : n;
-    for (uint64_t i = s; i < e; i++) {
-      uint32_t v = d[i];
+    uint64_t A = 0, B = 0;   // sum d_i, sum i * d_i, reduced mod 65521 every 4096 words
+    const uint64_t words = n / 4;
+    uint32_t since = 0;
+#pragma unroll 4
+    for (uint64_t w = t; w < words; w += 256) {
+      const uint32_t v = *(const u32_u*)(d + 4 * w);
+      const uint32_t s = (v & 0xff) + ((v >> 8) & 0xff) + ((v >> 16) & 0xff) + (v >> 24);
+      A += s;
+      B += (4 * w) * s + ((v >> 8) & 0xff) + 2 * ((v >> 16) & 0xff) + 3 * (v >> 24);
+      if (++since == 4096) {
+        A %= 65521u;
+        B %= 65521u;
+        since = 0;
+      }
+    }
+    for (uint64_t i = 4 * words + t; i < n; i += 256) {
+      const uint32_t v = d[i];
       A += v;
       B += i * v;
     }
@@ -605,10 +620,18 @@ __global__ __launch_bounds__(64) void zi_adler_kernel(IArgs a) {
       B += __shfl_xor(B, o);
     }
     if (lane == 0) {
+      red[0][t >> 6] = A;
+      red[1][t >> 6] = B;
+    }
+  }
+  __syncthreads();
+  if (t == 0 && r.status >= 0) {
+    const uint64_t n = r.out_len;
+    uint64_t A = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) % 65521u;
+    uint64_t B = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) % 65521u;
+    {
       uint32_t old = sp->adler;
       uint64_t s1 = old & 0xffff, s2 = old >> 16, nn = n % 65521u;
-      A %= 65521u;
-      B %= 65521u;
       uint64_t ns1 = (s1 + A) % 65521u;
       uint64_t ns2 = (s2 + nn * s1 + nn * A + 65521u - B) % 65521u;
       uint32_t ad = (uint32_t)((ns2 << 16) | ns1);
@@ -619,7 +642,7 @@ __global__ __launch_bounds__(64) void zi_adler_kernel(IArgs a) {
       }
     }
   }
-  if (lane == 0) {
+  if (t == 0) {
     a.res[ci] = r;
     a.out_len[ci] = r.out_len;
     a.status[ci] = r.status;
@@ -749,7 +772,7 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 255) / 256);
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zi_inflate_kernel, dim3(n), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
   return XCG_OK;
