@@ -405,11 +405,13 @@ __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
     int64_t cur = j - d;
     int best = 0, bq = -1;
     int64_t bs = 0, bsq = 0;
-    const uint32_t x01 = X[j] | ((uint32_t)X[j + 1] << 8);
+    const uint32_t x01 = *(const u16_u*)(X + j);
     int count = 0;
     for (;;) {
+      // the next link is loaded with the candidate's bytes (both depend on cur only)
+      const uint32_t dd = d16[cur];
       // longest_match: reject on bytes 0, 1 (and at best_len), then compare
-      if ((X[cur] | ((uint32_t)X[cur + 1] << 8)) == x01 && (best < 3 || X[cur + best] == X[j + best])) {
+      if (*(const u16_u*)(X + cur) == x01 && (best < 3 || X[cur + best] == X[j + best])) {
         int len = 2;
         while (len < cap) {
           uint32_t w = ld32(X + cur + len) ^ ld32(X + j + len);
@@ -431,7 +433,6 @@ __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
         bsq = bs;
       }
       if (count >= budget) break;
-      uint32_t dd = d16[cur];
       if (dd == 0) break;
       cur -= dd;
       if (cur <= limit) break;

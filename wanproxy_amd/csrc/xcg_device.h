@@ -24,6 +24,7 @@ constexpr uint32_t CLO = 0x80200400u;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(1))) u32x4_u;   // unaligned 16-B global access
 typedef uint32_t __attribute__((aligned(1))) u32_u;
+typedef uint16_t __attribute__((aligned(1))) u16_u;
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
