@@ -32,9 +32,9 @@ namespace xcg {
 namespace zi {
 
 constexpr int WSIZE = 32768;
-constexpr uint32_t RMASK = 8191;    // LDS ring of the last 8 KiB of output
-constexpr uint32_t NEAR = 4096;     // matches up to this distance copy inside the ring
-constexpr uint32_t FLUSH_AT = 2048; // output is flushed to HBM every 2 KiB
+constexpr uint32_t RMASK = 4095;    // LDS ring of the last 4 KiB of output
+constexpr uint32_t NEAR = 2048;     // matches up to this distance copy inside the ring
+constexpr uint32_t FLUSH_AT = 1024; // output is flushed to HBM every 1 KiB
 constexpr int PEND_CAP = 1024;
 constexpr int PRI = 9;              // primary table bits
 constexpr int IPAD = 512;           // zero bytes after a call's input in the scratch
@@ -108,7 +108,7 @@ struct TreeT {
 };
 // literal/length codes of skewed blocks run to 10-12 bits: an 11-bit primary
 // table keeps them off the canonical path; ~39 KiB of LDS in all (4 waves/CU)
-typedef TreeT<11, 288> LTree;
+typedef TreeT<10, 288> LTree;
 typedef TreeT<PRI, 32> DTree;
 typedef TreeT<7, 20> CTree;
 
