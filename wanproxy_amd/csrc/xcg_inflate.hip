@@ -235,7 +235,7 @@ __device__ unsigned long long g_zi_t[10];
 #define ZT_ADD(i, t0) (void)(t0)
 #endif
 
-__global__ __launch_bounds__(64) void zi_inflate_kernel(IArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi_inflate_kernel(IArgs a) {
 #ifdef XCG_ZI_TIMING
   uint64_t zt[10] = {0};
 #endif
