@@ -106,8 +106,9 @@ struct TreeT {
   uint16_t cnt[16];
   uint16_t sym[NS];         // symbols in canonical order (by length, then value)
 };
-// literal/length codes of skewed blocks run to 10-12 bits: an 11-bit primary
-// table keeps them off the canonical path; ~39 KiB of LDS in all (4 waves/CU)
+// literal/length codes of skewed blocks run to 10-12 bits: a 10-bit primary
+// table keeps most of them off the canonical path while a stream's LDS stays at
+// ~9.5 KiB (16 streams per CU, all 4096 of a batch resident at once)
 typedef TreeT<10, 288> LTree;
 typedef TreeT<PRI, 32> DTree;
 typedef TreeT<7, 20> CTree;
