@@ -204,3 +204,24 @@ def test_inflate_errors():
     assert got[1][0] == (b'', -1)
     assert got[2][0][1] == -1
     assert got[3][0] == (b'payload ' * 100, 1) and got[3][1] == (b'', 1)
+
+
+def test_distance_boundaries_both_ways():
+    """Back-references at distances around the inflate ring's limits (near copies
+    up to 2 KiB, ring 4 KiB, flush every 1 KiB) and zlib's own (258, 32 KiB
+    window): GPU deflate equals zlib call by call, and GPU inflate decodes
+    zlib's level-9 stream of the same data, cut at random points."""
+    rng = random.Random(90)
+    dists = [1, 2, 3, 257, 258, 259, 1023, 1024, 1025, 2047, 2048, 2049, 3000, 4095, 4096, 4097,
+             6000, 8191, 8192, 8193, 16384, 32506, 32507, 32767]
+    parts = []
+    for d in dists:
+        base = rng.randbytes(d)
+        parts.append(base + base[:rng.choice([3, 17, 258, 600])] + rng.randbytes(37))
+    data = b''.join(parts)
+    calls = [data[i:i + 50000] for i in range(0, len(data), 50000)] + [b'']
+    check_vs_zlib({6: [calls], 9: [calls]})
+    z = zlib.compress(data, 9)
+    got = inflate_streams([cuts(rng, z, 'random') + [b'']])[0]
+    assert b''.join(o for o, _ in got) == data
+    assert got[-1][1] == 1
