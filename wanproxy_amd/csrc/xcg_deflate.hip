@@ -150,22 +150,28 @@ struct ZArgs {
 };
 
 // ------------------------------------------------------------------- prep
-// X = history ++ data ++ zero pad.  Grid: (tiles of 4 KiB, calls).
+// X = history ++ data ++ zero pad, 16 bytes per thread (X and the history are
+// 256-byte aligned; WSIZE and XPAD are multiples of 16, so only the vector at
+// the data's end is assembled bytewise).  Grid: (tiles of 4 KiB, calls).
 __global__ __launch_bounds__(256) void zd_prep_kernel(ZArgs a) {
   const ZCall c = a.calls[blockIdx.y];
-  uint64_t span = (uint64_t)WSIZE + c.len + XPAD;
+  const uint64_t dend = (uint64_t)WSIZE + c.len, nv = (dend + XPAD + 15) / 16;
   uint8_t* X = a.X + c.x_off;
   const uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
   const uint8_t* d = a.in + c.in_off;
-  for (uint64_t j = (uint64_t)blockIdx.x * 4096 + threadIdx.x; j < span; j += (uint64_t)gridDim.x * 4096) {
-    for (int k = 0; k < 16; k++) {
-      uint64_t q = j + (uint64_t)k * 256;
-      if (q >= span) break;
-      uint8_t v = 0;
-      if (q < WSIZE) v = h[q];
-      else if (q < (uint64_t)WSIZE + c.len) v = d[q - WSIZE];
-      X[q] = v;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * 256) {
+    const uint64_t q = 16 * v;
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (q < WSIZE) {
+      r = *(const u32x4*)(h + q);
+    } else if (q + 16 <= dend) {
+      r = *(const u32x4_u*)(d + (q - WSIZE));
+    } else if (q < dend) {
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      for (uint64_t k = 0; q + k < dend; k++) w[k >> 2] |= (uint32_t)d[q + k - WSIZE] << (8 * (k & 3));
+      r = u32x4{w[0], w[1], w[2], w[3]};
     }
+    *(u32x4*)(X + q) = r;
   }
 }
 
