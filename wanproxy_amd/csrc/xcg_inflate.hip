@@ -84,18 +84,30 @@ struct IArgs {
   int32_t* status;
 };
 
-// carried bytes ++ new input into the scratch (grid: tiles, calls)
+// carried bytes ++ new input into the scratch, 16 bytes per thread (the
+// scratch slot is 256-byte aligned; vectors straddling the carried / new /
+// pad boundaries are assembled bytewise).  Grid: (tiles, calls).
 __global__ __launch_bounds__(256) void zi_prep_kernel(IArgs a) {
   const ICall c = a.calls[blockIdx.y];
   const IState* s = a.st + c.stream;
-  const uint32_t np = s->npend;
+  const uint64_t np = s->npend, dend = np + c.len;
   uint8_t* I = a.I + c.i_off;
-  const uint64_t span = (uint64_t)np + c.len + IPAD;
-  for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < span; q += (uint64_t)gridDim.x * 256) {
-    uint8_t v = 0;
-    if (q < np) v = s->pend[q];
-    else if (q < (uint64_t)np + c.len) v = a.in[c.in_off + q - np];
-    I[q] = v;
+  const uint8_t* d = a.in + c.in_off;
+  const uint64_t nv = (dend + IPAD + 15) / 16;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * 256) {
+    const uint64_t q = 16 * v;
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (q >= np && q + 16 <= dend) {
+      r = *(const u32x4_u*)(d + (q - np));
+    } else if (q < dend) {
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      for (uint64_t k = 0; k < 16 && q + k < dend; k++) {
+        const uint64_t x = q + k;
+        w[k >> 2] |= (uint32_t)(x < np ? s->pend[x] : d[x - np]) << (8 * (k & 3));
+      }
+      r = u32x4{w[0], w[1], w[2], w[3]};
+    }
+    *(u32x4*)(I + q) = r;
   }
 }
 
@@ -770,7 +782,7 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.res = (IRes*)(z->scratch + o_res);
   a.out_len = d_out_len;
   a.status = d_status;
-  uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 255) / 256);
+  uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 4095) / 4096);   // 4 KiB per block
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zi_inflate_kernel, dim3(n), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(256), 0, st, a);
