@@ -857,7 +857,6 @@ __device__ void scan_tree(TreeLds& s, const uint16_t* dl, int max_code) {
 // instead of one), then the code tables leave with the whole wave.
 __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[TB * TSTRIDE];
-  __shared__ uint32_t hist[L_CODES + D_CODES];
   __shared__ int ttype[TB];
   const int lane = threadIdx.x;
   const uint32_t nrec = a.bstart[a.n];
@@ -870,6 +869,7 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
     const ZCall c = a.calls[ci];
     if (bi - c.blk_off >= a.res[ci].nblocks) continue;
     TreeLds& s = *(TreeLds*)(raw + t * TSTRIDE);
+    uint32_t* hist = s.heap;   // the symbol counts live in the block's heap until build_tree
     for (int i = lane; i < L_CODES + D_CODES; i += 64) hist[i] = 0;
     __syncthreads();
     const ZBlock* B = a.blk + bi;
