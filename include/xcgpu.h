@@ -110,16 +110,38 @@ int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_lim
  * disk_bytes (xcodec/xcodec_cache_disk.cc: FIFO data blocks in index blocks
  * of 204 entries, (disk_bytes / 2048 - 18) / 205 index blocks).  A lookup
  * that misses the primary and hits the disk enters the hash into the primary;
- * a primary hit re-enters a hash the disk index lost.  XCG_SEM_STREAM batches
- * are bit-exact with the sequential XCodecEncoder on such a pair; the disk
- * level lives in HBM (its bytes, and the index as a GPU table).  In-band only
- * (XCG_EINVAL with XCG_FLAG_OOB / XCG_FLAG_NULLCACHE, or a volume without one
- * index block).  Decode batches and the single-segment host calls return
- * XCG_ENOTSUP on a pair context. */
+ * a primary hit re-enters a hash the disk index lost.  XCG_SEM_STREAM batches,
+ * decode batches and the single-segment host calls are bit-exact with the
+ * sequential XCodecEncoder / XCodecDecoder on such a pair; the disk level lives
+ * in HBM (its bytes, and the index as a GPU table).  In-band only (XCG_EINVAL
+ * with XCG_FLAG_OOB / XCG_FLAG_NULLCACHE, or a volume without one index
+ * block).  XCG_ENOTSUP (never a different result): a decode batch in which a
+ * hash it EXTRACTed leaves both levels before a later op names it (decode it
+ * in smaller batches), BACKREF ops.  Decode chunks of a bounded or pair
+ * context are < 2 MiB each (XCG_EINVAL). */
 int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
                         xcg_ctx **out);
-/* Pair context counters: st[0] primary entries, st[1] disk index entries,
- * st[2] disk entries written so far, st[3] disk index blocks. */
+/* One XCodecDisk shared by several pairs (xcodec/xcodec_cache_disk.h:33-69):
+ * its FIFO ring is common to every XCodecDiskCache front-end on it -- the
+ * local cache (XCodecDisk::local) and each peer cache XCodecCache::connect
+ * makes on it (XCodecDisk::connect, xcodec_cache_disk.cc:640-690) -- and when
+ * the write head enters an index block, every front loses its entries there
+ * (index_invalidate_entries, :327-382).  xcg_ctx_create_pair_on makes a pair
+ * context whose secondary is the next front (xuid) of `disk`; its cache
+ * references then interleave with the other fronts' in one ring, in the order
+ * the calls are made (the reference serialises them on its event thread).
+ * The disk lives until its last front and xcg_disk_destroy are gone.
+ * xcg_disk_stats: st[0] live index entries (all fronts), st[1] entries
+ * written, st[2] index blocks, st[3] fronts. */
+typedef struct xcg_disk xcg_disk;
+int xcg_disk_create(uint64_t disk_bytes, xcg_disk **out);
+void xcg_disk_destroy(xcg_disk *disk);
+int xcg_disk_stats(const xcg_disk *disk, uint64_t *st);
+int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,
+                           xcg_ctx **out);
+/* Pair context counters: st[0] primary entries, st[1] this front's disk index
+ * entries, st[2] disk entries written so far (all fronts), st[3] disk index
+ * blocks. */
 int xcg_pair_stats(xcg_ctx *ctx, uint64_t *st);
 void xcg_ctx_destroy(xcg_ctx *ctx);
 /* The XCG_FLAG_* the context was created with. */
@@ -133,7 +155,11 @@ int xcg_last_rounds(xcg_ctx *ctx);
 /* Single-segment host access to the persistent cache, for host adapters:
  * XCodecCache::lookup (xcodec/xcodec_cache.h:86) copies the 2048 bytes out
  * (XCG_ENOENT if absent); XCodecCache::enter/replace (:84-85) -- an existing
- * hash has its bytes replaced. */
+ * hash has its bytes replaced.  On bounded and pair caches these are the
+ * reference's calls with their side effects (LRU use; a pair's disk touch or
+ * promotion), and enter is <LEARN>'s lookup-then-replace-or-enter
+ * (xcodec/xcodec_pipe_pair.cc:311-327); on a pair, `hash` must be the
+ * segment's XCodecHash (XCG_EINVAL otherwise). */
 int xcg_cache_lookup_host(xcg_ctx *ctx, uint64_t hash, uint8_t *seg_out);
 int xcg_cache_enter_host(xcg_ctx *ctx, uint64_t hash, const uint8_t *seg);
 /* Declarations (hash, position in the chunk) chunk `chunk` of the last
@@ -334,6 +360,9 @@ int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in
 typedef struct xcg_zinflate xcg_zinflate;
 int xcg_zinflate_create(int device, uint32_t nstreams, xcg_zinflate **out);
 void xcg_zinflate_destroy(xcg_zinflate *z);
+/* The slot becomes a fresh InflatePipe (inflateInit): every InflatePipe
+ * construction on a reused slot calls it, as DeflatePipe does xcg_zdeflate_reset. */
+int xcg_zinflate_reset(xcg_zinflate *z, uint32_t stream);
 int xcg_zinflate_batch(xcg_zinflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
                        const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
                        const uint32_t *h_out_cap, uint32_t *d_out_len, int32_t *d_status, void *stream);

@@ -1,0 +1,219 @@
+/*
+ * xcgpu_binding.cc -- the GPU mirror of a reference XCodecCache object, with
+ * the geometry read from the object itself.
+ *
+ * The cache classes keep their configuration private: XCodecMemoryCache's
+ * memory_cache_limit_ (xcodec/xcodec_cache.h:276), XCodecCachePair's levels
+ * (:141-142), XCodecDiskCache's disk (xcodec/xcodec_cache_disk.h:94-99) and
+ * XCodecDisk's volume size (:38).  The reference headers are unchanged, so the
+ * binding reads those members through explicit template instantiations --
+ * the one place C++ waives access checking ([temp.explicit]) -- instead of
+ * asking wanproxy's config code to repeat them.  That is what makes caches
+ * created by XCodecCache::connect (xcodec/xcodec_cache.h:101-111: a bounded
+ * memory cache of the parent's limit, :297-301; a pair of connected levels,
+ * :158-161) mirror with their real geometry: the decoding side of every pipe
+ * pair (xcodec/xcodec_pipe_pair.cc:203) gets its caches that way.
+ */
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <typeinfo>
+
+#include <common/buffer.h>
+
+#include <xcodec/xcodec.h>
+#include <xcodec/xcodec_cache.h>
+#include <xcodec/xcodec_cache_disk.h>
+
+#include "xcgpu_binding.h"
+
+namespace {
+
+/* Member<Tag, &Class::member> defines member_of(Tag) returning the member
+ * pointer; the explicit instantiations below name the private members. */
+template <typename Tag, typename Tag::type M>
+struct Member {
+	friend typename Tag::type member_of(Tag) { return M; }
+};
+
+struct MemoryLimit {
+	typedef size_t XCodecMemoryCache::*type;
+	friend type member_of(MemoryLimit);
+};
+struct PairPrimary {
+	typedef XCodecCache *XCodecCachePair::*type;
+	friend type member_of(PairPrimary);
+};
+struct PairSecondary {
+	typedef XCodecCache *XCodecCachePair::*type;
+	friend type member_of(PairSecondary);
+};
+struct DiskOf {
+	typedef XCodecDisk *XCodecDiskCache::*type;
+	friend type member_of(DiskOf);
+};
+struct DiskBlocks {
+	typedef uint64_t XCodecDisk::*type;
+	friend type member_of(DiskBlocks);
+};
+
+template struct Member<MemoryLimit, &XCodecMemoryCache::memory_cache_limit_>;
+template struct Member<PairPrimary, &XCodecCachePair::primary_>;
+template struct Member<PairSecondary, &XCodecCachePair::secondary_>;
+template struct Member<DiskOf, &XCodecDiskCache::disk_>;
+template struct Member<DiskBlocks, &XCodecDisk::disk_blocks_>;
+
+xcgpu_binding::DiskResolver& resolver()
+{
+	static xcgpu_binding::DiskResolver fn = NULL;
+	return fn;
+}
+
+std::map<XCodecCache *, xcg_ctx *>& ctx_map()
+{
+	static std::map<XCodecCache *, xcg_ctx *> ctxs;
+	return ctxs;
+}
+
+std::map<XCodecCache *, std::string>& refusals()
+{
+	static std::map<XCodecCache *, std::string> r;
+	return r;
+}
+
+/* One engine disk per XCodecDisk (XCodecDisk::open shares one disk per path,
+ * xcodec_cache_disk.cc:826-838); kept for the life of the process, as the
+ * reference's disk_map keeps its disks. */
+std::map<const void *, xcg_disk *>& disk_map()
+{
+	static std::map<const void *, xcg_disk *> disks;
+	return disks;
+}
+
+/* The XCodecDisk under a disk level, and its volume size. */
+bool disk_of(XCodecCache *level, const void **disk, uint64_t *bytes)
+{
+	if (resolver() != NULL && resolver()(level, disk, bytes))
+		return true;
+	XCodecDiskCache *front = dynamic_cast<XCodecDiskCache *>(level);
+	if (front == NULL)
+		return false;
+	XCodecDisk *d = front->*member_of(DiskOf());
+	*disk = d;
+	*bytes = (d->*member_of(DiskBlocks())) * (uint64_t)XCG_SEGMENT_LENGTH;
+	return true;
+}
+
+}  // namespace
+
+namespace xcgpu_binding {
+
+void set_disk_resolver(DiskResolver fn)
+{
+	resolver() = fn;
+}
+
+Geometry geometry_of(XCodecCache *cache)
+{
+	Geometry g = { KIND_UNSUPPORTED, 0, NULL, 0, "a cache class the MI355X engine does not mirror" };
+	if (strstr(typeid(*cache).name(), "NullCache") != NULL) {
+		g.kind = KIND_NULL;
+		return g;
+	}
+	XCodecMemoryCache *m = dynamic_cast<XCodecMemoryCache *>(cache);
+	if (m != NULL) {
+		const size_t limit = m->*member_of(MemoryLimit());
+		g.kind = limit != 0 ? KIND_BOUNDED : KIND_MEMORY;
+		g.limit_bytes = (uint64_t)limit * XCG_SEGMENT_LENGTH;
+		return g;
+	}
+	XCodecCachePair *p = dynamic_cast<XCodecCachePair *>(cache);
+	if (p == NULL)
+		return g;
+	XCodecMemoryCache *primary = dynamic_cast<XCodecMemoryCache *>(p->*member_of(PairPrimary()));
+	if (primary == NULL) {
+		g.why = "an XCodecCachePair whose primary is not an XCodecMemoryCache";
+		return g;
+	}
+	const size_t limit = primary->*member_of(MemoryLimit());
+	if (!disk_of(p->*member_of(PairSecondary()), &g.disk, &g.disk_bytes)) {
+		g.why = "an XCodecCachePair whose secondary is not a disk cache";
+		return g;
+	}
+	if (limit == 0) {
+		/* An unbounded primary never evicts: every lookup the pair makes is
+		 * answered by the primary (xcodec_cache.h:217-221), so its visible
+		 * contents -- all the encoder and decoder depend on -- are an
+		 * unbounded memory cache's. */
+		g.kind = KIND_MEMORY;
+		return g;
+	}
+	g.kind = KIND_PAIR;
+	g.limit_bytes = (uint64_t)limit * XCG_SEGMENT_LENGTH;
+	return g;
+}
+
+xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
+{
+	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctx_map().find(cache);
+	if (it != ctx_map().end())
+		return it->second;
+	const Geometry g = geometry_of(cache);
+	if (g.kind == KIND_UNSUPPORTED) {
+		refusals()[cache] = std::string("cache is ") + g.why;
+		return NULL;
+	}
+	uint32_t flags = out_of_band ? XCG_FLAG_OOB : 0;
+	int device = 0;
+	const char *dev = getenv("XCGPU_DEVICE");
+	if (dev != NULL)
+		device = atoi(dev);
+	xcg_ctx *ctx = NULL;
+	int rc;
+	switch (g.kind) {
+	case KIND_NULL:
+		rc = xcg_ctx_create(device, flags | XCG_FLAG_NULLCACHE, &ctx);
+		break;
+	case KIND_BOUNDED:
+		rc = xcg_ctx_create_bounded(device, flags, g.limit_bytes, &ctx);
+		break;
+	case KIND_PAIR: {
+		xcg_disk *&disk = disk_map()[g.disk];
+		rc = XCG_OK;
+		if (disk == NULL)
+			rc = xcg_disk_create(g.disk_bytes, &disk);
+		if (rc == XCG_OK)
+			rc = xcg_ctx_create_pair_on(device, flags, g.limit_bytes, disk, &ctx);
+		break;
+	}
+	default:
+		rc = xcg_ctx_create(device, flags, &ctx);
+		break;
+	}
+	if (rc != XCG_OK) {
+		refusals()[cache] = std::string("MI355X engine: ") + xcg_strerror(rc) + " (XCGPU_DEVICE " +
+		                    std::to_string(device) + ")";
+		return NULL;
+	}
+	ctx_map()[cache] = ctx;
+	refusals().erase(cache);
+	return ctx;
+}
+
+const char *why_not(XCodecCache *cache)
+{
+	std::map<XCodecCache *, std::string>::const_iterator it = refusals().find(cache);
+	return it == refusals().end() ? "no MI355X device for the XCodec engine" : it->second.c_str();
+}
+
+void forget(XCodecCache *cache)
+{
+	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctx_map().find(cache);
+	if (it == ctx_map().end())
+		return;
+	xcg_ctx_destroy(it->second);
+	ctx_map().erase(it);
+}
+
+}  // namespace xcgpu_binding

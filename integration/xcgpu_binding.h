@@ -9,6 +9,15 @@
  * XCodecCache is kept as a mirror of every entry the engine makes, so the rest
  * of wanproxy (ASK/LEARN in xcodec_pipe_pair.cc, other caches) sees exactly the
  * reference's cache contents.
+ *
+ * The GPU mirror takes its geometry from the cache object itself
+ * (xcgpu_binding.cc), whoever made it: wanproxy's cache config, or
+ * XCodecCache::connect on the decoding side of a pipe pair
+ * (xcodec/xcodec_pipe_pair.cc:203 -> xcodec/xcodec_cache.h:101-111), which
+ * makes a bounded XCodecMemoryCache of its parent's limit (:297-301) or a new
+ * XCodecCachePair of connected levels (:158-161).  No registration call is
+ * needed anywhere.  Pairs whose disk levels are front-ends of one XCodecDisk
+ * share one engine disk (xcg_disk): one FIFO ring, as the reference's.
  */
 #ifndef XCGPU_BINDING_H
 #define XCGPU_BINDING_H
@@ -16,7 +25,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include <typeinfo>
 #include <map>
 
 #include "../include/xcgpu.h"
@@ -30,113 +38,46 @@ class XCodecCache;
 
 namespace xcgpu_binding {
 
-/* Cache kinds the engine mirrors exactly: XCodecMemoryCache (unbounded, or
- * bounded via set_cache_limit), XCodecCachePair of a bounded memory cache and
- * the local disk cache (via set_pair_geometry), and tack's TackNullCache
- * (lookups miss). */
-inline bool is_null_cache(XCodecCache *cache)
-{
-	return strstr(typeid(*cache).name(), "NullCache") != NULL;
-}
-
-inline std::map<XCodecCache *, xcg_ctx *>& ctx_map()
-{
-	static std::map<XCodecCache *, xcg_ctx *> ctxs;
-	return ctxs;
-}
-
-inline std::map<XCodecCache *, uint64_t>& limit_map();
-struct PairGeometry;
-inline std::map<XCodecCache *, PairGeometry>& pair_map();
-
-/* The GPU mirror lives as long as the cache object.  wanproxy and tack keep
- * their caches for the life of the process; a caller that deletes a cache
- * must call forget() first (the reference caches have no hook for it). */
-inline void forget(XCodecCache *cache)
-{
-	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctx_map().find(cache);
-	if (it == ctx_map().end())
-		return;
-	xcg_ctx_destroy(it->second);
-	ctx_map().erase(it);
-	limit_map().erase(cache);
-	pair_map().erase(cache);
-}
-
-/* Bounded memory caches: XCodecMemoryCache keeps memory_cache_limit_
- * private (xcodec/xcodec_cache.h:272-288), so the code that makes one with a
- * size (programs/wanproxy/wanproxy_config_class_cache.cc:66) tells the binding:
- * its GPU mirror is then created with xcg_ctx_create_bounded (LRU eviction). */
-inline std::map<XCodecCache *, uint64_t>& limit_map()
-{
-	static std::map<XCodecCache *, uint64_t> limits;
-	return limits;
-}
-
-inline void set_cache_limit(XCodecCache *cache, uint64_t memory_cache_limit_bytes)
-{
-	if (memory_cache_limit_bytes != 0)
-		limit_map()[cache] = memory_cache_limit_bytes;
-}
-
-/* wanproxy.conf's cache pair (XCodecCachePair of a bounded XCodecMemoryCache
- * and the local XCodecDiskCache, programs/wanproxy/wanproxy.conf:8-26): the
- * pair keeps its levels private (xcodec/xcodec_cache.h:140-153), so the code
- * that builds it (wanproxy_config_class_cache.cc) tells the binding the two
- * sizes; the GPU mirror is then an xcg_ctx_create_pair context. */
-struct PairGeometry {
-	uint64_t memory_limit_bytes;
-	uint64_t disk_bytes;
+/* What a cache object is, read from the object (xcgpu_binding.cc). */
+enum CacheKind {
+	KIND_UNSUPPORTED = 0,	/* a cache class the engine does not mirror */
+	KIND_NULL,		/* tack's TackNullCache: lookups miss (programs/tack/tack.cc:70-101) */
+	KIND_MEMORY,		/* XCodecMemoryCache, no limit (xcodec/xcodec_cache.h:245-365) */
+	KIND_BOUNDED,		/* XCodecMemoryCache with a limit: LRU eviction */
+	KIND_PAIR		/* XCodecCachePair(bounded memory, disk front-end) (:140-237) */
 };
 
-inline std::map<XCodecCache *, PairGeometry>& pair_map()
-{
-	static std::map<XCodecCache *, PairGeometry> pairs;
-	return pairs;
-}
+struct Geometry {
+	CacheKind kind;
+	uint64_t limit_bytes;	/* the memory (primary) limit, bytes */
+	const void *disk;	/* KIND_PAIR: identity of the XCodecDisk under the disk level */
+	uint64_t disk_bytes;	/* its volume size */
+	const char *why;	/* KIND_UNSUPPORTED: what is not mirrored */
+};
 
-inline void set_pair_geometry(XCodecCache *cache, uint64_t memory_limit_bytes, uint64_t disk_bytes)
-{
-	PairGeometry g = { memory_limit_bytes, disk_bytes };
-	pair_map()[cache] = g;
-}
+Geometry geometry_of(XCodecCache *cache);
 
-inline bool is_pair(XCodecCache *cache)
-{
-	return pair_map().find(cache) != pair_map().end();
-}
+/*
+ * A disk level class other than XCodecDiskCache (e.g. a test harness's
+ * restatement of XCodecDisk) can be resolved to its disk identity and size by
+ * a resolver; return false for objects it does not know.
+ */
+typedef bool (*DiskResolver)(XCodecCache *level, const void **disk, uint64_t *disk_bytes);
+void set_disk_resolver(DiskResolver fn);
 
-inline xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
+/* The GPU mirror of `cache`, created on first use; NULL if it cannot be made
+ * -- why_not() then says why (the adapters HALT with it). */
+xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band);
+const char *why_not(XCodecCache *cache);
+
+/* The GPU mirror lives as long as the cache object.  wanproxy and tack keep
+ * their caches for the life of the process (XCodecCache::connect's registry
+ * never deletes one); a caller that deletes a cache calls forget() first. */
+void forget(XCodecCache *cache);
+
+inline bool is_null_cache(XCodecCache *cache)
 {
-	std::map<XCodecCache *, xcg_ctx *>& ctxs = ctx_map();
-	std::map<XCodecCache *, xcg_ctx *>::iterator it = ctxs.find(cache);
-	if (it != ctxs.end())
-		return it->second;
-	/* a pair the binding was not told about (e.g. made by XCodecCachePair::
-	 * connect) cannot be mirrored: refuse rather than diverge */
-	if (strstr(typeid(*cache).name(), "XCodecCachePair") != NULL && !is_pair(cache))
-		return NULL;
-	uint32_t flags = out_of_band ? XCG_FLAG_OOB : 0;
-	if (is_null_cache(cache))
-		flags |= XCG_FLAG_NULLCACHE;
-	xcg_ctx *ctx = NULL;
-	int device = 0;
-	const char *dev = getenv("XCGPU_DEVICE");
-	if (dev != NULL)
-		device = atoi(dev);
-	std::map<XCodecCache *, uint64_t>::const_iterator lim = limit_map().find(cache);
-	std::map<XCodecCache *, PairGeometry>::const_iterator pg = pair_map().find(cache);
-	int rc;
-	if (pg != pair_map().end())
-		rc = xcg_ctx_create_pair(device, flags, pg->second.memory_limit_bytes, pg->second.disk_bytes, &ctx);
-	else if (lim != limit_map().end())
-		rc = xcg_ctx_create_bounded(device, flags, lim->second, &ctx);
-	else
-		rc = xcg_ctx_create(device, flags, &ctx);
-	if (rc != XCG_OK)
-		return NULL;
-	ctxs[cache] = ctx;
-	return ctx;
+	return geometry_of(cache).kind == KIND_NULL;
 }
 
 /* One BACKREF window per XCodecDecoder object (the reference's

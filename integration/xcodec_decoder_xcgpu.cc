@@ -122,10 +122,9 @@ mirror_skim(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a)
 /* Decoded size of in[a..) if every op resolves: literal and escaped bytes one
  * each, EXTRACT / REF / BACKREF one segment each (:73-185). */
 static uint64_t
-decoded_bound(const std::vector<uint8_t>& in, uint64_t a)
+decoded_bound(const std::vector<uint8_t>& in, uint64_t a, uint64_t b)
 {
 	uint64_t i = a, n = 0;
-	const uint64_t b = in.size();
 	while (i < b) {
 		const uint8_t *m = (const uint8_t *)memchr(&in[i], XCODEC_MAGIC, b - i);
 		if (m == NULL)
@@ -155,6 +154,72 @@ decoded_bound(const std::vector<uint8_t>& in, uint64_t a)
 	return n;
 }
 
+/*
+ * Cut in[a..) into pieces of whole ops of at most XCGPU_DECODE_PIECE bytes
+ * each (a bounded or pair decode batch numbers ops within 2 MiB chunks); the
+ * pieces of one call form one stream, so the cut changes nothing.  piece[k] is
+ * the start of piece k; the last entry is in.size().
+ */
+#define XCGPU_DECODE_PIECE (1u << 20)
+
+static void
+cut_pieces(const std::vector<uint8_t>& in, uint64_t a, std::vector<uint64_t>& piece)
+{
+	piece.clear();
+	piece.push_back(a);
+	uint64_t i = a;
+	const uint64_t b = in.size();
+	while (i < b) {
+		const uint8_t *m = (const uint8_t *)memchr(&in[i], XCODEC_MAGIC, b - i);
+		uint64_t at = m == NULL ? b : (uint64_t)(m - &in[0]);
+		uint64_t next = at;
+		if (at + 1 < b) {
+			const uint8_t op = in[at + 1];
+			next = at + (op == XCODEC_OP_EXTRACT ? 2 + XCODEC_SEGMENT_LENGTH :
+				     op == XCODEC_OP_REF ? 10 : op == XCODEC_OP_BACKREF ? 3 : 2);
+		} else {
+			next = b;
+		}
+		if (next > b)
+			next = b;
+		/* literal bytes may be cut anywhere outside an op (an ESCAPE is two bytes) */
+		while (at - piece.back() >= XCGPU_DECODE_PIECE) {
+			uint64_t c = piece.back() + XCGPU_DECODE_PIECE;
+			if (c > 0 && in[c - 1] == XCODEC_MAGIC)
+				c--;
+			piece.push_back(c);
+		}
+		if (next - piece.back() > XCGPU_DECODE_PIECE && at > piece.back())
+			piece.push_back(at);
+		i = next;
+	}
+	piece.push_back(b);
+}
+
+/* A cut point strictly inside piece [lo, hi) at an op boundary, or 0. */
+static uint64_t
+split_point(const std::vector<uint8_t>& in, uint64_t lo, uint64_t hi)
+{
+	const uint64_t mid = lo + (hi - lo) / 2;
+	uint64_t i = lo, best = 0;
+	while (i < hi) {
+		const uint8_t *m = (const uint8_t *)memchr(&in[i], XCODEC_MAGIC, hi - i);
+		if (m == NULL)
+			break;
+		const uint64_t at = (uint64_t)(m - &in[0]);
+		if (at > lo && (best == 0 || at <= mid))
+			best = at;
+		if (at > mid && best != 0)
+			break;
+		if (at + 1 >= hi)
+			break;
+		const uint8_t op = in[at + 1];
+		i = at + (op == XCODEC_OP_EXTRACT ? 2 + XCODEC_SEGMENT_LENGTH : op == XCODEC_OP_REF ? 10 :
+			  op == XCODEC_OP_BACKREF ? 3 : 2);
+	}
+	return best;
+}
+
 bool
 XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown_hashes)
 {
@@ -162,17 +227,20 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		return (true);
 	xcg_ctx *ctx = xcgpu_binding::ctx_for(cache_, cache_->out_of_band());
 	if (ctx == NULL)
-		HALT(log_) << "No MI355X device for the XCodec engine.";
+		HALT(log_) << "xcgpu: " << xcgpu_binding::why_not(cache_) << ".";
 	xcg_window *win = xcgpu_binding::window_for(this, ctx);
 	if (win == NULL)
 		HALT(log_) << "No device memory for the XCodec window.";
 
-	const uint32_t len = input->length();
+	const uint64_t len = input->length();
 	std::vector<uint8_t> in(len);
 	input->copyout(&in[0], len);
 	std::vector<uint8_t> out;
 	std::vector<uint64_t> unk(1u << 16);
-	uint64_t pos = 0;
+	std::vector<uint64_t> piece, coff, ooff, olen, cons;
+	std::vector<uint32_t> clen;
+	std::vector<int32_t> cst;
+	uint64_t pos = 0, batch_end = 0;
 	int32_t status = 0;
 	uint32_t nunk = 0;
 	xcg_decode_set_window(ctx, win);
@@ -182,22 +250,66 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	 * (ASK/LEARN, xcodec/xcodec_pipe_pair.cc:274-333) go to the GPU and the
 	 * decode continues from the blocking REF, as decode() itself would with
 	 * those hashes in its cache; what stays unknown is returned like
-	 * decode_skim (:196-272).
+	 * decode_skim (:196-272).  A batch the engine declines (XCG_ENOTSUP: on a
+	 * bounded or pair cache, more cache references than one batch models) is
+	 * decoded as successive smaller batches -- the same stream, so the same
+	 * result.
 	 */
+	cut_pieces(in, pos, piece);
+	size_t k0 = 0, per = piece.size() - 1;
 	for (;;) {
-		const uint64_t off = 0;
-		const uint32_t rest = (uint32_t)(len - pos);
-		uint64_t ooff = 0, olen = 0, consumed = 0;
-		out.resize(decoded_bound(in, pos) + 1);
-		int rc = xcg_decode_host(ctx, &in[pos], rest, &off, &rest, 1, &out[0], out.size(), &ooff, &olen, &status,
-		                         &consumed, &unk[0], unk.size(), &nunk);
+		const size_t k1 = k0 + per < piece.size() - 1 ? k0 + per : piece.size() - 1;
+		const uint32_t n = (uint32_t)(k1 - k0);
+		coff.resize(n); clen.resize(n); ooff.resize(n); olen.resize(n); cons.resize(n); cst.resize(n);
+		for (uint32_t j = 0; j < n; j++) {
+			coff[j] = piece[k0 + j] - pos;
+			clen[j] = (uint32_t)(piece[k0 + j + 1] - piece[k0 + j]);
+		}
+		const uint64_t span = piece[k1] - pos;
+		out.resize(decoded_bound(in, pos, piece[k1]) + 1);
+		nunk = 0;
+		int rc = xcg_decode_host(ctx, &in[pos], span, &coff[0], &clen[0], n, &out[0], out.size(), &ooff[0], &olen[0],
+		                         &cst[0], &cons[0], &unk[0], unk.size(), &nunk);
+		if (rc == XCG_ENOTSUP) {
+			if (n > 1) {
+				per = n / 2;
+				continue;
+			}
+			const uint64_t c = split_point(in, piece[k0], piece[k0 + 1]);
+			if (c == 0) {
+				xcg_decode_set_window(ctx, NULL);
+				HALT(log_) << "xcgpu decode: " << xcg_strerror(rc) << " (an op the engine does not model on "
+				           << "this cache).";
+			}
+			piece.insert(piece.begin() + k0 + 1, c);
+			per = 1;
+			continue;
+		}
 		if (rc != XCG_OK) {
 			xcg_decode_set_window(ctx, NULL);
 			HALT(log_) << "xcgpu decode failed: " << xcg_strerror(rc);
 		}
+		batch_end = piece[k1];
+		/* the pieces decoded, in order, up to the first that stopped */
+		uint64_t consumed = 0;
+		status = 0;
+		for (uint32_t j = 0; j < n; j++) {
+			if (cst[j] == 2)
+				break;
+			if (olen[j])
+				output->append(&out[ooff[j]], olen[j]);
+			consumed += cons[j];
+			if (cst[j] != 0) {
+				status = cst[j];
+				break;
+			}
+		}
 		mirror_extracts(cache_, in, pos, pos + consumed);
-		output->append(&out[0], olen);
 		pos += consumed;
+		if (status == 0 && k1 < piece.size() - 1) {	/* more batches of this call */
+			k0 = k1;
+			continue;
+		}
 		if (status != 1 || pos >= len)
 			break;
 		unsigned pushed = 0;
@@ -211,6 +323,45 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		}
 		if (pushed == 0)
 			break;
+		cut_pieces(in, pos, piece);
+		k0 = 0;
+		per = piece.size() - 1;
+	}
+	if (status == 1 && batch_end < len) {
+		/*
+		 * The stop fell in a batch that ended before the input did: the
+		 * engine skimmed up to batch_end.  decode_skim's lookups go on to the
+		 * end (:196-272), so the rest is decoded behind a REF no cache can
+		 * hold -- bits 32..35 of a real XCodecHash are always clear (mix()
+		 * shifts bits_hash by 36) -- which stops the batch at its first op and
+		 * leaves only the skim.
+		 */
+		std::vector<uint8_t> rest(10 + (len - batch_end));
+		static const uint64_t NOHASH = 0x0000000F00000000ull;
+		rest[0] = XCODEC_MAGIC;
+		rest[1] = XCODEC_OP_REF;
+		for (int b = 0; b < 8; b++)
+			rest[2 + b] = (uint8_t)(NOHASH >> (56 - 8 * b));
+		memcpy(&rest[10], &in[batch_end], len - batch_end);
+		cut_pieces(rest, 0, piece);
+		const uint32_t n = (uint32_t)(piece.size() - 1);
+		coff.resize(n); clen.resize(n); ooff.resize(n); olen.resize(n); cons.resize(n); cst.resize(n);
+		for (uint32_t j = 0; j < n; j++) {
+			coff[j] = piece[j];
+			clen[j] = (uint32_t)(piece[j + 1] - piece[j]);
+		}
+		std::vector<uint64_t> unk2(unk.size());
+		uint32_t nunk2 = 0;
+		uint8_t dummy[16];
+		int rc = xcg_decode_host(ctx, &rest[0], rest.size(), &coff[0], &clen[0], n, dummy, sizeof dummy, &ooff[0],
+		                         &olen[0], &cst[0], &cons[0], &unk2[0], unk2.size(), &nunk2);
+		if (rc != XCG_OK || cst[0] != 1) {
+			xcg_decode_set_window(ctx, NULL);
+			HALT(log_) << "xcgpu decode: skim of the rest failed: " << xcg_strerror(rc);
+		}
+		for (uint32_t k = 0; k < nunk2 && nunk < unk.size(); k++)
+			if (unk2[k] != NOHASH)
+				unk[nunk++] = unk2[k];
 	}
 	xcg_decode_set_window(ctx, NULL);
 

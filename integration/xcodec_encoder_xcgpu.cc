@@ -53,7 +53,7 @@ XCodecEncoder::encode(Buffer *output, Buffer *input, std::map<uint64_t, BufferSe
 
 	xcg_ctx *ctx = xcgpu_binding::ctx_for(cache_, !stream_);
 	if (ctx == NULL)
-		HALT(log_) << "No MI355X device for the XCodec engine.";
+		HALT(log_) << "xcgpu: " << xcgpu_binding::why_not(cache_) << ".";
 
 	const uint32_t len = input->length();
 	if (len > XCGPU_MAX_ENCODE)

@@ -159,6 +159,9 @@ InflatePipe::InflatePipe(void)
 		HALT(log_) << "Could not initialize inflate stream.";
 	uint32_t slot = p->free_slots.back();
 	p->free_slots.pop_back();
+	/* a reused slot still holds its last stream: inflateInit (inflate_pipe.cc:38-50) */
+	if (xcg_zinflate_reset(p->ctx, slot) != XCG_OK)
+		HALT(log_) << "Could not initialize inflate stream.";
 	p->slot_of[this] = slot;
 }
 

@@ -127,20 +127,40 @@ class Oracle:
             raise ValueError('disk too small for one index block')
         return c
 
-    def pair_stats(self, c):
-        """(disk index entries, disk entries written) of a pair cache."""
+    def pair_stats(self, c, disk_live=False):
+        """(disk index entries, disk entries written) of a pair cache; with
+        disk_live, also the index entries of every front on its disk."""
         st = np.zeros(4, np.uint64)
         if self.ref:
             f = getattr(self.lib, self._pre + 'pair_stats')
             f.argtypes = [C.c_void_p, _u64p]
             f(c, _p(st, _u64p))
-            return int(st[0]), int(st[1])
+            return (int(st[0]), int(st[1]), int(st[2])) if disk_live else (int(st[0]), int(st[1]))
         self.lib.xco_pair_stats.argtypes = [C.c_void_p, _u64p]
         self.lib.xco_pair_stats(c, _p(st, _u64p))
         return int(st[1]), int(st[2])
 
     def cache_free(self, c):
         self._cfree(c)
+
+    def cache_connect(self, parent, uuid: str):
+        """XCodecCache::connect(uuid, parent) (xcodec/xcodec_cache.h:101-111): what
+        XCodecPipePair's decoding side makes on <HELLO> (xcodec_pipe_pair.cc:203).
+        Reference / drop-in builds; the cache lives for the process."""
+        f = getattr(self.lib, self._pre + 'cache_connect')
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_void_p, C.c_char_p]
+        c = f(parent, uuid.encode())
+        if not c:
+            raise RuntimeError('connect failed')
+        return c
+
+    def cache_learn(self, cache, seg: bytes):
+        """XCodecPipePair's <LEARN> of one segment (xcodec_pipe_pair.cc:296-327)."""
+        f = getattr(self.lib, self._pre + 'cache_learn')
+        f.argtypes = [C.c_void_p, C.c_char_p]
+        assert len(seg) == SEG
+        f(cache, seg)
 
     # ---------------------------------------------------------------- encode
     def encode_batch(self, data, offs, lens, mode=MODE_INDEPENDENT, oob=False, cache=None):

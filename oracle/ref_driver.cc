@@ -45,101 +45,188 @@ public:
  * The disk secondary of wanproxy.conf's cache pair.  XCodecDisk /
  * XCodecDiskCache (xcodec/xcodec_cache_disk.{h,cc}) cannot be compiled here:
  * it needs UUID::generate / UUID::decode from common/uuid/uuid_libuuid.cc,
- * whose libuuid header the image lacks (no stand-in is written).  This class
- * RESTATES its in-memory behaviour for the local namespace, so the REAL
- * XCodecCachePair (xcodec/xcodec_cache.h:140-237) and the real encoder /
- * decoder run over it: FIFO data blocks in index blocks of 204 entries
- * (:72-101, :694-741), the next index block's entries leave the index when the
- * write head reaches it (:327-382), lookup re-hashes (:743-771), touch
- * re-enters a lost hash (:813-823), replace = remove + enter
- * (xcodec_cache_disk.h:130-134).  The bytes live in memory, not in a file.
+ * whose libuuid header the image lacks (no stand-in is written).  RefDisk and
+ * RefDiskCache RESTATE their in-memory behaviour, so the REAL XCodecCachePair
+ * (xcodec/xcodec_cache.h:140-237) and the real encoder / decoder run over it:
+ * one FIFO of data blocks in index blocks of 204 entries shared by every
+ * front-end (xuid) on the disk (:72-101, :694-741); when the write head enters
+ * an index block, each front loses the entries it still has there -- the
+ * index entry names the front, and a front's hash counts only if its index
+ * still points at that block (index_invalidate_entries, :327-382); lookup
+ * re-hashes (:743-771), touch re-enters a lost hash (:813-823), replace =
+ * remove + enter (xcodec_cache_disk.h:130-134); connect(uuid) gives the uuid's
+ * front, a new one on the lowest free xuid (XCodecDisk::connect, :640-690).
+ * The bytes live in memory, not in a file.
  */
+class RefDisk;
+
 class RefDiskCache : public XCodecCache {
+	friend class RefDisk;
+	RefDisk *disk_;
+	uint16_t xuid_;
+	std::map<uint64_t, uint64_t> index_;   /* hash -> data block (XCodecDiskCache::hash_cache_) */
+	RefDiskCache(const UUID& uuid, RefDisk *disk, uint16_t xuid)
+	: XCodecCache(uuid), disk_(disk), xuid_(xuid), index_()
+	{ }
+public:
+	XCodecCache *connect(const UUID& uuid);
+	void enter(const uint64_t& hash, BufferSegment *seg);
+	void replace(const uint64_t& hash, BufferSegment *seg);
+	BufferSegment *lookup(const uint64_t& hash);
+	void touch(const uint64_t& hash, BufferSegment *seg);
+	bool out_of_band(void) const { return false; }
+	uint64_t entries(void) const { return index_.size(); }
+	uint64_t written(void) const;
+	RefDisk *disk(void) const { return disk_; }
+};
+
+class RefDisk {
 	uint64_t nb_, slots_, clock_;
 	std::vector<uint64_t> key_;
-	std::vector<uint8_t> alive_;
+	std::vector<uint16_t> xuid_;
+	std::vector<uint8_t> used_;
 	std::vector<uint8_t> data_;
-	std::map<uint64_t, uint64_t> index_;
+	std::map<uint16_t, RefDiskCache *> fronts_;
+	std::map<std::string, uint16_t> uuid_xuid_;
 public:
-	RefDiskCache(const UUID& uuid, uint64_t disk_bytes)
-	: XCodecCache(uuid),
-	  nb_(((disk_bytes / XCODEC_SEGMENT_LENGTH) - 18) / 205),
+	const uint64_t bytes_;
+
+	RefDisk(uint64_t disk_bytes)
+	: nb_(((disk_bytes / XCODEC_SEGMENT_LENGTH) - 18) / 205),
 	  slots_(nb_ * 204),
 	  clock_(0),
 	  key_(slots_),
-	  alive_(slots_),
+	  xuid_(slots_),
+	  used_(slots_),
 	  data_(slots_ * XCODEC_SEGMENT_LENGTH),
-	  index_()
+	  fronts_(),
+	  uuid_xuid_(),
+	  bytes_(disk_bytes)
 	{ }
 
-	XCodecCache *connect(const UUID&) { return NULL; }
-
-	void enter(const uint64_t& hash, BufferSegment *seg)
+	/* XCodecDisk::local: the front of xuid 0 (registry_load establishes it). */
+	RefDiskCache *local(const UUID& uuid)
 	{
-		ASSERT("/ref/disk", index_.find(hash) == index_.end());
+		if (fronts_.find(0) == fronts_.end()) {
+			fronts_[0] = new RefDiskCache(uuid, this, 0);
+			uuid_xuid_[uuid.string_] = 0;
+		}
+		return fronts_[0];
+	}
+
+	RefDiskCache *connect(const UUID& uuid)
+	{
+		std::map<std::string, uint16_t>::const_iterator it = uuid_xuid_.find(uuid.string_);
+		if (it != uuid_xuid_.end())
+			return fronts_[it->second];
+		uint16_t xuid;
+		for (xuid = 0; xuid < 1024; xuid++)
+			if (fronts_.find(xuid) == fronts_.end())
+				break;
+		if (xuid == 1024)
+			return NULL;
+		RefDiskCache *c = new RefDiskCache(uuid, this, xuid);
+		fronts_[xuid] = c;
+		uuid_xuid_[uuid.string_] = xuid;
+		return c;
+	}
+
+	void enter(RefDiskCache *c, uint64_t hash, BufferSegment *seg)
+	{
+		ASSERT("/ref/disk", c->index_.find(hash) == c->index_.end());
 		uint64_t slot = clock_ % slots_;
 		seg->copyout(&data_[slot * XCODEC_SEGMENT_LENGTH], 0, XCODEC_SEGMENT_LENGTH);
 		key_[slot] = hash;
-		alive_[slot] = 1;
-		index_[hash] = slot;
+		xuid_[slot] = c->xuid_;
+		used_[slot] = 1;
+		c->index_[hash] = slot;
 		if (++clock_ % 204 == 0) {
 			uint64_t b = (clock_ / 204) % nb_;
 			for (uint64_t i = b * 204; i < (b + 1) * 204; i++) {
-				if (!alive_[i])
+				if (!used_[i])
 					continue;
-				index_.erase(key_[i]);
-				alive_[i] = 0;
+				std::map<uint16_t, RefDiskCache *>::iterator f = fronts_.find(xuid_[i]);
+				if (f == fronts_.end())
+					continue;
+				std::map<uint64_t, uint64_t>::iterator it = f->second->index_.find(key_[i]);
+				if (it == f->second->index_.end() || it->second != i)
+					continue;	/* absent, or the hash lives in a newer block */
+				f->second->index_.erase(it);
 			}
 		}
 	}
 
-	void remove(const uint64_t& hash)
+	void remove(RefDiskCache *c, uint64_t hash)
 	{
-		std::map<uint64_t, uint64_t>::iterator it = index_.find(hash);
-		if (it == index_.end())
-			return;
-		alive_[it->second] = 0;
-		index_.erase(it);
+		c->index_.erase(hash);
 	}
 
-	void replace(const uint64_t& hash, BufferSegment *seg)
+	BufferSegment *lookup(RefDiskCache *c, uint64_t hash)
 	{
-		remove(hash);
-		enter(hash, seg);
-	}
-
-	BufferSegment *lookup(const uint64_t& hash)
-	{
-		std::map<uint64_t, uint64_t>::iterator it = index_.find(hash);
-		if (it == index_.end())
+		std::map<uint64_t, uint64_t>::iterator it = c->index_.find(hash);
+		if (it == c->index_.end())
 			return NULL;
 		BufferSegment *seg = BufferSegment::create();
 		memcpy(seg->head(), &data_[it->second * XCODEC_SEGMENT_LENGTH], XCODEC_SEGMENT_LENGTH);
 		seg->set_length(XCODEC_SEGMENT_LENGTH);
 		if (XCodecHash::hash(seg->data()) != hash) {
 			seg->unref();
-			alive_[it->second] = 0;
-			index_.erase(it);
+			c->index_.erase(it);
 			return NULL;
 		}
 		return seg;
 	}
 
-	void touch(const uint64_t& hash, BufferSegment *seg)
-	{
-		if (index_.find(hash) == index_.end())
-			enter(hash, seg);
-	}
-
-	bool out_of_band(void) const { return false; }
-
-	uint64_t entries(void) const { return index_.size(); }
 	uint64_t written(void) const { return clock_; }
+	uint64_t live(void) const
+	{
+		uint64_t n = 0;
+		for (std::map<uint16_t, RefDiskCache *>::const_iterator f = fronts_.begin(); f != fronts_.end(); ++f)
+			n += f->second->entries();
+		return n;
+	}
 };
+
+XCodecCache *RefDiskCache::connect(const UUID& uuid) { return disk_->connect(uuid); }
+void RefDiskCache::enter(const uint64_t& hash, BufferSegment *seg) { disk_->enter(this, hash, seg); }
+void RefDiskCache::replace(const uint64_t& hash, BufferSegment *seg)
+{
+	disk_->remove(this, hash);
+	disk_->enter(this, hash, seg);
+}
+BufferSegment *RefDiskCache::lookup(const uint64_t& hash) { return disk_->lookup(this, hash); }
+void RefDiskCache::touch(const uint64_t& hash, BufferSegment *seg)
+{
+	if (index_.find(hash) == index_.end())
+		disk_->enter(this, hash, seg);
+}
+uint64_t RefDiskCache::written(void) const { return disk_->written(); }
+
+#ifdef XCGPU_DROPIN
+/* The binding finds the XCodecDisk under an XCodecDiskCache by itself; this
+ * harness's restated disk level is resolved here. */
+static bool ref_disk_resolver(XCodecCache *level, const void **disk, uint64_t *bytes)
+{
+	RefDiskCache *front = dynamic_cast<RefDiskCache *>(level);
+	if (front == NULL)
+		return false;
+	*disk = front->disk();
+	*bytes = front->disk()->bytes_;
+	return true;
+}
+static const bool ref_disk_resolver_set = (xcgpu_binding::set_disk_resolver(ref_disk_resolver), true);
+#endif
 
 static std::map<void *, std::pair<XCodecCache *, XCodecCache *> >& pair_levels()
 {
 	static std::map<void *, std::pair<XCodecCache *, XCodecCache *> > m;
+	return m;
+}
+
+/* the disk front under each pair the harness made or connected */
+static std::map<void *, RefDiskCache *>& pair_fronts()
+{
+	static std::map<void *, RefDiskCache *> m;
 	return m;
 }
 
@@ -188,48 +275,82 @@ void *xcr_cache_new(void)
 void *xcr_cache_new_limited(uint64_t limit_bytes)
 {
 	UUID uuid;
-	XCodecCache *c = new XCodecMemoryCache(uuid, (size_t)limit_bytes);
-#ifdef XCGPU_DROPIN
-	xcgpu_binding::set_cache_limit(c, limit_bytes);   /* as wanproxy_config_class_cache.cc would */
-#endif
-	return c;
+	return new XCodecMemoryCache(uuid, (size_t)limit_bytes);
 }
 
-/* XCodecCachePair(XCodecMemoryCache(uuid, memory_limit_bytes), disk of
- * disk_bytes): wanproxy.conf's memory + disk pair
+/* XCodecCachePair(XCodecMemoryCache(uuid, memory_limit_bytes), the local front
+ * of a disk of disk_bytes): wanproxy.conf's memory + disk pair
  * (programs/wanproxy/wanproxy.conf:8-26, wanproxy_config_class_cache.cc). */
 void *xcr_cache_new_pair(uint64_t memory_limit_bytes, uint64_t disk_bytes)
 {
 	UUID uuid;
 	XCodecCache *primary = new XCodecMemoryCache(uuid, (size_t)memory_limit_bytes);
-	XCodecCache *secondary = new RefDiskCache(uuid, disk_bytes);
+	RefDisk *disk = new RefDisk(disk_bytes);
+	RefDiskCache *secondary = disk->local(uuid);
 	XCodecCache *pair = new XCodecCachePair(primary, secondary);
-	pair_levels()[pair] = std::make_pair(primary, secondary);
-#ifdef XCGPU_DROPIN
-	xcgpu_binding::set_pair_geometry(pair, memory_limit_bytes, disk_bytes);
-#endif
+	pair_levels()[pair] = std::make_pair(primary, (XCodecCache *)NULL);
+	pair_fronts()[pair] = secondary;
 	return pair;
+}
+
+/* XCodecCache::connect(uuid, parent) (xcodec/xcodec_cache.h:101-111), as the
+ * decoding side of XCodecPipePair makes its cache on <HELLO>
+ * (xcodec/xcodec_pipe_pair.cc:203): the registered cache of that uuid, else
+ * parent->connect(uuid) -- a bounded memory cache of the parent's limit, or a
+ * pair of connected levels (the disk level: the uuid's front on the same
+ * disk).  Such caches live for the process, as in the reference. */
+void *xcr_cache_connect(void *parent, const char *uuid_string)
+{
+	UUID uuid;
+	uuid.string_ = uuid_string;
+	XCodecCache *c = XCodecCache::connect(uuid, (XCodecCache *)parent);
+	std::map<void *, RefDiskCache *>::iterator f = pair_fronts().find(parent);
+	if (c != NULL && f != pair_fronts().end())
+		pair_fronts()[c] = f->second->disk()->connect(uuid);   /* (the front the pair's connect made) */
+	return c;
 }
 
 void xcr_cache_free(void *c)
 {
 	RELEASE_CACHE((XCodecCache *)c);
 	std::map<void *, std::pair<XCodecCache *, XCodecCache *> >::iterator it = pair_levels().find(c);
-	if (it != pair_levels().end()) {       /* the pair does not own its levels */
+	if (it != pair_levels().end()) {       /* the pair does not own its levels (the disk stays) */
 		delete it->second.first;
-		delete it->second.second;
 		pair_levels().erase(it);
 	}
+	pair_fronts().erase(c);
 	delete (XCodecCache *)c;
 }
 
-/* Diagnostics of a pair made by xcr_cache_new_pair: [0] disk index entries,
- * [1] disk entries written. */
+/* XCodecPipePair's <LEARN> of one segment into a (peer) cache
+ * (xcodec/xcodec_pipe_pair.cc:296-327): lookup, then replace if the bytes
+ * differ, enter if absent. */
+void xcr_cache_learn(void *c, const uint8_t *bytes)
+{
+	XCodecCache *cache = (XCodecCache *)c;
+	Buffer b(bytes, XCODEC_SEGMENT_LENGTH);
+	BufferSegment *seg;
+	b.copyout(&seg, XCODEC_SEGMENT_LENGTH);
+	uint64_t hash = XCodecHash::hash(seg->data());
+	BufferSegment *oseg = cache->lookup(hash);
+	if (oseg != NULL) {
+		if (!oseg->equal(seg))
+			cache->replace(hash, seg);
+		oseg->unref();
+	} else {
+		cache->enter(hash, seg);
+	}
+	seg->unref();
+}
+
+/* Diagnostics of a pair: [0] disk index entries of its disk front, [1] disk
+ * entries written (the whole disk), [2] index entries of every front. */
 void xcr_pair_stats(void *c, uint64_t *st)
 {
-	RefDiskCache *d = (RefDiskCache *)pair_levels()[c].second;
+	RefDiskCache *d = pair_fronts()[c];
 	st[0] = d->entries();
 	st[1] = d->written();
+	st[2] = d->disk()->live();
 }
 
 /* mode 0: fresh XCodecMemoryCache per chunk; mode 1: one cache + one encoder

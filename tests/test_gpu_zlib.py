@@ -120,15 +120,16 @@ def test_errors():
 
 
 # ---------------------------------------------------------------- InflatePipe
-def inflate_streams(streams):
+def inflate_streams(streams, out_cap=None):
     """streams: [[input cut bytes...]] -> [[(produced, status)...]], call k of
-    every stream in batch k (InflatePipe::consume per cut)."""
+    every stream in batch k (InflatePipe::consume per cut).  out_cap: the first
+    output room of every call (consume_many repeats a -2 call with 4x more)."""
     from wanproxy_amd.zpipe import InflatePipes
     ctx = InflatePipes(len(streams))
     outs = [[] for _ in streams]
     for k in range(max(len(s) for s in streams)):
         items = [(i, s[k]) for i, s in enumerate(streams) if k < len(s)]
-        for (i, _), g in zip(items, ctx.consume_many(items)):
+        for (i, _), g in zip(items, ctx.consume_many(items, out_cap=out_cap)):
             outs[i].append(g)
     ctx.close()
     return outs
@@ -225,3 +226,53 @@ def test_distance_boundaries_both_ways():
     got = inflate_streams([cuts(rng, z, 'random') + [b'']])[0]
     assert b''.join(o for o, _ in got) == data
     assert got[-1][1] == 1
+
+
+def test_inflate_retry_after_no_room():
+    """Status -2 (output room too small) commits nothing, wherever it strikes:
+    inside a stored block, inside a Huffman block, right after the next
+    dynamic block's header.  Calls start with 256 bytes of room and are
+    repeated with 4x more; every call's output equals zlib's on the same cuts."""
+    from oracle.zlib_pipe import InflatePipeRef
+    rng = random.Random(77)
+    srcs, streams = [], []
+    for si in range(24):
+        level = [1, 6, 9, 0][si % 4]
+        # blocks of changing statistics: several dynamic blocks per call
+        data = b''.join(bytes(rng.choice(b'abcdefgh' if k % 2 else b'0123456789 ') for _ in range(rng.randint(200, 9000)))
+                        + rng.randbytes(rng.randint(0, 3000)) for k in range(12))
+        z = zlib.compress(data, level)
+        srcs.append(data)
+        cs, i = [], 0
+        while i < len(z):
+            n = rng.choice([5, 40, 700, 3000, 9000])
+            cs.append(z[i:i + n])
+            i += n
+        streams.append(cs + [b''])
+    got = inflate_streams(streams, out_cap=256)
+    for si, (src, cs) in enumerate(zip(srcs, streams)):
+        ref = InflatePipeRef()
+        for k, c in enumerate(cs[:-1]):
+            out, st = got[si][k]
+            assert out == ref.consume(c), (si, k)
+            assert st in (0, 1), (si, k, st)
+        assert b''.join(o for o, _ in got[si]) == src
+
+
+def test_inflate_slot_reuse_after_reset():
+    """A slot whose stream ended (or failed) serves a fresh InflatePipe after
+    xcg_zinflate_reset -- the adapter's constructor on a reused slot."""
+    from wanproxy_amd.zpipe import InflatePipes
+    ctx = InflatePipes(2)
+    a = zlib.compress(b'first stream ' * 50, 6)
+    b = zlib.compress(b'second stream ' * 70, 6)
+    assert ctx.consume_many([(0, a)]) == [(b'first stream ' * 50, 1)]
+    assert ctx.consume_many([(1, b'\x78\x9dgarbage')])[0][1] == -1
+    # without a reset the ended / failed slots refuse a new stream
+    assert ctx.consume_many([(0, b)])[0][1] == -1
+    ctx.reset(0)
+    ctx.reset(1)
+    assert ctx.consume_many([(0, b), (1, a[:10])]) == [(b'second stream ' * 70, 1),
+                                                        (zlib.decompressobj().decompress(a[:10]), 0)]
+    assert ctx.consume_many([(1, a[10:])]) == [(b'first stream ' * 50, 1)]
+    ctx.close()

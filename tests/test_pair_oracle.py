@@ -103,3 +103,29 @@ def test_pair_vs_reference_live(ref_oracle, oracle):
             res.append((lib.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c), lib.pair_stats(c)))
             lib.cache_free(c)
         assert res[0] == res[1], (t, chunk, limit, disk)
+
+
+def test_ref_shared_disk_fronts(ref_oracle):
+    """The restated XCodecDisk of the reference harness (oracle/ref_driver.cc
+    RefDisk): a pair XCodecCache::connect makes for a peer (xcodec_cache.h:158-161)
+    is a second front on the SAME disk (XCodecDisk::connect,
+    xcodec_cache_disk.cc:640-690).  Its writes lap the ring and take the local
+    front's entries with them (index_invalidate_entries walks every front,
+    :327-382); the connect registry returns the same cache for a uuid."""
+    from wanproxy_amd import synth
+    limit, disk = 50 * 2048, mpg.disk_bytes(1)          # 204 data blocks
+    pa = ref_oracle.cache_new_pair(limit, disk)
+    pb = ref_oracle.cache_connect(pa, '11111111-2222-4333-8444-555555555555')
+    assert ref_oracle.cache_connect(pa, '11111111-2222-4333-8444-555555555555') == pb
+    a = synth.stream(0xA, 300 * 2048, 0, 0)             # 300 unique segments
+    offs, lens = synth.chunks_of(a, 65536)
+    ref_oracle.encode_batch(a, offs, lens, mode=MODE_STREAM, cache=pa)
+    ea, wa, la = ref_oracle.pair_stats(pa, disk_live=True)
+    assert wa == 300 and 0 < ea <= 204 and la == ea
+    b = synth.stream(0xB, 250 * 2048, 0, 0)
+    offs, lens = synth.chunks_of(b, 65536)
+    ref_oracle.encode_batch(b, offs, lens, mode=MODE_STREAM, cache=pb)
+    ea2, wa2, la2 = ref_oracle.pair_stats(pa, disk_live=True)
+    eb2, wb2, _ = ref_oracle.pair_stats(pb, disk_live=True)
+    assert wa2 == wb2 == 550                             # one write head
+    assert ea2 == 0 and la2 == eb2 > 0                  # the peer front's lap took every local entry

@@ -66,6 +66,8 @@ struct XcgDecodeArgs {
   uint64_t win_count;
   XcgLruState* lru;      // bounded cache (null: unbounded)
   uint32_t maxd;         // EXTRACTs a chunk can hold (bounded: declaration rows per chunk)
+  XcgPairState* pair;    // XCodecCachePair (null: not a pair)
+  int no_window;         // the BACKREF window is left alone (<LEARN>, single-segment host calls)
 };
 extern "C" int xcg_launch_pack(const uint8_t*, const uint64_t*, const uint64_t*, uint32_t, uint8_t*, uint64_t*,
                                uint64_t*, hipStream_t);
@@ -194,8 +196,9 @@ struct xcg_ctx {
   // stream): the cache-inspection calls wait for this event only, never for
   // the whole device, so other contexts and streams keep running.
   hipEvent_t done_ev = nullptr;
-  XcgPairState* pair = nullptr;    // XCodecCachePair(memory, disk) (xcg_pair.hip)
+  XcgPairState* pair = nullptr;    // XCodecCachePair(memory, disk) (xcg_pair.hip): a front of a disk
   uint32_t pair_C = 0;             // its primary limit in segments
+  bool no_window = false;          // (single-segment host calls: decodes that leave the window alone)
   // Host-call staging (xcg_encode_call / xcg_encode_host): kept across calls,
   // so a per-call encode() allocates nothing and synchronises once.
   uint8_t* stage_h = nullptr;      // pinned
@@ -530,9 +533,29 @@ int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_lim
   return XCG_OK;
 }
 
-int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
-                        xcg_ctx** out) {
-  if (!out || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE))) return XCG_EINVAL;
+int xcg_disk_create(uint64_t disk_bytes, xcg_disk** out) {
+  if (!out) return XCG_EINVAL;
+  *out = nullptr;
+  XcgDiskState* K = nullptr;
+  const int rc = xcg_disk_state_create(disk_bytes, &K);
+  if (rc) return rc == -22 ? XCG_EINVAL : XCG_ENOMEM;
+  *out = (xcg_disk*)K;
+  return XCG_OK;
+}
+
+void xcg_disk_destroy(xcg_disk* d) { xcg_disk_state_release((XcgDiskState*)d); }
+
+int xcg_disk_stats(const xcg_disk* d, uint64_t* st) {
+  if (!d || !st) return XCG_EINVAL;
+  xcg_disk_state_stats((const XcgDiskState*)d, st);
+  return XCG_OK;
+}
+
+int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk* disk,
+                           xcg_ctx** out) {
+  if (!out || !disk || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)))
+    return XCG_EINVAL;
+  *out = nullptr;
   uint64_t C = memory_cache_limit_bytes / XCG_SEGMENT_LENGTH;   // xcodec_cache.h:283-287
   if (C == 0) C = 1;
   if (C > (1ull << 28)) return XCG_EINVAL;
@@ -541,13 +564,11 @@ int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
     DeviceGuard g(device);
-    const int prc = xcg_pair_state_create((uint32_t)C, disk_bytes, &P);
+    const int prc = xcg_pair_state_create((uint32_t)C, (XcgDiskState*)disk, &P);
     if (prc == -22) return XCG_EINVAL;
     if (prc) return XCG_ENOMEM;
   }
-  uint64_t st[4];
-  xcg_pair_state_stats(P, st);
-  const int rc = xcg_ctx_create_ex(device, flags, C + st[3] * 204, out);
+  const int rc = xcg_ctx_create_ex(device, flags, C + xcg_pair_state_disk_blocks(P), out);
   if (rc != XCG_OK) {
     DeviceGuard g(device);
     xcg_pair_state_destroy(P);
@@ -556,6 +577,17 @@ int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_
   (*out)->pair = P;
   (*out)->pair_C = (uint32_t)C;
   return XCG_OK;
+}
+
+int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
+                        xcg_ctx** out) {
+  if (!out) return XCG_EINVAL;
+  xcg_disk* d = nullptr;
+  int rc = xcg_disk_create(disk_bytes, &d);
+  if (rc != XCG_OK) return rc;
+  rc = xcg_ctx_create_pair_on(device, flags, memory_cache_limit_bytes, d, out);
+  xcg_disk_destroy(d);                 // (the front holds the disk from here)
+  return rc;
 }
 
 int xcg_pair_stats(xcg_ctx* c, uint64_t* st) {
@@ -750,9 +782,59 @@ int lru_host_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out
 }
 }  // namespace
 
+namespace {
+uint64_t host_seg_hash(const uint8_t* w) {   // XCodecHash::hash, xcodec/xcodec_hash.h:166-174
+  uint32_t s1 = 0, s2 = 0, b1 = 0, b2 = 0;
+  for (uint32_t k = 0; k < XCG_SEGMENT_LENGTH; ++k) {
+    s1 += (uint32_t)w[k] + 1u;
+    s2 += s1;
+    b1 += w[k] ? (uint32_t)__builtin_ctz(w[k]) + 1u : 0u;
+    b2 += b1;
+  }
+  return ((uint64_t)((b1 << 16) + b2) << 36) + (uint64_t)((s1 << 20) + s2);
+}
+
+// Single-segment host calls on a pair: a one-op decode batch that leaves the
+// BACKREF window alone.  A lookup is <REF hash> (XCodecCachePair::lookup, with
+// its LRU use / disk touch / promotion, xcodec_cache.h:208-230); an enter is
+// <EXTRACT seg> -- lookup, then nothing (same bytes), replace (other bytes) or
+// enter (absent), exactly <LEARN>'s sequence (xcodec_pipe_pair.cc:311-327).
+int pair_host_call(xcg_ctx* c, uint64_t hash, const uint8_t* in_seg, uint8_t* out_seg, int32_t* found) {
+  uint8_t op[2 + XCG_SEGMENT_LENGTH];
+  uint32_t len;
+  op[0] = 0xF1;
+  if (in_seg) {
+    op[1] = 0x01;
+    memcpy(op + 2, in_seg, XCG_SEGMENT_LENGTH);
+    len = 2 + XCG_SEGMENT_LENGTH;
+  } else {
+    op[1] = 0x02;
+    for (int k = 0; k < 8; ++k) op[2 + k] = (uint8_t)(hash >> (56 - 8 * k));
+    len = 10;
+  }
+  const uint64_t off = 0;
+  uint64_t ooff = 0, olen = 0, cons = 0, unk = 0;
+  int32_t st = 0;
+  uint32_t nunk = 0;
+  uint8_t out[XCG_SEGMENT_LENGTH];
+  c->no_window = true;
+  const int rc = xcg_decode_host(c, op, len, &off, &len, 1, out, sizeof out, &ooff, &olen, &st, &cons, &unk, 1, &nunk);
+  c->no_window = false;
+  if (rc != XCG_OK) return rc;
+  if (st < 0) return XCG_EHIP;
+  *found = st == 0 && olen == XCG_SEGMENT_LENGTH;
+  if (*found && out_seg) memcpy(out_seg, out, XCG_SEGMENT_LENGTH);
+  return XCG_OK;
+}
+}  // namespace
+
 int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
   if (!c || !seg_out) return XCG_EINVAL;
-  if (c->pair) return XCG_ENOTSUP;
+  if (c->pair) {
+    int32_t found = 0;
+    const int rc = pair_host_call(c, hash, nullptr, seg_out, &found);
+    return rc != XCG_OK ? rc : (found ? XCG_OK : XCG_ENOENT);
+  }
   if (c->bounded) {
     int32_t found = 0;
     const int rc = lru_host_call(c, hash, nullptr, seg_out, 0, &found);
@@ -766,7 +848,11 @@ int xcg_cache_lookup_host(xcg_ctx* c, uint64_t hash, uint8_t* seg_out) {
 
 int xcg_cache_enter_host(xcg_ctx* c, uint64_t hash, const uint8_t* seg) {
   if (!c || !seg) return XCG_EINVAL;
-  if (c->pair) return XCG_ENOTSUP;
+  if (c->pair) {
+    if (host_seg_hash(seg) != hash) return XCG_EINVAL;   // (a pair names a segment by its own hash)
+    int32_t found = 0;
+    return pair_host_call(c, hash, seg, nullptr, &found);
+  }
   if (c->bounded) {
     int32_t found = 0;
     return lru_host_call(c, hash, seg, nullptr, 1, &found);
@@ -1125,7 +1211,8 @@ int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_
   if (h_nunknown) *h_nunknown = 0;
   if (h_total_out) *h_total_out = 0;
   if (n == 0) return XCG_OK;
-  if (c->pair) return XCG_ENOTSUP;
+  // a bounded or pair batch numbers its ops by (chunk << 21 | offset)
+  if ((c->bounded || c->pair) && max_chunk_len >= (1u << 21)) return XCG_EINVAL;
   DeviceGuard g(c->device);
   ctx_order(c, (hipStream_t)stream);
   int rc = ensure_cache(c);
@@ -1142,7 +1229,12 @@ int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_
                   c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->ds.x_keys, c->ds.x_vals, c->ds.x_latest, c->ds.x_cap - 1,
                   c->ds.u_keys, c->ds.unknown, c->ds.unknown_pos, c->ds.nunknown, UNKNOWN_CAP, c->ds.scratch, c->ds.h_scratch,
                   c->ds.chunk_tmp, c->ds.d_tail, w->hash, w->seg, w->count, c->bounded ? &c->lru : nullptr,
-                  max_chunk_len / 2050 + 1};
+                  max_chunk_len / 2050 + 1, c->pair, c->no_window ? 1 : 0};
+  if (c->pair) {
+    const PairGpu G{d_enc, d_chunk_off, nullptr, 0u, c->g.pool, c->g.keys, c->g.vals, c->g.mask, c->g.filt,
+                    c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->g.nseg, c->d_status};
+    if (xcg_pair_sync(c->pair, &G, (hipStream_t)stream)) return XCG_EHIP;
+  }
   uint64_t total = 0, blockp = 0, berr = 0;
   uint32_t nunk = 0;
   const int lrc = xcg_launch_decode(&a, &total, &blockp, &berr, &nunk, (hipStream_t)stream);
@@ -1160,7 +1252,7 @@ int decode_batch_impl(xcg_ctx* c, const uint8_t* d_enc, const uint64_t* d_chunk_
     return XCG_EHIP;
   const int32_t st = *c->h_status;
   const uint64_t t_end = c->ds.h_scratch[7];
-  w->count += t_end;                                  // declares made: the window cursor advances
+  if (!c->no_window) w->count += t_end;               // declares made: the window cursor advances
   if (st & (1 << 9)) {
     (void)hipMemsetAsync(c->d_status, 0, 4, (hipStream_t)stream);
     return XCG_ENOTSUP;

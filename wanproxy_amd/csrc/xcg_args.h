@@ -149,13 +149,46 @@ struct LruBatch {
 };
 
 // XCodecCachePair of a bounded memory primary and a disk secondary (xcg_pair.hip).
+// The disk (XcgDiskState) is shared by every pair front on it, as XCodecDisk is
+// by its XCodecDiskCache front-ends.
+struct XcgDiskState;
 struct XcgPairState;
-extern "C" int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out);
+// What a pair commit / table rebuild touches on the GPU: the batch input and
+// its declaration rows (bytes of new entries), the pool, G and its filters.
+struct PairGpu {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const void* decl;       // uint4 rows: decl[c * maxd + d].z = the segment's offset in chunk c
+  uint32_t maxd;
+  uint8_t* pool;
+  uint64_t* g_keys;
+  uint64_t* g_vals;
+  uint32_t g_mask;
+  uint32_t* g_filt;
+  uint32_t* g_ftab;
+  uint32_t fmask;
+  uint32_t* g_gfilt;
+  uint32_t gmask;
+  uint32_t* nseg;
+  int32_t* status;
+};
+extern "C" int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out);
+extern "C" void xcg_disk_state_release(XcgDiskState* K);
+extern "C" void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st);
+extern "C" int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out);
 extern "C" void xcg_pair_state_destroy(XcgPairState* P);
 extern "C" int xcg_pair_state_clear(XcgPairState* P);
 extern "C" void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st);
 extern "C" uint32_t xcg_pair_state_last_base(const XcgPairState* P);
+extern "C" uint32_t xcg_pair_state_limit(const XcgPairState* P);
+extern "C" uint32_t xcg_pair_state_disk_blocks(const XcgPairState* P);
+extern "C" const uint64_t* xcg_pair_state_ptime(const XcgPairState* P);
+extern "C" int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st);
 extern "C" int xcg_pair_encode_stream(const XcgStreamArgs* a, XcgPairState* P, int* rounds_out, hipStream_t st);
+extern "C" int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st);
+extern "C" int xcg_pair_decode_pass(XcgPairState* P, const void* d_rows, const uint64_t* d_base, const uint64_t* d_cnt,
+                                    uint32_t n, uint64_t rows, uint64_t decls, int* same, hipStream_t st);
+extern "C" int xcg_pair_decode_commit(XcgPairState* P, const PairGpu* G, hipStream_t st);
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);
 extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a, XcgLruState* L, int* rounds_out, hipStream_t st);

@@ -759,6 +759,14 @@ __global__ __launch_bounds__(256) void dec_ops_kernel(DecParams prm, uint4* raw)
 // (a hit refreshes the entry) against the cache as it stands there.
 // ev[decl_base[c] + k]: (lo, hi, op offset, kind << 30 | ref) with GMISS =
 // no cache effect; ENTERs also as declaration rows.  One wave per chunk.
+//
+// PAIR (XCodecCachePair, xcg_pair.hip): ptime is the time a hash leaves both
+// levels.  A skim lookup can promote a disk-only hash and so evict another
+// (xcodec_cache.h:223-227), so each skim lookup sees the pair at its own time,
+// not at the stop.  An EXTRACT whose cached bytes differ is a REPLACE (op
+// offset | 1 << 31, GHIT): it takes a declaration row like an ENTER (the new
+// bytes' source), numbered with the ENTERs in op order.
+template <bool PAIR>
 __global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const uint4* raw, uint4* ev, uint32_t* nev,
                                                            uint4* drow, uint32_t* ndecl, uint32_t maxd,
                                                            uint64_t blockp, uint64_t* block_new, uint32_t* changes,
@@ -768,6 +776,7 @@ __global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const 
   const uint32_t cnt = (uint32_t)prm.n_decl[c];
   const uint64_t base = prm.decl_base[c];
   const uint64_t tb = blockp == ~0ull ? ~0ull : ((blockp >> 32 << 21) | (uint32_t)blockp);
+  const uint8_t* x = prm.in + prm.chunk_off[c];
   uint32_t nd = 0;
   bool chg = false;
   for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
@@ -775,7 +784,7 @@ __global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const 
     const bool valid = k < cnt;
     uint4 r = valid ? raw[base + k] : make_uint4(0u, 0u, 0u, 0u);
     const uint64_t here = spos(c, r.z), t = ((uint64_t)c << 21) | r.z;
-    uint32_t kind = EV_GMISS, ref = 0;
+    uint32_t kind = EV_GMISS, ref = 0, zflag = 0;
     bool enter = false;
     if (valid) {
       const uint64_t e = tab_lookup_t(prm.x, r.x, r.y);
@@ -787,18 +796,31 @@ __global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const 
           if (gv != ~0ull && t < prm.ptime[gv]) {
             kind = EV_GHIT;
             ref = (uint32_t)gv;
+            if (PAIR && r.w == OP_EXTRACT) {          // name reuse: the cached bytes differ
+              const u32x4_u* a = (const u32x4_u*)(x + r.z + 2);
+              const u32x4_u* b = (const u32x4_u*)(prm.pool + gv * (uint64_t)SEG);
+              bool same = true;
+              for (uint32_t q = 0; q < SEG / 16 && same; ++q) {
+                const u32x4 va = a[q], vb = b[q];
+                same = va[0] == vb[0] && va[1] == vb[1] && va[2] == vb[2] && va[3] == vb[3];
+              }
+              if (!same) {
+                zflag = 1u << 31;
+                enter = true;                         // (a declaration row; the kind stays GHIT)
+              }
+            }
           } else if (r.w == OP_EXTRACT) {
             enter = true;
           } else {
             atomicMin((unsigned long long*)block_new, (unsigned long long)here);   // unknown REF
           }
         }
-      } else if (r.w == OP_REF) {                     // decode_skim's lookup, cache as at the stop
+      } else if (r.w == OP_REF) {                     // decode_skim's lookup
         if (e != ~0ull && e < blockp) {
           kind = EV_HIT;
         } else {
           const uint64_t gv = tab_lookup_t(prm.g, r.x, r.y);
-          if (gv != ~0ull && tb < prm.ptime[gv]) {
+          if (gv != ~0ull && (PAIR ? t : tb) < prm.ptime[gv]) {
             kind = EV_GHIT;
             ref = (uint32_t)gv;
           }
@@ -808,15 +830,18 @@ __global__ __launch_bounds__(256) void dec_classify_kernel(DecParams prm, const 
     const uint64_t m = ballot(enter);
     if (enter) {
       const uint32_t d = nd + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      kind = EV_ENTER;
-      ref = d;
+      if (!zflag) {
+        kind = EV_ENTER;
+        ref = d;
+      }
       if (d < maxd) drow[(uint64_t)c * maxd + d] = make_uint4(r.x, r.y, r.z + 2u, 0u);
     }
     nd += (uint32_t)__builtin_popcountll(m);
     if (valid) {
       const uint32_t w = (kind << 30) | ref;
-      chg |= first || ev[base + k].w != w;
-      ev[base + k] = make_uint4(r.x, r.y, r.z, w);
+      const uint4 old = ev[base + k];
+      chg |= first || old.w != w || old.z != (r.z | zflag);
+      ev[base + k] = make_uint4(r.x, r.y, r.z | zflag, w);
     }
   }
   if (ballot(chg) != 0 && lane_id() == 0) atomicAdd(changes, 1u);
@@ -1004,6 +1029,8 @@ struct XcgDecodeArgs {
   uint64_t win_count;
   XcgLruState* lru;      // bounded cache (null: unbounded)
   uint32_t maxd;         // EXTRACTs a chunk can hold (bounded: declaration rows per chunk)
+  XcgPairState* pair;    // XCodecCachePair (null: not a pair)
+  int no_window;         // the BACKREF window is left alone (<LEARN>, single-segment host calls)
 };
 
 // Returns 0, -75 (output too small) or -5.  Outputs: total decoded bytes, the
@@ -1101,7 +1128,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     for (int pass = 0; pass < 64 && !agreed; ++pass) {
       if (hipMemsetAsync(blk, 0xFF, 8, stream) != hipSuccess || hipMemsetAsync(changes, 0, 4, stream) != hipSuccess)
         return fail(-5);
-      hipLaunchKernelGGL(dec_classify_kernel, grid, block, 0, stream, p, (const uint4*)raw, evs, nev32, drow, nd32,
+      hipLaunchKernelGGL(dec_classify_kernel<false>, grid, block, 0, stream, p, (const uint4*)raw, evs, nev32, drow, nd32,
                          a->maxd, blockp, blk, changes, pass == 0 ? 1 : 0);
       if (xcg_lru_times(&lb, L, stream)) return fail(-5);   // (synchronises)
       if (hipMemcpyAsync(a->h_scratch + 8, blk, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
@@ -1115,6 +1142,51 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
                 pass, L->h_tot[1], L->h_tot[2], L->h_tot[3], L->h_tot[8], nchg, (unsigned long long)blockp,
                 (unsigned long long)nb);
       agreed = nchg == 0 && nb == blockp;
+      blockp = nb;
+    }
+    if (!agreed) return fail(-75);
+  }
+  // Pair: classify every op against ptime (the time a hash leaves both
+  // levels), replay the classified ops through the pair's policy on the host
+  // (xcg_pair.hip), and repeat until the departure times the replay computes
+  // are the ones the classification used.
+  uint8_t* pair_mem = nullptr;
+  uint4* prow = nullptr;
+  if (a->pair) {
+    if (nbref > 0) return -95;                       // (BACKREF stop points are not modelled on a pair)
+    if (xcg_pair_decode_begin(a->pair, stream)) return -5;
+    const uint64_t m = ndecl ? ndecl : 1;
+    const uint64_t bytes = 32 * m + 16ull * n * a->maxd + 8ull * (n + 1) + 64;
+    if (hipMallocAsync((void**)&pair_mem, bytes, stream) != hipSuccess) return -5;
+    auto fail = [&](int rc) {
+      (void)hipFreeAsync(pair_mem, stream);
+      return rc;
+    };
+    raw = (uint4*)pair_mem;
+    evs = raw + m;
+    prow = evs + m;
+    uint32_t* nev32 = (uint32_t*)(prow + (uint64_t)n * a->maxd);
+    uint32_t* nd32 = nev32 + (n + 1);
+    uint64_t* blk = (uint64_t*)(((uintptr_t)(nd32 + n + 1) + 15) & ~(uintptr_t)15);
+    uint32_t* changes = (uint32_t*)(blk + 1);
+    hipLaunchKernelGGL(dec_ops_kernel, grid, block, 0, stream, p, raw);
+    p.ptime = xcg_pair_state_ptime(a->pair);
+    uint64_t blockp = ~0ull;
+    bool agreed = false;
+    for (int pass = 0; pass < 64 && !agreed; ++pass) {
+      if (hipMemsetAsync(blk, 0xFF, 8, stream) != hipSuccess || hipMemsetAsync(changes, 0, 4, stream) != hipSuccess)
+        return fail(-5);
+      hipLaunchKernelGGL(dec_classify_kernel<true>, grid, block, 0, stream, p, (const uint4*)raw, evs, nev32, prow, nd32,
+                         a->maxd, blockp, blk, changes, 1);
+      if (hipMemcpyAsync(a->h_scratch + 8, blk, 8, hipMemcpyDeviceToHost, stream) != hipSuccess) return fail(-5);
+      int same = 0;
+      const int prc = xcg_pair_decode_pass(a->pair, evs, p.decl_base, p.n_decl, n, ndecl, ndecl, &same, stream);
+      if (prc) return fail(prc);
+      const uint64_t nb = a->h_scratch[8];
+      if (getenv("XCG_PAIR_DEBUG"))
+        fprintf(stderr, "pair-dec: n %u pass %d same %d block %llx -> %llx\n", n, pass, same,
+                (unsigned long long)blockp, (unsigned long long)nb);
+      agreed = same && nb == blockp;
       blockp = nb;
     }
     if (!agreed) return fail(-75);
@@ -1149,6 +1221,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     (void)hipStreamSynchronize(stream);
     if (dfull) (void)hipFreeAsync(dfull, stream);
     if (lru_mem) (void)hipFreeAsync(lru_mem, stream);
+    if (pair_mem) (void)hipFreeAsync(pair_mem, stream);
     return -95;
   }
   *total_out = a->h_scratch[0];
@@ -1158,16 +1231,29 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   if (*total_out > a->out_cap) {
     if (dfull) (void)hipFreeAsync(dfull, stream);
     if (lru_mem) (void)hipFreeAsync(lru_mem, stream);
+    if (pair_mem) (void)hipFreeAsync(pair_mem, stream);
     return -75;
   }
   hipLaunchKernelGGL(decode_kernel<true>, grid, block, 0, stream, p);
   hipLaunchKernelGGL(decode_tend_kernel, dim3(1), dim3(1), 0, stream, p, ndecl);
-  if (!dfull) {
-    p.D = a->d_tail;
-    p.D_tail = true;
-    hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
+  if (!a->no_window) {
+    if (!dfull) {
+      p.D = a->d_tail;
+      p.D_tail = true;
+      hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
+    }
+    hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
   }
-  hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
+  if (a->pair) {
+    // the classification's declaration rows give each new entry's bytes
+    const PairGpu G{a->in, a->chunk_off, prow, a->maxd, a->pool, a->g_keys, a->g_vals, a->g_mask,
+                    a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask, a->nseg, a->status};
+    const int crc = xcg_pair_decode_commit(a->pair, &G, stream);
+    (void)hipFreeAsync(pair_mem, stream);
+    if (dfull) (void)hipFreeAsync(dfull, stream);
+    if (crc) return crc;
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   if (a->lru) {
     hipLaunchKernelGGL(dec_replace_kernel, grid, block, 0, stream, p, (const uint4*)raw, (const uint4*)evs, a->pool);
     const int crc = xcg_lru_commit(&lb, a->lru, stream);

@@ -402,8 +402,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
         if (stall) { q = q0; break; }
         __syncthreads();
         if (L.dlens[256] == 0 || !tables_for_block()) { mode = M_ERROR; break; }
-        for (uint32_t i = lane; i < nlen + ndist; i += 64) sp->lens[i] = L.dlens[i];   // for a later resume
-        mode = M_HUFF;
+        mode = M_HUFF;   // (its lengths reach sp->lens only when the call commits)
       } else {
         mode = M_ERROR;
         break;
@@ -548,6 +547,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
     if (np > PEND_CAP) status = -1;
     else {
       for (uint64_t i = lane; i < np; i += 64) sp->pend[i] = R.I[qb + i];
+      // A call that ends inside a dynamic block carries that block's code
+      // lengths for the next call's resume.  Written here, with the rest of
+      // the committed state, never while parsing: a call that ends in -2 (no
+      // room) must leave the stream exactly as it found it, and the block it
+      // resumes in is then still the one sp->lens describes.
+      if (mode == M_HUFF && btype == 2)
+        for (uint32_t i = lane; i < nlen + ndist; i += 64) sp->lens[i] = L.dlens[i];
       // history = the last 32 KiB of output: the old history moved down by this
       // call's output length (ascending, so no lane reads what another wrote),
       // then the output itself (flushed and fenced above)
@@ -788,6 +794,20 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
+  return XCG_OK;
+}
+
+// A fresh InflatePipe on slot `stream` (inflateInit, zlib/inflate_pipe.cc:38-50):
+// nothing of the slot's previous stream -- mode, totals, carried input,
+// history, adler32 -- survives.
+int xcg_zinflate_reset(xcg_zinflate* z, uint32_t stream) {
+  if (!z || stream >= z->nstreams) return XCG_EINVAL;
+  (void)hipSetDevice(z->device);
+  if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
+  IState s0;
+  memset(&s0, 0, sizeof s0);
+  s0.adler = 1;
+  if (hipMemcpy(z->st + stream, &s0, sizeof s0, hipMemcpyHostToDevice) != hipSuccess) return XCG_EHIP;
   return XCG_OK;
 }
 

@@ -239,6 +239,18 @@ struct EpochMap {
 // One primary slot / disk block / entity record each in one cache line:
 // the committed fields, then the pass's copy (valid while ep == the pass's
 // epoch).
+//
+// The disk is shared.  XCodecDisk is one FIFO for every XCodecDiskCache
+// front-end on it (xcodec/xcodec_cache_disk.h:33-69): the local cache and each
+// peer cache XCodecCache::connect makes (XCodecDisk::connect, xcodec_cache_
+// disk.cc:640-690) append to the same ring, index entries carry the front's
+// xuid, and when the write head enters an index block every front loses the
+// entries it still had there (index_invalidate_entries, :327-382, walking
+// xuid_cache_map_).  So the ring (XcgDiskState: blocks, their owner xuid, the
+// write clock) is one object; each pair context is a front (its xuid, its
+// primary, its hash index = the live blocks it owns).  A front's pass may
+// invalidate another front's entries: they are applied to that front when the
+// pass is kept, and reach its GPU table at its next call (pending list).
 struct PSlot {
   uint64_t key, okey;              // hash (NOKEY: free)
   uint32_t prev, next, pd;         // LRU links; the hash's disk block (NIL: not on disk)
@@ -246,8 +258,9 @@ struct PSlot {
 };
 struct DSlot {
   uint64_t key, okey;
-  uint32_t dp, odp;                // the hash's primary slot (NIL: disk only)
-  uint32_t owner, ep;
+  uint32_t dp, odp;                // the hash's primary slot in its owner front (NIL: disk only)
+  uint32_t owner, ep;              // (owner: entity of the pass's front, FOREIGN for another front's entry)
+  uint16_t xuid, oxuid;            // the front whose index entry this is (XCodecDisk index entry xuid)
   uint8_t live, olive;             // the disk index's entry for its hash
 };
 struct Ent {                       // a hash cached at the sub-batch start
@@ -259,27 +272,44 @@ struct NewEnt {                    // a declaration of the pass
   uint64_t key;
   uint32_t p, d, chunk, decl;
 };
+constexpr uint32_t FOREIGN = 0xFFFFFFFEu;
+
+struct XcgPairState;
+
+// One XCodecDisk: the ring and the fronts on it.
+struct XcgDiskState {
+  uint64_t nb = 0;                 // index blocks
+  uint32_t D = 0;                  // nb * 204 data blocks
+  uint64_t dclock = 0;             // entries written to the disk (every front)
+  uint32_t epoch = 0;              // pass epochs, unique across the fronts
+  std::vector<DSlot> ds;
+  std::vector<XcgPairState*> fronts;   // by xuid (nullptr: free)
+  int refs = 1;                    // the creator's reference + one per front
+};
 
 struct XcgPairState {
   uint32_t C = 0;                  // primary limit in segments
   uint64_t nb = 0;                 // disk index blocks
   uint32_t D = 0;                  // nb * 204 disk data blocks
+  XcgDiskState* disk = nullptr;
+  uint16_t xuid = 0;
   // committed scalars
   uint32_t head = NIL, tail = NIL, pcount = 0, ftop = 0;
   std::vector<uint32_t> pfree;     // free primary slots, pfree[0 .. ftop)
-  uint64_t dclock = 0;             // disk entries written
-  uint64_t dcount = 0;             // live disk index entries
+  uint64_t dlive = 0;              // this front's live disk index entries
   std::vector<PSlot> ps;
-  std::vector<DSlot> ds;
+  std::vector<DSlot>* dsp = nullptr;
+  // another front's kept pass took index entries of ours: ids to clear in keyg
+  std::vector<uint64_t> pending;
   // pass state
   uint32_t epoch = 0;
   std::vector<uint32_t> touchedP, touchedD;
   uint32_t s_head, s_tail, s_pcount, s_ftop;
-  uint64_t s_dclock, s_dcount;
+  uint64_t s_dclock, s_dlive;
   std::vector<Ent> es;
   std::vector<uint32_t> touchedE;
   std::vector<NewEnt> ns;
-  EpochMap bmap;                   // hash -> the pass's declaration
+  EpochMap bmap;                   // hash -> the pass's declaration (decode: any entity of the hash)
   // pass results
   bool split = false;
   std::vector<uint8_t> bad;        // per chunk: a recorded lookup the replay contradicts
@@ -287,6 +317,7 @@ struct XcgPairState {
   std::vector<uint4> writes;       // commit moves (dest, kind, a, b)
   uint32_t nstaged = 0;
   uint64_t enters = 0, refs = 0, appends = 0;
+  std::vector<uint64_t> leaves;    // decode: the (id, leave time) list ptime was last built from
   // device
   uint64_t* d_keyg = nullptr;      // [C + D]
   uint64_t* d_ptime = nullptr;     // [C + D]
@@ -301,10 +332,14 @@ struct XcgPairState {
   uint32_t* h_nev = nullptr;
   uint32_t h_nev_cap = 0;
   uint32_t* h_need = nullptr;
+  uint64_t* h_base = nullptr;      // decode: per-chunk row base and count (pinned)
+  uint32_t h_base_cap = 0;
   uint32_t last_base = 0;
   int prev_passes = 1;             // passes the last sub-batch needed
 
   uint32_t ids() const { return C + D; }
+  std::vector<DSlot>& ds() { return *dsp; }
+  const std::vector<DSlot>& ds() const { return *dsp; }
 
   // ---- the pass's view of a slot / block / entity (copied on first use)
   PSlot& P(uint32_t s) {
@@ -318,11 +353,11 @@ struct XcgPairState {
     return q;
   }
   DSlot& Dk(uint32_t i) {
-    DSlot& q = ds[i];
+    DSlot& q = ds()[i];
     if (q.ep != epoch) {
       q.ep = epoch;
-      q.okey = q.key; q.olive = q.live; q.odp = q.dp;
-      q.owner = q.live ? (q.dp != NIL ? q.dp : C + i) : NIL;
+      q.okey = q.key; q.olive = q.live; q.odp = q.dp; q.oxuid = q.xuid;
+      q.owner = !q.live ? NIL : (q.xuid != xuid ? FOREIGN : (q.dp != NIL ? q.dp : C + i));
       touchedD.push_back(i);
     }
     return q;
@@ -336,9 +371,9 @@ struct XcgPairState {
         e.p = q.key != NOKEY ? x : NIL;
         e.d = e.p != NIL ? q.pd : NIL;
       } else {
-        const DSlot& q = ds[x - C];
+        const DSlot& q = ds()[x - C];
         e.p = NIL;
-        e.d = q.live && q.dp == NIL ? x - C : NIL;
+        e.d = q.live && q.xuid == xuid && q.dp == NIL ? x - C : NIL;
       }
       e.ref = 0;
       e.leave = NEVER;
@@ -355,7 +390,10 @@ struct XcgPairState {
   // an entity's current primary slot / disk block
   uint32_t& ep(uint32_t x) { return is_new(x) ? ns[x - C - D].p : E(x).p; }
   uint32_t& ed(uint32_t x) { return is_new(x) ? ns[x - C - D].d : E(x).d; }
-  uint64_t ekey(uint32_t x) const { return is_new(x) ? ns[x - C - D].key : (x < C ? ps[x].key : ds[x - C].key); }
+  uint64_t ekey(uint32_t x) const {
+    return is_new(x) ? ns[x - C - D].key : (x < C ? ps[x].key : ds()[x - C].key);
+  }
+  bool present(uint32_t x) { return ep(x) != NIL || ed(x) != NIL; }
   // commit move of entity x's bytes to pool index `dest`
   void move_to(uint32_t dest, uint32_t x) {
     if (is_new(x)) writes.push_back(make_uint4(dest, 0u, ns[x - C - D].chunk, ns[x - C - D].decl));
@@ -403,7 +441,7 @@ struct XcgPairState {
       if (h.onext != NIL && h.ep == epoch) __builtin_prefetch(&ps[h.onext]);
       else if (h.next != NIL) __builtin_prefetch(&ps[h.next]);
       const uint32_t hd = h.ep == epoch ? h.opd : h.pd;
-      if (hd != NIL) __builtin_prefetch(&ds[hd]);
+      if (hd != NIL) __builtin_prefetch(&ds()[hd]);
     }
     q.okey = ekey(x);
     q.owner = x;
@@ -417,19 +455,20 @@ struct XcgPairState {
     ++enters;
   }
 
-  // XCodecDisk::enter (xcodec_cache_disk.cc:694-741)
+  // XCodecDisk::enter (xcodec_cache_disk.cc:694-741): the shared write head
   void d_append(uint32_t x, uint64_t t) {
     const uint32_t i = (uint32_t)(s_dclock % D);
     DSlot& q = Dk(i);
     q.okey = ekey(x);
     q.olive = 1;
+    q.oxuid = xuid;
     q.owner = x;
     const uint32_t p = ep(x);
     q.odp = p;
     if (p != NIL) P(p).opd = i;
     ed(x) = i;
     move_to(C + i, x);
-    ++s_dcount;
+    ++s_dlive;
     ++appends;
     if (++s_dclock % DISK_ENTRIES == 0) {          // the write head moves on: index_invalidate_entries
       const uint64_t b = (s_dclock / DISK_ENTRIES) % nb;
@@ -439,7 +478,8 @@ struct XcgPairState {
         const uint32_t y = r.owner;
         r.olive = 0;
         r.owner = NIL;
-        --s_dcount;
+        if (y == FOREIGN) continue;                // another front's entry: applied to it at keep()
+        --s_dlive;
         ed(y) = NIL;
         if (r.odp != NIL) P(r.odp).opd = NIL;      // now in the primary only
         else left(y, t);
@@ -469,31 +509,69 @@ struct XcgPairState {
     }
   }
 
-  // One replay pass over chunks [0, n) of the sub-batch: rows ev[c * maxe ..],
-  // nev[c].  Returns false if the pass is not the sequential one (bad[] and
-  // split tell why).
-  bool replay(uint32_t n, const uint4* ev, const uint32_t* nev, uint32_t maxe, uint32_t maxd) {
-    if (++epoch == 0) {
-      for (PSlot& q : ps) q.ep = 0;
-      for (DSlot& q : ds) q.ep = 0;
-      for (Ent& e : es) e.ep = 0;
-      epoch = 1;
+  // XCodecCachePair::replace (xcodec_cache.h:187-196) right after a lookup of
+  // x found other bytes (the decoder's name reuse, xcodec_decoder.cc:110-133;
+  // <LEARN>, xcodec_pipe_pair.cc:311-327): the primary keeps the slot (an LRU
+  // use: x is at the tail already) with the new bytes; the disk removes the
+  // hash and enters it again (XCodecDiskCache::replace, xcodec_cache_disk.h).
+  // The new bytes are a new entity y in x's place; x has left.
+  void replace(uint32_t x, uint64_t h, uint32_t c, uint32_t d, uint64_t t) {
+    const uint32_t y = C + D + (uint32_t)ns.size();
+    ns.push_back(NewEnt{h, NIL, NIL, c, d});
+    const uint32_t p = ep(x);                      // (the lookup made x primary-resident)
+    PSlot& q = P(p);
+    q.owner = y;
+    ep(y) = p;
+    ep(x) = NIL;
+    const uint32_t di = ed(x);
+    if (di != NIL) {                               // XCodecDisk::remove
+      DSlot& r = Dk(di);
+      r.olive = 0;
+      r.owner = NIL;
+      r.odp = NIL;
+      --s_dlive;
+      ed(x) = NIL;
+    }
+    q.opd = NIL;
+    move_to(p, y);
+    left(x, t);
+    bmap.put(h, y);
+    d_append(y, t);
+  }
+
+  void begin_pass(uint32_t n, uint64_t decls) {
+    epoch = ++disk->epoch;
+    if (epoch == 0) {                              // (2^32 passes: re-tag everything)
+      for (XcgPairState* f : disk->fronts) {
+        if (!f) continue;
+        for (PSlot& q : f->ps) q.ep = 0;
+        for (Ent& e : f->es) e.ep = 0;
+      }
+      for (DSlot& q : ds()) q.ep = 0;
+      epoch = disk->epoch = 1;
     }
     touchedP.clear();
     touchedD.clear();
     touchedE.clear();
     ns.clear();
-    bmap.reset((uint64_t)n * maxd);
+    bmap.reset(decls);
     writes.clear();
-    writes.reserve((size_t)n * maxd * 2);
-    ns.reserve((size_t)n * maxd);
+    writes.reserve((size_t)decls * 2);
+    ns.reserve((size_t)decls);
     nstaged = 0;
     enters = refs = appends = 0;
     split = false;
     bad.assign(n, 0);
     blo.assign(n, ~0u);
     bhi.assign(n, 0u);
-    s_head = head; s_tail = tail; s_pcount = pcount; s_ftop = ftop; s_dclock = dclock; s_dcount = dcount;
+    s_head = head; s_tail = tail; s_pcount = pcount; s_ftop = ftop; s_dclock = disk->dclock; s_dlive = dlive;
+  }
+
+  // One replay pass over chunks [0, n) of the sub-batch: rows ev[c * maxe ..],
+  // nev[c].  Returns false if the pass is not the sequential one (bad[] and
+  // split tell why).
+  bool replay(uint32_t n, const uint4* ev, const uint32_t* nev, uint32_t maxe, uint32_t maxd) {
+    begin_pass(n, (uint64_t)n * maxd);
     std::vector<uint32_t> order;
     bool ok = true;
     for (uint32_t c = 0; c < n && !split; ++c) {
@@ -516,7 +594,7 @@ struct XcgPairState {
             if (fr < C + D) {
               __builtin_prefetch(&es[fr]);
               if (fr < C) __builtin_prefetch(&ps[fr]);
-              else __builtin_prefetch(&ds[fr - C]);
+              else __builtin_prefetch(&ds()[fr - C]);
             }
           } else {
             bmap.prefetch(((uint64_t)f.y << 32) | f.x);
@@ -528,18 +606,17 @@ struct XcgPairState {
         const uint64_t h = ((uint64_t)e.y << 32) | e.x;
         if (kind == EV_GHIT || kind == EV_GMISS) {
           if (ref >= C + D) { mark_bad(c, e.z); ok = false; continue; }
-          const Ent& en = E(ref);
-          const bool present = en.p != NIL || en.d != NIL;
-          if (present != (kind == EV_GHIT)) { mark_bad(c, e.z); ok = false; }
-          if (present) lookup(ref, t);
+          const bool pr = present(ref);
+          if (pr != (kind == EV_GHIT)) { mark_bad(c, e.z); ok = false; }
+          if (pr) lookup(ref, t);
         } else if (kind == EV_HIT) {
           const uint32_t x = bmap.find(h);
           if (x == NIL) { mark_bad(c, e.z); ok = false; continue; }
-          if (ep(x) == NIL && ed(x) == NIL) { split = true; break; }   // made here, gone already
+          if (!present(x)) { split = true; break; }   // made here, gone already
           lookup(x, t);
         } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
           const uint32_t x0 = bmap.find(h);
-          if (x0 != NIL && (ep(x0) != NIL || ed(x0) != NIL)) { mark_bad(c, e.z); ok = false; continue; }
+          if (x0 != NIL && present(x0)) { mark_bad(c, e.z); ok = false; continue; }
           const uint32_t x = C + D + (uint32_t)ns.size();
           ns.push_back(NewEnt{h, NIL, NIL, c, ref});
           bmap.put(h, x);
@@ -551,17 +628,72 @@ struct XcgPairState {
     return ok && !split;
   }
 
-  // Keep the pass: its copies -> committed.
+  // One replay pass over a decode batch's classified ops (dec_classify_kernel
+  // in pair mode): chunk c's rows are rows[base[c] .. base[c] + cnt[c]) in op
+  // order, (lo, hi, op offset | REPLACE << 31, kind << 30 | ref).  ENTER (ref =
+  // declaration row) = an EXTRACT whose hash no level holds: enter both
+  // levels; HIT = a lookup of a hash an earlier EXTRACT of the batch named;
+  // GHIT (ref = id) = a lookup of a cached hash, REPLACE when an EXTRACT's
+  // bytes differ; GMISS = no cache effect.  A decode's references are fixed by
+  // the stream except for presence, which this pass computes (ptime); the
+  // caller classifies again under it until nothing changes.  Returns false
+  // when a lookup would find a hash the batch entered already gone from both
+  // levels (the stream then blocks or re-enters there: not modelled -- split).
+  bool replay_decode(uint32_t n, const uint4* rows, const uint64_t* base, const uint64_t* cnt, uint64_t decls) {
+    begin_pass(n, decls);
+    for (uint32_t c = 0; c < n; ++c) {
+      const uint4* r = rows + base[c];
+      const uint32_t m = (uint32_t)cnt[c];
+      uint32_t d_next = 0;                         // declaration rows in op order: ENTERs and REPLACEs
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint4 e = r[k];
+        const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
+        const bool rep = (e.z >> 31) != 0;
+        const uint64_t t = ((uint64_t)c << 21) | (e.z & 0x7FFFFFFFu);
+        const uint64_t h = ((uint64_t)e.y << 32) | e.x;
+        if (kind == EV_ENTER) {
+          const uint32_t x = C + D + (uint32_t)ns.size();
+          ns.push_back(NewEnt{h, NIL, NIL, c, ref});
+          d_next = ref + 1;
+          bmap.put(h, x);
+          p_enter(x, t);
+          d_append(x, t);
+        } else if (kind == EV_HIT) {
+          const uint32_t x = bmap.find(h);
+          if (x == NIL || !present(x)) { split = true; return false; }
+          lookup(x, t);
+        } else if (kind == EV_GHIT) {
+          if (ref >= C + D) { split = true; return false; }
+          if (bmap.find(h) == NIL) bmap.put(h, ref);
+          if (!present(ref)) continue;             // (classified under an older ptime: the next pass sees it)
+          lookup(ref, t);
+          if (rep) replace(ref, h, c, d_next++, t);
+        }
+      }
+    }
+    return true;
+  }
+
+  // Keep the pass: its copies -> committed; another front's entries the pass
+  // invalidated leave that front.
   void keep() {
     for (uint32_t s : touchedP) {
       PSlot& q = ps[s];
       q.key = q.okey; q.prev = q.oprev; q.next = q.onext; q.pd = q.opd;
     }
     for (uint32_t i : touchedD) {
-      DSlot& q = ds[i];
-      q.key = q.okey; q.live = q.olive; q.dp = q.odp;
+      DSlot& q = ds()[i];
+      if (q.live && !q.olive && q.xuid != xuid) {  // another front's index entry went
+        XcgPairState* f = q.xuid < disk->fronts.size() ? disk->fronts[q.xuid] : nullptr;
+        if (f) {
+          --f->dlive;
+          if (q.dp != NIL) f->ps[q.dp].pd = NIL;   // in its primary only now
+          else f->pending.push_back((uint64_t)f->C + i);
+        }
+      }
+      q.key = q.okey; q.live = q.olive; q.dp = q.odp; q.xuid = q.oxuid;
     }
-    head = s_head; tail = s_tail; pcount = s_pcount; ftop = s_ftop; dclock = s_dclock; dcount = s_dcount;
+    head = s_head; tail = s_tail; pcount = s_pcount; ftop = s_ftop; disk->dclock = s_dclock; dlive = s_dlive;
   }
 };
 
@@ -657,12 +789,12 @@ uint64_t host_hash(const uint8_t* w) {
 
 // Diagnostics (XCG_PAIR_VERIFY): every primary slot and live disk block holds
 // bytes of its hash, and G finds every level entry.
-void pair_verify(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
+void pair_verify(XcgPairState* P, const uint8_t* d_pool, hipStream_t st) {
   const uint64_t ids = P->ids();
   std::vector<uint8_t> pool(ids * SEG);
   std::vector<uint64_t> keyg(ids);
   (void)hipStreamSynchronize(st);
-  (void)hipMemcpy(pool.data(), a.pool, ids * SEG, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(pool.data(), d_pool, ids * SEG, hipMemcpyDeviceToHost);
   (void)hipMemcpy(keyg.data(), P->d_keyg, 8 * ids, hipMemcpyDeviceToHost);
   uint32_t bad = 0;
   for (uint32_t s = 0; s < P->C; ++s) {
@@ -671,25 +803,42 @@ void pair_verify(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
     if (host_hash(&pool[(uint64_t)s * SEG]) != q.key && bad++ < 5)
       fprintf(stderr, "pair verify: primary slot %u bytes do not hash to its key\n", s);
     if (keyg[s] != q.key && bad++ < 5) fprintf(stderr, "pair verify: keyg[%u] stale\n", s);
-    if (q.pd != NIL && (P->ds[q.pd].key != q.key || !P->ds[q.pd].live) && bad++ < 5)
+    if (q.pd != NIL && (P->ds()[q.pd].key != q.key || !P->ds()[q.pd].live || P->ds()[q.pd].xuid != P->xuid) &&
+        bad++ < 5)
       fprintf(stderr, "pair verify: slot %u links disk block %u of another hash\n", s, q.pd);
   }
+  uint64_t mine = 0;
   for (uint32_t i = 0; i < P->D; ++i) {
-    const DSlot& q = P->ds[i];
-    if (!q.live) continue;
+    const DSlot& q = P->ds()[i];
+    const bool own = q.live && q.xuid == P->xuid;
+    mine += own;
+    const uint64_t want = own && q.dp == NIL ? q.key : NOKEY;
+    if (keyg[P->C + i] != want && bad++ < 5) fprintf(stderr, "pair verify: keyg[C+%u] stale\n", i);
+    if (!own) continue;
     if (host_hash(&pool[((uint64_t)P->C + i) * SEG]) != q.key && bad++ < 5)
       fprintf(stderr, "pair verify: disk block %u bytes do not hash to its key\n", i);
-    const uint64_t want = q.dp == NIL ? q.key : NOKEY;
-    if (keyg[P->C + i] != want && bad++ < 5) fprintf(stderr, "pair verify: keyg[C+%u] stale\n", i);
     if (q.dp != NIL && P->ps[q.dp].key != q.key && bad++ < 5)
       fprintf(stderr, "pair verify: disk block %u links slot %u of another hash\n", i, q.dp);
   }
+  if (mine != P->dlive && bad++ < 5) fprintf(stderr, "pair verify: %llu own disk entries, count says %llu\n",
+                                             (unsigned long long)mine, (unsigned long long)P->dlive);
   fprintf(stderr, "pair verify: %u problems (primary %u, disk live %llu)\n", bad, P->pcount,
-          (unsigned long long)P->dcount);
+          (unsigned long long)P->dlive);
+}
+
+// G from scratch: wipe, then every id whose keyg holds a hash.
+void pair_rebuild(XcgPairState* P, const PairGpu& G, hipStream_t st) {
+  const HashTab g{G.g_keys, G.g_vals, G.g_mask};
+  const FiltSet fs{G.g_filt, G.g_ftab, G.fmask, G.g_gfilt, G.gmask};
+  PairWipe wp{g, G.g_filt, (u32x4*)G.g_ftab, G.fmask + 1, G.g_gfilt, G.gmask + 1, G.nseg};
+  hipLaunchKernelGGL(pair_wipe_kernel, dim3(1024), dim3(256), 0, st, wp);
+  const uint32_t ids = P->ids();
+  hipLaunchKernelGGL(pair_rebuild_kernel, dim3(grid_for(ids)), dim3(256), 0, st, (const uint64_t*)P->d_keyg, ids,
+                     g, fs, G.nseg, G.status);
 }
 
 // Commit a kept pass on the GPU: bytes, per-id keys, G and its filters.
-int pair_commit(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
+int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   // A primary slot can change hands more than once in a sub-batch (an entry
   // evicted to disk frees it again), and a small disk can lap within one:
   // only the last move into each destination stays.  (Sources are the input or
@@ -706,17 +855,18 @@ int pair_commit(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
     w.erase(w.begin(), w.begin() + (ptrdiff_t)k);
   }
   const uint32_t nw = (uint32_t)P->writes.size();
-  // per-id key updates for every slot the pass touched
+  // per-id key updates for every slot the pass touched (a disk block counts
+  // for this front only while its live index entry is this front's)
   std::vector<uint64_t> kv;
-  kv.reserve(2 * (P->touchedP.size() + P->touchedD.size()));
+  kv.reserve(2 * (P->touchedP.size() + P->touchedD.size() + P->pending.size()));
   for (uint32_t s : P->touchedP) {
     kv.push_back(s);
     kv.push_back(P->ps[s].key);
   }
   for (uint32_t i : P->touchedD) {
-    const DSlot& q = P->ds[i];
+    const DSlot& q = P->ds()[i];
     kv.push_back((uint64_t)P->C + i);
-    kv.push_back(q.live && q.dp == NIL ? q.key : NOKEY);
+    kv.push_back(q.live && q.xuid == P->xuid && q.dp == NIL ? q.key : NOKEY);
   }
   const uint32_t nk = (uint32_t)(kv.size() / 2);
   const uint64_t wbytes = 16ull * nw, kbytes = 8ull * kv.size();
@@ -729,40 +879,93 @@ int pair_commit(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
   if (upload(P, 0, wbytes + kbytes, st)) return -5;
   const uint4* w = (const uint4*)P->d_xfer;
   if (nw) {
-    hipLaunchKernelGGL(pair_stage_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, (const uint8_t*)a.pool,
+    hipLaunchKernelGGL(pair_stage_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, (const uint8_t*)G.pool,
                        P->d_staging);
-    hipLaunchKernelGGL(pair_move_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, a.in, a.chunk_off,
-                       (const uint4*)a.decl, a.maxd, (const uint8_t*)P->d_staging, a.pool);
+    hipLaunchKernelGGL(pair_move_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, G.in, G.chunk_off,
+                       (const uint4*)G.decl, G.maxd, (const uint8_t*)P->d_staging, G.pool);
   }
   if (nk)
     hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(nk)), dim3(256), 0, st, P->d_keyg,
                        (const uint64_t*)(P->d_xfer + wbytes), nk);
-  const HashTab g{a.g_keys, a.g_vals, a.g_mask};
-  PairWipe wp{g, a.g_filt, (u32x4*)a.g_ftab, a.fmask + 1, a.g_gfilt, a.gmask + 1, a.nseg};
-  hipLaunchKernelGGL(pair_wipe_kernel, dim3(1024), dim3(256), 0, st, wp);
-  const uint32_t ids = P->ids();
-  hipLaunchKernelGGL(pair_rebuild_kernel, dim3(grid_for(ids)), dim3(256), 0, st, (const uint64_t*)P->d_keyg, ids, g,
-                     FiltSet{a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask}, a.nseg, a.status);
+  pair_rebuild(P, G, st);
   // (the pinned transfer area is free again once the stream passes here)
   return hipStreamSynchronize(st) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Index entries another front's kept pass took from this one (the shared
+// ring's invalidations): clear their ids and rebuild G before this front's
+// next batch looks anything up.
+int pair_sync_pending(XcgPairState* P, const PairGpu& G, hipStream_t st) {
+  if (P->pending.empty()) return 0;
+  const uint32_t m = (uint32_t)P->pending.size();
+  std::vector<uint64_t> kv(2ull * m);
+  for (uint32_t j = 0; j < m; ++j) {
+    kv[2 * j] = P->pending[j];
+    kv[2 * j + 1] = NOKEY;
+  }
+  P->pending.clear();
+  if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * m) || ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * m))
+    return -5;
+  memcpy(P->h_xfer, kv.data(), 16ull * m);
+  if (upload(P, 0, 16ull * m, st)) return -5;
+  hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_keyg,
+                     (const uint64_t*)P->d_xfer, m);
+  pair_rebuild(P, G, st);
+  return hipStreamSynchronize(st) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+PairGpu gpu_of(const XcgStreamArgs& a) {
+  return PairGpu{a.in, a.chunk_off, a.decl, a.maxd, a.pool, a.g_keys, a.g_vals, a.g_mask,
+                 a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask, a.nseg, a.status};
 }
 
 }  // namespace
 
 extern "C" {
 
-int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out) {
+int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out) {
   const uint64_t blocks = disk_bytes / SEG;
-  if (C == 0 || blocks <= 18) return -22;
+  if (blocks <= 18) return -22;
   const uint64_t nb = (blocks - 18) / (1 + DISK_ENTRIES);   // xcodec_cache_disk.cc:110-111
-  if (nb == 0 || nb * DISK_ENTRIES + C >= (1ull << 30)) return -22;
+  if (nb == 0 || nb * DISK_ENTRIES >= (1ull << 29)) return -22;
+  XcgDiskState* K = new XcgDiskState;
+  K->nb = nb;
+  K->D = (uint32_t)(nb * DISK_ENTRIES);
+  K->ds.assign(K->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0, 0, 0});
+  *out = K;
+  return 0;
+}
+
+void xcg_disk_state_release(XcgDiskState* K) {
+  if (K && --K->refs == 0) delete K;
+}
+
+void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
+  uint64_t live = 0, fronts = 0;
+  for (const DSlot& q : K->ds) live += q.live;
+  for (const XcgPairState* f : K->fronts) fronts += f != nullptr;
+  st[0] = live;
+  st[1] = K->dclock;
+  st[2] = K->nb;
+  st[3] = fronts;
+}
+
+// A pair front on disk K (XCodecDisk::local for the first, ::connect for the
+// others: the lowest free xuid, xcodec_cache_disk.cc:640-690).
+int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
+  if (C == 0 || !K || (uint64_t)K->D + C >= (1ull << 30)) return -22;
+  uint32_t xuid = 0;
+  while (xuid < K->fronts.size() && K->fronts[xuid]) ++xuid;
+  if (xuid >= 1024) return -22;                             // XCDFS_XUID_COUNT
   XcgPairState* P = new XcgPairState;
   P->C = C;
-  P->nb = nb;
-  P->D = (uint32_t)(nb * DISK_ENTRIES);
+  P->nb = K->nb;
+  P->D = K->D;
+  P->disk = K;
+  P->dsp = &K->ds;
+  P->xuid = (uint16_t)xuid;
   const uint32_t D = P->D, ids = C + D;
   P->ps.assign(C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
-  P->ds.assign(D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0});
   P->es.assign(ids, Ent{NEVER, 0, NIL, NIL, 0});
   P->pfree.resize(C);
   for (uint32_t s = 0; s < C; ++s) P->pfree[s] = C - 1 - s;   // slot 0 first
@@ -774,10 +977,16 @@ int xcg_pair_state_create(uint32_t C, uint64_t disk_bytes, XcgPairState** out) {
     delete P;
     return -12;
   }
+  if (xuid >= K->fronts.size()) K->fronts.resize(xuid + 1, nullptr);
+  K->fronts[xuid] = P;
+  ++K->refs;
   *out = P;
   return 0;
 }
 
+// A front goes away (its XCodecCache is deleted): its entries stay in the
+// ring as entries of no live front (index_invalidate_entries skips an xuid
+// with no cache, xcodec_cache_disk.cc:360-364).
 void xcg_pair_state_destroy(XcgPairState* P) {
   if (!P) return;
   (void)hipFree(P->d_keyg); (void)hipFree(P->d_ptime); (void)hipFree(P->d_staging); (void)hipFree(P->d_xfer);
@@ -785,32 +994,132 @@ void xcg_pair_state_destroy(XcgPairState* P) {
   if (P->h_ev) (void)hipHostFree(P->h_ev);
   if (P->h_nev) (void)hipHostFree(P->h_nev);
   if (P->h_need) (void)hipHostFree(P->h_need);
+  if (P->h_base) (void)hipHostFree(P->h_base);
+  XcgDiskState* K = P->disk;
+  if (K) {
+    for (DSlot& q : K->ds)
+      if (q.live && q.xuid == P->xuid) q.live = 0;
+    K->fronts[P->xuid] = nullptr;
+    xcg_disk_state_release(K);
+  }
   delete P;
 }
 
-// Drop everything (XCodecCache objects have no clear; this is a fresh pair on
-// an empty volume).  The caller wipes G itself.
+// Drop everything this front holds (XCodecCache objects have no clear: this is
+// a fresh front; on a disk of its own, a fresh volume).  The caller wipes G.
 int xcg_pair_state_clear(XcgPairState* P) {
+  XcgDiskState* K = P->disk;
   P->ps.assign(P->C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
-  P->ds.assign(P->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0});
+  uint64_t others = 0;
+  for (const XcgPairState* f : K->fronts) others += f && f != P;
+  for (DSlot& q : K->ds) {
+    if (q.live && q.xuid == P->xuid) q.live = 0;
+    q.dp = q.xuid == P->xuid ? NIL : q.dp;
+  }
+  if (others == 0) {
+    K->ds.assign(K->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0, 0, 0});
+    K->dclock = 0;
+  }
   for (Ent& e : P->es) e.ep = 0;
-  P->epoch = 0;
   for (uint32_t s = 0; s < P->C; ++s) P->pfree[s] = P->C - 1 - s;
   P->ftop = P->C;
   P->head = P->tail = NIL;
   P->pcount = 0;
-  P->dclock = P->dcount = 0;
+  P->dlive = 0;
+  P->pending.clear();
   return hipMemset(P->d_keyg, 0xFF, 8ull * P->ids()) == hipSuccess ? 0 : -5;
 }
 
 void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st) {
   st[0] = P->pcount;
-  st[1] = P->dcount;
-  st[2] = P->dclock;
+  st[1] = P->dlive;
+  st[2] = P->disk->dclock;
   st[3] = P->nb;
 }
 
 uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; }
+uint32_t xcg_pair_state_limit(const XcgPairState* P) { return P->C; }
+uint32_t xcg_pair_state_disk_blocks(const XcgPairState* P) { return P->D; }
+const uint64_t* xcg_pair_state_ptime(const XcgPairState* P) { return P->d_ptime; }
+
+int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st) { return pair_sync_pending(P, *G, st); }
+
+// Decode on the pair, first step: ptime NEVER everywhere.
+int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st) {
+  P->leaves.clear();
+  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// One replay of a decode batch's classified ops (rows packed per chunk at
+// d_base[c], d_cnt[c] of them; `rows` total).  *same = the departure times it
+// computes equal those the classification used (then it was the sequential
+// decoder's).  Otherwise ptime is updated for the next classification.
+// Returns 0, -95 (a hash this batch entered is gone before a later lookup),
+// -5.
+int xcg_pair_decode_pass(XcgPairState* P, const void* d_rows, const uint64_t* d_base, const uint64_t* d_cnt,
+                         uint32_t n, uint64_t rows, uint64_t decls, int* same, hipStream_t st) {
+  if (P->h_ev_cap < rows + 1) {
+    if (P->h_ev) (void)hipHostFree(P->h_ev);
+    P->h_ev = nullptr;
+    P->h_ev_cap = 0;
+    if (hipHostMalloc(&P->h_ev, 16 * (rows + 1)) != hipSuccess) return -5;
+    P->h_ev_cap = rows + 1;
+  }
+  if (P->h_base_cap < n) {
+    if (P->h_base) (void)hipHostFree(P->h_base);
+    P->h_base = nullptr;
+    P->h_base_cap = 0;
+    if (hipHostMalloc(&P->h_base, 16ull * n) != hipSuccess) return -5;
+    P->h_base_cap = n;
+  }
+  if ((rows && hipMemcpyAsync(P->h_ev, d_rows, 16 * rows, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipMemcpyAsync(P->h_base, d_base, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(P->h_base + n, d_cnt, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return -5;
+  if (!P->replay_decode(n, P->h_ev, P->h_base, P->h_base + n, decls)) return -95;
+  std::vector<uint64_t> lv;
+  for (uint32_t x : P->touchedE)
+    if (P->es[x].leave != NEVER) {
+      lv.push_back(x);
+      lv.push_back(P->es[x].leave);
+    }
+  {
+    std::vector<std::pair<uint64_t, uint64_t>> pr(lv.size() / 2);
+    for (size_t j = 0; j < pr.size(); ++j) pr[j] = {lv[2 * j], lv[2 * j + 1]};
+    std::sort(pr.begin(), pr.end());
+    for (size_t j = 0; j < pr.size(); ++j) {
+      lv[2 * j] = pr[j].first;
+      lv[2 * j + 1] = pr[j].second;
+    }
+  }
+  *same = lv == P->leaves;
+  if (*same) return 0;
+  P->leaves = lv;
+  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+  const uint32_t m = (uint32_t)(lv.size() / 2);
+  if (m) {
+    if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * m) || ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * m))
+      return -5;
+    memcpy(P->h_xfer, lv.data(), 16ull * m);
+    if (upload(P, 0, 16ull * m, st)) return -5;
+    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_ptime,
+                       (const uint64_t*)P->d_xfer, m);
+  }
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -5;
+}
+
+// Keep the last decode replay and commit it (bytes from the batch input at the
+// declaration rows: G.decl[c * maxd + d].z = the EXTRACT payload's offset).
+int xcg_pair_decode_commit(XcgPairState* P, const PairGpu* G, hipStream_t st) {
+  P->keep();
+  const int rc = pair_commit(P, *G, st);
+  if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, G->pool, st);
+  P->leaves.clear();
+  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+  return rc;
+}
 
 // Stream-semantics encode of a batch on the pair, in sub-batches (see the top
 // of this file).  Returns 0, -75 (no consistent pass / overflow), -95 (one
@@ -818,6 +1127,7 @@ uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; 
 int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds_out, hipStream_t st) {
   const uint32_t n = a0->n;
   int rounds = 0;
+  if (pair_sync_pending(P, gpu_of(*a0), st)) return -5;
   // A sub-batch is bounded by the disk only: while it writes fewer than a lap
   // of disk blocks, nothing it declared can leave both levels within it (a
   // chunk writes at most maxd declarations plus its touches).
@@ -913,11 +1223,11 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     }
     const clk::time_point t3 = clk::now();
     P->keep();
-    if (pair_commit(P, a, st)) return -5;
+    if (pair_commit(P, gpu_of(a), st)) return -5;
     if (pair_debug())
       fprintf(stderr, "pair: ms seed %.2f seed-replay %.2f parse %.2f download %.2f replay %.2f commit %.2f\n",
               ms(t0, t1), ms(t1, t2), t_parse, t_dl, t_replay, ms(t3, clk::now()));
-    if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, a, st);
+    if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, a.pool, st);
     // the next sub-batch starts with every hash visible to its end
     hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
     P->last_base = i0;

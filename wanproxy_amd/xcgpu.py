@@ -73,6 +73,14 @@ def lib():
     L.xcg_ctx_create_bounded.restype = C.c_int
     L.xcg_ctx_create_pair.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_pair.restype = C.c_int
+    L.xcg_disk_create.argtypes = [C.c_uint64, C.POINTER(C.c_void_p)]
+    L.xcg_disk_create.restype = C.c_int
+    L.xcg_disk_destroy.argtypes = [vp]
+    L.xcg_disk_destroy.restype = None
+    L.xcg_disk_stats.argtypes = [vp, vp]
+    L.xcg_disk_stats.restype = C.c_int
+    L.xcg_ctx_create_pair_on.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_pair_on.restype = C.c_int
     L.xcg_pair_stats.argtypes = [vp, vp]
     L.xcg_pair_stats.restype = C.c_int
     L.xcg_ctx_flags.argtypes = [vp, vp]
@@ -156,23 +164,55 @@ def encode_bound(n: int) -> int:
     return 2 * int(n) + 16
 
 
+class Disk:
+    """One XCodecDisk shared by several pair contexts (xcg_disk_create): the
+    local cache's front and each peer front XCodecCache::connect makes append
+    to one FIFO ring (xcodec/xcodec_cache_disk.h:33-69)."""
+
+    def __init__(self, disk_bytes: int):
+        h = C.c_void_p()
+        _check(lib().xcg_disk_create(int(disk_bytes), C.byref(h)))
+        self.h = h
+
+    def stats(self):
+        """(live index entries of every front, entries written, index blocks, fronts)."""
+        st = (C.c_uint64 * 4)()
+        _check(lib().xcg_disk_stats(self.h, st))
+        return tuple(int(v) for v in st)
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().xcg_disk_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
     """An XCodecEncoder + cache configuration bound to one GPU."""
 
     def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
-                 cache_segments: int = 1 << 19, memory_cache_limit: int = 0, disk_bytes: int = 0):
+                 cache_segments: int = 1 << 19, memory_cache_limit: int = 0, disk_bytes: int = 0,
+                 disk: Disk = None):
         """memory_cache_limit (bytes): the bounded, LRU-evicting cache
         XCodecMemoryCache(uuid, memory_cache_limit) (xcodec/xcodec_cache.h:277)
         instead of an unbounded one of cache_segments capacity.  With
         disk_bytes too: wanproxy.conf's XCodecCachePair of that memory cache
-        and a disk of disk_bytes (xcodec/xcodec_cache.h:140-237)."""
+        and a disk of disk_bytes (xcodec/xcodec_cache.h:140-237); with `disk`
+        instead, the pair's secondary is the next front of that shared disk."""
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        if disk_bytes:
+        if disk is not None:
+            _check(lib().xcg_ctx_create_pair_on(device, self.flags, int(memory_cache_limit), disk.h, C.byref(h)))
+        elif disk_bytes:
             _check(lib().xcg_ctx_create_pair(device, self.flags, int(memory_cache_limit), int(disk_bytes), C.byref(h)))
         elif memory_cache_limit:
             _check(lib().xcg_ctx_create_bounded(device, self.flags, int(memory_cache_limit), C.byref(h)))
@@ -200,8 +240,8 @@ class Context:
         _check(lib().xcg_cache_enter_host(self.h, C.c_uint64(h), (C.c_uint8 * 2048).from_buffer_copy(seg)))
 
     def pair_stats(self):
-        """(primary entries, disk index entries, disk entries written, disk
-        index blocks) of a pair context."""
+        """(primary entries, this front's disk index entries, disk entries
+        written by every front, disk index blocks) of a pair context."""
         st = (C.c_uint64 * 4)()
         _check(lib().xcg_pair_stats(self.h, st))
         return tuple(int(v) for v in st)

@@ -47,6 +47,8 @@ def _lib():
         L.xcg_zinflate_create.restype = C.c_int
         L.xcg_zinflate_destroy.argtypes = [vp]
         L.xcg_zinflate_destroy.restype = None
+        L.xcg_zinflate_reset.argtypes = [vp, C.c_uint32]
+        L.xcg_zinflate_reset.restype = C.c_int
         L.xcg_zinflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.xcg_zinflate_batch.restype = C.c_int
         L._zd_bound = True
@@ -155,6 +157,10 @@ class InflatePipes:
 
     def __del__(self):
         self.close()
+
+    def reset(self, stream: int):
+        """Slot `stream` becomes a fresh InflatePipe (inflateInit)."""
+        _check(_lib().xcg_zinflate_reset(self.h, stream))
 
     def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, out_cap, d_out_len, d_status, stream=None):
         in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
