@@ -272,6 +272,24 @@ int xcg_decode_host(xcg_ctx *ctx, const uint8_t *h_enc, uint64_t enc_len, const 
                     uint64_t *h_out_len, int32_t *h_chunk_status, uint64_t *h_consumed, uint64_t *h_unknown,
                     uint32_t unknown_cap, uint32_t *h_nunknown);
 
+/* One XCodecDecoder::decode(output, input, unknown_hashes) call from host
+ * memory (xcodec/xcodec_decoder.cc:66-272), the way tack (-d, one call per
+ * 64 KiB read, programs/tack/tack.cc:329-359) and XCodecPipePair
+ * (xcodec_pipe_pair.cc:425-446) make it: h_in[0 .. len) continues the
+ * context's stream (cache, current window).  *h_status / *h_consumed as
+ * xcg_decode_batch's for one chunk; decode_skim's unknown hashes sorted in
+ * h_unknown.  On an unbounded cache an input of <= 1 MiB is decoded in ONE
+ * launch and one synchronisation on the context's staging and stream, and the
+ * XCodecHash of every EXTRACT before the stop comes back in op order
+ * (h_extract_hash, *h_nextract; XCG_NO_REFERENCES when not provided: other
+ * caches, larger inputs, BACKREF ops -- those take the batch decoder), so a
+ * host cache mirror needs no hashing.  XCG_EOVERFLOW if out_cap is too small
+ * (*h_out_len = the size needed; nothing is committed). */
+int xcg_decode_call(xcg_ctx *ctx, const uint8_t *h_in, uint32_t len, uint8_t *h_out, uint64_t out_cap,
+                    uint64_t *h_out_len, uint64_t *h_consumed, int32_t *h_status, uint64_t *h_unknown,
+                    uint32_t unknown_cap, uint32_t *h_nunknown, uint64_t *h_extract_hash, uint32_t extract_cap,
+                    uint32_t *h_nextract);
+
 /* Pack n output slots (d_out + d_out_off[i], d_out_len[i] bytes) back to back
  * into d_packed; d_packed_off[i] receives each chunk's offset and *d_total
  * (device) the packed size.  Asynchronous on `stream`. */

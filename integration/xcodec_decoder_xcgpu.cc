@@ -39,11 +39,15 @@ XCodecDecoder::~XCodecDecoder()
 	xcgpu_binding::forget_window(this);
 }
 
-/* Host cache mirror of the EXTRACTs in in[a..b) (enter / replace, :106-136). */
+/* Host cache mirror of the EXTRACTs in in[a..b) (enter / replace, :106-136).
+ * hashes: their XCodecHash in op order when the engine returned them (nh of
+ * them), else NULL and they are computed here. */
 static void
-mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, uint64_t b)
+mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, uint64_t b,
+                const uint64_t *hashes = NULL, uint32_t nh = 0)
 {
 	uint64_t i = a;
+	uint32_t e = 0;
 	while (i + 1 < b) {
 		if (in[i] != XCODEC_MAGIC) {
 			i++;
@@ -52,7 +56,8 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 		const uint8_t op = in[i + 1];
 		if (op == XCODEC_OP_EXTRACT) {
 			const uint8_t *p = &in[i + 2];
-			const uint64_t hash = XCodecHash::hash(p);
+			const uint64_t hash = hashes != NULL && e < nh ? hashes[e] : XCodecHash::hash(p);
+			e++;
 			Buffer tmp(p, XCODEC_SEGMENT_LENGTH);
 			BufferSegment *seg;
 			tmp.copyout(&seg, XCODEC_SEGMENT_LENGTH);
@@ -236,7 +241,7 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	std::vector<uint8_t> in(len);
 	input->copyout(&in[0], len);
 	std::vector<uint8_t> out;
-	std::vector<uint64_t> unk(1u << 16);
+	std::vector<uint64_t> unk(1u << 16), ext(1024);
 	std::vector<uint64_t> piece, coff, ooff, olen, cons;
 	std::vector<uint32_t> clen;
 	std::vector<int32_t> cst;
@@ -268,8 +273,16 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		const uint64_t span = piece[k1] - pos;
 		out.resize(decoded_bound(in, pos, piece[k1]) + 1);
 		nunk = 0;
-		int rc = xcg_decode_host(ctx, &in[pos], span, &coff[0], &clen[0], n, &out[0], out.size(), &ooff[0], &olen[0],
-		                         &cst[0], &cons[0], &unk[0], unk.size(), &nunk);
+		int rc;
+		uint32_t next = XCG_NO_REFERENCES;
+		if (n == 1) {		/* one launch, one synchronisation (xcg_decode_call) */
+			ooff[0] = 0;
+			rc = xcg_decode_call(ctx, &in[pos], clen[0], &out[0], out.size(), &olen[0], &cons[0], &cst[0],
+			                     &unk[0], unk.size(), &nunk, &ext[0], ext.size(), &next);
+		} else {
+			rc = xcg_decode_host(ctx, &in[pos], span, &coff[0], &clen[0], n, &out[0], out.size(), &ooff[0],
+			                     &olen[0], &cst[0], &cons[0], &unk[0], unk.size(), &nunk);
+		}
 		if (rc == XCG_ENOTSUP) {
 			if (n > 1) {
 				per = n / 2;
@@ -304,7 +317,8 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 				break;
 			}
 		}
-		mirror_extracts(cache_, in, pos, pos + consumed);
+		mirror_extracts(cache_, in, pos, pos + consumed, next == XCG_NO_REFERENCES ? NULL : &ext[0],
+		                next == XCG_NO_REFERENCES ? 0 : next);
 		pos += consumed;
 		if (status == 0 && k1 < piece.size() - 1) {	/* more batches of this call */
 			k0 = k1;

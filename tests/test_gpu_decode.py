@@ -151,3 +151,68 @@ def test_decode_fuzz_byte_splits(oracle, limit):
     ctx.close()
     oracle.decoder_free(odec)
     oracle.cache_free(oc)
+
+
+
+def _extract_hashes(o, buf, end):
+    """XCodecHash of every EXTRACT whose op starts before `end`, in op order."""
+    out, j = [], 0
+    while j < end:
+        if buf[j] != 0xf1 or j + 1 >= len(buf):
+            j += 1
+            continue
+        op = buf[j + 1]
+        if op == 0x01:
+            out.append(o.hash(buf[j + 2:j + 2050]))
+        j += {0x01: 2050, 0x02: 10, 0x03: 3}.get(op, 2)
+    return out
+
+
+def test_decode_call_like_reference(ref_oracle):
+    """xcg_decode_call (one decode() call in one launch and one synchronisation)
+    against the reference decoder, call by call on one persistent decoder and
+    cache: whole frames, frames out of order (unknown REFs: the stop point and
+    decode_skim's set), frames cut inside an op (partial op kept), 0xF1-heavy
+    literals, calls with <BACKREF>s (the batch decoder takes those), and last a
+    bad opcode.  The EXTRACT hashes it returns are the EXTRACTs before the stop."""
+    import random
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    from backref_streams import stream_with_backrefs
+    rng = random.Random(17)
+    d = synth.stream(0xDC11, 3 << 20, 45, 3)
+    offs, lens = synth.chunks_of(d, 65536)
+    enc = ref_oracle.encode_batch(d, offs, lens, mode=1)
+    calls = list(enc[:6]) + [enc[9], enc[7]] + list(enc[6:9])
+    blob = b''.join(enc[10:20])
+    i = 0
+    while i < len(blob):                                   # cuts anywhere, ops split across calls
+        n = rng.choice([1, 2, 9, 700, 2051, 40000, 100000])
+        calls.append(blob[i:i + n])
+        i += n
+    calls += list(enc[21:24])
+    bd = synth.stream(0xB4CC, 1 << 20, 40, 0)
+    calls += stream_with_backrefs(ref_oracle, bd, 65536, 0xB4CC, 0.2, 0)
+    calls += list(enc[24:27])
+    calls.append(enc[27][:5000] + bytes([0xf1, 0x07]) + enc[27][5000:])   # unsupported opcode: decode() is false
+    ctx = Context(0, cache_segments=1 << 16)
+    c = ref_oracle.cache_new()
+    dec = ref_oracle.decoder_new(c)
+    carry = b''
+    nfast = 0
+    for k, x in enumerate(calls):
+        buf = carry + x                                    # (a caller keeps what decode() did not consume)
+        ok, out, cons, unk = ref_oracle.decode(buf, c, decoder=dec)
+        st, gout, gcons, gunk, ext = ctx.decode_call(buf)
+        assert (st >= 0, gout, gcons, gunk) == (ok, out, cons, sorted(unk)), (k, st, len(out), len(gout), cons, gcons)
+        if ext is not None:
+            nfast += 1
+            assert ext == _extract_hashes(ref_oracle, buf, gcons), k
+        carry = buf[cons:] if ok and not unk else b''
+        if not ok:
+            assert k == len(calls) - 1
+            break
+    ref_oracle.decoder_free(dec)
+    ref_oracle.cache_free(c)
+    ctx.close()
+    assert nfast > 10

@@ -1363,6 +1363,99 @@ int xcg_decode_host(xcg_ctx* c, const uint8_t* h_enc, uint64_t enc_len, const ui
   return XCG_OK;
 }
 
+}  // extern "C"
+
+extern "C" int xcg_launch_decode_small(const uint8_t*, uint32_t, uint64_t*, uint64_t*, uint32_t, uint8_t*, uint32_t*,
+                                       uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t, int32_t*, void*,
+                                       uint32_t, uint8_t*, uint64_t, uint64_t*, uint8_t*, uint64_t, uint64_t*,
+                                       hipStream_t);
+extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap);
+extern "C" uint32_t xcg_decode_small_res_words(void);
+
+extern "C" {
+
+int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_out, uint64_t out_cap,
+                    uint64_t* h_out_len, uint64_t* h_consumed, int32_t* h_status, uint64_t* h_unknown,
+                    uint32_t unknown_cap, uint32_t* h_nunknown, uint64_t* h_extract_hash, uint32_t extract_cap,
+                    uint32_t* h_nextract) {
+  if (!c || !h_out_len || !h_consumed || !h_status || !h_nunknown || !h_nextract || (len && !h_in) ||
+      (out_cap && !h_out))
+    return XCG_EINVAL;
+  *h_out_len = *h_consumed = 0;
+  *h_status = 0;
+  *h_nunknown = 0;
+  *h_nextract = XCG_NO_REFERENCES;
+  if (len == 0) return XCG_OK;
+  DeviceGuard g(c->device);
+  const bool fast = !c->bounded && !c->pair && !(c->flags & XCG_FLAG_NULLCACHE) && len <= (1u << 20);
+  if (fast) {
+    int rc = ensure_cache(c);
+    if (rc == XCG_OK && !c->cur_win) {
+      rc = window_alloc(c->device, &c->own_win);
+      c->cur_win = c->own_win;
+    }
+    if (rc != XCG_OK) return rc;
+    const uint32_t ops_cap = len / 4 + 64;
+    const uint32_t rw = xcg_decode_small_res_words();
+    // device: input | output | results | op lists;  host: input | results | output
+    const size_t inb = align256(len), outb = align256(out_cap ? out_cap : 1), resb = align256(8ull * rw + 8);
+    const size_t scr = align256(xcg_decode_small_scratch(ops_cap));
+    rc = ensure_stage(c, inb + outb + resb + scr, inb + resb + outb);
+    if (rc != XCG_OK) return rc;
+    uint8_t* dm = c->stage_d;
+    uint8_t* hm = c->stage_h;
+    uint64_t* d_res = (uint64_t*)(dm + inb + outb);
+    uint64_t* h_res = (uint64_t*)(hm + inb);
+    uint8_t* h_o = hm + inb + resb;
+    const hipStream_t st = c->call_st;
+    memcpy(hm, h_in, len);
+    ctx_order(c, st);
+    xcg_window* w = c->cur_win;
+    if (hipMemcpyAsync(dm, hm, len, hipMemcpyHostToDevice, st) != hipSuccess ||
+        xcg_launch_decode_small(dm, len, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
+                                c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->d_status,
+                                dm + inb + outb + resb, ops_cap, dm + inb, out_cap, w->hash, w->seg, w->count,
+                                d_res, st) != 0 ||
+        hipMemcpyAsync(h_res, d_res, 8ull * rw, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_res + rw, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (out_cap && hipMemcpyAsync(h_o, dm + inb, out_cap, hipMemcpyDeviceToHost, st) != hipSuccess))
+      return XCG_EHIP;
+    ctx_mark(c, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
+    if (*(const int32_t*)(h_res + rw)) return XCG_EOVERFLOW;   // (cache capacity: the sticky word)
+    if (h_res[5] == 2) {
+      *h_out_len = h_res[7];
+      return XCG_EOVERFLOW;
+    }
+    if (h_res[5] == 0) {
+      const uint64_t ol = h_res[0];
+      memcpy(h_out, h_o, ol);
+      *h_out_len = ol;
+      *h_consumed = h_res[1];
+      *h_status = (int32_t)(int64_t)h_res[2];
+      w->count += h_res[3];
+      const uint32_t nu = (uint32_t)h_res[4];
+      std::vector<uint64_t> u(h_res + 8, h_res + 8 + nu);
+      std::sort(u.begin(), u.end());
+      const uint32_t ku = nu < unknown_cap ? nu : unknown_cap;
+      if (h_unknown && ku) memcpy(h_unknown, u.data(), 8ull * ku);
+      *h_nunknown = ku;
+      const uint32_t ne = (uint32_t)h_res[6];
+      if (ne <= extract_cap && ne <= 1024) {
+        if (ne && h_extract_hash) memcpy(h_extract_hash, h_res + 8 + 2048, 8ull * ne);
+        *h_nextract = ne;
+      }
+      return XCG_OK;
+    }
+    // (fallback: the batch decoder takes it; nothing was written)
+  }
+  const uint64_t off = 0;
+  uint64_t ooff = 0;
+  const int rc = xcg_decode_host(c, h_in, len, &off, &len, 1, h_out, out_cap, &ooff, h_out_len, h_status, h_consumed,
+                                 h_unknown, unknown_cap, h_nunknown);
+  return rc;
+}
+
 int xcg_pack_outputs(xcg_ctx* c, const uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,
                      uint32_t n, uint8_t* d_packed, uint64_t* d_packed_off, uint64_t* d_total, void* stream) {
   if (!c || (n && (!d_out || !d_out_off || !d_out_len || !d_packed || !d_packed_off || !d_total))) return XCG_EINVAL;

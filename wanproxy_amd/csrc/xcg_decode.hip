@@ -917,6 +917,324 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* src, const uin
   }
 }
 
+// ---------------------------------------- one decode() call, one workgroup
+//
+// XCodecDecoder::decode (xcodec/xcodec_decoder.cc:66-272) of ONE call's input
+// on an unbounded cache, as the drop-in adapter issues it (tack -d: one call
+// per 64 KiB read, programs/tack/tack.cc:329-359; XCodecPipePair: the buffered
+// frames, xcodec_pipe_pair.cc:425-446) -- the passes of the batch decoder
+// (scan, hash, resolve, emit, window, commit) in one launch, with __syncthreads
+// between them instead of kernel boundaries and host synchronisations.
+// Wave 0 walks the ops and lists them (literal runs, EXTRACT, REF) with their
+// output offsets and declare numbers; all waves hash the EXTRACTs into an LDS
+// table (earliest / latest position), resolve every REF (an earlier EXTRACT
+// of the call, else the cache; else it is unknown -- the first one is the stop
+// point and the rest form decode_skim's set), then copy every op before the
+// stop to its output offset, update the BACKREF window (window_slot over the
+// call's declare records) and commit the EXTRACTs before the stop.  Anything
+// the batch decoder refuses or this pass does not cover -- a BACKREF op, name
+// reuse inside the call, EXTRACTs on both sides of the stop, more than
+// SD_XSLOTS / 2 EXTRACTs or SD_UMAX unknown hashes -- sets `fallback` before
+// anything is written; the host then takes the batch path.
+constexpr uint32_t SD_XSLOTS = 2048, SD_USLOTS = 4096, SD_UMAX = 2048, SD_EMAX = 1024;
+constexpr uint32_t SD_LIT = 0, SD_EXT = 1, SD_REF = 2;
+
+struct SmallDec {
+  const uint8_t* in;
+  uint32_t len;
+  HashTab g;
+  uint8_t* pool;
+  uint32_t* nseg;
+  uint32_t seg_cap;
+  FiltSet fs;
+  int32_t* status;             // the context's sticky word
+  uint4* ops;                  // (type, in_off, out_off, declare number | nesc)
+  uint64_t* opv;               // EXTRACT / REF hash
+  uint4* D;                    // declare records (lo, hi, src lo, src hi)
+  uint32_t ops_cap;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* win_hash;
+  uint8_t* win_seg;
+  uint64_t win_count;
+  uint64_t* res;               // [0] out_len [1] consumed [2] status [3] declares before the stop
+                               // [4] unknowns [5] fallback [6] EXTRACTs before the stop [7] decoded size
+                               // then SD_UMAX unknown hashes, then SD_EMAX EXTRACT hashes (op order)
+};
+
+__global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
+  __shared__ uint64_t xk[SD_XSLOTS], xf[SD_XSLOTS], xl[SD_XSLOTS];
+  __shared__ uint64_t uk[SD_USLOTS];
+  __shared__ uint32_t s_nops, s_ndecl, s_next, s_nunk, s_fb, s_walk_st, s_walk_end;
+  __shared__ uint64_t s_stop;  // (position << 32) | declare number of the first unknown REF
+  __shared__ uint64_t s_olen;
+  const uint32_t t = threadIdx.x, w = t >> 6;
+  const int l = lane_id();
+  const uint8_t* x = a.in;
+  const uint32_t len = a.len;
+  for (uint32_t i = t; i < SD_XSLOTS; i += 1024) { xk[i] = EMPTY_KEY; xf[i] = ~0ull; xl[i] = 0; }
+  for (uint32_t i = t; i < SD_USLOTS; i += 1024) uk[i] = EMPTY_KEY;
+  if (t == 0) { s_nunk = 0; s_fb = 0; s_stop = ~0ull; s_next = 0; }
+  // ---- walk (wave 0): op list, output offsets, declare numbers
+  if (w == 0) {
+    uint32_t i = 0, k = 0, dn = 0, st = 0, fb = 0;
+    uint64_t olen = 0;
+    while (i < len) {
+      uint32_t nesc = 0;
+      const uint32_t m = next_op(x, i, len, nesc);
+      if (m > i) {                                           // literal run (:71-81, ESCAPE :91-94)
+        if (k >= a.ops_cap) { fb = 1; break; }
+        if (l == 0) a.ops[k] = make_uint4(SD_LIT, i, (uint32_t)olen, m - i);
+        ++k;
+        olen += (m - i) - nesc;
+      }
+      i = m;
+      if (i >= len) break;
+      if (len - i == 1) { st = 3; break; }
+      const uint32_t op = x[i + 1];
+      if (op == OP_EXTRACT) {
+        if (len - i < 2u + SEG) { st = 3; break; }
+        if (k >= a.ops_cap) { fb = 1; break; }
+        if (l == 0) a.ops[k] = make_uint4(SD_EXT, i, (uint32_t)olen, dn);
+        ++k; ++dn;
+        olen += SEG;
+        i += 2 + SEG;
+      } else if (op == OP_REF) {
+        if (len - i < 10u) { st = 3; break; }
+        uint64_t h, here;
+        const uint32_t r = ref_run(x, i, len, 0, ~0ull, h, here);
+        if (k + r > a.ops_cap) { fb = 1; break; }
+        if ((uint32_t)l < r) {
+          a.ops[k + l] = make_uint4(SD_REF, i + 10u * l, (uint32_t)(olen + (uint64_t)SEG * l), dn + l);
+          a.opv[k + l] = h;
+        }
+        k += r; dn += r;
+        olen += (uint64_t)SEG * r;
+        i += 10u * r;
+      } else if (op == OP_BACKREF) {
+        fb = 1;                                              // (the batch path models the window's BACKREFs)
+        break;
+      } else {
+        st = (uint32_t)-1;                                   // :183-184 unsupported opcode
+        break;
+      }
+    }
+    if (olen >= (1ull << 32)) fb = 1;
+    if (l == 0) {
+      s_nops = k; s_ndecl = dn; s_walk_st = st; s_walk_end = i; s_olen = olen;
+      if (fb) s_fb = 1;
+    }
+  }
+  __syncthreads();
+  const uint32_t nops = s_nops;
+  if (s_fb) {
+    if (t == 0) a.res[5] = 1;
+    return;
+  }
+  // ---- EXTRACT hashes (a wave per EXTRACT) into the LDS table
+  for (uint32_t k = w; k < nops; k += 16) {
+    const uint4 o = a.ops[k];
+    if (readfirst(o.x) != SD_EXT) continue;
+    const uint32_t pos = readfirst(o.y) + 2u;
+    const uint2 h = dec_window_hash(x + pos);
+    const uint64_t key = ((uint64_t)readfirst(h.y) << 32) | readfirst(h.x);
+    if (l == 0) {
+      a.opv[k] = key;
+      uint32_t i = mix32((uint32_t)key, (uint32_t)(key >> 32)) & (SD_XSLOTS - 1);
+      for (uint32_t n = 0; n < SD_XSLOTS; ++n) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&xk[i], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+        if (prev == EMPTY_KEY || prev == key) {
+          atomicMin((unsigned long long*)&xf[i], (unsigned long long)pos);
+          atomicMax((unsigned long long*)&xl[i], (unsigned long long)pos);
+          break;
+        }
+        i = (i + 1) & (SD_XSLOTS - 1);
+      }
+      atomicAdd(&s_next, 1u);
+    }
+  }
+  __syncthreads();
+  if (s_next > SD_XSLOTS / 2) {
+    if (t == 0) a.res[5] = 1;
+    return;
+  }
+  // ---- resolve every REF (a thread per op): an earlier EXTRACT of the call,
+  // else the cache; else unknown (:151-156; decode_skim's set, :196-272)
+  for (uint32_t k = t; k < nops; k += 1024) {
+    const uint4 o = a.ops[k];
+    uint64_t src = 0, key = 0;
+    if (o.x == SD_EXT) {
+      key = a.opv[k];
+      src = (uint64_t)(x + o.y + 2);
+    } else if (o.x == SD_REF) {
+      key = a.opv[k];
+      const uint64_t here = o.y;
+      uint32_t i = mix32((uint32_t)key, (uint32_t)(key >> 32)) & (SD_XSLOTS - 1);
+      uint64_t e = ~0ull;
+      for (uint32_t n = 0; n < SD_XSLOTS; ++n) {
+        const uint64_t kk = xk[i];
+        if (kk == key) { e = xf[i]; break; }
+        if (kk == EMPTY_KEY) break;
+        i = (i + 1) & (SD_XSLOTS - 1);
+      }
+      if (e != ~0ull && e < here) {
+        src = (uint64_t)(x + e);
+      } else {
+        const uint64_t gv = tab_lookup_t(a.g, (uint32_t)key, (uint32_t)(key >> 32));
+        if (gv != ~0ull) {
+          src = (uint64_t)(a.pool + gv * (uint64_t)SEG);
+        } else {
+          atomicMin((unsigned long long*)&s_stop, (unsigned long long)((here << 32) | o.w));
+          uint32_t j = mix32((uint32_t)key, (uint32_t)(key >> 32)) & (SD_USLOTS - 1);
+          for (uint32_t n = 0; n < SD_USLOTS; ++n) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&uk[j], (unsigned long long)EMPTY_KEY,
+                                            (unsigned long long)key);
+            if (prev == EMPTY_KEY) {
+              const uint32_t u = atomicAdd(&s_nunk, 1u);
+              if (u < SD_UMAX) a.res[8 + u] = key;
+              break;
+            }
+            if (prev == key) break;
+            j = (j + 1) & (SD_USLOTS - 1);
+          }
+        }
+      }
+    }
+    if (o.x != SD_LIT) a.D[o.w] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)src, (uint32_t)(src >> 32));
+  }
+  __syncthreads();
+  const uint64_t stop = s_stop;
+  const uint32_t stop_pos = stop == ~0ull ? ~0u : (uint32_t)(stop >> 32);
+  const uint32_t T = stop == ~0ull ? s_ndecl : (uint32_t)stop;   // declares before the stop
+  if (s_nunk > SD_UMAX) {
+    if (t == 0) a.res[5] = 1;
+    return;
+  }
+  // ---- what the batch decoder refuses (dec_precheck_kernel): several EXTRACTs
+  // of one hash before the stop with other bytes, or on both sides of it
+  for (uint32_t i = w; i < SD_XSLOTS; i += 16) {
+    if (xk[i] == EMPTY_KEY) continue;
+    const uint64_t f = xf[i], z = xl[i];
+    if (f >= stop_pos || z == f) continue;
+    bool bad = z >= stop_pos;
+    if (!bad) bad = !dec_equal2048(x + f, x + z);
+    if (bad && l == 0) atomicOr(&s_fb, 1u);
+  }
+  __syncthreads();
+  if (s_fb) {
+    if (t == 0) a.res[5] = 1;
+    return;
+  }
+  // ---- output: every op before the stop at its offset (a wave per op); the
+  // output ends at the stop REF's offset
+  if (stop != ~0ull)
+    for (uint32_t k = t; k < nops; k += 1024) {
+      const uint4 o = a.ops[k];
+      if (o.x == SD_REF && o.y == stop_pos) s_olen = o.z;
+    }
+  __syncthreads();
+  const uint64_t out_len = s_olen;
+  if (out_len > a.out_cap) {
+    if (t == 0) { a.res[5] = 2; a.res[7] = out_len; }      // (more room needed; nothing written)
+    return;
+  }
+  for (uint32_t k = w; k < nops; k += 16) {
+    const uint4 o = a.ops[k];
+    const uint32_t ty = readfirst(o.x), io = readfirst(o.y), oo = readfirst(o.z);
+    if (io >= stop_pos) continue;
+    if (ty == SD_LIT) {
+      (void)wave_unescape(a.out + oo, x, io, io + readfirst(o.w));
+    } else {
+      const uint4 d = a.D[readfirst(o.w)];
+      const uint8_t* src = (const uint8_t*)(((uint64_t)readfirst(d.w) << 32) | readfirst(d.z));
+      wave_copy2048(a.out + oo, src);
+    }
+  }
+  // ---- the BACKREF window after the call's declares (before the commit
+  // overwrites any pool bytes a REF's declare reads)
+  {
+    DecParams prm{};
+    prm.D = a.D;
+    prm.D_lo = 0;
+    prm.D_tail = false;
+    prm.win_hash = a.win_hash;
+    prm.win_seg = a.win_seg;
+    prm.win_count = a.win_count;
+    const uint64_t G = a.win_count + T;
+    for (uint32_t c = w; c < 256u && T > 0; c += 16) {
+      uint64_t h = 0, gd = 0;
+      const uint8_t* src = nullptr;
+      const bool ok = window_slot(prm, T, c, h, src, gd);
+      if (((G - 1u - c) & 255u) > G - 1u) continue;          // never written
+      if (!ok) {
+        if (l == 0) a.win_hash[c] = 0;
+        continue;
+      }
+      if (gd >= a.win_count) wave_copy2048(a.win_seg + (uint64_t)c * SEG, src);
+      if (l == 0) a.win_hash[c] = h;
+    }
+  }
+  __syncthreads();
+  // ---- commit: EXTRACTs before the stop enter the cache, or replace a cached
+  // segment's bytes (name reuse, :106-136)
+  for (uint32_t i = w; i < SD_XSLOTS; i += 16) {
+    const uint64_t key = xk[i];
+    if (key == EMPTY_KEY) continue;
+    const uint64_t f = xf[i];
+    if (f >= stop_pos) continue;
+    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+    const uint64_t gv = tab_lookup(a.g, lo, hi);
+    const uint8_t* src = x + f;
+    if (gv != ~0ull) {
+      uint8_t* dst = a.pool + gv * (uint64_t)SEG;
+      if (!dec_equal2048(dst, src)) wave_copy2048(dst, src);
+      continue;
+    }
+    uint32_t sg = 0;
+    if (l == 0) sg = atomicAdd(a.nseg, 1u);
+    sg = readfirst(sg);
+    if (sg >= a.seg_cap) {
+      if (l == 0) atomicOr(a.status, 4);
+      continue;
+    }
+    wave_copy2048(a.pool + (uint64_t)sg * SEG, src);
+    if (l == 0) {
+      if (!tab_insert_min(a.g, lo, hi, sg)) atomicOr(a.status, 2);
+      filt_insert(a.fs, lo, hi);
+    }
+  }
+  // ---- results: the EXTRACTs before the stop in op order (the host cache's
+  // mirror enters them without hashing again)
+  if (w == 0) {
+    uint32_t ne = 0;
+    for (uint32_t k0 = 0; k0 < nops; k0 += 64) {
+      const uint32_t k = k0 + (uint32_t)l;
+      bool is = false;
+      uint64_t key = 0;
+      if (k < nops) {
+        const uint4 o = a.ops[k];
+        is = o.x == SD_EXT && o.y < stop_pos;
+        if (is) key = a.opv[k];
+      }
+      const uint64_t m = ballot(is);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (is && ne + below < SD_EMAX) a.res[8 + SD_UMAX + ne + below] = key;
+      ne += (uint32_t)__builtin_popcountll(m);
+    }
+    if (l == 0) {
+      const int32_t wst = (int32_t)s_walk_st;
+      a.res[0] = out_len;
+      a.res[1] = stop != ~0ull ? stop_pos : s_walk_end;
+      a.res[2] = (uint64_t)(int64_t)(stop != ~0ull ? 1 : wst);
+      a.res[3] = T;
+      a.res[4] = s_nunk;
+      a.res[5] = 0;
+      a.res[6] = ne;
+      a.res[7] = out_len;
+    }
+  }
+}
+
 // Host-driven cache access (one wave): look a hash up and copy its segment
 // out, or enter a segment under a hash (XCodecCache::lookup / enter /
 // replace, xcodec/xcodec_cache.h:83-89).
@@ -1267,3 +1585,37 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+// One decode() call on an unbounded cache in one launch (decode_small_kernel).
+extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t* g_keys, uint64_t* g_vals,
+                                       uint32_t g_mask, uint8_t* pool, uint32_t* nseg, uint32_t seg_cap,
+                                       uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint32_t* gfilt, uint32_t gmask,
+                                       int32_t* status, void* scratch, uint32_t ops_cap, uint8_t* out, uint64_t out_cap,
+                                       uint64_t* win_hash, uint8_t* win_seg, uint64_t win_count, uint64_t* res,
+                                       hipStream_t stream) {
+  using namespace xcg;
+  SmallDec a;
+  a.in = in;
+  a.len = len;
+  a.g = HashTab{g_keys, g_vals, g_mask};
+  a.pool = pool;
+  a.nseg = nseg;
+  a.seg_cap = seg_cap;
+  a.fs = FiltSet{filt, ftab, fmask, gfilt, gmask};
+  a.status = status;
+  a.ops = (uint4*)scratch;
+  a.opv = (uint64_t*)(a.ops + ops_cap);
+  a.D = (uint4*)(a.opv + ops_cap);
+  a.ops_cap = ops_cap;
+  a.out = out;
+  a.out_cap = out_cap;
+  a.win_hash = win_hash;
+  a.win_seg = win_seg;
+  a.win_count = win_count;
+  a.res = res;
+  hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(1024), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap) { return 40ull * ops_cap; }
+extern "C" uint32_t xcg_decode_small_res_words(void) { return 8 + xcg::SD_UMAX + xcg::SD_EMAX; }

@@ -107,6 +107,9 @@ def lib():
     L.xcg_window_destroy.restype = None
     L.xcg_decode_set_window.argtypes = [vp, vp]
     L.xcg_decode_set_window.restype = C.c_int
+    L.xcg_decode_call.argtypes = [vp, C.c_char_p, C.c_uint32, vp, C.c_uint64, vp, vp, vp, vp, C.c_uint32, vp, vp,
+                                  C.c_uint32, vp]
+    L.xcg_decode_call.restype = C.c_int
     L.xcg_pack_outputs.argtypes = [vp, u8p, u64p, u64p, C.c_uint32, u8p, u64p, u64p, vp]
     L.xcg_pack_outputs.restype = C.c_int
     L.xcg_window_hashes.argtypes = [vp, u8p, C.c_uint64, u64p, vp]
@@ -363,6 +366,25 @@ class Context:
         out = d_out.cpu().numpy()
         outs = [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] != 2 else b'' for i in range(n)]
         return outs, st, cons, [int(u) for u in unk[:int(nunk[0])]]
+
+    def decode_call(self, data: bytes, out_cap: int = None):
+        """One XCodecDecoder::decode(output, input, unknown) call from host memory
+        (xcg_decode_call: one launch, one synchronisation on an unbounded cache).
+        Returns (status, out, consumed, unknown, extract_hashes or None)."""
+        n = len(data)
+        if out_cap is None:
+            out_cap = (n // 10 + 1) * 2048 + n
+        out = np.zeros(max(1, out_cap), np.uint8)
+        ol, cons = np.zeros(1, np.uint64), np.zeros(1, np.uint64)
+        st = np.zeros(1, np.int32)
+        unk = np.zeros(1 << 16, np.uint64)
+        nunk, ne = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        ext = np.zeros(1024, np.uint64)
+        _check(lib().xcg_decode_call(self.h, data, n, out.ctypes.data, out_cap, ol.ctypes.data, cons.ctypes.data,
+                                     st.ctypes.data, unk.ctypes.data, unk.size, nunk.ctypes.data, ext.ctypes.data,
+                                     ext.size, ne.ctypes.data))
+        hashes = None if int(ne[0]) == 0xFFFFFFFF else [int(h) for h in ext[:int(ne[0])]]
+        return (int(st[0]), out[:int(ol[0])].tobytes(), int(cons[0]), [int(u) for u in unk[:int(nunk[0])]], hashes)
 
     def window_hashes(self, data) -> np.ndarray:
         import torch
