@@ -13,9 +13,11 @@ figure all 4096 too).
 Multi-GPU (torchrun, one rank per GPU): every rank encodes its own 4096-chunk
 shard (seed 0xC2 + rank) with no collective in the timed loop -> weak scaling.
 With N > 1 the line also carries `sharded_configs`: BASELINE configs C4 (1 M x
-4 KiB packets) and C5 (8 GiB in 128 KiB calls), ONE stream each cut into
-contiguous per-rank ranges (wanproxy_amd/shard.py config_shard), each rank with
-a private cache, checked per shard against the oracle run on that shard alone.
+4 KiB packets, a private unbounded cache per rank) and C5 (8 GiB in 128 KiB
+calls, "cold cache with xcodec_cache_disk spill": a private XCodecCachePair of
+wanproxy.conf's 128 MiB memory cache over a 1 GiB disk per rank), ONE stream
+each cut into contiguous per-rank ranges (wanproxy_amd/shard.py config_shard),
+every chunk of every shard checked against the oracle run on that shard alone.
 
 rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
 """
@@ -496,12 +498,15 @@ def other_configs():
     # C5-PAIR: C5 on wanproxy.conf's whole cache, the 128 MiB memory cache over
     # a 1 GiB disk (XCodecCachePair), every chunk checked against the oracle's pair
     a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, lru_mib=128, lru_check=1.0,
-                           disk_mib=1024, no_decode=False)
+                           disk_mib=1024, no_decode=False, disk_laps=0)
+    # C5-PAIR-LAPS: the same with a disk the shard laps ~3 times (FIFO eviction
+    # and re-entry inside the measured figure)
+    lap = argparse.Namespace(**{**vars(a), 'disk_laps': 3})
     out = {}
-    for name, fn in (('C3', cb.run_c3), ('C4', cb.run_c4), ('C5', cb.run_c5), ('C5-LRU', cb.run_c5lru),
-                     ('C5-PAIR', cb.run_c5pair)):
+    for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, a),
+                         ('C5-PAIR', cb.run_c5pair, a), ('C5-PAIR-LAPS', cb.run_c5pair, lap)):
         try:
-            out[name] = fn(a)
+            out[name] = fn(ar)
         except BaseException as e:          # SystemExit from a parity check included
             out[name] = {'error': f'{type(e).__name__}: {e}'}
     return out
@@ -535,8 +540,9 @@ def sharded_configs(world, rank, dev, backend='nccl'):
     packets, C5 8 GiB/N), every rank encoding its range with a private cache
     (wanproxy's one encoder + cache per codec,
     programs/wanproxy/wanproxy_config_class_codec.cc:39-80).  Timed between
-    barriers, max wall over ranks; each rank checks a prefix of its range
-    against the oracle run on that range alone and decodes all of it back.
+    barriers, max wall over ranks; each rank checks all of its range against
+    the oracle run on that range alone (C5: with the same pair) and decodes
+    all of it back.
     Returns aggregate GiB/s (strong scaling: the dataset is fixed)."""
     import importlib.util
     import torch
@@ -553,9 +559,11 @@ def sharded_configs(world, rank, dev, backend='nccl'):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
     a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, world=world, rank=rank, reduce=reduce,
-                           no_decode=False, check_c4=16384, check_c5=512)
+                           no_decode=False, lru_mib=128, disk_mib=1024, lru_check=1.0, disk_laps=0)
     out = {}
-    for name, fn in (('C4', cb.run_c4), ('C5', cb.run_c5)):
+    # C5 as BASELINE.json configs[4] words it: "cold cache with xcodec_cache_disk
+    # spill" -- every rank's cache is wanproxy.conf's pair (shard.C5_PAIR)
+    for name, fn in (('C4', cb.run_c4), ('C5', cb.run_c5pair)):
         err = ''
         try:
             r = fn(a)
@@ -572,7 +580,7 @@ def sharded_configs(world, rank, dev, backend='nccl'):
         wall = r['encode_wall_s']           # already the max over ranks (reduce)
         out[name] = {'value': round(tot / 2**30 / wall, 2), 'unit': 'GiB/s', 'scaling': 'strong',
                      'dataset_bytes': int(tot), 'ms': round(wall * 1e3, 2), 'ranks': world,
-                     'rank0': {k: r[k] for k in ('config', 'shard', 'out_in', 'decode_GiBps', 'checked')}}
+                     'rank0': {k: r[k] for k in ('config', 'shard', 'out_in', 'checked', 'kernel') if k in r}}
     return out
 
 

@@ -130,14 +130,38 @@ def decode_device(ctx, encs, per: int, chunk: int, rehearse: bool = True):
     return d_dout[:o].cpu().numpy().tobytes(), secs
 
 
-def check_prefix(data, offs, lens, got, k, what):
+def check_prefix(data, offs, lens, got, k, what, cache=None):
+    """The first k chunks (None: all) equal the oracle's sequential encoder
+    (from an empty cache, or `cache`)."""
     from oracle.lib import Oracle
-    k = min(k, len(got))
-    exp = Oracle().encode_batch(data, offs[:k], lens[:k], mode=1)
+    k = len(got) if k is None else min(k, len(got))
+    exp = Oracle().encode_batch(data, offs[:k], lens[:k], mode=1, cache=cache)
     if got[:k] != exp:
         bad = next(i for i in range(k) if got[i] != exp[i])
         raise SystemExit(f'PARITY FAILURE ({what}) at chunk {bad}')
     return k
+
+
+def checked(k, n, unit='chunks'):
+    return f'all {n} {unit}' if k == n else f'first {k} of {n} {unit}'
+
+
+class KernelClock:
+    """Stream-parse kernel time (HIP events on its launch stream,
+    xcg_debug_stream_kernel_timing) over a region: tells a change in the
+    kernel from one in the host side around it."""
+
+    def __enter__(self):
+        from wanproxy_amd.xcgpu import lib, stream_kernel_time
+        self.prev = lib().xcg_debug_stream_kernel_timing(1)
+        stream_kernel_time()                      # (reset)
+        return self
+
+    def __exit__(self, *exc):
+        from wanproxy_amd.xcgpu import lib, stream_kernel_time
+        self.ms, self.launches = stream_kernel_time()
+        lib().xcg_debug_stream_kernel_timing(self.prev)
+        return False
 
 
 def torch_dev(args) -> int:
@@ -145,21 +169,29 @@ def torch_dev(args) -> int:
     return torch.cuda.current_device()
 
 
-def timed_encode(B: 'Batches', reps: int, clear_ctx=True, reduce=None):
+def timed_encode(B: 'Batches', reps: int, clear_ctx=True, reduce=None, clock=None):
     """Best of `reps` cold-cache encodes of the whole shard.  reduce: the
-    multi-GPU run's max-over-ranks (a barrier precedes every rep)."""
+    multi-GPU run's max-over-ranks (a barrier precedes every rep).  clock
+    (a dict): the last rep's stream-kernel ms and launches go there."""
     import torch
     walls = []
-    for _ in range(reps):
+    for r in range(reps):
         if clear_ctx:
             B.ctx.cache_clear()
         torch.cuda.synchronize(B.dev)
         if reduce is not None:
             reduce(None)
+        kc = KernelClock() if clock is not None and r == reps - 1 else None
+        if kc:
+            kc.__enter__()
         t0 = time.perf_counter()
         B.encode_all()
         torch.cuda.synchronize(B.dev)
         w = time.perf_counter() - t0
+        if kc:
+            kc.__exit__(None, None, None)
+            clock.update(stream_kernel_ms=round(kc.ms, 3), stream_kernel_launches=kc.launches,
+                         last_rep_wall_ms=round(w * 1e3, 3))
         walls.append(reduce(w) if reduce is not None else w)
     B.ctx.status()
     return min(walls)
@@ -173,9 +205,10 @@ def run_c2s(args):
     offs, lens = synth.chunks_of(data.tobytes(), 64 * KiB)
     ctx = Context(0, cache_segments=1 << 18)
     B = Batches(ctx, data, offs, lens, per=n)
-    wall = timed_encode(B, args.reps)
+    clock = {}
+    wall = timed_encode(B, args.reps, clock=clock)
     got = B.outputs()
-    k = check_prefix(data, offs, lens, got, 256, 'c2s')
+    k = check_prefix(data, offs, lens, got, None, 'c2s')
     dec, dsec = data.tobytes(), float('nan')
     if not args.no_decode:
         dctx = Context(0, cache_segments=1 << 18)
@@ -186,7 +219,8 @@ def run_c2s(args):
     return {'config': 'C2-S2: %d x 64 KiB, dup 50, one cache, chunk order' % n,
             'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 3),
             'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
-            'rounds': B.rounds, 'checked': f'first {k} chunks vs oracle; full decode round trip'}
+            'rounds': B.rounds, 'kernel': clock,
+            'checked': f'{checked(k, len(got))} vs the oracle; full decode round trip'}
 
 
 def run_c3(args):
@@ -213,16 +247,24 @@ def run_c3(args):
     B = Batches(ctx, data, offs, lens, per=per)
     B.encode_all()                                   # warm-up (untimed)
     warm = B.outputs()
-    k = check_prefix(data, offs, lens, warm, 128, 'c3 warm-up')
     warm_rounds = B.rounds
     import torch
     torch.cuda.synchronize(B.dev)
-    t0 = time.perf_counter()
-    B.encode_all()                                   # timed: against the warm cache
-    torch.cuda.synchronize(B.dev)
-    wall = time.perf_counter() - t0
+    with KernelClock() as kc:
+        t0 = time.perf_counter()
+        B.encode_all()                               # timed: against the warm cache
+        torch.cuda.synchronize(B.dev)
+        wall = time.perf_counter() - t0
     ctx.status()
     hot = B.outputs()
+    # both passes against the oracle's sequential encoder on ONE cache: the
+    # warm-up from empty, the timed re-encode against what the warm-up entered
+    from oracle.lib import Oracle
+    o = Oracle()
+    oc = o.cache_new()
+    k = check_prefix(data, offs, lens, warm, None, 'c3 warm-up', cache=oc)
+    k2 = check_prefix(data, offs, lens, hot, None, 'c3 timed re-encode', cache=oc)
+    o.cache_free(oc)
     dctx = Context(0, cache_segments=segs)
     dec0, _ = decode_device(dctx, warm, per=per, chunk=64 * KiB, rehearse=False)     # warms the decoder cache
     if dec0 != data.tobytes():
@@ -235,7 +277,9 @@ def run_c3(args):
             'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
             'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
             'warm_rounds': warm_rounds, 'rounds': B.rounds, 'batch_chunks': per,
-            'checked': f'warm-up first {k} chunks vs oracle; both passes decoded back to the input'}
+            'kernel': {'stream_kernel_ms': round(kc.ms, 3), 'stream_kernel_launches': kc.launches},
+            'checked': f'warm-up and timed re-encode: {checked(k2, len(hot))} each vs the oracle on one cache; '
+                       'both passes decoded back to the input'}
 
 
 def _shard(name, args):
@@ -256,9 +300,10 @@ def run_c4(args):
     dev = torch_dev(args)
     ctx = Context(dev, cache_segments=int(n * 2 * 1.05) + 4096)
     B = Batches(ctx, data, offs, lens, per=args.c4_batch)
-    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None))
+    clock = {}
+    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None), clock=clock)
     got = B.outputs()
-    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c4', 2048), 'c4')
+    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c4', None), 'c4')
     dec, dsec = data.tobytes(), float('nan')
     if not args.no_decode:
         dctx = Context(dev, cache_segments=int(n * 2 * 1.05) + 4096)
@@ -271,7 +316,8 @@ def run_c4(args):
          'batch_chunks': args.c4_batch, 'in_bytes': inb, 'encode_wall_s': wall,
          'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
          'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
-         'rounds': B.rounds[:8], 'checked': f'first {k} packets of the shard vs oracle; full decode round trip'}
+         'rounds': B.rounds[:8], 'kernel': clock,
+         'checked': f'{checked(k, len(got), "packets")} of the shard vs the oracle; full decode round trip'}
     ctx.close()
     return r
 
@@ -285,9 +331,10 @@ def run_c5(args):
     ctx = Context(dev, cache_segments=segs)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
     B = Batches(ctx, data, offs, lens, per=per)
-    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None))
+    clock = {}
+    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None), clock=clock)
     got = B.outputs()
-    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c5', 512), 'c5')
+    k = check_prefix(data, offs, lens, got, getattr(args, 'check_c5', None), 'c5')
     dec, dsec = data.tobytes(), float('nan')
     if not args.no_decode:
         dctx = Context(dev, cache_segments=segs)
@@ -300,7 +347,8 @@ def run_c5(args):
          'shard': _shard_desc(args, rng), 'in_bytes': inb, 'encode_wall_s': wall,
          'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
          'decode_GiBps': round(inb / 2**30 / dsec, 2), 'out_in': round(B.out_bytes() / inb, 5),
-         'rounds': B.rounds, 'checked': f'first {k} chunks of the shard vs oracle; full decode round trip'}
+         'rounds': B.rounds, 'kernel': clock,
+         'checked': f'{checked(k, len(got))} of the shard vs the oracle; full decode round trip'}
     ctx.close()
     return r
 
@@ -313,10 +361,11 @@ def run_c5lru(args):
     data, offs, lens, rng = _shard('C5', args)
     nbytes = data.size
     limit = args.lru_mib * MiB
-    ctx = Context(0, memory_cache_limit=limit)
+    ctx = Context(torch_dev(args), memory_cache_limit=limit)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
     B = Batches(ctx, data, offs, lens, per=per)
-    wall = timed_encode(B, args.reps)
+    clock = {}
+    wall = timed_encode(B, args.reps, clock=clock)
     got = B.outputs()
     k = min(len(got), max(64, int(args.lru_check * len(got))))
     o = Oracle()
@@ -336,25 +385,32 @@ def run_c5lru(args):
     return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, bounded %d MiB LRU cache' % (nbytes >> 20,
                                                                                                  args.lru_mib),
             'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
-            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds,
-            'checked': f'first {k} chunks vs the oracle with the same bounded cache; decoded back (unbounded decoder)'}
+            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds, 'kernel': clock,
+            'checked': f'{checked(k, len(got))} vs the oracle with the same bounded cache; '
+                       'decoded back (unbounded decoder)'}
 
 
 def run_c5pair(args):
     """C5 with wanproxy.conf's whole cache: XCodecCachePair of a bounded
     --lru-mib memory primary and a --disk-mib disk secondary
     (programs/wanproxy/wanproxy.conf:8-26; xcodec/xcodec_cache.h:140-237,
-    xcodec/xcodec_cache_disk.cc), every chunk checked against the oracle's pair."""
+    xcodec/xcodec_cache_disk.cc), every chunk checked against the oracle's
+    pair.  On N > 1 every rank runs its own pair over its shard (bench.py
+    sharded_configs; wanproxy_amd/shard.py C5_PAIR).  --disk-laps: a smaller
+    disk (the data laps it that many times), so FIFO eviction is in the figure."""
     from oracle.lib import Oracle
     from wanproxy_amd.xcgpu import Context
     data, offs, lens, rng = _shard('C5', args)
     nbytes = data.size
     limit = max(2048, int(args.lru_mib * MiB * min(1.0, args.scale * 8)))
     disk = max(1 << 20, int(args.disk_mib * MiB * min(1.0, args.scale * 8)))
-    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    if getattr(args, 'disk_laps', 0):
+        disk = max(1 << 20, int(nbytes * (1 - getattr(args, 'dup_hint', 0.2)) / args.disk_laps))
+    ctx = Context(torch_dev(args), memory_cache_limit=limit, disk_bytes=disk)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
     B = Batches(ctx, data, offs, lens, per=per)
-    wall = timed_encode(B, args.reps)
+    clock = {}
+    wall = timed_encode(B, args.reps, reduce=getattr(args, 'reduce', None), clock=clock)
     got = B.outputs()
     st = ctx.pair_stats()
     k = min(len(got), max(64, int(args.lru_check * len(got))))
@@ -370,18 +426,22 @@ def run_c5pair(args):
         raise SystemExit(f'PARITY FAILURE (c5pair disk counters {st} vs {ost})')
     dec = data.tobytes()
     if not args.no_decode:
-        dctx = Context(0, cache_segments=nbytes // 2048 + 4096)
+        dctx = Context(torch_dev(args), cache_segments=nbytes // 2048 + 4096)
         dec, _ = decode_device(dctx, got, per=per, chunk=128 * KiB)
+        dctx.close()
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c5pair)')
+    ctx.close()
     inb = data.size
+    d_entries = (disk // 2048 - 18) // 205 * 204
     return {'config': 'C5 shard: %d MiB in 128 KiB chunks, dup 20, XCodecCachePair(%d MiB LRU memory, %d MiB disk)'
                       % (nbytes >> 20, limit >> 20, disk >> 20),
+            'shard': _shard_desc(args, rng), 'in_bytes': inb, 'encode_wall_s': wall,
             'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
-            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds,
+            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds, 'kernel': clock,
             'pair_stats': {'primary_entries': st[0], 'disk_entries': st[1], 'disk_written': st[2],
-                           'disk_index_blocks': st[3]},
-            'checked': f'first {k} chunks (and the disk counters) vs the oracle with the same pair; '
+                           'disk_index_blocks': st[3], 'disk_laps': round(st[2] / max(1, d_entries), 2)},
+            'checked': f'{checked(k, len(got))} and the disk counters vs the oracle with the same pair; '
                        'decoded back (unbounded decoder)'}
 
 
@@ -395,6 +455,7 @@ def main():
     ap.add_argument('--lru-mib', type=int, default=128)
     ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
+    ap.add_argument('--disk-laps', type=float, default=0, help='c5pair: size the disk so the data laps it')
     ap.add_argument('--no-decode', action='store_true', help='skip the decode round trips (profiling runs)')
     args = ap.parse_args()
     import torch

@@ -47,6 +47,15 @@ def _worker(rank, world, port, q):
         dist.barrier()
         wall, nbytes = reduce_run(0.1 * (rank + 1), int(lens.astype(np.int64).sum()))
         res[name] = (lo, hi, d.tobytes(), [len(o) for o in out], wall, nbytes)
+    # C5 "with xcodec_cache_disk spill": the same C5 shard on a private pair of
+    # wanproxy.conf's geometry, scaled (bench.py sharded_configs -> run_c5pair)
+    from wanproxy_amd.shard import pair_geometry
+    d, offs, lens, _ = shard_data('C5', world, rank, 8 / 65536)
+    o = Oracle()
+    c = o.cache_new_pair(*pair_geometry(8 / 65536))
+    out = o.encode_batch(d, offs, lens, mode=1, cache=c)
+    res['C5-PAIR'] = ([len(x) for x in out], o.pair_stats(c))
+    o.cache_free(c)
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -76,3 +85,15 @@ def test_two_rank_gloo_shards():
         offs, lens = synth.chunks_of(full, unit)
         exp1 = Oracle().encode_batch(full, offs[units // 2:], lens[units // 2:], mode=1)
         assert l1 == [len(e) for e in exp1]
+    # C5-PAIR: each rank's shard from an empty pair of the scaled geometry
+    from wanproxy_amd.shard import pair_geometry
+    full = synth.stream(0xC5, 8 * (128 << 10), 20, 0)
+    offs, lens = synth.chunks_of(full, 128 << 10)
+    o = Oracle()
+    for r, sl in ((0, slice(0, 4)), (1, slice(4, 8))):
+        c = o.cache_new_pair(*pair_geometry(8 / 65536))
+        part = full[int(offs[sl][0]):int(offs[sl][-1] + lens[sl][-1])]
+        po, pl = synth.chunks_of(part, 128 << 10)
+        exp = o.encode_batch(part, po, pl, mode=1, cache=c)
+        assert res[r]['C5-PAIR'] == ([len(e) for e in exp], o.pair_stats(c))
+        o.cache_free(c)

@@ -30,6 +30,19 @@ DATASETS = {
 }
 
 
+# C5 "with xcodec_cache_disk spill" (BASELINE.json configs[4]): every rank's
+# codec cache is wanproxy.conf's pair, a 128 MiB memory cache over a 1 GiB disk
+# (programs/wanproxy/wanproxy.conf:8-26) -- one XCodecCachePair per shard.
+C5_PAIR = {'memory_limit': 128 << 20, 'disk_bytes': 1 << 30}
+
+
+def pair_geometry(scale: float = 1.0):
+    """(memory limit bytes, disk bytes) of a C5-PAIR shard's cache, scaled with
+    the data (--scale runs keep the cache-to-data ratio)."""
+    f = min(1.0, scale * 8)
+    return (max(2048, int(C5_PAIR['memory_limit'] * f)), max(1 << 20, int(C5_PAIR['disk_bytes'] * f)))
+
+
 def config_shard(name: str, world: int, rank: int, scale: float = 1.0):
     """Rank `rank`'s share of dataset `name` split over `world` ranks:
     (seed, dup, unit bytes, first byte, end byte) of the one stream.  bench.py
