@@ -534,7 +534,7 @@ struct XcgPairState {
     }
     q.opd = NIL;
     move_to(p, y);
-    left(x, t);
+    left(x, t + 1);                                // (x served this op's own lookup at t)
     bmap.put(h, y);
     d_append(y, t);
   }
