@@ -65,8 +65,19 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 			if (oseg == NULL) {
 				cache->enter(hash, seg);
 			} else {
-				if (!oseg->equal(seg))
+				if (!oseg->equal(seg)) {
 					cache->replace(hash, seg);
+					/*
+					 * XCodecMemoryCache::replace stores the new entry with
+					 * CacheEntry's implicit copy assignment (xcodec_cache.h:
+					 * 246-269, :333-336), which takes no reference: the cache
+					 * keeps a pointer the reference decoder's window and output
+					 * keep alive (:137-139).  The host mirror has neither, so
+					 * it keeps one reference itself (a 2 KiB segment per name
+					 * reuse, never freed) rather than leave the cache dangling.
+					 */
+					seg->ref();
+				}
 				oseg->unref();
 			}
 			seg->unref();

@@ -203,6 +203,21 @@ void RefDiskCache::touch(const uint64_t& hash, BufferSegment *seg)
 uint64_t RefDiskCache::written(void) const { return disk_->written(); }
 
 #ifdef XCGPU_DROPIN
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+/* Diagnostics: XCG_SEGV_TRACE=1 prints the native stack of a fatal signal. */
+static void segv_trace(int sig)
+{
+	void *fr[64];
+	int n = backtrace(fr, 64);
+	backtrace_symbols_fd(fr, n, 2);
+	signal(sig, SIG_DFL);
+	raise(sig);
+}
+static const bool segv_trace_set = getenv("XCG_SEGV_TRACE") != NULL &&
+    (signal(SIGSEGV, segv_trace), signal(SIGABRT, segv_trace), true);
+
 /* The binding finds the XCodecDisk under an XCodecDiskCache by itself; this
  * harness's restated disk level is resolved here. */
 static bool ref_disk_resolver(XCodecCache *level, const void **disk, uint64_t *bytes)

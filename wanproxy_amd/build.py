@@ -15,7 +15,7 @@ SRCS = ['csrc/xcg_api.hip', 'csrc/xcg_encode.hip', 'csrc/xcg_decode.hip', 'csrc/
 HDRS = ['csrc/xcg_device.h', 'csrc/xcg_cache.h', 'csrc/xcg_args.h', '../include/xcgpu.h']
 OUT = os.path.join(HERE, 'libxcgpu.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Wall']
+FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Wall'] + os.environ.get('XCG_EXTRA_FLAGS', '').split()
 
 
 def _newer(out: str, deps) -> bool:
