@@ -194,30 +194,48 @@ def _ref(h):
     return b'\xf1\x02' + h.to_bytes(8, 'big')
 
 
-def test_pair_decode_name_reuse(dropin, ref_oracle):
-    """<EXTRACT> of cached bytes under a hash the cache holds with other bytes
-    (name reuse, xcodec_decoder.cc:110-133): the pair replaces at both levels
-    (primary replace + disk remove / enter), and later REFs get the new bytes
-    -- on a primary hit and on a disk-only hit (promoted first)."""
+def name_reuse_calls(hash_fn):
+    """Decode calls exercising name reuse on a 3-slot pair (see below)."""
     x, y = _collision_pair()
-    h = ref_oracle.hash(x)
-    assert h == ref_oracle.hash(y) and x != y
+    h = hash_fn(x)
+    assert h == hash_fn(y) and x != y
     r = random.Random(5)
     fill = [bytes(r.getrandbits(8) | 1 for _ in range(SEG)) for _ in range(6)]
-    calls = [
+    return x, y, [
         _extract(x) + b'lit',
         _ref(h) + _extract(y) + _ref(h) + b'\xf1\x00',
         b''.join(_extract(s) for s in fill[:4]),         # push h out of a 3-slot primary (disk only)
         _extract(x) + _ref(h),                           # disk hit, promoted, then replaced back to x
         _ref(h) + b''.join(_extract(s) for s in fill[4:]) + _ref(h),
     ]
-    res = []
-    for o in (ref_oracle, dropin):
-        c = o.cache_new_pair(3 * SEG, mpg.disk_bytes(1))
-        res.append(decode_calls(o, c, calls) + [o.pair_stats(c)])
-        o.cache_free(c)
-    assert res[0] == res[1]
-    assert res[0][1][1] == x + y + y + b'\xf1'
+
+
+def name_reuse_run(o, calls):
+    c = o.cache_new_pair(3 * SEG, mpg.disk_bytes(1))
+    res = decode_calls(o, c, calls) + [o.pair_stats(c)]
+    o.cache_free(c)
+    return res
+
+
+def test_pair_decode_name_reuse(dropin):
+    """<EXTRACT> of cached bytes under a hash the cache holds with other bytes
+    (name reuse, xcodec_decoder.cc:110-133): the pair replaces at both levels
+    (primary replace + disk remove / enter), and later REFs get the new bytes
+    -- on a primary hit and on a disk-only hit (promoted first).
+
+    Checked against the oracle restatement, not the reference in-process: the
+    reference's XCodecMemoryCache::replace stores the new segment without a
+    reference (xcodec_cache.h:333-336), so when the replaced entry is evicted
+    its window's pointer dangles and the next window collision unrefs freed
+    memory (xcodec_window.h:77-80) -- a crash that comes and goes with the
+    heap.  tests/test_pair_oracle.py pins the restatement to the reference on
+    these calls in a child process."""
+    from oracle.lib import Oracle
+    port = Oracle()
+    x, y, calls = name_reuse_calls(port.hash)
+    exp = name_reuse_run(port, calls)
+    assert name_reuse_run(dropin, calls) == exp
+    assert exp[1][1] == x + y + y + b'\xf1'
 
 
 def test_shared_disk_contexts_vs_reference(ref_oracle):

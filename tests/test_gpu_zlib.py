@@ -272,7 +272,7 @@ def test_inflate_slot_reuse_after_reset():
     assert ctx.consume_many([(0, b)])[0][1] == -1
     ctx.reset(0)
     ctx.reset(1)
-    assert ctx.consume_many([(0, b), (1, a[:10])]) == [(b'second stream ' * 70, 1),
-                                                        (zlib.decompressobj().decompress(a[:10]), 0)]
-    assert ctx.consume_many([(1, a[10:])]) == [(b'first stream ' * 50, 1)]
+    head = zlib.decompressobj().decompress(a[:10])
+    assert ctx.consume_many([(0, b), (1, a[:10])]) == [(b'second stream ' * 70, 1), (head, 0)]
+    assert ctx.consume_many([(1, a[10:])]) == [((b'first stream ' * 50)[len(head):], 1)]
     ctx.close()

@@ -129,3 +129,42 @@ def test_ref_shared_disk_fronts(ref_oracle):
     eb2, wb2, _ = ref_oracle.pair_stats(pb, disk_live=True)
     assert wa2 == wb2 == 550                             # one write head
     assert ea2 == 0 and la2 == eb2 > 0                  # the peer front's lap took every local entry
+
+
+_NAME_REUSE_CHILD = r'''
+import hashlib, json, sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import test_gpu_pair_decode as t
+from oracle.lib import Oracle
+o = Oracle(ref=True)
+x, y, calls = t.name_reuse_calls(o.hash)
+res = t.name_reuse_run(o, calls)
+print(json.dumps([[r[0], hashlib.sha256(r[1]).hexdigest(), r[2], r[3]] for r in res[:-1]] + [list(res[-1])]))
+'''
+
+
+def test_name_reuse_port_vs_reference():
+    """The name-reuse calls of tests/test_gpu_pair_decode.py (pair replace at
+    both levels, xcodec_decoder.cc:110-133) on the restatement and on the
+    reference.  The reference runs in a child process: its replace keeps a
+    segment it holds no reference to (xcodec_cache.h:333-336) and a later window
+    collision unrefs it after eviction freed it (xcodec_window.h:77-80), which
+    may crash; only a clean exit is compared."""
+    import subprocess
+    import sys
+    if not os.path.exists(os.path.join(HERE, '..', 'oracle/_ref/libxcref.so')):
+        pytest.skip('oracle/_ref/libxcref.so not built (needs /root/reference)')
+    from oracle.lib import Oracle
+    sys.path.insert(0, HERE)
+    import test_gpu_pair_decode as t
+    port = Oracle()
+    x, y, calls = t.name_reuse_calls(port.hash)
+    res = t.name_reuse_run(port, calls)
+    exp = [[r[0], sha(r[1]), r[2], r[3]] for r in res[:-1]] + [list(res[-1])]
+    assert res[1][1] == x + y + y + b'\xf1'
+    p = subprocess.run([sys.executable, '-c', _NAME_REUSE_CHILD, HERE, os.path.dirname(HERE)],
+                       capture_output=True, text=True, timeout=120)
+    if p.returncode < 0:
+        pytest.xfail('reference crashed (signal %d): its replace/window use-after-free' % -p.returncode)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1]) == exp

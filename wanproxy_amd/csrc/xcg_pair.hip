@@ -382,6 +382,22 @@ struct XcgPairState {
     return e;
   }
   bool is_new(uint32_t x) const { return x >= C + D; }
+  // (XCG_PAIR_DEBUG) a recorded lookup the replay contradicts
+  void bad_row(uint32_t kind, uint32_t x, uint64_t h, uint64_t t) {
+    fprintf(stderr, "pair bad: xuid %u kind %u id %u%s t %llx hash %016llx key %016llx p %d d %d", xuid, kind, x,
+            is_new(x) ? " (new)" : "", (unsigned long long)t, (unsigned long long)h, (unsigned long long)ekey(x),
+            (int)ep(x), (int)ed(x));
+    if (x >= C && !is_new(x)) {
+      const DSlot& q = ds()[x - C];
+      fprintf(stderr, " | block live %u xuid %u dp %d olive %u oxuid %u odp %d ep %u/%u", q.live, q.xuid, (int)q.dp,
+              q.olive, q.oxuid, (int)q.odp, q.ep, epoch);
+    } else if (x < C) {
+      const PSlot& q = ps[x];
+      fprintf(stderr, " | slot key %016llx pd %d okey %016llx opd %d ep %u/%u", (unsigned long long)q.key, (int)q.pd,
+              (unsigned long long)q.okey, (int)q.opd, q.ep, epoch);
+    }
+    fprintf(stderr, "\n");
+  }
   void mark_bad(uint32_t c, uint32_t t) {
     bad[c] = 1;
     blo[c] = t < blo[c] ? t : blo[c];
@@ -607,7 +623,11 @@ struct XcgPairState {
         if (kind == EV_GHIT || kind == EV_GMISS) {
           if (ref >= C + D) { mark_bad(c, e.z); ok = false; continue; }
           const bool pr = present(ref);
-          if (pr != (kind == EV_GHIT)) { mark_bad(c, e.z); ok = false; }
+          if (pr != (kind == EV_GHIT)) {
+            mark_bad(c, e.z);
+            ok = false;
+            if (pair_debug()) bad_row(kind, ref, h, t);
+          }
           if (pr) lookup(ref, t);
         } else if (kind == EV_HIT) {
           const uint32_t x = bmap.find(h);
@@ -616,7 +636,12 @@ struct XcgPairState {
           lookup(x, t);
         } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
           const uint32_t x0 = bmap.find(h);
-          if (x0 != NIL && present(x0)) { mark_bad(c, e.z); ok = false; continue; }
+          if (x0 != NIL && present(x0)) {
+            mark_bad(c, e.z);
+            ok = false;
+            if (pair_debug()) bad_row(kind, x0, h, t);
+            continue;
+          }
           const uint32_t x = C + D + (uint32_t)ns.size();
           ns.push_back(NewEnt{h, NIL, NIL, c, ref});
           bmap.put(h, x);
@@ -683,7 +708,9 @@ struct XcgPairState {
     }
     for (uint32_t i : touchedD) {
       DSlot& q = ds()[i];
-      if (q.live && !q.olive && q.xuid != xuid) {  // another front's index entry went
+      // another front's index entry went: invalidated, and maybe rewritten with
+      // one of this front's entries since (only this front writes in its pass)
+      if (q.live && q.xuid != xuid && (!q.olive || q.oxuid != q.xuid)) {
         XcgPairState* f = q.xuid < disk->fronts.size() ? disk->fronts[q.xuid] : nullptr;
         if (f) {
           --f->dlive;
