@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <memory>
 #include <set>
 #include <unordered_map>
 #include <vector>
@@ -97,6 +98,28 @@ void frame_refs(const uint8_t* enc, uint64_t n, const uint8_t* in,
       pos += SEG;
     }
   }
+}
+
+// Decoded size of enc[0..n) if every op resolves (xcodec_decoder.cc:73-185):
+// literal and escaped bytes one each, EXTRACT / REF / BACKREF one segment
+// each; the walk stops at an incomplete or unknown op, as the decoder does.
+uint64_t decoded_bound(const uint8_t* enc, uint64_t n) {
+  uint64_t i = 0, out = 0;
+  while (i < n) {
+    const uint8_t* m = (const uint8_t*)memchr(enc + i, 0xF1, n - i);
+    if (!m) return out + (n - i);
+    const uint64_t at = (uint64_t)(m - enc);
+    out += at - i;
+    i = at;
+    if (i + 1 >= n) return out;
+    const uint8_t op = enc[i + 1];
+    if (op == 0x00) { out += 1; i += 2; }                       // escaped 0xF1
+    else if (op == 0x01) { out += SEG; i += 2 + SEG; }          // EXTRACT
+    else if (op == 0x02) { out += SEG; i += 10; }               // REF
+    else if (op == 0x03) { out += SEG; i += 3; }                // BACKREF
+    else return out;
+  }
+  return out;
 }
 
 }  // namespace
@@ -239,23 +262,20 @@ int xcg_pipe::decode_data() {
     }
     return XCG_OK;
   }
-  // One decode() call over everything buffered: up to 2048 output bytes per
-  // input byte (a BACKREF expands 3 -> 2048).
+  // One decode() call over everything buffered, into an output sized from
+  // the ops themselves (not filled: the decode writes what it returns).
   const uint64_t off = 0;
   const uint32_t len = (uint32_t)fbuf.size();
   uint64_t oo = 0, ol = 0, cons = 0;
   int32_t st = 0;
   std::vector<uint64_t> unk(1u << 16);
   uint32_t nunk = 0;
-  std::vector<uint8_t> out((size_t)len * 205 + 4096);
+  const uint64_t cap = decoded_bound(fbuf.data(), len) + 4096;
+  std::unique_ptr<uint8_t[]> out(new uint8_t[cap]);
   int rc = xcg_decode_set_window(dec, win);
-  for (int tries = 0; rc == XCG_OK && tries < 2; ++tries) {
-    rc = xcg_decode_host(dec, fbuf.data(), len, &off, &len, 1, out.data(), out.size(), &oo, &ol, &st, &cons,
+  if (rc == XCG_OK)
+    rc = xcg_decode_host(dec, fbuf.data(), len, &off, &len, 1, out.get(), cap, &oo, &ol, &st, &cons,
                          unk.data(), (uint32_t)unk.size(), &nunk);
-    if (rc != XCG_EOVERFLOW) break;
-    out.resize((size_t)len * SEG + 4096);                             // BACKREF-dense input
-    rc = XCG_OK;
-  }
   xcg_decode_set_window(dec, nullptr);
   if (rc != XCG_OK) return rc;
   if (st < 0) return XCG_EPROTO;                                     // decode() returned false
@@ -279,7 +299,7 @@ int xcg_pipe::decode_data() {
     }
     fbuf.erase(fbuf.begin(), fbuf.begin() + (ptrdiff_t)cons);
   }
-  to_local.insert(to_local.end(), out.begin() + (ptrdiff_t)oo, out.begin() + (ptrdiff_t)(oo + ol));
+  to_local.insert(to_local.end(), out.get() + oo, out.get() + oo + ol);
   for (uint32_t k = 0; k < nunk; ++k) unknown.insert(unk[k]);
   // <ASK>s in groups of ASK_MAX (:510-545)
   std::vector<uint64_t> hs(unknown.begin(), unknown.end());
