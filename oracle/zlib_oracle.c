@@ -337,6 +337,12 @@ typedef struct zr_stream {
     uint32_t adler;
     uint64_t match_start;
     uint64_t block_start;         /* stream position */
+    uint64_t strstart;            /* next loop top; < total when a flush call stopped early */
+    int avail, mlen;              /* deflate_slow's match_available / match_length across such a stop */
+    int ins;                      /* deflate_fast: s->insert, positions before strstart still to hash */
+    uint64_t acc; int nb;         /* bits of the last incomplete output byte (bi_buf after flush_pending) */
+    uint8_t *q; uint64_t qn, qcap;/* produced but not yet delivered: zlib's pending past the pipe's buffer */
+    uint64_t *fhead, *fprev;      /* deflate_fast: zlib's head[] / prev[] by stream position (NONE: NIL) */
     Syms sy;
     /* per-call scratch */
     uint64_t lo;                  /* stream position of x[0] */
@@ -345,16 +351,27 @@ typedef struct zr_stream {
 } zr_stream;
 
 zr_stream *zr_create(int level) {
-    if (level < 4 || level > 9) return NULL;   /* deflate_slow levels (wanproxy.conf: 6) */
+    if (level < 1 || level > 9) return NULL;   /* deflate_fast 1-3, deflate_slow 4-9 (wanproxy.conf: 6) */
     init_tables();
     zr_stream *s = calloc(1, sizeof(zr_stream));
     s->level = level;
     s->good = CFG[level][0]; s->lazy = CFG[level][1]; s->nice = CFG[level][2]; s->chain = CFG[level][3];
     s->adler = 1;
+    s->mlen = MIN_MATCH - 1;
+    if (level < 4) {
+        s->fhead = malloc(sizeof(uint64_t) * 32768);
+        s->fprev = malloc(sizeof(uint64_t) * WSIZE);
+        for (int i = 0; i < 32768; i++) s->fhead[i] = NONE;
+        for (unsigned i = 0; i < WSIZE; i++) s->fprev[i] = NONE;
+    }
     return s;
 }
 
-void zr_free(zr_stream *s) { free(s); }
+void zr_free(zr_stream *s) {
+    if (!s) return;
+    free(s->q); free(s->fhead); free(s->fprev);
+    free(s);
+}
 
 static uint32_t adler32(uint32_t a, const uint8_t *p, uint64_t n) {
     uint32_t s1 = a & 0xffff, s2 = a >> 16;
@@ -408,9 +425,19 @@ static void walk(const zr_stream *s, uint64_t p, uint64_t end, int budget, int n
 }
 typedef struct { uint64_t rd, end; } Feed;   /* stream positions read into zlib's window / available */
 
+/* deflate_fast's INSERT_STRING at q: the old head (zlib's hash_head), q becomes the head */
+static uint64_t fast_insert(zr_stream *s, uint64_t q) {
+    uint32_t h = hash3(s, q);
+    uint64_t hh = s->fhead[h];
+    s->fprev[q & (WSIZE - 1)] = hh;
+    s->fhead[h] = q;
+    return hh;
+}
+
 /* fill_window's effect on positions: slide (base += WSIZE) when strstart >=
- * WSIZE + MAX_DIST, then read what fits.  The window's bytes themselves are
- * not needed (see walk()). */
+ * WSIZE + MAX_DIST, then read what fits; deflate_fast also hashes the
+ * positions s->insert names once their bytes exist.  The window's bytes
+ * themselves are not needed (see walk()). */
 static void fill_window(zr_stream *s, uint64_t strstart, Feed *f) {
     do {
         uint64_t more = WINSZ - (f->rd - s->base);
@@ -418,6 +445,15 @@ static void fill_window(zr_stream *s, uint64_t strstart, Feed *f) {
         if (f->rd == f->end) break;
         uint64_t n = f->end - f->rd; if (n > more) n = more;
         f->rd += n;
+        if (s->fhead && f->rd - strstart + s->ins >= MIN_MATCH) {
+            uint64_t str = strstart - (uint64_t)s->ins;
+            while (s->ins) {
+                fast_insert(s, str);
+                str++;
+                s->ins--;
+                if (f->rd - strstart + s->ins < MIN_MATCH) break;
+            }
+        }
     } while (f->rd - strstart < MIN_LOOKAHEAD && f->rd < f->end);
 }
 
@@ -442,11 +478,146 @@ static uint64_t head_of(const zr_stream *s, uint64_t p, uint32_t lookahead) {
     return h;
 }
 
+/* DeflatePipe's buffer (deflate_pipe.cc:57-115).  Output reaches the pipe at
+ * flush_pending, i.e. after every block flush (b->n = bytes complete).  Under
+ * Z_NO_FLUSH (loop tops with >= MIN_LOOKAHEAD bytes of lookahead) the pipe
+ * takes everything, emptying its 64 KiB buffer whenever it fills, so when the
+ * Z_SYNC_FLUSH call begins the buffer holds n mod 65536 bytes, n = the bytes
+ * the consume took so far.  That call ends at the first block flush that
+ * leaves the buffer full (FLUSH_BLOCK's need_more): the consume delivers up
+ * to the boundary L = 65536 * (n / 65536 + 1) and the stream goes on from
+ * there at the next consume, without a sync marker. */
+typedef struct { uint64_t n; int stopped; } Pipe;
+
+static int flushed(Pipe *pp, const Bits *b, uint64_t la) {   /* 1: the flush call stops here */
+    if (la >= MIN_LOOKAHEAD) { pp->n = b->n; return 0; }
+    if (b->n >= 65536 * (pp->n / 65536 + 1)) { pp->stopped = 1; return 1; }
+    return 0;
+}
+
+/* deflate_slow (levels 4-9) over the match table from s->strstart.  Returns 1
+ * if the flush call stopped at a block flush (state saved for the next call). */
+static int scan_slow(zr_stream *s, Bits *b, Feed *f, Pipe *pp, int finishing) {
+    uint64_t p = s->strstart, lo = s->lo;
+    int match_length = s->mlen, match_available = s->avail;
+    for (;;) {
+        if (f->rd - p < MIN_LOOKAHEAD) {
+            fill_window(s, p, f);
+            if (f->rd - p == 0) break;
+        }
+        uint32_t lookahead = (uint32_t)(f->rd - p);
+        uint64_t head = head_of(s, p, lookahead);
+        int prev_length = match_length;
+        uint64_t prev_match = s->match_start;
+        match_length = MIN_MATCH - 1;
+        if (head != NONE && prev_length < s->lazy) {
+            uint64_t i = p - lo;
+            int quar = prev_length >= s->good;
+            int M = quar ? s->mquar[i] : s->mfull[i];
+            if (M > prev_length) {
+                match_length = M;
+                s->match_start = lo + (quar ? s->squar[i] : s->sfull[i]);
+            } else {
+                match_length = (uint32_t)prev_length <= lookahead ? prev_length : (int)lookahead;
+            }
+            if (match_length <= 5 && match_length == MIN_MATCH && p - s->match_start > TOO_FAR)
+                match_length = MIN_MATCH - 1;
+        }
+        if (prev_length >= MIN_MATCH && match_length <= prev_length) {
+            int bf = tally(s, (unsigned)(prev_length - MIN_MATCH), (unsigned)(p - 1 - prev_match));
+            p += (uint64_t)prev_length - 1;
+            match_available = 0;
+            match_length = MIN_MATCH - 1;
+            if (bf) {                                     /* FLUSH_BLOCK */
+                flush(s, b, p, 0);
+                if (!finishing && flushed(pp, b, lookahead)) goto stop;
+            }
+        } else if (match_available) {
+            int bf = tally(s, X(s, p - 1), 0);
+            if (bf) flush(s, b, p, 0);                    /* FLUSH_BLOCK_ONLY */
+            p++;
+            if (bf && !finishing && flushed(pp, b, lookahead)) goto stop;   /* avail_out == 0: need_more */
+        } else {
+            match_available = 1;
+            p++;
+        }
+    }
+    if (match_available) tally(s, X(s, p - 1), 0);
+    s->strstart = p;
+    s->avail = 0;
+    s->mlen = MIN_MATCH - 1;
+    return 0;
+stop:
+    s->strstart = p;
+    s->avail = match_available;
+    s->mlen = match_length;
+    return 1;
+}
+
+/* deflate_fast (levels 1-3): zlib's own chains (only the positions the parse
+ * hashes: loop tops, and the inside of matches no longer than max_lazy).
+ * Returns 1 if the flush call stopped at a block flush. */
+static int scan_fast(zr_stream *s, Bits *b, Feed *f, Pipe *pp, int finishing) {
+    uint64_t p = s->strstart;
+    const int max_insert = s->lazy;
+    for (;;) {
+        if (f->rd - p < MIN_LOOKAHEAD) {
+            fill_window(s, p, f);
+            if (f->rd - p == 0) break;
+        }
+        const uint64_t lookahead = f->rd - p;
+        uint64_t hh = NONE;
+        if (lookahead >= MIN_MATCH) hh = fast_insert(s, p);
+        int ml = 0;
+        uint64_t ms = 0;
+        if (hh != NONE && hh > s->base && p - hh <= MAX_DIST) {   /* longest_match from hash_head */
+            int cap = lookahead < MAX_MATCH ? (int)lookahead : MAX_MATCH;
+            int nice = s->nice < cap ? s->nice : cap, chain = s->chain, best = MIN_MATCH - 1;
+            uint64_t cur = hh, limit = p > MAX_DIST ? p - MAX_DIST : 0;
+            for (;;) {
+                int len = lcp(s, p, cur, cap);
+                if (len > best) { best = len; ms = cur; if (len >= nice) break; }
+                cur = s->fprev[cur & (WSIZE - 1)];
+                if (cur == NONE || cur <= limit || --chain == 0) break;
+            }
+            if (best >= MIN_MATCH) ml = best;
+        }
+        int bf;
+        if (ml >= MIN_MATCH) {
+            bf = tally(s, (unsigned)(ml - MIN_MATCH), (unsigned)(p - ms));
+            if ((uint64_t)ml <= (uint64_t)max_insert && lookahead - (uint64_t)ml >= MIN_MATCH) {
+                for (int k = 1; k < ml; k++) fast_insert(s, p + (uint64_t)k);
+            }
+            p += (uint64_t)ml;
+        } else {
+            bf = tally(s, X(s, p), 0);
+            p++;
+        }
+        if (bf) {                                         /* FLUSH_BLOCK */
+            flush(s, b, p, 0);
+            if (!finishing && flushed(pp, b, lookahead)) { s->strstart = p; return 1; }
+        }
+    }
+    s->strstart = p;
+    s->ins = p - s->base < MIN_MATCH - 1 ? (int)(p - s->base) : MIN_MATCH - 1;
+    return 0;
+}
+
+static void grow(zr_stream *s, uint64_t want) {
+    if (s->qcap >= want) return;
+    uint64_t c = s->qcap ? s->qcap : 65536;
+    while (c < want) c *= 2;
+    s->q = realloc(s->q, c);
+    s->qcap = c;
+}
+
 /* One DeflatePipe::consume(): n > 0 bytes, then Z_SYNC_FLUSH; n == 0: Z_FINISH.
- * Returns the bytes written to out (or -1 if cap was too small). */
+ * Returns the bytes the pipe produces (written to out), or -1 if cap was too small. */
 int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap) {
-    Bits b = {out, 0, cap, 0, 0, 0};
     if (s->finished) return 0;
+    const uint64_t p0 = s->strstart, end = s->total + n;
+    grow(s, s->qn + 2 * (n + (s->total - p0)) + 4096);
+    Bits b = {s->q, s->qn, s->qcap, s->acc, s->nb, 0};
     if (!s->started) {
         unsigned lf = s->level < 2 ? 0 : s->level < 6 ? 1 : s->level == 6 ? 2 : 3;
         unsigned header = ((8 + (7 << 4)) << 8) | (lf << 6);
@@ -454,7 +625,6 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
         put_byte(&b, header >> 8); put_byte(&b, header & 0xff);
         s->started = 1;
     }
-    uint64_t p = s->total, end = s->total + n;
     /* history the chains can reach + this call's bytes, by stream position */
     uint64_t lo = s->total > WSIZE ? s->total - WSIZE : 0;
     if (lo < s->base) lo = s->base;
@@ -465,81 +635,54 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
     memcpy(s->x + (s->total - lo), in, n);
     memset(s->x + span, 0, MAX_MATCH + 8);
     s->adler = adler32(s->adler, in, n);
+    s->prv = NULL;
+    s->mfull = s->mquar = NULL;
+    s->sfull = s->squar = NULL;
 
-    /* phase A: hash chains (prev links) over [lo, end - 2) */
-    s->prv = malloc(sizeof(uint32_t) * (span + 1));
-    uint32_t *headt = malloc(sizeof(uint32_t) * 32768);
-    for (int i = 0; i < 32768; i++) headt[i] = UINT32_MAX;
-    for (uint64_t q = lo; q < end; q++) {
-        if (q + 2 < end) {
-            uint32_t h = hash3(s, q);
-            s->prv[q - lo] = headt[h];
-            headt[h] = (uint32_t)(q - lo);
-        } else s->prv[q - lo] = UINT32_MAX;
-    }
-    free(headt);
-    /* phase B: match table for every position with >= MIN_MATCH lookahead */
-    s->mfull = calloc(span, 2); s->mquar = calloc(span, 2);
-    s->sfull = calloc(span, 4); s->squar = calloc(span, 4);
-    for (uint64_t q = p; q + 2 < end; q++) {
-        uint64_t i = q - lo;
-        if (prevlink(s, q) == NONE) continue;
-        walk(s, q, end, s->chain, s->nice, &s->mfull[i], &s->sfull[i]);
-        walk(s, q, end, s->chain >> 2, s->nice, &s->mquar[i], &s->squar[i]);
-    }
-
-    /* phase C: deflate_slow over the table */
-    Feed f = {s->total, end};
-    int flush_kind = n == 0 ? 2 : 1;              /* 1 = Z_SYNC_FLUSH, 2 = Z_FINISH */
-    {
-        int match_length = MIN_MATCH - 1, match_available = 0;
-        for (;;) {
-            if (f.rd - p < MIN_LOOKAHEAD) {
-                fill_window(s, p, &f);
-                if (f.rd - p == 0) break;
-            }
-            uint32_t lookahead = (uint32_t)(f.rd - p);
-            uint64_t head = head_of(s, p, lookahead);
-            int prev_length = match_length;
-            uint64_t prev_match = s->match_start;
-            match_length = MIN_MATCH - 1;
-            if (head != NONE && prev_length < s->lazy) {
-                uint64_t i = p - lo;
-                int quar = prev_length >= s->good;
-                int M = quar ? s->mquar[i] : s->mfull[i];
-                if (M > prev_length) {
-                    match_length = M;
-                    s->match_start = lo + (quar ? s->squar[i] : s->sfull[i]);
-                } else {
-                    match_length = (uint32_t)prev_length <= lookahead ? prev_length : (int)lookahead;
-                }
-                if (match_length <= 5 && match_length == MIN_MATCH && p - s->match_start > TOO_FAR)
-                    match_length = MIN_MATCH - 1;
-            }
-            if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-                int bf = tally(s, (unsigned)(prev_length - MIN_MATCH), (unsigned)(p - 1 - prev_match));
-                p += (uint64_t)prev_length - 1;
-                match_available = 0;
-                match_length = MIN_MATCH - 1;
-                if (bf) flush(s, &b, p, 0);
-            } else if (match_available) {
-                if (tally(s, X(s, p - 1), 0)) flush(s, &b, p, 0);
-                p++;
-            } else {
-                match_available = 1;
-                p++;
-            }
+    if (!s->fhead) {
+        /* phase A: hash chains (prev links) over [lo, end - 2) */
+        s->prv = malloc(sizeof(uint32_t) * (span + 1));
+        uint32_t *headt = malloc(sizeof(uint32_t) * 32768);
+        for (int i = 0; i < 32768; i++) headt[i] = UINT32_MAX;
+        for (uint64_t q = lo; q < end; q++) {
+            if (q + 2 < end) {
+                uint32_t h = hash3(s, q);
+                s->prv[q - lo] = headt[h];
+                headt[h] = (uint32_t)(q - lo);
+            } else s->prv[q - lo] = UINT32_MAX;
         }
-        if (match_available) tally(s, X(s, p - 1), 0);
+        free(headt);
+        /* phase B: match table for every position with >= MIN_MATCH lookahead */
+        s->mfull = calloc(span, 2); s->mquar = calloc(span, 2);
+        s->sfull = calloc(span, 4); s->squar = calloc(span, 4);
+        for (uint64_t q = p0; q + 2 < end; q++) {
+            uint64_t i = q - lo;
+            if (prevlink(s, q) == NONE) continue;
+            walk(s, q, end, s->chain, s->nice, &s->mfull[i], &s->sfull[i]);
+            walk(s, q, end, s->chain >> 2, s->nice, &s->mquar[i], &s->squar[i]);
+        }
     }
-    if (flush_kind == 2) {
-        flush(s, &b, p, 1);
+
+    /* phase C: the parse; a flush call may stop at a block flush */
+    Feed f = {s->total, end};
+    Pipe pp = {s->qn, 0};
+    const int finishing = n == 0;
+    int stopped = s->fhead ? scan_fast(s, &b, &f, &pp, finishing) : scan_slow(s, &b, &f, &pp, finishing);
+    uint64_t deliver;
+    if (finishing) {
+        flush(s, &b, s->strstart, 1);
         put_byte(&b, s->adler >> 24); put_byte(&b, (s->adler >> 16) & 0xff);
         put_byte(&b, (s->adler >> 8) & 0xff); put_byte(&b, s->adler & 0xff);
         s->finished = 1;
+        deliver = b.n;
     } else {
-        if (s->sy.n) flush(s, &b, p, 0);
-        stored_block(&b, NULL, 0, 0);            /* Z_SYNC_FLUSH marker */
+        if (!stopped && s->sy.n) {                         /* deflate_*'s last FLUSH_BLOCK(s, 0) */
+            flush(s, &b, s->strstart, 0);
+            stopped = flushed(&pp, &b, 0);
+        }
+        if (!stopped) stored_block(&b, NULL, 0, 0);       /* Z_SYNC_FLUSH marker */
+        const uint64_t lim = 65536 * (pp.n / 65536 + 1);
+        deliver = b.n < lim ? b.n : lim;
     }
     /* keep the last WSIZE bytes: the next call's chains reach back MAX_DIST */
     uint64_t keep = end - lo < WSIZE ? end - lo : WSIZE;
@@ -547,7 +690,20 @@ int64_t zr_consume(zr_stream *s, const uint8_t *in, uint64_t n, uint8_t *out, ui
     s->total = end;
     free(s->x); free(s->prv); free(s->mfull); free(s->mquar); free(s->sfull); free(s->squar);
     s->x = NULL;
-    return b.err ? -1 : (int64_t)b.n;
+    s->acc = b.acc; s->nb = b.nb;
+    if (b.err) return -1;
+    if (deliver > cap) return -1;
+    memcpy(out, s->q, deliver);
+    memmove(s->q, s->q + deliver, b.n - deliver);
+    s->qn = b.n - deliver;
+    return (int64_t)deliver;
 }
 
-uint64_t zr_bound(uint64_t n) { return 2 * n + 1024; }
+uint64_t zr_bound(uint64_t n) { return 2 * n + 4 * 65536 + 1024; }
+
+/* Test hook: positions the last flush call left for the next consume (a stop
+ * inside the flush call's tail), and bytes produced but not yet delivered. */
+void zr_carry(const zr_stream *s, uint64_t *deferred, uint64_t *pending) {
+    *deferred = s->total - s->strstart;
+    *pending = s->qn;
+}

@@ -3,8 +3,9 @@
 `DeflatePipeRef` drives the system zlib (1.2.11 in this image and on the GPU
 box; the pinned version of the dependency wanproxy's zlib stage links) in the
 exact call pattern of the reference's DeflatePipe::consume
-(zlib/deflate_pipe.cc:57-115): every input segment through deflate(Z_NO_FLUSH),
-then deflate(Z_SYNC_FLUSH); an empty consume is EOS, deflate(Z_FINISH).
+(zlib/deflate_pipe.cc:57-115), through oracle/deflate_pipe_ref.c: every Buffer
+segment through deflate(Z_NO_FLUSH), then one deflate(Z_SYNC_FLUSH) into the
+pipe's 64 KiB buffer; an empty consume is EOS, deflate(Z_FINISH).
 `InflatePipeRef` is the matching InflatePipe::consume (zlib/inflate_pipe.cc:
 54-139): inflate(Z_NO_FLUSH) per segment, then Z_SYNC_FLUSH / Z_FINISH.
 
@@ -23,29 +24,60 @@ ZLIB_VERSION = '1.2.11'
 
 
 class DeflatePipeRef:
+    """DeflatePipe(level) over the system zlib in the pipe's exact call pattern
+    (oracle/deflate_pipe_ref.c restates deflate_pipe.cc:57-115: segments of at
+    most 2048 bytes through deflate(Z_NO_FLUSH), then ONE deflate(Z_SYNC_FLUSH)
+    into the 64 KiB buffer; a full buffer ends the consume with output still
+    pending in zlib and, when a block flush filled it, no sync marker)."""
+
     def __init__(self, level: int = 6):
-        # deflateInit(&stream_, level): windowBits 15, memLevel 8, default strategy
+        lib = ZOracle.lib()
+        self.s = lib.dpr_create(level)
+        if not self.s:
+            raise ValueError(f'deflateInit({level}) failed')
+
+    def consume(self, data: bytes, segments=None) -> bytes:
+        """One consume(): the bytes of one Buffer, cut into `segments` lengths
+        (default: 2048-byte segments, BUFFER_SEGMENT_SIZE); b'' = EOS.  Returns
+        what the pipe produces."""
+        lib = ZOracle.lib()
+        cap = 2 * len(data) + 4 * 65536 + 1024
+        buf = C.create_string_buffer(cap)
+        if segments is None:
+            seg, nseg = None, 0
+        else:
+            arr = (C.c_uint32 * max(1, len(segments)))(*segments)
+            seg, nseg = arr, len(segments)
+        n = lib.dpr_consume(self.s, data, len(data), seg, nseg, buf, cap)
+        if n < 0:
+            raise RuntimeError('dpr_consume failed')
+        return buf.raw[:n]
+
+    def close(self):
+        if getattr(self, 's', None):
+            ZOracle.lib().dpr_free(self.s)
+            self.s = None
+
+    def __del__(self):
+        self.close()
+
+
+class DeflatePipeUnbounded:
+    """zlib driven with unbounded output per call (Python's zlib module): the
+    stream a DeflatePipe would emit if its flush call never ran out of room.
+    Kept to show where DeflatePipeRef's 64 KiB buffer changes the bytes."""
+
+    def __init__(self, level: int = 6):
         self.z = zlib.compressobj(level, zlib.DEFLATED, 15, 8, zlib.Z_DEFAULT_STRATEGY)
         self.done = False
 
-    def consume(self, data: bytes, segments=None) -> bytes:
-        """One consume(): the bytes of one Buffer (cut into `segments` lengths,
-        default one segment); b'' = EOS.  Returns what the pipe produces."""
+    def consume(self, data: bytes) -> bytes:
         if self.done:
             return b''
         if not data:
             self.done = True
             return self.z.flush(zlib.Z_FINISH)
-        out = []
-        if segments is None:
-            segments = [len(data)]
-        i = 0
-        for n in segments:
-            out.append(self.z.compress(data[i:i + n]))
-            i += n
-        assert i == len(data)
-        out.append(self.z.flush(zlib.Z_SYNC_FLUSH))
-        return b''.join(out)
+        return self.z.compress(data) + self.z.flush(zlib.Z_SYNC_FLUSH)
 
 
 class InflatePipeRef:
@@ -72,13 +104,19 @@ class ZOracle:
             lib.zr_consume.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64]
             lib.zr_bound.restype = C.c_uint64
             lib.zr_bound.argtypes = [C.c_uint64]
+            lib.dpr_create.restype = C.c_void_p
+            lib.dpr_create.argtypes = [C.c_int]
+            lib.dpr_free.argtypes = [C.c_void_p]
+            lib.dpr_consume.restype = C.c_int64
+            lib.dpr_consume.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                        C.c_char_p, C.c_uint64]
             cls._lib = lib
         return cls._lib
 
     def __init__(self, level: int = 6):
         self.s = self.lib().zr_create(level)
         if not self.s:
-            raise ValueError(f'level {level} not restated (4-9 only)')
+            raise ValueError(f'level {level} not restated (1-9 only)')
 
     def consume(self, data: bytes) -> bytes:
         lib = self.lib()

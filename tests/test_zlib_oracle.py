@@ -9,8 +9,8 @@ import zlib
 
 import pytest
 
-from oracle.zlib_pipe import DeflatePipeRef, InflatePipeRef, ZOracle, ZLIB_VERSION
-from tests.zlib_cases import cases, gen_bytes, wan_stream
+from oracle.zlib_pipe import DeflatePipeRef, DeflatePipeUnbounded, InflatePipeRef, ZOracle, ZLIB_VERSION
+from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, wan_stream
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -20,28 +20,30 @@ def test_zlib_version_pinned():
 
 
 def test_segmentation_does_not_change_output():
-    """DeflatePipe feeds each Buffer segment to deflate(Z_NO_FLUSH); the
-    output equals one deflate of the call's bytes (the model's premise)."""
+    """DeflatePipe feeds each Buffer segment (<= 2048 bytes, BUFFER_SEGMENT_SIZE)
+    to deflate(Z_NO_FLUSH); the output does not depend on where the segments
+    are cut (the model's premise), the 64 KiB flush-call stop included."""
     rng = random.Random(3)
-    for level, calls in cases(11, 12):
+    for level, calls in cases(11, 12) + fast_cases(12, 6) + stop_cases(13, (2, 6), range(0, 270, 45)):
         a, b = DeflatePipeRef(level), DeflatePipeRef(level)
         for c in calls:
             segs = []
             left = len(c)
             while left:
-                n = min(left, rng.choice([1, 7, 100, 2048, 4096]))
+                n = min(left, rng.choice([1, 7, 100, 2048, rng.randint(1, 2048)]))
                 segs.append(n)
                 left -= n
             assert a.consume(c) == b.consume(c, segs or None)
 
 
-def test_golden_fixture():
+@pytest.mark.parametrize('key', ['streams', 'fast', 'stops'])
+def test_golden_fixture(key):
     with open(os.path.join(ROOT, 'tests/golden/zlib.json')) as f:
         g = json.load(f)
     assert g['zlib'] == ZLIB_VERSION
-    streams = cases(7, 24)
-    assert len(streams) == len(g['streams'])
-    for (level, calls), rec in zip(streams, g['streams']):
+    streams = {'streams': lambda: cases(7, 24), 'fast': lambda: fast_cases(8, 12), 'stops': lambda: stop_cases(9)}[key]()
+    assert len(streams) == len(g[key])
+    for (level, calls), rec in zip(streams, g[key]):
         assert rec['level'] == level
         o, r = ZOracle(level), DeflatePipeRef(level)
         for c, e in zip(calls, rec['calls']):
@@ -49,6 +51,37 @@ def test_golden_fixture():
             got = o.consume(c)
             assert len(got) == e['out_len'] and hashlib.sha256(got).hexdigest() == e['out_sha256']
             assert r.consume(c) == got
+
+
+def test_flush_call_stops_at_the_pipe_buffer():
+    """The pipe's single Z_SYNC_FLUSH call into its 64 KiB buffer (deflate_pipe.cc:
+    34,86-105): a 64 KiB incompressible consume yields exactly 65536 bytes and no
+    sync marker, unlike zlib driven with unbounded output; the stream still
+    inflates to the input.  Both stop kinds occur: at the final block flush, and
+    inside the flush call's tail with positions left for the next consume."""
+    import ctypes as C
+    lib = ZOracle.lib()
+    lib.zr_carry.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    rng = random.Random(21)
+    kinds = set()
+    for level, calls in stop_cases(22, (1, 6), range(0, 270, 30)):
+        o, r, u = ZOracle(level), DeflatePipeRef(level), DeflatePipeUnbounded(level)
+        outs = []
+        for i, c in enumerate(calls):
+            got = o.consume(c)
+            assert got == r.consume(c)
+            outs.append(got)
+            if i == 0 and len(c) > 65536:                  # the first consume always stops
+                d, p = C.c_uint64(), C.c_uint64()
+                lib.zr_carry(o.s, C.byref(d), C.byref(p))
+                assert len(got) == 65536 and p.value > 0
+                kinds.add('tail' if d.value else 'final')
+            u.consume(c)
+        assert zlib.decompress(b''.join(outs)) == b''.join(calls)
+    assert kinds == {'tail', 'final'}
+    a, b = DeflatePipeRef(6), DeflatePipeUnbounded(6)
+    x = rng.randbytes(65536)
+    assert len(a.consume(x)) == 65536 and len(b.consume(x)) > 65536
 
 
 @pytest.mark.parametrize('seed', [1, 2, 3])
@@ -71,16 +104,24 @@ def test_oracle_vs_zlib_wan_stream_round_trip():
 
 
 def test_oracle_empty_stream_and_levels():
-    for level in range(4, 10):
+    for level in range(1, 10):
         assert ZOracle(level).consume(b'') == DeflatePipeRef(level).consume(b'')
-    for level in (0, 1, 2, 3):
-        with pytest.raises(ValueError):
-            ZOracle(level)
+    with pytest.raises(ValueError):
+        ZOracle(0)
+
+
+@pytest.mark.parametrize('seed', [1, 2])
+def test_oracle_fast_levels_vs_zlib(seed):
+    """deflate_fast (levels 1-3): the parse decides which positions are hashed."""
+    for level, calls in fast_cases(300 + seed, 10):
+        o, r = ZOracle(level), DeflatePipeRef(level)
+        for i, c in enumerate(calls):
+            assert o.consume(c) == r.consume(c), (seed, level, i, len(c))
 
 
 def test_oracle_tiny_calls():
     rng = random.Random(9)
-    for level in (4, 6, 9):
+    for level in (1, 3, 4, 6, 9):
         o, r = ZOracle(level), DeflatePipeRef(level)
         for _ in range(200):
             c = gen_bytes(rng, rng.randint(1, 6))

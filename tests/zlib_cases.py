@@ -56,6 +56,28 @@ def cases(seed: int, n: int, max_extra: int = 150000):
     return out
 
 
+def fast_cases(seed: int, n: int, max_extra: int = 150000):
+    """As cases(), at the deflate_fast levels 1-3."""
+    rng = random.Random(seed)
+    return [(rng.choice([1, 2, 3]), calls) for _, calls in cases(seed, n, max_extra)]
+
+
+def stop_cases(seed: int, levels=(1, 3, 4, 6, 9), offsets=range(-3, 270, 9)):
+    """Streams whose first consume is 4 * 16383 + j incompressible bytes: the
+    fourth block flush falls at loop top 65532 + j - ... of the call, inside
+    the Z_SYNC_FLUSH call's last MIN_LOOKAHEAD positions for most j, where the
+    pipe's 64 KiB buffer (deflate_pipe.cc:34,101-105) is full -- the consume
+    stops there and the rest of its positions are parsed with the next one's
+    bytes.  Then a short consume, another such consume and EOS."""
+    rng = random.Random(seed)
+    out = []
+    for level in levels:
+        for j in offsets:
+            out.append((level, [rng.randbytes(4 * 16383 + j), rng.randbytes(rng.randint(1, 70000)),
+                                rng.randbytes(4 * 16383 + j), b'']))
+    return out
+
+
 def wan_stream(seed: int, ncalls: int, call_bytes: int) -> list:
     """XCodec-output-like traffic: frames of mostly incompressible bytes with
     escapes, references (F1 02 + 8 bytes) and repeated literal runs."""
