@@ -341,16 +341,24 @@ uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
  * codecN.compressor zlib / compressor_level N, wanproxy.conf:32-41).
  * A context holds `nstreams` DeflatePipe(level) instances
  * (zlib/deflate_pipe.cc:36-50: deflateInit(level), windowBits 15, memLevel 8)
- * in HBM.  Output is bit-exact with zlib 1.2.11 for levels 4-9 (deflate_slow);
- * levels 0-3 return XCG_ENOTSUP.
+ * in HBM.  Output is bit-exact with zlib 1.2.11 driven by DeflatePipe::consume:
+ * levels 4-9 (deflate_slow); levels 0-3 return XCG_ENOTSUP.
  *   xcg_zdeflate_batch: one DeflatePipe::consume() per listed stream (a stream
  *   at most once per batch; successive batches continue the streams):
  *   h_len[i] > 0 bytes at d_in + h_in_off[i] = every segment through
- *   deflate(Z_NO_FLUSH), then deflate(Z_SYNC_FLUSH) (deflate_pipe.cc:57-115);
- *   h_len[i] == 0 = EOS: deflate(Z_FINISH) (zlib trailer; the stream is done).
- *   The produced bytes go to d_out + h_out_off[i] (4-byte aligned, room for
- *   xcg_zdeflate_bound(h_len[i])), their count to d_out_len[i].  Metadata
- *   arrays are host memory; the call is asynchronous on `stream`.
+ *   deflate(Z_NO_FLUSH), then ONE deflate(Z_SYNC_FLUSH) into the pipe's
+ *   64 KiB buffer (deflate_pipe.cc:57-115); h_len[i] == 0 = EOS:
+ *   deflate(Z_FINISH) (zlib trailer; the stream is done).
+ *   d_out + h_out_off[i] (4-byte aligned, room for xcg_zdeflate_bound(h_len[i]))
+ *   receives the call's new stream bytes, d_out_len[i] of them; d_deliver[i]
+ *   is how many bytes the consume produce()s: the stream's not yet delivered
+ *   bytes followed by these new ones, cut at d_deliver[i].  The pipe's flush
+ *   call ends when its 64 KiB buffer fills, so a consume can produce less
+ *   than it made (zlib keeps the rest pending; a stop at a block flush also
+ *   leaves out the sync marker and parses the last < 262 positions with the
+ *   next consume's bytes).  The caller keeps the undelivered bytes (at most
+ *   ~64 KiB per stream) and delivers them first next time.  Metadata arrays
+ *   are host memory; the call is asynchronous on `stream`.
  *   xcg_zdeflate_reset: the slot becomes a fresh DeflatePipe.
  */
 typedef struct xcg_zdeflate xcg_zdeflate;
@@ -360,10 +368,10 @@ void xcg_zdeflate_destroy(xcg_zdeflate *z);
 int xcg_zdeflate_reset(xcg_zdeflate *z, uint32_t stream);
 int xcg_zdeflate_batch(xcg_zdeflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
                        const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
-                       uint32_t *d_out_len, void *stream);
+                       uint32_t *d_out_len, uint64_t *d_deliver, void *stream);
 int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
                       const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
-                      uint32_t *h_out_len);
+                      uint32_t *h_out_len, uint64_t *h_deliver);
 
 /* Receiving side: `nstreams` InflatePipe instances (zlib/inflate_pipe.cc:33-46,
  * inflateInit) in HBM.  xcg_zinflate_batch: one InflatePipe::consume() per

@@ -40,6 +40,9 @@ struct DeflatePool {
 	xcg_zdeflate *ctx;
 	std::vector<uint32_t> free_slots;
 	std::map<const void *, uint32_t> slot_of;
+	/* bytes a consume made but did not produce: zlib's pending output past
+	 * the pipe's 64 KiB buffer (deflate_pipe.cc:34,86-105) */
+	std::map<const void *, std::vector<uint8_t> > held;
 };
 
 struct InflatePool {
@@ -121,6 +124,7 @@ DeflatePipe::~DeflatePipe()
 	DeflatePool *p = deflate_pool(level);
 	p->free_slots.push_back(p->slot_of[this]);
 	p->slot_of.erase(this);
+	p->held.erase(this);
 	deflate_levels().erase(this);
 }
 
@@ -134,13 +138,21 @@ DeflatePipe::consume(Buffer *in)
 	uint32_t len = bytes.size();
 	uint64_t in_off = 0, out_off = 0;
 	uint32_t out_len = 0;
+	uint64_t deliver = 0;
 	std::vector<uint8_t> obuf(xcg_zdeflate_bound(len));
 	int rc = xcg_zdeflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1, &obuf[0], &out_off,
-				   &out_len);
+				   &out_len, &deliver);
 	if (rc != XCG_OK)
 		HALT(log_) << "xcgpu deflate: " << xcg_strerror(rc);
+	/* produce the held bytes and the new ones up to `deliver`; keep the rest */
+	std::vector<uint8_t>& q = p->held[this];
+	q.insert(q.end(), obuf.begin(), obuf.begin() + out_len);
+	if (deliver > q.size())
+		HALT(log_) << "xcgpu deflate: delivers more than it made";
 	Buffer out;
-	out.append(&obuf[0], out_len);
+	if (deliver)
+		out.append(&q[0], deliver);
+	q.erase(q.begin(), q.begin() + deliver);
 	if (len == 0) {			/* Z_FINISH */
 		produce_eos(&out);
 		return;

@@ -90,23 +90,32 @@ def run(args) -> dict:
     d_ins = [torch.frombuffer(bytearray(b''.join(row)), dtype=torch.uint8).to(dev) for row in data]
     d_out = [torch.empty(S * ob, dtype=torch.uint8, device=dev) for _ in range(K)]
     d_len = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(K)]
+    d_dl = [torch.zeros(S, dtype=torch.int64, device=dev) for _ in range(K)]
     torch.cuda.synchronize()
     times = []
     for k in range(K):
         t0 = time.perf_counter()
-        ctx.batch_device(d_ins[k], in_off, lens, sids, d_out[k], out_off, d_len[k])
+        ctx.batch_device(d_ins[k], in_off, lens, sids, d_out[k], out_off, d_len[k], d_dl[k])
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
-    outs = []
+    # what each consume produces: the stream's undelivered bytes, then the new ones, cut at d_deliver
+    outs, held = [], [b''] * S
     for k in range(K):
         ol = d_len[k].cpu().numpy()
+        dl = d_dl[k].cpu().numpy()
         o = d_out[k].cpu().numpy()
-        outs.append([o[s * ob:s * ob + int(ol[s])].tobytes() for s in range(S)])
+        row = []
+        for s in range(S):
+            q = held[s] + o[s * ob:s * ob + int(ol[s])].tobytes()
+            row.append(q[:int(dl[s])])
+            held[s] = q[int(dl[s]):]
+        outs.append(row)
     # InflatePipe on the GPU over the same streams: step k consumes deflate output k
     from wanproxy_amd.zpipe import InflatePipes
     ictx = InflatePipes(S)
-    icap = B + 4096
+    icap = 2 * B + 65536
     zi_times, zi_ok = [], True
+    dec = [b''] * S
     for k in range(K):
         zl = np.array([len(outs[k][s]) for s in range(S)], dtype=np.uint32)
         zo = np.zeros(S, dtype=np.uint64)
@@ -125,8 +134,17 @@ def run(args) -> dict:
         st = d_st.cpu().numpy()
         ol = d_ol.cpu().numpy()
         o = d_o.cpu().numpy()
-        zi_ok = zi_ok and bool((st == 0).all()) and all(
-            o[s * icap:s * icap + int(ol[s])].tobytes() == data[k][s] for s in range(S))
+        zi_ok = zi_ok and bool((st == 0).all())
+        for s in range(S):
+            dec[s] += o[s * icap:s * icap + int(ol[s])].tobytes()
+    # decoded so far = a prefix of the input (a consume may hold bytes back), and all of it
+    # once the held-back bytes follow
+    for s in range(S):
+        whole = b''.join(data[k][s] for k in range(K))
+        zi_ok = zi_ok and whole.startswith(dec[s])
+        if s < 64:
+            d = zlib.decompressobj()
+            zi_ok = zi_ok and d.decompress(b''.join(outs[k][s] for k in range(K)) + held[s]) == whole
     ictx.close()
     zi_ms = 1e3 * float(np.median(zi_times[1:] if K > 1 else zi_times))
     nchk = max(1, int(S * args.check))
@@ -155,7 +173,8 @@ def run(args) -> dict:
         'checked': f'{nchk} of {S} streams x {K} calls vs zlib {zlib.ZLIB_RUNTIME_VERSION}, {bad} mismatches',
         'mismatches': bad,
         'inflate': {'GiBps': round(in_bytes / (zi_ms / 1e3) / 2**30, 3), 'ms_per_step': round(zi_ms, 3),
-                    'checked': 'every stream and step decoded back to its input' + ('' if zi_ok else ' -- MISMATCH')},
+                    'checked': 'every stream decoded to a prefix of its input; with the held-back bytes, '
+                               'to all of it (64 streams, CPU zlib)' + ('' if zi_ok else ' -- MISMATCH')},
         'cpu_zlib': {'GiBps': round(nchk * K * B / cpu_s / 2**30, 4), 'threads': args.cpu_threads,
                      'inflate_GiBps': round(nchk * K * B / cpu_inf_s / 2**30, 4),
                      'sample': f'{nchk} streams x {K} calls'},

@@ -11,7 +11,7 @@ import zlib
 import pytest
 
 from oracle.zlib_pipe import DeflatePipeRef
-from tests.zlib_cases import cases, gen_bytes, wan_stream
+from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, wan_stream
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -49,12 +49,14 @@ def check_vs_zlib(streams_by_level):
                                          f'got {len(g)} B, zlib {len(exp)} B, first difference at byte {i}')
 
 
-def test_golden_fixture_gpu():
+@pytest.mark.parametrize('key', ['streams', 'fast', 'stops'])
+def test_golden_fixture_gpu(key):
     with open(os.path.join(ROOT, 'tests/golden/zlib.json')) as f:
         g = json.load(f)
     by_level = {}
     recs = {}
-    for (level, calls), rec in zip(cases(7, 24), g['streams']):
+    streams = {'streams': lambda: cases(7, 24), 'fast': lambda: fast_cases(8, 12), 'stops': lambda: stop_cases(9)}[key]()
+    for (level, calls), rec in zip(streams, g[key]):
         by_level.setdefault(level, []).append(calls)
         recs.setdefault(level, []).append(rec)
     got = run_streams(by_level)
@@ -74,10 +76,31 @@ def test_random_streams_vs_zlib(seed):
     check_vs_zlib(by_level)
 
 
+def test_flush_call_stops_vs_zlib():
+    """Consumes whose Z_SYNC_FLUSH call fills DeflatePipe's 64 KiB buffer
+    (deflate_pipe.cc:34,86-105): at the final block flush (no marker, bytes
+    held back) and inside the flush call's tail (its last positions parsed
+    with the next consume's bytes); compressible consumes in between."""
+    rng = random.Random(12)
+    by_level = {}
+    for level, calls in stop_cases(13, (1, 2, 3, 4, 6, 9), range(-2, 272, 11)):
+        calls = calls[:2] + [gen_bytes(rng, rng.randint(1, 90000))] + calls[2:]
+        by_level.setdefault(level, []).append(calls)
+    check_vs_zlib(by_level)
+
+
+def test_fast_levels_vs_zlib():
+    """deflate_fast (levels 1-3): which positions are hashed depends on the parse."""
+    by_level = {}
+    for level, calls in fast_cases(31, 18):
+        by_level.setdefault(level, []).append(calls)
+    check_vs_zlib(by_level)
+
+
 def test_tiny_calls_vs_zlib():
     rng = random.Random(5)
     streams = [[gen_bytes(rng, rng.randint(1, 6)) for _ in range(40)] + [b''] for _ in range(8)]
-    check_vs_zlib({6: streams, 9: streams[:3], 4: streams[3:5]})
+    check_vs_zlib({6: streams, 9: streams[:3], 4: streams[3:5], 1: streams[5:], 3: streams[:2]})
 
 
 def test_many_streams_wan_traffic_round_trip():
@@ -100,14 +123,14 @@ def test_long_matches_and_slides():
     base = rng.randbytes(40000)
     s1 = [base * 13, bytes(300000), base[::-1] * 3 + base] + [b'']
     s2 = [gen_bytes(rng, 524288), gen_bytes(rng, 100000)] + [b'']
-    check_vs_zlib({6: [s1, s2], 9: [s1], 4: [s2]})
+    check_vs_zlib({6: [s1, s2], 9: [s1], 4: [s2], 1: [s1, s2], 2: [s2], 3: [s1]})
 
 
 def test_errors():
     from wanproxy_amd.xcgpu import XCGError
     from wanproxy_amd.zpipe import DeflatePipes
     with pytest.raises(XCGError):
-        DeflatePipes(1, 1)
+        DeflatePipes(10, 1)
     ctx = DeflatePipes(6, 2)
     with pytest.raises(XCGError):
         ctx.consume_many([(0, b'a'), (0, b'b')])
@@ -221,7 +244,7 @@ def test_distance_boundaries_both_ways():
         parts.append(base + base[:rng.choice([3, 17, 258, 600])] + rng.randbytes(37))
     data = b''.join(parts)
     calls = [data[i:i + 50000] for i in range(0, len(data), 50000)] + [b'']
-    check_vs_zlib({6: [calls], 9: [calls]})
+    check_vs_zlib({6: [calls], 9: [calls], 1: [calls], 3: [calls]})
     z = zlib.compress(data, 9)
     got = inflate_streams([cuts(rng, z, 'random') + [b'']])[0]
     assert b''.join(o for o, _ in got) == data

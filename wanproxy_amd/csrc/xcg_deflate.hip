@@ -63,6 +63,8 @@ constexpr int L_CODES = 286, D_CODES = 30, BL_CODES = 19, HEAP_SIZE = 2 * L_CODE
 constexpr int MAX_BITS = 15;
 constexpr int XPAD = 272;                                  // zeroed bytes after a call's data in X
 constexpr int TAB_WORDS = L_CODES + D_CODES + BL_CODES;    // per block: code | len << 16
+constexpr int DMAX = 264;            // >= MIN_LOOKAHEAD - 1: positions a stopped flush call can leave
+constexpr uint32_t PIPE_CHUNK = 65536;   // DeflatePipe's output buffer (DEFLATE_CHUNK_SIZE, deflate_pipe.cc:34)
 
 // configuration_table (deflate.c): good, lazy, nice, chain
 __constant__ int CFG[10][4] = {{0, 0, 0, 0},        {4, 4, 8, 4},     {4, 5, 16, 8},      {4, 6, 32, 32},
@@ -96,6 +98,14 @@ struct ZState {          // one DeflatePipe's z_stream, reduced to what the outp
   uint64_t base;         // stream position of zlib's window coord 0 (slides by WSIZE)
   uint32_t adler;        // adler32 of everything consumed (the Z_FINISH trailer)
   uint32_t flags;        // 1: header written, 2: finished (Z_STREAM_END)
+  // What a flush call that stopped at a full pipe buffer leaves (see zd_layout_kernel):
+  uint64_t pend;         // bytes produced but not delivered yet (zlib's pending past the buffer)
+  uint64_t block_start;  // stream position of the open block's start
+  uint64_t mstart;       // match_start (stream position)
+  uint32_t dlen;         // positions before `total` not parsed yet (strstart = total - dlen)
+  uint32_t avail, mlen;  // deflate_slow's match_available, match_length at strstart
+  uint32_t cbits, cnb;   // the last incomplete output byte: its cnb < 8 low bits
+  uint32_t pad;
 };
 
 struct ZCall {           // host-built, one per consume()
@@ -104,26 +114,37 @@ struct ZCall {           // host-built, one per consume()
   uint64_t t_off;             // tf / tq / sym: call-relative position 0
   uint32_t len, stream;
   uint32_t blk_off, blk_cap;  // block records
+  uint64_t m_off;             // deflate_fast: the call's hashed-position masks (words; bit j = X index j)
 };
 
 struct ZBlock {
   uint32_t sym_begin, sym_end;
   uint32_t start;        // X index of block_start
   uint32_t stored_len;
-  uint32_t flags;        // 1 storable (block_start not slid out), 2 last
+  uint32_t flags;        // 1 storable (block_start not slid out), 2 last, 4 flushed in the flush call
+                         // (a loop top with lookahead < MIN_LOOKAHEAD, or the call's final flush)
   uint32_t type;         // 0 stored, 1 static, 2 dynamic
   uint32_t lcodes, dcodes, blcodes, pad;
   uint64_t bits;         // Huffman blocks: 3 + trees + symbols + end-of-block
   uint64_t bit_off;      // start of the block in the call's output
+  // the parse state right after this flush (where a stopped flush call resumes)
+  int64_t bidx;          // X index of window coord 0
+  uint32_t p_after, ms;  // X indices: strstart, match_start
+  uint32_t avail, ml;
 };
 
 struct ZCallRes {
-  uint32_t nblocks;
+  uint32_t nblocks;      // blocks emitted (a stopped flush call drops the ones after the stop)
   uint32_t nsym;
   uint64_t base_end;     // stream position of coord 0 after the call
   uint32_t adler;        // adler32 after the call
-  uint32_t out_len;
-  uint64_t end_bit;      // bit offset after the last block
+  uint32_t out_len;      // output bytes the emit may touch (incl. a stop's incomplete last byte)
+  uint64_t end_bit;      // bit offset after the last emitted block
+  uint32_t stop;         // 0 none, else 1 + the block the flush call stopped at
+  uint32_t out_bytes;    // complete new bytes (what the caller appends to the undelivered ones)
+  uint64_t deliver;      // bytes DeflatePipe::consume produces now
+  uint32_t scan_end;     // X index the parse reached (all positions, unless stopped)
+  uint32_t pad;
 };
 
 struct ZArgs {
@@ -142,11 +163,21 @@ struct ZArgs {
   uint32_t* tabs;        // blk index * TAB_WORDS
   ZCallRes* res;
   uint32_t* out_len;     // caller's d_out_len
+  uint64_t* deliver;     // caller's d_deliver
   uint32_t n;                  // calls
   const uint32_t* mstart;      // first 256-position match tile of each call (n + 1, prefix)
   const uint32_t* gstart;      // first 64-position hash group of each call (n + 1, prefix)
   const uint32_t* bstart;      // first block record of each call (n + 1, prefix)
   int level;
+  // deflate_fast (levels 1-3): which positions zlib hashes depends on its parse.
+  // mcur: this round's guess (X index >= strstart; earlier ones from `ring`),
+  // mnext: the positions the round's parse hashes, ring: per stream, bit
+  // (position mod 32768) of the last 32 KiB, changed: per call, mnext != mcur.
+  int fast;
+  uint32_t* mcur;
+  uint32_t* mnext;
+  uint32_t* ring;
+  uint32_t* changed;
 };
 
 // ------------------------------------------------------------------- prep
@@ -266,7 +297,16 @@ __global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, con
   const uint32_t s0 = gstart[c0], split = gstart[c0 + 1];
   const ZCall cA = a.calls[c0];
   const ZCall cB = (split < g0 + HGROUPS && c0 + 1 < n) ? a.calls[c0 + 1] : cA;
-  const int64_t jloA = first_valid(a.st[cA.stream]), jloB = first_valid(a.st[cB.stream]);
+  const ZState sA = a.st[cA.stream], sB = a.st[cB.stream];
+  const int64_t jloA = first_valid(sA), jloB = first_valid(sB);
+  // deflate_fast: is X index j of a call hashed (zlib's INSERT_STRING)?
+  auto hashed = [&](bool B, int32_t j) -> bool {
+    const ZCall& c = B ? cB : cA;
+    const ZState& st = B ? sB : sA;
+    if (j >= WSIZE - (int32_t)st.dlen) return (a.mcur[c.m_off + (uint32_t)(j >> 5)] >> (j & 31)) & 1u;
+    const uint64_t q = st.total - WSIZE + (uint64_t)j;
+    return (a.ring[(uint64_t)c.stream * (WSIZE / 32) + ((q & (WSIZE - 1)) >> 5)] >> (q & 31)) & 1u;
+  };
   // per group (wave-uniform): the call's X base, the group's first position, the call's end
   auto group = [&](uint32_t k, const uint8_t*& x, int32_t& g, int32_t& jend) {
     const uint32_t gid = g0 + k;
@@ -291,7 +331,8 @@ __global__ __launch_bounds__(256) void zd_hashes_kernel(ZArgs a, uint32_t n, con
     int32_t g, jend;
     group(k, x, g, jend);
     const int32_t j = g + lane;
-    const bool valid = j + 2 < jend;
+    bool valid = j + 2 < jend;
+    if (a.fast && valid) valid = hashed(g0 + k >= split, j);   // a position zlib never hashes: no link, not a head
     uint32_t h = 0x8000u;    // invalid lanes form their own class
     if (valid) h = (((w[k] & 0xff) << 10) ^ (((w[k] >> 8) & 0xff) << 5) ^ ((w[k] >> 16) & 0xff)) & 0x7fffu;
     uint64_t m = ballot(valid);
@@ -388,12 +429,16 @@ __global__ __launch_bounds__(64) void zd_chain_kernel(ZArgs a) {
 // Entry: M (9 bits) | distance of the first candidate reaching M (15 bits) << 9
 // | ELIG << 31 (chain head exists, within MAX_DIST, lookahead >= 3).  The scan
 // also rejects a head at zlib's window coord 0 (NIL).
+// Entries are indexed t = X index - WSIZE + DMAX: positions a stopped flush
+// call left (the last s.dlen before the call's bytes) are parsed again now,
+// with this call's bytes as their lookahead.
 __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
   const uint32_t ci = call_of(a.mstart, a.n, blockIdx.x);
   const ZCall c = a.calls[ci];
-  const uint32_t rel = (blockIdx.x - a.mstart[ci]) * 256u + threadIdx.x;
-  if (rel >= c.len) return;
+  const uint32_t t = (blockIdx.x - a.mstart[ci]) * 256u + threadIdx.x;
   const ZState s = a.st[c.stream];
+  if (t < (uint32_t)DMAX - s.dlen || t >= (uint32_t)DMAX + c.len) return;
+  const int64_t rel = (int64_t)t - DMAX;
   const uint8_t* X = a.X + c.x_off;
   const uint16_t* d16 = a.d16 + c.x_off;
   const int64_t j = (int64_t)WSIZE + rel;
@@ -450,8 +495,8 @@ __global__ __launch_bounds__(256) void zd_match_kernel(ZArgs a) {
     ef = 0x80000000u | (uint32_t)best | (best ? (uint32_t)(j - bs) << 9 : 0);
     eq = 0x80000000u | (uint32_t)bq | (bq ? (uint32_t)(j - bsq) << 9 : 0);
   }
-  a.tf[c.t_off + rel] = ef;
-  a.tq[c.t_off + rel] = eq;
+  a.tf[c.t_off + t] = ef;
+  a.tq[c.t_off + t] = eq;
 }
 
 #ifdef XCG_ZD_TIMING
@@ -477,15 +522,15 @@ struct ScanWin {
   uint32_t d;
 };
 
-__device__ __forceinline__ void load_win(ScanWin& W, const ZArgs& a, const ZCall& c, int64_t w) {
+__device__ __forceinline__ void load_win(ScanWin& W, const ZArgs& a, const ZCall& c, int64_t w, int64_t p0) {
   const int lane = threadIdx.x;
   int64_t rel = w - WSIZE + lane;
   W.tf = 0;
   W.tq = 0;
   W.d = 0;
-  if (rel >= 0 && rel < (int64_t)c.len) {
-    W.tf = a.tf[c.t_off + rel];
-    W.tq = a.tq[c.t_off + rel];
+  if (w + lane >= p0 && rel < (int64_t)c.len) {
+    W.tf = a.tf[c.t_off + rel + DMAX];
+    W.tq = a.tq[c.t_off + rel + DMAX];
     W.d = a.d16[c.x_off + w + lane];
   }
   W.x = (rel - 1 < (int64_t)c.len) ? a.X[c.x_off + w - 1 + lane] : 0;
@@ -501,34 +546,45 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
   uint32_t* sym = a.sym + c.t_off;
   ZBlock* blk = a.blk + c.blk_off;
   const bool finish = c.len == 0;
-  // positions are X indices; bidx = X index of zlib's window coord 0
+  // positions are X indices; bidx = X index of zlib's window coord 0.  The
+  // parse resumes where the last call's left it (strstart = total - dlen, with
+  // its lazy-match state); data was read up to `total`.
   int64_t bidx = (int64_t)s.base - (int64_t)s.total + WSIZE;
   const int64_t end = (int64_t)WSIZE + c.len;
-  int64_t p = WSIZE, rd = WSIZE;
+  const int64_t p0 = (int64_t)WSIZE - s.dlen;
+  int64_t p = p0, rd = WSIZE;
   uint32_t nsym = 0, symbase = 0, nblk = 0;
-  int64_t block_start = p;
-  int ml = MIN_MATCH - 1, avail = 0;
-  int64_t ms = 0;
+  int64_t block_start = (int64_t)s.block_start - (int64_t)s.total + WSIZE;
+  int ml = (int)s.mlen, avail = (int)s.avail;
+  int64_t ms = (int64_t)s.mstart - (int64_t)s.total + WSIZE;
   ScanWin W, N;   // entries of [w, w + 64) and, loaded ahead, [w + 64, w + 128)
   int64_t w = p;
-  load_win(W, a, c, w);
-  load_win(N, a, c, w + 64);
+  load_win(W, a, c, w, p0);
+  load_win(N, a, c, w + 64, p0);
 #ifdef XCG_ZD_TIMING
   uint64_t n_fast = 0, n_slow = 0, n_fastpos = 0, t_scan = ZD_NOW();
 #endif
 
-  auto flush = [&](int64_t q, bool last) {
+  // FLUSH_BLOCK at strstart q; `tail`: inside the flush call (loop-top
+  // lookahead < MIN_LOOKAHEAD, or the final flush); the parse then stands at
+  // (pa, va, mla) -- where a consume that stops at this flush resumes
+  auto flush = [&](int64_t q, bool last, bool tail, int64_t pa, int va, int mla) {
     if (lane == 0) {
       ZBlock b;
       b.sym_begin = symbase;
       b.sym_end = symbase + nsym;
       b.start = (uint32_t)block_start;
       b.stored_len = (uint32_t)(q - block_start);
-      b.flags = (block_start >= bidx ? 1u : 0u) | (last ? 2u : 0u);
+      b.flags = (block_start >= bidx ? 1u : 0u) | (last ? 2u : 0u) | (tail ? 4u : 0u);
       b.type = 0;
       b.lcodes = b.dcodes = b.blcodes = b.pad = 0;
       b.bits = 0;
       b.bit_off = 0;
+      b.bidx = bidx;
+      b.p_after = (uint32_t)pa;
+      b.ms = (uint32_t)ms;
+      b.avail = (uint32_t)va;
+      b.ml = (uint32_t)mla;
       blk[nblk] = b;
     }
     nblk++;
@@ -574,9 +630,9 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
         w += 64;
       } else {
         w = p;
-        load_win(W, a, c, w);
+        load_win(W, a, c, w, p0);
       }
-      load_win(N, a, c, w + 64);
+      load_win(N, a, c, w + 64, p0);
     }
     const int li = (int)(p - w);
     if (avail && ml == MIN_MATCH - 1) {
@@ -602,7 +658,7 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
           n_fast++;
           n_fastpos += (uint64_t)k;
 #endif
-          if (nsym == SYMS_PER_BLOCK) flush(p - 1, false);
+          if (nsym == SYMS_PER_BLOCK) flush(p - 1, false, false, p, 1, MIN_MATCH - 1);
           continue;
         }
       }
@@ -633,10 +689,10 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
       p += prev_length - 1;
       avail = 0;
       ml = MIN_MATCH - 1;
-      if (nsym == SYMS_PER_BLOCK) flush(p, false);
+      if (nsym == SYMS_PER_BLOCK) flush(p, false, la < MIN_LOOKAHEAD, p, 0, MIN_MATCH - 1);
     } else if (avail) {
       put(readlane(W.x, li));
-      if (nsym == SYMS_PER_BLOCK) flush(p, false);
+      if (nsym == SYMS_PER_BLOCK) flush(p, false, la < MIN_LOOKAHEAD, p + 1, 1, ml);
       p++;
     } else {
       avail = 1;
@@ -654,14 +710,229 @@ __global__ __launch_bounds__(64) void zd_scan_kernel(ZArgs a) {
     atomicAdd(&g_zd_t[12], 1ull);
   }
 #endif
-  if (finish) flush(p, true);
-  else if (nsym) flush(p, false);
+  if (finish) flush(p, true, true, p, 0, MIN_MATCH - 1);
+  else if (nsym) flush(p, false, true, p, 0, MIN_MATCH - 1);
   if (lane == 0) {
     ZCallRes r = a.res[ci];
     r.nblocks = nblk;
     r.nsym = symbase;
     r.base_end = (uint64_t)((int64_t)s.total - WSIZE + bidx);
+    r.scan_end = (uint32_t)p;
     a.res[ci] = r;
+  }
+}
+
+// ------------------------------------------------------------------- deflate_fast
+// deflate_fast (deflate.c, levels 1-3) over the match table built from this
+// round's hashed-position guess (ZArgs::mcur); one wave per call.  zlib hashes
+// every loop top with >= MIN_MATCH bytes of lookahead and the inside of a match
+// only when it is at most max_lazy (= max_insert_length) long and leaves >=
+// MIN_MATCH bytes of lookahead; the positions this parse hashes go to mnext.
+// When mnext == mcur the table was zlib's (by induction over positions: a
+// loop top's chain holds exactly the positions hashed before it) and so is
+// the parse.
+__device__ __forceinline__ void mark_range(uint32_t* mk, int64_t lo, int64_t hi, int lane) {
+  if (hi <= lo) return;
+  const int64_t w0 = lo >> 5, w1 = (hi - 1) >> 5;
+  for (int64_t wd = w0 + lane; wd <= w1; wd += 64) {
+    const int64_t b0 = wd * 32, a0 = lo > b0 ? lo - b0 : 0, a1 = hi < b0 + 32 ? hi - b0 : 32;
+    const uint32_t m = (a1 - a0 == 32) ? ~0u : (((1u << (a1 - a0)) - 1u) << a0);
+    atomicOr(mk + wd, m);
+  }
+}
+
+__global__ __launch_bounds__(64) void zd_fscan_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.x;
+  const ZCall c = a.calls[ci];
+  const ZState s = a.st[c.stream];
+  const int lane = threadIdx.x;
+  const int max_insert = CFG[a.level][1];
+  uint32_t* sym = a.sym + c.t_off;
+  ZBlock* blk = a.blk + c.blk_off;
+  uint32_t* mk = a.mnext + c.m_off;
+  const bool finish = c.len == 0;
+  int64_t bidx = (int64_t)s.base - (int64_t)s.total + WSIZE;
+  const int64_t end = (int64_t)WSIZE + c.len;
+  const int64_t p0 = (int64_t)WSIZE - s.dlen;
+  int64_t p = p0, rd = WSIZE;
+  uint32_t nsym = 0, symbase = 0, nblk = 0;
+  int64_t block_start = (int64_t)s.block_start - (int64_t)s.total + WSIZE;
+  ScanWin W, N;
+  int64_t w = p;
+  load_win(W, a, c, w, p0);
+  load_win(N, a, c, w + 64, p0);
+  auto flush = [&](int64_t q, bool last, bool tail) {   // FLUSH_BLOCK at strstart q (after its symbol)
+    if (lane == 0) {
+      ZBlock b;
+      b.sym_begin = symbase;
+      b.sym_end = symbase + nsym;
+      b.start = (uint32_t)block_start;
+      b.stored_len = (uint32_t)(q - block_start);
+      b.flags = (block_start >= bidx ? 1u : 0u) | (last ? 2u : 0u) | (tail ? 4u : 0u);
+      b.type = 0;
+      b.lcodes = b.dcodes = b.blcodes = b.pad = 0;
+      b.bits = 0;
+      b.bit_off = 0;
+      b.bidx = bidx;
+      b.p_after = (uint32_t)q;
+      b.ms = 0;
+      b.avail = 0;
+      b.ml = MIN_MATCH - 1;
+      blk[nblk] = b;
+    }
+    nblk++;
+    symbase += nsym;
+    nsym = 0;
+    block_start = q;
+  };
+  __shared__ uint32_t sbuf[2048 + 64];
+  uint32_t sb_n = 0, sb_base = 0;
+  auto sflush = [&]() {
+    for (uint32_t i = lane; i < sb_n; i += 64) sym[sb_base + i] = sbuf[i];
+    sb_base += sb_n;
+    sb_n = 0;
+  };
+  auto put = [&](uint32_t v) {
+    if (lane == 0) sbuf[sb_n] = v;
+    sb_n++;
+    nsym++;
+    if (sb_n >= 2048) sflush();
+  };
+  for (;;) {
+    if (rd - p < MIN_LOOKAHEAD) {   // fill_window: slide, then read what fits
+      do {
+        int64_t more = WINSZ - (rd - bidx);
+        if (p - bidx >= WSIZE + MAX_DIST) {
+          bidx += WSIZE;
+          more += WSIZE;
+        }
+        if (rd == end) break;
+        int64_t nrd = end - rd;
+        if (nrd > more) nrd = more;
+        rd += nrd;
+      } while (rd - p < MIN_LOOKAHEAD && rd < end);
+      if (rd == p) break;
+    }
+    if (p >= w + 64) {
+      if (p < w + 128) {
+        W = N;
+        w += 64;
+      } else {
+        w = p;
+        load_win(W, a, c, w, p0);
+      }
+      load_win(N, a, c, w + 64, p0);
+    }
+    const int li = (int)(p - w);
+    // X[w + lane] (W.x holds X[w - 1 + lane])
+    uint32_t xs = __shfl(W.x, (lane + 1) & 63);
+    const uint32_t nx0 = readlane(N.x, 0);
+    if (lane == 63) xs = nx0;
+    {
+      // literal run: loop tops where no match starts (all hashed, lookahead >= MIN_LOOKAHEAD)
+      int64_t lim = w + 64;
+      if (rd - (MIN_LOOKAHEAD - 1) < lim) lim = rd - (MIN_LOOKAHEAD - 1);
+      const int64_t room = SYMS_PER_BLOCK - nsym;
+      if (p + room < lim) lim = p + room;
+      if (lim > p) {
+        const int64_t pos = w + lane;
+        const bool elig = (W.tf >> 31) && pos - (int64_t)W.d != bidx && (W.tf & 511u) >= MIN_MATCH;
+        const uint64_t m = ballot(elig && pos >= p && pos < lim);
+        const int64_t stop = m ? w + (int64_t)__builtin_ctzll(m) : lim;
+        const int64_t k = stop - p;
+        if (k > 0) {
+          if (lane >= li && lane < li + k) sbuf[sb_n + (lane - li)] = xs;
+          sb_n += (uint32_t)k;
+          nsym += (uint32_t)k;
+          if (sb_n >= 2048) sflush();
+          mark_range(mk, p, stop, lane);
+          p = stop;
+          if (nsym == SYMS_PER_BLOCK) flush(p, false, false);
+          continue;
+        }
+      }
+    }
+    // one loop top of deflate_fast at p
+    const uint32_t ef = readlane(W.tf, li), dd = readlane(W.d, li);
+    const int64_t la = rd - p;
+    if (la >= MIN_MATCH && lane == 0) atomicOr(mk + (p >> 5), 1u << (p & 31));   // INSERT_STRING
+    const bool head_ok = la >= MIN_MATCH && (ef >> 31) && (p - (int64_t)dd != bidx);
+    const int ml = head_ok ? (int)(ef & 511u) : 0;
+    if (ml >= MIN_MATCH) {
+      put((uint32_t)(ml - MIN_MATCH) | (((ef >> 9) & 0x7fffu) << 8));
+      if (ml <= max_insert && la - ml >= MIN_MATCH) mark_range(mk, p + 1, p + ml, lane);
+      p += ml;
+    } else {
+      put(readlane(xs, li));
+      p++;
+    }
+    if (nsym == SYMS_PER_BLOCK) flush(p, false, la < MIN_LOOKAHEAD);
+  }
+  sflush();
+  // s->insert = min(strstart, MIN_MATCH - 1): the last positions are hashed once their bytes exist
+  const int64_t ins = p - bidx < MIN_MATCH - 1 ? p - bidx : MIN_MATCH - 1;
+  mark_range(mk, p - ins, p, lane);
+  if (finish) flush(p, true, true);
+  else if (nsym) flush(p, false, true);
+  if (lane == 0) {
+    ZCallRes r = a.res[ci];
+    r.nblocks = nblk;
+    r.nsym = symbase;
+    r.base_end = (uint64_t)((int64_t)s.total - WSIZE + bidx);
+    r.scan_end = (uint32_t)p;
+    a.res[ci] = r;
+  }
+}
+
+// mnext == mcur over the positions the call parses? (changed[ci] = 1 if not)
+__global__ __launch_bounds__(256) void zd_mcmp_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.x;
+  const ZCall c = a.calls[ci];
+  const ZState s = a.st[c.stream];
+  const int64_t lo = (int64_t)WSIZE - s.dlen, hi = (int64_t)WSIZE + c.len;
+  bool diff = false;
+  for (int64_t wd = (lo >> 5) + threadIdx.x; wd <= ((hi - 1) >> 5); wd += 256) {
+    const int64_t b0 = wd * 32, a0 = lo > b0 ? lo - b0 : 0, a1 = hi < b0 + 32 ? hi - b0 : 32;
+    const uint32_t m = (a1 - a0 == 32) ? ~0u : (((1u << (a1 - a0)) - 1u) << a0);
+    if ((a.mcur[c.m_off + wd] ^ a.mnext[c.m_off + wd]) & m) diff = true;
+  }
+  if (__syncthreads_or(diff) && threadIdx.x == 0) a.changed[ci] = 1u;
+}
+
+// Round 0's guess: every position hashed.  Also clears mnext.
+__global__ __launch_bounds__(256) void zd_mfill_kernel(uint32_t* m, uint32_t* mn, uint64_t words) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256) {
+    m[i] = ~0u;
+    mn[i] = 0u;
+  }
+}
+__global__ __launch_bounds__(256) void zd_mzero_kernel(uint32_t* m, uint64_t words) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256) m[i] = 0u;
+}
+
+// The stream's ring of hashed positions after the call: bit (q mod 32768) for
+// the last 32 KiB; positions from strstart on come from the final mask.
+__global__ __launch_bounds__(256) void zd_ring_kernel(ZArgs a) {
+  const uint32_t ci = blockIdx.x;
+  const ZCall c = a.calls[ci];
+  const ZState s = a.st[c.stream];
+  const uint64_t hi = s.total + c.len, p0 = s.total - s.dlen;
+  const uint64_t lo = hi > (uint64_t)WSIZE ? hi - WSIZE : 0;
+  const uint64_t from = p0 > lo ? p0 : lo;
+  uint32_t* ring = a.ring + (uint64_t)c.stream * (WSIZE / 32);
+  const uint32_t* mk = a.mcur + c.m_off;
+  for (uint32_t r = threadIdx.x; r < (uint32_t)WSIZE / 32; r += 256) {
+    uint32_t v = ring[r];
+    for (int b = 0; b < 32; b++) {
+      const uint64_t slot = (uint64_t)r * 32 + b;
+      if (hi < (uint64_t)WSIZE && slot >= hi) continue;   // (no such position yet)
+      const uint64_t q = hi - WSIZE + ((slot - hi) & (WSIZE - 1));   // the position in [hi - 32768, hi) on this slot
+      if (q < from) continue;
+      const uint64_t j = q - (s.total - WSIZE);
+      const uint32_t bit = (mk[j >> 5] >> (j & 31)) & 1u;
+      v = (v & ~(1u << b)) | (bit << b);
+    }
+    ring[r] = v;
   }
 }
 
@@ -963,7 +1234,19 @@ __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
 }
 
 // ------------------------------------------------------------------- layout
-// One wave per call: block bit offsets, the call's length, zeroed output.
+// One wave per call: block bit offsets, the call's length, zeroed output, and
+// where DeflatePipe::consume (zlib/deflate_pipe.cc:57-115) stops.  Output
+// reaches the pipe at every block flush (flush_pending: the complete bytes).
+// Under Z_NO_FLUSH the pipe takes all of it, emptying its 64 KiB buffer as it
+// fills, so the one deflate(Z_SYNC_FLUSH) call starts with n mod 65536 bytes
+// in the buffer (n = the bytes the consume took so far, the ones zlib still
+// held from the last consume included) and returns at the first block flush
+// that leaves the buffer full (FLUSH_BLOCK's need_more): the consume produces
+// up to L = 65536 * (n / 65536 + 1), the rest stays pending, no sync marker
+// is written, and positions after that flush are parsed with the next
+// consume's bytes.  Otherwise the marker follows and the consume produces
+// min(all, L).  Bits of an incomplete last byte carry into the next call
+// (the call's output starts with them).
 __global__ __launch_bounds__(64) void zd_layout_kernel(ZArgs a) {
   const uint32_t ci = blockIdx.x;
   const ZCall c = a.calls[ci];
@@ -971,9 +1254,12 @@ __global__ __launch_bounds__(64) void zd_layout_kernel(ZArgs a) {
   const int lane = threadIdx.x;
   __shared__ uint32_t total_bytes;
   if (lane == 0) {
-    uint64_t off = (s.flags & 1) ? 0 : 16;   // zlib header on the first call
-    uint32_t nb = a.res[ci].nblocks;
+    uint64_t off = (s.flags & 1) ? s.cnb : 16;   // carried bits, or the zlib header on the first call
+    const uint32_t nb = a.res[ci].nblocks;
+    const bool finish = c.len == 0;
     bool last = false;
+    uint32_t stop = 0, nemit = nb;
+    uint64_t n = s.pend;                          // bytes the consume took before its flush call
     for (uint32_t k = 0; k < nb; k++) {
       ZBlock* B = a.blk + c.blk_off + k;
       B->bit_off = off;
@@ -983,19 +1269,38 @@ __global__ __launch_bounds__(64) void zd_layout_kernel(ZArgs a) {
         off = (off + 7) & ~7ull;   // bi_windup after the last block
         last = true;
       }
+      if (finish) continue;
+      const uint64_t avail = s.pend + (off >> 3);
+      if (!(B->flags & 4)) {
+        n = avail;
+      } else if (avail >= (uint64_t)PIPE_CHUNK * (n / PIPE_CHUNK + 1)) {
+        stop = k + 1;
+        nemit = k + 1;
+        break;
+      }
     }
-    a.res[ci].end_bit = off;
-    uint64_t bytes;
-    if (last) bytes = off / 8 + 4;                      // adler32 trailer
-    else bytes = ((off + 3 + 7) >> 3) + 4;              // Z_SYNC_FLUSH: empty stored block
-    total_bytes = (uint32_t)bytes;
-    a.res[ci].out_len = (uint32_t)bytes;
+    ZCallRes& r = a.res[ci];
+    r.end_bit = off;
+    r.nblocks = nemit;
+    r.stop = stop;
+    uint64_t bytes, room;
+    if (last) bytes = room = off / 8 + 4;                           // adler32 trailer
+    else if (stop) { bytes = off >> 3; room = (off + 7) >> 3; }     // no marker; the partial byte carries
+    else bytes = room = ((off + 3 + 7) >> 3) + 4;                   // Z_SYNC_FLUSH: empty stored block
+    const uint64_t lim = (uint64_t)PIPE_CHUNK * (n / PIPE_CHUNK + 1), all = s.pend + bytes;
+    r.deliver = finish ? all : (all < lim ? all : lim);
+    r.out_bytes = (uint32_t)bytes;
+    total_bytes = (uint32_t)room;
+    r.out_len = (uint32_t)room;
     a.out_len[ci] = (uint32_t)bytes;
+    a.deliver[ci] = r.deliver;
   }
   __syncthreads();
   uint32_t* o = (uint32_t*)(a.out + c.out_off);
   uint32_t words = (total_bytes + 3) / 4;
   for (uint32_t i = lane; i < words; i += 64) o[i] = 0;
+  __syncthreads();
+  if (lane == 0 && (s.flags & 1) && s.cnb) o[0] |= s.cbits;   // (the header call starts byte-aligned)
 }
 
 // ------------------------------------------------------------------- emit
@@ -1263,7 +1568,7 @@ __global__ __launch_bounds__(64) void zd_emit_kernel(ZArgs a) {
 #ifdef XCG_ZD_TIMING
   if (lane == 0) atomicAdd(&g_zd_t[15], 1ull);
 #endif
-  if (k == r.nblocks - 1 && lane == 0) {
+  if (k == r.nblocks - 1 && lane == 0 && !r.stop) {
     if (last) {   // Z_FINISH: adler32 trailer, big-endian (putShortMSB x2)
       uint64_t b = r.end_bit >> 3;
       uint32_t ad = s.adler;
@@ -1293,9 +1598,31 @@ __global__ __launch_bounds__(256) void zd_commit_kernel(ZArgs a) {
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     ZState s = a.st[c.stream];
+    const ZCallRes& r = a.res[ci];
+    const int64_t x2s = (int64_t)s.total - WSIZE;   // X index -> stream position
+    if (r.stop) {   // resume right after the block the flush call stopped at
+      const ZBlock& B = a.blk[c.blk_off + r.stop - 1];
+      s.base = (uint64_t)(x2s + B.bidx);
+      s.dlen = (uint32_t)((int64_t)WSIZE + c.len - (int64_t)B.p_after);
+      s.block_start = (uint64_t)(x2s + (int64_t)B.start + B.stored_len);
+      s.mstart = (uint64_t)(x2s + (int64_t)B.ms);
+      s.avail = B.avail;
+      s.mlen = B.ml;
+      const uint64_t e = r.end_bit;
+      s.cnb = (uint32_t)(e & 7);
+      s.cbits = s.cnb ? a.out[c.out_off + (e >> 3)] & ((1u << s.cnb) - 1u) : 0u;
+    } else {
+      s.base = r.base_end;
+      s.dlen = 0;
+      s.block_start = (uint64_t)((int64_t)s.total + c.len);
+      s.avail = 0;
+      s.mlen = MIN_MATCH - 1;
+      s.cnb = 0;
+      s.cbits = 0;
+    }
+    s.pend = s.pend + r.out_bytes - r.deliver;
     s.total += c.len;
-    s.base = a.res[ci].base_end;
-    s.adler = c.len ? a.res[ci].adler : s.adler;
+    s.adler = c.len ? r.adler : s.adler;
     s.flags |= 1u;
     if (c.len == 0) s.flags |= 2u;
     a.st[c.stream] = s;
@@ -1321,6 +1648,10 @@ struct xcg_zdeflate {
   void* h_meta = nullptr;     // pinned staging for meta
   size_t h_meta_cap = 0;
   hipEvent_t done = nullptr;
+  uint32_t* ring = nullptr;   // deflate_fast: per stream, the hashed positions of the last 32 KiB
+  uint32_t* h_changed = nullptr;   // pinned, per call (deflate_fast rounds)
+  size_t h_changed_cap = 0;
+  uint32_t last_rounds = 0;
 };
 
 namespace {
@@ -1342,25 +1673,34 @@ int grow(void** p, size_t* cap, size_t want, bool pinned) {
   return XCG_OK;
 }
 inline size_t al(size_t v, size_t a) { return (v + a - 1) / a * a; }
+ZState fresh_state() {   // deflateInit
+  ZState s;
+  memset(&s, 0, sizeof s);
+  s.adler = 1u;
+  s.mlen = MIN_MATCH - 1;
+  return s;
+}
 }  // namespace
 
 extern "C" {
 
-uint64_t xcg_zdeflate_bound(uint32_t len) { return (uint64_t)len + (len >> 1) + 128; }
+uint64_t xcg_zdeflate_bound(uint32_t len) { return (uint64_t)len + (len >> 1) + 2 * DMAX + 128; }
 
 int xcg_zdeflate_create(int device, int level, uint32_t nstreams, xcg_zdeflate** out) {
-  if (!out || level < 4 || level > 9 || nstreams == 0) return level >= 0 && level < 4 ? XCG_ENOTSUP : XCG_EINVAL;
+  if (!out || level < 1 || level > 9 || nstreams == 0) return level == 0 ? XCG_ENOTSUP : XCG_EINVAL;
   if (hipSetDevice(device) != hipSuccess) return XCG_EHIP;
   xcg_zdeflate* z = new xcg_zdeflate();
   z->device = device;
   z->level = level;
   z->nstreams = nstreams;
   if (hipMalloc(&z->st, sizeof(ZState) * nstreams) != hipSuccess ||
-      hipMalloc(&z->hist, (size_t)WSIZE * nstreams) != hipSuccess || hipEventCreateWithFlags(&z->done, hipEventDisableTiming) != hipSuccess) {
+      hipMalloc(&z->hist, (size_t)WSIZE * nstreams) != hipSuccess || hipEventCreateWithFlags(&z->done, hipEventDisableTiming) != hipSuccess ||
+      (level < 4 && (hipMalloc(&z->ring, (size_t)WSIZE / 8 * nstreams) != hipSuccess ||
+                     hipMemset(z->ring, 0, (size_t)WSIZE / 8 * nstreams) != hipSuccess))) {
     delete z;
     return XCG_ENOMEM;
   }
-  z->h_init.assign(nstreams, ZState{0, 0, 1u, 0u});
+  z->h_init.assign(nstreams, fresh_state());
   if (hipMemcpy(z->st, z->h_init.data(), sizeof(ZState) * nstreams, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(z->hist, 0, (size_t)WSIZE * nstreams) != hipSuccess) {
     delete z;
@@ -1376,6 +1716,8 @@ void xcg_zdeflate_destroy(xcg_zdeflate* z) {
   if (z->done) (void)hipEventSynchronize(z->done);
   (void)hipFree(z->st);
   (void)hipFree(z->hist);
+  (void)hipFree(z->ring);
+  if (z->h_changed) (void)hipHostFree(z->h_changed);
   (void)hipFree(z->scratch);
   (void)hipFree(z->meta);
   if (z->h_meta) (void)hipHostFree(z->h_meta);
@@ -1387,23 +1729,26 @@ int xcg_zdeflate_reset(xcg_zdeflate* z, uint32_t stream) {
   if (!z || stream >= z->nstreams) return XCG_EINVAL;
   (void)hipSetDevice(z->device);
   if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
-  ZState s0{0, 0, 1u, 0u};
+  const ZState s0 = fresh_state();
   if (hipMemcpy(z->st + stream, &s0, sizeof s0, hipMemcpyHostToDevice) != hipSuccess) return XCG_EHIP;
+  if (z->ring && hipMemset(z->ring + (size_t)stream * (WSIZE / 32), 0, WSIZE / 8) != hipSuccess) return XCG_EHIP;
   return XCG_OK;
 }
 
 int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
                        const uint32_t* h_stream, uint32_t n, uint8_t* d_out, const uint64_t* h_out_off,
-                       uint32_t* d_out_len, void* stream) {
-  if (!z || n == 0 || !h_in_off || !h_len || !h_stream || !h_out_off || !d_out || !d_out_len) return XCG_EINVAL;
+                       uint32_t* d_out_len, uint64_t* d_deliver, void* stream) {
+  if (!z || n == 0 || !h_in_off || !h_len || !h_stream || !h_out_off || !d_out || !d_out_len || !d_deliver)
+    return XCG_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   (void)hipSetDevice(z->device);
   // host plan: scratch offsets, tiles, block maps
   std::vector<ZCall> calls(n);
   std::vector<uint32_t> mstart(n + 1), gstart(n + 1), bstart(n + 1);
   std::vector<uint8_t> seen(z->nstreams, 0);
-  size_t xo = 0, to = 0;
+  size_t xo = 0, to = 0, mo = 0;
   uint32_t bo = 0;
+  const bool fast = z->level < 4;
   for (uint32_t i = 0; i < n; i++) {
     if (h_stream[i] >= z->nstreams || seen[h_stream[i]] || (h_out_off[i] & 3) || h_len[i] > (1u << 24))
       return XCG_EINVAL;
@@ -1415,13 +1760,15 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
     c.stream = h_stream[i];
     c.x_off = xo;
     xo += al((size_t)WSIZE + c.len + XPAD, 256);
-    c.t_off = to;
-    to += al((size_t)c.len + 1, 64);
+    c.m_off = mo;                                 // (deflate_fast masks: one bit per X index)
+    mo += fast ? al(((size_t)WSIZE + c.len + 64) / 32 + 1, 64) : 0;
+    c.t_off = to;                                 // (parsed positions: up to DMAX left by the last call)
+    to += al((size_t)c.len + DMAX + 1, 64);
     c.blk_off = bo;
-    c.blk_cap = c.len / SYMS_PER_BLOCK + 2;
+    c.blk_cap = (c.len + DMAX) / SYMS_PER_BLOCK + 2;
     bstart[i] = bo;
     bo += c.blk_cap;
-    mstart[i + 1] = mstart[i] + (c.len + 255) / 256;
+    mstart[i + 1] = mstart[i] + (c.len + DMAX + 255) / 256;
     gstart[i + 1] = gstart[i] + ((uint32_t)WSIZE + c.len + 63) / 64 + 1;
   }
   bstart[n] = bo;
@@ -1431,7 +1778,8 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
          o_tq = al(o_tf + 4 * to, 256),
          o_sym = al(o_tq + 4 * to, 256), o_blk = al(o_sym + 4 * to, 256),
          o_tab = al(o_blk + sizeof(ZBlock) * bo, 256), o_res = al(o_tab + 4ull * TAB_WORDS * bo, 256),
-         o_end = al(o_res + sizeof(ZCallRes) * n, 256);
+         o_ma = al(o_res + sizeof(ZCallRes) * n, 256), o_mb = al(o_ma + 4 * mo, 256), o_chg = al(o_mb + 4 * mo, 256),
+         o_end = al(o_chg + 4ull * n, 256);
   // the previous batch may still read the scratch
   if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
   if (grow((void**)&z->scratch, &z->scratch_cap, o_end, false)) return XCG_ENOMEM;
@@ -1461,24 +1809,64 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.tabs = (uint32_t*)(z->scratch + o_tab);
   a.res = (ZCallRes*)(z->scratch + o_res);
   a.out_len = d_out_len;
+  a.deliver = d_deliver;
   a.n = n;
   a.mstart = (const uint32_t*)(dm + m_ms);
   a.gstart = (const uint32_t*)(dm + m_gs);
   a.bstart = (const uint32_t*)(dm + m_bs);
   a.level = z->level;
+  a.fast = fast ? 1 : 0;
+  uint32_t* mA = (uint32_t*)(z->scratch + o_ma);
+  uint32_t* mB = (uint32_t*)(z->scratch + o_mb);
+  a.mcur = mA;
+  a.mnext = mB;
+  a.ring = z->ring;
+  a.changed = (uint32_t*)(z->scratch + o_chg);
   uint32_t maxlen = 0;
   for (uint32_t i = 0; i < n; i++) maxlen = std::max(maxlen, h_len[i]);
   uint32_t prep_tiles = std::min<uint32_t>(64, ((uint32_t)WSIZE + maxlen + XPAD + 4095) / 4096);
   hipLaunchKernelGGL(zd_prep_kernel, dim3(prep_tiles, n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(zd_hashes_kernel, dim3((groups + 4 * HGROUPS - 1) / (4 * HGROUPS)), dim3(256), 0, st, a, n,
-                     a.gstart);
-  hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
-  if (mtiles) hipLaunchKernelGGL(zd_match_kernel, dim3(mtiles), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(zd_scan_kernel, dim3(n), dim3(64), 0, st, a);
+  const unsigned hgrid = (groups + 4 * HGROUPS - 1) / (4 * HGROUPS);
+  if (!fast) {
+    hipLaunchKernelGGL(zd_hashes_kernel, dim3(hgrid), dim3(256), 0, st, a, n, a.gstart);
+    hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
+    if (mtiles) hipLaunchKernelGGL(zd_match_kernel, dim3(mtiles), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(zd_scan_kernel, dim3(n), dim3(64), 0, st, a);
+  } else {
+    // deflate_fast: which positions zlib hashes depends on its own parse.  Guess
+    // (round 0: all), build the chains and the match table from the guess, parse,
+    // and repeat with the parse's hashed positions until they reproduce the guess
+    // (the correct prefix grows every round, so this ends).
+    if (grow((void**)&z->h_changed, &z->h_changed_cap, 4ull * n, true)) return XCG_ENOMEM;
+    const unsigned mgrid = (unsigned)std::min<size_t>(4096, (mo + 255) / 256 + 1);
+    hipLaunchKernelGGL(zd_mfill_kernel, dim3(mgrid), dim3(256), 0, st, mA, mB, (uint64_t)mo);
+    uint32_t rounds = 0;
+    for (;;) {
+      rounds++;
+      if (hipMemsetAsync(a.changed, 0, 4ull * n, st) != hipSuccess) return XCG_EHIP;
+      hipLaunchKernelGGL(zd_hashes_kernel, dim3(hgrid), dim3(256), 0, st, a, n, a.gstart);
+      hipLaunchKernelGGL(zd_chain_kernel, dim3(n), dim3(64), 0, st, a);
+      if (mtiles) hipLaunchKernelGGL(zd_match_kernel, dim3(mtiles), dim3(256), 0, st, a);
+      hipLaunchKernelGGL(zd_fscan_kernel, dim3(n), dim3(64), 0, st, a);
+      hipLaunchKernelGGL(zd_mcmp_kernel, dim3(n), dim3(256), 0, st, a);
+      if (hipMemcpyAsync(z->h_changed, a.changed, 4ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return XCG_EHIP;
+      bool any = false;
+      for (uint32_t i = 0; i < n && !any; i++) any = z->h_changed[i] != 0;
+      std::swap(a.mcur, a.mnext);   // the parse's positions are the next guess (and, when equal, final)
+      if (!any) break;
+      if (rounds > 100000) return XCG_EOVERFLOW;
+      hipLaunchKernelGGL(zd_mzero_kernel, dim3(mgrid), dim3(256), 0, st, a.mnext,
+                         (uint64_t)mo);
+    }
+    z->last_rounds = rounds;
+  }
   hipLaunchKernelGGL(zd_trees_kernel, dim3((bo + TB - 1) / TB), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_layout_kernel, dim3(n), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a);
+  if (fast) hipLaunchKernelGGL(zd_ring_kernel, dim3(n), dim3(256), 0, st, a);   // (before commit moves the state)
   hipLaunchKernelGGL(zd_commit_kernel, dim3(8, n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
@@ -1490,8 +1878,8 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
 // lengths to h_out_len.  Synchronous.
 int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
                       const uint32_t* h_stream, uint32_t n, uint8_t* h_out, const uint64_t* h_out_off,
-                      uint32_t* h_out_len) {
-  if (!z || n == 0) return XCG_EINVAL;
+                      uint32_t* h_out_len, uint64_t* h_deliver) {
+  if (!z || n == 0 || !h_deliver) return XCG_EINVAL;
   (void)hipSetDevice(z->device);
   uint64_t in_end = 0, out_end = 0;
   std::vector<uint64_t> doff(n);
@@ -1502,20 +1890,23 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
   }
   uint8_t *d_in = nullptr, *d_out = nullptr;
   uint32_t* d_len = nullptr;
+  uint64_t* d_dl = nullptr;
   int rc = XCG_OK;
   if (hipMalloc(&d_in, in_end + 1) != hipSuccess || hipMalloc(&d_out, out_end) != hipSuccess ||
-      hipMalloc(&d_len, 4ull * n) != hipSuccess) {
+      hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_dl, 8ull * n) != hipSuccess) {
     rc = XCG_ENOMEM;
   }
   if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
-  if (!rc) rc = xcg_zdeflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), d_len, nullptr);
+  if (!rc) rc = xcg_zdeflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), d_len, d_dl, nullptr);
   if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
   if (!rc && hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
+  if (!rc && hipMemcpy(h_deliver, d_dl, 8ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
   for (uint32_t i = 0; !rc && i < n; i++)
     if (hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
   (void)hipFree(d_in);
   (void)hipFree(d_out);
   (void)hipFree(d_len);
+  (void)hipFree(d_dl);
   return rc;
 }
 

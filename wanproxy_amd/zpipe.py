@@ -39,9 +39,9 @@ def _lib():
         L.xcg_zdeflate_destroy.restype = None
         L.xcg_zdeflate_reset.argtypes = [vp, C.c_uint32]
         L.xcg_zdeflate_reset.restype = C.c_int
-        L.xcg_zdeflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
+        L.xcg_zdeflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
         L.xcg_zdeflate_batch.restype = C.c_int
-        L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp]
+        L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
         L.xcg_zdeflate_host.restype = C.c_int
         L.xcg_zinflate_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(vp)]
         L.xcg_zinflate_create.restype = C.c_int
@@ -56,7 +56,7 @@ def _lib():
 
 
 def bound(n: int) -> int:
-    return int(n) + (int(n) >> 1) + 128
+    return int(_lib().xcg_zdeflate_bound(int(n)))
 
 
 class DeflatePipes:
@@ -67,6 +67,7 @@ class DeflatePipes:
         self.level, self.nstreams, self.device = level, nstreams, device
         h = C.c_void_p()
         rc = _lib().xcg_zdeflate_create(device, level, nstreams, C.byref(h))
+        self.undelivered = {}           # stream -> bytes the pipe made but has not produced yet
         if rc == XCG_ENOTSUP:
             raise XCGError(f'zlib level {level}: only levels 4-9 (deflate_slow) are implemented')
         _check(rc)
@@ -82,13 +83,16 @@ class DeflatePipes:
 
     def reset(self, stream: int):
         _check(_lib().xcg_zdeflate_reset(self.h, stream))
+        self.undelivered.pop(stream, None)
 
     def pipe(self, stream: int) -> 'DeflatePipe':
         return DeflatePipe(self, stream)
 
-    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, d_out_len, stream=None):
-        """Device-resident batch: d_in / d_out / d_out_len are torch CUDA
-        tensors; in_off / lens / streams / out_off host numpy arrays."""
+    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, d_out_len, d_deliver, stream=None):
+        """Device-resident batch: d_in / d_out / d_out_len (int32) / d_deliver
+        (int64) are torch CUDA tensors; in_off / lens / streams / out_off host
+        numpy arrays.  d_out_len: the new stream bytes at out_off; d_deliver:
+        what the consume produces (the stream's undelivered bytes first)."""
         in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         streams = np.ascontiguousarray(streams, dtype=np.uint32)
@@ -96,7 +100,8 @@ class DeflatePipes:
         n = int(lens.size)
         _check(_lib().xcg_zdeflate_batch(self.h, C.c_void_p(d_in.data_ptr()), in_off.ctypes.data, lens.ctypes.data,
                                          streams.ctypes.data, n, C.c_void_p(d_out.data_ptr()), out_off.ctypes.data,
-                                         C.c_void_p(d_out_len.data_ptr()), _stream_ptr(stream)))
+                                         C.c_void_p(d_out_len.data_ptr()), C.c_void_p(d_deliver.data_ptr()),
+                                         _stream_ptr(stream)))
 
     def consume_many(self, items):
         """items: [(stream, bytes)] (each stream at most once).  Returns the
@@ -117,11 +122,22 @@ class DeflatePipes:
         d_in = torch.frombuffer(bytearray(blob or b'\0'), dtype=torch.uint8).to(dev)
         d_out = torch.empty(int(bounds.sum()), dtype=torch.uint8, device=dev)
         d_len = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.batch_device(d_in, in_off, lens, streams, d_out, out_off, d_len)
+        d_dl = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.batch_device(d_in, in_off, lens, streams, d_out, out_off, d_len, d_dl)
         torch.cuda.synchronize(dev)
         ol = d_len.cpu().numpy().astype(np.uint64)
+        dl = d_dl.cpu().numpy()
         out = d_out.cpu().numpy()
-        return [out[int(out_off[i]):int(out_off[i] + ol[i])].tobytes() for i in range(n)]
+        res = []
+        for i in range(n):
+            st = int(streams[i])
+            q = self.undelivered.get(st, b'') + out[int(out_off[i]):int(out_off[i] + ol[i])].tobytes()
+            k = int(dl[i])
+            if k > len(q):
+                raise XCGError(f'deflate stream {st}: delivers {k} of {len(q)} bytes')
+            res.append(q[:k])
+            self.undelivered[st] = q[k:]
+        return res
 
 
 class DeflatePipe:
