@@ -341,8 +341,8 @@ uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
  * codecN.compressor zlib / compressor_level N, wanproxy.conf:32-41).
  * A context holds `nstreams` DeflatePipe(level) instances
  * (zlib/deflate_pipe.cc:36-50: deflateInit(level), windowBits 15, memLevel 8)
- * in HBM.  Output is bit-exact with zlib 1.2.11 driven by DeflatePipe::consume:
- * levels 4-9 (deflate_slow); levels 0-3 return XCG_ENOTSUP.
+ * in HBM.  Output is bit-exact with zlib 1.2.11 driven by DeflatePipe::consume at
+ * every level: 4-9 deflate_slow, 1-3 deflate_fast, 0 deflate_stored.
  *   xcg_zdeflate_batch: one DeflatePipe::consume() per listed stream (a stream
  *   at most once per batch; successive batches continue the streams):
  *   h_len[i] > 0 bytes at d_in + h_in_off[i] = every segment through
@@ -369,9 +369,20 @@ int xcg_zdeflate_reset(xcg_zdeflate *z, uint32_t stream);
 int xcg_zdeflate_batch(xcg_zdeflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
                        const uint32_t *h_stream, uint32_t n, uint8_t *d_out, const uint64_t *h_out_off,
                        uint32_t *d_out_len, uint64_t *d_deliver, void *stream);
+/* The same with the Buffer's segments: call i's bytes are cut into h_nseg[i]
+ * segments whose lengths follow in h_seg (all calls' lists concatenated).
+ * Level 0's stored blocks follow the segments (deflate_stored copies what
+ * each deflate() call is given); levels 1-9 do not depend on them.
+ * xcg_zdeflate_batch cuts every call into 2048-byte segments (BUFFER_SEGMENT_SIZE,
+ * common/buffer.h:52: a Buffer filled by append). */
+int xcg_zdeflate_batch_seg(xcg_zdeflate *z, const uint8_t *d_in, const uint64_t *h_in_off, const uint32_t *h_len,
+                           const uint32_t *h_stream, uint32_t n, const uint32_t *h_seg, const uint32_t *h_nseg,
+                           uint8_t *d_out, const uint64_t *h_out_off, uint32_t *d_out_len, uint64_t *d_deliver,
+                           void *stream);
+/* Host buffers, synchronous; segments as in xcg_zdeflate_batch_seg (h_seg NULL: 2048-byte cuts). */
 int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
-                      const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
-                      uint32_t *h_out_len, uint64_t *h_deliver);
+                      const uint32_t *h_stream, uint32_t n, const uint32_t *h_seg, const uint32_t *h_nseg,
+                      uint8_t *h_out, const uint64_t *h_out_off, uint32_t *h_out_len, uint64_t *h_deliver);
 
 /* Receiving side: `nstreams` InflatePipe instances (zlib/inflate_pipe.cc:33-46,
  * inflateInit) in HBM.  xcg_zinflate_batch: one InflatePipe::consume() per

@@ -133,15 +133,21 @@ DeflatePipe::consume(Buffer *in)
 {
 	DeflatePool *p = deflate_pool(deflate_levels()[this]);
 	uint32_t slot = p->slot_of[this];
+	/* the Buffer's segments: deflate() gets one per call (deflate_pipe.cc:66-84),
+	 * which level 0's stored blocks follow */
+	std::vector<uint32_t> segs;
+	for (Buffer::SegmentIterator it = in->segments(); !it.end(); it.next())
+		segs.push_back((*it)->length());
 	std::vector<uint8_t> bytes;
 	take_all(in, bytes);
 	uint32_t len = bytes.size();
+	uint32_t nseg = segs.size();
 	uint64_t in_off = 0, out_off = 0;
 	uint32_t out_len = 0;
 	uint64_t deliver = 0;
 	std::vector<uint8_t> obuf(xcg_zdeflate_bound(len));
-	int rc = xcg_zdeflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1, &obuf[0], &out_off,
-				   &out_len, &deliver);
+	int rc = xcg_zdeflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1,
+				   segs.empty() ? NULL : &segs[0], &nseg, &obuf[0], &out_off, &out_len, &deliver);
 	if (rc != XCG_OK)
 		HALT(log_) << "xcgpu deflate: " << xcg_strerror(rc);
 	/* produce the held bytes and the new ones up to `deliver`; keep the rest */

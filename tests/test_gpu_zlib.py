@@ -11,7 +11,7 @@ import zlib
 import pytest
 
 from oracle.zlib_pipe import DeflatePipeRef
-from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, wan_stream
+from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, stored_cases, wan_stream
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -49,13 +49,14 @@ def check_vs_zlib(streams_by_level):
                                          f'got {len(g)} B, zlib {len(exp)} B, first difference at byte {i}')
 
 
-@pytest.mark.parametrize('key', ['streams', 'fast', 'stops'])
+@pytest.mark.parametrize('key', ['streams', 'fast', 'stops', 'stored'])
 def test_golden_fixture_gpu(key):
     with open(os.path.join(ROOT, 'tests/golden/zlib.json')) as f:
         g = json.load(f)
     by_level = {}
     recs = {}
-    streams = {'streams': lambda: cases(7, 24), 'fast': lambda: fast_cases(8, 12), 'stops': lambda: stop_cases(9)}[key]()
+    streams = {'streams': lambda: cases(7, 24), 'fast': lambda: fast_cases(8, 12), 'stops': lambda: stop_cases(9),
+               'stored': lambda: stored_cases(10, 10)}[key]()
     for (level, calls), rec in zip(streams, g[key]):
         by_level.setdefault(level, []).append(calls)
         recs.setdefault(level, []).append(rec)
@@ -97,10 +98,42 @@ def test_fast_levels_vs_zlib():
     check_vs_zlib(by_level)
 
 
+def test_stored_level_segments_vs_zlib():
+    """Level 0 (deflate_stored): block sizes follow each deflate() call's
+    segment and the pipe's 64 KiB buffer; 24 streams with random Buffer
+    segmentations, every consume equal to zlib's on the same segments."""
+    from wanproxy_amd.zpipe import DeflatePipes
+    rng = random.Random(44)
+    streams = [calls for _, calls in stored_cases(45, 24)]
+    segs = []
+    for calls in streams:
+        row = []
+        for c in calls:
+            out, t = [], 0
+            mode = rng.choice(['full', 'random', 'small'])
+            while t < len(c):
+                k = {'full': 2048, 'random': rng.randint(1, 2048), 'small': rng.randint(1, 64)}[mode]
+                out.append(min(k, len(c) - t))
+                t += out[-1]
+            row.append(out)
+        segs.append(row)
+    ctx = DeflatePipes(0, len(streams))
+    got = [[] for _ in streams]
+    for k in range(max(len(x) for x in streams)):
+        items = [(i, s[k], segs[i][k] if s[k] else None) for i, s in enumerate(streams) if k < len(s)]
+        for (i, _, _), g in zip(items, ctx.consume_many(items)):
+            got[i].append(g)
+    ctx.close()
+    for i, calls in enumerate(streams):
+        ref = DeflatePipeRef(0)
+        for k, c in enumerate(calls):
+            assert got[i][k] == ref.consume(c, segs[i][k] if c else None), (i, k, len(c))
+
+
 def test_tiny_calls_vs_zlib():
     rng = random.Random(5)
     streams = [[gen_bytes(rng, rng.randint(1, 6)) for _ in range(40)] + [b''] for _ in range(8)]
-    check_vs_zlib({6: streams, 9: streams[:3], 4: streams[3:5], 1: streams[5:], 3: streams[:2]})
+    check_vs_zlib({6: streams, 9: streams[:3], 4: streams[3:5], 1: streams[5:], 3: streams[:2], 0: streams[2:6]})
 
 
 def test_many_streams_wan_traffic_round_trip():
@@ -123,7 +156,7 @@ def test_long_matches_and_slides():
     base = rng.randbytes(40000)
     s1 = [base * 13, bytes(300000), base[::-1] * 3 + base] + [b'']
     s2 = [gen_bytes(rng, 524288), gen_bytes(rng, 100000)] + [b'']
-    check_vs_zlib({6: [s1, s2], 9: [s1], 4: [s2], 1: [s1, s2], 2: [s2], 3: [s1]})
+    check_vs_zlib({6: [s1, s2], 9: [s1], 4: [s2], 1: [s1, s2], 2: [s2], 3: [s1], 0: [s1, s2]})
 
 
 def test_errors():

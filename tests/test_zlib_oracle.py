@@ -10,7 +10,7 @@ import zlib
 import pytest
 
 from oracle.zlib_pipe import DeflatePipeRef, DeflatePipeUnbounded, InflatePipeRef, ZOracle, ZLIB_VERSION
-from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, wan_stream
+from tests.zlib_cases import cases, fast_cases, gen_bytes, stop_cases, stored_cases, wan_stream
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -127,3 +127,69 @@ def test_oracle_tiny_calls():
             c = gen_bytes(rng, rng.randint(1, 6))
             assert o.consume(c) == r.consume(c)
         assert o.consume(b'') == r.consume(b'')
+
+
+# ------------------------------------------------------------------ level 0
+class StoredPlanCPU:
+    """The engine's level-0 planner (wanproxy_amd/csrc/xcg_stored_plan.h, the
+    host half of the GPU path) run on the CPU by oracle/stored_plan_harness.cc."""
+    _lib = None
+
+    def __init__(self):
+        import ctypes as C
+        if StoredPlanCPU._lib is None:
+            L = C.CDLL(os.path.join(ROOT, 'oracle/build/libstoredplan.so'))
+            L.sp_new.restype = C.c_void_p
+            L.sp_free.argtypes = [C.c_void_p]
+            L.sp_consume.restype = C.c_int64
+            L.sp_consume.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_char_p,
+                                     C.c_uint64]
+            StoredPlanCPU._lib = L
+        self.C = C
+        self.s = StoredPlanCPU._lib.sp_new()
+
+    def consume(self, data, segments=None):
+        C = self.C
+        arr = (C.c_uint32 * max(1, len(segments)))(*segments) if segments else None
+        buf = C.create_string_buffer(2 * len(data) + 300000)
+        n = StoredPlanCPU._lib.sp_consume(self.s, data, len(data), arr, len(segments) if segments else 0, buf,
+                                          len(buf))
+        assert n >= 0
+        return buf.raw[:n]
+
+    def __del__(self):
+        if getattr(self, 's', None):
+            StoredPlanCPU._lib.sp_free(self.s)
+
+
+def _segments(rng, n):
+    out, t = [], 0
+    mode = rng.choice(['full', 'random', 'small'])
+    while t < n:
+        k = {'full': 2048, 'random': rng.randint(1, 2048), 'small': rng.randint(1, 64)}[mode]
+        out.append(min(k, n - t))
+        t += out[-1]
+    return out
+
+
+@pytest.mark.parametrize('seed', [1, 2, 3])
+def test_stored_plan_vs_zlib(seed):
+    """Level 0: deflate_stored's block sizes follow the segments each deflate()
+    call gets and the pipe's 64 KiB buffer; the planner reproduces zlib's output
+    call by call for random segmentations (<= 2048 bytes, BUFFER_SEGMENT_SIZE)."""
+    rng = random.Random(seed)
+    for _, calls in stored_cases(400 + seed, 12):
+        p, r = StoredPlanCPU(), DeflatePipeRef(0)
+        for k, c in enumerate(calls):
+            segs = _segments(rng, len(c)) if c else None
+            assert p.consume(c, segs) == r.consume(c, segs), (seed, k, len(c))
+
+
+def test_stored_golden():
+    with open(os.path.join(ROOT, 'tests/golden/zlib.json')) as f:
+        g = json.load(f)
+    for (level, calls), rec in zip(stored_cases(10, 10), g['stored']):
+        p = StoredPlanCPU()
+        for c, e in zip(calls, rec['calls']):
+            got = p.consume(c)
+            assert len(got) == e['out_len'] and hashlib.sha256(got).hexdigest() == e['out_sha256']

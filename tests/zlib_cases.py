@@ -62,6 +62,20 @@ def fast_cases(seed: int, n: int, max_extra: int = 150000):
     return [(rng.choice([1, 2, 3]), calls) for _, calls in cases(seed, n, max_extra)]
 
 
+def stored_cases(seed: int, n: int):
+    """Level 0 (deflate_stored): consumes around its 32 KiB / 64 KiB thresholds."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        sizes = [rng.choice([1, 7, 2048, 32763, 32768, 40000, 65530, 65536, 70000, 140000, rng.randint(1, 200000)])
+                 for _ in range(rng.randint(1, 6))]
+        calls = [gen_bytes(rng, s) for s in sizes]
+        if rng.random() < 0.8:
+            calls.append(b'')
+        out.append((0, calls))
+    return out
+
+
 def stop_cases(seed: int, levels=(1, 3, 4, 6, 9), offsets=range(-3, 270, 9)):
     """Streams whose first consume is 4 * 16383 + j incompressible bytes: the
     fourth block flush falls at loop top 65532 + j - ... of the call, inside

@@ -47,6 +47,7 @@
 
 #include "../../include/xcgpu.h"
 #include "xcg_device.h"
+#include "xcg_stored_plan.h"
 
 namespace xcg {
 namespace zd {
@@ -1629,6 +1630,60 @@ __global__ __launch_bounds__(256) void zd_commit_kernel(ZArgs a) {
   }
 }
 
+// ------------------------------------------------------------------- level 0
+// deflate_stored (deflate.c, zlib 1.2.11) writes no Huffman codes: a stream
+// is stored blocks (5 header bytes + raw bytes) whose sizes follow zlib's
+// control flow over avail_in (the Buffer's segments, <= 2048 bytes each) and
+// avail_out (DeflatePipe's 64 KiB buffer, deflate_pipe.cc:57-115): it copies
+// blocks straight to next_out while they are >= 32 KiB (or flush everything),
+// and otherwise collects input in its 64 KiB window and emits from there.
+// The host replays that control flow over lengths only (StoredPlan) and the
+// GPU moves the bytes (zs_copy_kernel): every piece of a call's output is a
+// header, a range of the stream (this call's input, or earlier bytes from the
+// stream's 64 KiB ring) or the adler32 trailer.
+__global__ __launch_bounds__(256) void zs_copy_kernel(const ZPiece* pc, const ZCall* calls, const ZState* st,
+                                                      const uint8_t* in, const uint8_t* ring, uint8_t* out) {
+  const ZPiece p = pc[blockIdx.x];
+  const ZCall c = calls[p.call];
+  uint8_t* o = out + c.out_off + p.out;
+  if (p.kind == 0) {
+    if (threadIdx.x < p.len) o[threadIdx.x] = (uint8_t)(p.src >> (8 * threadIdx.x));
+    return;
+  }
+  if (p.kind == 2) {
+    const uint32_t ad = st[c.stream].adler;
+    if (threadIdx.x < 4) o[threadIdx.x] = (uint8_t)(ad >> (24 - 8 * threadIdx.x));
+    return;
+  }
+  const uint64_t total = st[c.stream].total;           // stream position of this call's first byte
+  const uint8_t* r = ring + (uint64_t)c.stream * (2 * WSIZE);
+  for (uint32_t i = threadIdx.x; i < p.len; i += 256) {
+    const uint64_t q = p.src + i;
+    o[i] = q >= total ? in[c.in_off + (q - total)] : r[q & (2 * WSIZE - 1)];
+  }
+}
+
+// The stream's last 64 KiB (ring by position) after the call; adler, position.
+__global__ __launch_bounds__(256) void zs_commit_kernel(ZArgs a) {
+  const ZCall c = a.calls[blockIdx.x];
+  const ZState s0 = a.st[c.stream];
+  uint8_t* r = a.hist + (uint64_t)c.stream * (2 * WSIZE);
+  const uint32_t keep = c.len < 2u * WSIZE ? c.len : 2u * WSIZE;
+  for (uint32_t i = threadIdx.x; i < keep; i += 256) {
+    const uint64_t q = s0.total + c.len - keep + i;
+    r[q & (2 * WSIZE - 1)] = a.in[c.in_off + (c.len - keep + i)];
+  }
+  if (threadIdx.x == 0) {
+    ZState s = s0;
+    s.total += c.len;
+    s.adler = c.len ? a.res[blockIdx.x].adler : s.adler;
+    s.flags |= 1u;
+    if (c.len == 0) s.flags |= 2u;
+    a.st[c.stream] = s;
+  }
+}
+
+
 }  // namespace zd
 }  // namespace xcg
 
@@ -1652,6 +1707,7 @@ struct xcg_zdeflate {
   uint32_t* h_changed = nullptr;   // pinned, per call (deflate_fast rounds)
   size_t h_changed_cap = 0;
   uint32_t last_rounds = 0;
+  std::vector<StoredPlan> splan;   // level 0: zlib's control state per stream (host, lengths only)
 };
 
 namespace {
@@ -1687,20 +1743,22 @@ extern "C" {
 uint64_t xcg_zdeflate_bound(uint32_t len) { return (uint64_t)len + (len >> 1) + 2 * DMAX + 128; }
 
 int xcg_zdeflate_create(int device, int level, uint32_t nstreams, xcg_zdeflate** out) {
-  if (!out || level < 1 || level > 9 || nstreams == 0) return level == 0 ? XCG_ENOTSUP : XCG_EINVAL;
+  if (!out || level < 0 || level > 9 || nstreams == 0) return XCG_EINVAL;
   if (hipSetDevice(device) != hipSuccess) return XCG_EHIP;
   xcg_zdeflate* z = new xcg_zdeflate();
   z->device = device;
   z->level = level;
   z->nstreams = nstreams;
   if (hipMalloc(&z->st, sizeof(ZState) * nstreams) != hipSuccess ||
-      hipMalloc(&z->hist, (size_t)WSIZE * nstreams) != hipSuccess || hipEventCreateWithFlags(&z->done, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&z->hist, (size_t)WSIZE * (level == 0 ? 2 : 1) * nstreams) != hipSuccess ||
+      hipEventCreateWithFlags(&z->done, hipEventDisableTiming) != hipSuccess ||
       (level < 4 && (hipMalloc(&z->ring, (size_t)WSIZE / 8 * nstreams) != hipSuccess ||
                      hipMemset(z->ring, 0, (size_t)WSIZE / 8 * nstreams) != hipSuccess))) {
     delete z;
     return XCG_ENOMEM;
   }
   z->h_init.assign(nstreams, fresh_state());
+  if (level == 0) z->splan.assign(nstreams, StoredPlan());
   if (hipMemcpy(z->st, z->h_init.data(), sizeof(ZState) * nstreams, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(z->hist, 0, (size_t)WSIZE * nstreams) != hipSuccess) {
     delete z;
@@ -1732,16 +1790,98 @@ int xcg_zdeflate_reset(xcg_zdeflate* z, uint32_t stream) {
   const ZState s0 = fresh_state();
   if (hipMemcpy(z->st + stream, &s0, sizeof s0, hipMemcpyHostToDevice) != hipSuccess) return XCG_EHIP;
   if (z->ring && hipMemset(z->ring + (size_t)stream * (WSIZE / 32), 0, WSIZE / 8) != hipSuccess) return XCG_EHIP;
+  if (!z->splan.empty()) z->splan[stream] = StoredPlan();
   return XCG_OK;
 }
 
-int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
-                       const uint32_t* h_stream, uint32_t n, uint8_t* d_out, const uint64_t* h_out_off,
-                       uint32_t* d_out_len, uint64_t* d_deliver, void* stream) {
-  if (!z || n == 0 || !h_in_off || !h_len || !h_stream || !h_out_off || !d_out || !d_out_len || !d_deliver)
+}  // extern "C"
+
+namespace {
+// Level 0: the host replays zlib's control flow per consume (StoredPlan), the
+// GPU computes adler32, moves the pieces and keeps each stream's last 64 KiB.
+int stored_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                 const uint32_t* h_stream, uint32_t n, const uint32_t* h_seg, const uint32_t* h_nseg, uint8_t* d_out,
+                 const uint64_t* h_out_off, uint32_t* d_out_len, uint64_t* d_deliver, hipStream_t st) {
+  std::vector<ZCall> calls(n);
+  std::vector<ZPiece> pieces;
+  std::vector<uint32_t> made32(n);
+  std::vector<uint64_t> deliver(n);
+  std::vector<uint8_t> seen(z->nstreams, 0);
+  uint64_t so = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (h_stream[i] >= z->nstreams || seen[h_stream[i]] || (h_out_off[i] & 3) || h_len[i] > (1u << 24))
+      return XCG_EINVAL;
+    seen[h_stream[i]] = 1;
+  }
+  // the plan mutates the streams' host state: check everything first, then plan
+  for (uint32_t i = 0; i < n; i++) {
+    ZCall& c = calls[i];
+    memset(&c, 0, sizeof c);
+    c.in_off = h_in_off[i];
+    c.out_off = h_out_off[i];
+    c.len = h_len[i];
+    c.stream = h_stream[i];
+    const size_t first = pieces.size();
+    uint64_t made = 0;
+    const uint32_t ns = h_nseg ? h_nseg[i] : 0;
+    if (!z->splan[c.stream].consume(c.len, h_seg ? h_seg + so : nullptr, ns, pieces, &made, &deliver[i]))
+      return XCG_EINVAL;
+    so += ns;
+    if (made > xcg_zdeflate_bound(c.len)) return XCG_EOVERFLOW;
+    made32[i] = (uint32_t)made;
+    for (size_t k = first; k < pieces.size(); k++) pieces[k].call = i;
+  }
+  size_t m_calls = 0, m_pc = al(sizeof(ZCall) * n, 256), m_len = al(m_pc + sizeof(ZPiece) * pieces.size(), 256),
+         m_dl = al(m_len + 4ull * n, 256), m_end = al(m_dl + 8ull * n, 256);
+  if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
+  const size_t r_res = sizeof(ZCallRes) * n;
+  if (grow((void**)&z->scratch, &z->scratch_cap, al(r_res, 256), false)) return XCG_ENOMEM;
+  if (grow(&z->meta, &z->meta_cap, m_end, false) || grow(&z->h_meta, &z->h_meta_cap, m_end, true)) return XCG_ENOMEM;
+  uint8_t* hm = (uint8_t*)z->h_meta;
+  memcpy(hm + m_calls, calls.data(), sizeof(ZCall) * n);
+  if (!pieces.empty()) memcpy(hm + m_pc, pieces.data(), sizeof(ZPiece) * pieces.size());
+  memcpy(hm + m_len, made32.data(), 4ull * n);
+  memcpy(hm + m_dl, deliver.data(), 8ull * n);
+  if (hipMemcpyAsync(z->meta, hm, m_end, hipMemcpyHostToDevice, st) != hipSuccess) return XCG_EHIP;
+  uint8_t* dm = (uint8_t*)z->meta;
+  if (hipMemcpyAsync(d_out_len, dm + m_len, 4ull * n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(d_deliver, dm + m_dl, 8ull * n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return XCG_EHIP;
+  ZArgs a;
+  memset(&a, 0, sizeof a);
+  a.calls = (const ZCall*)(dm + m_calls);
+  a.st = z->st;
+  a.hist = z->hist;
+  a.in = d_in;
+  a.out = d_out;
+  a.res = (ZCallRes*)z->scratch;
+  a.n = n;
+  a.level = 0;
+  hipLaunchKernelGGL(zd_adler_kernel, dim3(n), dim3(256), 0, st, a);
+  if (!pieces.empty())
+    hipLaunchKernelGGL(zs_copy_kernel, dim3((unsigned)pieces.size()), dim3(256), 0, st, (const ZPiece*)(dm + m_pc),
+                       a.calls, (const ZState*)z->st, d_in, (const uint8_t*)z->hist, d_out);
+  hipLaunchKernelGGL(zs_commit_kernel, dim3(n), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) return XCG_EHIP;
+  if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
+  return XCG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int xcg_zdeflate_batch_seg(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                           const uint32_t* h_stream, uint32_t n, const uint32_t* h_seg, const uint32_t* h_nseg,
+                           uint8_t* d_out, const uint64_t* h_out_off, uint32_t* d_out_len, uint64_t* d_deliver,
+                           void* stream) {
+  if (!z || n == 0 || !h_in_off || !h_len || !h_stream || !h_out_off || !d_out || !d_out_len || !d_deliver ||
+      (h_seg && !h_nseg))
     return XCG_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   (void)hipSetDevice(z->device);
+  if (z->level == 0)
+    return stored_batch(z, d_in, h_in_off, h_len, h_stream, n, h_seg, h_nseg, d_out, h_out_off, d_out_len, d_deliver,
+                        st);
   // host plan: scratch offsets, tiles, block maps
   std::vector<ZCall> calls(n);
   std::vector<uint32_t> mstart(n + 1), gstart(n + 1), bstart(n + 1);
@@ -1873,12 +2013,19 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
   return XCG_OK;
 }
 
+int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_in_off, const uint32_t* h_len,
+                       const uint32_t* h_stream, uint32_t n, uint8_t* d_out, const uint64_t* h_out_off,
+                       uint32_t* d_out_len, uint64_t* d_deliver, void* stream) {
+  return xcg_zdeflate_batch_seg(z, d_in, h_in_off, h_len, h_stream, n, nullptr, nullptr, d_out, h_out_off, d_out_len,
+                                d_deliver, stream);
+}
+
 // Host buffers: one consume() per listed stream, inputs concatenated in h_in
 // at h_in_off, outputs to h_out at h_out_off (room for xcg_zdeflate_bound);
 // lengths to h_out_len.  Synchronous.
 int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
-                      const uint32_t* h_stream, uint32_t n, uint8_t* h_out, const uint64_t* h_out_off,
-                      uint32_t* h_out_len, uint64_t* h_deliver) {
+                      const uint32_t* h_stream, uint32_t n, const uint32_t* h_seg, const uint32_t* h_nseg,
+                      uint8_t* h_out, const uint64_t* h_out_off, uint32_t* h_out_len, uint64_t* h_deliver) {
   if (!z || n == 0 || !h_deliver) return XCG_EINVAL;
   (void)hipSetDevice(z->device);
   uint64_t in_end = 0, out_end = 0;
@@ -1897,7 +2044,9 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
     rc = XCG_ENOMEM;
   }
   if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
-  if (!rc) rc = xcg_zdeflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), d_len, d_dl, nullptr);
+  if (!rc)
+    rc = xcg_zdeflate_batch_seg(z, d_in, h_in_off, h_len, h_stream, n, h_seg, h_nseg, d_out, doff.data(), d_len, d_dl,
+                                nullptr);
   if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
   if (!rc && hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
   if (!rc && hipMemcpy(h_deliver, d_dl, 8ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;

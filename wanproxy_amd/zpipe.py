@@ -41,7 +41,9 @@ def _lib():
         L.xcg_zdeflate_reset.restype = C.c_int
         L.xcg_zdeflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
         L.xcg_zdeflate_batch.restype = C.c_int
-        L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
+        L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.xcg_zdeflate_batch_seg.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]
+        L.xcg_zdeflate_batch_seg.restype = C.c_int
         L.xcg_zdeflate_host.restype = C.c_int
         L.xcg_zinflate_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(vp)]
         L.xcg_zinflate_create.restype = C.c_int
@@ -69,7 +71,7 @@ class DeflatePipes:
         rc = _lib().xcg_zdeflate_create(device, level, nstreams, C.byref(h))
         self.undelivered = {}           # stream -> bytes the pipe made but has not produced yet
         if rc == XCG_ENOTSUP:
-            raise XCGError(f'zlib level {level}: only levels 4-9 (deflate_slow) are implemented')
+            raise XCGError(f'zlib level {level}: not supported')
         _check(rc)
         self.h = h
 
@@ -88,7 +90,8 @@ class DeflatePipes:
     def pipe(self, stream: int) -> 'DeflatePipe':
         return DeflatePipe(self, stream)
 
-    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, d_out_len, d_deliver, stream=None):
+    def batch_device(self, d_in, in_off, lens, streams, d_out, out_off, d_out_len, d_deliver, stream=None,
+                     segments=None):
         """Device-resident batch: d_in / d_out / d_out_len (int32) / d_deliver
         (int64) are torch CUDA tensors; in_off / lens / streams / out_off host
         numpy arrays.  d_out_len: the new stream bytes at out_off; d_deliver:
@@ -98,19 +101,31 @@ class DeflatePipes:
         streams = np.ascontiguousarray(streams, dtype=np.uint32)
         out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
         n = int(lens.size)
-        _check(_lib().xcg_zdeflate_batch(self.h, C.c_void_p(d_in.data_ptr()), in_off.ctypes.data, lens.ctypes.data,
-                                         streams.ctypes.data, n, C.c_void_p(d_out.data_ptr()), out_off.ctypes.data,
-                                         C.c_void_p(d_out_len.data_ptr()), C.c_void_p(d_deliver.data_ptr()),
-                                         _stream_ptr(stream)))
+        seg = nseg = None
+        if segments is not None:     # per call: the Buffer's segment lengths (None: 2048-byte cuts)
+            per = [list(sg) if sg is not None else [min(2048, int(lens[i]) - k) for k in range(0, int(lens[i]), 2048)]
+                   for i, sg in enumerate(segments)]
+            nseg = np.array([len(x) for x in per], dtype=np.uint32)
+            seg = np.array([v for x in per for v in x] or [0], dtype=np.uint32)
+        _check(_lib().xcg_zdeflate_batch_seg(self.h, C.c_void_p(d_in.data_ptr()), in_off.ctypes.data,
+                                             lens.ctypes.data, streams.ctypes.data, n,
+                                             seg.ctypes.data if seg is not None else None,
+                                             nseg.ctypes.data if nseg is not None else None,
+                                             C.c_void_p(d_out.data_ptr()), out_off.ctypes.data,
+                                             C.c_void_p(d_out_len.data_ptr()), C.c_void_p(d_deliver.data_ptr()),
+                                             _stream_ptr(stream)))
 
     def consume_many(self, items):
-        """items: [(stream, bytes)] (each stream at most once).  Returns the
-        produced bytes per item, in order."""
+        """items: [(stream, bytes)] or [(stream, bytes, segments)] (each stream
+        at most once; segments: the Buffer's segment lengths, which level 0's
+        stored blocks follow).  Returns the produced bytes per item, in order."""
         import torch
         dev = torch.device('cuda', self.device)
         n = len(items)
         if n == 0:
             return []
+        segs = [it[2] if len(it) > 2 else None for it in items]
+        items = [(it[0], it[1]) for it in items]
         lens = np.array([len(d) for _, d in items], dtype=np.uint32)
         streams = np.array([s for s, _ in items], dtype=np.uint32)
         in_off = np.zeros(n, dtype=np.uint64)
@@ -123,7 +138,8 @@ class DeflatePipes:
         d_out = torch.empty(int(bounds.sum()), dtype=torch.uint8, device=dev)
         d_len = torch.zeros(n, dtype=torch.int32, device=dev)
         d_dl = torch.zeros(n, dtype=torch.int64, device=dev)
-        self.batch_device(d_in, in_off, lens, streams, d_out, out_off, d_len, d_dl)
+        self.batch_device(d_in, in_off, lens, streams, d_out, out_off, d_len, d_dl,
+                          segments=segs if any(x is not None for x in segs) else None)
         torch.cuda.synchronize(dev)
         ol = d_len.cpu().numpy().astype(np.uint64)
         dl = d_dl.cpu().numpy()
