@@ -3,11 +3,14 @@
  * and InflatePipe with their reference headers unchanged (zlib/deflate_pipe.h,
  * zlib/inflate_pipe.h); this file replaces zlib/deflate_pipe.cc and
  * zlib/inflate_pipe.cc in zlib/lib.mk.  Every pipe is a slot
- * of one process-wide GPU context per direction (and level): a
- * DeflatePipe(level) consume() is one xcg_zdeflate call on its slot, an
- * InflatePipe consume() one xcg_zinflate call.  Output bytes equal zlib
- * 1.2.11's for levels 4-9 (wanproxy.conf uses 6); levels 0-3 HALT at
- * construction.  The z_stream member the headers declare is left unused.
+ * of a process-wide pool of GPU contexts per direction (and level; device
+ * XCGPU_DEVICE, default 0): a DeflatePipe(level) consume() is one xcg_zdeflate
+ * call on its slot, an InflatePipe consume() one xcg_zinflate call.  Output
+ * bytes equal zlib 1.2.11's driven by the reference loop at every level 0-9
+ * (wanproxy.conf uses 6), including where that loop's single Z_SYNC_FLUSH call
+ * into its 64 KiB buffer stops early (the held-back bytes are produced first
+ * by the next consume).  The z_stream member the headers declare is left
+ * unused.
  *
  * Reference behaviour kept (zlib/deflate_pipe.cc:57-115,
  * zlib/inflate_pipe.cc:54-139): a non-empty consume produces the bytes after
@@ -16,6 +19,7 @@
  * stream's end, produce_error on a data error or bytes after the end.
  */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -33,22 +37,66 @@
 
 namespace {
 
-/* Slots: one per live pipe, handed back on destruction. */
+/*
+ * Slots: a GPU context holds XCGPU_ZLIB_SLOTS pipes; a pool grows by another
+ * context when every slot is taken (no limit on live pipes beyond device
+ * memory), and a destroyed pipe's slot is reused (after a reset: the fresh
+ * z_stream the reference's constructor makes).
+ */
 const uint32_t XCGPU_ZLIB_SLOTS = 4096;
 
+int xcgpu_device(void)
+{
+	const char *dev = getenv("XCGPU_DEVICE");	/* as the XCodec binding (xcgpu_binding.cc) */
+	return dev != NULL ? atoi(dev) : 0;
+}
+
+struct Slot {
+	uint32_t ctx, slot;
+};
+
 struct DeflatePool {
-	xcg_zdeflate *ctx;
-	std::vector<uint32_t> free_slots;
-	std::map<const void *, uint32_t> slot_of;
+	int level;
+	std::vector<xcg_zdeflate *> ctx;
+	std::vector<Slot> free_slots;
+	std::map<const void *, Slot> slot_of;
 	/* bytes a consume made but did not produce: zlib's pending output past
 	 * the pipe's 64 KiB buffer (deflate_pipe.cc:34,86-105) */
 	std::map<const void *, std::vector<uint8_t> > held;
+
+	int grow(void)
+	{
+		xcg_zdeflate *z = NULL;
+		int rc = xcg_zdeflate_create(xcgpu_device(), level, XCGPU_ZLIB_SLOTS, &z);
+		if (rc != XCG_OK)
+			return rc;
+		ctx.push_back(z);
+		for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--) {
+			Slot s = { (uint32_t)ctx.size() - 1, i - 1 };
+			free_slots.push_back(s);
+		}
+		return XCG_OK;
+	}
 };
 
 struct InflatePool {
-	xcg_zinflate *ctx;
-	std::vector<uint32_t> free_slots;
-	std::map<const void *, uint32_t> slot_of;
+	std::vector<xcg_zinflate *> ctx;
+	std::vector<Slot> free_slots;
+	std::map<const void *, Slot> slot_of;
+
+	int grow(void)
+	{
+		xcg_zinflate *z = NULL;
+		int rc = xcg_zinflate_create(xcgpu_device(), XCGPU_ZLIB_SLOTS, &z);
+		if (rc != XCG_OK)
+			return rc;
+		ctx.push_back(z);
+		for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--) {
+			Slot s = { (uint32_t)ctx.size() - 1, i - 1 };
+			free_slots.push_back(s);
+		}
+		return XCG_OK;
+	}
 };
 
 DeflatePool *deflate_pool(int level)
@@ -58,12 +106,7 @@ DeflatePool *deflate_pool(int level)
 	if (it != pools.end())
 		return it->second;
 	DeflatePool *p = new DeflatePool();
-	if (xcg_zdeflate_create(0, level, XCGPU_ZLIB_SLOTS, &p->ctx) != XCG_OK) {
-		delete p;
-		return NULL;
-	}
-	for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--)
-		p->free_slots.push_back(i - 1);
+	p->level = level;
 	pools[level] = p;
 	return p;
 }
@@ -71,16 +114,8 @@ DeflatePool *deflate_pool(int level)
 InflatePool *inflate_pool(void)
 {
 	static InflatePool *p;
-	if (p != NULL)
-		return p;
-	InflatePool *q = new InflatePool();
-	if (xcg_zinflate_create(0, XCGPU_ZLIB_SLOTS, &q->ctx) != XCG_OK) {
-		delete q;
-		return NULL;
-	}
-	for (uint32_t i = XCGPU_ZLIB_SLOTS; i > 0; i--)
-		q->free_slots.push_back(i - 1);
-	p = q;
+	if (p == NULL)
+		p = new InflatePool();
 	return p;
 }
 
@@ -107,12 +142,12 @@ DeflatePipe::DeflatePipe(int level)
   stream_()
 {
 	DeflatePool *p = deflate_pool(level);
-	if (p == NULL || p->free_slots.empty())
-		HALT(log_) << "Could not initialize deflate stream (MI355X engine: levels 4-9, "
-			   << XCGPU_ZLIB_SLOTS << " pipes).";
-	uint32_t slot = p->free_slots.back();
+	int rc = p->free_slots.empty() ? p->grow() : XCG_OK;
+	if (rc != XCG_OK)	/* deflateInit's failure (bad level, no device / memory) */
+		HALT(log_) << "Could not initialize deflate stream: " << xcg_strerror(rc);
+	Slot slot = p->free_slots.back();
 	p->free_slots.pop_back();
-	if (xcg_zdeflate_reset(p->ctx, slot) != XCG_OK)
+	if (xcg_zdeflate_reset(p->ctx[slot.ctx], slot.slot) != XCG_OK)
 		HALT(log_) << "Could not initialize deflate stream.";
 	p->slot_of[this] = slot;
 	deflate_levels()[this] = level;
@@ -132,7 +167,7 @@ void
 DeflatePipe::consume(Buffer *in)
 {
 	DeflatePool *p = deflate_pool(deflate_levels()[this]);
-	uint32_t slot = p->slot_of[this];
+	Slot slot = p->slot_of[this];
 	/* the Buffer's segments: deflate() gets one per call (deflate_pipe.cc:66-84),
 	 * which level 0's stored blocks follow */
 	std::vector<uint32_t> segs;
@@ -146,7 +181,7 @@ DeflatePipe::consume(Buffer *in)
 	uint32_t out_len = 0;
 	uint64_t deliver = 0;
 	std::vector<uint8_t> obuf(xcg_zdeflate_bound(len));
-	int rc = xcg_zdeflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1,
+	int rc = xcg_zdeflate_host(p->ctx[slot.ctx], bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot.slot, 1,
 				   segs.empty() ? NULL : &segs[0], &nseg, &obuf[0], &out_off, &out_len, &deliver);
 	if (rc != XCG_OK)
 		HALT(log_) << "xcgpu deflate: " << xcg_strerror(rc);
@@ -173,12 +208,13 @@ InflatePipe::InflatePipe(void)
   stream_()
 {
 	InflatePool *p = inflate_pool();
-	if (p == NULL || p->free_slots.empty())
-		HALT(log_) << "Could not initialize inflate stream.";
-	uint32_t slot = p->free_slots.back();
+	int rc = p->free_slots.empty() ? p->grow() : XCG_OK;
+	if (rc != XCG_OK)
+		HALT(log_) << "Could not initialize inflate stream: " << xcg_strerror(rc);
+	Slot slot = p->free_slots.back();
 	p->free_slots.pop_back();
 	/* a reused slot still holds its last stream: inflateInit (inflate_pipe.cc:38-50) */
-	if (xcg_zinflate_reset(p->ctx, slot) != XCG_OK)
+	if (xcg_zinflate_reset(p->ctx[slot.ctx], slot.slot) != XCG_OK)
 		HALT(log_) << "Could not initialize inflate stream.";
 	p->slot_of[this] = slot;
 }
@@ -194,7 +230,7 @@ void
 InflatePipe::consume(Buffer *in)
 {
 	InflatePool *p = inflate_pool();
-	uint32_t slot = p->slot_of[this];
+	Slot slot = p->slot_of[this];
 	std::vector<uint8_t> bytes;
 	take_all(in, bytes);
 	uint32_t len = bytes.size();
@@ -204,8 +240,8 @@ InflatePipe::consume(Buffer *in)
 	std::vector<uint8_t> obuf;
 	for (;;) {		/* -2: more output room, nothing was committed */
 		obuf.resize(cap);
-		int rc = xcg_zinflate_host(p->ctx, bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot, 1, &obuf[0],
-					   &out_off, &cap, &out_len, &status);
+		int rc = xcg_zinflate_host(p->ctx[slot.ctx], bytes.empty() ? NULL : &bytes[0], &in_off, &len, &slot.slot, 1,
+					   &obuf[0], &out_off, &cap, &out_len, &status);
 		if (rc != XCG_OK)
 			HALT(log_) << "xcgpu inflate: " << xcg_strerror(rc);
 		if (status != -2)

@@ -134,3 +134,54 @@ class ZOracle:
 
     def __del__(self):
         self.close()
+
+
+class ReferencePipes:
+    """wanproxy's DeflatePipe / InflatePipe classes themselves, through
+    oracle/zpipe_driver.cc: `ref` = the reference's zlib/deflate_pipe.cc and
+    zlib/inflate_pipe.cc compiled from /root/reference over the system zlib
+    (oracle/_ref/libzpref.so); `dropin` = integration/zlib_pipes_xcgpu.cc, the
+    engine-backed bodies of the same classes (oracle/_ref/libzpdropin.so)."""
+    _libs = {}
+
+    def __init__(self, which: str = 'ref'):
+        if which not in self._libs:
+            name = {'ref': 'libzpref.so', 'dropin': 'libzpdropin.so'}[which]
+            L = C.CDLL(os.path.join(HERE, '_ref', name))
+            L.zp_new.restype = C.c_void_p
+            L.zp_new.argtypes = [C.c_int, C.c_int]
+            L.zp_free.argtypes = [C.c_void_p, C.c_int]
+            L.zp_consume.restype = C.c_int64
+            L.zp_consume.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_char_p,
+                                     C.c_uint64, C.POINTER(C.c_int)]
+            self._libs[which] = L
+        self.L = self._libs[which]
+
+    def pipe(self, kind: str, level: int = 6) -> 'ReferencePipe':
+        return ReferencePipe(self.L, 0 if kind == 'deflate' else 1, level)
+
+
+class ReferencePipe:
+    def __init__(self, L, kind: int, level: int):
+        self.L, self.kind = L, kind
+        self.h = L.zp_new(kind, level)
+
+    def consume(self, data: bytes, segments=None):
+        """-> (produced bytes, status: 0 produce, 1 produce_eos, -1 produce_error)"""
+        arr = (C.c_uint32 * max(1, len(segments)))(*segments) if segments else None
+        cap = 8 * len(data) + 4 * 65536 + 4096
+        buf = C.create_string_buffer(cap)
+        st = C.c_int(0)
+        n = self.L.zp_consume(self.h, self.kind, data, len(data), arr, len(segments) if segments else 0, buf, cap,
+                              C.byref(st))
+        if n < 0:
+            raise RuntimeError('zp_consume: output room')
+        return buf.raw[:n], st.value
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.L.zp_free(self.h, self.kind)
+            self.h = None
+
+    def __del__(self):
+        self.close()

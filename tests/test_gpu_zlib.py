@@ -332,3 +332,56 @@ def test_inflate_slot_reuse_after_reset():
     assert ctx.consume_many([(0, b), (1, a[:10])]) == [(b'second stream ' * 70, 1), (head, 0)]
     assert ctx.consume_many([(1, a[10:])]) == [((b'first stream ' * 50)[len(head):], 1)]
     ctx.close()
+
+
+# ------------------------------------------------- drop-in classes (adapter)
+def test_dropin_classes_vs_reference_pipes():
+    """integration/zlib_pipes_xcgpu.cc -- the engine-backed DeflatePipe /
+    InflatePipe bodies -- against the reference's own classes
+    (zlib/deflate_pipe.cc, zlib/inflate_pipe.cc compiled from /root/reference),
+    both driven through oracle/zpipe_driver.cc with the same Buffers: every
+    level 0-9, random segmentations (level 0's blocks follow them), consumes
+    whose flush call stops at the 64 KiB buffer, pipes created and destroyed
+    while others live (slot reuse), and the inflate side on the same bytes."""
+    from oracle.zlib_pipe import ReferencePipes
+    ref, gpu = ReferencePipes('ref'), ReferencePipes('dropin')
+    rng = random.Random(71)
+    streams = (cases(72, 6) + fast_cases(73, 4) + stored_cases(74, 4) + stop_cases(75, (0, 1, 6), range(5, 270, 88)))
+    for si, (level, calls) in enumerate(streams):
+        a, b = gpu.pipe('deflate', level), ref.pipe('deflate', level)
+        z = []
+        for k, c in enumerate(calls):
+            segs = None
+            if c and rng.random() < 0.6:
+                segs, t = [], 0
+                while t < len(c):
+                    segs.append(min(rng.randint(1, 2048), len(c) - t))
+                    t += segs[-1]
+            g, e = a.consume(c, segs), b.consume(c, segs)
+            assert g == e, (si, level, k, len(c), len(g[0]), len(e[0]))
+            z.append(g[0])
+        if calls and not calls[-1]:
+            zz = b''.join(z)
+            cut = [zz[i:i + rng.choice([1, 700, 3000, 65536])] for i in range(0, len(zz), 3000)]
+            ia, ib = gpu.pipe('inflate'), ref.pipe('inflate')
+            for x in cut:
+                assert ia.consume(x) == ib.consume(x), (si, len(x))
+            assert ia.consume(b'') == ib.consume(b'') == (b'', 1)
+            ia.close()
+            ib.close()
+        a.close()
+        b.close()
+
+
+def test_dropin_pool_grows_past_one_context():
+    """More live DeflatePipes than one context's 4096 slots: the adapter's pool
+    adds a context (no HALT); pipes on both contexts match the reference."""
+    from oracle.zlib_pipe import ReferencePipes
+    gpu, ref = ReferencePipes('dropin'), ReferencePipes('ref')
+    pipes = [gpu.pipe('deflate', 6) for _ in range(4100)]
+    rng = random.Random(5)
+    for i in (0, 4095, 4096, 4099):
+        data = gen_bytes(rng, 5000)
+        assert pipes[i].consume(data) == ref.pipe('deflate', 6).consume(data), i
+    for p in pipes:
+        p.close()

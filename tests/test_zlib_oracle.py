@@ -193,3 +193,38 @@ def test_stored_golden():
         for c, e in zip(calls, rec['calls']):
             got = p.consume(c)
             assert len(got) == e['out_len'] and hashlib.sha256(got).hexdigest() == e['out_sha256']
+
+
+# ---------------------------------------------------------- reference pipes
+def _ref_available():
+    return os.path.exists(os.path.join(ROOT, 'oracle/_ref/libzpref.so'))
+
+
+@pytest.mark.skipif(not _ref_available(), reason='oracle/_ref/libzpref.so not built')
+def test_checker_is_the_reference_pipe():
+    """DeflatePipeRef (oracle/deflate_pipe_ref.c, the loop of deflate_pipe.cc:
+    57-115 restated over the system zlib) equals the reference's own
+    DeflatePipe class (zlib/deflate_pipe.cc compiled from /root/reference,
+    oracle/_ref/libzpref.so) call by call, at every level, on random Buffer
+    segmentations; and the reference InflatePipe produces zlib's inflate."""
+    from oracle.zlib_pipe import ReferencePipes
+    R = ReferencePipes('ref')
+    rng = random.Random(17)
+    streams = (cases(57, 8) + fast_cases(58, 6) + stored_cases(59, 6) +
+               stop_cases(60, (2, 5), range(0, 270, 90)))
+    for level, calls in streams:
+        a, b = R.pipe('deflate', level), DeflatePipeRef(level)
+        z = []
+        for c in calls:
+            segs = _segments(rng, len(c)) if c and rng.random() < 0.6 else None
+            got, st = a.consume(c, segs)
+            assert got == b.consume(c, segs), (level, len(c))
+            assert st == (0 if c else 1)
+            z.append(got)
+        if calls and not calls[-1]:
+            inf, ref = R.pipe('inflate'), InflatePipeRef()
+            zz = b''.join(z)
+            cut = [zz[i:i + 3000] for i in range(0, len(zz), 3000)]
+            out = b''.join(inf.consume(x)[0] for x in cut)
+            assert out == b''.join(ref.consume(x) for x in cut) == b''.join(calls)
+            assert inf.consume(b'') == (b'', 1)

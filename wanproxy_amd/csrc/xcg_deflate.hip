@@ -1708,6 +1708,12 @@ struct xcg_zdeflate {
   size_t h_changed_cap = 0;
   uint32_t last_rounds = 0;
   std::vector<StoredPlan> splan;   // level 0: zlib's control state per stream (host, lengths only)
+  // host-buffer calls (xcg_zdeflate_host: the drop-in DeflatePipe::consume):
+  // kept staging and a private stream, one synchronisation per call
+  hipStream_t hst = nullptr;
+  uint8_t* hs_h = nullptr;         // pinned
+  uint8_t* hs_d = nullptr;
+  size_t hs_hcap = 0, hs_dcap = 0;
 };
 
 namespace {
@@ -1776,6 +1782,9 @@ void xcg_zdeflate_destroy(xcg_zdeflate* z) {
   (void)hipFree(z->hist);
   (void)hipFree(z->ring);
   if (z->h_changed) (void)hipHostFree(z->h_changed);
+  if (z->hs_h) (void)hipHostFree(z->hs_h);
+  (void)hipFree(z->hs_d);
+  if (z->hst) (void)hipStreamDestroy(z->hst);
   (void)hipFree(z->scratch);
   (void)hipFree(z->meta);
   if (z->h_meta) (void)hipHostFree(z->h_meta);
@@ -2026,8 +2035,9 @@ int xcg_zdeflate_batch(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t* h_i
 int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
                       const uint32_t* h_stream, uint32_t n, const uint32_t* h_seg, const uint32_t* h_nseg,
                       uint8_t* h_out, const uint64_t* h_out_off, uint32_t* h_out_len, uint64_t* h_deliver) {
-  if (!z || n == 0 || !h_deliver) return XCG_EINVAL;
+  if (!z || n == 0 || !h_deliver || !h_out_len || !h_in_off || !h_len) return XCG_EINVAL;
   (void)hipSetDevice(z->device);
+  if (!z->hst && hipStreamCreateWithFlags(&z->hst, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
   uint64_t in_end = 0, out_end = 0;
   std::vector<uint64_t> doff(n);
   for (uint32_t i = 0; i < n; i++) {
@@ -2035,28 +2045,24 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
     doff[i] = out_end;
     out_end += al(xcg_zdeflate_bound(h_len[i]), 4);
   }
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  uint32_t* d_len = nullptr;
-  uint64_t* d_dl = nullptr;
-  int rc = XCG_OK;
-  if (hipMalloc(&d_in, in_end + 1) != hipSuccess || hipMalloc(&d_out, out_end) != hipSuccess ||
-      hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_dl, 8ull * n) != hipSuccess) {
-    rc = XCG_ENOMEM;
-  }
-  if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
-  if (!rc)
-    rc = xcg_zdeflate_batch_seg(z, d_in, h_in_off, h_len, h_stream, n, h_seg, h_nseg, d_out, doff.data(), d_len, d_dl,
-                                nullptr);
-  if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
-  if (!rc && hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
-  if (!rc && hipMemcpy(h_deliver, d_dl, 8ull * n, hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
-  for (uint32_t i = 0; !rc && i < n; i++)
-    if (hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess) rc = XCG_EHIP;
-  (void)hipFree(d_in);
-  (void)hipFree(d_out);
-  (void)hipFree(d_len);
-  (void)hipFree(d_dl);
-  return rc;
+  // staging: [in][out][out_len n][deliver n]
+  const size_t o_out = al(in_end + 1, 256), o_len = al(o_out + out_end, 256), o_dl = al(o_len + 4ull * n, 256),
+               o_end = al(o_dl + 8ull * n, 256);
+  if (grow((void**)&z->hs_h, &z->hs_hcap, o_end, true) || grow((void**)&z->hs_d, &z->hs_dcap, o_end, false))
+    return XCG_ENOMEM;
+  if (in_end) memcpy(z->hs_h, h_in, in_end);
+  if (in_end && hipMemcpyAsync(z->hs_d, z->hs_h, in_end, hipMemcpyHostToDevice, z->hst) != hipSuccess) return XCG_EHIP;
+  int rc = xcg_zdeflate_batch_seg(z, z->hs_d, h_in_off, h_len, h_stream, n, h_seg, h_nseg, z->hs_d + o_out,
+                                  doff.data(), (uint32_t*)(z->hs_d + o_len), (uint64_t*)(z->hs_d + o_dl), z->hst);
+  if (rc != XCG_OK) return rc;
+  // the outputs' room (<= 1.5x the input) comes back with the lengths: one synchronisation
+  if (hipMemcpyAsync(z->hs_h + o_out, z->hs_d + o_out, o_end - o_out, hipMemcpyDeviceToHost, z->hst) != hipSuccess ||
+      hipStreamSynchronize(z->hst) != hipSuccess)
+    return XCG_EHIP;
+  memcpy(h_out_len, z->hs_h + o_len, 4ull * n);
+  memcpy(h_deliver, z->hs_h + o_dl, 8ull * n);
+  for (uint32_t i = 0; i < n; i++) memcpy(h_out + h_out_off[i], z->hs_h + o_out + doff[i], h_out_len[i]);
+  return XCG_OK;
 }
 
 #ifdef XCG_ZD_TIMING

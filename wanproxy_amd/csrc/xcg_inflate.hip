@@ -685,6 +685,12 @@ struct xcg_zinflate {
   void* h_meta = nullptr;
   size_t h_meta_cap = 0;
   hipEvent_t done = nullptr;
+  // host-buffer calls (xcg_zinflate_host: the drop-in InflatePipe::consume):
+  // kept staging and a private stream
+  hipStream_t hst = nullptr;
+  uint8_t* hs_h = nullptr;         // pinned
+  uint8_t* hs_d = nullptr;
+  size_t hs_hcap = 0, hs_dcap = 0;
 };
 
 namespace {
@@ -744,6 +750,9 @@ void xcg_zinflate_destroy(xcg_zinflate* z) {
   (void)hipFree(z->meta);
   if (z->h_meta) (void)hipHostFree(z->h_meta);
   if (z->done) (void)hipEventDestroy(z->done);
+  if (z->hs_h) (void)hipHostFree(z->hs_h);
+  (void)hipFree(z->hs_d);
+  if (z->hst) (void)hipStreamDestroy(z->hst);
   delete z;
 }
 
@@ -816,8 +825,9 @@ int xcg_zinflate_reset(xcg_zinflate* z, uint32_t stream) {
 int xcg_zinflate_host(xcg_zinflate* z, const uint8_t* h_in, const uint64_t* h_in_off, const uint32_t* h_len,
                       const uint32_t* h_stream, uint32_t n, uint8_t* h_out, const uint64_t* h_out_off,
                       const uint32_t* h_out_cap, uint32_t* h_out_len, int32_t* h_status) {
-  if (!z || n == 0) return XCG_EINVAL;
+  if (!z || n == 0 || !h_in_off || !h_len || !h_out_cap || !h_out_len || !h_status) return XCG_EINVAL;
   (void)hipSetDevice(z->device);
+  if (!z->hst && hipStreamCreateWithFlags(&z->hst, hipStreamNonBlocking) != hipSuccess) return XCG_EHIP;
   uint64_t in_end = 0, out_end = 0;
   std::vector<uint64_t> doff(n);
   for (uint32_t i = 0; i < n; i++) {
@@ -825,27 +835,31 @@ int xcg_zinflate_host(xcg_zinflate* z, const uint8_t* h_in, const uint64_t* h_in
     doff[i] = out_end;
     out_end += ial(h_out_cap[i] ? h_out_cap[i] : 1, 4);
   }
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  uint32_t* d_len = nullptr;
-  int32_t* d_st = nullptr;
-  int rc = XCG_OK;
-  if (hipMalloc(&d_in, in_end + 1) != hipSuccess || hipMalloc(&d_out, out_end) != hipSuccess ||
-      hipMalloc(&d_len, 4ull * n) != hipSuccess || hipMalloc(&d_st, 4ull * n) != hipSuccess)
-    rc = XCG_ENOMEM;
-  if (!rc && in_end && hipMemcpy(d_in, h_in, in_end, hipMemcpyHostToDevice) != hipSuccess) rc = XCG_EHIP;
-  if (!rc) rc = xcg_zinflate_batch(z, d_in, h_in_off, h_len, h_stream, n, d_out, doff.data(), h_out_cap, d_len, d_st, nullptr);
-  if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) rc = XCG_EHIP;
-  if (!rc && (hipMemcpy(h_out_len, d_len, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess ||
-              hipMemcpy(h_status, d_st, 4ull * n, hipMemcpyDeviceToHost) != hipSuccess))
-    rc = XCG_EHIP;
-  for (uint32_t i = 0; !rc && i < n; i++)
-    if (h_out_len[i] && hipMemcpy(h_out + h_out_off[i], d_out + doff[i], h_out_len[i], hipMemcpyDeviceToHost) != hipSuccess)
-      rc = XCG_EHIP;
-  (void)hipFree(d_in);
-  (void)hipFree(d_out);
-  (void)hipFree(d_len);
-  (void)hipFree(d_st);
-  return rc;
+  // staging: [len n][status n][in][out]
+  const size_t o_st = ial(4ull * n, 256), o_in = ial(o_st + 4ull * n, 256), o_out = ial(o_in + in_end + 1, 256),
+               o_end = ial(o_out + out_end, 256);
+  if (igrow((void**)&z->hs_h, &z->hs_hcap, o_end, true) || igrow((void**)&z->hs_d, &z->hs_dcap, o_end, false))
+    return XCG_ENOMEM;
+  if (in_end) memcpy(z->hs_h + o_in, h_in, in_end);
+  if (in_end && hipMemcpyAsync(z->hs_d + o_in, z->hs_h + o_in, in_end, hipMemcpyHostToDevice, z->hst) != hipSuccess)
+    return XCG_EHIP;
+  int rc = xcg_zinflate_batch(z, z->hs_d + o_in, h_in_off, h_len, h_stream, n, z->hs_d + o_out, doff.data(), h_out_cap,
+                              (uint32_t*)z->hs_d, (int32_t*)(z->hs_d + o_st), z->hst);
+  if (rc != XCG_OK) return rc;
+  if (hipMemcpyAsync(z->hs_h, z->hs_d, o_in, hipMemcpyDeviceToHost, z->hst) != hipSuccess ||
+      hipStreamSynchronize(z->hst) != hipSuccess)
+    return XCG_EHIP;
+  memcpy(h_out_len, z->hs_h, 4ull * n);
+  memcpy(h_status, z->hs_h + o_st, 4ull * n);
+  // the outputs: only what was produced (the room is up to 8x the input)
+  for (uint32_t i = 0; i < n; i++)
+    if (h_out_len[i] && hipMemcpyAsync(z->hs_h + o_out + doff[i], z->hs_d + o_out + doff[i], h_out_len[i],
+                                       hipMemcpyDeviceToHost, z->hst) != hipSuccess)
+      return XCG_EHIP;
+  if (hipStreamSynchronize(z->hst) != hipSuccess) return XCG_EHIP;
+  for (uint32_t i = 0; i < n; i++)
+    if (h_out_len[i]) memcpy(h_out + h_out_off[i], z->hs_h + o_out + doff[i], h_out_len[i]);
+  return XCG_OK;
 }
 
 #ifdef XCG_ZI_TIMING
