@@ -524,13 +524,18 @@ def zlib_stage(streams=2048, steps=3, check=0.25, threads=16):
     zb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(zb)
     out = {}
-    for kind in ('xcodec', 'text'):
-        a = argparse.Namespace(kind=kind, streams=streams, call_bytes=65536, steps=steps, level=6, check=check,
+    for kind, level in (('xcodec', 6), ('text', 6), ('text', 1)):
+        a = argparse.Namespace(kind=kind, streams=streams, call_bytes=65536, steps=steps, level=level, check=check,
                                cpu_threads=threads)
         try:
-            out[kind] = zb.run(a)
+            out[kind if level == 6 else f'{kind}_level{level}'] = zb.run(a)
         except BaseException as e:
-            out[kind] = {'error': f'{type(e).__name__}: {e}'}
+            out[kind if level == 6 else f'{kind}_level{level}'] = {'error': f'{type(e).__name__}: {e}'}
+    # the drop-in classes one consume at a time (wanproxy's call pattern) beside the reference's
+    try:
+        out['per_call'] = {k: zb.per_call(k, 6, 256) for k in ('xcodec', 'text')}
+    except BaseException as e:
+        out['per_call'] = {'error': f'{type(e).__name__}: {e}'}
     return out
 
 

@@ -384,6 +384,10 @@ int xcg_zdeflate_host(xcg_zdeflate *z, const uint8_t *h_in, const uint64_t *h_in
                       const uint32_t *h_stream, uint32_t n, const uint32_t *h_seg, const uint32_t *h_nseg,
                       uint8_t *h_out, const uint64_t *h_out_off, uint32_t *h_out_len, uint64_t *h_deliver);
 
+/* Diagnostics: parse rounds the last levels 1-3 batch took (deflate_fast's
+ * hashed positions guessed, then reproduced; 0 for other levels). */
+uint32_t xcg_debug_zdeflate_rounds(const xcg_zdeflate *z);
+
 /* Receiving side: `nstreams` InflatePipe instances (zlib/inflate_pipe.cc:33-46,
  * inflateInit) in HBM.  xcg_zinflate_batch: one InflatePipe::consume() per
  * listed stream (at most once per batch): h_len[i] bytes at d_in + h_in_off[i]

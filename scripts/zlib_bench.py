@@ -60,6 +60,47 @@ def zlib_ref(streams_calls, level, threads):
         return list(ex.map(one, streams_calls))
 
 
+def per_call(kind: str = 'xcodec', level: int = 6, calls: int = 256) -> dict:
+    """DeflatePipe::consume / InflatePipe::consume one call at a time, as wanproxy
+    makes them (one per read per connection): the drop-in classes
+    (integration/zlib_pipes_xcgpu.cc over the engine) beside the reference's own
+    classes over the system zlib on this host (zlib/deflate_pipe.cc,
+    inflate_pipe.cc), both through oracle/zpipe_driver.cc, same Buffers; every
+    call's output compared."""
+    from oracle.zlib_pipe import ReferencePipes
+    data = [row[0] for row in workload(kind, 1, 65536, calls)]
+    res = {'kind': kind, 'level': level, 'calls': calls, 'call_bytes': 65536}
+    outs = {}
+    for which in ('dropin', 'ref'):
+        R = ReferencePipes(which)
+        d = R.pipe('deflate', level)
+        zs, t = [], []
+        for k, c in enumerate(data):
+            t0 = time.perf_counter()
+            z, _ = d.consume(c)
+            if k:                                   # (the first call: header, context warm-up)
+                t.append(time.perf_counter() - t0)
+            zs.append(z)
+        i = R.pipe('inflate')
+        back, ti = [], []
+        for k, z in enumerate(zs):
+            t0 = time.perf_counter()
+            o, _ = i.consume(z)
+            if k:
+                ti.append(time.perf_counter() - t0)
+            back.append(o)
+        outs[which] = zs
+        key = 'gpu_dropin' if which == 'dropin' else 'reference_cpu'
+        res[key] = {'deflate_us_per_call': round(1e6 * float(np.median(t)), 1),
+                    'inflate_us_per_call': round(1e6 * float(np.median(ti)), 1),
+                    'inflated_ok': b''.join(data).startswith(b''.join(back))}
+        d.close()
+        i.close()
+    res['checked'] = ('every deflate call equal to the reference class' if outs['dropin'] == outs['ref']
+                      else 'MISMATCH')
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--kind', default='xcodec', choices=['xcodec', 'text'])
@@ -69,7 +110,12 @@ def main():
     ap.add_argument('--level', type=int, default=6)
     ap.add_argument('--check', type=float, default=1.0, help='fraction of streams checked against zlib')
     ap.add_argument('--cpu-threads', type=int, default=16)
-    res = run(ap.parse_args())
+    ap.add_argument('--per-call', action='store_true', help='the drop-in classes one consume at a time vs the reference')
+    args = ap.parse_args()
+    if args.per_call:
+        print(json.dumps(per_call(args.kind, args.level, 256)))
+        return
+    res = run(args)
     print(json.dumps(res))
     if res.get('mismatches') or 'MISMATCH' in res['inflate']['checked']:
         sys.exit(1)
@@ -92,12 +138,13 @@ def run(args) -> dict:
     d_len = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(K)]
     d_dl = [torch.zeros(S, dtype=torch.int64, device=dev) for _ in range(K)]
     torch.cuda.synchronize()
-    times = []
+    times, rounds = [], []
     for k in range(K):
         t0 = time.perf_counter()
         ctx.batch_device(d_ins[k], in_off, lens, sids, d_out[k], out_off, d_len[k], d_dl[k])
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
+        rounds.append(ctx.last_rounds)
     # what each consume produces: the stream's undelivered bytes, then the new ones, cut at d_deliver
     outs, held = [], [b''] * S
     for k in range(K):
@@ -170,6 +217,7 @@ def run(args) -> dict:
         'kind': args.kind, 'level': args.level, 'streams': S, 'call_bytes': B, 'steps': K,
         'value': round(in_bytes / (ms / 1e3) / 2**30, 3), 'ms_per_step': round(ms, 3),
         'out_in': round(out_bytes / in_bytes, 5),
+        'parse_rounds': rounds if args.level in (1, 2, 3) else None,
         'checked': f'{nchk} of {S} streams x {K} calls vs zlib {zlib.ZLIB_RUNTIME_VERSION}, {bad} mismatches',
         'mismatches': bad,
         'inflate': {'GiBps': round(in_bytes / (zi_ms / 1e3) / 2**30, 3), 'ms_per_step': round(zi_ms, 3),

@@ -2065,6 +2065,8 @@ int xcg_zdeflate_host(xcg_zdeflate* z, const uint8_t* h_in, const uint64_t* h_in
   return XCG_OK;
 }
 
+uint32_t xcg_debug_zdeflate_rounds(const xcg_zdeflate* z) { return z ? z->last_rounds : 0; }
+
 #ifdef XCG_ZD_TIMING
 int xcg_debug_zd_times(uint64_t* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zd_t), 8 * 16) != hipSuccess) return XCG_EHIP;

@@ -44,6 +44,8 @@ def _lib():
         L.xcg_zdeflate_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.xcg_zdeflate_batch_seg.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]
         L.xcg_zdeflate_batch_seg.restype = C.c_int
+        L.xcg_debug_zdeflate_rounds.argtypes = [vp]
+        L.xcg_debug_zdeflate_rounds.restype = C.c_uint32
         L.xcg_zdeflate_host.restype = C.c_int
         L.xcg_zinflate_create.argtypes = [C.c_int, C.c_uint32, C.POINTER(vp)]
         L.xcg_zinflate_create.restype = C.c_int
@@ -86,6 +88,11 @@ class DeflatePipes:
     def reset(self, stream: int):
         _check(_lib().xcg_zdeflate_reset(self.h, stream))
         self.undelivered.pop(stream, None)
+
+    @property
+    def last_rounds(self) -> int:
+        """levels 1-3: parse rounds the last batch took"""
+        return int(_lib().xcg_debug_zdeflate_rounds(self.h))
 
     def pipe(self, stream: int) -> 'DeflatePipe':
         return DeflatePipe(self, stream)
