@@ -248,11 +248,17 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	if (win == NULL)
 		HALT(log_) << "No device memory for the XCodec window.";
 
+	/* call scratch kept across calls (a std::vector zero-fills what it grows:
+	 * per call that was 512 KiB of unknown-hash room alone) */
+	static thread_local std::vector<uint8_t> in, out;
+	static thread_local std::vector<uint64_t> unk, ext;
 	const uint64_t len = input->length();
-	std::vector<uint8_t> in(len);
+	in.resize(len);			/* (shrinking keeps the storage; growing fills only the new tail) */
 	input->copyout(&in[0], len);
-	std::vector<uint8_t> out;
-	std::vector<uint64_t> unk(1u << 16), ext(1024);
+	if (unk.size() < (1u << 16)) {
+		unk.resize(1u << 16);
+		ext.resize(1024);
+	}
 	std::vector<uint64_t> piece, coff, ooff, olen, cons;
 	std::vector<uint32_t> clen;
 	std::vector<int32_t> cst;

@@ -1397,16 +1397,17 @@ int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_ou
     if (rc != XCG_OK) return rc;
     const uint32_t ops_cap = len / 4 + 64;
     const uint32_t rw = xcg_decode_small_res_words();
-    // device: input | output | results | op lists;  host: input | results | output
-    const size_t inb = align256(len), outb = align256(out_cap ? out_cap : 1), resb = align256(8ull * rw + 8);
+    // device: input | output | results | op lists;  host: input | output | results (one D2H brings
+    // both back; the results' last word is the context's sticky word)
+    const size_t inb = align256(len), outb = align256(out_cap ? out_cap : 1), resb = align256(8ull * rw);
     const size_t scr = align256(xcg_decode_small_scratch(ops_cap));
-    rc = ensure_stage(c, inb + outb + resb + scr, inb + resb + outb);
+    rc = ensure_stage(c, inb + outb + resb + scr, inb + outb + resb);
     if (rc != XCG_OK) return rc;
     uint8_t* dm = c->stage_d;
     uint8_t* hm = c->stage_h;
     uint64_t* d_res = (uint64_t*)(dm + inb + outb);
-    uint64_t* h_res = (uint64_t*)(hm + inb);
-    uint8_t* h_o = hm + inb + resb;
+    uint64_t* h_res = (uint64_t*)(hm + inb + outb);
+    uint8_t* h_o = hm + inb;
     const hipStream_t st = c->call_st;
     memcpy(hm, h_in, len);
     ctx_order(c, st);
@@ -1416,13 +1417,11 @@ int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_ou
                                 c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->d_status,
                                 dm + inb + outb + resb, ops_cap, dm + inb, out_cap, w->hash, w->seg, w->count,
                                 d_res, st) != 0 ||
-        hipMemcpyAsync(h_res, d_res, 8ull * rw, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_res + rw, c->d_status, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        (out_cap && hipMemcpyAsync(h_o, dm + inb, out_cap, hipMemcpyDeviceToHost, st) != hipSuccess))
+        hipMemcpyAsync(h_o, dm + inb, outb + 8ull * rw, hipMemcpyDeviceToHost, st) != hipSuccess)
       return XCG_EHIP;
     ctx_mark(c, st);
     if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
-    if (*(const int32_t*)(h_res + rw)) return XCG_EOVERFLOW;   // (cache capacity: the sticky word)
+    if ((uint32_t)h_res[rw - 1]) return XCG_EOVERFLOW;   // (cache capacity: the sticky word)
     if (h_res[5] == 2) {
       *h_out_len = h_res[7];
       return XCG_EOVERFLOW;

@@ -937,6 +937,10 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* src, const uin
 // SD_XSLOTS / 2 EXTRACTs or SD_UMAX unknown hashes -- sets `fallback` before
 // anything is written; the host then takes the batch path.
 constexpr uint32_t SD_XSLOTS = 2048, SD_USLOTS = 4096, SD_UMAX = 2048, SD_EMAX = 1024;
+// A call's input up to this size is staged in LDS first (with the tables:
+// 80 KiB + 78 KiB of the 160 KiB): the op walk is a chain of dependent reads,
+// one per op, that would each wait on HBM.
+constexpr uint32_t SD_LDS_IN = 80000;
 constexpr uint32_t SD_LIT = 0, SD_EXT = 1, SD_REF = 2;
 
 struct SmallDec {
@@ -959,7 +963,8 @@ struct SmallDec {
   uint64_t win_count;
   uint64_t* res;               // [0] out_len [1] consumed [2] status [3] declares before the stop
                                // [4] unknowns [5] fallback [6] EXTRACTs before the stop [7] decoded size
-                               // then SD_UMAX unknown hashes, then SD_EMAX EXTRACT hashes (op order)
+                               // then SD_UMAX unknown hashes, then SD_EMAX EXTRACT hashes (op order),
+                               // then the context's sticky word
 };
 
 __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
@@ -968,13 +973,24 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   __shared__ uint32_t s_nops, s_ndecl, s_next, s_nunk, s_fb, s_walk_st, s_walk_end;
   __shared__ uint64_t s_stop;  // (position << 32) | declare number of the first unknown REF
   __shared__ uint64_t s_olen;
+  __shared__ uint4 xin[SD_LDS_IN / 16];
   const uint32_t t = threadIdx.x, w = t >> 6;
   const int l = lane_id();
-  const uint8_t* x = a.in;
   const uint32_t len = a.len;
+  const uint8_t* x = a.in;
+  if (len <= SD_LDS_IN) {                                    // stage the input (coalesced 16-byte loads)
+    const uint32_t nv = len / 16;
+    for (uint32_t i = t; i < nv; i += 1024) xin[i] = ((const uint4*)a.in)[i];
+    uint8_t* xb = (uint8_t*)xin;
+    for (uint32_t i = nv * 16 + t; i < len; i += 1024) xb[i] = a.in[i];
+    x = xb;
+  }
   for (uint32_t i = t; i < SD_XSLOTS; i += 1024) { xk[i] = EMPTY_KEY; xf[i] = ~0ull; xl[i] = 0; }
   for (uint32_t i = t; i < SD_USLOTS; i += 1024) uk[i] = EMPTY_KEY;
-  if (t == 0) { s_nunk = 0; s_fb = 0; s_stop = ~0ull; s_next = 0; }
+  if (t == 0) {
+    s_nunk = 0; s_fb = 0; s_stop = ~0ull; s_next = 0;
+    a.res[8 + SD_UMAX + SD_EMAX] = (uint64_t)(uint32_t)*a.status;   // (the paths that return early)
+  }
   // ---- walk (wave 0): op list, output offsets, declare numbers
   if (w == 0) {
     uint32_t i = 0, k = 0, dn = 0, st = 0, fb = 0;
@@ -1223,6 +1239,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     }
     if (l == 0) {
       const int32_t wst = (int32_t)s_walk_st;
+      a.res[8 + SD_UMAX + SD_EMAX] = (uint64_t)(uint32_t)*a.status;
       a.res[0] = out_len;
       a.res[1] = stop != ~0ull ? stop_pos : s_walk_end;
       a.res[2] = (uint64_t)(int64_t)(stop != ~0ull ? 1 : wst);
@@ -1618,4 +1635,4 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
 }
 
 extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap) { return 40ull * ops_cap; }
-extern "C" uint32_t xcg_decode_small_res_words(void) { return 8 + xcg::SD_UMAX + xcg::SD_EMAX; }
+extern "C" uint32_t xcg_decode_small_res_words(void) { return 8 + xcg::SD_UMAX + xcg::SD_EMAX + 1; }
