@@ -12,7 +12,11 @@ int main(int argc, char** argv) {
   XcgPairState* P = new XcgPairState;
   P->C = C; P->nb = nb; P->D = D;
   P->ps.assign(C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
-  P->ds.assign(D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0});
+  XcgDiskState* K = new XcgDiskState;
+  K->nb = nb; K->D = D;
+  K->ds.assign(D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0, 0, 0});
+  K->fronts.push_back(P);
+  P->disk = K; P->dsp = &K->ds; P->xuid = 0;
   P->es.assign(ids, Ent{NEVER, 0, NIL, NIL, 0});
   P->pfree.resize(C);
   for (uint32_t s = 0; s < C; ++s) P->pfree[s] = C - 1 - s;
@@ -26,7 +30,7 @@ int main(int argc, char** argv) {
     // chunk c: ~52 declarations, ~8 lookups of cached hashes (the sub-batch start state)
     std::vector<uint32_t> live;
     for (uint32_t s = 0; s < C; ++s) if (P->ps[s].key != NOKEY) live.push_back(s);
-    for (uint32_t i = 0; i < D; ++i) if (P->ds[i].live && P->ds[i].dp == NIL) live.push_back(C + i);
+    for (uint32_t i = 0; i < D; ++i) if (P->ds()[i].live && P->ds()[i].dp == NIL) live.push_back(C + i);
     for (uint32_t c = 0; c < n; ++c) {
       uint32_t k = 0, d = 0;
       for (uint32_t w = 0; w < 60; ++w) {

@@ -940,7 +940,7 @@ constexpr uint32_t SD_XSLOTS = 2048, SD_USLOTS = 4096, SD_UMAX = 2048, SD_EMAX =
 // A call's input up to this size is staged in LDS first (with the tables:
 // 80 KiB + 78 KiB of the 160 KiB): the op walk is a chain of dependent reads,
 // one per op, that would each wait on HBM.
-constexpr uint32_t SD_LDS_IN = 80000;
+constexpr uint32_t SD_LDS_IN = 76000;
 constexpr uint32_t SD_LIT = 0, SD_EXT = 1, SD_REF = 2;
 
 struct SmallDec {
@@ -974,6 +974,9 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   __shared__ uint64_t s_stop;  // (position << 32) | declare number of the first unknown REF
   __shared__ uint64_t s_olen;
   __shared__ uint4 xin[SD_LDS_IN / 16];
+  __shared__ uint16_t xlist[SD_XSLOTS / 2];                  // the occupied EXTRACT slots
+  __shared__ uint16_t wcopy[256];                            // window slots that take a new segment
+  __shared__ uint32_t s_nx, s_nw;
   const uint32_t t = threadIdx.x, w = t >> 6;
   const int l = lane_id();
   const uint32_t len = a.len;
@@ -1069,11 +1072,16 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       atomicAdd(&s_next, 1u);
     }
   }
+  if (t == 0) { s_nx = 0; s_nw = 0; }
   __syncthreads();
   if (s_next > SD_XSLOTS / 2) {
     if (t == 0) a.res[5] = 1;
     return;
   }
+  // occupied slots of the EXTRACT table, once (the precheck and the commit walk
+  // only these instead of all SD_XSLOTS)
+  for (uint32_t i = t; i < SD_XSLOTS; i += 1024)
+    if (xk[i] != EMPTY_KEY) xlist[atomicAdd(&s_nx, 1u)] = (uint16_t)i;
   // ---- resolve every REF (a thread per op): an earlier EXTRACT of the call,
   // else the cache; else unknown (:151-156; decode_skim's set, :196-272)
   for (uint32_t k = t; k < nops; k += 1024) {
@@ -1128,8 +1136,9 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   }
   // ---- what the batch decoder refuses (dec_precheck_kernel): several EXTRACTs
   // of one hash before the stop with other bytes, or on both sides of it
-  for (uint32_t i = w; i < SD_XSLOTS; i += 16) {
-    if (xk[i] == EMPTY_KEY) continue;
+  const uint32_t nx = s_nx;
+  for (uint32_t q = w; q < nx; q += 16) {
+    const uint32_t i = xlist[q];
     const uint64_t f = xf[i], z = xl[i];
     if (f >= stop_pos || z == f) continue;
     bool bad = z >= stop_pos;
@@ -1167,8 +1176,51 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     }
   }
   // ---- the BACKREF window after the call's declares (before the commit
-  // overwrites any pool bytes a REF's declare reads)
-  {
+  // overwrites any pool bytes a REF's declare reads).  Up to 256 declares: a
+  // thread per slot against the call's declared hashes in LDS (uk is free
+  // again); only slots this call declares into take a segment; an older slot
+  // whose hash the call declares again is emptied (XCodecWindow::declare,
+  // xcodec_window.h:68-90).  More declares: window_slot per slot.
+  if (T > 0 && T <= 256) {
+    for (uint32_t i = t; i < T; i += 1024) {
+      const uint4 d = a.D[i];
+      uk[i] = ((uint64_t)d.y << 32) | d.x;
+    }
+    __syncthreads();
+    if (t < 256) {
+      const uint32_t c = t;
+      const uint64_t W = a.win_count, G = W + T;
+      const uint64_t r = (G - 1u - c) & 255u;
+      if (r <= G - 1u) {                                     // (else never written)
+        const uint64_t g = G - 1u - r;
+        if (g >= W) {
+          const uint32_t tl = (uint32_t)(g - W);
+          const uint64_t h = uk[tl];
+          bool dup = false;
+          for (uint32_t k = tl + 1; k < T; ++k) dup |= uk[k] == h;
+          if (dup) {
+            a.win_hash[c] = 0;
+          } else {
+            a.win_hash[c] = h;
+            wcopy[atomicAdd(&s_nw, 1u)] = (uint16_t)(c | (tl << 8));   // (tl < 256)
+          }
+        } else {
+          const uint64_t h = a.win_hash[c];
+          if (h != 0) {
+            bool dup = false;
+            for (uint32_t k = 0; k < T; ++k) dup |= uk[k] == h;
+            if (dup) a.win_hash[c] = 0;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = w; q < s_nw; q += 16) {
+      const uint32_t e = wcopy[q], c = e & 255u, tl = e >> 8;
+      const uint4 d = a.D[tl];
+      wave_copy2048(a.win_seg + (uint64_t)c * SEG, (const uint8_t*)(((uint64_t)d.w << 32) | d.z));
+    }
+  } else {
     DecParams prm{};
     prm.D = a.D;
     prm.D_lo = 0;
@@ -1193,9 +1245,9 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   __syncthreads();
   // ---- commit: EXTRACTs before the stop enter the cache, or replace a cached
   // segment's bytes (name reuse, :106-136)
-  for (uint32_t i = w; i < SD_XSLOTS; i += 16) {
+  for (uint32_t q = w; q < nx; q += 16) {
+    const uint32_t i = xlist[q];
     const uint64_t key = xk[i];
-    if (key == EMPTY_KEY) continue;
     const uint64_t f = xf[i];
     if (f >= stop_pos) continue;
     const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
