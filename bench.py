@@ -192,7 +192,8 @@ def pmc_traffic(n):
     summary (scripts/profile.sh + scripts/prof_summary.py: FETCH_SIZE doubled
     per MI355X_MICROARCH.md "HBM", plus WRITE_SIZE), when it was taken on this
     same workload; PMC counters cannot be read from inside the timed run."""
-    for name in ('r02_c2_independent_summary.json', 'r01_c2_independent_summary.json'):
+    for name in ('r03_c2_independent_summary.json', 'r02_c2_independent_summary.json',
+                 'r01_c2_independent_summary.json'):
         p = os.path.join(ROOT, 'profiles', name)
         if n != NCHUNKS or not os.path.exists(p):
             continue
@@ -205,13 +206,14 @@ def pmc_traffic(n):
 def pmc_stream_traffic():
     """HBM bytes of the seeded C2-S2 stream-parse launch (the bench's S2 step)
     from the committed scripts/profile_stream.sh summary."""
-    p = os.path.join(ROOT, 'profiles', 'r02_stream_pmc_summary.json')
-    if not os.path.exists(p):
-        return None, None
-    g = json.load(open(p)).get('c2s_seeded', {})
-    if 'hbm_bytes' not in g:
-        return None, None
-    return int(g['hbm_bytes'] / max(1, g['dispatches'])), 'profiles/r02_stream_pmc_summary.json c2s_seeded (rocprofv3 --pmc)'
+    for name in ('r03_stream_pmc_summary.json', 'r02_stream_pmc_summary.json'):
+        p = os.path.join(ROOT, 'profiles', name)
+        if not os.path.exists(p):
+            continue
+        g = json.load(open(p)).get('c2s_seeded', {})
+        if 'hbm_bytes' in g:
+            return int(g['hbm_bytes'] / max(1, g['dispatches'])), f'profiles/{name} c2s_seeded (rocprofv3 --pmc)'
+    return None, None
 
 
 def timed(fn, steps, stream, kernel_time=False):

@@ -38,4 +38,21 @@ if 'FETCH_SIZE' in out and 'WRITE_SIZE' in out:
     out['hbm_traffic_bytes_per_launch'] = out['hbm_read_bytes_corrected'] + out['hbm_write_bytes']
     if 'avg_ns' in out:
         out['hbm_GBps'] = out['hbm_traffic_bytes_per_launch'] / out['avg_ns']
+# the headline launch alone (the 4096-chunk batch: the largest grid in the trace);
+# run_kernel_stats also counts the host-inclusive sub-batch launches
+import glob  # noqa: E402
+tr = glob.glob(os.path.join(src, 'trace', '**', 'run_kernel_trace.csv'), recursive=True)
+if tr:
+    rows = [r for r in csv.DictReader(open(tr[0])) if kname in r['Kernel_Name']]
+    if rows:
+        gmax = max(int(r['Grid_Size_X']) for r in rows)
+        full = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) for r in rows if int(r['Grid_Size_X']) == gmax]
+        out['avg_ns_full_batch'] = sum(full) / len(full)
+        out['calls_full_batch'] = len(full)
+        out['grid_full_batch'] = gmax
+        if 'hbm_traffic_bytes_per_launch' in out:
+            out['hbm_GBps_full_batch'] = out['hbm_traffic_bytes_per_launch'] / out['avg_ns_full_batch']
+        out['note'] = ('avg_ns / calls include the host-inclusive sub-batch launches; avg_ns_full_batch is the '
+                       'headline launch alone (kernel trace, largest grid); PMC counters come from --no-extras runs '
+                       '(headline launches only)')
 print(json.dumps(out, indent=1))
