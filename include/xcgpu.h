@@ -434,6 +434,13 @@ int xcg_debug_stream_kernel_timing(int on);
  * resuming off (same output). */
 int xcg_debug_restart_counts(xcg_ctx *ctx, uint64_t *resumed, uint64_t *spliced);
 int xcg_debug_stream_kernel_time(double *ms, uint32_t *launches);
+/* Diagnostics: with env XCG_DECODE_PHASES set, each one-launch decode()
+ * (xcg_decode_call) records clock stamps at its kernel's phase boundaries;
+ * us[0] = summed kernel time, us[k] = summed duration of phase k (1 stage,
+ * 2 walk, 3 EXTRACT hashes, 4 resolve, 5 precheck, 6 output size, 7 output
+ * copy, 8 window, 9 commit, 10 results), microseconds.  Returns (and resets)
+ * the call count. */
+uint32_t xcg_debug_decode_phases(double *us, uint32_t n);
 
 /* Every window hash: d_hash[s] = XCodecHash over d_x[s .. s+2048) for
  * s in [0, len - 2048]. */

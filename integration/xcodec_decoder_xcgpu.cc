@@ -28,6 +28,46 @@
 
 #include "xcgpu_binding.h"
 
+#ifdef XCGPU_ADAPTER_TIMING
+/* (diagnostics build only: per-section host time of decode(), medians over the
+ * calls, printed at exit) */
+#include <stdio.h>
+#include <time.h>
+#include <algorithm>
+namespace {
+struct AdapterTiming {
+	double cur[8] = {0};
+	std::vector<double> t[8];
+	~AdapterTiming() {
+		static const char *nm[8] = {"total", "copyin", "cut", "bound", "engine", "append", "mirror", "other"};
+		if (t[0].empty())
+			return;
+		fprintf(stderr, "decode adapter, median us per call over %zu calls:", t[0].size());
+		for (int k = 0; k < 7; k++) {
+			std::sort(t[k].begin(), t[k].end());
+			fprintf(stderr, " %s %.2f", nm[k], t[k][t[k].size() / 2]);
+		}
+		fprintf(stderr, "\n");
+	}
+} g_at;
+inline double at_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3; }
+inline void at_end(double v) {
+	g_at.cur[0] = v;
+	for (int k = 0; k < 7; k++) {
+		g_at.t[k].push_back(g_at.cur[k]);
+		g_at.cur[k] = 0;
+	}
+}
+}
+#define AT_MARK(v) const double v = at_now()
+#define AT_ADD(k, a, b) ((k) == 0 ? at_end((b) - (a)) : (void)(g_at.cur[k] += (b) - (a)))
+#define AT_CALL() do { } while (0)
+#else
+#define AT_MARK(v) do { } while (0)
+#define AT_ADD(k, a, b) do { } while (0)
+#define AT_CALL() do { } while (0)
+#endif
+
 XCodecDecoder::XCodecDecoder(XCodecCache *cache)
 : log_("/xcodec/decoder"),
   cache_(cache),
@@ -241,6 +281,8 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 {
 	if (input->empty())
 		return (true);
+	AT_MARK(at0);
+	AT_CALL();
 	xcg_ctx *ctx = xcgpu_binding::ctx_for(cache_, cache_->out_of_band());
 	if (ctx == NULL)
 		HALT(log_) << "xcgpu: " << xcgpu_binding::why_not(cache_) << ".";
@@ -254,7 +296,10 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	static thread_local std::vector<uint64_t> unk, ext;
 	const uint64_t len = input->length();
 	in.resize(len);			/* (shrinking keeps the storage; growing fills only the new tail) */
+	AT_MARK(at1);
 	input->copyout(&in[0], len);
+	AT_MARK(at2);
+	AT_ADD(1, at1, at2);
 	if (unk.size() < (1u << 16)) {
 		unk.resize(1u << 16);
 		ext.resize(1024);
@@ -266,6 +311,7 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	int32_t status = 0;
 	uint32_t nunk = 0;
 	xcg_decode_set_window(ctx, win);
+	AT_MARK(at3);
 	/*
 	 * The GPU decodes from pos until the end, a bad op, or a REF its cache
 	 * does not hold.  In the last case the hashes the host cache learned
@@ -278,6 +324,8 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 	 * result.
 	 */
 	cut_pieces(in, pos, piece);
+	AT_MARK(at4);
+	AT_ADD(2, at3, at4);
 	size_t k0 = 0, per = piece.size() - 1;
 	for (;;) {
 		const size_t k1 = k0 + per < piece.size() - 1 ? k0 + per : piece.size() - 1;
@@ -288,7 +336,10 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 			clen[j] = (uint32_t)(piece[k0 + j + 1] - piece[k0 + j]);
 		}
 		const uint64_t span = piece[k1] - pos;
+		AT_MARK(at5);
 		out.resize(decoded_bound(in, pos, piece[k1]) + 1);
+		AT_MARK(at6);
+		AT_ADD(3, at5, at6);
 		nunk = 0;
 		int rc;
 		uint32_t next = XCG_NO_REFERENCES;
@@ -300,6 +351,8 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 			rc = xcg_decode_host(ctx, &in[pos], span, &coff[0], &clen[0], n, &out[0], out.size(), &ooff[0],
 			                     &olen[0], &cst[0], &cons[0], &unk[0], unk.size(), &nunk);
 		}
+		AT_MARK(at7);
+		AT_ADD(4, at6, at7);
 		if (rc == XCG_ENOTSUP) {
 			if (n > 1) {
 				per = n / 2;
@@ -334,8 +387,12 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 				break;
 			}
 		}
+		AT_MARK(at8);
+		AT_ADD(5, at7, at8);
 		mirror_extracts(cache_, in, pos, pos + consumed, next == XCG_NO_REFERENCES ? NULL : &ext[0],
 		                next == XCG_NO_REFERENCES ? 0 : next);
+		AT_MARK(at9);
+		AT_ADD(6, at8, at9);
 		pos += consumed;
 		if (status == 0 && k1 < piece.size() - 1) {	/* more batches of this call */
 			k0 = k1;
@@ -409,5 +466,7 @@ XCodecDecoder::decode(Buffer *output, Buffer *input, std::set<uint64_t>& unknown
 		}
 		return (true);
 	}
+	AT_MARK(at10);
+	AT_ADD(0, at0, at10);
 	return (status >= 0);
 }

@@ -30,3 +30,36 @@ for name, o in (('gpu_dropin', Oracle(dropin=True)), ('reference_cpu', ref)):
         o.cache_free(c)
     assert b''.join(g[1] for g in got) == bytes(d)
     print(name, f'{dt / len(encs) * 1e6:.1f} us per decode call')
+
+# xcg_decode_call alone (no class adapter, no host cache mirror), preallocated
+import ctypes as C  # noqa: E402
+from wanproxy_amd import xcgpu  # noqa: E402
+L = xcgpu.lib()
+L.xcg_debug_decode_phases.argtypes = [C.c_void_p, C.c_uint32]
+L.xcg_debug_decode_phases.restype = C.c_uint32
+out = np.zeros(4 * 65536, np.uint8)
+ol, cons = np.zeros(1, np.uint64), np.zeros(1, np.uint64)
+st = np.zeros(1, np.int32)
+unk = np.zeros(1 << 16, np.uint64)
+nunk, ne = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+ext = np.zeros(1024, np.uint64)
+args = (out.ctypes.data, out.size, ol.ctypes.data, cons.ctypes.data, st.ctypes.data, unk.ctypes.data, unk.size,
+        nunk.ctypes.data, ext.ctypes.data, ext.size, ne.ctypes.data)
+ph = np.zeros(16, np.float64)
+for rep in range(2):
+    ctx = xcgpu.Context()
+    L.xcg_debug_decode_phases(ph.ctypes.data, 16)
+    t0 = time.perf_counter()
+    tot = 0
+    for e in encs:
+        assert L.xcg_decode_call(ctx.h, e, len(e), *args) == 0
+        tot += int(ol[0])
+    dt = time.perf_counter() - t0
+    calls = L.xcg_debug_decode_phases(ph.ctypes.data, 16)
+    ctx.close()
+    assert tot == len(d)
+print('xcg_decode_call', f'{dt / len(encs) * 1e6:.1f} us per call')
+if calls:
+    names = ['kernel', 'stage', 'walk', 'extract hashes', 'resolve', 'precheck', 'output size', 'output copy', 'window',
+             'commit', 'results']
+    print('phases (us per call):', ', '.join(f'{n} {ph[i] / calls:.2f}' for i, n in enumerate(names)))

@@ -1368,9 +1368,24 @@ int xcg_decode_host(xcg_ctx* c, const uint8_t* h_enc, uint64_t enc_len, const ui
 extern "C" int xcg_launch_decode_small(const uint8_t*, uint32_t, uint64_t*, uint64_t*, uint32_t, uint8_t*, uint32_t*,
                                        uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t, int32_t*, void*,
                                        uint32_t, uint8_t*, uint64_t, uint64_t*, uint8_t*, uint64_t, uint64_t*,
-                                       hipStream_t);
+                                       uint64_t*, hipStream_t);
 extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap);
 extern "C" uint32_t xcg_decode_small_res_words(void);
+extern "C" uint32_t xcg_decode_small_phases(void);
+
+// Diagnostics: with XCG_DECODE_PHASES set, every one-launch decode() records
+// clock stamps at its phase boundaries (decode_small_kernel); the sums of the
+// phase durations and the call count come back through
+// xcg_debug_decode_phases.  (Costs a synchronous copy per call.)
+namespace {
+std::mutex g_dph_mu;
+std::vector<double> g_dph_sum;
+uint32_t g_dph_calls = 0;
+bool dphase_on() {
+  static const bool on = getenv("XCG_DECODE_PHASES") != nullptr;
+  return on;
+}
+}  // namespace
 
 extern "C" {
 
@@ -1401,7 +1416,9 @@ int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_ou
     // both back; the results' last word is the context's sticky word)
     const size_t inb = align256(len), outb = align256(out_cap ? out_cap : 1), resb = align256(8ull * rw);
     const size_t scr = align256(xcg_decode_small_scratch(ops_cap));
-    rc = ensure_stage(c, inb + outb + resb + scr, inb + outb + resb);
+    const uint32_t nph = xcg_decode_small_phases();
+    const size_t timb = dphase_on() ? align256(8ull * nph) : 0;
+    rc = ensure_stage(c, inb + outb + resb + scr + timb, inb + outb + resb);
     if (rc != XCG_OK) return rc;
     uint8_t* dm = c->stage_d;
     uint8_t* hm = c->stage_h;
@@ -1416,11 +1433,23 @@ int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_ou
         xcg_launch_decode_small(dm, len, c->g.keys, c->g.vals, c->g.mask, c->g.pool, c->g.nseg, c->g.seg_cap,
                                 c->g.filt, c->g.ftab, c->g.fmask, c->g.gfilt, c->g.gmask, c->d_status,
                                 dm + inb + outb + resb, ops_cap, dm + inb, out_cap, w->hash, w->seg, w->count,
-                                d_res, st) != 0 ||
+                                d_res, timb ? (uint64_t*)(dm + inb + outb + resb + scr) : nullptr, st) != 0 ||
         hipMemcpyAsync(h_o, dm + inb, outb + 8ull * rw, hipMemcpyDeviceToHost, st) != hipSuccess)
       return XCG_EHIP;
     ctx_mark(c, st);
     if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
+    if (timb) {
+      std::vector<uint64_t> tm(nph, 0);
+      if (hipMemcpy(tm.data(), dm + inb + outb + resb + scr, 8ull * nph, hipMemcpyDeviceToHost) == hipSuccess &&
+          h_res[5] == 0) {
+        std::lock_guard<std::mutex> g(g_dph_mu);
+        g_dph_sum.resize(nph, 0.0);
+        for (uint32_t k = 1; k < nph; ++k)
+          if (tm[k] >= tm[k - 1]) g_dph_sum[k] += (double)(tm[k] - tm[k - 1]) * 0.01;   // 100 MHz clock
+        g_dph_sum[0] += (double)(tm[nph - 1] - tm[0]) * 0.01;
+        ++g_dph_calls;
+      }
+    }
     if ((uint32_t)h_res[rw - 1]) return XCG_EOVERFLOW;   // (cache capacity: the sticky word)
     if (h_res[5] == 2) {
       *h_out_len = h_res[7];
@@ -1453,6 +1482,15 @@ int xcg_decode_call(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_ou
   const int rc = xcg_decode_host(c, h_in, len, &off, &len, 1, h_out, out_cap, &ooff, h_out_len, h_status, h_consumed,
                                  h_unknown, unknown_cap, h_nunknown);
   return rc;
+}
+
+uint32_t xcg_debug_decode_phases(double* us, uint32_t n) {
+  std::lock_guard<std::mutex> g(g_dph_mu);
+  for (uint32_t k = 0; k < n; ++k) us[k] = k < g_dph_sum.size() ? g_dph_sum[k] : 0.0;
+  const uint32_t calls = g_dph_calls;
+  g_dph_sum.assign(g_dph_sum.size(), 0.0);
+  g_dph_calls = 0;
+  return calls;
 }
 
 int xcg_pack_outputs(xcg_ctx* c, const uint8_t* d_out, const uint64_t* d_out_off, const uint64_t* d_out_len,

@@ -102,7 +102,10 @@ __device__ __forceinline__ uint64_t spos(uint32_t chunk, uint32_t off) { return 
 
 // Next real op at or after i in x[0..len): an 0xF1 not followed by 0x00.
 // Returns its position (or len) and the number of ESCAPE pairs before it.
-__device__ __forceinline__ uint32_t next_op(const uint8_t* x, uint32_t i, uint32_t len, uint32_t& nesc) {
+// (P: a generic pointer, or an LDS-qualified one for input staged in LDS -- then
+// the walk's loads wait on LDS alone, not on the global stores queued behind them)
+template <typename P>
+__device__ __forceinline__ uint32_t next_op(P x, uint32_t i, uint32_t len, uint32_t& nesc) {
   const int l = lane_id();
   nesc = 0;
   // Fast path: the op follows immediately (EXTRACT/REF-dense streams).
@@ -179,13 +182,20 @@ __device__ __noinline__ uint32_t wave_unescape(uint8_t* dst, const uint8_t* x, u
   return written;
 }
 
-__device__ __noinline__ uint2 dec_window_hash(const uint8_t* w) {
+// 16 bytes at any alignment, from global memory or from LDS
+typedef const __attribute__((address_space(3))) uint8_t* lds_u8p;
+typedef const __attribute__((address_space(3))) u32x4_u* lds_u32x4p;
+__device__ __forceinline__ u32x4 load16(const uint8_t* p) { return *(const u32x4_u*)p; }
+__device__ __forceinline__ u32x4 load16(lds_u8p p) { return *(lds_u32x4p)p; }
+
+template <typename P>
+__device__ __noinline__ uint2 dec_window_hash(P w) {
   const int l = lane_id();
   uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const uint32_t k0 = 1024u * h + 16u * l;
-    const u32x4 v = *(const u32x4_u*)(w + k0);
+    const u32x4 v = load16(w + k0);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t c = byte_of(v[k >> 2], k & 3);
@@ -213,7 +223,8 @@ __device__ __noinline__ bool dec_equal2048(const uint8_t* a, const uint8_t* b) {
   return ballot(!ok) == 0;
 }
 
-__device__ __forceinline__ uint64_t be64(const uint8_t* p) {
+template <typename P>
+__device__ __forceinline__ uint64_t be64(P p) {
   uint64_t h = 0;
   for (int k = 0; k < 8; ++k) h = (h << 8) | p[k];
   return h;
@@ -302,7 +313,8 @@ __device__ __forceinline__ const uint8_t* ref_source_t(const DecParams& prm, uin
 // round of lane-parallel table lookups per 64 REFs instead of one dependent
 // chain per REF.  Returns the run length (1..64, uniform); lanes < run get
 // their hash and stream position.
-__device__ __forceinline__ uint32_t ref_run(const uint8_t* x, uint32_t i, uint32_t len, uint32_t chunk,
+template <typename P>
+__device__ __forceinline__ uint32_t ref_run(P x, uint32_t i, uint32_t len, uint32_t chunk,
                                             uint64_t limit, uint64_t& h, uint64_t& here) {
   const uint32_t l = (uint32_t)lane_id();
   const uint32_t o = i + 10u * l;
@@ -965,7 +977,10 @@ struct SmallDec {
                                // [4] unknowns [5] fallback [6] EXTRACTs before the stop [7] decoded size
                                // then SD_UMAX unknown hashes, then SD_EMAX EXTRACT hashes (op order),
                                // then the context's sticky word
+  uint64_t* tim;               // (diagnostics, nullable) SD_PHASES clock stamps at the phase boundaries
 };
+constexpr uint32_t SD_PHASES = 11;
+#define SD_STAMP(k) do { if (a.tim && threadIdx.x == 0) a.tim[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   __shared__ uint64_t xk[SD_XSLOTS], xf[SD_XSLOTS], xl[SD_XSLOTS];
@@ -981,26 +996,40 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   const int l = lane_id();
   const uint32_t len = a.len;
   const uint8_t* x = a.in;
-  if (len <= SD_LDS_IN) {                                    // stage the input (coalesced 16-byte loads)
+  SD_STAMP(0);
+  const bool staged = len <= SD_LDS_IN;
+  constexpr uint32_t SV = (SD_LDS_IN / 16 + 1023) / 1024;    // 16-byte loads per thread
+  if (staged) {                                              // stage the input (all loads in flight together)
     const uint32_t nv = len / 16;
-    for (uint32_t i = t; i < nv; i += 1024) xin[i] = ((const uint4*)a.in)[i];
+    uint4 v[SV];
+#pragma unroll
+    for (uint32_t j = 0; j < SV; ++j)
+      if (t + 1024u * j < nv) v[j] = ((const uint4*)a.in)[t + 1024u * j];
+#pragma unroll
+    for (uint32_t j = 0; j < SV; ++j)
+      if (t + 1024u * j < nv) xin[t + 1024u * j] = v[j];
     uint8_t* xb = (uint8_t*)xin;
     for (uint32_t i = nv * 16 + t; i < len; i += 1024) xb[i] = a.in[i];
     x = xb;
   }
+  const lds_u8p xs = (lds_u8p)(const uint8_t*)xin;
   for (uint32_t i = t; i < SD_XSLOTS; i += 1024) { xk[i] = EMPTY_KEY; xf[i] = ~0ull; xl[i] = 0; }
   for (uint32_t i = t; i < SD_USLOTS; i += 1024) uk[i] = EMPTY_KEY;
   if (t == 0) {
     s_nunk = 0; s_fb = 0; s_stop = ~0ull; s_next = 0;
     a.res[8 + SD_UMAX + SD_EMAX] = (uint64_t)(uint32_t)*a.status;   // (the paths that return early)
   }
+  if (a.tim) {
+    __syncthreads();
+    SD_STAMP(1);
+  }
   // ---- walk (wave 0): op list, output offsets, declare numbers
-  if (w == 0) {
+  auto walk = [&](auto xp) {
     uint32_t i = 0, k = 0, dn = 0, st = 0, fb = 0;
     uint64_t olen = 0;
     while (i < len) {
       uint32_t nesc = 0;
-      const uint32_t m = next_op(x, i, len, nesc);
+      const uint32_t m = next_op(xp, i, len, nesc);
       if (m > i) {                                           // literal run (:71-81, ESCAPE :91-94)
         if (k >= a.ops_cap) { fb = 1; break; }
         if (l == 0) a.ops[k] = make_uint4(SD_LIT, i, (uint32_t)olen, m - i);
@@ -1010,7 +1039,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       i = m;
       if (i >= len) break;
       if (len - i == 1) { st = 3; break; }
-      const uint32_t op = x[i + 1];
+      const uint32_t op = xp[i + 1];
       if (op == OP_EXTRACT) {
         if (len - i < 2u + SEG) { st = 3; break; }
         if (k >= a.ops_cap) { fb = 1; break; }
@@ -1021,7 +1050,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       } else if (op == OP_REF) {
         if (len - i < 10u) { st = 3; break; }
         uint64_t h, here;
-        const uint32_t r = ref_run(x, i, len, 0, ~0ull, h, here);
+        const uint32_t r = ref_run(xp, i, len, 0, ~0ull, h, here);
         if (k + r > a.ops_cap) { fb = 1; break; }
         if ((uint32_t)l < r) {
           a.ops[k + l] = make_uint4(SD_REF, i + 10u * l, (uint32_t)(olen + (uint64_t)SEG * l), dn + l);
@@ -1043,8 +1072,13 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       s_nops = k; s_ndecl = dn; s_walk_st = st; s_walk_end = i; s_olen = olen;
       if (fb) s_fb = 1;
     }
+  };
+  if (w == 0) {
+    if (staged) walk(xs);
+    else walk(a.in);
   }
   __syncthreads();
+  SD_STAMP(2);
   const uint32_t nops = s_nops;
   if (s_fb) {
     if (t == 0) a.res[5] = 1;
@@ -1055,7 +1089,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     const uint4 o = a.ops[k];
     if (readfirst(o.x) != SD_EXT) continue;
     const uint32_t pos = readfirst(o.y) + 2u;
-    const uint2 h = dec_window_hash(x + pos);
+    const uint2 h = staged ? dec_window_hash(xs + pos) : dec_window_hash(x + pos);
     const uint64_t key = ((uint64_t)readfirst(h.y) << 32) | readfirst(h.x);
     if (l == 0) {
       a.opv[k] = key;
@@ -1074,6 +1108,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   }
   if (t == 0) { s_nx = 0; s_nw = 0; }
   __syncthreads();
+  SD_STAMP(3);
   if (s_next > SD_XSLOTS / 2) {
     if (t == 0) a.res[5] = 1;
     return;
@@ -1127,6 +1162,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     if (o.x != SD_LIT) a.D[o.w] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)src, (uint32_t)(src >> 32));
   }
   __syncthreads();
+  SD_STAMP(4);
   const uint64_t stop = s_stop;
   const uint32_t stop_pos = stop == ~0ull ? ~0u : (uint32_t)(stop >> 32);
   const uint32_t T = stop == ~0ull ? s_ndecl : (uint32_t)stop;   // declares before the stop
@@ -1146,6 +1182,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     if (bad && l == 0) atomicOr(&s_fb, 1u);
   }
   __syncthreads();
+  SD_STAMP(5);
   if (s_fb) {
     if (t == 0) a.res[5] = 1;
     return;
@@ -1158,6 +1195,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       if (o.x == SD_REF && o.y == stop_pos) s_olen = o.z;
     }
   __syncthreads();
+  SD_STAMP(6);
   const uint64_t out_len = s_olen;
   if (out_len > a.out_cap) {
     if (t == 0) { a.res[5] = 2; a.res[7] = out_len; }      // (more room needed; nothing written)
@@ -1174,6 +1212,10 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       const uint8_t* src = (const uint8_t*)(((uint64_t)readfirst(d.w) << 32) | readfirst(d.z));
       wave_copy2048(a.out + oo, src);
     }
+  }
+  if (a.tim) {
+    __syncthreads();
+    SD_STAMP(7);
   }
   // ---- the BACKREF window after the call's declares (before the commit
   // overwrites any pool bytes a REF's declare reads).  Up to 256 declares: a
@@ -1243,6 +1285,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
     }
   }
   __syncthreads();
+  SD_STAMP(8);
   // ---- commit: EXTRACTs before the stop enter the cache, or replace a cached
   // segment's bytes (name reuse, :106-136)
   for (uint32_t q = w; q < nx; q += 16) {
@@ -1270,6 +1313,10 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       if (!tab_insert_min(a.g, lo, hi, sg)) atomicOr(a.status, 2);
       filt_insert(a.fs, lo, hi);
     }
+  }
+  if (a.tim) {
+    __syncthreads();
+    SD_STAMP(9);
   }
   // ---- results: the EXTRACTs before the stop in op order (the host cache's
   // mirror enters them without hashing again)
@@ -1302,6 +1349,7 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
       a.res[7] = out_len;
     }
   }
+  SD_STAMP(10);
 }
 
 // Host-driven cache access (one wave): look a hash up and copy its segment
@@ -1661,7 +1709,7 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
                                        uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint32_t* gfilt, uint32_t gmask,
                                        int32_t* status, void* scratch, uint32_t ops_cap, uint8_t* out, uint64_t out_cap,
                                        uint64_t* win_hash, uint8_t* win_seg, uint64_t win_count, uint64_t* res,
-                                       hipStream_t stream) {
+                                       uint64_t* tim, hipStream_t stream) {
   using namespace xcg;
   SmallDec a;
   a.in = in;
@@ -1682,9 +1730,11 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
   a.win_seg = win_seg;
   a.win_count = win_count;
   a.res = res;
+  a.tim = tim;
   hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(1024), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap) { return 40ull * ops_cap; }
 extern "C" uint32_t xcg_decode_small_res_words(void) { return 8 + xcg::SD_UMAX + xcg::SD_EMAX + 1; }
+extern "C" uint32_t xcg_decode_small_phases(void) { return xcg::SD_PHASES; }
