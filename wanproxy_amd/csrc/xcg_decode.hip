@@ -978,11 +978,13 @@ struct SmallDec {
                                // then SD_UMAX unknown hashes, then SD_EMAX EXTRACT hashes (op order),
                                // then the context's sticky word
   uint64_t* tim;               // (diagnostics, nullable) SD_PHASES clock stamps at the phase boundaries
+  uint32_t* flag;              // (nullable) completion word in host memory: seq is stored there last
+  uint32_t seq;
 };
 constexpr uint32_t SD_PHASES = 11;
 #define SD_STAMP(k) do { if (a.tim && threadIdx.x == 0) a.tim[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-__global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
+__device__ __forceinline__ void decode_small_body(const SmallDec& a) {
   __shared__ uint64_t xk[SD_XSLOTS], xf[SD_XSLOTS], xl[SD_XSLOTS];
   __shared__ uint64_t uk[SD_USLOTS];
   __shared__ uint32_t s_nops, s_ndecl, s_next, s_nunk, s_fb, s_walk_st, s_walk_end;
@@ -1352,6 +1354,19 @@ __global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
   SD_STAMP(10);
 }
 
+// The call's input, output and results may live in host memory (the
+// zero-copy call path: the input is staged into LDS first, the output and
+// results cross PCIe as posted writes); the host then waits on `flag`,
+// stored after every other write of the block is visible system-wide.
+__global__ __launch_bounds__(1024) void decode_small_kernel(SmallDec a) {
+  decode_small_body(a);
+  if (a.flag) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Host-driven cache access (one wave): look a hash up and copy its segment
 // out, or enter a segment under a hash (XCodecCache::lookup / enter /
 // replace, xcodec/xcodec_cache.h:83-89).
@@ -1709,7 +1724,7 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
                                        uint32_t* filt, uint32_t* ftab, uint32_t fmask, uint32_t* gfilt, uint32_t gmask,
                                        int32_t* status, void* scratch, uint32_t ops_cap, uint8_t* out, uint64_t out_cap,
                                        uint64_t* win_hash, uint8_t* win_seg, uint64_t win_count, uint64_t* res,
-                                       uint64_t* tim, hipStream_t stream) {
+                                       uint64_t* tim, uint32_t* flag, uint32_t seq, hipStream_t stream) {
   using namespace xcg;
   SmallDec a;
   a.in = in;
@@ -1731,6 +1746,8 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
   a.win_count = win_count;
   a.res = res;
   a.tim = tim;
+  a.flag = flag;
+  a.seq = seq;
   hipLaunchKernelGGL(decode_small_kernel, dim3(1), dim3(1024), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -1738,3 +1755,4 @@ extern "C" int xcg_launch_decode_small(const uint8_t* in, uint32_t len, uint64_t
 extern "C" uint64_t xcg_decode_small_scratch(uint32_t ops_cap) { return 40ull * ops_cap; }
 extern "C" uint32_t xcg_decode_small_res_words(void) { return 8 + xcg::SD_UMAX + xcg::SD_EMAX + 1; }
 extern "C" uint32_t xcg_decode_small_phases(void) { return xcg::SD_PHASES; }
+extern "C" uint32_t xcg_decode_small_lds_in(void) { return xcg::SD_LDS_IN; }
