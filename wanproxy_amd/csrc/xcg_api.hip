@@ -661,7 +661,10 @@ int xcg_cache_clear(xcg_ctx* c) {
   if (!c) return XCG_EINVAL;
   if (!c->g.keys) return XCG_OK;
   DeviceGuard g(c->device);
-  if (ctx_wait(c) != XCG_OK) return XCG_EHIP;
+  // The wipe is ordered behind the context's last work on the device; only a
+  // pair, whose metadata lives on the host, waits for that work here.
+  if (c->pair && ctx_wait(c) != XCG_OK) return XCG_EHIP;
+  ctx_order(c, nullptr);
   // (the LRU clock keeps running: slots keep their last-reference times, which
   // must stay below every later batch's)
   if (c->pair && xcg_pair_state_clear(c->pair) != 0) return XCG_EHIP;

@@ -243,4 +243,49 @@ __device__ __forceinline__ void filt_insert(const FiltSet& f, uint32_t lo, uint3
   ftab_insert(f.ftab, f.fmask, lo, hi);
 }
 
+// tab_insert_min + filt_insert with a shorter chain of memory round trips (a
+// thread per key, e.g. a batch table build or a commit): the fingerprint
+// bucket is loaded together with the table's first CAS, the value's atomicMin
+// and the filter ORs return nothing, and the bucket is updated from the loaded
+// copy -- on gfx9 each returning atomic waits for every older memory operation
+// of the wave, so the plain sequence cost about four round trips, this two.
+__device__ __forceinline__ bool tab_insert_min_filt(HashTab t, const FiltSet& f, uint32_t lo, uint32_t hi,
+                                                    uint64_t val) {
+  const uint32_t k = probe_key(lo), fp = fp16_of(k);
+  uint32_t* s = f.ftab + 4 * fbucket(k, f.fmask);
+  const u32x4 q = *(const u32x4*)s;
+  const uint64_t key = ((uint64_t)hi << 32) | lo;
+  uint32_t i = tab_slot(lo, hi, t.mask);
+  bool ok = false;
+  for (uint32_t n = 0; n <= t.mask; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&t.keys[i], (unsigned long long)EMPTY_KEY,
+                                    (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) {
+      (void)atomicMin((unsigned long long*)&t.vals[i], (unsigned long long)val);
+      ok = true;
+      break;
+    }
+    i = (i + 1) & t.mask;
+  }
+  atomicOr(f.filt + (filt_word_ofs(k) >> 2), filt_mask(k));
+  atomicOr(f.gfilt + gfilt_word(k, f.gmask), gfilt_mask(k));
+  // the bucket, as ftab_insert, starting from the loaded copy
+  for (int w = 0; w < 4; ++w) {
+    uint32_t old = q[w];
+    for (;;) {
+      const uint32_t a = old & 0xFFFFu, b = old >> 16;
+      if (a == fp || (w < 3 && b == fp)) return ok;
+      uint32_t nw;
+      if (a == 0u) nw = old | fp;
+      else if (w < 3 && b == 0u) nw = old | (fp << 16);
+      else break;
+      const uint32_t got = atomicCAS(s + w, old, nw);
+      if (got == old) return ok;
+      old = got;
+    }
+  }
+  atomicOr(s + 3, FOVF16 << 16);
+  return ok;
+}
+
 }  // namespace xcg

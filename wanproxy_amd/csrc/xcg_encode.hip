@@ -1358,18 +1358,28 @@ namespace xcg {
 // B <- every declaration of this round (earliest chunk wins per hash), and the
 // round's lane filter = the persistent cache's filter + B.  One thread per
 // (chunk, declaration).
+constexpr uint32_t PREP_TABLE = 1, PREP_FILTERS = 2;   // (what a round's prep / build covers)
+
+// what: PREP_TABLE (the table and the counters), PREP_FILTERS, or both.  A
+// verification builds the table alone: the filters of its declarations are
+// only needed if a re-parse follows (then a filters-only pass adds them).
 __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                                 uint32_t maxd, HashTab b, FiltSet fs, uint32_t* bcount,
-                                                                int32_t* status) {
+                                                                int32_t* status, uint32_t what) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = (uint32_t)(i / maxd), k = (uint32_t)(i % maxd);
   const bool have = c < n && k < ndecl[c];
   const uint64_t m = ballot(have);
-  if (lane_id() == 0 && m) atomicAdd(bcount + ((i >> 6) & 63u), (uint32_t)__builtin_popcountll(m));
+  if ((what & PREP_TABLE) && lane_id() == 0 && m) atomicAdd(bcount + ((i >> 6) & 63u), (uint32_t)__builtin_popcountll(m));
   if (!have) return;
   const uint4 d = decl[i];
-  if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
-  filt_insert(fs, d.x, d.y);
+  if (what == (PREP_TABLE | PREP_FILTERS)) {
+    if (!tab_insert_min_filt(b, fs, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
+  } else if (what == PREP_TABLE) {
+    if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
+  } else {
+    filt_insert(fs, d.x, d.y);
+  }
 }
 
 // Restart backup (before a re-parse round that may resume chunks from their
@@ -1457,10 +1467,15 @@ __global__ __launch_bounds__(256) void restart_splice_kernel(uint32_t n, uint4* 
 // are in flight together, and the batch's ~32 k waves hide HBM latency (one
 // wave per chunk walking its tiles four at a time left each wave waiting).
 constexpr uint32_t SEED_TILES = 8;
+// With b.keys set, the kernel also builds round 1's batch table and filters
+// from the tiles (what build_batch_table_kernel does from the lists): lane 0
+// of each wave inserts its tiles' hashes as they are made, so the table's
+// atomics overlap the other waves' hashing instead of a second pass.
 __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, const uint64_t* chunk_off,
                                                           const uint32_t* chunk_len, uint32_t n, uint32_t maxd,
                                                           uint4* decl, uint32_t* ndecl, uint32_t* nhits,
-                                                          uint32_t* changed) {
+                                                          uint32_t* changed, HashTab b, FiltSet fs, uint32_t* bcount,
+                                                          int32_t* status) {
   const uint32_t wpc = (maxd + SEED_TILES - 1) / SEED_TILES;       // waves per chunk
   const uint32_t w = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
   const uint32_t c = w / wpc, k0 = (w % wpc) * SEED_TILES;
@@ -1476,6 +1491,7 @@ __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, con
   if (k0 >= m) return;
   // lane l sums bytes [16 l, 16 l + 16) and [1024 + 16 l, ...) of each tile
   u32x4 v[SEED_TILES][2];
+  uint32_t mlo = 0, mhi = 0;
 #pragma unroll
   for (uint32_t t = 0; t < SEED_TILES; ++t)
 #pragma unroll
@@ -1493,29 +1509,44 @@ __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, con
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t q0 = 1024u * h + 16u * l;
-      uint32_t sx = 0, wx = 0, sf = 0, wf = 0;
+      uint32_t sx = 0, wx = 0;
+      int sf = 0, wf = 0;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
         const uint32_t d = v[t][h][w4];
         const uint32_t wts = (4u * w4) | ((4u * w4 + 1) << 8) | ((4u * w4 + 2) << 16) | ((4u * w4 + 3) << 24);
         sx = __builtin_amdgcn_udot4(d, 0x01010101u, sx, false);
         wx = __builtin_amdgcn_udot4(d, wts, wx, false);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const uint32_t f = ffbl(byte_of(d, b));
-          sf += f;
-          wf += (uint32_t)(4 * w4 + b) * f;
-        }
+        // the four bytes' ffbl (-1 for a zero byte) packed as signed bytes, then
+        // summed plain and k-weighted by v_dot4_i32_i8 (8 VALU per word, not 12)
+        auto fb = [d](int b) {   // (the compiler's ffbl reads the byte in place: v_ffbl_b32_sdwa)
+          return (uint32_t)(__builtin_ffs((int)__builtin_amdgcn_ubfe(d, 8u * b, 8u)) - 1);
+        };
+        const uint32_t p = __builtin_amdgcn_perm(fb(1), fb(0), 0x0c0c0400u) |
+                           __builtin_amdgcn_perm(fb(3), fb(2), 0x04000c0cu);
+        sf = __builtin_amdgcn_sdot4((int)p, 0x01010101, sf, false);
+        wf = __builtin_amdgcn_sdot4((int)p, (int)wts, wf, false);
       }
-      sf += 16u;
-      wf += 120u;
+      sf += 16;
+      wf += 120;
       X1 += sx; X2 += (2048u - q0) * sx - wx;
       F1 += sf; F2 += (2048u - q0) * sf - wf;
     }
     X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
-    if (l == 0) decl[(uint64_t)c * maxd + k0 + t] = make_uint4((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4,
-                                                                (k0 + t) * SEG, 0u);
+    if ((uint32_t)l == t) {                        // lane t keeps tile t's hash
+      mlo = (X1 << 20) + X2 + CLO;
+      mhi = ((F1 << 16) + F2) << 4;
+    }
   }
+  // lanes 0 .. tiles-1: the declaration records and, with a table, its inserts
+  // (all of the wave's tiles in one chain of round trips)
+  const uint32_t tiles = min(SEED_TILES, m - k0);
+  if ((uint32_t)l < tiles) {
+    const uint32_t k = k0 + (uint32_t)l;
+    decl[(uint64_t)c * maxd + k] = make_uint4(mlo, mhi, k * SEG, 0u);
+    if (b.keys && !tab_insert_min_filt(b, fs, mlo, mhi, ((uint64_t)c << 32) | (k * SEG))) atomicOr(status, 2);
+  }
+  if (b.keys && l == 0 && k0 == 0) atomicAdd(bcount + (c & 63u), m);   // (the chunk's count, once)
 }
 
 // Everything a round clears or copies before its batch table is built, in
@@ -1535,21 +1566,34 @@ struct RoundPrep {
   uint32_t* vflags;
   HashTab at;           // (keys == nullptr: no (a)-probe) newly visible hashes
   uint32_t* abits;
+  uint32_t n;           // verification: need[0..n) cleared, bad_t / bad_hi (nullable) reset
+  uint32_t* need;
+  uint32_t* bad_t;
+  uint32_t* bad_hi;
+  uint32_t what;        // PREP_TABLE: the table, counters and verification state; PREP_FILTERS: the filters
 };
 __global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool g_empty = *a.nseg == 0u;
+  if (a.what & PREP_FILTERS) {
+    for (uint64_t i = i0; i < FILT_WORDS; i += stride) a.r_filt[i] = g_empty ? 0u : a.g_filt[i];
+    for (uint64_t i = i0; i < a.ftab_n; i += stride) a.r_ftab[i] = g_empty ? u32x4{0u, 0u, 0u, 0u} : a.g_ftab[i];
+    for (uint64_t i = i0; i < a.gfilt_n; i += stride) a.r_gfilt[i] = g_empty ? 0u : a.g_gfilt[i];
+  }
+  if (!(a.what & PREP_TABLE)) return;
   for (uint64_t i = i0; i <= a.tab.mask; i += stride) { a.tab.keys[i] = EMPTY_KEY; a.tab.vals[i] = ~0ull; }
   if (a.rt.keys)
     for (uint64_t i = i0; i <= a.rt.mask; i += stride) { a.rt.keys[i] = EMPTY_KEY; a.rt.vals[i] = ~0ull; }
+  if (a.rt.keys && a.need)
+    for (uint64_t i = i0; i < a.n; i += stride) {
+      a.need[i] = 0u;
+      if (a.bad_t) { a.bad_t[i] = ~0u; a.bad_hi[i] = 0u; }
+    }
   if (a.rt.keys && a.at.keys) {
     for (uint64_t i = i0; i <= a.at.mask; i += stride) { a.at.keys[i] = EMPTY_KEY; a.at.vals[i] = ~0ull; }
     for (uint64_t i = i0; i < XCG_VERIFY_A_WORDS; i += stride) a.abits[i] = 0u;
   }
-  for (uint64_t i = i0; i < FILT_WORDS; i += stride) a.r_filt[i] = g_empty ? 0u : a.g_filt[i];
-  for (uint64_t i = i0; i < a.ftab_n; i += stride) a.r_ftab[i] = g_empty ? u32x4{0u, 0u, 0u, 0u} : a.g_ftab[i];
-  for (uint64_t i = i0; i < a.gfilt_n; i += stride) a.r_gfilt[i] = g_empty ? 0u : a.g_gfilt[i];
   if (i0 < 64) a.bcount[i0] = 0u;
   if (i0 == 0) {
     *a.changed = ~0u;
@@ -1635,18 +1679,20 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
 // from its start (bad_t 0); then (a) by the probe and (b), which also give
 // the times of the first and last affected lookup (bad_t / bad_hi, for the
 // re-parse restart; ~0 / 0 until then).
-__global__ __launch_bounds__(256) void verify_check_kernel(uint32_t n, const uint32_t* nhits, uint32_t maxh,
-                                                           const uint32_t* nev, uint32_t maxe, bool probe,
-                                                           const uint32_t* vflags, uint32_t* need, uint32_t* any,
-                                                           uint32_t* bad_t, uint32_t* bad_hi) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void verify_check_body(uint32_t bid, uint32_t n, const uint32_t* nhits, uint32_t maxh,
+                                                  const uint32_t* nev, uint32_t maxe, bool probe,
+                                                  const uint32_t* vflags, uint32_t* need, uint32_t* any,
+                                                  uint32_t* bad_t, uint32_t* bad_hi) {
+  const uint32_t k = bid * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const bool conservative = !probe || vflags[3] > XCG_VERIFY_A_LIMIT;
   const bool f = (k >= vflags[0] && conservative) || nhits[k] > maxh || (nev && nev[k] > maxe);
-  need[k] = f ? 1u : 0u;
-  if (bad_t) {
-    bad_t[k] = f ? 0u : ~0u;
-    bad_hi[k] = f ? ~1u : 0u;
+  if (f) {                                       // (need / bad_t / bad_hi start cleared: round_prep)
+    need[k] = 1u;
+    if (bad_t) {
+      bad_t[k] = 0u;
+      bad_hi[k] = ~1u;
+    }
   }
   if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
 }
@@ -1673,20 +1719,19 @@ __device__ __forceinline__ void flag_chunk(uint32_t k, uint32_t lo, uint32_t hi,
 // against the newly visible hashes' Bloom filter in LDS, then exactly; a
 // window of chunk k whose hash became visible to k flags k at that window's
 // lookup time 2 s + 1.  Blocks loop over the (chunk, span) items.
-__global__ __launch_bounds__(256) void verify_probe_kernel(const uint8_t* in, const uint64_t* chunk_off,
-                                                           const uint32_t* chunk_len, uint32_t n, uint32_t spc,
-                                                           const uint32_t* vflags, HashTab at, const uint32_t* abits,
-                                                           uint32_t* need, uint32_t* any, uint32_t* bad_t,
-                                                           uint32_t* bad_hi) {
-  __shared__ uint32_t sb[XCG_VERIFY_A_WORDS];
+__device__ __forceinline__ void verify_probe_body(uint32_t bid, uint32_t nblk, uint32_t* sb, const uint8_t* in,
+                                                  const uint64_t* chunk_off, const uint32_t* chunk_len, uint32_t n,
+                                                  uint32_t spc, const uint32_t* vflags, HashTab at,
+                                                  const uint32_t* abits, uint32_t* need, uint32_t* any,
+                                                  uint32_t* bad_t, uint32_t* bad_hi) {
   const uint32_t a_first = vflags[0], acount = vflags[3];
   if (acount == 0u || acount > XCG_VERIFY_A_LIMIT || a_first >= n) return;
   for (uint32_t i = threadIdx.x; i < XCG_VERIFY_A_WORDS / 4; i += blockDim.x)
     ((u32x4*)sb)[i] = ((const u32x4*)abits)[i];
   __syncthreads();
   const int l = lane_id();
-  const uint64_t items = (uint64_t)(n - a_first) * spc, nw = (uint64_t)gridDim.x * 4u;
-  for (uint64_t it = (uint64_t)blockIdx.x * 4u + readfirst(threadIdx.x >> 6); it < items; it += nw) {
+  const uint64_t items = (uint64_t)(n - a_first) * spc, nw = (uint64_t)nblk * 4u;
+  for (uint64_t it = (uint64_t)bid * 4u + readfirst(threadIdx.x >> 6); it < items; it += nw) {
     const uint32_t k = a_first + (uint32_t)(it / spc);
     const int64_t len = chunk_len[k], npos = len - SEG + 1, p = (int64_t)(it % spc) * SEG;
     if (p >= npos) continue;
@@ -1740,10 +1785,10 @@ __global__ __launch_bounds__(256) void verify_probe_kernel(const uint8_t* in, co
 
 // (b) from the reference rows (bounded caches: batch hits carry their lookup
 // times), one wave per chunk; the hit lists' verify_hits_kernel otherwise.
-__global__ __launch_bounds__(256) void verify_hit_events_kernel(uint32_t n, const uint4* ev, const uint32_t* nev,
-                                                                uint32_t maxe, HashTab rt, uint32_t* need,
-                                                                uint32_t* any, uint32_t* bad_t, uint32_t* bad_hi) {
-  const uint32_t k = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+__device__ __forceinline__ void verify_hit_events_body(uint32_t bid, uint32_t n, const uint4* ev, const uint32_t* nev,
+                                                       uint32_t maxe, HashTab rt, uint32_t* need, uint32_t* any,
+                                                       uint32_t* bad_t, uint32_t* bad_hi) {
+  const uint32_t k = bid * 4u + readfirst(threadIdx.x >> 6);
   if (k >= n) return;
   const uint32_t cnt = min(nev[k], maxe);
   uint32_t lo = ~0u, hi = 0u;
@@ -1756,9 +1801,9 @@ __global__ __launch_bounds__(256) void verify_hit_events_kernel(uint32_t n, cons
   }
   flag_chunk(k, lo, hi, need, any, bad_t, bad_hi);
 }
-__global__ __launch_bounds__(256) void verify_hits_kernel(uint32_t n, const uint64_t* hits, const uint32_t* nhits,
-                                                          uint32_t maxh, HashTab rt, uint32_t* need, uint32_t* any) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void verify_hits_body(uint32_t bid, uint32_t n, const uint64_t* hits, const uint32_t* nhits,
+                                                 uint32_t maxh, HashTab rt, uint32_t* need, uint32_t* any) {
+  const uint64_t j = (uint64_t)bid * blockDim.x + threadIdx.x;
   const uint32_t k = (uint32_t)(j / maxh), i = (uint32_t)(j % maxh);
   bool f = false;
   if (k < n && i < nhits[k]) {
@@ -1770,11 +1815,37 @@ __global__ __launch_bounds__(256) void verify_hits_kernel(uint32_t n, const uint
   if (ballot(f) != 0 && lane_id() == 0) atomicOr(any, 1u);
 }
 
-// Declarations in the batch table just built (for the next batch's seeding
-// policy): vflags[2] = sum of the build's counters.
-__global__ void count_decls_kernel(const uint32_t* bcount, uint32_t* out) {
-  const uint32_t v = wave_sum(bcount[lane_id()]);
-  if (lane_id() == 0) *out = v;
+// The verification's flagging passes in one launch (they only set flags, so
+// their order does not matter; round_prep cleared need / bad_t / bad_hi):
+// blocks [0, bc) the per-chunk check (block 0 also sums the declaration
+// counters into vflags[2]), [bc, bc + bp) the (a)-probe, the rest the (b)
+// hit check -- four launches' gaps fewer per round.
+struct VerifyFlags {
+  uint32_t n, bc, bp, bh;
+  const uint32_t* nhits; uint32_t maxh; const uint64_t* hits;
+  const uint32_t* nev; uint32_t maxe; const uint4* ev;
+  bool probe; uint32_t* vflags; uint32_t* need; uint32_t* bad_t; uint32_t* bad_hi;
+  const uint8_t* in; const uint64_t* chunk_off; const uint32_t* chunk_len; uint32_t spc;
+  HashTab at; const uint32_t* abits; HashTab rt; const uint32_t* bcount;
+};
+__global__ __launch_bounds__(256) void verify_flags_kernel(VerifyFlags v) {
+  __shared__ uint32_t sb[XCG_VERIFY_A_WORDS];
+  const uint32_t b = blockIdx.x;
+  uint32_t* any = v.vflags + 1;
+  if (b < v.bc) {
+    if (b == 0 && threadIdx.x < 64) {
+      const uint32_t t = wave_sum(v.bcount[lane_id()]);
+      if (lane_id() == 0) v.vflags[2] = t;
+    }
+    verify_check_body(b, v.n, v.nhits, v.maxh, v.nev, v.maxe, v.probe, v.vflags, v.need, any, v.bad_t, v.bad_hi);
+  } else if (b < v.bc + v.bp) {
+    verify_probe_body(b - v.bc, v.bp, sb, v.in, v.chunk_off, v.chunk_len, v.n, v.spc, v.vflags, v.at, v.abits, v.need,
+                      any, v.bad_t, v.bad_hi);
+  } else if (v.ev) {
+    verify_hit_events_body(b - v.bc - v.bp, v.n, v.ev, v.nev, v.maxe, v.rt, v.need, any, v.bad_t, v.bad_hi);
+  } else {
+    verify_hits_body(b - v.bc - v.bp, v.n, v.hits, v.nhits, v.maxh, v.rt, v.need, any);
+  }
 }
 
 // Segment numbers of the committed declarations: seg_base[c] = nseg + the
@@ -1817,9 +1888,14 @@ __global__ __launch_bounds__(1024) void commit_scan_kernel(const uint32_t* ndecl
 
 // Commit the converged declarations into the persistent cache
 // (XCodecMemoryCache::enter, xcodec_cache.h:303-325).  Block (chunk c, part q)
-// takes declarations q*256 .. q*256+255 of chunk c: one thread each inserts
-// the hash (segments numbered by one atomic per block), then the block's
-// waves copy the 2048-byte segments into the pool.
+// takes declarations q*256 .. q*256+255 of chunk c, whose segments are
+// seg_base[c] + q*256 + j in declaration order.  Each wave first copies four
+// 2048-byte segments at a time into the pool with all eight 16-byte loads per
+// lane in flight together (the input offsets staged in LDS), then each thread
+// inserts its declaration's hash.  The copy is issued
+// before the inserts: on gfx9 an atomic's return waits on every older memory
+// operation of the wave, so inserts first serialised each segment copy behind
+// the insert chain (70 -> 44 us for C2-S2's ~66 k declarations).
 __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                      uint32_t maxd, const uint8_t* in, const uint64_t* chunk_off,
                                                      HashTab g, uint8_t* pool, const uint32_t* seg_base,
@@ -1834,27 +1910,41 @@ __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const ui
   const uint32_t s_base = seg_base[c] + k0;
   const uint32_t k = k0 + threadIdx.x;
   const bool have = k < nd;
-  const uint32_t seg = s_base + threadIdx.x;
+  __shared__ uint32_t zoff[256];                   // the declarations' input offsets
+  uint4 d = make_uint4(0u, 0u, 0u, 0u);
+  if (have) d = decl[(uint64_t)c * maxd + k];
+  zoff[threadIdx.x] = d.z;
+  __syncthreads();
+  const int l = lane_id();
+  const uint32_t wv = readfirst(threadIdx.x >> 6);
+  const uint8_t* x = in + chunk_off[c];
+  for (uint32_t j0 = 4u * wv; j0 < cnt; j0 += 16u) {
+    u32x4 v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      if (j0 + j < cnt) {
+        const uint8_t* src = x + readfirst(zoff[j0 + j]);
+        v[2 * j] = *(const u32x4_u*)(src + 32 * l);
+        v[2 * j + 1] = *(const u32x4_u*)(src + 32 * l + 16);
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t sg = s_base + j0 + j;
+      if (j0 + j < cnt && sg < seg_cap) {
+        uint8_t* dst = pool + (uint64_t)sg * SEG;
+        *(u32x4_u*)(dst + 32 * l) = v[2 * j];
+        *(u32x4_u*)(dst + 32 * l + 16) = v[2 * j + 1];
+      }
+    }
+  }
   if (have) {
-    const uint4 d = decl[(uint64_t)c * maxd + k];
+    const uint32_t seg = s_base + threadIdx.x;
     if (seg >= seg_cap) {
       atomicOr(status, 4);
     } else {
-      if (!tab_insert_min(g, d.x, d.y, seg)) atomicOr(status, 2);
-      filt_insert(fs, d.x, d.y);
+      if (!tab_insert_min_filt(g, fs, d.x, d.y, seg)) atomicOr(status, 2);
     }
-  }
-  // the block's segments are s_base + (0 .. cnt), in declaration order
-  const uint32_t base = s_base;
-  const int l = lane_id();
-  const uint8_t* x = in + chunk_off[c];
-  for (uint32_t j = readfirst(threadIdx.x >> 6); j < cnt; j += 4) {
-    const uint32_t sg = base + j;
-    if (sg >= seg_cap) break;
-    const uint8_t* src = x + readfirst(decl[(uint64_t)c * maxd + k0 + j].z);
-    uint8_t* dst = pool + (uint64_t)sg * SEG;
-    *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
-    *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
   }
 }
 
@@ -1880,7 +1970,8 @@ extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream
   if (a->n == 0) return 0;
   const uint32_t seed_waves = a->n * ((a->maxd + xcg::SEED_TILES - 1) / xcg::SEED_TILES);
   hipLaunchKernelGGL(xcg::seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
-                     a->chunk_len, a->n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
+                     a->chunk_len, a->n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed,
+                     xcg::HashTab{nullptr, nullptr, 0u}, xcg::FiltSet{}, nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -1936,8 +2027,18 @@ static void ktime_end(hipEvent_t e0, hipStream_t s) {
   g_ktime_ev.emplace_back(e0, e1);
 }
 
+// One event per device and host thread: the verification's flags copied back.
+static hipEvent_t flags_event() {
+  static thread_local hipEvent_t ev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) return nullptr;
+  return ev[dev];
+}
+
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
   using namespace xcg;
+
   const uint32_t n = a->n;
   if (n == 0) return 0;
   EncParams prm{a->in, a->chunk_off, a->chunk_len, n, a->flags, a->out, a->out_off, a->out_len, a->stats, a->status};
@@ -2026,15 +2127,38 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.use_b = false;
   prm.skip_below = 0;
   prm.lf = LaneFilter{a->g_filt, (const u32x4*)a->g_ftab, a->fmask, a->g_gfilt, a->gmask};
+  HashTab tabs[2] = {HashTab{a->b_keys, a->b_vals, a->b_mask}, HashTab{a->b2_keys, a->b2_vals, a->b_mask}};
+  const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
+  // (a) by probing the windows (a_bits null: the conservative flag)
+  const bool probe = a->a_bits && a->a_keys;
+  const HashTab at = probe ? HashTab{a->a_keys, a->a_vals, XCG_VERIFY_A_CAP - 1} : HashTab{nullptr, nullptr, 0u};
+  int cur = 0;
+  int dev_cus = (int)wgs;
+  // A round's batch table, filters and counters cleared / copied from the cache's.
+  const bool rsr = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;   // (= rs_rounds below)
+  auto prep = [&](int t, bool verify, uint32_t what) -> bool {
+    RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
+                 a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
+                 verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags, at, a->a_bits, n, a->need,
+                 rsr ? a->bad_t : nullptr, rsr ? a->bad_hi : nullptr, what};
+    hipLaunchKernelGGL(round_prep_kernel, dim3(4 * dev_cus), dim3(256), 0, stream, rp);
+    return hipGetLastError() == hipSuccess;
+  };
+  bool seed_built = false;
   int rounds = 0;
   uint32_t fc = 0;
   if (keep) {
     // the previous pass's declaration lists seed round 1 (a bounded cache's
     // eviction times changed under them)
   } else if (seeded) {
+    // round 1's table and filters are built by the seed itself (after the
+    // round's prep has cleared them)
+    if (!prep(cur, false, PREP_TABLE | PREP_FILTERS)) return -5;
     const uint32_t seed_waves = n * ((a->maxd + SEED_TILES - 1) / SEED_TILES);
     hipLaunchKernelGGL(seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
-                       a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed);
+                       a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed, tabs[cur],
+                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
+    seed_built = true;
   } else {
     launch();
     rounds = 1;
@@ -2050,16 +2174,9 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   // round's batch table with the one the round parsed against and flags the
   // chunks whose lookups could change; only those are re-parsed.  No flag =
   // the fixed point, which is the sequential result.
-  HashTab tabs[2] = {HashTab{a->b_keys, a->b_vals, a->b_mask}, HashTab{a->b2_keys, a->b2_vals, a->b_mask}};
-  const HashTab rt{a->r_keys, a->r_vals, a->r_mask};
-  // (a) by probing the windows (a_bits null: the conservative flag)
-  const bool probe = a->a_bits && a->a_keys;
-  const HashTab at = probe ? HashTab{a->a_keys, a->a_vals, XCG_VERIFY_A_CAP - 1} : HashTab{nullptr, nullptr, 0u};
   // later rounds resume flagged chunks too (bounded / pair: the verification
   // gives the affected lookups' times)
   const bool rs_rounds = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;
-  int cur = 0;
-  int dev_cus = (int)wgs;
   // Commit the declaration lists into the persistent cache; with a gate, only
   // if the verification that precedes it in the stream flagged nothing.
   bool committed = false;
@@ -2074,15 +2191,12 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
                        (const uint32_t*)seg_base, a->seg_cap,
                        FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask}, a->status, gate);
   };
-  auto build = [&](int t, bool verify) -> bool {
-    RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
-                 a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
-                 verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags, at, a->a_bits};
-    hipLaunchKernelGGL(round_prep_kernel, dim3(4 * dev_cus), dim3(256), 0, stream, rp);
+  auto build = [&](int t, bool verify, uint32_t what) -> bool {
+    if (!prep(t, verify, what)) return false;
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
                        (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, tabs[t],
-                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
+                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status, what);
     return hipGetLastError() == hipSuccess;
   };
   // A re-parse round whose flagged chunks (their first contradicted lookup in
@@ -2111,7 +2225,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     }
   };
   if (n > 1 && fc != ~0u) {
-    if (!build(cur, false)) return -5;
+    if (!seed_built && !build(cur, false, PREP_TABLE | PREP_FILTERS)) return -5;
     prm.use_b = true;
     prm.b = tabs[cur];
     prm.skip_below = seeded ? 0 : fc + 1;            // (seeded: round 1 parses every chunk)
@@ -2130,34 +2244,37 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     for (uint32_t r = 2; r <= n + 1; ++r) {
       // verify round r-1 (parsed against tabs[cur]) against its own declarations
       const int nxt = cur ^ 1;
-      if (!build(nxt, true)) return -5;
+      if (!build(nxt, true, PREP_TABLE)) return -5;   // (filters only if a re-parse follows)
       const uint64_t slots = 2ull * (a->b_mask + 1);
       hipLaunchKernelGGL(verify_diff_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, tabs[cur],
                          tabs[nxt], a->in, a->chunk_off, rt, a->vflags, at, a->a_bits, a->status);
       uint32_t* vbad_t = rs_rounds ? a->bad_t : nullptr;
       uint32_t* vbad_hi = rs_rounds ? a->bad_hi : nullptr;
-      hipLaunchKernelGGL(verify_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n,
-                         (const uint32_t*)a->nhits, a->maxh, (const uint32_t*)(a->ev ? a->nev : nullptr), a->maxe,
-                         probe, (const uint32_t*)a->vflags, a->need, a->vflags + 1, vbad_t, vbad_hi);
-      if (probe) {
-        const uint64_t items = (uint64_t)n * a->maxd;   // (chunk, 2048-position span) pairs, maxd per chunk
-        const uint64_t blocks = (items + 3) / 4, cap = 5ull * (uint64_t)dev_cus;   // (32 KiB of LDS each)
-        hipLaunchKernelGGL(verify_probe_kernel, dim3((unsigned)(blocks < cap ? blocks : cap)), dim3(256), 0, stream,
-                           a->in, a->chunk_off, a->chunk_len, n, a->maxd, (const uint32_t*)a->vflags, at,
-                           (const uint32_t*)a->a_bits, a->need, a->vflags + 1, vbad_t, vbad_hi);
+      {
+        VerifyFlags v{};
+        v.n = n;
+        v.bc = (n + 255) / 256;
+        if (probe) {
+          const uint64_t items = (uint64_t)n * a->maxd;   // (chunk, 2048-position span) pairs, maxd per chunk
+          const uint64_t blocks = (items + 3) / 4, cap = 5ull * (uint64_t)dev_cus;   // (32 KiB of LDS each)
+          v.bp = (uint32_t)(blocks < cap ? blocks : cap);
+        }
+        v.bh = a->ev ? (n + 3) / 4 : (uint32_t)(((uint64_t)n * a->maxh + 255) / 256);
+        v.nhits = (const uint32_t*)a->nhits; v.maxh = a->maxh; v.hits = (const uint64_t*)a->hits;
+        v.nev = (const uint32_t*)(a->ev ? a->nev : nullptr); v.maxe = a->maxe; v.ev = (const uint4*)a->ev;
+        v.probe = probe; v.vflags = a->vflags; v.need = a->need; v.bad_t = vbad_t; v.bad_hi = vbad_hi;
+        v.in = a->in; v.chunk_off = a->chunk_off; v.chunk_len = a->chunk_len; v.spc = a->maxd;
+        v.at = at; v.abits = (const uint32_t*)a->a_bits; v.rt = rt; v.bcount = (const uint32_t*)a->bcount;
+        hipLaunchKernelGGL(verify_flags_kernel, dim3(v.bc + v.bp + v.bh), dim3(256), 0, stream, v);
       }
-      if (a->ev) {
-        hipLaunchKernelGGL(verify_hit_events_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, n, (const uint4*)a->ev,
-                           (const uint32_t*)a->nev, a->maxe, rt, a->need, a->vflags + 1, vbad_t, vbad_hi);
-      } else {
-        const uint64_t nh = (uint64_t)n * a->maxh;
-        hipLaunchKernelGGL(verify_hits_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, n,
-                           (const uint64_t*)a->hits, (const uint32_t*)a->nhits, a->maxh, rt, a->need, a->vflags + 1);
-      }
-      hipLaunchKernelGGL(count_decls_kernel, dim3(1), dim3(64), 0, stream, (const uint32_t*)a->bcount, a->vflags + 2);
       if (hipMemcpyAsync(a->h_vflags, a->vflags, 16, hipMemcpyDeviceToHost, stream) != hipSuccess) return -5;
-      commit(a->vflags + 1);                           // runs while the host waits, if nothing was flagged
-      if (hipStreamSynchronize(stream) != hipSuccess) return -5;
+      // The host waits for the flags alone: the commit (a no-op if anything was
+      // flagged) runs on the device while the host returns and queues the next
+      // batch behind it, so the device does not idle through the host's turn.
+      const hipEvent_t vev = flags_event();
+      if (!vev || hipEventRecord(vev, stream) != hipSuccess) return -5;
+      commit(a->vflags + 1);
+      if (hipEventSynchronize(vev) != hipSuccess) return -5;
       if (a->decls_out) *a->decls_out = a->h_vflags[2];
       if (stream_debug())
         fprintf(stderr, "stream: n %u round %u first (a)-flag %d any %u newly visible %u\n", n, r,
@@ -2168,6 +2285,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
         break;
       }
       if (hipMemsetAsync(a->changed, 0xFF, 4, stream) != hipSuccess) return -5;
+      if (!build(nxt, false, PREP_FILTERS)) return -5;   // the re-parse's filters: cache + round r-1's lists
       cur = nxt;
       prm.b = tabs[cur];
       prm.need = a->need;
