@@ -1856,32 +1856,55 @@ __global__ __launch_bounds__(256) void verify_flags_kernel(VerifyFlags v) {
 // behind a verification and does nothing if that verification flagged chunks.
 __global__ __launch_bounds__(1024) void commit_scan_kernel(const uint32_t* ndecl, uint32_t n, uint32_t* seg_base,
                                                            uint32_t* nseg, const uint32_t* gate) {
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x;
+  // tiles of 1024 x 8 counts: each thread loads its 8 consecutive counts as
+  // two 16-byte loads (coalesced across the wave), the block scans the 1024
+  // thread sums (wave scans + the 16 wave totals: two barriers a tile, where a
+  // Hillis-Steele pass per 4096 counts took twenty -- 54 us at 65 k chunks)
+  constexpr uint32_t PER = 8;
+  __shared__ uint32_t wtot[16];
+  const uint32_t t = threadIdx.x, wv = t >> 6;
   if (gate && *gate) return;
   uint32_t carry = *nseg;
-  for (uint32_t base = 0; base < n; base += 4096) {     // tiles of 4096 (as exclusive_scan_kernel)
-    const uint32_t i0 = base + 4 * t;
-    uint32_t v[4];
+  for (uint32_t base = 0; base < n; base += 1024 * PER) {
+    const uint32_t i0 = base + PER * t;
+    uint32_t v[PER];
+    if (i0 + PER <= n) {
+      const uint4 a0 = *(const uint4*)(ndecl + i0), a1 = *(const uint4*)(ndecl + i0 + 4);
+      v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = i0 + k < n ? ndecl[i0 + k] : 0u;
-    const uint32_t sum = v[0] + v[1] + v[2] + v[3];
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-      const uint32_t u = t >= d ? part[t - d] : 0u;
-      __syncthreads();
-      part[t] += u;
-      __syncthreads();
+      for (uint32_t k = 0; k < PER; ++k) v[k] = i0 + k < n ? ndecl[i0 + k] : 0u;
     }
-    uint32_t run = carry + part[t] - sum;
+    uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (i0 + k < n) seg_base[i0 + k] = run;
+    for (uint32_t k = 0; k < PER; ++k) sum += v[k];
+    const uint32_t incl = wave_incl_scan(sum);
+    if (lane_id() == 63) wtot[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) {
+      const uint32_t x = wtot[q];
+      before += q < wv ? x : 0u;
+      total += x;
+    }
+    uint32_t o[PER];
+    uint32_t run = carry + before + incl - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      o[k] = run;
       run += v[k];
     }
-    carry += part[1023];
-    __syncthreads();
+    if (i0 + PER <= n) {
+      *(uint4*)(seg_base + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+      *(uint4*)(seg_base + i0 + 4) = make_uint4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (i0 + k < n) seg_base[i0 + k] = o[k];
+    }
+    carry += total;
+    __syncthreads();                                   // (wtot is reused)
   }
   if (t == 0) *nseg = carry;
 }
@@ -2151,14 +2174,19 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     // the previous pass's declaration lists seed round 1 (a bounded cache's
     // eviction times changed under them)
   } else if (seeded) {
-    // round 1's table and filters are built by the seed itself (after the
-    // round's prep has cleared them)
-    if (!prep(cur, false, PREP_TABLE | PREP_FILTERS)) return -5;
+    // Round 1's table and filters are built by the seed itself (after the
+    // round's prep has cleared them) when its waves hash full groups of tiles;
+    // with small chunks (a wave per chunk of one or two tiles) the waves would
+    // sit on their inserts at low occupancy (C4's 4 KiB packets: seed 66 ->
+    // 342 us), so the separate build keeps them.
+    const bool fuse = a->maxd > SEED_TILES;
+    if (fuse && !prep(cur, false, PREP_TABLE | PREP_FILTERS)) return -5;
     const uint32_t seed_waves = n * ((a->maxd + SEED_TILES - 1) / SEED_TILES);
     hipLaunchKernelGGL(seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
-                       a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed, tabs[cur],
+                       a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed,
+                       fuse ? tabs[cur] : HashTab{nullptr, nullptr, 0u},
                        FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
-    seed_built = true;
+    seed_built = fuse;
   } else {
     launch();
     rounds = 1;
