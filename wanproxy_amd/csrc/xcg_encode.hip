@@ -2158,12 +2158,14 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   int cur = 0;
   int dev_cus = (int)wgs;
   // A round's batch table, filters and counters cleared / copied from the cache's.
-  const bool rsr = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;   // (= rs_rounds below)
+  // later rounds resume flagged chunks too (bounded / pair: the verification
+  // gives the affected lookups' times)
+  const bool rs_rounds = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;
   auto prep = [&](int t, bool verify, uint32_t what) -> bool {
     RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
                  a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
                  verify ? rt : HashTab{nullptr, nullptr, 0u}, a->vflags, at, a->a_bits, n, a->need,
-                 rsr ? a->bad_t : nullptr, rsr ? a->bad_hi : nullptr, what};
+                 rs_rounds ? a->bad_t : nullptr, rs_rounds ? a->bad_hi : nullptr, what};
     hipLaunchKernelGGL(round_prep_kernel, dim3(4 * dev_cus), dim3(256), 0, stream, rp);
     return hipGetLastError() == hipSuccess;
   };
@@ -2202,9 +2204,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   // round's batch table with the one the round parsed against and flags the
   // chunks whose lookups could change; only those are re-parsed.  No flag =
   // the fixed point, which is the sequential result.
-  // later rounds resume flagged chunks too (bounded / pair: the verification
-  // gives the affected lookups' times)
-  const bool rs_rounds = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;
+
   // Commit the declaration lists into the persistent cache; with a gate, only
   // if the verification that precedes it in the stream flagged nothing.
   bool committed = false;
