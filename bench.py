@@ -541,6 +541,44 @@ def zlib_stage(streams=2048, steps=3, check=0.25, threads=16):
     return out
 
 
+def summary(line):
+    """The line's figures in one short object, printed last (a record that
+    keeps only the tail of stdout still carries every headline number)."""
+    def g(d, *path):
+        for p in path:
+            if not isinstance(d, dict) or p not in d:
+                return None
+            d = d[p]
+        return d
+    s = {'headline_GiBps': line.get('value'), 'headline_frac': g(line, 'roofline', 'frac'),
+         'S2_stream_GiBps': g(line, 'stream_semantics', 'value'),
+         'S2_stream_frac': g(line, 'stream_semantics', 'roofline', 'frac'),
+         'S2_decode_GiBps': g(line, 'decode', 'value'),
+         'tack_loop_us_per_call': {
+             'encode': [g(line, 'tack_loop', 'gpu_dropin', 'us_per_call'),
+                        g(line, 'tack_loop', 'reference_cpu', 'us_per_call')],
+             'decode': [g(line, 'tack_loop', 'gpu_dropin', 'decode_us_per_call'),
+                        g(line, 'tack_loop', 'reference_cpu', 'decode_us_per_call')],
+             'order': '[drop-in, reference]'},
+         'host_inclusive_GiBps': g(line, 'host_inclusive', 'value'),
+         'cpu_baseline_GiBps': g(line, 'cpu_baseline', 'value')}
+    cf = line.get('configs') or {}
+    s['configs_encode_GiBps'] = {k: (v.get('encode_GiBps') if 'error' not in v else 'error')
+                                 for k, v in cf.items()}
+    s['configs_rounds'] = {k: v.get('rounds') for k, v in cf.items() if k.startswith('C5-')}
+    z = line.get('zlib_stage') or {}
+    if z:
+        s['zlib_GiBps'] = {k: [g(z, k, 'value'), g(z, k, 'inflate', 'GiBps')]
+                           for k in ('xcodec', 'text', 'text_level1') if k in z}
+        pc = z.get('per_call') or {}
+        s['zlib_per_call_us'] = {k: {'deflate': [g(pc, k, 'gpu_dropin', 'deflate_us_per_call'),
+                                                 g(pc, k, 'reference_cpu', 'deflate_us_per_call')],
+                                     'inflate': [g(pc, k, 'gpu_dropin', 'inflate_us_per_call'),
+                                                 g(pc, k, 'reference_cpu', 'inflate_us_per_call')]}
+                                 for k in ('xcodec', 'text') if k in pc}
+    return s
+
+
 def sharded_configs(world, rank, dev, backend='nccl'):
     """N > 1: BASELINE configs C4 and C5 as ONE dataset each, split into
     contiguous per-rank ranges (wanproxy_amd/shard.py config_shard: C4 2^20/N
@@ -707,15 +745,21 @@ def main():
                          'kernel': 'encode_independent_kernel', 'kernel_ms': round(kern_ms, 4),
                          'algorithmic_bytes_per_launch': in_bytes + out_bytes},
         }
-        line.update(extras)
+        # Order: the bulky side tables first, the figures a reader looks for
+        # last -- a record that keeps only the tail of stdout still holds the
+        # stream / decode / tack-loop figures and the summary.
         if sharded is not None:
             line['sharded_configs'] = sharded
         if world == 1 and not args.no_extras and not args.no_configs:
             line['configs'] = other_configs()
         if world == 1 and not args.no_extras and not args.no_zlib:
             line['zlib_stage'] = zlib_stage(threads=host_cpus()['threads'])
+        if 'host_inclusive' in extras:
+            line['host_inclusive'] = extras.pop('host_inclusive')
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(data, offs, lens, args.cpu_seconds)
+        line.update(extras)
+        line['summary'] = summary(line)
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

@@ -142,10 +142,16 @@ Geometry geometry_of(XCodecCache *cache)
 		return g;
 	}
 	if (limit == 0) {
-		/* An unbounded primary never evicts: every lookup the pair makes is
-		 * answered by the primary (xcodec_cache.h:217-221), so its visible
-		 * contents -- all the encoder and decoder depend on -- are an
-		 * unbounded memory cache's. */
+		/* An unbounded primary never evicts, so the pair behaves as an
+		 * unbounded memory cache as long as the disk holds nothing the
+		 * primary lacks.  It can: XCodecCachePair::lookup sends a primary miss
+		 * to the secondary (xcodec_cache.h:217-229), and the disk may hold
+		 * what an earlier pair on the same disk front entered (a peer uuid's
+		 * earlier connection: XCodecDisk::connect returns its existing front)
+		 * or what a reloaded volume held.  The engine mirrors this pair as an
+		 * unbounded memory cache and does not see those entries: it emits an
+		 * EXTRACT where the reference emits a REF (known
+		 * departures). */
 		g.kind = KIND_MEMORY;
 		return g;
 	}

@@ -238,13 +238,14 @@ cut_pieces(const std::vector<uint8_t>& in, uint64_t a, std::vector<uint64_t>& pi
 		}
 		if (next > b)
 			next = b;
-		/* literal bytes may be cut anywhere outside an op (an ESCAPE is two bytes) */
-		while (at - piece.back() >= XCGPU_DECODE_PIECE) {
-			uint64_t c = piece.back() + XCGPU_DECODE_PIECE;
-			if (c > 0 && in[c - 1] == XCODEC_MAGIC)
-				c--;
-			piece.push_back(c);
-		}
+		/*
+		 * Literal bytes may be cut anywhere outside an op.  The cut lies in
+		 * [i, at]: i is where the last op ended, and the run [i, at) holds no
+		 * 0xF1 (at is the first at or after i; an ESCAPE is an op at `at`), so
+		 * every such cut is on an op boundary as it stands.
+		 */
+		while (at - piece.back() >= XCGPU_DECODE_PIECE)
+			piece.push_back(piece.back() + XCGPU_DECODE_PIECE);
 		if (next - piece.back() > XCGPU_DECODE_PIECE && at > piece.back())
 			piece.push_back(at);
 		i = next;

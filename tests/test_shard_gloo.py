@@ -48,7 +48,12 @@ def _worker(rank, world, port, q):
         wall, nbytes = reduce_run(0.1 * (rank + 1), int(lens.astype(np.int64).sum()))
         res[name] = (lo, hi, d.tobytes(), [len(o) for o in out], wall, nbytes)
     # C5 "with xcodec_cache_disk spill": the same C5 shard on a private pair of
-    # wanproxy.conf's geometry, scaled (bench.py sharded_configs -> run_c5pair)
+    # wanproxy.conf's geometry, scaled (bench.py sharded_configs -> run_c5pair).
+    # A SLICING check only: the oracle stands in for the rank's GPU, so this
+    # shows that shard_data cuts the pair's stream as bench.py does and that
+    # each rank starts from an empty pair.  The GPU pair path per rank is
+    # checked on the GPU (tests/test_gpu_pair.py) and, at N > 1, by bench.py's
+    # sharded_configs, which compares every rank's output with the oracle.
     from wanproxy_amd.shard import pair_geometry
     d, offs, lens, _ = shard_data('C5', world, rank, 8 / 65536)
     o = Oracle()

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -196,7 +197,8 @@ struct xcg_ctx {
   // stream): the cache-inspection calls wait for this event only, never for
   // the whole device, so other contexts and streams keep running.
   hipEvent_t done_ev = nullptr;
-  XcgPairState* pair = nullptr;    // XCodecCachePair(memory, disk) (xcg_pair.hip): a front of a disk
+  hipEvent_t flags_ev = nullptr;   // stream batches: behind the verification flags' copy (xcg_encode.hip)
+  XcgPairState* pair = nullptr;   // XCodecCachePair(memory, disk) (xcg_pair.hip): a front of a disk
   uint32_t pair_C = 0;             // its primary limit in segments
   bool no_window = false;          // (single-segment host calls: decodes that leave the window alone)
   // Host-call staging (xcg_encode_call / xcg_encode_host): kept across calls,
@@ -620,8 +622,10 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
     return XCG_ENOMEM;
   }
   if (hipMemset(c->d_status, 0, 16) != hipSuccess ||
-      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->flags_ev, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(c->d_status);
+    if (c->done_ev) (void)hipEventDestroy(c->done_ev);
     delete c;
     return XCG_EHIP;
   }
@@ -640,6 +644,7 @@ void xcg_ctx_destroy(xcg_ctx* c) {
   free_dscratch(c->ds);
   window_free(c->own_win);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+  if (c->flags_ev) (void)hipEventDestroy(c->flags_ev);
   xcg_pair_state_destroy(c->pair);
   if (c->stage_h) (void)hipHostFree(c->stage_h);
   if (c->zc_h) (void)hipHostFree(c->zc_h);
@@ -1012,6 +1017,7 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     a.a_keys = c->bs.a_keys;
     a.a_vals = c->bs.a_vals;
     a.a_bits = getenv("XCG_NO_APROBE") ? nullptr : c->bs.a_bits;
+    a.flags_ev = c->flags_ev;
     if (c->pair || c->bounded) {
       BatchScratch& b = c->bs;
       a.eo = b.eo; a.bad_t = b.bad_t; a.bad_hi = b.bad_hi; a.bslot = b.bslot; a.b_count = b.b_count;
@@ -1485,8 +1491,15 @@ int decode_call_zc(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_out
                               (uint64_t*)(dzb + 256 + inb + outb), nullptr, (uint32_t*)dzb, seq, st) != 0)
     return XCG_EHIP;
   ctx_mark(c, st);
+  // Spin (with a pause per poll, so a sibling hyperthread keeps its share) for
+  // about the kernel's expected time; past ZC_SPIN_NS block in the runtime
+  // instead, which sleeps -- so a slow or stuck kernel costs the caller's
+  // event-loop thread no more than that much busy time.
+  constexpr int64_t ZC_SPIN_NS = 2000000;
+  const auto t_spin = std::chrono::steady_clock::now();
   for (uint64_t n = 1;; ++n) {
     if (__atomic_load_n((const uint32_t*)flag, __ATOMIC_ACQUIRE) == seq) break;
+    __builtin_ia32_pause();
     if ((n & 1023) == 0) {
       const hipError_t e = hipStreamQuery(st);
       if (e == hipSuccess) {
@@ -1494,6 +1507,12 @@ int decode_call_zc(xcg_ctx* c, const uint8_t* h_in, uint32_t len, uint8_t* h_out
         return XCG_EHIP;                             // (finished without storing the word)
       }
       if (e != hipErrorNotReady) return XCG_EHIP;
+      if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_spin).count() >
+          ZC_SPIN_NS) {
+        if (hipStreamSynchronize(st) != hipSuccess) return XCG_EHIP;
+        if (__atomic_load_n((const uint32_t*)flag, __ATOMIC_ACQUIRE) != seq) return XCG_EHIP;
+        break;
+      }
     }
   }
   return decode_call_results(w, h_res, rw, h_o, h_out, h_out_len, h_consumed, h_status, h_unknown, unknown_cap,

@@ -86,6 +86,9 @@ struct XcgStreamArgs {
   uint64_t* a_keys;      // [XCG_VERIFY_A_CAP]
   uint64_t* a_vals;
   uint32_t* a_bits;      // [XCG_VERIFY_A_WORDS]
+  // the context's event behind the verification flags' copy (hipEvent_t; null:
+  // the driver makes one for the call)
+  void* flags_ev;
 };
 
 // (a)-probe sizes: at most A_LIMIT newly visible hashes per verification (more:

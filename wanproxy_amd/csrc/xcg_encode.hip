@@ -2050,14 +2050,24 @@ static void ktime_end(hipEvent_t e0, hipStream_t s) {
   g_ktime_ev.emplace_back(e0, e1);
 }
 
-// One event per device and host thread: the verification's flags copied back.
-static hipEvent_t flags_event() {
-  static thread_local hipEvent_t ev[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) return nullptr;
-  return ev[dev];
-}
+// The event behind the verification flags' copy: the context's (destroyed with
+// it), or one made for this call when the caller passes none.
+struct FlagsEvent {
+  hipEvent_t ev = nullptr;
+  bool own = false;
+  explicit FlagsEvent(void* given) {
+    if (given) {
+      ev = (hipEvent_t)given;
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+      own = true;
+    } else {
+      ev = nullptr;
+    }
+  }
+  ~FlagsEvent() {
+    if (own) (void)hipEventDestroy(ev);
+  }
+};
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream) {
   using namespace xcg;
@@ -2084,6 +2094,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.rs = RestartArgs{};
   const size_t tbytes = ((size_t)a->fmask + 1) * 16;
   const size_t gbytes = ((size_t)a->gmask + 1) * 4;
+  FlagsEvent flags_ev(a->flags_ev);
   int dev = 0;
   int cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -2299,7 +2310,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       // The host waits for the flags alone: the commit (a no-op if anything was
       // flagged) runs on the device while the host returns and queues the next
       // batch behind it, so the device does not idle through the host's turn.
-      const hipEvent_t vev = flags_event();
+      const hipEvent_t vev = flags_ev.ev;
       if (!vev || hipEventRecord(vev, stream) != hipSuccess) return -5;
       commit(a->vflags + 1);
       if (hipEventSynchronize(vev) != hipSuccess) return -5;

@@ -2,7 +2,8 @@
 // control flow in DeflatePipe::consume's call pattern (zlib/deflate_pipe.cc:
 // 57-115), over lengths only.  Host code shared by the engine
 // (xcg_deflate.hip: the GPU moves the bytes the plan names) and its CPU test
-// (tests/test_stored_plan.py checks the plan against the system zlib).
+// (tests/test_zlib_oracle.py runs the plan through oracle/stored_plan_harness.cc
+// and checks it against the system zlib).
 #pragma once
 #include <stdint.h>
 #include <string.h>
