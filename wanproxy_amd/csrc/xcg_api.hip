@@ -95,6 +95,7 @@ struct GpuCache {
   uint32_t fmask = 0;
   uint32_t* gfilt = nullptr;    // global lane filter: gmask + 1 words (~1 per segment)
   uint32_t gmask = 0;
+  bool pool_borrowed = false;   // (a pair front's pool: owned by its XcgPairState)
 };
 
 struct BatchScratch {
@@ -259,7 +260,8 @@ uint32_t pow2_at_least(uint64_t v) {
 }
 
 void free_cache(GpuCache& g) {
-  (void)hipFree(g.keys); (void)hipFree(g.vals); (void)hipFree(g.pool); (void)hipFree(g.nseg);
+  (void)hipFree(g.keys); (void)hipFree(g.vals); (void)hipFree(g.nseg);
+  if (!g.pool_borrowed) (void)hipFree(g.pool);
   (void)hipFree(g.filt); (void)hipFree(g.ftab); (void)hipFree(g.gfilt);
   g = GpuCache{};
 }
@@ -377,8 +379,12 @@ int ensure_cache(xcg_ctx* c) {
   g.fmask = fb - 1;
   const uint32_t gw = pow2_at_least(fkeys < 131072 ? 65536 : fkeys / 2);
   g.gmask = gw - 1;
+  // A pair front's pool is its primary followed by the disk's blocks, mapped
+  // by the pair state (one physical disk behind every front, xcg_pair.hip).
+  g.pool_borrowed = c->pair != nullptr;
+  if (c->pair) g.pool = xcg_pair_state_pool(c->pair);
   if (hipMalloc(&g.keys, 8ull * cap) != hipSuccess || hipMalloc(&g.vals, 8ull * cap) != hipSuccess ||
-      hipMalloc(&g.pool, segs * (uint64_t)XCG_SEGMENT_LENGTH + 16) != hipSuccess ||
+      (!c->pair && hipMalloc(&g.pool, segs * (uint64_t)XCG_SEGMENT_LENGTH + 16) != hipSuccess) ||
       hipMalloc(&g.nseg, 16) != hipSuccess || hipMalloc(&g.filt, 4ull * FILT_WORDS) != hipSuccess ||
       hipMalloc(&g.ftab, 16ull * fb) != hipSuccess || hipMalloc(&g.gfilt, 4ull * gw) != hipSuccess) {
     free_cache(g);

@@ -189,8 +189,10 @@ extern "C" const uint64_t* xcg_pair_state_ptime(const XcgPairState* P);
 extern "C" int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st);
 extern "C" int xcg_pair_encode_stream(const XcgStreamArgs* a, XcgPairState* P, int* rounds_out, hipStream_t st);
 extern "C" int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st);
-extern "C" int xcg_pair_decode_pass(XcgPairState* P, const void* d_rows, const uint64_t* d_base, const uint64_t* d_cnt,
-                                    uint32_t n, uint64_t rows, uint64_t decls, int* same, hipStream_t st);
+extern "C" int xcg_pair_decode_pass(XcgPairState* P, const PairGpu* G, const void* d_rows, const uint64_t* d_base,
+                                    const uint64_t* d_cnt, uint32_t n, uint64_t rows, uint32_t maxd, int* same,
+                                    hipStream_t st);
+extern "C" uint8_t* xcg_pair_state_pool(const XcgPairState* P);
 extern "C" int xcg_pair_decode_commit(XcgPairState* P, const PairGpu* G, hipStream_t st);
 
 extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out, hipStream_t stream);

@@ -1630,7 +1630,9 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
                          a->maxd, blockp, blk, changes, 1);
       if (hipMemcpyAsync(a->h_scratch + 8, blk, 8, hipMemcpyDeviceToHost, stream) != hipSuccess) return fail(-5);
       int same = 0;
-      const int prc = xcg_pair_decode_pass(a->pair, evs, p.decl_base, p.n_decl, n, ndecl, ndecl, &same, stream);
+      const PairGpu G{a->in, a->chunk_off, prow, a->maxd, a->pool, a->g_keys, a->g_vals, a->g_mask,
+                      a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask, a->nseg, a->status};
+      const int prc = xcg_pair_decode_pass(a->pair, &G, evs, p.decl_base, p.n_decl, n, ndecl, a->maxd, &same, stream);
       if (prc) return fail(prc);
       const uint64_t nb = a->h_scratch[8];
       if (getenv("XCG_PAIR_DEBUG"))

@@ -2,8 +2,9 @@
 // XCodecMemoryCache primary (:245-365, XCodecLRU xcodec/xcodec_lru.h) and an
 // XCodecDisk secondary (xcodec/xcodec_cache_disk.{h,cc}): wanproxy.conf's
 // cache, `memory` + `disk` under a `pair` (programs/wanproxy/wanproxy.conf:
-// 8-26).  Stream-semantics encode batches stay bit-exact with the sequential
-// XCodecEncoder on such a pair.
+// 8-26).  Stream-semantics encode and decode batches stay bit-exact with the
+// sequential XCodecEncoder / XCodecDecoder on such a pair.  Everything --
+// the pair's state and its policy -- lives on the GPU.
 //
 // Semantics (restated from the reference):
 //   lookup(h)  primary hit: LRU use, then the disk's touch -- re-enter h if
@@ -17,25 +18,53 @@
 //              index (xcodec_cache_disk.cc:694-741, :327-382).
 // A hash is visible while it is in either level.
 //
-// Division of work.  The GPU parses (encode_stream_kernel, the same rounds as
-// every stream batch) against G = one table over the union of both levels:
-// id s < C = primary slot s, id C + i = disk data block i (a hash in both maps
-// to its primary slot); the pool holds C + nb*204 segments, so `pool + id *
-// 2048` is the hash's bytes either way.  The parse takes, per id, the batch
-// time from which the hash is gone from both levels (ptime) as given and
-// records every cache reference it makes, in order (ENTER / HIT / GHIT /
-// GMISS, xcg_cache.h).  The host replays those references through the pair's
-// exact policy over metadata only (XcgPairState below: the primary's LRU list, the
-// disk ring, the links between them) -- a sequential walk over a few tens of
-// thousands of references -- and checks every recorded lookup against it.
+// State in HBM.  Per front (one XCodecCache object): the primary's slots
+// (pkey: hash, pdisk: the number of the same hash's disk entry) and its LRU
+// order (lru[0 .. pcount), least recent first).  Per disk (shared by the fronts
+// on it, as XCodecDisk is by its XCodecDiskCache front-ends): per data block
+// the hash, the entry number written there (dent, NOENT when removed) and the
+// writing front's xuid.  An entry's index block is invalidated when the write
+// clock reaches 204 * (e / 204 + nb) (the write head entering that block one lap
+// on), so liveness is a function of the clock and nothing is swept.  The pool
+// holds C primary segments and the disk's data blocks; with HIP virtual memory
+// the disk's blocks are ONE physical allocation mapped behind every front's
+// primary, so `pool + id * 2048` addresses both and N fronts cost one disk.
+//
+// Division of work.  The parse (encode_stream_kernel, the same rounds as every
+// stream batch) runs against G = one table over both levels (id s < C = primary
+// slot s, id C + i = disk block i; a hash in both maps to its primary slot),
+// takes per id the batch time from which the hash is gone from both levels
+// (ptime) as given, and records every cache reference it makes (ENTER / HIT /
+// GHIT / GMISS, xcg_cache.h).  The replay below recomputes the pair's state
+// along those references with data-parallel passes instead of a sequential
+// walk (tests/pair_model.py states the formulation and checks it against a
+// sequential replay of the reference's policy):
+//  * primary residency at a reference is an LRU stack distance: the entity of
+//    reference j (previous reference p) is still in the primary iff fewer than
+//    C distinct entities were referenced in (p, j), i.e. fewer than C
+//    references k in (p, j) have their own previous reference before p.  The
+//    primary's content at the start is a prefix of pseudo references in LRU
+//    order.  Short gaps are decided by a prefix count; long ones by a block
+//    table of 2-D prefix counts plus two partial block scans;
+//  * evictions: the i-th miss of a full primary evicts the entity of the i-th
+//    *terminal* reference (an entity's last reference before a miss of it, or
+//    its last) in sequence order;
+//  * the disk clock is the prefix count of appends (every enter, and every
+//    primary hit on an entity whose disk entry has died: XCodecDisk::touch);
+//    touches depend on the clock through the deaths, so the clock is the least
+//    fixed point of "touches under this clock", reached by monotone rounds;
+//  * presence at a lookup = primary residency or a live disk entry; a recorded
+//    lookup that contradicts it flags its chunk, and the time each cached entity
+//    leaves both levels becomes ptime for the re-parse.
 // All consistent = the sequential encoder's result (by induction over stream
-// time); otherwise the inconsistent chunks are parsed again under the replay's
-// ptime.  An entry a sub-batch made must not leave both levels and then be
-// looked up within it (the parse sees the batch's declarations to its end);
-// the replay detects that and the sub-batch is halved.  The commit then moves bytes on the GPU (input ->
-// new primary / disk slots, disk -> promoted primary slots, primary -> touched
-// disk slots, through a staging copy) and rebuilds G and its probe filters.
+// time); otherwise the flagged chunks are parsed again under the new ptime.  An
+// entry a sub-batch made must not leave both levels within it (the parse sees
+// the batch's declarations to its end): a sub-batch writes less than a disk lap,
+// which guarantees that.  The commit then places the final primary residents,
+// writes the appended disk blocks and rebuilds G -- all on the device.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -51,64 +80,724 @@
 namespace xcg {
 
 constexpr uint32_t DISK_ENTRIES = 204;   // XCDFS_ENTRIES_PER_INDEX_BLOCK, xcodec_cache_disk.cc:87
+constexpr uint64_t NOENT = ~0ull;        // no disk entry
+constexpr uint64_t NOKEY = ~0ull;
+constexpr uint64_t NEVERT = ~0ull;       // ptime: visible to the end
+constexpr uint32_t NIL = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(256) void pair_fill64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
+// Position kinds.  A position is a pseudo reference (the primary at the start,
+// LRU order) or a recorded row.
+enum : uint8_t { K_PSEUDO = 0, K_ENTER = 1, K_LOOKUP = 2, K_GMISS = 3, K_SKIP = 4, K_REPL = 5 };
+
+struct PairCnt {                          // device counters of one pass
+  uint32_t split;                         // a row list overflowed: a smaller sub-batch
+  uint32_t nbad;                          // recorded lookups the replay contradicts
+  uint32_t unsorted;                      // a chunk's rows out of time order
+  uint32_t changed;                       // touches moved (fixed-point round) / ptime moved (decode)
+  uint32_t nslow;                         // stack-distance queries for the block table
+  uint32_t nmove, nstage, nomiss;         // commit moves, staged moves
+  uint32_t nohit;                         // (decode) a HIT with no earlier definer
+  uint32_t pad[7];
+};
+
+struct PairDev {
+  // the front
+  uint32_t C, xuid, P;                    // limit, front id, primary entries at the start
+  uint64_t* pkey;                         // [C]
+  uint64_t* pdisk;                        // [C] number of the same hash's disk entry (NOENT)
+  const uint32_t* lru;                    // [P] slots, least recent first
+  uint64_t* ptime;                        // [C + D]
+  // the disk
+  uint32_t D, nb;
+  uint64_t dclock0;
+  uint64_t* dkey;                         // [D]
+  uint64_t* dent;                         // [D]
+  uint32_t* dxuid;                        // [D]
+  // rows
+  int dec;                                // decode rows (packed, REPLACE flags) vs encode rows
+  uint32_t n, maxd, maxe;
+  const uint4* ev;
+  const uint32_t* nev;                    // encode: rows per chunk
+  const uint64_t* base64;                 // decode: row base per chunk
+  const uint64_t* cnt64;                  // decode: rows per chunk
+  uint32_t* pbase;                        // encode: position base per chunk (exclusive scan) [n + 1]
+  uint32_t* pcnt;                         // encode: rows per chunk [n + 1]
+  // positions [np)
+  uint32_t newb, etot, np;
+  uint32_t* ent;                          // entity (decode REPL rows: the replaced entity)
+  uint32_t* yent;                         // decode REPL rows: the new entity (else NIL)
+  uint8_t* kind;
+  uint64_t* tim;                          // stream time (chunk << 21 | t)
+  uint64_t* hsh;
+  uint32_t* skey;                         // sort input keys (entity, etot = none) / values (position)
+  uint32_t* sval;
+  uint32_t* sk;                           // sorted
+  uint32_t* sv;
+  int32_t* prv;                           // previous reference of the same entity (-1)
+  int32_t* nxt;                           // next reference (-1)
+  uint32_t* isr;                          // 1: a reference [np + 1]
+  uint32_t* rc;                           // exclusive prefix of isr [np + 1]
+  uint8_t* phit;                          // primary hit (a lookup / GMISS whose entity is resident)
+  uint32_t* app;                          // appends at the position [np + 1]
+  uint32_t* clk;                          // exclusive prefix of app [np + 1]
+  uint32_t* etch;                         // [newb] touch position of an initial entity (NIL)
+  uint32_t* erep;                         // [newb] (decode) position of the REPLACE that ends it (NIL)
+  uint32_t* erun;                         // [etot] sorted index of the entity's first element (NIL)
+  uint32_t* slow;                         // positions for the block table
+  uint32_t* tab;                          // [nbk * (nbk + 1)] 2-D prefix counts
+  uint32_t bsh, nbk;                      // table block = 1 << bsh positions
+  uint32_t* f1;                           // misses / final residents [np + 1]
+  uint32_t* f2;                           // terminals / new residents [np + 1]
+  uint32_t* r1;                           // exclusive prefixes [np + 1]
+  uint32_t* r2;
+  uint32_t* missrow;                      // position of the i-th miss
+  uint32_t* occ;                          // [C] slot kept / free list
+  uint32_t* freel;                        // [C]
+  uint32_t* lru2;                         // [C] the next LRU order
+  uint4* moves;                           // commit moves
+  PairCnt* cnt;
+  HashTab bm;                             // hash -> ENTER position (encode)
+  HashTab g;                              // the front's G (leave: which disk blocks are entities)
+  uint32_t* need;                         // per chunk: flagged; earliest / latest contradicted time
+  uint32_t* bad_t;
+  uint32_t* bad_hi;
+};
+
+__device__ __forceinline__ uint64_t death_of(uint64_t e, uint32_t nb) {
+  return e == NOENT ? 0ull : (uint64_t)DISK_ENTRIES * (e / DISK_ENTRIES + nb);
+}
+
+// The live disk entry an initial entity (id < newb) had at the pass start.
+__device__ __forceinline__ uint64_t e0_of(const PairDev& d, uint32_t x) {
+  uint64_t e;
+  if (x < d.C) {
+    e = d.pdisk[x];
+  } else {
+    const uint32_t i = x - d.C;
+    if (d.dxuid[i] != d.xuid) return NOENT;
+    e = d.dent[i];
+  }
+  if (e == NOENT || d.dent[e % d.D] != e || d.dclock0 >= death_of(e, d.nb)) return NOENT;
+  return e;
+}
+
+__device__ __forceinline__ void mark_bad(const PairDev& d, uint64_t tm) {
+  const uint32_t c = (uint32_t)(tm >> 21), t = (uint32_t)tm & 0x1FFFFFu;
+  d.need[c] = 1u;
+  atomicMin(d.bad_t + c, t);
+  atomicMax(d.bad_hi + c, t);
+  atomicAdd(&d.cnt->nbad, 1u);
+}
+
+__global__ __launch_bounds__(256) void pr_fill64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ __launch_bounds__(256) void pr_fill32_kernel(uint32_t* p, uint64_t n, uint32_t v) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = v;
 }
 
-// dst[kv[2j]] = kv[2j + 1]
-__global__ __launch_bounds__(256) void pair_scatter64_kernel(uint64_t* dst, const uint64_t* kv, uint32_t n) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < n) dst[kv[2 * j]] = kv[2 * j + 1];
+__global__ __launch_bounds__(256) void pr_iota_kernel(uint32_t* p, uint32_t n, uint32_t base) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = base + i;
 }
 
-// Seed tiles in a batch table: hash -> earliest (chunk << 32 | position).
-__global__ __launch_bounds__(256) void pair_seed_table_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
-                                                              uint32_t maxd, HashTab b, int32_t* status) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = (uint32_t)(i / maxd), d = (uint32_t)(i % maxd);
-  if (c >= n || d >= ndecl[c]) return;
-  const uint4 dd = decl[i];
-  if (!tab_insert_min(b, dd.x, dd.y, ((uint64_t)c << 32) | dd.z)) atomicOr(status, 2);
+constexpr uint32_t HITMARK = 0xFFFFFFFEu;   // yent of a decode HIT row (resolved by hash)
+
+// Encode: rows per chunk (a chunk whose list overflowed splits the sub-batch).
+__global__ __launch_bounds__(256) void pr_count_kernel(PairDev d) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > d.n) return;
+  if (c == d.n) { d.pcnt[c] = 0u; return; }
+  const uint32_t m = d.nev[c];
+  if (m > d.maxe) atomicOr(&d.cnt->split, 1u);
+  d.pcnt[c] = m < d.maxe ? m : d.maxe;
 }
 
-// First guess of a sub-batch's references, before any parse: every chunk
-// parses as its 2048-byte tiling (its cold parse), a tile found in G being a
-// lookup hit, a repeat of an earlier tile of the batch a hit on that
-// declaration, and every other tile a declaration, entered while the window
-// 2048 bytes on (or after the last window) is examined.  One event per tile,
-// in the same row format the parse records.
-__global__ __launch_bounds__(256) void pair_seed_events_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
-                                                               uint32_t maxd, const uint32_t* chunk_len, HashTab g,
-                                                               HashTab b, uint4* ev, uint32_t* nev, uint32_t maxe) {
+// Pseudo references: the primary at the start, least recent first.
+__global__ __launch_bounds__(256) void pr_pseudo_kernel(PairDev d) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= d.P) return;
+  const uint32_t s = d.lru[r];
+  d.ent[r] = s;
+  d.yent[r] = NIL;
+  d.kind[r] = K_PSEUDO;
+  d.tim[r] = 0;
+  d.hsh[r] = d.pkey[s];
+  d.app[r] = 0u;
+}
+
+// Rows -> positions, one wave per chunk.  ENTER: a new entity numbered by its
+// declaration row; GHIT / GMISS: the G id it found; HIT: resolved afterwards.
+// Decode rows: a GHIT with the REPLACE flag (name reuse, xcodec_decoder.cc:
+// 110-133) makes a new entity from the declaration row numbered with the
+// ENTERs in op order; GMISS rows have no cache effect.
+__global__ __launch_bounds__(256) void pr_rows_kernel(PairDev d) {
   const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
-  if (c >= n) return;
-  const uint32_t nd = min(ndecl[c], maxe), last = chunk_len[c] - SEG;
-  for (uint32_t d = (uint32_t)lane_id(); d < nd; d += 64) {
-    const uint4 dd = decl[(uint64_t)c * maxd + d];
-    const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
-    uint4 e;
-    if (gv != ~0ull) {
-      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, (EV_GHIT << 30) | (uint32_t)gv);
-    } else if (tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z)) {
-      const uint32_t t = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
-      e = make_uint4(dd.x, dd.y, t, (EV_ENTER << 30) | d);
-    } else {
-      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, EV_HIT << 30);
-    }
-    ev[(uint64_t)c * maxe + d] = e;
+  if (c >= d.n) return;
+  uint32_t m;
+  uint64_t rb, pb;
+  if (d.dec) {
+    m = (uint32_t)d.cnt64[c];
+    rb = d.base64[c];
+    pb = d.P + d.base64[c];
+  } else {
+    m = min(d.nev[c], d.maxe);
+    rb = (uint64_t)c * d.maxe;
+    pb = d.P + d.pbase[c];
   }
-  if (lane_id() == 0) nev[c] = nd;
+  uint32_t ndecl = 0;
+  for (uint32_t k0 = 0; k0 < m; k0 += 64) {
+    const uint32_t k = k0 + (uint32_t)lane_id();
+    const bool valid = k < m;
+    const uint4 e = valid ? d.ev[rb + k] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t kd = e.w >> 30, ref = e.w & EV_REF_MASK;
+    const bool rep = d.dec && (e.z >> 31) != 0u;
+    const uint32_t t = d.dec ? (e.z & 0x7FFFFFFFu) : e.z;
+    const bool isdecl = valid && d.dec && (kd == EV_ENTER || (kd == EV_GHIT && rep));
+    const uint64_t dm = ballot(isdecl);
+    const uint32_t dnum = ndecl + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+    ndecl += (uint32_t)__builtin_popcountll(dm);
+    if (!valid) continue;
+    if (k > 0 && (d.dec ? (d.ev[rb + k - 1].z & 0x7FFFFFFFu) : d.ev[rb + k - 1].z) > t) atomicOr(&d.cnt->unsorted, 1u);
+    const uint64_t pos = pb + k;
+    const uint64_t tm = ((uint64_t)c << 21) | t;
+    d.tim[pos] = tm;
+    d.hsh[pos] = ((uint64_t)e.y << 32) | e.x;
+    d.yent[pos] = NIL;
+    uint32_t x = NIL;
+    uint8_t kk = K_SKIP;
+    uint32_t a = 0u;
+    if (kd == EV_ENTER) {
+      if (ref < d.maxd) {
+        x = d.newb + c * d.maxd + ref;
+        kk = K_ENTER;
+        a = 1u;
+        if (!d.dec && !tab_insert_min(d.bm, e.x, e.y, pos)) atomicOr(&d.cnt->split, 2u);
+      } else {
+        atomicOr(&d.cnt->split, 4u);
+      }
+    } else if (kd == EV_HIT) {
+      kk = K_LOOKUP;                                 // (entity resolved by pr_resolve_kernel)
+      if (d.dec) d.yent[pos] = HITMARK;
+    } else if (kd == EV_GHIT) {
+      if (ref < d.newb) {
+        x = ref;
+        kk = K_LOOKUP;
+        if (rep) {
+          if (dnum < d.maxd) {
+            kk = K_REPL;
+            d.yent[pos] = d.newb + c * d.maxd + dnum;
+            d.erep[ref] = (uint32_t)pos;
+            a = 1u;
+          } else {
+            atomicOr(&d.cnt->split, 4u);
+          }
+        }
+      } else if (!d.dec) {
+        mark_bad(d, tm);
+      }
+    } else {                                         // EV_GMISS
+      if (d.dec) {
+        kk = K_SKIP;                                 // (decode: no cache effect)
+      } else if (ref < d.newb) {
+        x = ref;
+        kk = K_GMISS;
+      } else {
+        mark_bad(d, tm);
+      }
+    }
+    d.ent[pos] = x;
+    d.kind[pos] = kk;
+    d.app[pos] = a;
+  }
+}
+
+// Decode definers of a hash for HIT resolution: ENTER / REPL rows (the entity
+// they make) and GHIT rows (the cached entity); bm maps hash -> a chain head.
+// A decode HIT resolves to the latest ENTER / REPL of its hash before it, else
+// the first GHIT before it (XcgPairState's bmap: a GHIT puts only when absent,
+// xcodec_decoder.cc's lookups).  Done by sorting (hash, position) pairs: see
+// pr_dec_hits_kernel.
+//
+// Encode HIT resolution: the ENTER of the hash (the table holds the earliest;
+// a second ENTER of a hash present in the sub-batch contradicts the replay).
+__global__ __launch_bounds__(256) void pr_resolve_kernel(PairDev d) {
+  const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= d.np) return;
+  uint8_t kk = d.kind[pos];
+  if (pos >= d.P && !d.dec) {
+    const uint64_t h = d.hsh[pos];
+    if (kk == K_LOOKUP && d.ent[pos] == NIL) {
+      const uint64_t v = tab_lookup_t(d.bm, (uint32_t)h, (uint32_t)(h >> 32));
+      if (v != ~0ull && v < pos) {
+        d.ent[pos] = d.ent[v];
+      } else {
+        kk = K_SKIP;
+        d.kind[pos] = kk;
+        mark_bad(d, d.tim[pos]);
+      }
+    } else if (kk == K_ENTER) {
+      const uint64_t v = tab_lookup_t(d.bm, (uint32_t)h, (uint32_t)(h >> 32));
+      if (v != pos) {                                // a second ENTER of a hash the sub-batch holds
+        kk = K_SKIP;
+        d.kind[pos] = kk;
+        d.app[pos] = 0u;
+        mark_bad(d, d.tim[pos]);
+      }
+    }
+  }
+  if (kk != K_SKIP && d.ent[pos] >= d.etot) {        // (a decode HIT with no definer: the pass returns -95)
+    kk = K_SKIP;
+    d.kind[pos] = kk;
+  }
+  const bool r = kk != K_SKIP && kk != K_GMISS;
+  d.skey[pos] = kk == K_SKIP ? d.etot : d.ent[pos];
+  d.sval[pos] = pos;
+  d.isr[pos] = r ? 1u : 0u;
+  if (pos == 0) { d.isr[d.np] = 0u; d.app[d.np] = 0u; }
+}
+
+// Decode HIT resolution over rows sorted by (hash, position): sk = hash rank
+// key is not needed -- the sort is by hash (64-bit keys, stable), values are
+// positions.  For every HIT: walk back in its hash run to the latest ENTER /
+// REPL; if none, the first GHIT of the run before it.
+__global__ __launch_bounds__(256) void pr_dec_hits_kernel(PairDev d, const uint64_t* hk, const uint32_t* hv,
+                                                          uint32_t m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t pos = hv[i];
+  if (d.kind[pos] != K_LOOKUP || d.ent[pos] != NIL) return;
+  const uint64_t h = hk[i];
+  uint32_t x = NIL, first_ghit = NIL;
+  for (int64_t j = (int64_t)i - 1; j >= 0 && hk[j] == h; --j) {
+    const uint32_t q = hv[j];
+    const uint8_t kq = d.kind[q];
+    if (kq == K_ENTER) { x = d.ent[q]; break; }
+    if (kq == K_REPL) { x = d.yent[q]; break; }
+    if (kq == K_LOOKUP && d.ent[q] != NIL && d.ent[q] < d.newb) first_ghit = d.ent[q];
+  }
+  if (x == NIL) x = first_ghit;
+  if (x == NIL) {
+    atomicOr(&d.cnt->nohit, 1u);
+    return;
+  }
+  d.ent[pos] = x;
+}
+
+// Per sorted element: the entity's previous / next reference (GMISS rows are
+// not references) and the first element of each entity's run.
+__global__ __launch_bounds__(256) void pr_links_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = d.sk[i];
+  if (e >= d.etot) return;
+  const uint32_t pos = d.sv[i];
+  if (i == 0 || d.sk[i - 1] != e) d.erun[e] = i;
+  int64_t j = (int64_t)i - 1;
+  while (j >= 0 && d.sk[j] == e && d.kind[d.sv[j]] == K_GMISS) --j;
+  d.prv[pos] = (j >= 0 && d.sk[j] == e) ? (int32_t)d.sv[j] : -1;
+  if (d.kind[pos] != K_GMISS) {
+    uint32_t q = i + 1;
+    while (q < d.np && d.sk[q] == e && d.kind[d.sv[q]] == K_GMISS) ++q;
+    d.nxt[pos] = (q < d.np && d.sk[q] == e) ? (int32_t)d.sv[q] : -1;
+  } else {
+    d.nxt[pos] = -1;
+  }
+}
+
+// Decode REPLACE rows: the new entity continues the replaced one's place in
+// the primary (the slot keeps its LRU position, xcodec_cache.h:187-196), so
+// for the stack distance the replaced entity's references and the new one's
+// form one chain through the REPLACE row.
+__global__ __launch_bounds__(256) void pr_repl_links_kernel(PairDev d) {
+  const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= d.np || d.kind[pos] != K_REPL) return;
+  const uint32_t y = d.yent[pos];
+  const uint32_t i = d.erun[y];
+  if (i == NIL) { d.nxt[pos] = -1; return; }
+  // y's first reference (its run holds only references: HITs)
+  const uint32_t q = d.sv[i];
+  d.nxt[pos] = (int32_t)q;
+  d.prv[q] = (int32_t)pos;
+}
+
+// Primary hits from the stack distance: short gaps by the reference count
+// alone, the rest queued for the block table.
+__global__ __launch_bounds__(256) void pr_hits_kernel(PairDev d) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d.np || j < d.P) return;
+  const uint8_t kk = d.kind[j];
+  uint8_t h = 0;
+  if (kk == K_LOOKUP || kk == K_GMISS || kk == K_REPL) {
+    const int32_t p = d.prv[j];
+    if (p >= 0) {
+      const uint32_t between = d.rc[j] - d.rc[p + 1];
+      if (between < d.C) h = 1;
+      else d.slow[atomicAdd(&d.cnt->nslow, 1u)] = j;
+    }
+  }
+  d.phit[j] = h;
+}
+
+// Block table: H[b][v] = references k in block b whose previous reference is
+// in block v - 1 (v = 0: none).
+__global__ __launch_bounds__(256) void pr_tab_hist_kernel(PairDev d) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= d.np || !d.isr[k]) return;
+  const int32_t p = d.prv[k];
+  const uint32_t v = p < 0 ? 0u : ((uint32_t)p >> d.bsh) + 1u;
+  atomicAdd(d.tab + (uint64_t)(k >> d.bsh) * (d.nbk + 1) + v, 1u);
+}
+// Row prefix over v (inclusive), one wave per row.
+__global__ __launch_bounds__(256) void pr_tab_rows_kernel(PairDev d) {
+  const uint32_t b = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (b >= d.nbk) return;
+  uint32_t* row = d.tab + (uint64_t)b * (d.nbk + 1);
+  uint32_t carry = 0;
+  for (uint32_t v0 = 0; v0 <= d.nbk; v0 += 64) {
+    const uint32_t v = v0 + (uint32_t)lane_id();
+    const uint32_t x = v <= d.nbk ? row[v] : 0u;
+    const uint32_t s = wave_incl_scan(x) + carry;
+    if (v <= d.nbk) row[v] = s;
+    carry = readlane(s, 63);
+  }
+}
+// Column prefix over b (exclusive) in 32 segments: segment sums, their prefix,
+// then each segment's rows.
+constexpr uint32_t TSEG = 32;
+__global__ __launch_bounds__(256) void pr_tab_cols_kernel(PairDev d, uint32_t* segsum, int phase) {
+  const uint32_t w = d.nbk + 1;
+  const uint32_t per = (d.nbk + TSEG - 1) / TSEG;
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (phase == 1) {                                  // prefix over the segments, per column
+    if (id >= w) return;
+    uint32_t acc = 0;
+    for (uint32_t s = 0; s < TSEG; ++s) {
+      const uint32_t x = segsum[(uint64_t)s * w + id];
+      segsum[(uint64_t)s * w + id] = acc;
+      acc += x;
+    }
+    return;
+  }
+  if (id >= (uint64_t)w * TSEG) return;
+  const uint32_t v = (uint32_t)(id % w), s = (uint32_t)(id / w);
+  const uint32_t b0 = s * per, b1 = min(d.nbk, b0 + per);
+  if (phase == 0) {
+    uint32_t acc = 0;
+    for (uint32_t b = b0; b < b1; ++b) acc += d.tab[(uint64_t)b * w + v];
+    segsum[(uint64_t)s * w + v] = acc;
+  } else {
+    uint32_t acc = segsum[(uint64_t)s * w + v];
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t x = d.tab[(uint64_t)b * w + v];
+      d.tab[(uint64_t)b * w + v] = acc;
+      acc += x;
+    }
+  }
+}
+// One wave per queued position j (previous reference p):
+//   count = T[jb][pb] + #{m in [pb*B, p): nxt(m) < jb*B} + #{k in [jb*B, j): prv(k) < p} - rc[p + 1]
+// = distinct entities referenced in (p, j); a hit iff < C.
+__global__ __launch_bounds__(256) void pr_tab_query_kernel(PairDev d) {
+  const uint32_t q = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (q >= d.cnt->nslow) return;
+  const uint32_t j = d.slow[q];
+  const uint32_t p = (uint32_t)d.prv[j];
+  const uint32_t jb = j >> d.bsh, pb = p >> d.bsh;
+  uint32_t cnt = d.tab[(uint64_t)jb * (d.nbk + 1) + pb];
+  const uint32_t lim1 = jb << d.bsh;
+  for (uint32_t m = (pb << d.bsh) + (uint32_t)lane_id(); m < p + 63u; m += 64) {
+    const bool ok = m < p && d.isr[m] && d.nxt[m] >= 0 && (uint32_t)d.nxt[m] < lim1;
+    cnt += (uint32_t)__builtin_popcountll(ballot(ok));
+  }
+  for (uint32_t k = lim1 + (uint32_t)lane_id(); k < j + 63u; k += 64) {
+    const bool ok = k < j && d.isr[k] && d.prv[k] < (int32_t)p;
+    cnt += (uint32_t)__builtin_popcountll(ballot(ok));
+  }
+  cnt -= d.rc[p + 1];
+  if (lane_id() == 0) d.phit[j] = cnt < d.C ? 1 : 0;
+}
+
+// One fixed-point round of the disk clock: per initial entity, the first
+// primary hit at which its disk entry is dead (died, or none) is a touch
+// (XCodecDisk::touch re-enters the hash).  One thread per entity run.
+__global__ __launch_bounds__(256) void pr_touch_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = d.sk[i];
+  if (e >= d.newb || (i > 0 && d.sk[i - 1] == e)) return;
+  const uint64_t dth = death_of(e0_of(d, e), d.nb);
+  uint32_t tp = NIL;
+  for (uint32_t q = i; q < d.np && d.sk[q] == e; ++q) {
+    const uint32_t pos = d.sv[q];
+    const uint8_t kk = d.kind[pos];
+    if (pos >= d.P && (kk == K_LOOKUP || kk == K_REPL) && d.phit[pos] && d.dclock0 + d.clk[pos] >= dth) {
+      tp = pos;
+      break;
+    }
+  }
+  const uint32_t old = d.etch[e];
+  if (old == tp) return;
+  if (old != NIL) d.app[old] -= 1u;
+  if (tp != NIL) d.app[tp] += 1u;
+  d.etch[e] = tp;
+  atomicAdd(&d.cnt->changed, 1u);
+}
+
+// Presence at every recorded lookup (primary residency or a live disk entry);
+// a lookup the parse recorded the other way flags its chunk (encode).
+__global__ __launch_bounds__(256) void pr_check_kernel(PairDev d) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d.np || j < d.P) return;
+  const uint8_t kk = d.kind[j];
+  if (kk != K_LOOKUP && kk != K_GMISS) return;
+  if (d.dec && d.yent[j] != HITMARK) return;        // (decode: only HITs are checked)
+  const uint32_t x = d.ent[j];
+  if (x >= d.newb) return;                           // (a batch entity: on disk to the sub-batch's end)
+  const uint32_t tp = d.etch[x];
+  const uint32_t rp = d.dec ? d.erep[x] : NIL;
+  const bool disk = (tp != NIL && tp < j) || d.dclock0 + d.clk[j] < death_of(e0_of(d, x), d.nb);
+  const bool present = (d.phit[j] || disk) && !(rp != NIL && rp < j);
+  if (d.dec) {
+    if (!present) atomicOr(&d.cnt->split, 8u);       // a hash this batch named is gone: smaller batches
+  } else if (present != (kk == K_LOOKUP)) {
+    mark_bad(d, d.tim[j]);
+  }
+}
+
+// Misses (references that enter the primary) and terminal references (the
+// last before a miss of the same entity, or the last).
+__global__ __launch_bounds__(256) void pr_missterm_kernel(PairDev d) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > d.np) return;
+  uint32_t miss = 0, term = 0;
+  if (k < d.np && d.isr[k]) {
+    miss = k >= d.P && !d.phit[k] ? 1u : 0u;
+    const int32_t nx = d.nxt[k];
+    term = (nx < 0 || !d.phit[nx]) ? 1u : 0u;
+  }
+  d.f1[k] = miss;
+  d.f2[k] = term;
+}
+__global__ __launch_bounds__(256) void pr_missrow_kernel(PairDev d) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < d.np && d.f1[k]) d.missrow[d.r1[k]] = k;
+}
+
+// Position at which the entity of terminal reference k is evicted (NIL: not
+// in this sub-batch).  M misses, the i-th (1-based) evicts once i > C - P.
+__device__ __forceinline__ uint32_t evict_pos(const PairDev& d, uint32_t k, uint32_t M) {
+  const int64_t i = (int64_t)d.r2[k] + 1 + ((int64_t)d.C - (int64_t)d.P);
+  return (i >= 1 && i <= (int64_t)M) ? d.missrow[i - 1] : NIL;
+}
+
+// ptime for the next parse: per id, the batch time from which the hash is in
+// neither level (NEVERT: not within the sub-batch; 0: gone at its start).
+// Decode: also whether anything moved (the classification repeats until not).
+__global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d, uint32_t M) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= d.newb) return;
+  uint64_t pt = NEVERT;
+  bool entity;
+  if (id < d.C) {
+    entity = d.pkey[id] != NOKEY;
+  } else {
+    const uint32_t i = id - d.C;
+    const uint64_t k = d.dkey[i];
+    entity = d.dxuid[i] == d.xuid && d.dent[i] != NOENT && k != NOKEY &&
+             tab_lookup_t(d.g, (uint32_t)k, (uint32_t)(k >> 32)) == id;
+  }
+  if (entity) {
+    const uint64_t e0 = e0_of(d, id);
+    const uint32_t tp = d.etch[id];
+    // the position after which the initial disk entry is dead (P: from the start)
+    uint32_t dr = NIL;
+    if (e0 == NOENT) {
+      dr = d.P;
+    } else {
+      const uint64_t dth = death_of(e0, d.nb);
+      if (d.dclock0 + d.clk[d.np] >= dth) {            // binary search: first q with clock(q + 1) >= death
+        uint32_t lo = d.P, hi = d.np - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (d.dclock0 + d.clk[mid + 1] >= dth) hi = mid; else lo = mid + 1;
+        }
+        dr = lo;
+      }
+    }
+    // walk the primary spans [a, b) of the entity's references; the first
+    // uncovered position at which the disk entry is dead (and not yet touched
+    // again) is the departure.  A REPLACE row ends the entity outright.
+    uint32_t cur = d.P, leave = NIL;
+    bool in_prim_start = id < d.C;
+    auto gap = [&](uint32_t g0, uint32_t g1) {
+      if (leave != NIL || g0 >= g1) return;
+      const uint32_t k = dr == NIL ? NIL : max(g0, dr);
+      if (k != NIL && k < g1 && (tp == NIL || k < tp)) leave = k;
+    };
+    const uint32_t r0 = d.erun[id];
+    if (r0 != NIL) {
+      for (uint32_t q = r0; q < d.np && d.sk[q] == id && leave == NIL; ++q) {
+        const uint32_t a = d.sv[q];
+        const uint8_t kk = d.kind[a];
+        if (kk == K_GMISS) continue;
+        if (a >= d.P) gap(cur, a);
+        if (kk == K_REPL) {                            // replaced: gone right after its own lookup
+          if (leave == NIL) { leave = a; pt = d.tim[a] + 1; }
+          break;
+        }
+        const int32_t nx = d.nxt[a];
+        const uint32_t b = (nx >= 0 && d.phit[nx]) ? (uint32_t)nx : evict_pos(d, a, M);
+        cur = max(cur, b == NIL ? NIL : b);
+        if (b == NIL) break;
+      }
+    }
+    if (leave == NIL && cur != NIL) gap(cur, d.np);
+    if (leave != NIL && pt == NEVERT) {
+      const bool present_at_start = in_prim_start || e0 != NOENT;
+      pt = (!present_at_start || leave < d.P) ? 0ull : d.tim[leave];
+    }
+  }
+  if (d.ptime[id] != pt) {
+    d.ptime[id] = pt;
+    atomicOr(&d.cnt->changed, 1u);
+  }
+}
+
+// Commit, step 1: the final primary residents -- last references that are
+// terminal and not evicted -- and the slots initial residents keep.
+__global__ __launch_bounds__(256) void pr_final_kernel(PairDev d, uint32_t E) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > d.np) return;
+  uint32_t fin = 0, nw = 0;
+  if (k < d.np && d.isr[k] && d.nxt[k] < 0 && d.r2[k] >= E) {
+    const uint32_t x = d.kind[k] == K_REPL ? d.yent[k] : d.ent[k];
+    fin = 1u;
+    if (x < d.C) d.occ[x] = 1u;
+    else nw = 1u;
+  }
+  d.f1[k] = fin;
+  d.f2[k] = nw;
+}
+// step 2: free slots (never used, or an initial resident's that left)
+__global__ __launch_bounds__(256) void pr_free_kernel(PairDev d, const uint32_t* frank) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= d.C) return;
+  if (!d.occ[s]) {
+    d.freel[frank[s]] = s;
+    d.pkey[s] = NOKEY;
+    d.pdisk[s] = NOENT;
+  }
+}
+
+__device__ __forceinline__ void add_move(const PairDev& d, uint32_t dest, uint32_t x) {
+  const uint32_t j = atomicAdd(&d.cnt->nmove, 1u);
+  if (x >= d.newb) {
+    const uint32_t r = x - d.newb;
+    d.moves[j] = make_uint4(dest, 0u, r / d.maxd, r % d.maxd);
+  } else {
+    d.moves[j] = make_uint4(dest, 1u, x, atomicAdd(&d.cnt->nstage, 1u));
+  }
+}
+
+// The disk entry an entity holds at the end of the sub-batch (NOENT: none).
+__device__ __forceinline__ uint64_t final_disk(const PairDev& d, uint32_t x, uint64_t dend) {
+  if (x >= d.newb) {                                 // its ENTER (or REPLACE) append
+    const uint32_t i = d.erun[x];
+    // (a REPLACE-made entity's run starts at its first HIT; its append is at the REPLACE row: prv)
+    uint32_t pos = d.sv[i];
+    if (d.kind[pos] != K_ENTER) pos = (uint32_t)d.prv[pos];
+    const uint32_t extra = d.kind[pos] == K_REPL && d.etch[d.ent[pos]] == pos ? 1u : 0u;
+    return d.dclock0 + d.clk[pos] + extra;
+  }
+  const uint32_t tp = d.etch[x];
+  if (tp != NIL) return d.dclock0 + d.clk[tp];
+  const uint64_t e0 = e0_of(d, x);
+  return (e0 != NOENT && dend < death_of(e0, d.nb)) ? e0 : NOENT;
+}
+
+// step 3: place every final resident (new LRU order; new slots from the free
+// list), with its key, disk link and, for a new slot, a byte move.
+__global__ __launch_bounds__(256) void pr_place_kernel(PairDev d, uint64_t dend) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= d.np || !d.f1[k]) return;
+  const uint32_t x = d.kind[k] == K_REPL ? d.yent[k] : d.ent[k];
+  uint32_t s;
+  if (x < d.C) {
+    s = x;
+  } else {
+    s = d.freel[d.r2[k]];
+    add_move(d, s, x);
+  }
+  d.lru2[d.r1[k]] = s;
+  d.pkey[s] = d.hsh[k];
+  uint64_t fd = NOENT;
+  if (x == NIL) return;
+  if (d.kind[k] == K_REPL && x == d.yent[k]) {
+    // new bytes under the replaced name: the append at this row after the touch (if any)
+    fd = d.dclock0 + d.clk[k] + (d.etch[d.ent[k]] == k ? 1u : 0u);
+  } else {
+    fd = final_disk(d, x, dend);
+  }
+  d.pdisk[s] = fd;
+}
+
+// step 4: the disk appends: per appending position the entry number, the data
+// block, its key and owner, and a byte move.  A REPLACE row appends the new
+// entity after the replaced one's touch (which XCodecDisk::remove then takes
+// out at once).
+__global__ __launch_bounds__(256) void pr_append_kernel(PairDev d) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d.np || j < d.P || !d.app[j]) return;
+  const uint8_t kk = d.kind[j];
+  uint64_t e = d.dclock0 + d.clk[j];
+  const uint32_t x = d.ent[j];
+  if (x < d.newb && d.etch[x] == j) {               // a touch of x
+    const uint32_t i = (uint32_t)(e % d.D);
+    if (kk == K_REPL || (d.dec && d.erep[x] != NIL)) {   // removed again by the (later) replace
+      d.dkey[i] = NOKEY;
+      d.dent[i] = NOENT;
+      d.dxuid[i] = d.xuid;
+    } else {
+      d.dkey[i] = d.hsh[j];
+      d.dent[i] = e;
+      d.dxuid[i] = d.xuid;
+      add_move(d, d.C + i, x);
+    }
+    ++e;
+  }
+  if (kk == K_ENTER || kk == K_REPL) {
+    const uint32_t y = kk == K_REPL ? d.yent[j] : x;
+    const uint32_t i = (uint32_t)(e % d.D);
+    d.dkey[i] = d.hsh[j];
+    d.dent[i] = e;
+    d.dxuid[i] = d.xuid;
+    add_move(d, d.C + i, y);
+  }
+}
+
+// Decode REPLACE: the replaced entity's disk entry (if live) is removed.
+__global__ __launch_bounds__(256) void pr_remove_kernel(PairDev d) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d.np || d.kind[j] != K_REPL) return;
+  const uint32_t x = d.ent[j];
+  if (x >= d.newb || d.etch[x] != NIL) return;       // (touched: the append kernel writes it removed)
+  const uint64_t e0 = e0_of(d, x);
+  if (e0 == NOENT) return;
+  const uint32_t i = (uint32_t)(e0 % d.D);
+  d.dkey[i] = NOKEY;
+  d.dent[i] = NOENT;
 }
 
 // Commit moves: w = (destination pool index, kind, a, b); kind 0: the bytes of
 // declaration b of chunk a (input), kind 1: the pre-batch bytes of pool index a
 // (staged first into staging slot b, so no move reads what another overwrote).
-__global__ __launch_bounds__(256) void pair_stage_kernel(const uint4* w, uint32_t nw, const uint8_t* pool,
+__global__ __launch_bounds__(256) void pair_stage_kernel(const uint4* w, const PairCnt* cnt, const uint8_t* pool,
                                                          uint8_t* staging) {
   const uint32_t j = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
-  if (j >= nw) return;
+  if (j >= cnt->nmove) return;
   const uint4 m = w[j];
   if (m.y != 1u) return;
   const uint8_t* src = pool + (uint64_t)m.z * SEG;
@@ -118,11 +807,11 @@ __global__ __launch_bounds__(256) void pair_stage_kernel(const uint4* w, uint32_
   *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
 }
 
-__global__ __launch_bounds__(256) void pair_move_kernel(const uint4* w, uint32_t nw, const uint8_t* in,
+__global__ __launch_bounds__(256) void pair_move_kernel(const uint4* w, const PairCnt* cnt, const uint8_t* in,
                                                         const uint64_t* chunk_off, const uint4* decl, uint32_t maxd,
                                                         const uint8_t* staging, uint8_t* pool) {
   const uint32_t j = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
-  if (j >= nw) return;
+  if (j >= cnt->nmove) return;
   const uint4 m = w[j];
   const uint8_t* src = m.y == 0u ? in + chunk_off[m.z] + decl[(uint64_t)m.z * maxd + m.w].z
                                  : staging + (uint64_t)m.w * SEG;
@@ -149,12 +838,21 @@ __global__ __launch_bounds__(256) void pair_wipe_kernel(PairWipe w) {
   if (i0 == 0) *w.nseg = 0u;
 }
 
-// G from the per-id keys (EMPTY_KEY: no hash there, or a disk block whose hash
-// also sits in the primary), plus the probe filters and the key count.
-__global__ __launch_bounds__(256) void pair_rebuild_kernel(const uint64_t* keyg, uint32_t n, HashTab g, FiltSet fs,
-                                                           uint32_t* nseg, int32_t* status) {
+// G from the state: every primary slot with a hash, and every live disk entry
+// of this front (a hash in both levels maps to its primary slot: the smaller id).
+__global__ __launch_bounds__(256) void pair_rebuild_kernel(const uint64_t* pkey, uint32_t C, const uint64_t* dkey,
+                                                           const uint64_t* dent, const uint32_t* dxuid, uint32_t D,
+                                                           uint32_t nb, uint32_t xuid, uint64_t dclock, HashTab g,
+                                                           FiltSet fs, uint32_t* nseg, int32_t* status) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t k = id < n ? keyg[id] : EMPTY_KEY;
+  uint64_t k = EMPTY_KEY;
+  if (id < C) {
+    k = pkey[id];
+  } else if (id < C + D) {
+    const uint32_t i = id - C;
+    const uint64_t e = dent[i];
+    if (dxuid[i] == xuid && e != NOENT && dclock < death_of(e, nb)) k = dkey[i];
+  }
   const bool have = k != EMPTY_KEY;
   if (have) {
     if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), id)) atomicOr(status, 2);
@@ -164,779 +862,496 @@ __global__ __launch_bounds__(256) void pair_rebuild_kernel(const uint64_t* keyg,
   if (lane_id() == 0 && m) atomicAdd(nseg, (uint32_t)__builtin_popcountll(m));
 }
 
-}  // namespace xcg
-
-namespace {
-
-using namespace xcg;
-constexpr uint32_t NIL = 0xFFFFFFFFu;
-constexpr uint64_t NEVER = ~0ull;
-constexpr uint64_t NOKEY = ~0ull;
-
-bool pair_debug() {
-  static const bool on = getenv("XCG_PAIR_DEBUG") != nullptr;
-  return on;
+// First guess of a sub-batch's references, before any parse: every chunk
+// parses as its 2048-byte tiling (its cold parse), a tile found in G being a
+// lookup hit, a repeat of an earlier tile of the batch a hit on that
+// declaration, and every other tile a declaration, entered while the window
+// 2048 bytes on (or after the last window) is examined.  One event per tile,
+// in the same row format the parse records.
+__global__ __launch_bounds__(256) void pair_seed_table_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                              uint32_t maxd, HashTab b, int32_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(i / maxd), dd = (uint32_t)(i % maxd);
+  if (c >= n || dd >= ndecl[c]) return;
+  const uint4 r = decl[i];
+  if (!tab_insert_min(b, r.x, r.y, ((uint64_t)c << 32) | r.z)) atomicOr(status, 2);
+}
+__global__ __launch_bounds__(256) void pair_seed_events_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
+                                                               uint32_t maxd, const uint32_t* chunk_len, HashTab g,
+                                                               HashTab b, uint4* ev, uint32_t* nev, uint32_t maxe) {
+  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  if (c >= n) return;
+  const uint32_t nd = min(ndecl[c], maxe), last = chunk_len[c] - SEG;
+  for (uint32_t k = (uint32_t)lane_id(); k < nd; k += 64) {
+    const uint4 dd = decl[(uint64_t)c * maxd + k];
+    const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
+    uint4 e;
+    if (gv != ~0ull) {
+      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, (EV_GHIT << 30) | (uint32_t)gv);
+    } else if (tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z)) {
+      const uint32_t t = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
+      e = make_uint4(dd.x, dd.y, t, (EV_ENTER << 30) | k);
+    } else {
+      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, EV_HIT << 30);
+    }
+    ev[(uint64_t)c * maxe + k] = e;
+  }
+  if (lane_id() == 0) nev[c] = nd;
 }
 
-// Open-addressed u64 -> u32 map whose slots are tagged with an epoch, so a
-// new pass clears it in O(1); one 16-byte slot per probe.
-struct EpochMap {
-  struct Slot {
-    uint64_t key;
-    uint32_t val, tag;
-  };
-  std::vector<Slot> t;
-  uint64_t mask = 0;
-  uint32_t epoch = 0;
-  void reset(uint64_t want) {
-    uint64_t cap = 1024;
-    while (cap < 2 * want + 16) cap <<= 1;
-    if (cap > t.size()) {
-      t.assign(cap, Slot{0, 0, 0});
-      epoch = 0;
-    }
-    mask = t.size() - 1;
-    if (++epoch == 0) {
-      for (Slot& q : t) q.tag = 0;
-      epoch = 1;
-    }
+// Statistics: this front's live disk entries (xuid) or every live entry (xuid ~0).
+__global__ __launch_bounds__(256) void pair_count_live_kernel(const uint64_t* dent, const uint32_t* dxuid, uint32_t D,
+                                                              uint32_t nb, uint64_t dclock, uint32_t xuid,
+                                                              uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool live = false;
+  if (i < D) {
+    const uint64_t e = dent[i];
+    live = e != NOENT && dclock < death_of(e, nb) && (xuid == NIL || dxuid[i] == xuid);
   }
-  static uint64_t mixk(uint64_t k) {
-    k ^= k >> 31;
-    k *= 0x9E3779B97F4A7C15ull;
-    return k ^ (k >> 29);
-  }
-  void prefetch(uint64_t k) const { __builtin_prefetch(&t[mixk(k) & mask]); }
-  uint32_t find(uint64_t k) const {
-    for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
-      const Slot& q = t[i];
-      if (q.tag != epoch) return NIL;
-      if (q.key == k) return q.val;
-    }
-  }
-  void put(uint64_t k, uint32_t v) {
-    for (uint64_t i = mixk(k) & mask;; i = (i + 1) & mask) {
-      Slot& q = t[i];
-      if (q.tag != epoch || q.key == k) {
-        q.tag = epoch;
-        q.key = k;
-        q.val = v;
-        return;
-      }
-    }
-  }
-};
+  const uint64_t m = ballot(live);
+  if (lane_id() == 0 && m) atomicAdd(out, (uint32_t)__builtin_popcountll(m));
+}
 
-}  // namespace
+// A front goes away or is cleared: its disk entries leave the index.
+__global__ __launch_bounds__(256) void pair_drop_front_kernel(uint64_t* dkey, uint64_t* dent, const uint32_t* dxuid,
+                                                              uint32_t D, uint32_t xuid) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < D && (xuid == NIL || dxuid[i] == xuid)) {
+    dent[i] = NOENT;
+    dkey[i] = NOKEY;
+  }
+}
 
-// The pair's metadata (host, authoritative) and one replay pass over a
-// sub-batch's references.  Slots: primary s in [0, C), disk data block i in
-// [0, D).  Entities: the hash in primary slot s at the sub-batch start is
-// entity s, a hash only on disk at the start is entity C + i, the pass's own
-// declarations are C + D + k.  A pass never writes the committed arrays: it
-// works on epoch-tagged copies of the slots it touches, which the commit
-// copies back (so an inconsistent pass is dropped for free).
-// One primary slot / disk block / entity record each in one cache line:
-// the committed fields, then the pass's copy (valid while ep == the pass's
-// epoch).
-//
-// The disk is shared.  XCodecDisk is one FIFO for every XCodecDiskCache
-// front-end on it (xcodec/xcodec_cache_disk.h:33-69): the local cache and each
-// peer cache XCodecCache::connect makes (XCodecDisk::connect, xcodec_cache_
-// disk.cc:640-690) append to the same ring, index entries carry the front's
-// xuid, and when the write head enters an index block every front loses the
-// entries it still had there (index_invalidate_entries, :327-382, walking
-// xuid_cache_map_).  So the ring (XcgDiskState: blocks, their owner xuid, the
-// write clock) is one object; each pair context is a front (its xuid, its
-// primary, its hash index = the live blocks it owns).  A front's pass may
-// invalidate another front's entries: they are applied to that front when the
-// pass is kept, and reach its GPU table at its next call (pending list).
-struct PSlot {
-  uint64_t key, okey;              // hash (NOKEY: free)
-  uint32_t prev, next, pd;         // LRU links; the hash's disk block (NIL: not on disk)
-  uint32_t oprev, onext, opd, owner, ep;
-};
-struct DSlot {
-  uint64_t key, okey;
-  uint32_t dp, odp;                // the hash's primary slot in its owner front (NIL: disk only)
-  uint32_t owner, ep;              // (owner: entity of the pass's front, FOREIGN for another front's entry)
-  uint16_t xuid, oxuid;            // the front whose index entry this is (XCodecDisk index entry xuid)
-  uint8_t live, olive;             // the disk index's entry for its hash
-};
-struct Ent {                       // a hash cached at the sub-batch start
-  uint64_t leave;                  // time it left both levels (NEVER)
-  uint32_t ep, p, d;
-  uint8_t ref;
-};
-struct NewEnt {                    // a declaration of the pass
-  uint64_t key;
-  uint32_t p, d, chunk, decl;
-};
-constexpr uint32_t FOREIGN = 0xFFFFFFFEu;
+}  // namespace xcg
+
+// ---------------------------------------------------------------------------
+// Host side: the state objects and the passes' drivers.
 
 struct XcgPairState;
 
-// One XCodecDisk: the ring and the fronts on it.
+// One XCodecDisk: the ring's blocks (device arrays) and the fronts on it.
 struct XcgDiskState {
   uint64_t nb = 0;                 // index blocks
   uint32_t D = 0;                  // nb * 204 data blocks
   uint64_t dclock = 0;             // entries written to the disk (every front)
-  uint32_t epoch = 0;              // pass epochs, unique across the fronts
-  std::vector<DSlot> ds;
+  int device = -1;                 // bound by the first front
+  uint64_t* dkey = nullptr;
+  uint64_t* dent = nullptr;
+  uint32_t* dxuid = nullptr;
+  // the data blocks' bytes: one physical allocation mapped behind every front's primary
+  bool vmm = false;
+  hipMemGenericAllocationHandle_t pool_h{};
+  size_t pool_bytes = 0;
   std::vector<XcgPairState*> fronts;   // by xuid (nullptr: free)
   int refs = 1;                    // the creator's reference + one per front
 };
 
 struct XcgPairState {
   uint32_t C = 0;                  // primary limit in segments
-  uint64_t nb = 0;                 // disk index blocks
-  uint32_t D = 0;                  // nb * 204 disk data blocks
+  uint32_t D = 0, nb = 0;
   XcgDiskState* disk = nullptr;
   uint16_t xuid = 0;
-  // committed scalars
-  uint32_t head = NIL, tail = NIL, pcount = 0, ftop = 0;
-  std::vector<uint32_t> pfree;     // free primary slots, pfree[0 .. ftop)
-  uint64_t dlive = 0;              // this front's live disk index entries
-  std::vector<PSlot> ps;
-  std::vector<DSlot>* dsp = nullptr;
-  // another front's kept pass took index entries of ours: ids to clear in keyg
-  std::vector<uint64_t> pending;
-  // pass state
-  uint32_t epoch = 0;
-  std::vector<uint32_t> touchedP, touchedD;
-  uint32_t s_head, s_tail, s_pcount, s_ftop;
-  uint64_t s_dclock, s_dlive;
-  std::vector<Ent> es;
-  std::vector<uint32_t> touchedE;
-  std::vector<NewEnt> ns;
-  EpochMap bmap;                   // hash -> the pass's declaration (decode: any entity of the hash)
-  // pass results
-  bool split = false;
-  std::vector<uint8_t> bad;        // per chunk: a recorded lookup the replay contradicts
-  std::vector<uint32_t> blo, bhi;  // ... the in-chunk times of the first and last such lookup
-  std::vector<uint4> writes;       // commit moves (dest, kind, a, b)
-  uint32_t nstaged = 0;
-  uint64_t enters = 0, refs = 0, appends = 0;
-  std::vector<uint64_t> leaves;    // decode: the (id, leave time) list ptime was last built from
-  // device
-  uint64_t* d_keyg = nullptr;      // [C + D]
-  uint64_t* d_ptime = nullptr;     // [C + D]
-  uint8_t* d_staging = nullptr;
-  uint64_t staging_cap = 0;
-  uint8_t* d_xfer = nullptr;       // upload area (moves, key updates, ptime list)
-  uint64_t xfer_cap = 0;
-  uint8_t* h_xfer = nullptr;       // pinned
-  uint64_t h_xfer_cap = 0;
-  uint4* h_ev = nullptr;           // pinned copy of the reference rows
-  uint64_t h_ev_cap = 0;
-  uint32_t* h_nev = nullptr;
-  uint32_t h_nev_cap = 0;
-  uint32_t* h_need = nullptr;
-  uint64_t* h_base = nullptr;      // decode: per-chunk row base and count (pinned)
-  uint32_t h_base_cap = 0;
+  uint32_t pcount = 0;             // primary entries
+  uint64_t gclock = 0;             // disk clock when G was last rebuilt
+  bool gstale = false;
+  // device state
+  uint64_t* pkey = nullptr;        // [C]
+  uint64_t* pdisk = nullptr;       // [C]
+  uint32_t* lru = nullptr;         // [C]
+  uint32_t* lru2 = nullptr;        // [C]
+  uint64_t* ptime = nullptr;       // [C + D]
+  // the pool (C primary segments, then the disk's blocks)
+  uint8_t* pool = nullptr;
+  bool pool_vmm = false;
+  void* va = nullptr;
+  size_t va_bytes = 0, prim_bytes = 0;
+  hipMemGenericAllocationHandle_t prim_h{};
+  // pass scratch, grown on demand
+  uint64_t np_cap = 0, n_cap = 0, et_cap = 0, tab_cap = 0, stg_cap = 0, tmp_cap = 0, bm_cap = 0, hk_cap = 0;
+  uint32_t* ent = nullptr; uint32_t* yent = nullptr; uint8_t* kind = nullptr; uint64_t* tim = nullptr;
+  uint64_t* hsh = nullptr; uint32_t* skey = nullptr; uint32_t* sval = nullptr; uint32_t* sk = nullptr;
+  uint32_t* sv = nullptr; int32_t* prv = nullptr; int32_t* nxt = nullptr; uint32_t* isr = nullptr;
+  uint32_t* rc = nullptr; uint8_t* phit = nullptr; uint32_t* app = nullptr; uint32_t* clk = nullptr;
+  uint32_t* slow = nullptr; uint32_t* f1 = nullptr; uint32_t* f2 = nullptr; uint32_t* r1 = nullptr;
+  uint32_t* r2 = nullptr; uint32_t* missrow = nullptr; uint4* moves = nullptr;
+  uint32_t* pbase = nullptr;       // [n + 1]
+  uint32_t* pcnt = nullptr;        // [n + 1]
+  uint32_t* etch = nullptr;        // [C + D]
+  uint32_t* erep = nullptr;        // [C + D]
+  uint32_t* erun = nullptr;        // [etot]
+  uint32_t* tab = nullptr;         // block table + its segment sums
+  uint32_t* occ = nullptr; uint32_t* freel = nullptr; uint32_t* ofl = nullptr; uint32_t* ofr = nullptr;
+  uint64_t* hk = nullptr; uint64_t* hk2 = nullptr; uint32_t* hv = nullptr; uint32_t* hv2 = nullptr;
+  uint64_t* bm_keys = nullptr; uint64_t* bm_vals = nullptr;
+  uint8_t* staging = nullptr;
+  void* tmp = nullptr;
+  xcg::PairCnt* cnt = nullptr;
+  uint32_t* h_small = nullptr;     // pinned: small readbacks
+  xcg::PairCnt* h_cnt = nullptr;   // pinned
+  // the last pass (kept for the commit)
+  xcg::PairDev last{};
+  uint32_t last_M = 0;
+  bool last_ranked = false;
+  uint64_t last_appends = 0;
+  // sub-batch bookkeeping
+  uint64_t appends = 0;            // disk blocks the last committed sub-batch wrote
   uint32_t last_base = 0;
-  int prev_passes = 1;             // passes the last sub-batch needed
-
-  uint32_t ids() const { return C + D; }
-  std::vector<DSlot>& ds() { return *dsp; }
-  const std::vector<DSlot>& ds() const { return *dsp; }
-
-  // ---- the pass's view of a slot / block / entity (copied on first use)
-  PSlot& P(uint32_t s) {
-    PSlot& q = ps[s];
-    if (q.ep != epoch) {
-      q.ep = epoch;
-      q.okey = q.key; q.oprev = q.prev; q.onext = q.next; q.opd = q.pd;
-      q.owner = q.key != NOKEY ? s : NIL;
-      touchedP.push_back(s);
-    }
-    return q;
-  }
-  DSlot& Dk(uint32_t i) {
-    DSlot& q = ds()[i];
-    if (q.ep != epoch) {
-      q.ep = epoch;
-      q.okey = q.key; q.olive = q.live; q.odp = q.dp; q.oxuid = q.xuid;
-      q.owner = !q.live ? NIL : (q.xuid != xuid ? FOREIGN : (q.dp != NIL ? q.dp : C + i));
-      touchedD.push_back(i);
-    }
-    return q;
-  }
-  Ent& E(uint32_t x) {
-    Ent& e = es[x];
-    if (e.ep != epoch) {
-      e.ep = epoch;
-      if (x < C) {
-        const PSlot& q = ps[x];              // committed fields: the sub-batch start
-        e.p = q.key != NOKEY ? x : NIL;
-        e.d = e.p != NIL ? q.pd : NIL;
-      } else {
-        const DSlot& q = ds()[x - C];
-        e.p = NIL;
-        e.d = q.live && q.xuid == xuid && q.dp == NIL ? x - C : NIL;
-      }
-      e.ref = 0;
-      e.leave = NEVER;
-      touchedE.push_back(x);
-    }
-    return e;
-  }
-  bool is_new(uint32_t x) const { return x >= C + D; }
-  // (XCG_PAIR_DEBUG) a recorded lookup the replay contradicts
-  void bad_row(uint32_t kind, uint32_t x, uint64_t h, uint64_t t) {
-    fprintf(stderr, "pair bad: xuid %u kind %u id %u%s t %llx hash %016llx key %016llx p %d d %d", xuid, kind, x,
-            is_new(x) ? " (new)" : "", (unsigned long long)t, (unsigned long long)h, (unsigned long long)ekey(x),
-            (int)ep(x), (int)ed(x));
-    if (x >= C && !is_new(x)) {
-      const DSlot& q = ds()[x - C];
-      fprintf(stderr, " | block live %u xuid %u dp %d olive %u oxuid %u odp %d ep %u/%u", q.live, q.xuid, (int)q.dp,
-              q.olive, q.oxuid, (int)q.odp, q.ep, epoch);
-    } else if (x < C) {
-      const PSlot& q = ps[x];
-      fprintf(stderr, " | slot key %016llx pd %d okey %016llx opd %d ep %u/%u", (unsigned long long)q.key, (int)q.pd,
-              (unsigned long long)q.okey, (int)q.opd, q.ep, epoch);
-    }
-    fprintf(stderr, "\n");
-  }
-  void mark_bad(uint32_t c, uint32_t t) {
-    bad[c] = 1;
-    blo[c] = t < blo[c] ? t : blo[c];
-    bhi[c] = t > bhi[c] ? t : bhi[c];
-  }
-  // an entity's current primary slot / disk block
-  uint32_t& ep(uint32_t x) { return is_new(x) ? ns[x - C - D].p : E(x).p; }
-  uint32_t& ed(uint32_t x) { return is_new(x) ? ns[x - C - D].d : E(x).d; }
-  uint64_t ekey(uint32_t x) const {
-    return is_new(x) ? ns[x - C - D].key : (x < C ? ps[x].key : ds()[x - C].key);
-  }
-  bool present(uint32_t x) { return ep(x) != NIL || ed(x) != NIL; }
-  // commit move of entity x's bytes to pool index `dest`
-  void move_to(uint32_t dest, uint32_t x) {
-    if (is_new(x)) writes.push_back(make_uint4(dest, 0u, ns[x - C - D].chunk, ns[x - C - D].decl));
-    else writes.push_back(make_uint4(dest, 1u, x, nstaged++));
-  }
-  // x is in neither level from time t on.  A cached entry's departure becomes
-  // its ptime; one this sub-batch made has no ptime (the parse sees the batch's
-  // declarations to its end), so a later lookup of it splits the sub-batch.
-  void left(uint32_t x, uint64_t t) {
-    if (!is_new(x)) E(x).leave = t;
-  }
-
-  // ---- the primary's LRU list (xcodec_lru.h: enter / use move to the tail, evict takes the head)
-  void unlink(PSlot& q) {
-    const uint32_t p = q.oprev, n = q.onext;
-    if (p != NIL) P(p).onext = n; else s_head = n;
-    if (n != NIL) P(n).oprev = p; else s_tail = p;
-  }
-  void append(uint32_t s, PSlot& q) {
-    q.oprev = s_tail;
-    q.onext = NIL;
-    if (s_tail != NIL) P(s_tail).onext = s; else s_head = s;
-    s_tail = s;
-  }
-
-  // XCodecMemoryCache::enter (xcodec_cache.h:303-325)
-  void p_enter(uint32_t x, uint64_t t) {
-    uint32_t s;
-    if (s_pcount == C) {
-      s = s_head;
-      PSlot& q = P(s);
-      const uint32_t y = q.owner;
-      unlink(q);
-      --s_pcount;
-      ep(y) = NIL;
-      if (q.opd != NIL) Dk(q.opd).odp = NIL;      // now on disk only
-      else left(y, t);
-    } else {
-      s = pfree[--s_ftop];
-    }
-    PSlot& q = P(s);
-    if (s_head != NIL) {                           // the next victim and what it links to
-      const PSlot& h = ps[s_head];
-      __builtin_prefetch(&es[s_head < C ? s_head : 0]);
-      if (h.onext != NIL && h.ep == epoch) __builtin_prefetch(&ps[h.onext]);
-      else if (h.next != NIL) __builtin_prefetch(&ps[h.next]);
-      const uint32_t hd = h.ep == epoch ? h.opd : h.pd;
-      if (hd != NIL) __builtin_prefetch(&ds()[hd]);
-    }
-    q.okey = ekey(x);
-    q.owner = x;
-    ep(x) = s;
-    append(s, q);
-    ++s_pcount;
-    const uint32_t dj = ed(x);
-    q.opd = dj;
-    if (dj != NIL) Dk(dj).odp = s;
-    move_to(s, x);
-    ++enters;
-  }
-
-  // XCodecDisk::enter (xcodec_cache_disk.cc:694-741): the shared write head
-  void d_append(uint32_t x, uint64_t t) {
-    const uint32_t i = (uint32_t)(s_dclock % D);
-    DSlot& q = Dk(i);
-    q.okey = ekey(x);
-    q.olive = 1;
-    q.oxuid = xuid;
-    q.owner = x;
-    const uint32_t p = ep(x);
-    q.odp = p;
-    if (p != NIL) P(p).opd = i;
-    ed(x) = i;
-    move_to(C + i, x);
-    ++s_dlive;
-    ++appends;
-    if (++s_dclock % DISK_ENTRIES == 0) {          // the write head moves on: index_invalidate_entries
-      const uint64_t b = (s_dclock / DISK_ENTRIES) % nb;
-      for (uint32_t j = (uint32_t)(b * DISK_ENTRIES); j < (uint32_t)((b + 1) * DISK_ENTRIES); ++j) {
-        DSlot& r = Dk(j);
-        if (!r.olive) continue;
-        const uint32_t y = r.owner;
-        r.olive = 0;
-        r.owner = NIL;
-        if (y == FOREIGN) continue;                // another front's entry: applied to it at keep()
-        --s_dlive;
-        ed(y) = NIL;
-        if (r.odp != NIL) P(r.odp).opd = NIL;      // now in the primary only
-        else left(y, t);
-      }
-    }
-  }
-
-  // XCodecCachePair::lookup on a hash present in a level (:208-230)
-  void lookup(uint32_t x, uint64_t t) {
-    if (!is_new(x)) {
-      Ent& e = E(x);
-      if (!e.ref) {
-        e.ref = 1;
-        ++refs;                                    // distinct cached entries referenced
-      }
-    }
-    const uint32_t p = ep(x);
-    if (p != NIL) {
-      PSlot& q = P(p);
-      if (s_tail != p) {                           // XCodecLRU::use
-        unlink(q);
-        append(p, q);
-      }
-      if (ed(x) == NIL) d_append(x, t);            // XCodecDisk::touch
-    } else {
-      p_enter(x, t);                               // promotion
-    }
-  }
-
-  // XCodecCachePair::replace (xcodec_cache.h:187-196) right after a lookup of
-  // x found other bytes (the decoder's name reuse, xcodec_decoder.cc:110-133;
-  // <LEARN>, xcodec_pipe_pair.cc:311-327): the primary keeps the slot (an LRU
-  // use: x is at the tail already) with the new bytes; the disk removes the
-  // hash and enters it again (XCodecDiskCache::replace, xcodec_cache_disk.h).
-  // The new bytes are a new entity y in x's place; x has left.
-  void replace(uint32_t x, uint64_t h, uint32_t c, uint32_t d, uint64_t t) {
-    const uint32_t y = C + D + (uint32_t)ns.size();
-    ns.push_back(NewEnt{h, NIL, NIL, c, d});
-    const uint32_t p = ep(x);                      // (the lookup made x primary-resident)
-    PSlot& q = P(p);
-    q.owner = y;
-    ep(y) = p;
-    ep(x) = NIL;
-    const uint32_t di = ed(x);
-    if (di != NIL) {                               // XCodecDisk::remove
-      DSlot& r = Dk(di);
-      r.olive = 0;
-      r.owner = NIL;
-      r.odp = NIL;
-      --s_dlive;
-      ed(x) = NIL;
-    }
-    q.opd = NIL;
-    move_to(p, y);
-    left(x, t + 1);                                // (x served this op's own lookup at t)
-    bmap.put(h, y);
-    d_append(y, t);
-  }
-
-  void begin_pass(uint32_t n, uint64_t decls) {
-    epoch = ++disk->epoch;
-    if (epoch == 0) {                              // (2^32 passes: re-tag everything)
-      for (XcgPairState* f : disk->fronts) {
-        if (!f) continue;
-        for (PSlot& q : f->ps) q.ep = 0;
-        for (Ent& e : f->es) e.ep = 0;
-      }
-      for (DSlot& q : ds()) q.ep = 0;
-      epoch = disk->epoch = 1;
-    }
-    touchedP.clear();
-    touchedD.clear();
-    touchedE.clear();
-    ns.clear();
-    bmap.reset(decls);
-    writes.clear();
-    writes.reserve((size_t)decls * 2);
-    ns.reserve((size_t)decls);
-    nstaged = 0;
-    enters = refs = appends = 0;
-    split = false;
-    bad.assign(n, 0);
-    blo.assign(n, ~0u);
-    bhi.assign(n, 0u);
-    s_head = head; s_tail = tail; s_pcount = pcount; s_ftop = ftop; s_dclock = disk->dclock; s_dlive = dlive;
-  }
-
-  // One replay pass over chunks [0, n) of the sub-batch: rows ev[c * maxe ..],
-  // nev[c].  Returns false if the pass is not the sequential one (bad[] and
-  // split tell why).
-  bool replay(uint32_t n, const uint4* ev, const uint32_t* nev, uint32_t maxe, uint32_t maxd) {
-    begin_pass(n, (uint64_t)n * maxd);
-    std::vector<uint32_t> order;
-    bool ok = true;
-    for (uint32_t c = 0; c < n && !split; ++c) {
-      const uint32_t cnt = nev[c];
-      if (cnt > maxe) { split = true; break; }     // (reference list overflow: a smaller sub-batch)
-      const uint4* r = ev + (uint64_t)c * maxe;
-      // rows are in stream order; a stable sort by time guards it
-      bool sorted = true;
-      for (uint32_t k = 1; k < cnt; ++k) sorted &= r[k - 1].z <= r[k].z;
-      if (!sorted) {
-        order.resize(cnt);
-        for (uint32_t k = 0; k < cnt; ++k) order[k] = k;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return r[a].z < r[b].z; });
-      }
-      for (uint32_t k = 0; k < cnt && !split; ++k) {
-        if (k + 8 < cnt) {                         // memory-level parallelism: touch ahead
-          const uint4 f = r[sorted ? k + 8 : order[k + 8]];
-          const uint32_t fk = f.w >> 30, fr = f.w & EV_REF_MASK;
-          if (fk == EV_GHIT || fk == EV_GMISS) {
-            if (fr < C + D) {
-              __builtin_prefetch(&es[fr]);
-              if (fr < C) __builtin_prefetch(&ps[fr]);
-              else __builtin_prefetch(&ds()[fr - C]);
-            }
-          } else {
-            bmap.prefetch(((uint64_t)f.y << 32) | f.x);
-          }
-        }
-        const uint4 e = r[sorted ? k : order[k]];
-        const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
-        const uint64_t t = ((uint64_t)c << 21) | e.z;
-        const uint64_t h = ((uint64_t)e.y << 32) | e.x;
-        if (kind == EV_GHIT || kind == EV_GMISS) {
-          if (ref >= C + D) { mark_bad(c, e.z); ok = false; continue; }
-          const bool pr = present(ref);
-          if (pr != (kind == EV_GHIT)) {
-            mark_bad(c, e.z);
-            ok = false;
-            if (pair_debug()) bad_row(kind, ref, h, t);
-          }
-          if (pr) lookup(ref, t);
-        } else if (kind == EV_HIT) {
-          const uint32_t x = bmap.find(h);
-          if (x == NIL) { mark_bad(c, e.z); ok = false; continue; }
-          if (!present(x)) { split = true; break; }   // made here, gone already
-          lookup(x, t);
-        } else {                                   // EV_ENTER: encode_declaration's enter (:284-286)
-          const uint32_t x0 = bmap.find(h);
-          if (x0 != NIL && present(x0)) {
-            mark_bad(c, e.z);
-            ok = false;
-            if (pair_debug()) bad_row(kind, x0, h, t);
-            continue;
-          }
-          const uint32_t x = C + D + (uint32_t)ns.size();
-          ns.push_back(NewEnt{h, NIL, NIL, c, ref});
-          bmap.put(h, x);
-          p_enter(x, t);
-          d_append(x, t);
-        }
-      }
-    }
-    return ok && !split;
-  }
-
-  // One replay pass over a decode batch's classified ops (dec_classify_kernel
-  // in pair mode): chunk c's rows are rows[base[c] .. base[c] + cnt[c]) in op
-  // order, (lo, hi, op offset | REPLACE << 31, kind << 30 | ref).  ENTER (ref =
-  // declaration row) = an EXTRACT whose hash no level holds: enter both
-  // levels; HIT = a lookup of a hash an earlier EXTRACT of the batch named;
-  // GHIT (ref = id) = a lookup of a cached hash, REPLACE when an EXTRACT's
-  // bytes differ; GMISS = no cache effect.  A decode's references are fixed by
-  // the stream except for presence, which this pass computes (ptime); the
-  // caller classifies again under it until nothing changes.  Returns false
-  // when a lookup would find a hash the batch entered already gone from both
-  // levels (the stream then blocks or re-enters there: not modelled -- split).
-  bool replay_decode(uint32_t n, const uint4* rows, const uint64_t* base, const uint64_t* cnt, uint64_t decls) {
-    begin_pass(n, decls);
-    for (uint32_t c = 0; c < n; ++c) {
-      const uint4* r = rows + base[c];
-      const uint32_t m = (uint32_t)cnt[c];
-      uint32_t d_next = 0;                         // declaration rows in op order: ENTERs and REPLACEs
-      for (uint32_t k = 0; k < m; ++k) {
-        const uint4 e = r[k];
-        const uint32_t kind = e.w >> 30, ref = e.w & EV_REF_MASK;
-        const bool rep = (e.z >> 31) != 0;
-        const uint64_t t = ((uint64_t)c << 21) | (e.z & 0x7FFFFFFFu);
-        const uint64_t h = ((uint64_t)e.y << 32) | e.x;
-        if (kind == EV_ENTER) {
-          const uint32_t x = C + D + (uint32_t)ns.size();
-          ns.push_back(NewEnt{h, NIL, NIL, c, ref});
-          d_next = ref + 1;
-          bmap.put(h, x);
-          p_enter(x, t);
-          d_append(x, t);
-        } else if (kind == EV_HIT) {
-          const uint32_t x = bmap.find(h);
-          if (x == NIL || !present(x)) { split = true; return false; }
-          lookup(x, t);
-        } else if (kind == EV_GHIT) {
-          if (ref >= C + D) { split = true; return false; }
-          if (bmap.find(h) == NIL) bmap.put(h, ref);
-          if (!present(ref)) continue;             // (classified under an older ptime: the next pass sees it)
-          lookup(ref, t);
-          if (rep) replace(ref, h, c, d_next++, t);
-        }
-      }
-    }
-    return true;
-  }
-
-  // Keep the pass: its copies -> committed; another front's entries the pass
-  // invalidated leave that front.
-  void keep() {
-    for (uint32_t s : touchedP) {
-      PSlot& q = ps[s];
-      q.key = q.okey; q.prev = q.oprev; q.next = q.onext; q.pd = q.opd;
-    }
-    for (uint32_t i : touchedD) {
-      DSlot& q = ds()[i];
-      // another front's index entry went: invalidated, and maybe rewritten with
-      // one of this front's entries since (only this front writes in its pass)
-      if (q.live && q.xuid != xuid && (!q.olive || q.oxuid != q.xuid)) {
-        XcgPairState* f = q.xuid < disk->fronts.size() ? disk->fronts[q.xuid] : nullptr;
-        if (f) {
-          --f->dlive;
-          if (q.dp != NIL) f->ps[q.dp].pd = NIL;   // in its primary only now
-          else f->pending.push_back((uint64_t)f->C + i);
-        }
-      }
-      q.key = q.okey; q.live = q.olive; q.dp = q.odp; q.xuid = q.oxuid;
-    }
-    head = s_head; tail = s_tail; pcount = s_pcount; ftop = s_ftop; disk->dclock = s_dclock; dlive = s_dlive;
-  }
+  int prev_passes = 1;
 };
 
 namespace {
 
+using namespace xcg;
+
+bool pair_debug() {
+  static const bool on = getenv("XCG_PAIR_DEBUG") != nullptr;
+  return on;
+}
+
 unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
 
-int ensure_dev(uint8_t** p, uint64_t* cap, uint64_t want) {
-  if (*cap >= want) return 0;
+template <class T>
+bool grow(T** p, uint64_t* cap, uint64_t want) {
+  if (*cap >= want) return true;
   (void)hipFree(*p);
   *p = nullptr;
   *cap = 0;
-  if (hipMalloc(p, want) != hipSuccess) return -5;
+  if (hipMalloc(p, want * sizeof(T)) != hipSuccess) return false;
   *cap = want;
-  return 0;
-}
-int ensure_pinned(uint8_t** p, uint64_t* cap, uint64_t want) {
-  if (*cap >= want) return 0;
-  if (*p) (void)hipHostFree(*p);
-  *p = nullptr;
-  *cap = 0;
-  if (hipHostMalloc(p, want) != hipSuccess) return -5;
-  *cap = want;
-  return 0;
+  return true;
 }
 
-// Upload `bytes` from the pinned transfer area to the device one (offset o).
-int upload(XcgPairState* P, uint64_t o, uint64_t bytes, hipStream_t st) {
-  if (!bytes) return 0;
-  return hipMemcpyAsync(P->d_xfer + o, P->h_xfer + o, bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -5;
-}
-
-// ptime for the next parse: NEVER everywhere, then the replay's departures.
-int upload_ptime(XcgPairState* P, hipStream_t st) {
-  const uint32_t ids = P->ids();
-  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)ids, NEVER);
-  uint64_t* kv = (uint64_t*)P->h_xfer;
-  uint32_t m = 0;
-  for (uint32_t x : P->touchedE)
-    if (P->es[x].leave != NEVER) {
-      kv[2 * m] = x;
-      kv[2 * m + 1] = P->es[x].leave;
-      ++m;
+// Pass scratch for np positions, n chunks, etot entities.
+int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
+  if (np + 1 > P->np_cap) {
+    const uint64_t cap = std::max<uint64_t>(np + 1, P->np_cap + P->np_cap / 2);
+    void** arrs[] = {(void**)&P->ent, (void**)&P->yent, (void**)&P->kind, (void**)&P->tim, (void**)&P->hsh,
+                     (void**)&P->skey, (void**)&P->sval, (void**)&P->sk, (void**)&P->sv, (void**)&P->prv,
+                     (void**)&P->nxt, (void**)&P->isr, (void**)&P->rc, (void**)&P->phit, (void**)&P->app,
+                     (void**)&P->clk, (void**)&P->slow, (void**)&P->f1, (void**)&P->f2, (void**)&P->r1,
+                     (void**)&P->r2, (void**)&P->missrow, (void**)&P->moves};
+    const size_t sz[] = {4, 4, 1, 8, 8, 4, 4, 4, 4, 4, 4, 4, 4, 1, 4, 4, 4, 4, 4, 4, 4, 4, 32};
+    for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); ++k) {
+      (void)hipFree(*arrs[k]);
+      *arrs[k] = nullptr;
     }
-  if (m) {
-    if (upload(P, 0, 16ull * m, st)) return -5;
-    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_ptime,
-                       (const uint64_t*)P->d_xfer, m);
+    P->np_cap = 0;
+    for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); ++k)
+      if (hipMalloc(arrs[k], (cap + 1) * sz[k]) != hipSuccess) return -5;
+    P->np_cap = cap;
   }
-  // (the pinned area is reused by the next upload only after a stream sync)
-  return hipStreamSynchronize(st) == hipSuccess ? 0 : -5;
+  if (n + 1 > P->n_cap) {
+    (void)hipFree(P->pbase);
+    (void)hipFree(P->pcnt);
+    P->pbase = P->pcnt = nullptr;
+    P->n_cap = 0;
+    if (hipMalloc(&P->pbase, 4 * (n + 1)) != hipSuccess || hipMalloc(&P->pcnt, 4 * (n + 1)) != hipSuccess) return -5;
+    P->n_cap = n + 1;
+  }
+  uint64_t ec = P->et_cap;
+  if (!grow(&P->erun, &ec, etot)) return -5;
+  P->et_cap = ec;
+  // rocprim temporary storage for the largest sort / scan of this size
+  size_t a = 0, b = 0, c = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
+  (void)rocprim::exclusive_scan(nullptr, b, P->isr, P->rc, 0u, (size_t)std::max(np, n) + 1,
+                                rocprim::plus<uint32_t>());
+  (void)rocprim::radix_sort_pairs(nullptr, c, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)np, 0, 64);
+  const uint64_t want = std::max(std::max(a, b), c) + 256;
+  if (want > P->tmp_cap) {
+    (void)hipFree(P->tmp);
+    P->tmp = nullptr;
+    P->tmp_cap = 0;
+    if (hipMalloc(&P->tmp, want) != hipSuccess) return -5;
+    P->tmp_cap = want;
+  }
+  return 0;
 }
 
-// The reference rows of a sub-batch, to the host.
-int download_refs(XcgPairState* P, const XcgStreamArgs& a, hipStream_t st) {
-  const uint64_t rows = (uint64_t)a.n * a.maxe;
-  if (P->h_ev_cap < rows) {
-    if (P->h_ev) (void)hipHostFree(P->h_ev);
-    P->h_ev = nullptr;
-    P->h_ev_cap = 0;
-    if (hipHostMalloc(&P->h_ev, 16 * rows) != hipSuccess) return -5;
-    P->h_ev_cap = rows;
-  }
-  if (P->h_nev_cap < a.n) {
-    if (P->h_nev) (void)hipHostFree(P->h_nev);
-    if (P->h_need) (void)hipHostFree(P->h_need);
-    P->h_nev = P->h_need = nullptr;
-    P->h_nev_cap = 0;
-    if (hipHostMalloc(&P->h_nev, 4ull * a.n) != hipSuccess || hipHostMalloc(&P->h_need, 12ull * a.n) != hipSuccess)
+int scan_u32(XcgPairState* P, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st) {
+  size_t tb = P->tmp_cap;
+  return rocprim::exclusive_scan(P->tmp, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), st) == hipSuccess
+             ? 0 : -5;
+}
+
+int read_small(XcgPairState* P, const void* src, size_t bytes, hipStream_t st) {
+  return hipMemcpyAsync(P->h_small, src, bytes, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                 hipStreamSynchronize(st) == hipSuccess
+             ? 0 : -5;
+}
+int read_cnt(XcgPairState* P, hipStream_t st) {
+  return hipMemcpyAsync(P->h_cnt, P->cnt, sizeof(PairCnt), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                 hipStreamSynchronize(st) == hipSuccess
+             ? 0 : -5;
+}
+
+// Where the rows of a pass come from.
+struct RowSrc {
+  int dec;
+  uint32_t n, maxd;
+  const uint4* ev;
+  const uint32_t* nev;             // encode
+  uint32_t maxe;
+  const uint64_t* base64;          // decode
+  const uint64_t* cnt64;
+  uint64_t rows;                   // decode: rows in all
+  uint32_t* need;                  // encode: per chunk flags / contradicted times
+  uint32_t* bad_t;
+  uint32_t* bad_hi;
+};
+
+struct PassOut {
+  uint32_t nbad = 0;
+  bool split = false;
+  bool changed = false;            // (want_leave) ptime moved
+  uint64_t appends = 0;
+};
+
+// One replay pass (see the top of this file).  want_leave: compute ptime from
+// the departures even if every lookup agrees (decode, seed guesses).
+int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave, PassOut* out, hipStream_t st) {
+  XcgDiskState* K = P->disk;
+  const uint32_t n = rs.n;
+  const uint32_t newb = P->C + P->D;
+  const uint64_t etot64 = (uint64_t)newb + (uint64_t)n * rs.maxd;
+  if (etot64 >= (1ull << 31)) return -95;
+  const uint32_t etot = (uint32_t)etot64;
+  if (!P->cnt) {
+    if (hipMalloc(&P->cnt, sizeof(PairCnt)) != hipSuccess || hipHostMalloc(&P->h_cnt, sizeof(PairCnt)) != hipSuccess ||
+        hipHostMalloc(&P->h_small, 256) != hipSuccess)
       return -5;
-    P->h_nev_cap = a.n;
   }
-  if (hipMemcpyAsync(P->h_nev, a.nev, 4ull * a.n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(P->h_ev, a.ev, 16 * rows, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
+  if (hipMemsetAsync(P->cnt, 0, sizeof(PairCnt), st) != hipSuccess) return -5;
+  PairDev d{};
+  d.C = P->C; d.xuid = P->xuid; d.P = P->pcount;
+  d.pkey = P->pkey; d.pdisk = P->pdisk; d.lru = P->lru; d.ptime = P->ptime;
+  d.D = P->D; d.nb = P->nb; d.dclock0 = K->dclock;
+  d.dkey = K->dkey; d.dent = K->dent; d.dxuid = K->dxuid;
+  d.dec = rs.dec; d.n = n; d.maxd = rs.maxd; d.maxe = rs.maxe; d.ev = rs.ev; d.nev = rs.nev;
+  d.base64 = rs.base64; d.cnt64 = rs.cnt64;
+  d.newb = newb; d.etot = etot;
+  d.need = rs.need; d.bad_t = rs.bad_t; d.bad_hi = rs.bad_hi;
+  d.g = g;
+  // rows per chunk -> positions
+  uint64_t R;
+  if (ensure_scratch(P, (uint64_t)P->pcount + 1, n, etot)) return -5;
+  if (!rs.dec) {
+    d.pbase = P->pbase;
+    d.pcnt = P->pcnt;
+    d.cnt = P->cnt;
+    hipLaunchKernelGGL(pr_count_kernel, dim3(grid_for(n + 1)), dim3(256), 0, st, d);
+    if (scan_u32(P, P->pcnt, P->pbase, (uint64_t)n + 1, st) || read_small(P, P->pbase + n, 4, st)) return -5;
+    R = P->h_small[0];
+  } else {
+    R = rs.rows;
+  }
+  const uint64_t np = (uint64_t)P->pcount + R;
+  if (np >= (1ull << 31)) return -95;
+  if (ensure_scratch(P, np, n, etot)) return -5;
+  d.np = (uint32_t)np;
+  d.ent = P->ent; d.yent = P->yent; d.kind = P->kind; d.tim = P->tim; d.hsh = P->hsh;
+  d.skey = P->skey; d.sval = P->sval; d.sk = P->sk; d.sv = P->sv; d.prv = P->prv; d.nxt = P->nxt;
+  d.isr = P->isr; d.rc = P->rc; d.phit = P->phit; d.app = P->app; d.clk = P->clk; d.slow = P->slow;
+  d.f1 = P->f1; d.f2 = P->f2; d.r1 = P->r1; d.r2 = P->r2; d.missrow = P->missrow; d.moves = P->moves;
+  d.pbase = P->pbase; d.pcnt = P->pcnt; d.cnt = P->cnt; d.etch = P->etch; d.erep = P->erep; d.erun = P->erun;
+  d.lru2 = P->lru2; d.occ = P->occ; d.freel = P->freel;
+  // encode: hash -> ENTER position
+  if (!rs.dec) {
+    const uint64_t want = std::max<uint64_t>(1024, 2ull << (64 - __builtin_clzll(R + 1)));
+    uint64_t kc = P->bm_cap, vc = P->bm_cap;
+    if (!grow(&P->bm_keys, &kc, want) || !grow(&P->bm_vals, &vc, want)) return -5;
+    P->bm_cap = std::min(kc, vc);
+    d.bm = HashTab{P->bm_keys, P->bm_vals, (uint32_t)(want - 1)};
+    hipLaunchKernelGGL(pr_fill64_kernel, dim3(grid_for(want)), dim3(256), 0, st, P->bm_keys, want, EMPTY_KEY);
+    hipLaunchKernelGGL(pr_fill64_kernel, dim3(grid_for(want)), dim3(256), 0, st, P->bm_vals, want, ~0ull);
+  }
+  hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(newb)), dim3(256), 0, st, P->etch, (uint64_t)newb, NIL);
+  if (rs.dec) hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(newb)), dim3(256), 0, st, P->erep, (uint64_t)newb, NIL);
+  hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(etot)), dim3(256), 0, st, P->erun, (uint64_t)etot, NIL);
+  if (P->pcount) hipLaunchKernelGGL(pr_pseudo_kernel, dim3(grid_for(P->pcount)), dim3(256), 0, st, d);
+  if (n) hipLaunchKernelGGL(pr_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, st, d);
+  if (rs.dec && R) {                               // decode HITs: latest definer of the hash
+    uint64_t c1 = P->hk_cap, c2 = P->hk_cap, c3 = P->hk_cap, c4 = P->hk_cap;
+    if (!grow(&P->hk, &c1, R) || !grow(&P->hk2, &c2, R) || !grow(&P->hv, &c3, R) || !grow(&P->hv2, &c4, R))
+      return -5;
+    P->hk_cap = std::min(std::min(c1, c2), std::min(c3, c4));
+    if (hipMemcpyAsync(P->hk, P->hsh + P->pcount, 8 * R, hipMemcpyDeviceToDevice, st) != hipSuccess) return -5;
+    // values: positions P .. np-1
+    hipLaunchKernelGGL(pr_iota_kernel, dim3(grid_for(R)), dim3(256), 0, st, P->hv, (uint32_t)R, P->pcount);
+    size_t tb = P->tmp_cap;
+    if (rocprim::radix_sort_pairs(P->tmp, tb, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)R, 0, 64, st) != hipSuccess)
+      return -5;
+    hipLaunchKernelGGL(pr_dec_hits_kernel, dim3(grid_for(R)), dim3(256), 0, st, d, (const uint64_t*)P->hk2,
+                       (const uint32_t*)P->hv2, (uint32_t)R);
+  }
+  hipLaunchKernelGGL(pr_resolve_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  // entity runs: sort positions by entity (stable: positions stay in order)
+  {
+    const uint32_t bits = 32 - __builtin_clz(etot | 1u);
+    size_t tb = P->tmp_cap;
+    if (rocprim::radix_sort_pairs(P->tmp, tb, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, bits, st) !=
+        hipSuccess)
+      return -5;
+  }
+  hipLaunchKernelGGL(pr_links_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (rs.dec) hipLaunchKernelGGL(pr_repl_links_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (scan_u32(P, P->isr, P->rc, np + 1, st)) return -5;
+  hipLaunchKernelGGL(pr_hits_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (read_cnt(P, st)) return -5;
+  const uint32_t nslow = P->h_cnt->nslow;
+  if (P->h_cnt->nohit) return -95;
+  if (nslow) {                                     // the block table for long gaps
+    uint32_t bsh = 8;
+    while ((np >> bsh) > 1024) ++bsh;
+    const uint32_t nbk = (uint32_t)((np + (1ull << bsh) - 1) >> bsh);
+    const uint64_t w = (uint64_t)nbk + 1;
+    const uint64_t cells = (uint64_t)nbk * w + TSEG * w;
+    uint64_t tc = P->tab_cap;
+    if (!grow(&P->tab, &tc, cells)) return -5;
+    P->tab_cap = tc;
+    d.tab = P->tab;
+    d.bsh = bsh;
+    d.nbk = nbk;
+    if (hipMemsetAsync(P->tab, 0, 4 * (uint64_t)nbk * w, st) != hipSuccess) return -5;
+    hipLaunchKernelGGL(pr_tab_hist_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(pr_tab_rows_kernel, dim3((nbk + 3) / 4), dim3(256), 0, st, d);
+    uint32_t* segsum = P->tab + (uint64_t)nbk * w;
+    hipLaunchKernelGGL(pr_tab_cols_kernel, dim3(grid_for(w * TSEG)), dim3(256), 0, st, d, segsum, 0);
+    hipLaunchKernelGGL(pr_tab_cols_kernel, dim3(grid_for(w)), dim3(256), 0, st, d, segsum, 1);
+    hipLaunchKernelGGL(pr_tab_cols_kernel, dim3(grid_for(w * TSEG)), dim3(256), 0, st, d, segsum, 2);
+    hipLaunchKernelGGL(pr_tab_query_kernel, dim3((nslow + 3) / 4), dim3(256), 0, st, d);
+  }
+  // the disk clock: monotone rounds to the least fixed point
+  int rounds = 0;
+  for (;; ++rounds) {
+    if (scan_u32(P, P->app, P->clk, np + 1, st)) return -5;
+    if (rounds >= 64) return -75;
+    if (hipMemsetAsync(&P->cnt->changed, 0, 4, st) != hipSuccess) return -5;
+    hipLaunchKernelGGL(pr_touch_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    if (read_cnt(P, st)) return -5;
+    if (P->h_cnt->changed == 0) break;
+  }
+  hipLaunchKernelGGL(pr_check_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (hipMemcpyAsync(P->h_small, P->clk + np, 4, hipMemcpyDeviceToHost, st) != hipSuccess || read_cnt(P, st))
+    return -5;
+  out->appends = P->h_small[0];
+  out->nbad = P->h_cnt->nbad;
+  out->split = P->h_cnt->split != 0 || P->h_cnt->unsorted != 0;
+  P->last = d;
+  P->last_ranked = false;
+  P->last_appends = out->appends;
+  if (pair_debug())
+    fprintf(stderr, "pair-replay: dec %d n %u rows %llu P %u slow %u touch-rounds %d appends %llu bad %u split %u "
+                    "unsorted %u\n", rs.dec, n, (unsigned long long)R, P->pcount, nslow, rounds,
+            (unsigned long long)out->appends, out->nbad, P->h_cnt->split, P->h_cnt->unsorted);
+  if (out->split) return 0;
+  if (want_leave || out->nbad) {
+    hipLaunchKernelGGL(pr_missterm_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d);
+    if (scan_u32(P, P->f1, P->r1, np + 1, st) || scan_u32(P, P->f2, P->r2, np + 1, st)) return -5;
+    hipLaunchKernelGGL(pr_missrow_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    if (read_small(P, P->r1 + np, 4, st)) return -5;
+    P->last_M = P->h_small[0];
+    P->last_ranked = true;
+    if (hipMemsetAsync(&P->cnt->changed, 0, 4, st) != hipSuccess) return -5;
+    hipLaunchKernelGGL(pr_leave_kernel, dim3(grid_for(newb)), dim3(256), 0, st, d, P->last_M);
+    if (read_cnt(P, st)) return -5;
+    out->changed = P->h_cnt->changed != 0;
+  }
+  return 0;
+}
+
+// The primary's arrays must outlive one replay; the commit's slot arrays too.
+int ensure_front_arrays(XcgPairState* P) {
+  if (P->occ) return 0;
+  if (hipMalloc(&P->occ, 4ull * P->C) != hipSuccess || hipMalloc(&P->freel, 4ull * P->C) != hipSuccess ||
+      hipMalloc(&P->ofl, 4ull * (P->C + 1)) != hipSuccess || hipMalloc(&P->ofr, 4ull * (P->C + 1)) != hipSuccess)
     return -5;
   return 0;
 }
 
-// XCodecHash::hash of one segment (xcodec/xcodec_hash.h:166-174), host side,
-// for the XCG_PAIR_VERIFY diagnostics.
-uint64_t host_hash(const uint8_t* w) {
-  uint32_t s1 = 0, s2 = 0, b1 = 0, b2 = 0;
-  for (int k = 0; k < SEG; ++k) {
-    s1 += (uint32_t)w[k] + 1u;
-    s2 += s1;
-    b1 += w[k] ? (uint32_t)__builtin_ctz(w[k]) + 1u : 0u;
-    b2 += b1;
-  }
-  const uint32_t bits = (b1 << 16) + b2, bytes = (s1 << 20) + s2;
-  return ((uint64_t)bits << 36) + (uint64_t)bytes;
-}
-
-// Diagnostics (XCG_PAIR_VERIFY): every primary slot and live disk block holds
-// bytes of its hash, and G finds every level entry.
-void pair_verify(XcgPairState* P, const uint8_t* d_pool, hipStream_t st) {
-  const uint64_t ids = P->ids();
-  std::vector<uint8_t> pool(ids * SEG);
-  std::vector<uint64_t> keyg(ids);
-  (void)hipStreamSynchronize(st);
-  (void)hipMemcpy(pool.data(), d_pool, ids * SEG, hipMemcpyDeviceToHost);
-  (void)hipMemcpy(keyg.data(), P->d_keyg, 8 * ids, hipMemcpyDeviceToHost);
-  uint32_t bad = 0;
-  for (uint32_t s = 0; s < P->C; ++s) {
-    const PSlot& q = P->ps[s];
-    if (q.key == NOKEY) continue;
-    if (host_hash(&pool[(uint64_t)s * SEG]) != q.key && bad++ < 5)
-      fprintf(stderr, "pair verify: primary slot %u bytes do not hash to its key\n", s);
-    if (keyg[s] != q.key && bad++ < 5) fprintf(stderr, "pair verify: keyg[%u] stale\n", s);
-    if (q.pd != NIL && (P->ds()[q.pd].key != q.key || !P->ds()[q.pd].live || P->ds()[q.pd].xuid != P->xuid) &&
-        bad++ < 5)
-      fprintf(stderr, "pair verify: slot %u links disk block %u of another hash\n", s, q.pd);
-  }
-  uint64_t mine = 0;
-  for (uint32_t i = 0; i < P->D; ++i) {
-    const DSlot& q = P->ds()[i];
-    const bool own = q.live && q.xuid == P->xuid;
-    mine += own;
-    const uint64_t want = own && q.dp == NIL ? q.key : NOKEY;
-    if (keyg[P->C + i] != want && bad++ < 5) fprintf(stderr, "pair verify: keyg[C+%u] stale\n", i);
-    if (!own) continue;
-    if (host_hash(&pool[((uint64_t)P->C + i) * SEG]) != q.key && bad++ < 5)
-      fprintf(stderr, "pair verify: disk block %u bytes do not hash to its key\n", i);
-    if (q.dp != NIL && P->ps[q.dp].key != q.key && bad++ < 5)
-      fprintf(stderr, "pair verify: disk block %u links slot %u of another hash\n", i, q.dp);
-  }
-  if (mine != P->dlive && bad++ < 5) fprintf(stderr, "pair verify: %llu own disk entries, count says %llu\n",
-                                             (unsigned long long)mine, (unsigned long long)P->dlive);
-  fprintf(stderr, "pair verify: %u problems (primary %u, disk live %llu)\n", bad, P->pcount,
-          (unsigned long long)P->dlive);
-}
-
-// G from scratch: wipe, then every id whose keyg holds a hash.
+// G from the state: wipe, then every primary slot and live own disk block.
 void pair_rebuild(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   const HashTab g{G.g_keys, G.g_vals, G.g_mask};
   const FiltSet fs{G.g_filt, G.g_ftab, G.fmask, G.g_gfilt, G.gmask};
   PairWipe wp{g, G.g_filt, (u32x4*)G.g_ftab, G.fmask + 1, G.g_gfilt, G.gmask + 1, G.nseg};
   hipLaunchKernelGGL(pair_wipe_kernel, dim3(1024), dim3(256), 0, st, wp);
-  const uint32_t ids = P->ids();
-  hipLaunchKernelGGL(pair_rebuild_kernel, dim3(grid_for(ids)), dim3(256), 0, st, (const uint64_t*)P->d_keyg, ids,
-                     g, fs, G.nseg, G.status);
+  XcgDiskState* K = P->disk;
+  hipLaunchKernelGGL(pair_rebuild_kernel, dim3(grid_for((uint64_t)P->C + P->D)), dim3(256), 0, st,
+                     (const uint64_t*)P->pkey, P->C, (const uint64_t*)K->dkey, (const uint64_t*)K->dent,
+                     (const uint32_t*)K->dxuid, P->D, P->nb, (uint32_t)P->xuid, K->dclock, g, fs, G.nseg, G.status);
+  P->gclock = K->dclock;
+  P->gstale = false;
 }
 
-// Commit a kept pass on the GPU: bytes, per-id keys, G and its filters.
+__global__ __launch_bounds__(256) void pr_notocc_kernel(const uint32_t* occ, uint32_t C, uint32_t* fl) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s <= C) fl[s] = s < C && !occ[s] ? 1u : 0u;
+}
+
+// Commit the last (consistent) pass: final primary, disk appends, bytes, G.
 int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
-  // A primary slot can change hands more than once in a sub-batch (an entry
-  // evicted to disk frees it again), and a small disk can lap within one:
-  // only the last move into each destination stays.  (Sources are the input or
-  // pre-sub-batch bytes, staged before any move.)
-  {
-    std::vector<uint4>& w = P->writes;
-    std::vector<uint8_t> seen(P->ids(), 0);
-    size_t k = w.size();
-    for (size_t j = w.size(); j-- > 0;) {
-      if (seen[w[j].x]) continue;
-      seen[w[j].x] = 1;
-      w[--k] = w[j];
-    }
-    w.erase(w.begin(), w.begin() + (ptrdiff_t)k);
+  XcgDiskState* K = P->disk;
+  PairDev d = P->last;
+  const uint64_t np = d.np;
+  if (ensure_front_arrays(P)) return -5;
+  d.occ = P->occ; d.freel = P->freel; d.lru2 = P->lru2;
+  if (!P->last_ranked) {
+    hipLaunchKernelGGL(pr_missterm_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d);
+    if (scan_u32(P, P->f1, P->r1, np + 1, st) || scan_u32(P, P->f2, P->r2, np + 1, st)) return -5;
+    hipLaunchKernelGGL(pr_missrow_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    if (read_small(P, P->r1 + np, 4, st)) return -5;
+    P->last_M = P->h_small[0];
   }
-  const uint32_t nw = (uint32_t)P->writes.size();
-  // per-id key updates for every slot the pass touched (a disk block counts
-  // for this front only while its live index entry is this front's)
-  std::vector<uint64_t> kv;
-  kv.reserve(2 * (P->touchedP.size() + P->touchedD.size() + P->pending.size()));
-  for (uint32_t s : P->touchedP) {
-    kv.push_back(s);
-    kv.push_back(P->ps[s].key);
-  }
-  for (uint32_t i : P->touchedD) {
-    const DSlot& q = P->ds()[i];
-    kv.push_back((uint64_t)P->C + i);
-    kv.push_back(q.live && q.xuid == P->xuid && q.dp == NIL ? q.key : NOKEY);
-  }
-  const uint32_t nk = (uint32_t)(kv.size() / 2);
-  const uint64_t wbytes = 16ull * nw, kbytes = 8ull * kv.size();
-  if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, wbytes + kbytes + 16) ||
-      ensure_dev(&P->d_xfer, &P->xfer_cap, wbytes + kbytes + 16) ||
-      ensure_dev(&P->d_staging, &P->staging_cap, (uint64_t)(P->nstaged ? P->nstaged : 1) * SEG))
+  const uint32_t M = P->last_M;
+  const int64_t E64 = (int64_t)d.P + (int64_t)M - (int64_t)P->C;
+  const uint32_t E = E64 > 0 ? (uint32_t)E64 : 0u;
+  const uint64_t dend = K->dclock + P->last_appends;
+  if (hipMemsetAsync(P->occ, 0, 4ull * P->C, st) != hipSuccess ||
+      hipMemsetAsync(&P->cnt->nmove, 0, 8, st) != hipSuccess)
     return -5;
-  memcpy(P->h_xfer, P->writes.data(), wbytes);
-  memcpy(P->h_xfer + wbytes, kv.data(), kbytes);
-  if (upload(P, 0, wbytes + kbytes, st)) return -5;
-  const uint4* w = (const uint4*)P->d_xfer;
-  if (nw) {
-    hipLaunchKernelGGL(pair_stage_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, (const uint8_t*)G.pool,
-                       P->d_staging);
-    hipLaunchKernelGGL(pair_move_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, w, nw, G.in, G.chunk_off,
-                       (const uint4*)G.decl, G.maxd, (const uint8_t*)P->d_staging, G.pool);
+  // (terminal ranks r2 are consumed by pr_final before f1 / f2 / r1 / r2 are reused)
+  hipLaunchKernelGGL(pr_final_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d, E);
+  if (scan_u32(P, P->f1, P->r1, np + 1, st) || scan_u32(P, P->f2, P->r2, np + 1, st)) return -5;
+  hipLaunchKernelGGL(pr_notocc_kernel, dim3(grid_for(P->C + 1)), dim3(256), 0, st, (const uint32_t*)P->occ, P->C,
+                     P->ofl);
+  if (scan_u32(P, P->ofl, P->ofr, (uint64_t)P->C + 1, st)) return -5;
+  hipLaunchKernelGGL(pr_free_kernel, dim3(grid_for(P->C)), dim3(256), 0, st, d, (const uint32_t*)P->ofr);
+  hipLaunchKernelGGL(pr_place_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, dend);
+  if (d.dec) hipLaunchKernelGGL(pr_remove_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(pr_append_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (hipMemcpyAsync(P->h_small, P->r1 + np, 4, hipMemcpyDeviceToHost, st) != hipSuccess || read_cnt(P, st))
+    return -5;
+  const uint32_t pc = P->h_small[0], nmove = P->h_cnt->nmove, nstage = P->h_cnt->nstage;
+  if (pc > P->C) return -5;
+  uint64_t sc = P->stg_cap;
+  if (!grow(&P->staging, &sc, (uint64_t)std::max<uint32_t>(nstage, 1) * SEG)) return -5;
+  P->stg_cap = sc;
+  if (nmove) {
+    hipLaunchKernelGGL(pair_stage_kernel, dim3((nmove + 3) / 4), dim3(256), 0, st, (const uint4*)P->moves,
+                       (const PairCnt*)P->cnt, (const uint8_t*)G.pool, P->staging);
+    hipLaunchKernelGGL(pair_move_kernel, dim3((nmove + 3) / 4), dim3(256), 0, st, (const uint4*)P->moves,
+                       (const PairCnt*)P->cnt, G.in, G.chunk_off, (const uint4*)G.decl, G.maxd,
+                       (const uint8_t*)P->staging, G.pool);
   }
-  if (nk)
-    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(nk)), dim3(256), 0, st, P->d_keyg,
-                       (const uint64_t*)(P->d_xfer + wbytes), nk);
+  std::swap(P->lru, P->lru2);
+  P->pcount = pc;
+  K->dclock = dend;
+  P->appends = P->last_appends;
   pair_rebuild(P, G, st);
-  // (the pinned transfer area is free again once the stream passes here)
   return hipStreamSynchronize(st) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// Index entries another front's kept pass took from this one (the shared
-// ring's invalidations): clear their ids and rebuild G before this front's
-// next batch looks anything up.
-int pair_sync_pending(XcgPairState* P, const PairGpu& G, hipStream_t st) {
-  if (P->pending.empty()) return 0;
-  const uint32_t m = (uint32_t)P->pending.size();
-  std::vector<uint64_t> kv(2ull * m);
-  for (uint32_t j = 0; j < m; ++j) {
-    kv[2 * j] = P->pending[j];
-    kv[2 * j + 1] = NOKEY;
-  }
-  P->pending.clear();
-  if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * m) || ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * m))
-    return -5;
-  memcpy(P->h_xfer, kv.data(), 16ull * m);
-  if (upload(P, 0, 16ull * m, st)) return -5;
-  hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_keyg,
-                     (const uint64_t*)P->d_xfer, m);
+int fill_ptime(XcgPairState* P, hipStream_t st) {
+  hipLaunchKernelGGL(pr_fill64_kernel, dim3(1024), dim3(256), 0, st, P->ptime, (uint64_t)P->C + P->D, NEVERT);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Entries another front's writes retired (the clock crossed an index block
+// since G was built): rebuild G before this front looks anything up.
+int pair_sync_front(XcgPairState* P, const PairGpu& G, hipStream_t st) {
+  XcgDiskState* K = P->disk;
+  if (!P->gstale && K->dclock / DISK_ENTRIES == P->gclock / DISK_ENTRIES) return 0;
   pair_rebuild(P, G, st);
   return hipStreamSynchronize(st) == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -944,6 +1359,100 @@ int pair_sync_pending(XcgPairState* P, const PairGpu& G, hipStream_t st) {
 PairGpu gpu_of(const XcgStreamArgs& a) {
   return PairGpu{a.in, a.chunk_off, a.decl, a.maxd, a.pool, a.g_keys, a.g_vals, a.g_mask,
                  a.g_filt, a.g_ftab, a.fmask, a.g_gfilt, a.gmask, a.nseg, a.status};
+}
+
+// The disk's device arrays, on the first front's device.
+int disk_bind(XcgDiskState* K, int device) {
+  if (K->device >= 0) return K->device == device ? 0 : -22;
+  const uint64_t D = K->D;
+  if (hipMalloc(&K->dkey, 8 * D) != hipSuccess || hipMalloc(&K->dent, 8 * D) != hipSuccess ||
+      hipMalloc(&K->dxuid, 4 * D) != hipSuccess || hipMemset(K->dkey, 0xFF, 8 * D) != hipSuccess ||
+      hipMemset(K->dent, 0xFF, 8 * D) != hipSuccess || hipMemset(K->dxuid, 0xFF, 4 * D) != hipSuccess) {
+    (void)hipFree(K->dkey); (void)hipFree(K->dent); (void)hipFree(K->dxuid);
+    K->dkey = K->dent = nullptr;
+    K->dxuid = nullptr;
+    return -12;
+  }
+  K->device = device;
+  return 0;
+}
+
+size_t round_up(size_t v, size_t g) { return (v + g - 1) / g * g; }
+
+// The front's pool: C primary segments followed by the disk's D blocks at
+// pool + (C + i) * 2048.  HIP virtual memory maps the disk's one physical
+// allocation behind every front; without it each front allocates its own copy
+// (a front reads only the blocks it wrote itself, so that is correct too).
+int map_pool(XcgPairState* P, int device) {
+  XcgDiskState* K = P->disk;
+  if (!getenv("XCG_NO_VMM")) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    bool ok = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) == hipSuccess &&
+              gran > 0;
+    if (ok && !K->vmm && K->pool_bytes == 0) {
+      const size_t sd = round_up((size_t)K->D * SEG + 256, gran);
+      if (hipMemCreate(&K->pool_h, sd, &prop, 0) == hipSuccess) {
+        K->pool_bytes = sd;
+        K->vmm = true;
+      }
+    }
+    ok = ok && K->vmm;
+    const size_t sp = round_up((size_t)P->C * SEG, gran ? gran : 1);
+    bool prim = false, reserved = false, m1 = false, m2 = false;
+    if (ok) prim = ok = hipMemCreate(&P->prim_h, sp, &prop, 0) == hipSuccess;
+    if (ok) reserved = ok = hipMemAddressReserve(&P->va, sp + K->pool_bytes, 0, nullptr, 0) == hipSuccess;
+    if (ok) m1 = ok = hipMemMap(P->va, sp, 0, P->prim_h, 0) == hipSuccess;
+    if (ok) m2 = ok = hipMemMap((char*)P->va + sp, K->pool_bytes, 0, K->pool_h, 0) == hipSuccess;
+    if (ok) {
+      hipMemAccessDesc acc{};
+      acc.location = prop.location;
+      acc.flags = hipMemAccessFlagsProtReadWrite;
+      ok = hipMemSetAccess(P->va, sp + K->pool_bytes, &acc, 1) == hipSuccess;
+    }
+    if (ok) {
+      P->pool_vmm = true;
+      P->prim_bytes = sp;
+      P->va_bytes = sp + K->pool_bytes;
+      P->pool = (uint8_t*)P->va + sp - (size_t)P->C * SEG;
+      return 0;
+    }
+    if (m2) (void)hipMemUnmap((char*)P->va + sp, K->pool_bytes);
+    if (m1) (void)hipMemUnmap(P->va, sp);
+    if (reserved) (void)hipMemAddressFree(P->va, sp + K->pool_bytes);
+    if (prim) (void)hipMemRelease(P->prim_h);
+    P->va = nullptr;
+    (void)hipGetLastError();
+  }
+  if (hipMalloc(&P->pool, ((uint64_t)P->C + P->D) * SEG + 256) != hipSuccess) return -12;
+  P->pool_vmm = false;
+  return 0;
+}
+
+void unmap_pool(XcgPairState* P) {
+  if (P->pool_vmm) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemUnmap((char*)P->va + P->prim_bytes, P->va_bytes - P->prim_bytes);
+    (void)hipMemUnmap(P->va, P->prim_bytes);
+    (void)hipMemAddressFree(P->va, P->va_bytes);
+    (void)hipMemRelease(P->prim_h);
+  } else {
+    (void)hipFree(P->pool);
+  }
+  P->pool = nullptr;
+}
+
+void free_scratch(XcgPairState* P) {
+  void* arrs[] = {P->ent, P->yent, P->kind, P->tim, P->hsh, P->skey, P->sval, P->sk, P->sv, P->prv, P->nxt,
+                  P->isr, P->rc, P->phit, P->app, P->clk, P->slow, P->f1, P->f2, P->r1, P->r2, P->missrow,
+                  P->moves, P->pbase, P->pcnt, P->etch, P->erep, P->erun, P->tab, P->occ, P->freel, P->ofl, P->ofr, P->hk, P->hk2,
+                  P->hv, P->hv2, P->bm_keys, P->bm_vals, P->staging, P->tmp, P->cnt};
+  for (void* p : arrs) (void)hipFree(p);
+  if (P->h_small) (void)hipHostFree(P->h_small);
+  if (P->h_cnt) (void)hipHostFree(P->h_cnt);
 }
 
 }  // namespace
@@ -958,19 +1467,30 @@ int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out) {
   XcgDiskState* K = new XcgDiskState;
   K->nb = nb;
   K->D = (uint32_t)(nb * DISK_ENTRIES);
-  K->ds.assign(K->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0, 0, 0});
   *out = K;
   return 0;
 }
 
 void xcg_disk_state_release(XcgDiskState* K) {
-  if (K && --K->refs == 0) delete K;
+  if (!K || --K->refs > 0) return;
+  (void)hipFree(K->dkey); (void)hipFree(K->dent); (void)hipFree(K->dxuid);
+  if (K->vmm) (void)hipMemRelease(K->pool_h);
+  delete K;
 }
 
 void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
   uint64_t live = 0, fronts = 0;
-  for (const DSlot& q : K->ds) live += q.live;
   for (const XcgPairState* f : K->fronts) fronts += f != nullptr;
+  if (K->device >= 0) {
+    uint32_t* d = nullptr;
+    uint32_t h = 0;
+    if (hipMalloc(&d, 4) == hipSuccess && hipMemset(d, 0, 4) == hipSuccess) {
+      hipLaunchKernelGGL(pair_count_live_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr,
+                         (const uint64_t*)K->dent, (const uint32_t*)K->dxuid, K->D, (uint32_t)K->nb, K->dclock, NIL, d);
+      if (hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost) == hipSuccess) live = h;
+    }
+    (void)hipFree(d);
+  }
   st[0] = live;
   st[1] = K->dclock;
   st[2] = K->nb;
@@ -978,29 +1498,34 @@ void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
 }
 
 // A pair front on disk K (XCodecDisk::local for the first, ::connect for the
-// others: the lowest free xuid, xcodec_cache_disk.cc:640-690).
+// others: the lowest free xuid, xcodec_cache_disk.cc:640-690), on the current
+// device.
 int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
   if (C == 0 || !K || (uint64_t)K->D + C >= (1ull << 30)) return -22;
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return -5;
+  const int brc = disk_bind(K, device);
+  if (brc) return brc;
   uint32_t xuid = 0;
   while (xuid < K->fronts.size() && K->fronts[xuid]) ++xuid;
   if (xuid >= 1024) return -22;                             // XCDFS_XUID_COUNT
   XcgPairState* P = new XcgPairState;
   P->C = C;
-  P->nb = K->nb;
+  P->nb = (uint32_t)K->nb;
   P->D = K->D;
   P->disk = K;
-  P->dsp = &K->ds;
   P->xuid = (uint16_t)xuid;
-  const uint32_t D = P->D, ids = C + D;
-  P->ps.assign(C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
-  P->es.assign(ids, Ent{NEVER, 0, NIL, NIL, 0});
-  P->pfree.resize(C);
-  for (uint32_t s = 0; s < C; ++s) P->pfree[s] = C - 1 - s;   // slot 0 first
-  P->ftop = C;
-  if (hipMalloc(&P->d_keyg, 8ull * ids) != hipSuccess || hipMalloc(&P->d_ptime, 8ull * ids) != hipSuccess ||
-      hipMemset(P->d_keyg, 0xFF, 8ull * ids) != hipSuccess || hipMemset(P->d_ptime, 0xFF, 8ull * ids) != hipSuccess) {
-    (void)hipFree(P->d_keyg);
-    (void)hipFree(P->d_ptime);
+  P->gclock = K->dclock;
+  const uint64_t ids = (uint64_t)C + P->D;
+  if (hipMalloc(&P->pkey, 8ull * C) != hipSuccess || hipMalloc(&P->pdisk, 8ull * C) != hipSuccess ||
+      hipMalloc(&P->lru, 4ull * C) != hipSuccess || hipMalloc(&P->lru2, 4ull * C) != hipSuccess ||
+      hipMalloc(&P->ptime, 8 * ids) != hipSuccess || hipMalloc(&P->etch, 4 * ids) != hipSuccess ||
+      hipMalloc(&P->erep, 4 * ids) != hipSuccess ||
+      hipMemset(P->pkey, 0xFF, 8ull * C) != hipSuccess || hipMemset(P->pdisk, 0xFF, 8ull * C) != hipSuccess ||
+      hipMemset(P->ptime, 0xFF, 8 * ids) != hipSuccess || ensure_front_arrays(P) != 0 || map_pool(P, device) != 0) {
+    (void)hipFree(P->pkey); (void)hipFree(P->pdisk); (void)hipFree(P->lru); (void)hipFree(P->lru2);
+    (void)hipFree(P->ptime);
+    free_scratch(P);
     delete P;
     return -12;
   }
@@ -1011,21 +1536,23 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
   return 0;
 }
 
-// A front goes away (its XCodecCache is deleted): its entries stay in the
-// ring as entries of no live front (index_invalidate_entries skips an xuid
-// with no cache, xcodec_cache_disk.cc:360-364).
+uint8_t* xcg_pair_state_pool(const XcgPairState* P) { return P->pool; }
+
+// A front goes away (its XCodecCache is deleted): its entries leave the ring's
+// index (XCodecDisk::disconnect).
 void xcg_pair_state_destroy(XcgPairState* P) {
   if (!P) return;
-  (void)hipFree(P->d_keyg); (void)hipFree(P->d_ptime); (void)hipFree(P->d_staging); (void)hipFree(P->d_xfer);
-  if (P->h_xfer) (void)hipHostFree(P->h_xfer);
-  if (P->h_ev) (void)hipHostFree(P->h_ev);
-  if (P->h_nev) (void)hipHostFree(P->h_nev);
-  if (P->h_need) (void)hipHostFree(P->h_need);
-  if (P->h_base) (void)hipHostFree(P->h_base);
   XcgDiskState* K = P->disk;
+  (void)hipDeviceSynchronize();
+  if (K && K->dent)
+    hipLaunchKernelGGL(pair_drop_front_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr, K->dkey, K->dent,
+                       (const uint32_t*)K->dxuid, K->D, (uint32_t)P->xuid);
+  (void)hipDeviceSynchronize();
+  unmap_pool(P);
+  (void)hipFree(P->pkey); (void)hipFree(P->pdisk); (void)hipFree(P->lru); (void)hipFree(P->lru2);
+  (void)hipFree(P->ptime);
+  free_scratch(P);
   if (K) {
-    for (DSlot& q : K->ds)
-      if (q.live && q.xuid == P->xuid) q.live = 0;
     K->fronts[P->xuid] = nullptr;
     xcg_disk_state_release(K);
   }
@@ -1036,115 +1563,70 @@ void xcg_pair_state_destroy(XcgPairState* P) {
 // a fresh front; on a disk of its own, a fresh volume).  The caller wipes G.
 int xcg_pair_state_clear(XcgPairState* P) {
   XcgDiskState* K = P->disk;
-  P->ps.assign(P->C, PSlot{NOKEY, NOKEY, NIL, NIL, NIL, NIL, NIL, NIL, NIL, 0});
   uint64_t others = 0;
   for (const XcgPairState* f : K->fronts) others += f && f != P;
-  for (DSlot& q : K->ds) {
-    if (q.live && q.xuid == P->xuid) q.live = 0;
-    q.dp = q.xuid == P->xuid ? NIL : q.dp;
-  }
-  if (others == 0) {
-    K->ds.assign(K->D, DSlot{NOKEY, NOKEY, NIL, NIL, NIL, 0, 0, 0, 0, 0});
-    K->dclock = 0;
-  }
-  for (Ent& e : P->es) e.ep = 0;
-  for (uint32_t s = 0; s < P->C; ++s) P->pfree[s] = P->C - 1 - s;
-  P->ftop = P->C;
-  P->head = P->tail = NIL;
+  if (hipMemset(P->pkey, 0xFF, 8ull * P->C) != hipSuccess || hipMemset(P->pdisk, 0xFF, 8ull * P->C) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(pair_drop_front_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr, K->dkey, K->dent,
+                     (const uint32_t*)K->dxuid, K->D, others ? (uint32_t)P->xuid : NIL);
+  if (!others) K->dclock = 0;
   P->pcount = 0;
-  P->dlive = 0;
-  P->pending.clear();
-  return hipMemset(P->d_keyg, 0xFF, 8ull * P->ids()) == hipSuccess ? 0 : -5;
+  P->gclock = K->dclock;
+  P->gstale = false;
+  P->prev_passes = 1;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -5;
 }
 
 void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st) {
+  const XcgDiskState* K = P->disk;
+  uint32_t h = 0;
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, 4) == hipSuccess && hipMemset(d, 0, 4) == hipSuccess) {
+    hipLaunchKernelGGL(pair_count_live_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr, (const uint64_t*)K->dent,
+                       (const uint32_t*)K->dxuid, K->D, (uint32_t)K->nb, K->dclock, (uint32_t)P->xuid, d);
+    (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(d);
   st[0] = P->pcount;
-  st[1] = P->dlive;
-  st[2] = P->disk->dclock;
+  st[1] = h;
+  st[2] = K->dclock;
   st[3] = P->nb;
 }
 
 uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; }
 uint32_t xcg_pair_state_limit(const XcgPairState* P) { return P->C; }
 uint32_t xcg_pair_state_disk_blocks(const XcgPairState* P) { return P->D; }
-const uint64_t* xcg_pair_state_ptime(const XcgPairState* P) { return P->d_ptime; }
+const uint64_t* xcg_pair_state_ptime(const XcgPairState* P) { return P->ptime; }
 
-int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st) { return pair_sync_pending(P, *G, st); }
+int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st) { return pair_sync_front(P, *G, st); }
 
 // Decode on the pair, first step: ptime NEVER everywhere.
-int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st) {
-  P->leaves.clear();
-  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
-  return hipGetLastError() == hipSuccess ? 0 : -5;
-}
+int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st) { return fill_ptime(P, st); }
 
 // One replay of a decode batch's classified ops (rows packed per chunk at
 // d_base[c], d_cnt[c] of them; `rows` total).  *same = the departure times it
 // computes equal those the classification used (then it was the sequential
 // decoder's).  Otherwise ptime is updated for the next classification.
-// Returns 0, -95 (a hash this batch entered is gone before a later lookup),
-// -5.
-int xcg_pair_decode_pass(XcgPairState* P, const void* d_rows, const uint64_t* d_base, const uint64_t* d_cnt,
-                         uint32_t n, uint64_t rows, uint64_t decls, int* same, hipStream_t st) {
-  if (P->h_ev_cap < rows + 1) {
-    if (P->h_ev) (void)hipHostFree(P->h_ev);
-    P->h_ev = nullptr;
-    P->h_ev_cap = 0;
-    if (hipHostMalloc(&P->h_ev, 16 * (rows + 1)) != hipSuccess) return -5;
-    P->h_ev_cap = rows + 1;
-  }
-  if (P->h_base_cap < n) {
-    if (P->h_base) (void)hipHostFree(P->h_base);
-    P->h_base = nullptr;
-    P->h_base_cap = 0;
-    if (hipHostMalloc(&P->h_base, 16ull * n) != hipSuccess) return -5;
-    P->h_base_cap = n;
-  }
-  if ((rows && hipMemcpyAsync(P->h_ev, d_rows, 16 * rows, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-      hipMemcpyAsync(P->h_base, d_base, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(P->h_base + n, d_cnt, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return -5;
-  if (!P->replay_decode(n, P->h_ev, P->h_base, P->h_base + n, decls)) return -95;
-  std::vector<uint64_t> lv;
-  for (uint32_t x : P->touchedE)
-    if (P->es[x].leave != NEVER) {
-      lv.push_back(x);
-      lv.push_back(P->es[x].leave);
-    }
-  {
-    std::vector<std::pair<uint64_t, uint64_t>> pr(lv.size() / 2);
-    for (size_t j = 0; j < pr.size(); ++j) pr[j] = {lv[2 * j], lv[2 * j + 1]};
-    std::sort(pr.begin(), pr.end());
-    for (size_t j = 0; j < pr.size(); ++j) {
-      lv[2 * j] = pr[j].first;
-      lv[2 * j + 1] = pr[j].second;
-    }
-  }
-  *same = lv == P->leaves;
-  if (*same) return 0;
-  P->leaves = lv;
-  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
-  const uint32_t m = (uint32_t)(lv.size() / 2);
-  if (m) {
-    if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * m) || ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * m))
-      return -5;
-    memcpy(P->h_xfer, lv.data(), 16ull * m);
-    if (upload(P, 0, 16ull * m, st)) return -5;
-    hipLaunchKernelGGL(pair_scatter64_kernel, dim3(grid_for(m)), dim3(256), 0, st, P->d_ptime,
-                       (const uint64_t*)P->d_xfer, m);
-  }
-  return hipStreamSynchronize(st) == hipSuccess ? 0 : -5;
+// Returns 0, -95 (a batch the pair model declines: a hash this batch named
+// gone before a later lookup, more than a disk lap of writes), -5.
+int xcg_pair_decode_pass(XcgPairState* P, const PairGpu* G, const void* d_rows, const uint64_t* d_base,
+                         const uint64_t* d_cnt, uint32_t n, uint64_t rows, uint32_t maxd, int* same, hipStream_t st) {
+  RowSrc rs{1, n, maxd, (const uint4*)d_rows, nullptr, 0u, d_base, d_cnt, rows, nullptr, nullptr, nullptr};
+  const uint64_t lap = P->D > 2 * DISK_ENTRIES ? P->D - 2 * DISK_ENTRIES : 1;
+  PassOut o;
+  const HashTab g{G->g_keys, G->g_vals, G->g_mask};
+  const int rc = replay(P, rs, g, true, &o, st);
+  if (rc) return rc;
+  if (o.split || o.appends > lap) return -95;
+  *same = !o.changed;
+  return 0;
 }
 
 // Keep the last decode replay and commit it (bytes from the batch input at the
 // declaration rows: G.decl[c * maxd + d].z = the EXTRACT payload's offset).
 int xcg_pair_decode_commit(XcgPairState* P, const PairGpu* G, hipStream_t st) {
-  P->keep();
   const int rc = pair_commit(P, *G, st);
-  if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, G->pool, st);
-  P->leaves.clear();
-  hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+  if (fill_ptime(P, st)) return -5;
   return rc;
 }
 
@@ -1154,7 +1636,7 @@ int xcg_pair_decode_commit(XcgPairState* P, const PairGpu* G, hipStream_t st) {
 int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds_out, hipStream_t st) {
   const uint32_t n = a0->n;
   int rounds = 0;
-  if (pair_sync_pending(P, gpu_of(*a0), st)) return -5;
+  if (pair_sync_front(P, gpu_of(*a0), st)) return -5;
   // A sub-batch is bounded by the disk only: while it writes fewer than a lap
   // of disk blocks, nothing it declared can leave both levels within it (a
   // chunk writes at most maxd declarations plus its touches).
@@ -1164,6 +1646,7 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
   uint32_t i0 = 0;
   using clk = std::chrono::steady_clock;
   auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const HashTab g{a0->g_keys, a0->g_vals, a0->g_mask};
   while (i0 < n) {
     const clk::time_point t0 = clk::now();
     const uint32_t m = per < n - i0 ? per : n - i0;
@@ -1174,31 +1657,45 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     a.out_off += i0;
     a.out_len += i0;
     if (a.stats) a.stats += 4ull * i0;
-    a.ptime = P->d_ptime;
+    a.ptime = P->ptime;
     a.no_commit = 1;
+    RowSrc rs{0, m, a.maxd, (const uint4*)a.ev, a.nev, a.maxe, nullptr, nullptr, 0, a.need, a.bad_t, a.bad_hi};
+    auto clear_flags = [&]() {
+      return hipMemsetAsync(a.need, 0, 4ull * m, st) == hipSuccess &&
+             (!a.bad_t || (hipMemsetAsync(a.bad_t, 0xFF, 4ull * m, st) == hipSuccess &&
+                           hipMemsetAsync(a.bad_hi, 0, 4ull * m, st) == hipSuccess));
+    };
+    uint32_t* scratch_flags = nullptr;
+    if (!a.bad_t) {                                  // (no restart arrays: flags into scratch)
+      if (hipMallocAsync((void**)&scratch_flags, 8ull * m, st) != hipSuccess) return -5;
+      rs.bad_t = scratch_flags;
+      rs.bad_hi = scratch_flags + m;
+    }
+    auto done_scratch = [&]() {
+      if (scratch_flags) (void)hipFreeAsync(scratch_flags, st);
+    };
     // The rounds start from each chunk's tiling (its cold parse).  ptime is
     // NEVER (no cached entry leaves) unless the last sub-batch needed more than
     // one pass: then the first guess is the tiling seed's own references,
     // replayed (a cached tile is a lookup hit, a repeat of an earlier tile a hit
     // on its declaration, every other tile a declaration).
-    if (xcg_launch_seed_tiling(&a, st)) return -5;
+    if (xcg_launch_seed_tiling(&a, st)) { done_scratch(); return -5; }
     const clk::time_point t1 = clk::now();
     if (P->prev_passes > 1) {
-      const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};
-      hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, (uint64_t)b.mask + 1, NOKEY);
-      hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
+      const HashTab b{a.b_keys, a.b_vals, a.b_mask};
+      hipLaunchKernelGGL(pr_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, (uint64_t)b.mask + 1, EMPTY_KEY);
+      hipLaunchKernelGGL(pr_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
       hipLaunchKernelGGL(pair_seed_table_kernel, dim3(grid_for((uint64_t)m * a.maxd)), dim3(256), 0, st, m,
                          (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
       hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
                          (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe);
-      if (download_refs(P, a, st)) return -5;
-      (void)P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
-      if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
-          ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
-        return -5;
+      if (!clear_flags()) { done_scratch(); return -5; }
+      PassOut o;
+      const int rc = replay(P, rs, g, true, &o, st);
+      if (rc) { done_scratch(); return rc; }
     }
     const clk::time_point t2 = clk::now();
-    double t_parse = 0, t_dl = 0, t_replay = 0;
+    double t_parse = 0, t_replay = 0;
     bool done = false, split = false;
     int passes = 0;
     for (int pass = 0; pass < MAX_PASSES && !done && !split; ++pass) {
@@ -1209,54 +1706,42 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
       const clk::time_point q0 = clk::now();
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
-      if (rc) return rc;
+      if (rc) { done_scratch(); return rc; }
       if (pair_debug()) (void)hipStreamSynchronize(st);
       const clk::time_point q1 = clk::now();
-      if (download_refs(P, a, st)) return -5;
+      if (!clear_flags()) { done_scratch(); return -5; }
+      PassOut o;
+      const int prc = replay(P, rs, g, false, &o, st);
+      if (prc == -75) { split = true; break; }
+      if (prc) { done_scratch(); return prc; }
       const clk::time_point q2 = clk::now();
-      const bool ok = P->replay(m, P->h_ev, P->h_nev, a.maxe, a.maxd);
-      const clk::time_point q3 = clk::now();
       t_parse += ms(q0, q1);
-      t_dl += ms(q1, q2);
-      t_replay += ms(q2, q3);
-      uint32_t nbad = 0;
-      for (uint32_t c = 0; c < m; ++c) nbad += P->bad[c];
+      t_replay += ms(q1, q2);
       if (pair_debug())
-        fprintf(stderr, "pair: chunks %u+%u pass %d rounds %d enters %llu refs %llu appends %llu bad %u split %d\n",
-                i0, m, pass, r, (unsigned long long)P->enters, (unsigned long long)P->refs,
-                (unsigned long long)P->appends, nbad, (int)P->split);
-      if (P->split) split = true;
-      else if (ok) done = true;
-      else {
-        for (uint32_t c = 0; c < m; ++c) {
-          P->h_need[c] = P->bad[c];
-          P->h_need[m + c] = P->blo[c];
-          P->h_need[2 * m + c] = P->bhi[c];
-        }
-        if (hipMemcpyAsync(a.need, P->h_need, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess) return -5;
-        if (a.bad_t && (hipMemcpyAsync(a.bad_t, P->h_need + m, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(a.bad_hi, P->h_need + 2 * m, 4ull * m, hipMemcpyHostToDevice, st) != hipSuccess))
-          return -5;
-        if (ensure_pinned(&P->h_xfer, &P->h_xfer_cap, 16ull * (P->touchedE.size() + 1)) ||
-            ensure_dev(&P->d_xfer, &P->xfer_cap, 16ull * (P->touchedE.size() + 1)) || upload_ptime(P, st))
-          return -5;
-      }
+        fprintf(stderr, "pair: chunks %u+%u pass %d rounds %d appends %llu bad %u split %d\n", i0, m, pass, r,
+                (unsigned long long)o.appends, o.nbad, (int)o.split);
+      if (o.split || o.appends > lap) split = true;
+      else if (o.nbad == 0) done = true;
+      // else: the replay flagged the chunks (need / bad_t / bad_hi) and set ptime
     }
     if (!done) {
+      done_scratch();
       if (m == 1) return split ? -95 : -75;
       per = m / 2;                                 // redo this part in halves
       P->prev_passes = MAX_PASSES;
+      if (fill_ptime(P, st)) return -5;
       continue;
     }
     const clk::time_point t3 = clk::now();
-    P->keep();
-    if (pair_commit(P, gpu_of(a), st)) return -5;
+    const PairGpu G = gpu_of(a);
+    if (pair_commit(P, G, st)) { done_scratch(); return -5; }
+    done_scratch();
     if (pair_debug())
-      fprintf(stderr, "pair: ms seed %.2f seed-replay %.2f parse %.2f download %.2f replay %.2f commit %.2f\n",
-              ms(t0, t1), ms(t1, t2), t_parse, t_dl, t_replay, ms(t3, clk::now()));
-    if (getenv("XCG_PAIR_VERIFY")) pair_verify(P, a.pool, st);
+      fprintf(stderr, "pair: ms seed %.2f seed-replay %.2f parse %.2f replay %.2f commit %.2f (primary %u, clock %llu)\n",
+              ms(t0, t1), ms(t1, t2), t_parse, t_replay, ms(t3, clk::now()), P->pcount,
+              (unsigned long long)P->disk->dclock);
     // the next sub-batch starts with every hash visible to its end
-    hipLaunchKernelGGL(pair_fill64_kernel, dim3(1024), dim3(256), 0, st, P->d_ptime, (uint64_t)P->ids(), NEVER);
+    if (fill_ptime(P, st)) return -5;
     P->last_base = i0;
     P->prev_passes = passes;
     i0 += m;
