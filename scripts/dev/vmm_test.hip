@@ -24,9 +24,10 @@ __global__ void check(const uint32_t* p, uint64_t n, uint32_t tag, uint32_t* bad
     if (p[i] != ((uint32_t)i ^ tag)) atomicAdd(bad, 1u);
 }
 
-int main() {
+int main(int argc, char** argv) {
   int dev = 0;
   CK(hipSetDevice(dev));
+  const bool host_part = argc > 1;
   int vmm = 0;
   CK(hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, dev));
   printf("VMM supported attr: %d\n", vmm);
@@ -99,5 +100,44 @@ int main() {
   CK(hipMemRelease(hp2));
   CK(hipMemRelease(hd));
   printf("VMM OK\n");
+  // a host-memory physical allocation mapped into the device VA (a spill tier)
+  if (host_part) {
+    hipMemAllocationProp hp = {};
+    hp.type = hipMemAllocationTypePinned;
+    hp.location.type = hipMemLocationTypeHost;
+    hp.location.id = 0;
+    size_t hg = 0;
+    hipError_t e = hipMemGetAllocationGranularity(&hg, &hp, hipMemAllocationGranularityMinimum);
+    printf("host granularity: %s %zu\n", hipGetErrorString(e), hg);
+    hipMemGenericAllocationHandle_t hh;
+    e = hipMemCreate(&hh, 64 * (hg ? hg : gran), &hp, 0);
+    printf("host hipMemCreate: %s\n", hipGetErrorString(e));
+    if (e == hipSuccess) {
+      void* hv = nullptr;
+      const size_t hs = 64 * (hg ? hg : gran);
+      CK(hipMemAddressReserve(&hv, hs, 0, nullptr, 0));
+      e = hipMemMap(hv, hs, 0, hh, 0);
+      printf("host hipMemMap: %s\n", hipGetErrorString(e));
+      if (e == hipSuccess) {
+        hipMemAccessDesc da = {};
+        da.location.type = hipMemLocationTypeDevice;
+        da.location.id = dev;
+        da.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(hv, hs, &da, 1);
+        printf("host hipMemSetAccess(device): %s\n", hipGetErrorString(e));
+        if (e == hipSuccess) {
+          CK(hipMemset(bad, 0, 4));
+          hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, (uint32_t*)hv, hs / 4, 0x4242u);
+          hipLaunchKernelGGL(check, dim3(256), dim3(256), 0, 0, (const uint32_t*)hv, hs / 4, 0x4242u, bad);
+          CK(hipDeviceSynchronize());
+          CK(hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost));
+          printf("host-backed range via the device: mismatches %u\n", h);
+        }
+        (void)hipMemUnmap(hv, hs);
+      }
+      (void)hipMemAddressFree(hv, hs);
+      (void)hipMemRelease(hh);
+    }
+  }
   return 0;
 }

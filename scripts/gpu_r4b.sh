@@ -11,3 +11,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -2 gpurun_out/pytest.log
 XCG_PAIR_DEBUG=1 timeout -k 10 300 python -u scripts/configs_bench.py c5pair --reps 1 --no-decode > gpurun_out/c5pair.json 2> gpurun_out/c5pair_dbg.err || { echo "c5pair failed"; tail -20 gpurun_out/c5pair_dbg.err; exit 1; }
 head -c 1500 gpurun_out/c5pair.json
+timeout -k 10 60 ./scripts/dev/vmm_test host > gpurun_out/vmm_host.txt 2>&1; echo "vmm host rc=$?" >> gpurun_out/vmm_host.txt; cat gpurun_out/vmm_host.txt
+head -c 1500 gpurun_out/c5pair.json

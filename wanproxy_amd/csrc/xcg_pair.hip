@@ -140,7 +140,9 @@ struct PairDev {
   uint8_t* phit;                          // primary hit (a lookup / GMISS whose entity is resident)
   uint32_t* app;                          // appends at the position [np + 1]
   uint32_t* clk;                          // exclusive prefix of app [np + 1]
-  uint32_t* etch;                         // [newb] touch position of an initial entity (NIL)
+  uint32_t* elast;                        // [etot] position of the entity's last append (NIL)
+  uint8_t* tflag;                         // [np] a touch at the position
+  uint64_t* ddeath;                       // [np] death clock of the entity's disk entry current at the row
   uint32_t* erep;                         // [newb] (decode) position of the REPLACE that ends it (NIL)
   uint32_t* erun;                         // [etot] sorted index of the entity's first element (NIL)
   uint32_t* slow;                         // positions for the block table
@@ -520,48 +522,72 @@ __global__ __launch_bounds__(256) void pr_tab_query_kernel(PairDev d) {
   if (lane_id() == 0) d.phit[j] = cnt < d.C ? 1 : 0;
 }
 
-// One fixed-point round of the disk clock: per initial entity, the first
-// primary hit at which its disk entry is dead (died, or none) is a touch
-// (XCodecDisk::touch re-enters the hash).  One thread per entity run.
+// The disk entry a REPLACE-made entity starts with: the REPLACE row's append
+// (after the replaced entity's touch there, if any).
+__device__ __forceinline__ uint64_t repl_entry(const PairDev& d, uint32_t rp) {
+  return d.dclock0 + d.clk[rp] + d.tflag[rp];
+}
+
+// One fixed-point round of the disk clock.  Per entity run, in stream order:
+// the entity's current disk entry (the initial one, its ENTER's, or its last
+// touch's) and, at every primary hit, a touch if that entry has died by the
+// row's clock (XCodecDisk::touch re-enters the hash; an entry can die and be
+// re-entered more than once when the sub-batch laps a small disk).  Each row
+// also records the death clock of the entry current at it (presence checks).
 __global__ __launch_bounds__(256) void pr_touch_kernel(PairDev d) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.np) return;
   const uint32_t e = d.sk[i];
-  if (e >= d.newb || (i > 0 && d.sk[i - 1] == e)) return;
-  const uint64_t dth = death_of(e0_of(d, e), d.nb);
-  uint32_t tp = NIL;
+  if (e >= d.etot || (i > 0 && d.sk[i - 1] == e)) return;
+  uint64_t cur = e < d.newb ? e0_of(d, e) : NOENT;
+  uint32_t last = NIL;
+  bool first = true;
+  uint32_t chg = 0;
   for (uint32_t q = i; q < d.np && d.sk[q] == e; ++q) {
     const uint32_t pos = d.sv[q];
+    if (pos < d.P) continue;
     const uint8_t kk = d.kind[pos];
-    if (pos >= d.P && (kk == K_LOOKUP || kk == K_REPL) && d.phit[pos] && d.dclock0 + d.clk[pos] >= dth) {
-      tp = pos;
-      break;
+    if (first && e >= d.newb && kk != K_ENTER) {       // a REPLACE-made entity: its first row is a HIT
+      const int32_t rp = d.prv[pos];
+      if (rp >= 0 && d.kind[rp] == K_REPL) cur = repl_entry(d, (uint32_t)rp);
     }
+    first = false;
+    const uint64_t ck = d.dclock0 + d.clk[pos];
+    const uint64_t dth = death_of(cur, d.nb);
+    d.ddeath[pos] = dth;
+    uint8_t t = 0;
+    if ((kk == K_LOOKUP || kk == K_REPL) && d.phit[pos] && ck >= dth) {
+      t = 1;
+      cur = ck;
+      last = pos;
+    } else if (kk == K_ENTER) {
+      cur = ck;
+      last = pos;
+    }
+    if (d.tflag[pos] != t) {
+      d.tflag[pos] = t;
+      ++chg;
+    }
+    d.app[pos] = ((kk == K_ENTER || kk == K_REPL) ? 1u : 0u) + t;
   }
-  const uint32_t old = d.etch[e];
-  if (old == tp) return;
-  if (old != NIL) d.app[old] -= 1u;
-  if (tp != NIL) d.app[tp] += 1u;
-  d.etch[e] = tp;
-  atomicAdd(&d.cnt->changed, 1u);
+  d.elast[e] = last;
+  if (chg) atomicAdd(&d.cnt->changed, chg);
 }
 
-// Presence at every recorded lookup (primary residency or a live disk entry);
-// a lookup the parse recorded the other way flags its chunk (encode).
+// Presence at every recorded lookup: primary residency or a live disk entry.
+// Encode: a lookup the parse recorded the other way flags its chunk; a lookup
+// of an entity the sub-batch made and lost again splits the sub-batch (the
+// parse sees the batch's declarations to its end).  Decode: HITs only.
 __global__ __launch_bounds__(256) void pr_check_kernel(PairDev d) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= d.np || j < d.P) return;
   const uint8_t kk = d.kind[j];
   if (kk != K_LOOKUP && kk != K_GMISS) return;
-  if (d.dec && d.yent[j] != HITMARK) return;        // (decode: only HITs are checked)
+  if (d.dec && d.yent[j] != HITMARK) return;
   const uint32_t x = d.ent[j];
-  if (x >= d.newb) return;                           // (a batch entity: on disk to the sub-batch's end)
-  const uint32_t tp = d.etch[x];
-  const uint32_t rp = d.dec ? d.erep[x] : NIL;
-  const bool disk = (tp != NIL && tp < j) || d.dclock0 + d.clk[j] < death_of(e0_of(d, x), d.nb);
-  const bool present = (d.phit[j] || disk) && !(rp != NIL && rp < j);
-  if (d.dec) {
-    if (!present) atomicOr(&d.cnt->split, 8u);       // a hash this batch named is gone: smaller batches
+  const bool present = d.phit[j] || d.dclock0 + d.clk[j] < d.ddeath[j];
+  if (d.dec || x >= d.newb) {
+    if (!present) atomicOr(&d.cnt->split, 8u);
   } else if (present != (kk == K_LOOKUP)) {
     mark_bad(d, d.tim[j]);
   }
@@ -593,9 +619,23 @@ __device__ __forceinline__ uint32_t evict_pos(const PairDev& d, uint32_t k, uint
   return (i >= 1 && i <= (int64_t)M) ? d.missrow[i - 1] : NIL;
 }
 
+// The position whose append brings the clock to `death` (the entry is dead
+// after it), or NIL when the sub-batch does not get there.
+__device__ __forceinline__ uint32_t death_row(const PairDev& d, uint64_t death) {
+  if (d.dclock0 + d.clk[d.np] < death) return NIL;
+  uint32_t lo = d.P, hi = d.np - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (d.dclock0 + d.clk[mid + 1] >= death) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
 // ptime for the next parse: per id, the batch time from which the hash is in
-// neither level (NEVERT: not within the sub-batch; 0: gone at its start).
-// Decode: also whether anything moved (the classification repeats until not).
+// neither level (NEVERT: not within the sub-batch; 0: gone at its start) = the
+// first position no primary span [reference, its exit) and no disk span
+// [append, death) covers.  Decode: also whether anything moved (the
+// classification repeats until not).
 __global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d, uint32_t M) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= d.newb) return;
@@ -611,53 +651,45 @@ __global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d, uint32_t M) {
   }
   if (entity) {
     const uint64_t e0 = e0_of(d, id);
-    const uint32_t tp = d.etch[id];
-    // the position after which the initial disk entry is dead (P: from the start)
-    uint32_t dr = NIL;
-    if (e0 == NOENT) {
-      dr = d.P;
+    const bool present_at_start = id < d.C || e0 != NOENT;
+    if (!present_at_start) {
+      pt = 0;
     } else {
-      const uint64_t dth = death_of(e0, d.nb);
-      if (d.dclock0 + d.clk[d.np] >= dth) {            // binary search: first q with clock(q + 1) >= death
-        uint32_t lo = d.P, hi = d.np - 1;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (d.dclock0 + d.clk[mid + 1] >= dth) hi = mid; else lo = mid + 1;
+      const uint32_t r0 = d.erun[id];
+      const uint32_t dr0 = e0 == NOENT ? d.P : death_row(d, death_of(e0, d.nb));
+      uint32_t cur = d.P, lv = NIL;
+      for (int guard = 0; guard < (1 << 22); ++guard) {
+        uint32_t to = NIL;
+        bool cov = false;
+        if (e0 != NOENT && (dr0 == NIL || cur < dr0)) { cov = true; to = dr0; }
+        if (!cov && r0 != NIL) {                     // a primary span [reference, its exit)
+          for (uint32_t q = r0; q < d.np && d.sk[q] == id; ++q) {
+            const uint32_t a = d.sv[q];
+            const uint8_t kk = d.kind[a];
+            if (kk == K_GMISS) continue;
+            if (a >= d.P && a > cur) break;          // (references are in order)
+            if (kk == K_REPL) { cov = true; to = NIL; break; }   // (gone at the REPLACE: below)
+            const int32_t nx = d.nxt[a];
+            const uint32_t b = (nx >= 0 && d.phit[nx]) ? (uint32_t)nx : evict_pos(d, a, M);
+            if (b == NIL || b > cur) { cov = true; to = b; break; }
+          }
         }
-        dr = lo;
-      }
-    }
-    // walk the primary spans [a, b) of the entity's references; the first
-    // uncovered position at which the disk entry is dead (and not yet touched
-    // again) is the departure.  A REPLACE row ends the entity outright.
-    uint32_t cur = d.P, leave = NIL;
-    bool in_prim_start = id < d.C;
-    auto gap = [&](uint32_t g0, uint32_t g1) {
-      if (leave != NIL || g0 >= g1) return;
-      const uint32_t k = dr == NIL ? NIL : max(g0, dr);
-      if (k != NIL && k < g1 && (tp == NIL || k < tp)) leave = k;
-    };
-    const uint32_t r0 = d.erun[id];
-    if (r0 != NIL) {
-      for (uint32_t q = r0; q < d.np && d.sk[q] == id && leave == NIL; ++q) {
-        const uint32_t a = d.sv[q];
-        const uint8_t kk = d.kind[a];
-        if (kk == K_GMISS) continue;
-        if (a >= d.P) gap(cur, a);
-        if (kk == K_REPL) {                            // replaced: gone right after its own lookup
-          if (leave == NIL) { leave = a; pt = d.tim[a] + 1; }
-          break;
+        if (!cov && r0 != NIL) {                     // a touch's disk span [touch, death)
+          for (uint32_t q = r0; q < d.np && d.sk[q] == id; ++q) {
+            const uint32_t a = d.sv[q];
+            if (a < d.P || !d.tflag[a]) continue;
+            if (a > cur) break;
+            const uint32_t b = death_row(d, death_of(d.dclock0 + d.clk[a], d.nb));
+            if (b == NIL || b > cur) { cov = true; to = b; break; }
+          }
         }
-        const int32_t nx = d.nxt[a];
-        const uint32_t b = (nx >= 0 && d.phit[nx]) ? (uint32_t)nx : evict_pos(d, a, M);
-        cur = max(cur, b == NIL ? NIL : b);
-        if (b == NIL) break;
+        if (!cov) { lv = cur; break; }
+        if (to == NIL || to >= d.np) break;          // covered to the end
+        cur = to;
       }
-    }
-    if (leave == NIL && cur != NIL) gap(cur, d.np);
-    if (leave != NIL && pt == NEVERT) {
-      const bool present_at_start = in_prim_start || e0 != NOENT;
-      pt = (!present_at_start || leave < d.P) ? 0ull : d.tim[leave];
+      const uint32_t rp = d.dec ? d.erep[id] : NIL;  // replaced: gone right after its own lookup
+      if (rp != NIL && (lv == NIL || lv > rp)) pt = d.tim[rp] + 1;
+      else if (lv != NIL) pt = d.tim[lv];
     }
   }
   if (d.ptime[id] != pt) {
@@ -704,18 +736,20 @@ __device__ __forceinline__ void add_move(const PairDev& d, uint32_t dest, uint32
 
 // The disk entry an entity holds at the end of the sub-batch (NOENT: none).
 __device__ __forceinline__ uint64_t final_disk(const PairDev& d, uint32_t x, uint64_t dend) {
-  if (x >= d.newb) {                                 // its ENTER (or REPLACE) append
+  uint64_t e = NOENT;
+  const uint32_t la = d.elast[x];
+  if (la != NIL) {
+    e = d.dclock0 + d.clk[la];                       // (an ENTER's or a touch's: the row's first append)
+  } else if (x >= d.newb) {                          // a REPLACE-made entity never touched
     const uint32_t i = d.erun[x];
-    // (a REPLACE-made entity's run starts at its first HIT; its append is at the REPLACE row: prv)
-    uint32_t pos = d.sv[i];
-    if (d.kind[pos] != K_ENTER) pos = (uint32_t)d.prv[pos];
-    const uint32_t extra = d.kind[pos] == K_REPL && d.etch[d.ent[pos]] == pos ? 1u : 0u;
-    return d.dclock0 + d.clk[pos] + extra;
+    if (i != NIL) {
+      const int32_t rp = d.prv[d.sv[i]];
+      if (rp >= 0 && d.kind[rp] == K_REPL) e = repl_entry(d, (uint32_t)rp);
+    }
+  } else {
+    e = e0_of(d, x);
   }
-  const uint32_t tp = d.etch[x];
-  if (tp != NIL) return d.dclock0 + d.clk[tp];
-  const uint64_t e0 = e0_of(d, x);
-  return (e0 != NOENT && dend < death_of(e0, d.nb)) ? e0 : NOENT;
+  return (e != NOENT && dend < death_of(e, d.nb)) ? e : NOENT;
 }
 
 // step 3: place every final resident (new LRU order; new slots from the free
@@ -737,7 +771,8 @@ __global__ __launch_bounds__(256) void pr_place_kernel(PairDev d, uint64_t dend)
   if (x == NIL) return;
   if (d.kind[k] == K_REPL && x == d.yent[k]) {
     // new bytes under the replaced name: the append at this row after the touch (if any)
-    fd = d.dclock0 + d.clk[k] + (d.etch[d.ent[k]] == k ? 1u : 0u);
+    fd = repl_entry(d, k);
+    if (dend >= death_of(fd, d.nb)) fd = NOENT;
   } else {
     fd = final_disk(d, x, dend);
   }
@@ -745,47 +780,43 @@ __global__ __launch_bounds__(256) void pr_place_kernel(PairDev d, uint64_t dend)
 }
 
 // step 4: the disk appends: per appending position the entry number, the data
-// block, its key and owner, and a byte move.  A REPLACE row appends the new
-// entity after the replaced one's touch (which XCodecDisk::remove then takes
-// out at once).
-__global__ __launch_bounds__(256) void pr_append_kernel(PairDev d) {
+// block, its key and owner, and a byte move -- for the last write into each
+// block only (a small disk can be lapped within a sub-batch).  A REPLACE row
+// appends the new entity after the replaced one's touch; the replaced entity's
+// current entry leaves the index (XCodecDisk::remove).
+__device__ __forceinline__ void disk_write(const PairDev& d, uint64_t e, uint64_t dend, uint64_t key, uint32_t x,
+                                           bool removed) {
+  if (e + d.D < dend) return;                        // (written over later in this sub-batch)
+  const uint32_t i = (uint32_t)(e % d.D);
+  d.dkey[i] = removed ? NOKEY : key;
+  d.dent[i] = removed ? NOENT : e;
+  d.dxuid[i] = d.xuid;
+  if (!removed) add_move(d, d.C + i, x);
+}
+__global__ __launch_bounds__(256) void pr_append_kernel(PairDev d, uint64_t dend) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= d.np || j < d.P || !d.app[j]) return;
   const uint8_t kk = d.kind[j];
   uint64_t e = d.dclock0 + d.clk[j];
   const uint32_t x = d.ent[j];
-  if (x < d.newb && d.etch[x] == j) {               // a touch of x
-    const uint32_t i = (uint32_t)(e % d.D);
-    if (kk == K_REPL || (d.dec && d.erep[x] != NIL)) {   // removed again by the (later) replace
-      d.dkey[i] = NOKEY;
-      d.dent[i] = NOENT;
-      d.dxuid[i] = d.xuid;
-    } else {
-      d.dkey[i] = d.hsh[j];
-      d.dent[i] = e;
-      d.dxuid[i] = d.xuid;
-      add_move(d, d.C + i, x);
-    }
+  if (d.tflag[j]) {                                  // a touch of x
+    const bool removed = kk == K_REPL || (d.dec && x < d.newb && d.erep[x] != NIL && d.elast[x] == j);
+    disk_write(d, e, dend, d.hsh[j], x, removed);
     ++e;
   }
-  if (kk == K_ENTER || kk == K_REPL) {
-    const uint32_t y = kk == K_REPL ? d.yent[j] : x;
-    const uint32_t i = (uint32_t)(e % d.D);
-    d.dkey[i] = d.hsh[j];
-    d.dent[i] = e;
-    d.dxuid[i] = d.xuid;
-    add_move(d, d.C + i, y);
-  }
+  if (kk == K_ENTER) disk_write(d, e, dend, d.hsh[j], x, false);
+  if (kk == K_REPL) disk_write(d, e, dend, d.hsh[j], d.yent[j], false);
 }
 
-// Decode REPLACE: the replaced entity's disk entry (if live) is removed.
-__global__ __launch_bounds__(256) void pr_remove_kernel(PairDev d) {
+// Decode REPLACE of an entity that appended nothing in this batch: its
+// initial entry leaves the index (unless this batch wrote over that block).
+__global__ __launch_bounds__(256) void pr_remove_kernel(PairDev d, uint64_t dend) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= d.np || d.kind[j] != K_REPL) return;
   const uint32_t x = d.ent[j];
-  if (x >= d.newb || d.etch[x] != NIL) return;       // (touched: the append kernel writes it removed)
+  if (x >= d.newb || d.elast[x] != NIL) return;
   const uint64_t e0 = e0_of(d, x);
-  if (e0 == NOENT) return;
+  if (e0 == NOENT || e0 + d.D < dend) return;
   const uint32_t i = (uint32_t)(e0 % d.D);
   d.dkey[i] = NOKEY;
   d.dent[i] = NOENT;
@@ -977,7 +1008,10 @@ struct XcgPairState {
   uint32_t* r2 = nullptr; uint32_t* missrow = nullptr; uint4* moves = nullptr;
   uint32_t* pbase = nullptr;       // [n + 1]
   uint32_t* pcnt = nullptr;        // [n + 1]
-  uint32_t* etch = nullptr;        // [C + D]
+  uint32_t* elast = nullptr;       // [etot]
+  uint64_t el_cap = 0;
+  uint8_t* tflag = nullptr;        // [np]
+  uint64_t* ddeath = nullptr;      // [np]
   uint32_t* erep = nullptr;        // [C + D]
   uint32_t* erun = nullptr;        // [etot]
   uint32_t* tab = nullptr;         // block table + its segment sums
@@ -1030,8 +1064,9 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
                      (void**)&P->skey, (void**)&P->sval, (void**)&P->sk, (void**)&P->sv, (void**)&P->prv,
                      (void**)&P->nxt, (void**)&P->isr, (void**)&P->rc, (void**)&P->phit, (void**)&P->app,
                      (void**)&P->clk, (void**)&P->slow, (void**)&P->f1, (void**)&P->f2, (void**)&P->r1,
-                     (void**)&P->r2, (void**)&P->missrow, (void**)&P->moves};
-    const size_t sz[] = {4, 4, 1, 8, 8, 4, 4, 4, 4, 4, 4, 4, 4, 1, 4, 4, 4, 4, 4, 4, 4, 4, 32};
+                     (void**)&P->r2, (void**)&P->missrow, (void**)&P->moves, (void**)&P->tflag,
+                     (void**)&P->ddeath};
+    const size_t sz[] = {4, 4, 1, 8, 8, 4, 4, 4, 4, 4, 4, 4, 4, 1, 4, 4, 4, 4, 4, 4, 4, 4, 32, 1, 8};
     for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); ++k) {
       (void)hipFree(*arrs[k]);
       *arrs[k] = nullptr;
@@ -1049,9 +1084,10 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
     if (hipMalloc(&P->pbase, 4 * (n + 1)) != hipSuccess || hipMalloc(&P->pcnt, 4 * (n + 1)) != hipSuccess) return -5;
     P->n_cap = n + 1;
   }
-  uint64_t ec = P->et_cap;
-  if (!grow(&P->erun, &ec, etot)) return -5;
+  uint64_t ec = P->et_cap, lc = P->el_cap;
+  if (!grow(&P->erun, &ec, etot) || !grow(&P->elast, &lc, etot)) return -5;
   P->et_cap = ec;
+  P->el_cap = lc;
   // rocprim temporary storage for the largest sort / scan of this size
   size_t a = 0, b = 0, c = 0;
   (void)rocprim::radix_sort_pairs(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
@@ -1154,7 +1190,7 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
   d.skey = P->skey; d.sval = P->sval; d.sk = P->sk; d.sv = P->sv; d.prv = P->prv; d.nxt = P->nxt;
   d.isr = P->isr; d.rc = P->rc; d.phit = P->phit; d.app = P->app; d.clk = P->clk; d.slow = P->slow;
   d.f1 = P->f1; d.f2 = P->f2; d.r1 = P->r1; d.r2 = P->r2; d.missrow = P->missrow; d.moves = P->moves;
-  d.pbase = P->pbase; d.pcnt = P->pcnt; d.cnt = P->cnt; d.etch = P->etch; d.erep = P->erep; d.erun = P->erun;
+  d.pbase = P->pbase; d.pcnt = P->pcnt; d.cnt = P->cnt; d.elast = P->elast; d.tflag = P->tflag; d.ddeath = P->ddeath; d.erep = P->erep; d.erun = P->erun;
   d.lru2 = P->lru2; d.occ = P->occ; d.freel = P->freel;
   // encode: hash -> ENTER position
   if (!rs.dec) {
@@ -1166,7 +1202,7 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
     hipLaunchKernelGGL(pr_fill64_kernel, dim3(grid_for(want)), dim3(256), 0, st, P->bm_keys, want, EMPTY_KEY);
     hipLaunchKernelGGL(pr_fill64_kernel, dim3(grid_for(want)), dim3(256), 0, st, P->bm_vals, want, ~0ull);
   }
-  hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(newb)), dim3(256), 0, st, P->etch, (uint64_t)newb, NIL);
+  if (hipMemsetAsync(P->tflag, 0, np + 1, st) != hipSuccess) return -5;
   if (rs.dec) hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(newb)), dim3(256), 0, st, P->erep, (uint64_t)newb, NIL);
   hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(etot)), dim3(256), 0, st, P->erun, (uint64_t)etot, NIL);
   if (P->pcount) hipLaunchKernelGGL(pr_pseudo_kernel, dim3(grid_for(P->pcount)), dim3(256), 0, st, d);
@@ -1318,8 +1354,8 @@ int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   if (scan_u32(P, P->ofl, P->ofr, (uint64_t)P->C + 1, st)) return -5;
   hipLaunchKernelGGL(pr_free_kernel, dim3(grid_for(P->C)), dim3(256), 0, st, d, (const uint32_t*)P->ofr);
   hipLaunchKernelGGL(pr_place_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, dend);
-  if (d.dec) hipLaunchKernelGGL(pr_remove_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(pr_append_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (d.dec) hipLaunchKernelGGL(pr_remove_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, dend);
+  hipLaunchKernelGGL(pr_append_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, dend);
   if (hipMemcpyAsync(P->h_small, P->r1 + np, 4, hipMemcpyDeviceToHost, st) != hipSuccess || read_cnt(P, st))
     return -5;
   const uint32_t pc = P->h_small[0], nmove = P->h_cnt->nmove, nstage = P->h_cnt->nstage;
@@ -1448,7 +1484,7 @@ void unmap_pool(XcgPairState* P) {
 void free_scratch(XcgPairState* P) {
   void* arrs[] = {P->ent, P->yent, P->kind, P->tim, P->hsh, P->skey, P->sval, P->sk, P->sv, P->prv, P->nxt,
                   P->isr, P->rc, P->phit, P->app, P->clk, P->slow, P->f1, P->f2, P->r1, P->r2, P->missrow,
-                  P->moves, P->pbase, P->pcnt, P->etch, P->erep, P->erun, P->tab, P->occ, P->freel, P->ofl, P->ofr, P->hk, P->hk2,
+                  P->moves, P->pbase, P->pcnt, P->elast, P->tflag, P->ddeath, P->erep, P->erun, P->tab, P->occ, P->freel, P->ofl, P->ofr, P->hk, P->hk2,
                   P->hv, P->hv2, P->bm_keys, P->bm_vals, P->staging, P->tmp, P->cnt};
   for (void* p : arrs) (void)hipFree(p);
   if (P->h_small) (void)hipHostFree(P->h_small);
@@ -1519,7 +1555,7 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
   const uint64_t ids = (uint64_t)C + P->D;
   if (hipMalloc(&P->pkey, 8ull * C) != hipSuccess || hipMalloc(&P->pdisk, 8ull * C) != hipSuccess ||
       hipMalloc(&P->lru, 4ull * C) != hipSuccess || hipMalloc(&P->lru2, 4ull * C) != hipSuccess ||
-      hipMalloc(&P->ptime, 8 * ids) != hipSuccess || hipMalloc(&P->etch, 4 * ids) != hipSuccess ||
+      hipMalloc(&P->ptime, 8 * ids) != hipSuccess ||
       hipMalloc(&P->erep, 4 * ids) != hipSuccess ||
       hipMemset(P->pkey, 0xFF, 8ull * C) != hipSuccess || hipMemset(P->pdisk, 0xFF, 8ull * C) != hipSuccess ||
       hipMemset(P->ptime, 0xFF, 8 * ids) != hipSuccess || ensure_front_arrays(P) != 0 || map_pool(P, device) != 0) {
@@ -1612,12 +1648,11 @@ int xcg_pair_decode_begin(XcgPairState* P, hipStream_t st) { return fill_ptime(P
 int xcg_pair_decode_pass(XcgPairState* P, const PairGpu* G, const void* d_rows, const uint64_t* d_base,
                          const uint64_t* d_cnt, uint32_t n, uint64_t rows, uint32_t maxd, int* same, hipStream_t st) {
   RowSrc rs{1, n, maxd, (const uint4*)d_rows, nullptr, 0u, d_base, d_cnt, rows, nullptr, nullptr, nullptr};
-  const uint64_t lap = P->D > 2 * DISK_ENTRIES ? P->D - 2 * DISK_ENTRIES : 1;
   PassOut o;
   const HashTab g{G->g_keys, G->g_vals, G->g_mask};
   const int rc = replay(P, rs, g, true, &o, st);
   if (rc) return rc;
-  if (o.split || o.appends > lap) return -95;
+  if (o.split) return -95;
   *same = !o.changed;
   return 0;
 }
@@ -1720,7 +1755,7 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
       if (pair_debug())
         fprintf(stderr, "pair: chunks %u+%u pass %d rounds %d appends %llu bad %u split %d\n", i0, m, pass, r,
                 (unsigned long long)o.appends, o.nbad, (int)o.split);
-      if (o.split || o.appends > lap) split = true;
+      if (o.split) split = true;
       else if (o.nbad == 0) done = true;
       // else: the replay flagged the chunks (need / bad_t / bad_hi) and set ptime
     }
