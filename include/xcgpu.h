@@ -113,7 +113,8 @@ int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_lim
  * a primary hit re-enters a hash the disk index lost.  XCG_SEM_STREAM batches,
  * decode batches and the single-segment host calls are bit-exact with the
  * sequential XCodecEncoder / XCodecDecoder on such a pair; the disk level lives
- * in HBM (its bytes, and the index as a GPU table).  In-band only (XCG_EINVAL
+ * on the device (its index as GPU arrays, its bytes in HBM or, past free HBM,
+ * in pinned host memory: xcg_disk_create_ex).  In-band only (XCG_EINVAL
  * with XCG_FLAG_OOB / XCG_FLAG_NULLCACHE, or a volume without one index
  * block).  XCG_ENOTSUP (never a different result): a decode batch in which a
  * hash it EXTRACTed leaves both levels before a later op names it (decode it
@@ -135,6 +136,18 @@ int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_
  * written, st[2] index blocks, st[3] fronts. */
 typedef struct xcg_disk xcg_disk;
 int xcg_disk_create(uint64_t disk_bytes, xcg_disk **out);
+/* The disk's data blocks are one allocation mapped (HIP virtual memory) behind
+ * the primary of every front on the disk, so N fronts cost one disk.  Where
+ * the blocks live: HBM when the volume fits beside what the device already
+ * holds (4 GiB kept free), otherwise pinned host memory behind the same device
+ * addresses -- a spill level below HBM that the kernels read and write over
+ * PCIe.  XCG_DISK_HOST / XCG_DISK_DEVICE force one tier (DEVICE: fail rather
+ * than spill).  xcg_disk_tier: 0 HBM, 1 host memory, -1 before the first
+ * front (the tier is chosen when the first front binds the disk to a device). */
+#define XCG_DISK_HOST 1u
+#define XCG_DISK_DEVICE 2u
+int xcg_disk_create_ex(uint64_t disk_bytes, uint32_t flags, xcg_disk **out);
+int xcg_disk_tier(const xcg_disk *disk);
 void xcg_disk_destroy(xcg_disk *disk);
 int xcg_disk_stats(const xcg_disk *disk, uint64_t *st);
 int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,

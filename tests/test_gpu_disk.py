@@ -1,0 +1,92 @@
+"""The disk level's storage (XCodecDisk, xcodec/xcodec_cache_disk.{h,cc}):
+one set of data blocks shared by every front on a disk (the reference's one
+volume file), and the spill tier below HBM (the blocks in pinned host memory
+behind the same device addresses).  Output parity is the pair's (the real
+XCodecCachePair over the RefDisk restatement, oracle/ref_driver.cc)."""
+import importlib.util
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_spec = importlib.util.spec_from_file_location('make_pair_golden', os.path.join(HERE, 'golden/make_pair_golden.py'))
+mpg = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(mpg)
+SEG = 2048
+
+
+def _uuid(k):
+    return '%08x-0000-4000-8000-%012x' % (0xD15C, k)
+
+
+@pytest.mark.parametrize('tier', [0, 1])
+def test_shared_disk_tiers_vs_reference(ref_oracle, tier):
+    """Two fronts on one disk encoding in alternation, with the blocks in HBM
+    (tier 0) or spilled to pinned host memory (tier 1): every chunk and every
+    front's disk counters equal the reference's local + connected pair."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, Disk
+    limit, disk = 100 * SEG, mpg.disk_bytes(2)
+    da = synth.stream(0xA12 + tier, 2 << 20, 30, 0)
+    db = synth.stream(0xB23 + tier, 2 << 20, 30, 0)
+    oa, la = synth.chunks_of(da, 65536)
+    ob, lb = synth.chunks_of(db, 65536)
+    pa = ref_oracle.cache_new_pair(limit, disk)
+    pb = ref_oracle.cache_connect(pa, _uuid(tier))
+    exp = []
+    for k in range(0, len(oa), 4):
+        exp.append(ref_oracle.encode_batch(da, oa[k:k + 4], la[k:k + 4], mode=MODE_STREAM, cache=pa))
+        exp.append(ref_oracle.encode_batch(db, ob[k:k + 4], lb[k:k + 4], mode=MODE_STREAM, cache=pb))
+    est = [ref_oracle.pair_stats(pa, disk_live=True), ref_oracle.pair_stats(pb, disk_live=True)]
+    K = Disk(disk, tier=Disk.HOST if tier else Disk.DEVICE)
+    assert K.tier() == -1
+    ca = Context(0, memory_cache_limit=limit, disk=K)
+    cb = Context(0, memory_cache_limit=limit, disk=K)
+    if tier and K.tier() != tier:
+        ca.close()
+        cb.close()
+        K.close()
+        pytest.skip('host-located virtual memory is not available in this HIP runtime (the disk stayed in HBM)')
+    assert K.tier() == tier
+    got = []
+    for k in range(0, len(oa), 4):
+        got.append(ca.encode_chunks(da, oa[k:k + 4], la[k:k + 4], semantics=XCG_SEM_STREAM))
+        got.append(cb.encode_chunks(db, ob[k:k + 4], lb[k:k + 4], semantics=XCG_SEM_STREAM))
+    sa, sb, ks = ca.pair_stats(), cb.pair_stats(), K.stats()
+    ca.close()
+    cb.close()
+    K.close()
+    for k, (a, b) in enumerate(zip(exp, got)):
+        assert a == b, k
+    assert (sa[1], sa[2], ks[0]) == est[0]
+    assert (sb[1], sb[2], ks[0]) == est[1]
+    assert ks[1] > 3 * 2 * 204, 'the shared disk never lapped'
+
+
+def test_fronts_share_one_disk_of_hbm():
+    """wanproxy.conf's 1 GiB disk with three fronts on it (the local cache and
+    two connected peers): the device holds one disk's blocks, not three."""
+    import torch
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, Disk
+    from wanproxy_amd import synth
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(0)
+    K = Disk(1 << 30, tier=Disk.DEVICE)
+    ctxs = [Context(0, memory_cache_limit=128 << 20, disk=K) for _ in range(3)]
+    d = synth.stream(0xD15, 1 << 20, 20, 0)
+    offs, lens = synth.chunks_of(d, 65536)
+    for c in ctxs:                                   # (allocates each front's tables and scratch)
+        c.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(0)
+    used = free0 - free1
+    assert K.tier() == 0
+    for c in ctxs:
+        c.close()
+    K.close()
+    # one disk (1 GiB) + three primaries (128 MiB) + per-front tables and
+    # scratch (~0.2 GiB each); three copies of the disk would be >= 3 GiB
+    assert used < 2.2 * (1 << 30), used

@@ -551,17 +551,22 @@ int xcg_ctx_create_bounded(int device, uint32_t flags, uint64_t memory_cache_lim
   return XCG_OK;
 }
 
-int xcg_disk_create(uint64_t disk_bytes, xcg_disk** out) {
-  if (!out) return XCG_EINVAL;
+int xcg_disk_create(uint64_t disk_bytes, xcg_disk** out) { return xcg_disk_create_ex(disk_bytes, 0, out); }
+
+int xcg_disk_create_ex(uint64_t disk_bytes, uint32_t flags, xcg_disk** out) {
+  if (!out || (flags & ~(XCG_DISK_HOST | XCG_DISK_DEVICE)) || flags == (XCG_DISK_HOST | XCG_DISK_DEVICE))
+    return XCG_EINVAL;
   *out = nullptr;
   XcgDiskState* K = nullptr;
-  const int rc = xcg_disk_state_create(disk_bytes, &K);
+  const int rc = xcg_disk_state_create(disk_bytes, flags, &K);
   if (rc) return rc == -22 ? XCG_EINVAL : XCG_ENOMEM;
   *out = (xcg_disk*)K;
   return XCG_OK;
 }
 
 void xcg_disk_destroy(xcg_disk* d) { xcg_disk_state_release((XcgDiskState*)d); }
+
+int xcg_disk_tier(const xcg_disk* d) { return d ? xcg_disk_state_tier((const XcgDiskState*)d) : XCG_EINVAL; }
 
 int xcg_disk_stats(const xcg_disk* d, uint64_t* st) {
   if (!d || !st) return XCG_EINVAL;

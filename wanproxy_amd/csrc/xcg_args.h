@@ -175,7 +175,8 @@ struct PairGpu {
   uint32_t* nseg;
   int32_t* status;
 };
-extern "C" int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out);
+extern "C" int xcg_disk_state_create(uint64_t disk_bytes, uint32_t flags, XcgDiskState** out);
+extern "C" int xcg_disk_state_tier(const XcgDiskState* K);
 extern "C" void xcg_disk_state_release(XcgDiskState* K);
 extern "C" void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st);
 extern "C" int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out);

@@ -971,6 +971,8 @@ struct XcgDiskState {
   uint64_t* dent = nullptr;
   uint32_t* dxuid = nullptr;
   // the data blocks' bytes: one physical allocation mapped behind every front's primary
+  uint32_t flags = 0;              // XCG_DISK_* (xcgpu.h)
+  int tier = -1;                   // where the blocks live: 0 HBM, 1 pinned host memory (-1: not yet)
   bool vmm = false;
   hipMemGenericAllocationHandle_t pool_h{};
   size_t pool_bytes = 0;
@@ -1430,10 +1432,45 @@ int map_pool(XcgPairState* P, int device) {
     bool ok = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) == hipSuccess &&
               gran > 0;
     if (ok && !K->vmm && K->pool_bytes == 0) {
+      // The disk's blocks: HBM, unless the volume does not fit beside what the
+      // device already holds (keep 4 GiB free) or the caller asks for the host
+      // tier -- then pinned host memory behind the same addresses, which the
+      // kernels read and write over PCIe (a spill level below HBM).
       const size_t sd = round_up((size_t)K->D * SEG + 256, gran);
-      if (hipMemCreate(&K->pool_h, sd, &prop, 0) == hipSuccess) {
+      size_t fr = 0, tot = 0;
+      const bool fits = hipMemGetInfo(&fr, &tot) == hipSuccess && fr > sd + (4ull << 30);
+      const bool want_host = (K->flags & 1u) != 0 || (!(K->flags & 2u) && !fits);
+      if (!want_host && hipMemCreate(&K->pool_h, sd, &prop, 0) == hipSuccess) {
         K->pool_bytes = sd;
         K->vmm = true;
+        K->tier = 0;
+      } else if (!(K->flags & 2u)) {
+        (void)hipGetLastError();
+        hipMemAllocationProp hp{};
+        hp.type = hipMemAllocationTypePinned;
+        hp.location.type = hipMemLocationTypeHost;
+        hp.location.id = 0;
+        size_t hg = 0;
+        const hipError_t e1 = hipMemGetAllocationGranularity(&hg, &hp, hipMemAllocationGranularityMinimum);
+        const hipError_t e2 = e1 == hipSuccess && hg && gran % hg == 0 ? hipMemCreate(&K->pool_h, sd, &hp, 0)
+                                                                        : hipErrorInvalidValue;
+        if (e2 == hipSuccess) {
+          K->pool_bytes = sd;
+          K->vmm = true;
+          K->tier = 1;
+        } else {
+          // (host-located VMM needs a runtime that has it: ROCm 7.2's does, the
+          // 7.0 runtime PyTorch bundles refuses it) -- stay on the device
+          if (pair_debug())
+            fprintf(stderr, "pair: host tier not available (granularity %s %zu, create %s)\n", hipGetErrorString(e1),
+                    hg, hipGetErrorString(e2));
+          (void)hipGetLastError();
+          if (hipMemCreate(&K->pool_h, sd, &prop, 0) == hipSuccess) {
+            K->pool_bytes = sd;
+            K->vmm = true;
+            K->tier = 0;
+          }
+        }
       }
     }
     ok = ok && K->vmm;
@@ -1449,6 +1486,9 @@ int map_pool(XcgPairState* P, int device) {
       acc.flags = hipMemAccessFlagsProtReadWrite;
       ok = hipMemSetAccess(P->va, sp + K->pool_bytes, &acc, 1) == hipSuccess;
     }
+    if (!ok && pair_debug())
+      fprintf(stderr, "pair: pool mapping failed (prim %d reserved %d map %d/%d tier %d): %s\n", (int)prim, (int)reserved,
+              (int)m1, (int)m2, K->tier, hipGetErrorString(hipGetLastError()));
     if (ok) {
       P->pool_vmm = true;
       P->prim_bytes = sp;
@@ -1495,7 +1535,7 @@ void free_scratch(XcgPairState* P) {
 
 extern "C" {
 
-int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out) {
+int xcg_disk_state_create(uint64_t disk_bytes, uint32_t flags, XcgDiskState** out) {
   const uint64_t blocks = disk_bytes / SEG;
   if (blocks <= 18) return -22;
   const uint64_t nb = (blocks - 18) / (1 + DISK_ENTRIES);   // xcodec_cache_disk.cc:110-111
@@ -1503,6 +1543,7 @@ int xcg_disk_state_create(uint64_t disk_bytes, XcgDiskState** out) {
   XcgDiskState* K = new XcgDiskState;
   K->nb = nb;
   K->D = (uint32_t)(nb * DISK_ENTRIES);
+  K->flags = flags;
   *out = K;
   return 0;
 }
@@ -1573,6 +1614,7 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
 }
 
 uint8_t* xcg_pair_state_pool(const XcgPairState* P) { return P->pool; }
+int xcg_disk_state_tier(const XcgDiskState* K) { return K->tier; }
 
 // A front goes away (its XCodecCache is deleted): its entries leave the ring's
 // index (XCodecDisk::disconnect).

@@ -79,6 +79,10 @@ def lib():
     L.xcg_disk_destroy.restype = None
     L.xcg_disk_stats.argtypes = [vp, vp]
     L.xcg_disk_stats.restype = C.c_int
+    L.xcg_disk_create_ex.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.xcg_disk_create_ex.restype = C.c_int
+    L.xcg_disk_tier.argtypes = [vp]
+    L.xcg_disk_tier.restype = C.c_int
     L.xcg_ctx_create_pair_on.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_pair_on.restype = C.c_int
     L.xcg_pair_stats.argtypes = [vp, vp]
@@ -172,10 +176,16 @@ class Disk:
     local cache's front and each peer front XCodecCache::connect makes append
     to one FIFO ring (xcodec/xcodec_cache_disk.h:33-69)."""
 
-    def __init__(self, disk_bytes: int):
+    HOST, DEVICE = 1, 2          # XCG_DISK_HOST / XCG_DISK_DEVICE: force the blocks' tier
+
+    def __init__(self, disk_bytes: int, tier: int = 0):
         h = C.c_void_p()
-        _check(lib().xcg_disk_create(int(disk_bytes), C.byref(h)))
+        _check(lib().xcg_disk_create_ex(int(disk_bytes), int(tier), C.byref(h)))
         self.h = h
+
+    def tier(self) -> int:
+        """Where the data blocks live: 0 HBM, 1 pinned host memory (-1: no front yet)."""
+        return int(lib().xcg_disk_tier(self.h))
 
     def stats(self):
         """(live index entries of every front, entries written, index blocks, fronts)."""
