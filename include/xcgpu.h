@@ -148,6 +148,23 @@ int xcg_disk_create(uint64_t disk_bytes, xcg_disk **out);
 #define XCG_DISK_DEVICE 2u
 int xcg_disk_create_ex(uint64_t disk_bytes, uint32_t flags, xcg_disk **out);
 int xcg_disk_tier(const xcg_disk *disk);
+/* The volume file (XCodecDisk::open, xcodec/xcodec_cache_disk.cc:824-871; its
+ * layout :72-101: 18 registry blocks of 36-byte UUIDs, nb index blocks of a
+ * u64 counter and 204 (u16 xuid, u64 hash) entries, the data blocks).
+ * xcg_disk_open reopens a volume a previous process saved -- the reference's
+ * reload (:107-237): registered fronts, the write head at the lowest counter,
+ * the other index blocks loaded in counter order with the first and last 80
+ * checked against their data -- or starts a fresh one when `path` is absent
+ * or empty.  xcg_disk_save writes the volume as the reference's file stands at
+ * that moment (data blocks written at every enter, an index block when it
+ * fills).  Fronts find their entries again by UUID: xcg_ctx_create_pair_uuid
+ * makes the front of a 36-character UUID string (XCodecDisk::connect: the
+ * registered xuid, else the lowest free one, registered); the local front is
+ * the first one made on a fresh volume (xuid 0). */
+int xcg_disk_open(const char *path, uint64_t disk_bytes, uint32_t flags, xcg_disk **out);
+int xcg_disk_save(xcg_disk *disk, const char *path);
+int xcg_ctx_create_pair_uuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,
+                             const char *uuid36, xcg_ctx **out);
 void xcg_disk_destroy(xcg_disk *disk);
 int xcg_disk_stats(const xcg_disk *disk, uint64_t *st);
 int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,

@@ -127,6 +127,37 @@ class Oracle:
             raise ValueError('disk too small for one index block')
         return c
 
+    def cache_open_pair(self, memory_limit_bytes: int, disk_bytes: int, path: str, local_uuid: str):
+        """wanproxy.conf's pair over the disk volume file at `path`
+        (XCodecDisk::open, xcodec_cache_disk.cc:824-871): reopened when the file
+        holds a volume (the constructor's reload, :107-237), else fresh with
+        local_uuid registered.  Reference build only (the restated RefDisk)."""
+        f = getattr(self.lib, self._pre + 'cache_open_pair')
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_uint64, C.c_uint64, C.c_char_p, C.c_char_p]
+        c = f(memory_limit_bytes, disk_bytes, path.encode(), local_uuid.encode())
+        if not c:
+            raise RuntimeError('could not open the volume')
+        return c
+
+    def cache_pair_front(self, pair, uuid: str, memory_limit_bytes: int):
+        """A fresh pair over `uuid`'s front of the disk under `pair` (a
+        restarted process's connect on a reopened volume)."""
+        f = getattr(self.lib, self._pre + 'cache_pair_front')
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
+        c = f(pair, uuid.encode(), memory_limit_bytes)
+        if not c:
+            raise RuntimeError('connect failed')
+        return c
+
+    def disk_save(self, pair, path: str):
+        """Write the volume under `pair` as the reference's file stands now."""
+        f = getattr(self.lib, self._pre + 'disk_save')
+        f.argtypes = [C.c_void_p, C.c_char_p]
+        if f(pair, path.encode()) != 0:
+            raise RuntimeError('could not write the volume')
+
     def pair_stats(self, c, disk_live=False):
         """(disk index entries, disk entries written) of a pair cache; with
         disk_live, also the index entries of every front on its disk."""

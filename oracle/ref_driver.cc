@@ -17,7 +17,11 @@
 #include <xcodec/xcodec_encoder.h>
 #include <xcodec/xcodec_hash.h>
 
+#include <ctype.h>
+#include <fcntl.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <map>
 #include <vector>
@@ -56,7 +60,8 @@ public:
  * re-hashes (:743-771), touch re-enters a lost hash (:813-823), replace =
  * remove + enter (xcodec_cache_disk.h:130-134); connect(uuid) gives the uuid's
  * front, a new one on the lowest free xuid (XCodecDisk::connect, :640-690).
- * The bytes live in memory, not in a file.
+ * The bytes live in memory; save() / the path constructor write and reload
+ * the reference's volume file (below).
  */
 class RefDisk;
 
@@ -80,6 +85,35 @@ public:
 	RefDisk *disk(void) const { return disk_; }
 };
 
+/*
+ * The volume file (xcodec_cache_disk.cc:72-101): 18 registry blocks of
+ * 36-byte UUID strings (56 per block, 1024 xuids), nb index blocks (a u64
+ * counter, then 204 x (u16 xuid, u64 hash)), nb * 204 data blocks
+ * (data_block_address :305-311).  The reference writes a data block at every
+ * enter and an index block when it fills (:694-741); save() writes what such a
+ * volume holds at that moment.  Reopening restates XCodecDisk::XCodecDisk
+ * (:107-237): the registry gives the fronts, index blocks are scanned in order
+ * up to the first free one (counter 0), the lowest counter is the write head
+ * and is not loaded, the others load in counter order (a later entry of a hash
+ * replaces an earlier one), the first and last 80 are checked against their
+ * data blocks' hashes (index_load_entries :408-478), fronts without entries
+ * leave the registry (registry_collect :496-528).
+ */
+static const unsigned REG_BLOCKS = 18, REG_ENTRIES = 2048 / 36, CHECK_BOUNDARY = 80;
+
+static bool uuid_string_ok(const uint8_t *u)	/* uuid_parse's format: 8-4-4-4-12 hex digits */
+{
+	for (unsigned i = 0; i < 36; i++) {
+		if (i == 8 || i == 13 || i == 18 || i == 23) {
+			if (u[i] != '-')
+				return false;
+		} else if (!isxdigit(u[i])) {
+			return false;
+		}
+	}
+	return true;
+}
+
 class RefDisk {
 	uint64_t nb_, slots_, clock_;
 	std::vector<uint64_t> key_;
@@ -88,6 +122,9 @@ class RefDisk {
 	std::vector<uint8_t> data_;
 	std::map<uint16_t, RefDiskCache *> fronts_;
 	std::map<std::string, uint16_t> uuid_xuid_;
+	std::vector<uint64_t> ctr_;	/* per index block: the counter it was last written with (0: never) */
+	uint64_t ibc_;			/* index_block_counter_: the counter of the block being filled */
+	std::vector<uint8_t> reg_;	/* the registry blocks */
 public:
 	const uint64_t bytes_;
 
@@ -101,17 +138,190 @@ public:
 	  data_(slots_ * XCODEC_SEGMENT_LENGTH),
 	  fronts_(),
 	  uuid_xuid_(),
+	  ctr_(nb_, 0),
+	  ibc_(1),
+	  reg_(REG_BLOCKS * 2048, 0),
 	  bytes_(disk_bytes)
 	{ }
 
-	/* XCodecDisk::local: the front of xuid 0 (registry_load establishes it). */
+	/* XCodecDisk::registry_write (:603-627): reads the xuid's registry block,
+	 * patches the UUID in, and writes the block back to block 0 (sic). */
+	void registry_write(uint16_t xuid, const uint8_t *u36)
+	{
+		uint8_t blk[2048];
+		memcpy(blk, &reg_[(xuid / REG_ENTRIES) * 2048], 2048);
+		memcpy(&blk[(xuid % REG_ENTRIES) * 36], u36, 36);
+		memcpy(&reg_[0], blk, 2048);
+	}
+
+	/* XCodecDisk::local: the front of xuid 0 (registry_load establishes it;
+	 * a reopened volume's local front keeps its registered UUID). */
 	RefDiskCache *local(const UUID& uuid)
 	{
 		if (fronts_.find(0) == fronts_.end()) {
 			fronts_[0] = new RefDiskCache(uuid, this, 0);
 			uuid_xuid_[uuid.string_] = 0;
+			if (uuid.string_.length() == 36)
+				registry_write(0, (const uint8_t *)uuid.string_.data());
 		}
 		return fronts_[0];
+	}
+
+	/* Write the volume as the reference's would stand now. */
+	bool save(const char *path) const
+	{
+		int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0600);
+		if (fd == -1)
+			return false;
+		bool ok = ftruncate(fd, (off_t)bytes_) == 0;
+		ok = ok && pwrite(fd, &reg_[0], reg_.size(), 0) == (ssize_t)reg_.size();
+		std::vector<uint8_t> ib(2048);
+		for (uint64_t b = 0; ok && b < nb_; b++) {
+			memset(&ib[0], 0, ib.size());
+			if (ctr_[b] != 0) {
+				uint8_t *q = &ib[0];
+				memcpy(q, &ctr_[b], 8);
+				q += 8;
+				for (uint64_t j = 0; j < 204; j++, q += 10) {
+					memcpy(q, &xuid_[b * 204 + j], 2);
+					memcpy(q + 2, &key_[b * 204 + j], 8);
+				}
+			}
+			ok = pwrite(fd, &ib[0], 2048, (off_t)((REG_BLOCKS + b) * 2048)) == 2048;
+		}
+		ok = ok && pwrite(fd, &data_[0], data_.size(), (off_t)((REG_BLOCKS + nb_) * 2048)) == (ssize_t)data_.size();
+		close(fd);
+		return ok;
+	}
+
+	/* Reopen a volume (XCodecDisk::XCodecDisk, :107-237). */
+	bool load(const char *path, const UUID& local_uuid)
+	{
+		int fd = ::open(path, O_RDONLY);
+		if (fd == -1)
+			return false;
+		std::vector<uint8_t> vol(bytes_, 0);
+		ssize_t got = pread(fd, &vol[0], vol.size(), 0);
+		close(fd);
+		if (got < 0)
+			return false;
+		memcpy(&reg_[0], &vol[0], reg_.size());
+		/* registry_load (:556-601) */
+		for (uint16_t xuid = 0; xuid < REG_BLOCKS * REG_ENTRIES && xuid < 1024; xuid++) {
+			const uint8_t *u = &reg_[(xuid / REG_ENTRIES) * 2048 + (xuid % REG_ENTRIES) * 36];
+			bool zero = true;
+			for (unsigned i = 0; i < 36; i++)
+				zero &= u[i] == 0;
+			if (zero || !uuid_string_ok(u))
+				continue;
+			UUID uuid;
+			uuid.string_ = std::string((const char *)u, 36);
+			if (uuid_xuid_.find(uuid.string_) != uuid_xuid_.end())
+				continue;
+			fronts_[xuid] = new RefDiskCache(uuid, this, xuid);
+			uuid_xuid_[uuid.string_] = xuid;
+		}
+		if (fronts_.empty())
+			local(local_uuid);
+		/* the index blocks' counters, in block order, to the first free one */
+		std::map<uint64_t, uint64_t> cmap;
+		uint64_t ibc = 0;
+		for (uint64_t o = 0; o < nb_; o++) {
+			uint64_t counter;
+			memcpy(&counter, &vol[(REG_BLOCKS + o) * 2048], 8);
+			if (counter == 0) {
+				cmap[0] = o;
+				break;
+			}
+			if (counter > ibc)
+				ibc = counter + 1;
+			cmap[counter] = o;
+		}
+		uint64_t cib = 0;
+		if (!cmap.empty()) {
+			cib = cmap.begin()->second;
+			cmap.erase(cmap.begin());
+		}
+		for (uint64_t o = 0; o < nb_; o++)
+			memcpy(&ctr_[o], &vol[(REG_BLOCKS + o) * 2048], 8);
+		memcpy(&data_[0], &vol[(REG_BLOCKS + nb_) * 2048], data_.size());
+		for (uint64_t o = 0; o < nb_; o++) {	/* the ring's slots as the file holds them */
+			const uint8_t *q = &vol[(REG_BLOCKS + o) * 2048 + 8];
+			for (uint64_t j = 0; j < 204; j++, q += 10) {
+				memcpy(&xuid_[o * 204 + j], q, 2);
+				memcpy(&key_[o * 204 + j], q + 2, 8);
+				used_[o * 204 + j] = key_[o * 204 + j] != 0;
+			}
+		}
+		unsigned leading = CHECK_BOUNDARY;
+		while (!cmap.empty()) {
+			bool check;
+			if (leading != 0) {
+				check = true;
+				leading--;
+			} else {
+				check = cmap.size() <= CHECK_BOUNDARY;
+			}
+			load_entries(cmap.begin()->second, check, &cib);
+			cmap.erase(cmap.begin());
+		}
+		/* registry_collect (:496-528) */
+		for (std::map<uint16_t, RefDiskCache *>::iterator f = fronts_.begin(); f != fronts_.end();) {
+			if (!f->second->index_.empty() || f->first == 0) {
+				++f;
+				continue;
+			}
+			static const uint8_t zero36[36] = {0};
+			registry_write(f->first, zero36);
+			uuid_xuid_.erase(f->second->get_uuid().string_);
+			delete f->second;
+			fronts_.erase(f++);
+		}
+		ibc_ = ibc == 0 ? 1 : ibc;
+		clock_ = cib * 204;			/* the write head: entry 0 of block cib */
+		return true;
+	}
+
+	/* XCodecDisk::index_load_entries (:408-478) on the file's image. */
+	void load_entries(uint64_t b, bool check, uint64_t *cib)
+	{
+		for (uint64_t j = 0; j < 204; j++) {
+			const uint64_t slot = b * 204 + j;
+			const uint64_t hash = key_[slot];
+			if (hash == 0)
+				continue;
+			std::map<uint16_t, RefDiskCache *>::iterator f = fronts_.find(xuid_[slot]);
+			if (f == fronts_.end())
+				continue;
+			f->second->index_.erase(hash);		/* ("Replacing previous cache entry.") */
+			if (check && XCodecHash::hash(&data_[slot * XCODEC_SEGMENT_LENGTH]) != hash) {
+				if (*cib > b) {			/* rewrite the block with errors */
+					invalidate(b);
+					*cib = b;
+					return;
+				}
+				continue;
+			}
+			f->second->index_[hash] = slot;
+		}
+	}
+
+	/* XCodecDisk::index_invalidate_entries (:327-382) for block b. */
+	void invalidate(uint64_t b)
+	{
+		if (ctr_[b] == 0)
+			return;
+		for (uint64_t i = b * 204; i < (b + 1) * 204; i++) {
+			if (!used_[i])
+				continue;
+			std::map<uint16_t, RefDiskCache *>::iterator f = fronts_.find(xuid_[i]);
+			if (f == fronts_.end())
+				continue;
+			std::map<uint64_t, uint64_t>::iterator it = f->second->index_.find(key_[i]);
+			if (it == f->second->index_.end() || it->second != i)
+				continue;
+			f->second->index_.erase(it);
+		}
 	}
 
 	RefDiskCache *connect(const UUID& uuid)
@@ -128,6 +338,8 @@ public:
 		RefDiskCache *c = new RefDiskCache(uuid, this, xuid);
 		fronts_[xuid] = c;
 		uuid_xuid_[uuid.string_] = xuid;
+		if (uuid.string_.length() == 36)
+			registry_write(xuid, (const uint8_t *)uuid.string_.data());
 		return c;
 	}
 
@@ -141,6 +353,9 @@ public:
 		used_[slot] = 1;
 		c->index_[hash] = slot;
 		if (++clock_ % 204 == 0) {
+			ctr_[(clock_ / 204 - 1) % nb_] = ibc_;	/* the filled index block is written (:708-734) */
+			if (++ibc_ == 0)
+				ibc_ = 1;
 			uint64_t b = (clock_ / 204) % nb_;
 			for (uint64_t i = b * 204; i < (b + 1) * 204; i++) {
 				if (!used_[i])
@@ -323,6 +538,56 @@ void *xcr_cache_connect(void *parent, const char *uuid_string)
 	if (c != NULL && f != pair_fronts().end())
 		pair_fronts()[c] = f->second->disk()->connect(uuid);   /* (the front the pair's connect made) */
 	return c;
+}
+
+/* wanproxy.conf's pair over a disk volume at `path` (XCodecDisk::open,
+ * :824-871): reopened when the file holds one, else fresh; the local front
+ * registers local_uuid on a fresh volume. */
+void *xcr_cache_open_pair(uint64_t memory_limit_bytes, uint64_t disk_bytes, const char *path, const char *local_uuid)
+{
+	UUID uuid;
+	uuid.string_ = local_uuid;
+	XCodecCache *primary = new XCodecMemoryCache(uuid, (size_t)memory_limit_bytes);
+	RefDisk *disk = new RefDisk(disk_bytes);
+	struct stat st;
+	if (::stat(path, &st) == 0 && st.st_size > 0 && !disk->load(path, uuid))
+		return NULL;
+	RefDiskCache *secondary = disk->local(uuid);
+	XCodecCache *pair = new XCodecCachePair(primary, secondary);
+	pair_levels()[pair] = std::make_pair(primary, (XCodecCache *)NULL);
+	pair_fronts()[pair] = secondary;
+	return pair;
+}
+
+/* A new pair (fresh bounded memory cache) over the front of `uuid` on the disk
+ * under `pair` -- what a restarted process's connect(uuid) builds on a
+ * reopened volume; made directly, so this process's registry of caches by
+ * UUID (XCodecCache::connect's first step) does not hand back the pair an
+ * earlier connect made. */
+void *xcr_cache_pair_front(void *pair, const char *uuid_string, uint64_t memory_limit_bytes)
+{
+	std::map<void *, RefDiskCache *>::iterator f = pair_fronts().find(pair);
+	if (f == pair_fronts().end())
+		return NULL;
+	UUID uuid;
+	uuid.string_ = uuid_string;
+	RefDiskCache *front = f->second->disk()->connect(uuid);
+	if (front == NULL)
+		return NULL;
+	XCodecCache *primary = new XCodecMemoryCache(uuid, (size_t)memory_limit_bytes);
+	XCodecCache *c = new XCodecCachePair(primary, front);
+	pair_levels()[c] = std::make_pair(primary, (XCodecCache *)NULL);
+	pair_fronts()[c] = front;
+	return c;
+}
+
+/* Write the volume under a pair (the reference's file at this moment). */
+int xcr_disk_save(void *pair, const char *path)
+{
+	std::map<void *, RefDiskCache *>::iterator f = pair_fronts().find(pair);
+	if (f == pair_fronts().end())
+		return -1;
+	return f->second->disk()->save(path) ? 0 : -1;
 }
 
 void xcr_cache_free(void *c)

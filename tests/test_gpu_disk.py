@@ -90,3 +90,77 @@ def test_fronts_share_one_disk_of_hbm():
     # one disk (1 GiB) + three primaries (128 MiB) + per-front tables and
     # scratch (~0.2 GiB each); three copies of the disk would be >= 3 GiB
     assert used < 2.2 * (1 << 30), used
+
+
+def _vol_case(rng_seed, parts, chunk=65536, size=3 << 20):
+    from wanproxy_amd import synth
+    d = synth.stream(rng_seed, size * parts, 25, 0)
+    offs, lens = synth.chunks_of(d, chunk)
+    k = len(offs) // parts
+    return d, [(offs[i * k:(i + 1) * k], lens[i * k:(i + 1) * k]) for i in range(parts)]
+
+
+@pytest.mark.parametrize('nb', [3, 12])
+def test_volume_reopen_vs_reference(ref_oracle, tmp_path, nb):
+    """A process encodes on wanproxy.conf's pair over a volume file, saves it,
+    a second process reopens it (a fresh memory cache over the reloaded disk:
+    XCodecDisk::XCodecDisk, xcodec_cache_disk.cc:107-237) and encodes on; a
+    connected peer's front finds its entries again by UUID.  Every chunk equals
+    the reference's pair over the restated disk saved and reopened the same way
+    (oracle/ref_driver.cc RefDisk::save / load); the reopened encoder REFs
+    segments only the first process declared."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, Disk
+    limit, disk = 40 * SEG, mpg.disk_bytes(nb)
+    local, peer = _uuid(0x100 + nb), _uuid(0x200 + nb)
+    d, parts = _vol_case(0x7E1 + nb, 3)
+    e, eparts = _vol_case(0x8E1 + nb, 2)
+    # the reference: run 1 (local + peer), save, run 2 on the reopened volume
+    vref = str(tmp_path / 'ref.vol')
+    pa = ref_oracle.cache_open_pair(limit, disk, vref, local)
+    pb = ref_oracle.cache_pair_front(pa, peer, limit)
+    # run 1: the peer, then the local cache (whose entries are then the newest)
+    exp1 = [ref_oracle.encode_batch(e, o, l, mode=MODE_STREAM, cache=pb) for o, l in eparts[:1]]
+    exp1 += [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa) for o, l in parts[:2]]
+    ref_oracle.disk_save(pa, vref)
+    pa2 = ref_oracle.cache_open_pair(limit, disk, vref, _uuid(0x999))
+    pb2 = ref_oracle.cache_pair_front(pa2, peer, limit)
+    # run 2: the local cache sends the last part again, then the peer goes on
+    exp2 = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa2) for o, l in parts[1:2]]
+    exp2 += [ref_oracle.encode_batch(e, o, l, mode=MODE_STREAM, cache=pb2) for o, l in eparts[1:]]
+    # the engine, the same calls
+    vgpu = str(tmp_path / 'gpu.vol')
+    K = Disk(disk, path=vgpu)
+    ca = Context(0, memory_cache_limit=limit, disk=K, uuid=local)
+    cb = Context(0, memory_cache_limit=limit, disk=K, uuid=peer)
+    got1 = [cb.encode_chunks(e, o, l, semantics=XCG_SEM_STREAM) for o, l in eparts[:1]]
+    got1 += [ca.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts[:2]]
+    K.save(vgpu)
+    vgpu_saved = str(tmp_path / 'gpu_saved.vol')
+    K.save(vgpu_saved)
+    ca.close()
+    cb.close()
+    K.close()
+    K2 = Disk(disk, path=vgpu)
+    ca2 = Context(0, memory_cache_limit=limit, disk=K2, uuid=local)
+    cb2 = Context(0, memory_cache_limit=limit, disk=K2, uuid=peer)
+    got2 = [ca2.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts[1:2]]
+    got2 += [cb2.encode_chunks(e, o, l, semantics=XCG_SEM_STREAM) for o, l in eparts[1:]]
+    st = (ca2.pair_stats(), cb2.pair_stats())
+    ca2.close()
+    cb2.close()
+    K2.close()
+    assert got1 == exp1
+    # the engine's saved volume is the reference's file, byte for byte
+    # (registry, index blocks with their counters and entries, data blocks)
+    a, b = open(vref, 'rb').read(), open(vgpu_saved, 'rb').read()
+    if a != b:
+        k = next(i for i in range(min(len(a), len(b))) if a[i] != b[i]) if len(a) == len(b) else -1
+        pytest.fail(f'saved volumes differ: sizes {len(a)} {len(b)}, first differing byte {k} (block {k // 2048})')
+    assert got2 == exp2
+    # the reopened volume made a difference: without it the same calls declare more
+    pf = ref_oracle.cache_new_pair(limit, disk)
+    fresh = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pf) for o, l in parts[1:2]]
+    assert sum(map(len, sum(exp2[:1], []))) < sum(map(len, sum(fresh, [])))
+    # and each front's index holds what the reference's holds
+    assert (st[0][1], st[1][1]) == (ref_oracle.pair_stats(pa2)[0], ref_oracle.pair_stats(pb2)[0])

@@ -168,3 +168,38 @@ def test_name_reuse_port_vs_reference():
         pytest.xfail('reference crashed (signal %d): its replace/window use-after-free' % -p.returncode)
     assert p.returncode == 0, p.stderr[-2000:]
     assert json.loads(p.stdout.strip().splitlines()[-1]) == exp
+
+
+def test_ref_volume_save_reopen(ref_oracle, tmp_path):
+    """The restated disk's volume file (oracle/ref_driver.cc RefDisk::save /
+    load, restating xcodec_cache_disk.cc:72-101 and :107-237): a reopened
+    volume indexes exactly the entries of its written index blocks other than
+    the write head's (the last entry of a hash wins), and saving it again
+    without new writes gives the same file."""
+    import struct
+    from wanproxy_amd import synth
+    spec = importlib.util.spec_from_file_location('make_pair_golden', os.path.join(HERE, 'golden/make_pair_golden.py'))
+    mpg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mpg)
+    nb, limit = 5, 30 * 2048
+    disk = mpg.disk_bytes(nb)
+    local = '0000aaaa-0000-4000-8000-000000000001'
+    d = synth.stream(0xF11E, 3 << 20, 25, 0)
+    offs, lens = synth.chunks_of(d, 65536)
+    v1, v2 = str(tmp_path / 'a.vol'), str(tmp_path / 'b.vol')
+    pa = ref_oracle.cache_open_pair(limit, disk, v1, local)
+    ref_oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=pa)
+    ref_oracle.disk_save(pa, v1)
+    vol = open(v1, 'rb').read()
+    ctr = [struct.unpack_from('<Q', vol, (18 + b) * 2048)[0] for b in range(nb)]
+    head = min(range(nb), key=lambda b: ctr[b]) if 0 not in ctr else ctr.index(0)
+    want = {}
+    for b in sorted((b for b in range(nb) if ctr[b] and b != head), key=lambda b: ctr[b]):
+        for j in range(204):
+            x, h = struct.unpack_from('<HQ', vol, (18 + b) * 2048 + 8 + 10 * j)
+            if h and x == 0:
+                want[h] = b * 204 + j
+    pb = ref_oracle.cache_open_pair(limit, disk, v1, '0000aaaa-0000-4000-8000-0000000000ff')
+    assert ref_oracle.pair_stats(pb)[0] == len(want) > 0
+    ref_oracle.disk_save(pb, v2)
+    assert open(v2, 'rb').read() == vol

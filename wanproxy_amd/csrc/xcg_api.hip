@@ -566,6 +566,23 @@ int xcg_disk_create_ex(uint64_t disk_bytes, uint32_t flags, xcg_disk** out) {
 
 void xcg_disk_destroy(xcg_disk* d) { xcg_disk_state_release((XcgDiskState*)d); }
 
+int xcg_disk_open(const char* path, uint64_t disk_bytes, uint32_t flags, xcg_disk** out) {
+  if (!out || !path || (flags & ~(XCG_DISK_HOST | XCG_DISK_DEVICE)) || flags == (XCG_DISK_HOST | XCG_DISK_DEVICE))
+    return XCG_EINVAL;
+  *out = nullptr;
+  XcgDiskState* K = nullptr;
+  const int rc = xcg_disk_state_open(path, disk_bytes, flags, &K);
+  if (rc) return rc == -22 ? XCG_EINVAL : (rc == -2 ? XCG_ENOENT : XCG_ENOMEM);
+  *out = (xcg_disk*)K;
+  return XCG_OK;
+}
+
+int xcg_disk_save(xcg_disk* d, const char* path) {
+  if (!d || !path) return XCG_EINVAL;
+  const int rc = xcg_disk_state_save((XcgDiskState*)d, path);
+  return rc == 0 ? XCG_OK : (rc == -2 ? XCG_ENOENT : XCG_EHIP);
+}
+
 int xcg_disk_tier(const xcg_disk* d) { return d ? xcg_disk_state_tier((const XcgDiskState*)d) : XCG_EINVAL; }
 
 int xcg_disk_stats(const xcg_disk* d, uint64_t* st) {
@@ -576,6 +593,11 @@ int xcg_disk_stats(const xcg_disk* d, uint64_t* st) {
 
 int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk* disk,
                            xcg_ctx** out) {
+  return xcg_ctx_create_pair_uuid(device, flags, memory_cache_limit_bytes, disk, nullptr, out);
+}
+
+int xcg_ctx_create_pair_uuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk* disk,
+                             const char* uuid36, xcg_ctx** out) {
   if (!out || !disk || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)))
     return XCG_EINVAL;
   *out = nullptr;
@@ -587,7 +609,7 @@ int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_lim
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
     DeviceGuard g(device);
-    const int prc = xcg_pair_state_create((uint32_t)C, (XcgDiskState*)disk, &P);
+    const int prc = xcg_pair_state_create((uint32_t)C, (XcgDiskState*)disk, uuid36, &P);
     if (prc == -22) return XCG_EINVAL;
     if (prc) return XCG_ENOMEM;
   }

@@ -70,8 +70,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <ctype.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
+#include <map>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "xcg_cache.h"
@@ -788,7 +796,7 @@ __device__ __forceinline__ void disk_write(const PairDev& d, uint64_t e, uint64_
                                            bool removed) {
   if (e + d.D < dend) return;                        // (written over later in this sub-batch)
   const uint32_t i = (uint32_t)(e % d.D);
-  d.dkey[i] = removed ? NOKEY : key;
+  d.dkey[i] = key;                                   // (the volume's index entry, even when removed)
   d.dent[i] = removed ? NOENT : e;
   d.dxuid[i] = d.xuid;
   if (!removed) add_move(d, d.C + i, x);
@@ -818,8 +826,7 @@ __global__ __launch_bounds__(256) void pr_remove_kernel(PairDev d, uint64_t dend
   const uint64_t e0 = e0_of(d, x);
   if (e0 == NOENT || e0 + d.D < dend) return;
   const uint32_t i = (uint32_t)(e0 % d.D);
-  d.dkey[i] = NOKEY;
-  d.dent[i] = NOENT;
+  d.dent[i] = NOENT;                                 // (XCodecDisk::remove leaves the volume's index block as it is)
 }
 
 // Commit moves: w = (destination pool index, kind, a, b); kind 0: the bytes of
@@ -944,13 +951,14 @@ __global__ __launch_bounds__(256) void pair_count_live_kernel(const uint64_t* de
   if (lane_id() == 0 && m) atomicAdd(out, (uint32_t)__builtin_popcountll(m));
 }
 
-// A front goes away or is cleared: its disk entries leave the index.
+// A front goes away or is cleared: its disk entries leave the index (the
+// volume's index blocks keep them unless the whole volume is reset).
 __global__ __launch_bounds__(256) void pair_drop_front_kernel(uint64_t* dkey, uint64_t* dent, const uint32_t* dxuid,
                                                               uint32_t D, uint32_t xuid) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < D && (xuid == NIL || dxuid[i] == xuid)) {
     dent[i] = NOENT;
-    dkey[i] = NOKEY;
+    if (xuid == NIL) dkey[i] = NOKEY;
   }
 }
 
@@ -977,6 +985,21 @@ struct XcgDiskState {
   hipMemGenericAllocationHandle_t pool_h{};
   size_t pool_bytes = 0;
   std::vector<XcgPairState*> fronts;   // by xuid (nullptr: free)
+  // the volume (xcodec_cache_disk.cc:72-101): its size, per index block the
+  // counter it was last written with, the counter of the block being filled,
+  // the registry's blocks and the UUID each xuid has there
+  uint64_t bytes = 0;
+  std::vector<uint64_t> ctr;
+  uint64_t ibc = 1;
+  std::vector<uint8_t> reg;
+  std::vector<std::string> uuid;
+  // a reopened volume's ring, waiting for the first front's device
+  bool pending = false;
+  bool ring_loaded = false;
+  bool zeroed = false;             // a fresh volume's blocks read as zeros (as the reference's ftruncate'd file)
+  std::vector<uint64_t> h_key, h_ent;
+  std::vector<uint32_t> h_xuid;
+  std::vector<uint8_t> h_data;
   int refs = 1;                    // the creator's reference + one per front
 };
 
@@ -1374,6 +1397,12 @@ int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   }
   std::swap(P->lru, P->lru2);
   P->pcount = pc;
+  // index blocks filled by this commit are written with the running counter
+  // (XCodecDisk::enter, xcodec_cache_disk.cc:708-738; 0 means unused)
+  for (uint64_t m = K->dclock / DISK_ENTRIES + 1; m <= dend / DISK_ENTRIES; ++m) {
+    K->ctr[(m - 1) % K->nb] = K->ibc;
+    if (++K->ibc == 0) K->ibc = 1;
+  }
   K->dclock = dend;
   P->appends = P->last_appends;
   pair_rebuild(P, G, st);
@@ -1531,6 +1560,159 @@ void free_scratch(XcgPairState* P) {
   if (P->h_cnt) (void)hipHostFree(P->h_cnt);
 }
 
+// XCodecHash::hash of one segment (xcodec/xcodec_hash.h:166-174), host side:
+// the reload's check of an index entry against its data block.
+uint64_t host_hash(const uint8_t* w) {
+  uint32_t s1 = 0, s2 = 0, b1 = 0, b2 = 0;
+  for (int k = 0; k < SEG; ++k) {
+    s1 += (uint32_t)w[k] + 1u;
+    s2 += s1;
+    b1 += w[k] ? (uint32_t)__builtin_ctz(w[k]) + 1u : 0u;
+    b2 += b1;
+  }
+  const uint32_t bits = (b1 << 16) + b2, bytes = (s1 << 20) + s2;
+  return ((uint64_t)bits << 36) + (uint64_t)bytes;
+}
+
+constexpr uint32_t REG_BLOCKS = 18, REG_ENTRIES = 2048 / 36, CHECK_BOUNDARY = 80, XUIDS = 1024;
+
+// XCodecDisk::registry_write (xcodec_cache_disk.cc:603-627): the xuid's
+// registry block with the UUID patched in, written back to block 0 (as the
+// reference does).
+void registry_write(XcgDiskState* K, uint32_t xuid, const char* u36) {
+  uint8_t blk[2048];
+  memcpy(blk, &K->reg[(xuid / REG_ENTRIES) * 2048], 2048);
+  memcpy(&blk[(xuid % REG_ENTRIES) * 36], u36, 36);
+  memcpy(&K->reg[0], blk, 2048);
+}
+
+// uuid_parse's format (common/uuid/uuid_libuuid.cc UUID::decode): 8-4-4-4-12 hex.
+bool uuid_ok(const uint8_t* u) {
+  for (int i = 0; i < 36; ++i) {
+    if (i == 8 || i == 13 || i == 18 || i == 23) {
+      if (u[i] != '-') return false;
+    } else if (!isxdigit(u[i])) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// A reopened volume (XCodecDisk::XCodecDisk, xcodec_cache_disk.cc:107-237):
+// the registry gives the fronts; index blocks are scanned in block order up
+// to the first free one (counter 0); the lowest counter is the write head and
+// is not loaded; the rest load in counter order, a later entry of a hash
+// replacing an earlier one, the first and last 80 checked against their data
+// blocks (index_load_entries :408-478); fronts left without entries leave the
+// registry (registry_collect :496-528).  In the engine's clock model the write
+// head's entry 0 is clock 204 * (nb + head), and a block b loaded from the last
+// lap holds entries numbered from 204 * (nb + head - ((head - b) mod nb)): each
+// dies when the head reaches b again, as the reference invalidates it.
+int load_volume(XcgDiskState* K, const std::vector<uint8_t>& vol) {
+  const uint64_t nb = K->nb, D = K->D;
+  memcpy(&K->reg[0], &vol[0], K->reg.size());
+  std::unordered_map<std::string, uint32_t> seen;
+  for (uint32_t x = 0; x < REG_BLOCKS * REG_ENTRIES && x < XUIDS; ++x) {
+    const uint8_t* u = &K->reg[(x / REG_ENTRIES) * 2048 + (x % REG_ENTRIES) * 36];
+    bool zero = true;
+    for (int i = 0; i < 36; ++i) zero &= u[i] == 0;
+    if (zero || !uuid_ok(u)) continue;
+    const std::string us((const char*)u, 36);
+    if (seen.count(us)) continue;
+    seen[us] = x;
+    K->uuid[x] = us;
+  }
+  std::map<uint64_t, uint64_t> cmap;
+  uint64_t ibc = 0;
+  for (uint64_t o = 0; o < nb; ++o) {
+    uint64_t counter;
+    memcpy(&counter, &vol[(REG_BLOCKS + o) * 2048], 8);
+    if (counter == 0) {
+      cmap[0] = o;
+      break;
+    }
+    if (counter > ibc) ibc = counter + 1;
+    cmap[counter] = o;
+  }
+  uint64_t cib = 0;
+  if (!cmap.empty()) {
+    cib = cmap.begin()->second;
+    cmap.erase(cmap.begin());
+  }
+  K->h_key.assign(D, NOKEY);
+  K->h_ent.assign(D, NOENT);
+  K->h_xuid.assign(D, 0xFFFFFFFFu);
+  K->h_data.assign((size_t)D * SEG, 0);
+  memcpy(&K->h_data[0], &vol[(REG_BLOCKS + nb) * 2048], (size_t)D * SEG);
+  for (uint64_t o = 0; o < nb; ++o) {
+    memcpy(&K->ctr[o], &vol[(REG_BLOCKS + o) * 2048], 8);
+    const uint8_t* q = &vol[(REG_BLOCKS + o) * 2048 + 8];
+    for (uint64_t j = 0; j < DISK_ENTRIES; ++j, q += 10) {
+      uint16_t xu;
+      uint64_t h;
+      memcpy(&xu, q, 2);
+      memcpy(&h, q + 2, 8);
+      if (h == 0) continue;
+      K->h_key[o * DISK_ENTRIES + j] = h;
+      K->h_xuid[o * DISK_ENTRIES + j] = xu;
+    }
+  }
+  std::vector<std::unordered_map<uint64_t, uint64_t>> index(XUIDS);   // per xuid: hash -> slot
+  auto invalidate = [&](uint64_t b) {
+    if (K->ctr[b] == 0) return;
+    for (uint64_t i = b * DISK_ENTRIES; i < (b + 1) * DISK_ENTRIES; ++i) {
+      const uint32_t xu = K->h_xuid[i];
+      if (K->h_key[i] == NOKEY || xu >= XUIDS || K->uuid[xu].empty()) continue;
+      auto it = index[xu].find(K->h_key[i]);
+      if (it != index[xu].end() && it->second == i) index[xu].erase(it);
+    }
+  };
+  unsigned leading = CHECK_BOUNDARY;
+  while (!cmap.empty()) {
+    bool check;
+    if (leading != 0) {
+      check = true;
+      --leading;
+    } else {
+      check = cmap.size() <= CHECK_BOUNDARY;
+    }
+    const uint64_t b = cmap.begin()->second;
+    cmap.erase(cmap.begin());
+    for (uint64_t j = 0; j < DISK_ENTRIES; ++j) {
+      const uint64_t slot = b * DISK_ENTRIES + j;
+      const uint64_t h = K->h_key[slot];
+      const uint32_t xu = K->h_xuid[slot];
+      if (h == NOKEY || xu >= XUIDS || K->uuid[xu].empty()) continue;
+      index[xu].erase(h);                                   // ("Replacing previous cache entry.")
+      if (check && host_hash(&K->h_data[slot * SEG]) != h) {
+        if (cib > b) {                                      // rewrite the block with errors
+          invalidate(b);
+          cib = b;
+          break;
+        }
+        continue;
+      }
+      index[xu][h] = slot;
+    }
+  }
+  for (uint32_t x = 1; x < XUIDS; ++x) {                    // registry_collect
+    if (K->uuid[x].empty() || !index[x].empty()) continue;
+    static const char zero36[36] = {0};
+    registry_write(K, x, zero36);
+    K->uuid[x].clear();
+  }
+  for (uint32_t x = 0; x < XUIDS; ++x)
+    for (const auto& kv : index[x]) {
+      const uint64_t slot = kv.second, b = slot / DISK_ENTRIES;
+      const uint64_t bn = nb + cib - ((cib + nb - b) % nb);
+      K->h_ent[slot] = DISK_ENTRIES * bn + slot % DISK_ENTRIES;
+    }
+  K->ibc = ibc == 0 ? 1 : ibc;
+  K->dclock = DISK_ENTRIES * (nb + cib);
+  K->pending = true;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1544,6 +1726,10 @@ int xcg_disk_state_create(uint64_t disk_bytes, uint32_t flags, XcgDiskState** ou
   K->nb = nb;
   K->D = (uint32_t)(nb * DISK_ENTRIES);
   K->flags = flags;
+  K->bytes = disk_bytes;
+  K->ctr.assign(nb, 0);
+  K->reg.assign(18 * 2048, 0);
+  K->uuid.assign(1024, std::string());
   *out = K;
   return 0;
 }
@@ -1577,15 +1763,30 @@ void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
 // A pair front on disk K (XCodecDisk::local for the first, ::connect for the
 // others: the lowest free xuid, xcodec_cache_disk.cc:640-690), on the current
 // device.
-int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
+int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, XcgPairState** out) {
   if (C == 0 || !K || (uint64_t)K->D + C >= (1ull << 30)) return -22;
+  if (uuid36 && (strlen(uuid36) != 36 || !uuid_ok((const uint8_t*)uuid36))) return -22;
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return -5;
   const int brc = disk_bind(K, device);
   if (brc) return brc;
-  uint32_t xuid = 0;
-  while (xuid < K->fronts.size() && K->fronts[xuid]) ++xuid;
-  if (xuid >= 1024) return -22;                             // XCDFS_XUID_COUNT
+  // XCodecDisk::connect (:640-690): a registered uuid's xuid, else the lowest
+  // xuid nothing holds (no registry entry, no front)
+  auto bound = [&](uint32_t x) { return x < K->fronts.size() && K->fronts[x] != nullptr; };
+  uint32_t xuid = XUIDS;
+  if (uuid36)
+    for (uint32_t x = 0; x < XUIDS; ++x)
+      if (K->uuid[x] == uuid36) { xuid = x; break; }
+  if (xuid < XUIDS && bound(xuid)) return -22;               // (one engine front per disk front)
+  const bool registered = xuid < XUIDS;
+  if (!registered)
+    for (xuid = 0; xuid < XUIDS && (bound(xuid) || !K->uuid[xuid].empty()); ++xuid) {
+    }
+  if (xuid >= XUIDS) return -22;                            // XCDFS_XUID_COUNT
+  if (uuid36 && !registered) {
+    K->uuid[xuid] = uuid36;
+    registry_write(K, xuid, uuid36);
+  }
   XcgPairState* P = new XcgPairState;
   P->C = C;
   P->nb = (uint32_t)K->nb;
@@ -1606,10 +1807,117 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, XcgPairState** out) {
     delete P;
     return -12;
   }
+  if (!K->pending && !K->zeroed) {
+    if (hipMemset(P->pool + (uint64_t)C * SEG, 0, (uint64_t)K->D * SEG) != hipSuccess) return -5;
+    K->zeroed = K->vmm;
+  }
+  if (K->pending) {                                         // a reopened volume's ring and blocks
+    const uint64_t D = K->D;
+    if (!K->ring_loaded &&
+        (hipMemcpy(K->dkey, K->h_key.data(), 8 * D, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(K->dent, K->h_ent.data(), 8 * D, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(K->dxuid, K->h_xuid.data(), 4 * D, hipMemcpyHostToDevice) != hipSuccess))
+      return -5;
+    K->ring_loaded = true;
+    if (hipMemcpy(P->pool + (uint64_t)C * SEG, K->h_data.data(), D * SEG, hipMemcpyHostToDevice) != hipSuccess)
+      return -5;
+    if (K->vmm) {                                            // (one copy serves every front)
+      K->pending = false;
+      K->zeroed = true;                                      // (the blocks hold the volume's bytes)
+      std::vector<uint64_t>().swap(K->h_key);
+      std::vector<uint64_t>().swap(K->h_ent);
+      std::vector<uint32_t>().swap(K->h_xuid);
+      std::vector<uint8_t>().swap(K->h_data);
+    }
+  }
+  P->gstale = true;                                          // (G from the disk's entries at the first call)
   if (xuid >= K->fronts.size()) K->fronts.resize(xuid + 1, nullptr);
   K->fronts[xuid] = P;
   ++K->refs;
   *out = P;
+  return 0;
+}
+
+// Write the volume as the reference's file stands now (registry, every
+// written index block with its counter and entries, the data blocks).
+int xcg_disk_state_save(XcgDiskState* K, const char* path) {
+  const uint64_t nb = K->nb, D = K->D;
+  std::vector<uint64_t> key(D, NOKEY);
+  std::vector<uint32_t> xu(D, 0xFFFFFFFFu);
+  std::vector<uint8_t> data((size_t)D * SEG, 0);
+  if (K->pending && !K->ring_loaded) {
+    key = K->h_key;
+    xu = K->h_xuid;
+    data = K->h_data;
+  } else if (K->device >= 0) {
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(key.data(), K->dkey, 8 * D, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(xu.data(), K->dxuid, 4 * D, hipMemcpyDeviceToHost) != hipSuccess)
+      return -5;
+    // the blocks' bytes: one mapping serves (shared blocks); per-front copies
+    // hold each front's own blocks
+    std::vector<uint8_t> tmp;
+    bool first = true;
+    for (XcgPairState* f : K->fronts) {
+      if (!f) continue;
+      if (K->vmm || first) {
+        if (hipMemcpy(data.data(), f->pool + (uint64_t)f->C * SEG, D * SEG, hipMemcpyDeviceToHost) != hipSuccess)
+          return -5;
+        first = false;
+        if (K->vmm) break;
+        continue;
+      }
+      tmp.resize((size_t)D * SEG);
+      if (hipMemcpy(tmp.data(), f->pool + (uint64_t)f->C * SEG, D * SEG, hipMemcpyDeviceToHost) != hipSuccess)
+        return -5;
+      for (uint64_t i = 0; i < D; ++i)
+        if (xu[i] == f->xuid) memcpy(&data[i * SEG], &tmp[i * SEG], SEG);
+    }
+  }
+  const int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0600);
+  if (fd == -1) return -2;
+  bool ok = ftruncate(fd, (off_t)K->bytes) == 0;
+  ok = ok && pwrite(fd, K->reg.data(), K->reg.size(), 0) == (ssize_t)K->reg.size();
+  std::vector<uint8_t> ib(2048);
+  for (uint64_t b = 0; ok && b < nb; ++b) {
+    memset(ib.data(), 0, ib.size());
+    if (K->ctr[b] != 0) {
+      uint8_t* q = ib.data();
+      memcpy(q, &K->ctr[b], 8);
+      q += 8;
+      for (uint64_t j = 0; j < DISK_ENTRIES; ++j, q += 10) {
+        const uint64_t i = b * DISK_ENTRIES + j;
+        const uint64_t h = key[i] == NOKEY ? 0 : key[i];
+        const uint16_t x = h == 0 ? 0 : (uint16_t)xu[i];
+        memcpy(q, &x, 2);
+        memcpy(q + 2, &h, 8);
+      }
+    }
+    ok = pwrite(fd, ib.data(), 2048, (off_t)((REG_BLOCKS + b) * 2048)) == 2048;
+  }
+  ok = ok && pwrite(fd, data.data(), data.size(), (off_t)((REG_BLOCKS + nb) * 2048)) == (ssize_t)data.size();
+  close(fd);
+  return ok ? 0 : -5;
+}
+
+// Open a volume file: reloaded when it holds one, else a fresh disk.
+int xcg_disk_state_open(const char* path, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out) {
+  XcgDiskState* K = nullptr;
+  const int rc = xcg_disk_state_create(disk_bytes, flags, &K);
+  if (rc) return rc;
+  struct stat st;
+  if (::stat(path, &st) == 0 && st.st_size > 0) {
+    std::vector<uint8_t> vol(disk_bytes, 0);
+    const int fd = ::open(path, O_RDONLY);
+    if (fd == -1 || pread(fd, vol.data(), vol.size(), 0) < 0) {
+      if (fd != -1) close(fd);
+      delete K;
+      return -2;
+    }
+    close(fd);
+    load_volume(K, vol);
+  }
+  *out = K;
   return 0;
 }
 
@@ -1647,7 +1955,11 @@ int xcg_pair_state_clear(XcgPairState* P) {
     return -5;
   hipLaunchKernelGGL(pair_drop_front_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr, K->dkey, K->dent,
                      (const uint32_t*)K->dxuid, K->D, others ? (uint32_t)P->xuid : NIL);
-  if (!others) K->dclock = 0;
+  if (!others) {                                             // a fresh volume
+    K->dclock = 0;
+    K->ctr.assign(K->nb, 0);
+    K->ibc = 1;
+  }
   P->pcount = 0;
   P->gclock = K->dclock;
   P->gstale = false;

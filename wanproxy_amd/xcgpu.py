@@ -83,6 +83,12 @@ def lib():
     L.xcg_disk_create_ex.restype = C.c_int
     L.xcg_disk_tier.argtypes = [vp]
     L.xcg_disk_tier.restype = C.c_int
+    L.xcg_disk_open.argtypes = [C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.xcg_disk_open.restype = C.c_int
+    L.xcg_disk_save.argtypes = [vp, C.c_char_p]
+    L.xcg_disk_save.restype = C.c_int
+    L.xcg_ctx_create_pair_uuid.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_pair_uuid.restype = C.c_int
     L.xcg_ctx_create_pair_on.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_pair_on.restype = C.c_int
     L.xcg_pair_stats.argtypes = [vp, vp]
@@ -178,10 +184,19 @@ class Disk:
 
     HOST, DEVICE = 1, 2          # XCG_DISK_HOST / XCG_DISK_DEVICE: force the blocks' tier
 
-    def __init__(self, disk_bytes: int, tier: int = 0):
+    def __init__(self, disk_bytes: int, tier: int = 0, path: str = None):
+        """With `path`: the volume file there (xcg_disk_open: reopened when it
+        holds one, else fresh)."""
         h = C.c_void_p()
-        _check(lib().xcg_disk_create_ex(int(disk_bytes), int(tier), C.byref(h)))
+        if path is not None:
+            _check(lib().xcg_disk_open(path.encode(), int(disk_bytes), int(tier), C.byref(h)))
+        else:
+            _check(lib().xcg_disk_create_ex(int(disk_bytes), int(tier), C.byref(h)))
         self.h = h
+
+    def save(self, path: str):
+        """Write the volume as the reference's file stands now (xcg_disk_save)."""
+        _check(lib().xcg_disk_save(self.h, path.encode()))
 
     def tier(self) -> int:
         """Where the data blocks live: 0 HBM, 1 pinned host memory (-1: no front yet)."""
@@ -210,20 +225,24 @@ class Context:
 
     def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
                  cache_segments: int = 1 << 19, memory_cache_limit: int = 0, disk_bytes: int = 0,
-                 disk: Disk = None):
+                 disk: Disk = None, uuid: str = None):
         """memory_cache_limit (bytes): the bounded, LRU-evicting cache
         XCodecMemoryCache(uuid, memory_cache_limit) (xcodec/xcodec_cache.h:277)
         instead of an unbounded one of cache_segments capacity.  With
         disk_bytes too: wanproxy.conf's XCodecCachePair of that memory cache
         and a disk of disk_bytes (xcodec/xcodec_cache.h:140-237); with `disk`
-        instead, the pair's secondary is the next front of that shared disk."""
+        instead, the pair's secondary is the next front of that shared disk
+        (with `uuid`, that UUID's front: XCodecDisk::connect)."""
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        if disk is not None:
+        if disk is not None and uuid is not None:
+            _check(lib().xcg_ctx_create_pair_uuid(device, self.flags, int(memory_cache_limit), disk.h, uuid.encode(),
+                                                  C.byref(h)))
+        elif disk is not None:
             _check(lib().xcg_ctx_create_pair_on(device, self.flags, int(memory_cache_limit), disk.h, C.byref(h)))
         elif disk_bytes:
             _check(lib().xcg_ctx_create_pair(device, self.flags, int(memory_cache_limit), int(disk_bytes), C.byref(h)))
