@@ -29,6 +29,11 @@ st = d_st.cpu().numpy().view(np.uint32).reshape(N, 4).astype(np.float64)
 w3 = st[:, 3].astype(np.int64)
 vec, evt, tot, pcs, nev = st[:, 0] / 100, st[:, 1] / 100, st[:, 2] / 100, w3 & 0xFFFF, w3 >> 16
 rest = tot - vec - evt
-print(f'independent: per chunk (us, median) total {np.median(tot):.0f} vector {np.median(vec):.0f} exact events '
-      f'{np.median(evt):.0f} ({np.median(nev):.0f} events, {np.median(evt / np.maximum(nev, 1)):.1f} us each) '
-      f'rest {np.median(rest):.0f}; pieces {np.median(pcs):.0f}')
+slot1 = os.environ.get('PH_SLOT1', 'exact events')   # what the build's XCG_PHASES_SLOT1 put in word 1
+if slot1 == 'exact events':
+    print(f'independent: per chunk (us, median) total {np.median(tot):.0f} vector {np.median(vec):.0f} exact events '
+          f'{np.median(evt):.0f} ({np.median(nev):.0f} events, {np.median(evt / np.maximum(nev, 1)):.1f} us each) '
+          f'rest {np.median(rest):.0f}; pieces {np.median(pcs):.0f}')
+else:
+    print(f'independent: per chunk (us, median) total {np.median(tot):.1f} vector {np.median(vec):.1f} '
+          f'{slot1} {np.median(evt):.1f}; pieces {np.median(pcs):.0f}')

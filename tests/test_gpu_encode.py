@@ -179,3 +179,60 @@ def test_independent_fuzz(oracle):
         exp = oracle.encode_batch(d, offs, lens, mode=2 if mode == 2 else 0, oob=mode != 0)
         bad = [k for k in range(len(exp)) if got[k] != exp[k]]
         assert not bad, (case, kind, mode, bad[:5])
+
+
+def _dm_key(block):
+    """The independent kernel's direct-mapped probe key of a 2048-byte window:
+    -(X2 + CLO) mod 2^32, X2 = sum (2048 - k) x_k (roll_probe_dm, xcg_encode.hip)."""
+    w = np.arange(2048, 0, -1, dtype=np.uint64)
+    x2 = int((w * block.astype(np.uint64)).sum()) & 0xFFFFFFFF
+    return (-(x2 + 0x80200400)) & 0xFFFFFFFF
+
+
+def _block_in_slot(rng, slot):
+    """A random 2 KiB block whose key lands in direct-mapped slot `slot`
+    (bits 2..12 of the key): bytes 2016 and 2047 (weights 32 and 1) absorb
+    the difference."""
+    b = rng.integers(0, 256, 2048, dtype=np.uint8)
+    b[2016] = 0
+    b[2047] = 0
+    r = (_dm_key(b) - 4 * slot) % 8192          # raising X2 by r lowers the key by r
+    b[2016] = r >> 5
+    b[2047] = r & 31
+    assert (_dm_key(b) >> 2) & 2047 == slot
+    return b
+
+
+@pytest.mark.parametrize('ncoll', [2, 5, 9, 30])
+def test_direct_mapped_slot_collisions(ctx, oracle, ncoll):
+    """Chunks whose declarations share direct-mapped key slots (1 slot + up
+    to 32 overflow keys per chunk: the N1 / N8 / N32 compare variants), then
+    repeat those blocks -- aligned, unaligned and cut -- so the REFs must be
+    found through the overflow keys."""
+    rng = np.random.default_rng(0xD1 + ncoll)
+    chunks_, lens = [], []
+    for c in range(6):
+        slot = int(rng.integers(0, 2048))
+        coll = [_block_in_slot(rng, slot) for _ in range(ncoll)]
+        fresh = [rng.integers(0, 256, 2048, dtype=np.uint8) for _ in range(max(0, 40 - ncoll))]
+        blocks = coll + fresh
+        parts = list(blocks)
+        for k in range(22):   # repeats of colliding and fresh blocks, some shifted by a few bytes
+            src = blocks[int(rng.integers(0, len(blocks)))] if k % 2 else coll[int(rng.integers(0, ncoll))]
+            if k % 3 == 2:
+                parts.append(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8))
+            parts.append(src)
+        b = np.concatenate(parts)[:131072 - int(rng.integers(0, 3000)) * (c % 2)]
+        chunks_.append(b)
+        lens.append(b.size)
+    offs = np.zeros(len(lens), np.uint64)
+    offs[1:] = np.cumsum(np.array(lens, np.uint64))[:-1]
+    allb = np.concatenate(chunks_)
+    lens = np.array(lens, np.uint32)
+    got = ctx.encode_chunks(allb, offs, lens)
+    ctx.status()
+    exp = oracle.encode_batch(allb, offs, lens, mode=0)
+    bad = [i for i in range(len(got)) if got[i] != exp[i]]
+    assert not bad, bad
+    # the repeats really were found (REFs in the oracle's output)
+    assert sum(e.count(b'\xf1\x02') for e in exp) >= 6 * 10

@@ -50,14 +50,16 @@ namespace xcg {
 // address is a single and-or of K.
 // Overflow keys a chunk's table holds: 8, or 32 for frames of up to 512 KiB
 // (~256 declarations in 1024 buckets: a tail of 9+ three-key buckets happens).
-template <int MAXD>
-constexpr int ovf_cap() { return MAXD > 72 ? 32 : 8; }
+// Independent chunks' direct-mapped tables (DMV, roll_probe_dm): 32, a key
+// overflowing as soon as its slot is taken.
+template <int MAXD, bool DMV = false>
+constexpr int ovf_cap() { return MAXD > 72 || DMV ? 32 : 8; }
 
-template <int LOGNB, int MAXD>
+template <int LOGNB, int MAXD, bool DMV = false>
 struct WaveRecs {
   static constexpr int NB = 1 << LOGNB;
   uint32_t rlo[MAXD], rhi[MAXD], rc[MAXD];  // exact hash + chunk position
-  uint32_t ovf_k[ovf_cap<MAXD>()];          // keys whose bucket was full
+  uint32_t ovf_k[ovf_cap<MAXD, DMV>()];     // keys whose bucket was full
 };
 
 template <int LOGNB>
@@ -68,7 +70,7 @@ __device__ __forceinline__ uint32_t kempty(uint32_t b) { return (~b & ((1u << LO
 template <int LOGNB, int MAXD, int W>
 struct IndepLDS {
   uint32_t key[W][2 << LOGNB];
-  WaveRecs<LOGNB, MAXD> rec[W];
+  WaveRecs<LOGNB, MAXD, (MAXD <= 72)> rec[W];
 };
 constexpr int GSLOTS_DECL = 8;   // = GSLOTS (pass-1 queue depth per lane)
 template <int LOGNB, int MAXD, int W>
@@ -207,8 +209,10 @@ __device__ __forceinline__ void wave_put_ref(uint8_t* dst, uint32_t lo, uint32_t
 // ------------------------------------------------------------ exact checks
 
 // XCodecHash::hash of the 2048-byte window at w (xcodec_hash.h:166-174),
-// whole wave: lane l sums bytes [16l, 16l+16) and [1024+16l, +16).
-__device__ __noinline__ uint2 wave_window_hash(const uint8_t* w) {
+// whole wave: lane l sums bytes [16l, 16l+16) and [1024+16l, +16).  z = the
+// window's direct-mapped probe key -(X2 + CLO) (independent chunks, see
+// roll_probe_dm).
+__device__ __noinline__ uint3 wave_window_hash(const uint8_t* w) {
   const int l = lane_id();
   uint32_t X1 = 0, X2 = 0, F1 = 0, F2 = 0;
 #pragma unroll
@@ -224,7 +228,7 @@ __device__ __noinline__ uint2 wave_window_hash(const uint8_t* w) {
     }
   }
   X1 = wave_sum(X1); X2 = wave_sum(X2); F1 = wave_sum(F1); F2 = wave_sum(F2);
-  return make_uint2((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4);
+  return make_uint3((X1 << 20) + X2 + CLO, ((F1 << 16) + F2) << 4, 0u - (X2 + CLO));
 }
 
 // Byte-equality of two 2048-byte segments (BufferSegment::equal in
@@ -248,9 +252,9 @@ __device__ __noinline__ bool wave_equal2048(const uint8_t* a, const uint8_t* b) 
 __device__ __forceinline__ uint32_t escape_u(uint8_t* dst, const uint8_t* x, uint32_t a, uint32_t b) {
   return readfirst(wave_escape(dst, x, a, b));
 }
-__device__ __forceinline__ uint2 window_hash_u(const uint8_t* w) {
-  const uint2 h = wave_window_hash(w);
-  return make_uint2(readfirst(h.x), readfirst(h.y));
+__device__ __forceinline__ uint3 window_hash_u(const uint8_t* w) {
+  const uint3 h = wave_window_hash(w);
+  return make_uint3(readfirst(h.x), readfirst(h.y), readfirst(h.z));
 }
 __device__ __forceinline__ bool equal2048_u(const uint8_t* a, const uint8_t* b) {
   return readfirst((uint32_t)wave_equal2048(a, b)) != 0u;
@@ -472,6 +476,100 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
   return __builtin_bitreverse32(ev) | (GLB ? gq.gev : 0u);   // ev: position j was shifted in at bit 31 - j
 }
 
+// Independent chunks of up to 128 KiB (the headline path): the wave's table
+// holds only its own chunk's declarations (at most 63), so its probe key need
+// not be -lo, which the persistent cache's filters are built on.  It is NX2 =
+// -(X2 + CLO), the rolled weighted sum itself (no key instruction), in a
+// direct-mapped table of 2 << LOGNB slots (slot = bits 2.. of the key; one
+// compare; a key whose slot is taken is an overflow key).  EVW false: return
+// only the lanes with a possible hit (per lane, the minimum of slot ^ key over
+// its positions is 0), no per-position event bit -- in independent chunks
+// almost every piece has none, and a piece that has one is rolled again with
+// EVW true for its event word.  Per position: 4 VALU to roll, 1 for the LDS
+// address, 1.5 for the xor / min3 (vs 9 for roll_probe's event word).
+template <int LOGNB>
+__device__ __forceinline__ uint32_t dm_slot_mask() { return ((2u << LOGNB) - 1u) << 2; }
+template <int LOGNB>
+__device__ __forceinline__ uint32_t dm_empty(uint32_t slot) { return (~slot & ((2u << LOGNB) - 1u)) << 2; }
+
+template <int LOGNB, bool C0, int NOVF, bool EVW>
+__device__ __forceinline__ uint64_t roll_probe_dm(const Piece& P, uint32_t NX1, uint32_t NX2, const char* kblk,
+                                                  uint32_t kofs, uint32_t c0k, int rvis, const uint32_t* ovp,
+                                                  uint32_t novf) {
+  const uint32_t KM = (uint32_t)opaque((int)dm_slot_mask<LOGNB>());
+  const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
+  const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
+  // (unused overflow slots repeat a real overflow key)
+  uint32_t o[NOVF > 0 ? NOVF : 1];
+#pragma unroll
+  for (int k = 0; k < NOVF; ++k) o[k] = readfirst(ovp[(uint32_t)k < novf ? k : 0]);
+  uint64_t vis_hi = 0, vis_lo = 0;
+  int vB = 0;
+  if (C0) {
+    const int A = rvis >> 5;
+    vB = rvis & 31;
+    auto from_lane = [](int t) -> uint64_t { return t <= 0 ? ~0ull : (t >= 64 ? 0ull : (~0ull << t)); };
+    vis_hi = from_lane(A + 1);
+    vis_lo = from_lane(A);
+  }
+  static_assert(EVW || !C0, "a piece with a pending candidate takes the event word directly");
+  uint32_t ev = 0, amin = ~0u;
+  auto roll4 = [&](int g, uint32_t (&kv)[4], uint32_t (&e)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = 4 * g + t;
+      kv[t] = NX2;
+      if (j < 31) {
+        const uint32_t xo = byte_of(xa[j >> 2], j & 3);
+        const uint32_t xn = byte_of(xb[j >> 2], j & 3);
+        NX1 += xo - xn;
+        NX2 += NX1 + (xo << 11);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) e[t] = *(const uint32_t*)(kblk + ((kv[t] & KM) | kofs));
+  };
+  uint32_t kc[4], ec[4];
+  roll4(0, kc, ec);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    uint32_t kn[4], en[4];
+    if (g < 7) roll4(g + 1, kn, en);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = 4 * g + t;
+      if (EVW) {
+        uint64_t hit = lanes_eq(ec[t], kc[t]);
+        if (C0) hit |= lanes_eq(kc[t], c0k) & (j < vB ? vis_hi : vis_lo);
+#pragma unroll
+        for (int k = 0; k < NOVF; ++k) hit |= lanes_eq(o[k], kc[t]);
+        ev = shift_in(ev, hit);
+      }
+    }
+    if (!EVW) {
+      // per lane: the minimum of (slot ^ key) over the positions is 0 iff one
+      // matched -- xor + half a min3 per position, no SGPR round trip
+      uint32_t xx[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) xx[t] = ec[t] ^ kc[t];
+      amin = min(amin, min(xx[0], xx[1]));
+      amin = min(amin, min(xx[2], xx[3]));
+#pragma unroll
+      for (int k = 0; k < NOVF; ++k) {
+#pragma unroll
+        for (int t = 0; t < 4; t += 2) amin = min(amin, min(o[k] ^ kc[t], o[k] ^ kc[t + 1]));
+      }
+    }
+    if (EVW) asm volatile("" : "+v"(ev));
+    __builtin_amdgcn_sched_barrier(0);
+    if (g < 7) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { kc[t] = kn[t]; ec[t] = en[t]; }
+    }
+  }
+  return EVW ? (uint64_t)__builtin_bitreverse32(ev) : ballot(amin == 0u);
+}
+
 // ------------------------------------------------------------------ kernel
 
 // Waves sharing a SIMD issue by priority, then age: with equal priorities the
@@ -506,8 +604,11 @@ struct GlbView {
 
 template <int LOGNB, int MAXD, bool STREAM, bool LRU = false>
 __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, const uint32_t kofs,
-                                             WaveRecs<LOGNB, MAXD>& T, const uint32_t chunk, const GlbView gs) {
+                                             WaveRecs<LOGNB, MAXD, (!STREAM && MAXD <= 72)>& T, const uint32_t chunk,
+                                             const GlbView gs) {
   constexpr int NB = 1 << LOGNB;
+  // independent chunks of up to 128 KiB: direct-mapped NX2 keys (roll_probe_dm)
+  constexpr bool DM = !STREAM && MAXD <= 72;
   const int l = lane_id();
 
   const uint8_t* x = prm.in + prm.chunk_off[chunk];
@@ -523,10 +624,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #endif
 #ifdef XCG_PHASES
 #ifndef XCG_PHASES_SLOT1
-#define XCG_PHASES_SLOT1 0   // 1: stats word 1 = piece setup time instead of exact-event time
+#define XCG_PHASES_SLOT1 0   // stats word 1: 0 exact-event time, 1 piece setup time, 2 prefetch wait
 #endif
   // diagnostics build: time in the vector phase and in REF-chaining probes
-  uint64_t ph_vec = 0, ph_chain = 0, ph_ev = 0, ph_setup = 0;
+  uint64_t ph_vec = 0, ph_chain = 0, ph_ev = 0, ph_setup = 0, ph_wait = 0;
   uint32_t ph_nev = 0;
 #endif
   // A chunk longer than the launch's bound would overrun the records sized
@@ -549,7 +650,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   }
 
   uint32_t* const keyt = (uint32_t*)(kblk + kofs);
-  for (int k = l; k < 2 * NB; k += 64) keyt[k] = kempty<LOGNB>((uint32_t)k >> 1);
+  for (int k = l; k < 2 * NB; k += 64) keyt[k] = DM ? dm_empty<LOGNB>((uint32_t)k) : kempty<LOGNB>((uint32_t)k >> 1);
   uint32_t ndecl = 0, novf = 0;
 
   const int last = L - SEG;                        // last window start
@@ -558,6 +659,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   bool have_cand = false;
   int cand = 0;
   uint32_t cand_lo = 0, cand_hi = 0;
+  uint32_t cand_k = 0;                             // (DM) the candidate's probe key
   // In-band independent encoding never outputs a declared hash, and its hi half
   // only matters when a later window matches the declaration's lo: then it is
   // computed from the declared bytes (lookup).  HI_LAZY (odd) marks "not yet";
@@ -583,7 +685,23 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   // Insert a declaration into the LDS table (XCodecMemoryCache::enter,
   // xcodec_cache.h:303-325) -- by lane 0, visible to later LDS reads of the
   // wave (LDS ops of one wave complete in order).
-  auto insert = [&](uint32_t lo, uint32_t hi, uint32_t c) {
+  auto insert = [&](uint32_t lo, uint32_t hi, uint32_t c, uint32_t k2) {
+    if (DM) {
+      const uint32_t d = ndecl++;
+      const uint32_t sl = (k2 >> 2) & ((2u << LOGNB) - 1u), ke = dm_empty<LOGNB>(sl);
+      const uint32_t s0 = readfirst(keyt[sl]);
+      if (l == 0) {
+        T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
+        if (s0 == ke) keyt[sl] = k2;
+        else if (novf < (uint32_t)ovf_cap<MAXD, DM>()) T.ovf_k[novf] = k2;
+      }
+      if (s0 != ke) {
+        if (novf < (uint32_t)ovf_cap<MAXD, DM>()) ++novf;
+        else if (l == 0 && prm.status) atomicOr(prm.status, 1);
+      }
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
     const uint32_t d = ndecl++;
     const uint32_t k = probe_key(lo);
     const uint32_t b = kbucket<LOGNB>(k), ke = kempty<LOGNB>(b);
@@ -681,7 +799,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   auto declare = [&](int at) {
     if (LRU) record(cand_lo, cand_hi, 2u * (uint32_t)at, EV_ENTER, n_extract);
     if (cand > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)cand);
-    if (!nullcache && !c0_in_table) insert(cand_lo, cand_hi, (uint32_t)cand);
+    if (!nullcache && !c0_in_table) insert(cand_lo, cand_hi, (uint32_t)cand, cand_k);
     if (oob) {
       wave_put_ref(out + olen, cand_lo, cand_hi);           // :288-295
       olen += 10;
@@ -769,7 +887,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         }
         for (uint32_t d = 0; d < nd_r; ++d) {           // the own records and key table so far
           const uint4 r = odl[d];
-          insert(readfirst(r.x), readfirst(r.y), readfirst(r.z));
+          insert(readfirst(r.x), readfirst(r.y), readfirst(r.z), 0u);   // (stream: keyed by lo)
           if (l == 0) gs.ro[d] = r.w;
         }
         if (l == 0) {
@@ -1008,7 +1126,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         lo = 0u - readfirst(k0);
         hi = readfirst(lane_window_hi(P, 0));
       } else {
-        const uint2 h = window_hash_u(x + s);
+        const uint3 h = window_hash_u(x + s);
         lo = h.x; hi = h.y;
       }
       const int d = lookup(lo, hi);                 // stream records carry their hi
@@ -1048,7 +1166,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       // c0 = the pending candidate; once it is visible from the piece start on,
       // it goes straight into the table (a REF can no longer cancel it).
       if (have_cand && !c0_in_table && cand + SEG <= p) {
-        insert(cand_lo, cand_hi, (uint32_t)cand);
+        insert(cand_lo, cand_hi, (uint32_t)cand, cand_k);
         c0_in_table = true;
       }
       if (pe - s <= 2) {
@@ -1060,14 +1178,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         const bool c0 = have_cand && !c0_in_table;
         const int vis = cand + SEG;
         const int rvis = vis - p;
-        const uint32_t c0k = probe_key(cand_lo);
+        const uint32_t c0k = DM ? cand_k : probe_key(cand_lo);
         // Bucket overflows are rare (three of a chunk's keys in one 2-slot
         // bucket); one overflow key costs one compare, more cost eight (32
         // beyond eight, in frames of up to 512 KiB).
-        constexpr int OC = ovf_cap<MAXD>();
+        constexpr int OC = ovf_cap<MAXD, DM>();
         uint32_t ovk[OC];
   #pragma unroll
-        for (int k = 0; k < OC; ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
+        for (int k = 0; k < (DM ? 1 : OC); ++k) ovk[k] = novf ? readfirst(T.ovf_k[(uint32_t)k < novf ? k : 0]) : 0u;
         const uint32_t sa0 = gs.sofs + 4u * (uint32_t)lane_id();
         GlbQ gq{gs.lds, gs.lfo, prm.lf.gfilt, prm.lf.gmask, prm.lf.ftab, prm.lf.fmask, sa0, sa0, sa0 + 256u * GSLOTS,
                 0u, 0u};
@@ -1089,7 +1207,26 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
           if (OC == 8 || novf <= 8) return c0 ? roll(T1{}, N8{}, glbt) : roll(T0{}, N8{}, glbt);
           return c0 ? roll(T1{}, NC{}, glbt) : roll(T0{}, NC{}, glbt);
         };
-        if (STREAM && gs.fmode == 1) {
+        if constexpr (DM) {
+          // the lane mask of possible hits first; the event word only if any
+          auto rolld = [&](auto c0t, auto novft, auto evwt) -> uint64_t {
+            return roll_probe_dm<LOGNB, decltype(c0t)::value, decltype(novft)::value, decltype(evwt)::value>(
+                P, NX1, NX2, kblk, kofs, c0k, rvis, T.ovf_k, novf);
+          };
+          auto by_novf_dm = [&](auto evwt) -> uint64_t {
+            if (novf == 0) return rolld(T0{}, N0{}, evwt);
+            if (novf == 1) return rolld(T0{}, N1{}, evwt);
+            return rolld(T0{}, N8{}, evwt);
+          };
+          if (c0 || novf > 8) {   // (rare: the event word straight away)
+            if (novf == 0) ev = (uint32_t)rolld(T1{}, N0{}, T1{});
+            else if (novf == 1) ev = (uint32_t)rolld(T1{}, N1{}, T1{});
+            else if (novf <= 8) ev = (uint32_t)rolld(T1{}, N8{}, T1{});
+            else ev = (uint32_t)(c0 ? rolld(T1{}, NC{}, T1{}) : rolld(T0{}, NC{}, T1{}));
+          } else {
+            ev = by_novf_dm(T0{}) != 0 ? (uint32_t)by_novf_dm(T1{}) : 0u;
+          }
+        } else if (STREAM && gs.fmode == 1) {
           ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
         } else if (STREAM && gs.fmode == 2) {
           ev = by_novf(std::integral_constant<int, STREAM ? 2 : 0>{});
@@ -1108,7 +1245,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     }
     // The prefetch has had the vector phase to land; take it before the
     // resolve phase issues this piece's stores.
+#ifdef XCG_PHASES
+    const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
+#endif
     vuse(nb0); vuse(nb1);                          // (unconditional: so the compiler sees them waited)
+#ifdef XCG_PHASES
+    ph_wait += __builtin_amdgcn_s_memrealtime() - tw0;
+#endif
 
 #ifdef XCG_PHASES
     ph_vec += __builtin_amdgcn_s_memrealtime() - tv0;
@@ -1124,14 +1267,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       const uint32_t mm = readlane(m, lw);
       return p + 32 * lw + __builtin_ctz(mm);
     };
-    auto hash_at = [&](int pos, uint32_t& lo, uint32_t& hi) {
+    auto hash_at = [&](int pos, uint32_t& lo, uint32_t& hi, uint32_t& k2) {
       const int rel = pos - p;
       if ((rel & 31) == 0) {
         lo = 0u - readlane(k0, rel >> 5);
         hi = lazy_hi ? HI_LAZY : readfirst(lane_window_hi(P, rel >> 5));
+        k2 = DM ? readlane(NX2, rel >> 5) : 0u;
       } else {
-        const uint2 h = window_hash_u(x + pos);
-        lo = h.x; hi = h.y;
+        const uint3 h = window_hash_u(x + pos);
+        lo = h.x; hi = h.y; k2 = h.z;
       }
     };
 
@@ -1152,11 +1296,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // then the window is hashed again.
         uint32_t lo = 0, hi = 0;
         int d = -1, fill = -1;
+        uint3 hh;
         for (;;) {
-          uint2 hh;
           if (fill < 0 && ((s - p) & 31) == 0) {   // a lane's first window: the hash from registers
             hh.x = 0u - readlane(k0, (s - p) >> 5);
             hh.y = readfirst(lane_window_hi(P, (s - p) >> 5));
+            hh.z = DM ? readlane(NX2, (s - p) >> 5) : 0u;
           } else {
             hh = window_hash_u(fill >= 0 ? x + readfirst(T.rc[fill]) : x + s);
           }
@@ -1197,13 +1342,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         }
         // fingerprint false positive: an ordinary miss
         if (!have_cand) {
-          have_cand = true; cand = s; cand_lo = lo; cand_hi = hi; c0_in_table = false;
+          have_cand = true; cand = s; cand_lo = lo; cand_hi = hi; cand_k = hh.z; c0_in_table = false;
         }
         ++s;
         continue;
       }
       if (!have_cand) {                                       // :246-248
-        hash_at(s, cand_lo, cand_hi);
+        hash_at(s, cand_lo, cand_hi, cand_k);
         have_cand = true;
         cand = s;
         c0_in_table = false;
@@ -1256,10 +1401,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #if defined(XCG_PHASES)
       // diagnostics build: {vector phase, REF-chaining probes, whole chunk} (100 MHz ticks), pieces
       prm.stats[4 * chunk + 0] = (uint32_t)ph_vec;
-      prm.stats[4 * chunk + 1] = (uint32_t)(XCG_PHASES_SLOT1 ? ph_setup : ph_ev);
+      prm.stats[4 * chunk + 1] = (uint32_t)(XCG_PHASES_SLOT1 == 2 ? ph_wait : XCG_PHASES_SLOT1 ? ph_setup : ph_ev);
       prm.stats[4 * chunk + 2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
       prm.stats[4 * chunk + 3] = (ph_nev << 16) | n_pieces;
-      (void)ph_chain; (void)ph_setup; (void)ph_ev;
+      (void)ph_chain; (void)ph_setup; (void)ph_ev; (void)ph_wait;
       (void)n_extract; (void)n_ref; (void)n_coll;
 #elif defined(XCG_TIMING)
       // diagnostics build: {start, end} (100 MHz realtime, low words), HW_ID, XCC_ID
