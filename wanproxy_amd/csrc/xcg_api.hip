@@ -210,6 +210,7 @@ struct xcg_ctx {
   hipStream_t call_st = nullptr;
   hipStream_t last_mark = nullptr; // stream of the last ctx_mark (ctx_order on it needs no wait)
   bool marked = false;
+  bool mark_pending = false;       // done_ev not yet recorded behind the last call (ctx_flush_mark)
   // zero-copy staging of the one-launch decode() (coherent pinned host memory
   // the kernel reads and writes directly): [flag 256][input][output][results]
   uint8_t* zc_h = nullptr;
@@ -235,21 +236,33 @@ struct DeviceGuard {
 
 constexpr uint32_t FILT_WORDS = (1u << 19) / 32;   // xcg_cache.h FILT_LOG2
 
+// The context's last call was enqueued on last_mark; done_ev is recorded
+// behind it only when another stream or a host wait needs it.  Recording it
+// later on the same stream marks the same point or a later one (never an
+// earlier one), and back-to-back calls on one stream -- the batched encode's
+// steady state -- enqueue nothing but their kernels (a marker per call cost
+// the headline launch ~5-10 us of gap).
+void ctx_flush_mark(xcg_ctx* c) {
+  if (c->mark_pending && c->done_ev) (void)hipEventRecord(c->done_ev, c->last_mark);
+  c->mark_pending = false;
+}
 // The context's work so far is complete (its last call's stream reached the
 // event) -- the per-context replacement for a device-wide synchronise.
 int ctx_wait(xcg_ctx* c) {
+  ctx_flush_mark(c);
   return c->done_ev && hipEventSynchronize(c->done_ev) != hipSuccess ? XCG_EHIP : XCG_OK;
 }
 void ctx_mark(xcg_ctx* c, hipStream_t st) {
-  if (c->done_ev) (void)hipEventRecord(c->done_ev, st);
   c->last_mark = st;
   c->marked = true;
+  c->mark_pending = true;
 }
 // Work enqueued on `st` starts after the context's last enqueued work (a cache
 // clear on another stream, the previous call of another stream): the
 // reference's calls on one cache are serialised, and so are these.
 void ctx_order(xcg_ctx* c, hipStream_t st) {
   if (c->marked && c->last_mark == st && st != nullptr) return;   // (in stream order already)
+  ctx_flush_mark(c);
   if (c->done_ev) (void)hipStreamWaitEvent(st, c->done_ev, 0);
 }
 

@@ -579,10 +579,10 @@ __device__ __forceinline__ uint64_t roll_probe_dm(const Piece& P, uint32_t NX1, 
 // yields until the others catch up), so the four finish nearly together;
 // only the last 1/16 is age-ordered.
 __device__ __forceinline__ void progress_priority(int s, int L) {
-  const int q = (16 * s) / L;                      // sixteenths of the chunk parsed, uniform
-  if (q < 8) __builtin_amdgcn_s_setprio(3);
-  else if (q < 12) __builtin_amdgcn_s_setprio(2);
-  else if (q < 15) __builtin_amdgcn_s_setprio(1);
+  const int s16 = 16 * s;                          // sixteenths of the chunk parsed: 16 s / L (no division)
+  if (s16 < 8 * L) __builtin_amdgcn_s_setprio(3);
+  else if (s16 < 12 * L) __builtin_amdgcn_s_setprio(2);
+  else if (s16 < 15 * L) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
 }
 
@@ -1161,6 +1161,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     ph_setup += tv0 - tp0;
 #endif
     uint32_t ev = 0;
+    bool quiet = false;                            // (DM) no lane has a possible hit in this piece
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
     if (!nullcache) {
       // c0 = the pending candidate; once it is visible from the piece start on,
@@ -1218,13 +1219,19 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
             if (novf == 1) return rolld(T0{}, N1{}, evwt);
             return rolld(T0{}, N8{}, evwt);
           };
+#ifdef XCG_EXP_NOVEC   // (timing experiment only: output is wrong)
+          if (true) {
+            ev = 0;
+          } else
+#endif
           if (c0 || novf > 8) {   // (rare: the event word straight away)
             if (novf == 0) ev = (uint32_t)rolld(T1{}, N0{}, T1{});
             else if (novf == 1) ev = (uint32_t)rolld(T1{}, N1{}, T1{});
             else if (novf <= 8) ev = (uint32_t)rolld(T1{}, N8{}, T1{});
             else ev = (uint32_t)(c0 ? rolld(T1{}, NC{}, T1{}) : rolld(T0{}, NC{}, T1{}));
           } else {
-            ev = by_novf_dm(T0{}) != 0 ? (uint32_t)by_novf_dm(T1{}) : 0u;
+            quiet = by_novf_dm(T0{}) == 0;
+            ev = quiet ? 0u : (uint32_t)by_novf_dm(T1{});
           }
         } else if (STREAM && gs.fmode == 1) {
           ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
@@ -1279,6 +1286,32 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       }
     };
 
+#ifdef XCG_EXP_NORESOLVE   // (timing experiment only: output is wrong)
+    s = pe;
+#endif
+    // Independent chunks' steady state: the candidate set at the previous
+    // piece's start is declared here (its key went into the table before the
+    // vector phase, its body was stored from registers), nothing matched, and
+    // the next candidate is this piece's first window -- the resolve loop
+    // below would do exactly this, through two event searches.
+    if (DM && quiet && !oob && !nullcache && have_cand && c0_in_table && cand + SEG == s && s == p && base == cand &&
+        spec_cand == cand && spec_olen == olen) {
+      if (l < 2) out[olen + l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);   // encode_declaration :300-302
+      olen += 2 + SEG;
+      ++n_extract;
+      base = s;
+      cand = s;                                     // :246-248, the hash from registers
+      cand_lo = 0u - readlane(k0, 0);
+      cand_hi = lazy_hi ? HI_LAZY : readfirst(lane_window_hi(P, 0));
+      cand_k = readlane(NX2, 0);
+      c0_in_table = false;
+      uint8_t* dst = out + olen + 2 + 32 * lane_id();
+      *(u32x4_u*)dst = P.a0;
+      *(u32x4_u*)(dst + 16) = P.a1;
+      spec_cand = s;
+      spec_olen = olen;
+      s = pe;
+    }
     while (s < pe) {
       if (have_cand && cand + SEG <= s) declare(s);           // :183-190
       const int e = nullcache ? INT32_MAX : next_event(s);
@@ -1355,8 +1388,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         if (s == p && base == s && !oob) {
           // Declaration body = bytes [p, p + 2048) = the A registers.
           uint8_t* dst = out + olen + 2 + 32 * lane_id();
+#if defined(XCG_EXP_ALIGNSTORE)   // (timing experiments only: output is wrong)
+          dst = out + ((olen + 2) & ~15u) + 32 * lane_id();
+#endif
+#ifndef XCG_EXP_NOSTORE
           *(u32x4_u*)dst = P.a0;
           *(u32x4_u*)(dst + 16) = P.a1;
+#endif
           spec_cand = s;
           spec_olen = olen;
         }
@@ -1425,8 +1463,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 }
 
 
+#ifndef XCG_INDEP_OCC
+#define XCG_INDEP_OCC 4
+#endif
+#ifndef XCG_INDEP_LOGNB
+#define XCG_INDEP_LOGNB 10
+#endif
 template <int LOGNB, int MAXD>
-__global__ __launch_bounds__(256, 4) void encode_independent_kernel(EncParams prm) {
+__global__ __launch_bounds__(256, XCG_INDEP_OCC) void encode_independent_kernel(EncParams prm) {
   __shared__ IndepLDS<LOGNB, MAXD, 4> S;
   const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
   const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
@@ -1462,7 +1506,7 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   }
 }
 
-template __global__ void encode_independent_kernel<10, 72>(EncParams);
+template __global__ void encode_independent_kernel<XCG_INDEP_LOGNB, 72>(EncParams);
 template __global__ void encode_independent_kernel<11, 264>(EncParams);
 template __global__ void encode_stream_kernel<8, 72, 16, false>(EncParams);
 template __global__ void encode_stream_kernel<8, 72, 8, false>(EncParams);
@@ -1487,7 +1531,7 @@ extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t
   prm.max_len = max_chunk_len;
   dim3 grid((n + 3) / 4), block(256);
   if (max_chunk_len <= (1u << 17)) {
-    hipLaunchKernelGGL((xcg::encode_independent_kernel<10, 72>), grid, block, 0, stream, prm);
+    hipLaunchKernelGGL((xcg::encode_independent_kernel<XCG_INDEP_LOGNB, 72>), grid, block, 0, stream, prm);
   } else if (max_chunk_len <= (1u << 19)) {
     hipLaunchKernelGGL((xcg::encode_independent_kernel<11, 264>), grid, block, 0, stream, prm);
   } else {
