@@ -1294,8 +1294,15 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // vector phase, its body was stored from registers), nothing matched, and
     // the next candidate is this piece's first window -- the resolve loop
     // below would do exactly this, through two event searches.
+    // The new candidate can no longer be cancelled: positions before its
+    // declaration point (the next piece's start) are all in this quiet piece.
+    // So it enters the table now (XCodecMemoryCache::enter at its declaration,
+    // visible from the next piece on), its slot read overlapping the stores.
     if (DM && quiet && !oob && !nullcache && have_cand && c0_in_table && cand + SEG == s && s == p && base == cand &&
-        spec_cand == cand && spec_olen == olen) {
+        spec_cand == cand && spec_olen == olen && pe == p + SEG) {
+      const uint32_t k2 = readlane(NX2, 0);
+      const uint32_t sl = (k2 >> 2) & ((2u << LOGNB) - 1u);
+      const uint32_t s0v = keyt[sl];
       if (l < 2) out[olen + l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);   // encode_declaration :300-302
       olen += 2 + SEG;
       ++n_extract;
@@ -1303,14 +1310,26 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       cand = s;                                     // :246-248, the hash from registers
       cand_lo = 0u - readlane(k0, 0);
       cand_hi = lazy_hi ? HI_LAZY : readfirst(lane_window_hi(P, 0));
-      cand_k = readlane(NX2, 0);
-      c0_in_table = false;
+      cand_k = k2;
       uint8_t* dst = out + olen + 2 + 32 * lane_id();
       *(u32x4_u*)dst = P.a0;
       *(u32x4_u*)(dst + 16) = P.a1;
       spec_cand = s;
       spec_olen = olen;
       s = pe;
+      // insert (as insert() above, its slot already read)
+      const uint32_t d = ndecl++, ke = dm_empty<LOGNB>(sl), s0 = readfirst(s0v);
+      if (l == 0) {
+        T.rlo[d] = cand_lo; T.rhi[d] = cand_hi; T.rc[d] = (uint32_t)cand;
+        if (s0 == ke) keyt[sl] = k2;
+        else if (novf < (uint32_t)ovf_cap<MAXD, DM>()) T.ovf_k[novf] = k2;
+      }
+      if (s0 != ke) {
+        if (novf < (uint32_t)ovf_cap<MAXD, DM>()) ++novf;
+        else if (l == 0 && prm.status) atomicOr(prm.status, 1);
+      }
+      __builtin_amdgcn_wave_barrier();
+      c0_in_table = true;
     }
     while (s < pe) {
       if (have_cand && cand + SEG <= s) declare(s);           // :183-190
