@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // Prefetch the next contiguous piece's entering bytes; they land while
     // this piece rolls (issued after every use of this piece's loads).
     nb_start = p + SEG;
-    if (nb_start <= last) {
+    if (nb_start < last) {                         // (nb_start == last: decided as this piece's tail1 window)
       nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
       nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
     }
@@ -1264,7 +1264,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     ph_vec += __builtin_amdgcn_s_memrealtime() - tv0;
 #endif
     // ---- resolve phase (wave-uniform)
+    // A chunk whose last window is one past a full piece (every chunk of
+    // 2048 k + 2048 bytes: C2's 64 KiB, C4's 4 KiB) decides that window here,
+    // as an event (hashed by the one window-hash call site), instead of in a
+    // piece of its own.
+    const bool tail1 = pe == p + SEG && last == pe;
+    const int pe_x = tail1 ? pe + 1 : pe;
     auto next_event = [&](int from) -> int {
+      if (tail1 && from == pe) return from;
       const int rel = from - p;
       const int ls = rel >> 5, bs = rel & 31;
       uint32_t m = l < ls ? 0u : (l == ls ? (ev & (0xFFFFFFFFu << bs)) : ev);
@@ -1276,7 +1283,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     };
     auto hash_at = [&](int pos, uint32_t& lo, uint32_t& hi, uint32_t& k2) {
       const int rel = pos - p;
-      if ((rel & 31) == 0) {
+      if ((rel & 31) == 0 && rel < SEG) {
         lo = 0u - readlane(k0, rel >> 5);
         hi = lazy_hi ? HI_LAZY : readfirst(lane_window_hi(P, rel >> 5));
         k2 = DM ? readlane(NX2, rel >> 5) : 0u;
@@ -1331,7 +1338,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       __builtin_amdgcn_wave_barrier();
       c0_in_table = true;
     }
-    while (s < pe) {
+    while (s < pe_x) {
       if (have_cand && cand + SEG <= s) declare(s);           // :183-190
       const int e = nullcache ? INT32_MAX : next_event(s);
       if (e == s) {
@@ -1350,7 +1357,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         int d = -1, fill = -1;
         uint3 hh;
         for (;;) {
-          if (fill < 0 && ((s - p) & 31) == 0) {   // a lane's first window: the hash from registers
+          if (fill < 0 && ((s - p) & 31) == 0 && s - p < SEG) {   // a lane's first window: the hash from registers
             hh.x = 0u - readlane(k0, (s - p) >> 5);
             hh.y = readfirst(lane_window_hi(P, (s - p) >> 5));
             hh.z = DM ? readlane(NX2, (s - p) >> 5) : 0u;
@@ -1372,7 +1379,9 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // an earlier chunk of the batch.  src = that segment's bytes.
         const uint8_t* src = d >= 0 ? x + readfirst(T.rc[d]) : nullptr;
         if (LRU && d >= 0) record(lo, hi, 2u * (uint32_t)s + 1u, EV_HIT, 0u);
-        if (STREAM && src == nullptr) src = cache_src(lo, hi, s);
+        // (through the lane filter first: the forced events of a chunk's last
+        // one or two windows and own-table false positives have not passed it)
+        if (STREAM && src == nullptr && glb_pass(probe_key(lo))) src = cache_src(lo, hi, s);
         if (src != nullptr) {
           if (equal2048_u(src, x + s)) {
             if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
