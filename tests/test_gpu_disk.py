@@ -164,3 +164,61 @@ def test_volume_reopen_vs_reference(ref_oracle, tmp_path, nb):
     assert sum(map(len, sum(exp2[:1], []))) < sum(map(len, sum(fresh, [])))
     # and each front's index holds what the reference's holds
     assert (st[0][1], st[1][1]) == (ref_oracle.pair_stats(pa2)[0], ref_oracle.pair_stats(pb2)[0])
+
+
+def test_host_tier_in_a_process_without_torch(ref_oracle, tmp_path):
+    """The spill tier where it is meant to run: a process that links
+    libxcgpu.so and never loads PyTorch (wanproxy with the drop-in), whose HIP
+    runtime maps pinned host memory behind device addresses.  Two fronts on a
+    host-tier disk (tests/native/disk_tier_driver.c) encode in alternation;
+    every chunk and the counters equal the reference's local + connected pair.
+    (In this pytest process PyTorch's bundled HIP runtime is loaded, which has
+    no host-located virtual memory: test_shared_disk_tiers_vs_reference skips
+    its tier-1 case here.)"""
+    import struct
+    import subprocess
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    drv = os.path.join(HERE, 'native', 'disk_tier_driver')
+    if not os.path.exists(drv):
+        pytest.fail('tests/native/disk_tier_driver not built (__graft_entry__.build())')
+    limit, disk = 100 * SEG, mpg.disk_bytes(2)
+    da = synth.stream(0xA17, 2 << 20, 30, 0)
+    db = synth.stream(0xB27, 2 << 20, 30, 0)
+    pa_, pb_ = tmp_path / 'a.bin', tmp_path / 'b.bin'
+    pa_.write_bytes(da)
+    pb_.write_bytes(db)
+    outp = tmp_path / 'out.bin'
+    env = {k: v for k, v in os.environ.items() if k != 'LD_LIBRARY_PATH'}
+    r = subprocess.run([drv, str(pa_), str(pb_), str(outp), str(limit), str(disk), '1'], capture_output=True,
+                       text=True, timeout=120, env=env)
+    if r.returncode != 0 and 'host' in r.stderr.lower():
+        pytest.skip('this HIP runtime maps no host memory behind device addresses: ' + r.stderr.strip())
+    assert r.returncode == 0, r.stderr
+    blob = outp.read_bytes()
+    oa, la = synth.chunks_of(da, 65536)
+    ob, lb = synth.chunks_of(db, 65536)
+    pa = ref_oracle.cache_new_pair(limit, disk)
+    pb = ref_oracle.cache_connect(pa, _uuid(0x7157))
+    exp = []
+    for k in range(0, max(len(oa), len(ob)), 4):
+        if k < len(oa):
+            exp += ref_oracle.encode_batch(da, oa[k:k + 4], la[k:k + 4], mode=MODE_STREAM, cache=pa)
+        if k < len(ob):
+            exp += ref_oracle.encode_batch(db, ob[k:k + 4], lb[k:k + 4], mode=MODE_STREAM, cache=pb)
+    got, pos = [], 0
+    for _ in exp:
+        (n,) = struct.unpack_from('<Q', blob, pos)
+        got.append(blob[pos + 8:pos + 8 + n])
+        pos += 8 + n
+    st = struct.unpack_from('<12Qq', blob, pos)
+    assert pos + 13 * 8 == len(blob)
+    tier = st[12]
+    if tier != 1:
+        pytest.skip(f'the disk stayed in HBM (tier {tier}): this runtime maps no host memory behind device addresses')
+    for k, (a, b) in enumerate(zip(exp, got)):
+        assert a == b, k
+    est = [ref_oracle.pair_stats(pa, disk_live=True), ref_oracle.pair_stats(pb, disk_live=True)]
+    assert (st[1], st[2], st[8]) == est[0]
+    assert (st[5], st[6], st[8]) == est[1]
+    assert st[9] > 3 * 2 * 204, 'the shared disk never lapped'

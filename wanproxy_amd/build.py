@@ -68,6 +68,20 @@ def build_synth(force: bool = False) -> str:
     return SYNTH_OUT
 
 
+NATIVE_SRC = os.path.join(HERE, '..', 'tests', 'native', 'disk_tier_driver.c')
+NATIVE_OUT = os.path.join(HERE, '..', 'tests', 'native', 'disk_tier_driver')
+
+
+def build_native_tests(force: bool = False) -> str:
+    """C drivers of the ABI that GPU tests run in processes without PyTorch
+    (tests/native: test infrastructure, linked against the in-tree library)."""
+    if force or not _newer(NATIVE_OUT, [NATIVE_SRC, OUT]):
+        subprocess.run(['gcc', '-O2', '-Wall', '-o', NATIVE_OUT + '.tmp', NATIVE_SRC, '-L' + HERE, '-l:libxcgpu.so',
+                        '-Wl,-rpath,$ORIGIN/../../wanproxy_amd'], check=True)
+        os.replace(NATIVE_OUT + '.tmp', NATIVE_OUT)
+    return NATIVE_OUT
+
+
 if __name__ == '__main__':
     print(build_lib(force=True, verbose=True))
     print(build_synth(force=True))
