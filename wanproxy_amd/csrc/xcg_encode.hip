@@ -259,6 +259,15 @@ __device__ __forceinline__ uint3 window_hash_u(const uint8_t* w) {
 __device__ __forceinline__ bool equal2048_u(const uint8_t* a, const uint8_t* b) {
   return readfirst((uint32_t)wave_equal2048(a, b)) != 0u;
 }
+// The same compare when the window is a piece start: its bytes are the A
+// registers (lane l holds [32 l, 32 l + 32)), so only the other side is read.
+__device__ __forceinline__ bool equal2048_regs(const uint8_t* a, const u32x4& w0, const u32x4& w1) {
+  const uint32_t o = 32u * (uint32_t)lane_id();
+  const u32x4 v0 = *(const u32x4_u*)(a + o), v1 = *(const u32x4_u*)(a + o + 16);
+  const bool ok = v0[0] == w0[0] && v0[1] == w0[1] && v0[2] == w0[2] && v0[3] == w0[3] && v1[0] == w1[0] &&
+                  v1[1] == w1[1] && v1[2] == w1[2] && v1[3] == w1[3];
+  return ballot(!ok) == 0;
+}
 
 // ------------------------------------------------------------ vector phase
 
@@ -1135,7 +1144,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       // (straight to the exact tables after the LDS lane filter: a chain probe
       // hits often, and both tables cost one round trip together)
       if (src == nullptr && glb_pass(probe_key(lo))) src = cache_src(lo, hi, s);
-      if (src != nullptr && equal2048_u(src, x + s)) {
+      if (src != nullptr && (s == p ? equal2048_regs(src, P.a0, P.a1) : equal2048_u(src, x + s))) {
         wave_put_ref(out + olen, lo, hi);           // encode_reference :342-372
         olen += 10;
         ref_made();
@@ -1383,7 +1392,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
         // one or two windows and own-table false positives have not passed it)
         if (STREAM && src == nullptr && glb_pass(probe_key(lo))) src = cache_src(lo, hi, s);
         if (src != nullptr) {
-          if (equal2048_u(src, x + s)) {
+          if (s == p ? equal2048_regs(src, P.a0, P.a1) : equal2048_u(src, x + s)) {
             if (spec_cand >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // speculative body lands first
             if (s > base) olen += escape_u(out + olen, x, (uint32_t)base, (uint32_t)s);
             wave_put_ref(out + olen, lo, hi);                 // encode_reference :342-372
