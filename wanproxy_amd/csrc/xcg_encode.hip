@@ -1100,8 +1100,13 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     // this piece rolls (issued after every use of this piece's loads).
     nb_start = p + SEG;
     if (nb_start < last) {                         // (nb_start == last: decided as this piece's tail1 window)
-      nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
-      nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
+      if (p + 3 * SEG <= L) {                      // (uniform) every lane's 32 bytes inside the chunk: no guards
+        nb0 = *(const u32x4*)(x + q0 + 2 * SEG);
+        nb1 = *(const u32x4*)(x + q0 + 2 * SEG + 16);
+      } else {
+        nb0 = load16_aligned_safe(x, q0 + 2 * SEG, L);
+        nb1 = load16_aligned_safe(x, q0 + 2 * SEG + 16, L);
+      }
     }
 
     // ---- REF chaining (stream semantics).  The previous piece ended with a
