@@ -361,6 +361,11 @@ struct GlbQ {
 
 // Pass 2 over the queued keys of the current half; resets the queue.
 __device__ __forceinline__ void glb_flush(GlbQ& gq) {
+#ifdef XCG_EXP_NOPASS2   // (timing experiment only: output is wrong)
+  gq.pm = 0;
+  gq.sa = gq.sa0;
+  return;
+#endif
   const uint32_t cnt = (gq.sa - gq.sa0) >> 8;
   uint32_t rem = gq.pm;
 #pragma unroll
