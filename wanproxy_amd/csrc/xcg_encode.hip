@@ -699,21 +699,25 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   // Insert a declaration into the LDS table (XCodecMemoryCache::enter,
   // xcodec_cache.h:303-325) -- by lane 0, visible to later LDS reads of the
   // wave (LDS ops of one wave complete in order).
+  // (DM) enter into slot sl of the direct-mapped table, whose word s0 the
+  // caller has read
+  auto insert_dm = [&](uint32_t lo, uint32_t hi, uint32_t c, uint32_t k2, uint32_t sl, uint32_t s0) {
+    const uint32_t d = ndecl++, ke = dm_empty<LOGNB>(sl);
+    if (l == 0) {
+      T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
+      if (s0 == ke) keyt[sl] = k2;
+      else if (novf < (uint32_t)ovf_cap<MAXD, DM>()) T.ovf_k[novf] = k2;
+    }
+    if (s0 != ke) {
+      if (novf < (uint32_t)ovf_cap<MAXD, DM>()) ++novf;
+      else if (l == 0 && prm.status) atomicOr(prm.status, 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
   auto insert = [&](uint32_t lo, uint32_t hi, uint32_t c, uint32_t k2) {
     if (DM) {
-      const uint32_t d = ndecl++;
-      const uint32_t sl = (k2 >> 2) & ((2u << LOGNB) - 1u), ke = dm_empty<LOGNB>(sl);
-      const uint32_t s0 = readfirst(keyt[sl]);
-      if (l == 0) {
-        T.rlo[d] = lo; T.rhi[d] = hi; T.rc[d] = c;
-        if (s0 == ke) keyt[sl] = k2;
-        else if (novf < (uint32_t)ovf_cap<MAXD, DM>()) T.ovf_k[novf] = k2;
-      }
-      if (s0 != ke) {
-        if (novf < (uint32_t)ovf_cap<MAXD, DM>()) ++novf;
-        else if (l == 0 && prm.status) atomicOr(prm.status, 1);
-      }
-      __builtin_amdgcn_wave_barrier();
+      const uint32_t sl = (k2 >> 2) & ((2u << LOGNB) - 1u);
+      insert_dm(lo, hi, c, k2, sl, readfirst(keyt[sl]));
       return;
     }
     const uint32_t d = ndecl++;
@@ -1343,18 +1347,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
       spec_cand = s;
       spec_olen = olen;
       s = pe;
-      // insert (as insert() above, its slot already read)
-      const uint32_t d = ndecl++, ke = dm_empty<LOGNB>(sl), s0 = readfirst(s0v);
-      if (l == 0) {
-        T.rlo[d] = cand_lo; T.rhi[d] = cand_hi; T.rc[d] = (uint32_t)cand;
-        if (s0 == ke) keyt[sl] = k2;
-        else if (novf < (uint32_t)ovf_cap<MAXD, DM>()) T.ovf_k[novf] = k2;
-      }
-      if (s0 != ke) {
-        if (novf < (uint32_t)ovf_cap<MAXD, DM>()) ++novf;
-        else if (l == 0 && prm.status) atomicOr(prm.status, 1);
-      }
-      __builtin_amdgcn_wave_barrier();
+      insert_dm(cand_lo, cand_hi, (uint32_t)cand, k2, sl, readfirst(s0v));   // (its slot already read)
       c0_in_table = true;
     }
     while (s < pe_x) {
