@@ -1509,11 +1509,14 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
 #ifndef XCG_INDEP_LOGNB
 #define XCG_INDEP_LOGNB 10
 #endif
+#ifndef XCG_INDEP_W
+#define XCG_INDEP_W 4         // chunk-waves per workgroup
+#endif
 template <int LOGNB, int MAXD>
-__global__ __launch_bounds__(256, XCG_INDEP_OCC) void encode_independent_kernel(EncParams prm) {
-  __shared__ IndepLDS<LOGNB, MAXD, 4> S;
+__global__ __launch_bounds__(64 * XCG_INDEP_W, XCG_INDEP_OCC) void encode_independent_kernel(EncParams prm) {
+  __shared__ IndepLDS<LOGNB, MAXD, XCG_INDEP_W> S;
   const int wv = (int)readfirst(threadIdx.x >> 6);   // wave-uniform: keeps the parse state in SGPRs
-  const uint32_t chunk = blockIdx.x * 4u + (uint32_t)wv;
+  const uint32_t chunk = blockIdx.x * (uint32_t)XCG_INDEP_W + (uint32_t)wv;
   if (chunk >= prm.n) return;
   encode_chunk<LOGNB, MAXD, false>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk,
                                    GlbView{nullptr, 0u, 0u, 0, nullptr, nullptr});
@@ -1569,7 +1572,7 @@ extern "C" int xcg_launch_encode_independent(const uint8_t* d_in, const uint64_t
   if (n == 0) return 0;
   xcg::EncParams prm{d_in, d_chunk_off, d_chunk_len, n, flags, d_out, d_out_off, d_out_len, d_stats, d_status};
   prm.max_len = max_chunk_len;
-  dim3 grid((n + 3) / 4), block(256);
+  dim3 grid((n + XCG_INDEP_W - 1) / XCG_INDEP_W), block(64 * XCG_INDEP_W);
   if (max_chunk_len <= (1u << 17)) {
     hipLaunchKernelGGL((xcg::encode_independent_kernel<XCG_INDEP_LOGNB, 72>), grid, block, 0, stream, prm);
   } else if (max_chunk_len <= (1u << 19)) {
