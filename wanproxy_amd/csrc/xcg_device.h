@@ -108,5 +108,16 @@ __device__ __forceinline__ u32x4 load16_aligned_safe(const uint8_t* x, int q, in
   if (q > -16 && q < len) r = *(const u32x4*)(x + q);
   return r;
 }
+// The same as a streaming (non-temporal) load: a chunk's bytes are read once,
+// and marking them so keeps them from evicting the L2-resident probe tables
+// (lane filter, fingerprint buckets, hash tables) that every position reads.
+__device__ __forceinline__ u32x4 load16_stream(const uint8_t* p) {
+  return __builtin_nontemporal_load((const u32x4*)p);
+}
+__device__ __forceinline__ u32x4 load16_aligned_safe_stream(const uint8_t* x, int q, int len) {
+  u32x4 r = {0u, 0u, 0u, 0u};
+  if (q > -16 && q < len) r = load16_stream(x + q);
+  return r;
+}
 
 }  // namespace xcg
