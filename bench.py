@@ -41,7 +41,8 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-le
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks (one per GPU); without an outer launcher N > 1 starts N ranks itself')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--chunks', type=int, default=NCHUNKS)
@@ -629,10 +630,49 @@ def sharded_configs(world, rank, dev, backend='nccl'):
     return out
 
 
+def launch_plan(gpus, env):
+    """How this invocation runs: ('rank', world) -- one rank of an outer
+    launcher (torchrun sets WORLD_SIZE) or the only rank; ('spawn', N) -- no
+    outer launcher and --gpus N > 1: start N ranks as children.  An outer
+    launcher whose world differs from --gpus is an error (ValueError)."""
+    outer = env.get('WORLD_SIZE')
+    if outer is not None:
+        world = int(outer)
+        if gpus is not None and gpus != world:
+            raise ValueError(f'--gpus {gpus} under a launcher of WORLD_SIZE {world}')
+        return 'rank', world
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise ValueError(f'--gpus {n}')
+    return ('spawn', n) if n > 1 else ('rank', 1)
+
+
+def spawn_ranks(n, argv):
+    """--gpus N without an outer launcher: N ranks under torch.distributed.run
+    as a child process (this process never touches the GPU, and is not
+    replaced: the child's exit status is returned), rendezvous on 127.0.0.1."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    try:
+        how, world = launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        raise SystemExit(f'bench.py: {e}')
+    if how == 'spawn':
+        raise SystemExit(spawn_ranks(world, sys.argv[1:]))
     import torch
-    world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:

@@ -160,11 +160,34 @@ int xcg_disk_tier(const xcg_disk *disk);
  * fills).  Fronts find their entries again by UUID: xcg_ctx_create_pair_uuid
  * makes the front of a 36-character UUID string (XCodecDisk::connect: the
  * registered xuid, else the lowest free one, registered); the local front is
- * the first one made on a fresh volume (xuid 0). */
+ * the first one made on a fresh volume (xuid 0).  A front made without a UUID
+ * is XCodecDisk::local (:635-641): xuid 0 when the volume registered it and no
+ * front holds it, else the lowest free xuid under a generated UUID (on a fresh
+ * volume that is xuid 0, as registry_load's local UUID, :575-596).  A volume
+ * whose registry is empty gets a local UUID at open, as registry_load does.
+ * xcg_disk_save writes the data blocks whether or not any front is left. */
 int xcg_disk_open(const char *path, uint64_t disk_bytes, uint32_t flags, xcg_disk **out);
 int xcg_disk_save(xcg_disk *disk, const char *path);
 int xcg_ctx_create_pair_uuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,
                              const char *uuid36, xcg_ctx **out);
+/* The drop-in's disk (integration/xcgpu_binding.cc): the engine disk of a host
+ * XCodecDisk is read from the descriptor the host object keeps its volume open
+ * on (XCodecDisk::fd_, xcodec_cache_disk.h:38; the file as the host's reload
+ * left it, :107-237), with the reference's reload semantics; a descriptor of an
+ * empty file gives a fresh disk.  xcg_ctx_create_pair_xuid binds the front a
+ * host XCodecDiskCache already is (its xuid_, xcodec_cache_disk.h:106; uuid36
+ * its UUID, or NULL), so the engine's fronts are the host disk's whatever
+ * order they are bound in (xuid -1: as xcg_ctx_create_pair_uuid).  XCG_EINVAL
+ * when that xuid is held by another front or the UUID is registered at
+ * another xuid.  xcg_disk_head: the write head as XCodecDisk keeps it
+ * (current_index_block_, index_block_next_, :701-727) -- after a reload, the
+ * host object's and the engine's agree.  xcg_pair_xuid: a pair context's
+ * front. */
+int xcg_disk_open_fd(int fd, uint64_t disk_bytes, uint32_t flags, xcg_disk **out);
+int xcg_ctx_create_pair_xuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,
+                             const char *uuid36, int xuid, xcg_ctx **out);
+int xcg_disk_head(const xcg_disk *disk, uint64_t *index_block, uint64_t *next_entry);
+int xcg_pair_xuid(const xcg_ctx *ctx);
 void xcg_disk_destroy(xcg_disk *disk);
 int xcg_disk_stats(const xcg_disk *disk, uint64_t *st);
 int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,

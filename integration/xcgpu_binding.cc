@@ -15,6 +15,7 @@
  * pair (xcodec/xcodec_pipe_pair.cc:203) gets its caches that way.
  */
 #include <string.h>
+#include <unistd.h>
 
 #include <map>
 #include <string>
@@ -57,12 +58,32 @@ struct DiskBlocks {
 	typedef uint64_t XCodecDisk::*type;
 	friend type member_of(DiskBlocks);
 };
+struct DiskFd {
+	typedef int XCodecDisk::*type;
+	friend type member_of(DiskFd);
+};
+struct DiskHeadBlock {
+	typedef uint64_t XCodecDisk::*type;
+	friend type member_of(DiskHeadBlock);
+};
+struct DiskHeadNext {
+	typedef size_t XCodecDisk::*type;
+	friend type member_of(DiskHeadNext);
+};
+struct FrontXuid {
+	typedef uint16_t XCodecDiskCache::*type;
+	friend type member_of(FrontXuid);
+};
 
 template struct Member<MemoryLimit, &XCodecMemoryCache::memory_cache_limit_>;
 template struct Member<PairPrimary, &XCodecCachePair::primary_>;
 template struct Member<PairSecondary, &XCodecCachePair::secondary_>;
 template struct Member<DiskOf, &XCodecDiskCache::disk_>;
 template struct Member<DiskBlocks, &XCodecDisk::disk_blocks_>;
+template struct Member<DiskFd, &XCodecDisk::fd_>;
+template struct Member<DiskHeadBlock, &XCodecDisk::current_index_block_>;
+template struct Member<DiskHeadNext, &XCodecDisk::index_block_next_>;
+template struct Member<FrontXuid, &XCodecDiskCache::xuid_>;
 
 xcgpu_binding::DiskResolver& resolver()
 {
@@ -91,18 +112,65 @@ std::map<const void *, xcg_disk *>& disk_map()
 	return disks;
 }
 
-/* The XCodecDisk under a disk level, and its volume size. */
-bool disk_of(XCodecCache *level, const void **disk, uint64_t *bytes)
+/* The XCodecDisk under a disk level, its volume size and the front's xuid and
+ * UUID; with want_volume also the descriptor the XCodecDisk keeps its volume
+ * open on (XCodecDisk::open, xcodec_cache_disk.cc:840-871) and its write
+ * head. */
+bool disk_of(XCodecCache *level, xcgpu_binding::DiskInfo *info, bool want_volume)
 {
-	if (resolver() != NULL && resolver()(level, disk, bytes))
+	if (resolver() != NULL && resolver()(level, info, want_volume))
 		return true;
 	XCodecDiskCache *front = dynamic_cast<XCodecDiskCache *>(level);
 	if (front == NULL)
 		return false;
 	XCodecDisk *d = front->*member_of(DiskOf());
-	*disk = d;
-	*bytes = (d->*member_of(DiskBlocks())) * (uint64_t)XCG_SEGMENT_LENGTH;
+	info->disk = d;
+	info->bytes = (d->*member_of(DiskBlocks())) * (uint64_t)XCG_SEGMENT_LENGTH;
+	info->xuid = front->*member_of(FrontXuid());
+	info->uuid = front->get_uuid().string_;
+	if (want_volume) {
+		info->fd = d->*member_of(DiskFd());
+		info->close_fd = false;
+		info->head_known = true;
+		info->head_block = d->*member_of(DiskHeadBlock());
+		info->head_next = d->*member_of(DiskHeadNext());
+	}
 	return true;
+}
+
+/* The engine disk under a pair's disk level: one per XCodecDisk, read from the
+ * volume the host object reloaded (XCodecDisk::XCodecDisk,
+ * xcodec_cache_disk.cc:107-237 -- the engine applies the same reload to the
+ * same file, so both start from the same index, registry and write head). */
+int engine_disk(XCodecCache *level, const xcgpu_binding::DiskInfo& g, xcg_disk **out, std::string *why)
+{
+	xcg_disk *&disk = disk_map()[g.disk];
+	if (disk != NULL) {
+		*out = disk;
+		return XCG_OK;
+	}
+	xcgpu_binding::DiskInfo v;
+	if (!disk_of(level, &v, true))
+		return XCG_EINVAL;
+	int rc = v.fd >= 0 ? xcg_disk_open_fd(v.fd, v.bytes, 0, &disk) : xcg_disk_create(v.bytes, &disk);
+	if (v.close_fd && v.fd >= 0)
+		close(v.fd);
+	if (rc != XCG_OK) {
+		disk = NULL;
+		return rc;
+	}
+	uint64_t hb = 0, hn = 0;
+	if (v.head_known && (xcg_disk_head(disk, &hb, &hn) != XCG_OK || hb != v.head_block || hn != v.head_next)) {
+		*why = "the disk volume's reload put the engine's write head at index block " + std::to_string(hb) +
+		       " entry " + std::to_string(hn) + ", the host XCodecDisk's is at " + std::to_string(v.head_block) +
+		       " entry " + std::to_string(v.head_next) + " (the host disk was written to before its first pair "
+		       "reached the engine)";
+		xcg_disk_destroy(disk);
+		disk = NULL;
+		return XCG_EINVAL;
+	}
+	*out = disk;
+	return XCG_OK;
 }
 
 }  // namespace
@@ -116,7 +184,10 @@ void set_disk_resolver(DiskResolver fn)
 
 Geometry geometry_of(XCodecCache *cache)
 {
-	Geometry g = { KIND_UNSUPPORTED, 0, NULL, 0, "a cache class the MI355X engine does not mirror" };
+	Geometry g;
+	g.kind = KIND_UNSUPPORTED;
+	g.limit_bytes = 0;
+	g.why = "a cache class the MI355X engine does not mirror";
 	if (strstr(typeid(*cache).name(), "NullCache") != NULL) {
 		g.kind = KIND_NULL;
 		return g;
@@ -137,7 +208,7 @@ Geometry geometry_of(XCodecCache *cache)
 		return g;
 	}
 	const size_t limit = primary->*member_of(MemoryLimit());
-	if (!disk_of(p->*member_of(PairSecondary()), &g.disk, &g.disk_bytes)) {
+	if (!disk_of(p->*member_of(PairSecondary()), &g.disk, false)) {
 		g.why = "an XCodecCachePair whose secondary is not a disk cache";
 		return g;
 	}
@@ -176,6 +247,7 @@ xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 	if (dev != NULL)
 		device = atoi(dev);
 	xcg_ctx *ctx = NULL;
+	std::string why;
 	int rc;
 	switch (g.kind) {
 	case KIND_NULL:
@@ -185,12 +257,15 @@ xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 		rc = xcg_ctx_create_bounded(device, flags, g.limit_bytes, &ctx);
 		break;
 	case KIND_PAIR: {
-		xcg_disk *&disk = disk_map()[g.disk];
-		rc = XCG_OK;
-		if (disk == NULL)
-			rc = xcg_disk_create(g.disk_bytes, &disk);
+		/* the pair's disk level is the host front of xuid g.disk.xuid: the
+		 * engine binds the same front of the same (reloaded) disk */
+		XCodecCache *level = dynamic_cast<XCodecCachePair *>(cache)->*member_of(PairSecondary());
+		xcg_disk *disk = NULL;
+		rc = engine_disk(level, g.disk, &disk, &why);
 		if (rc == XCG_OK)
-			rc = xcg_ctx_create_pair_on(device, flags, g.limit_bytes, disk, &ctx);
+			rc = xcg_ctx_create_pair_xuid(device, flags, g.limit_bytes, disk,
+			                              g.disk.uuid.length() == 36 ? g.disk.uuid.c_str() : NULL, g.disk.xuid,
+			                              &ctx);
 		break;
 	}
 	default:
@@ -198,8 +273,8 @@ xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 		break;
 	}
 	if (rc != XCG_OK) {
-		refusals()[cache] = std::string("MI355X engine: ") + xcg_strerror(rc) + " (XCGPU_DEVICE " +
-		                    std::to_string(device) + ")";
+		refusals()[cache] = std::string("MI355X engine: ") + (why.empty() ? xcg_strerror(rc) : why.c_str()) +
+		                    " (XCGPU_DEVICE " + std::to_string(device) + ")";
 		return NULL;
 	}
 	ctx_map()[cache] = ctx;

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <map>
+#include <string>
 
 #include "../include/xcgpu.h"
 
@@ -47,11 +48,26 @@ enum CacheKind {
 	KIND_PAIR		/* XCodecCachePair(bounded memory, disk front-end) (:140-237) */
 };
 
+/* The disk level of a pair: the XCodecDisk under it and which front it is. */
+struct DiskInfo {
+	const void *disk;	/* identity of the XCodecDisk under the disk level */
+	uint64_t bytes;		/* its volume size */
+	int xuid;		/* the front's xuid on it (XCodecDiskCache::xuid_), -1 unknown */
+	std::string uuid;	/* the front's UUID (XCodecCache::get_uuid) */
+	/* asked for only when the engine disk is made (want_volume): */
+	int fd;			/* the volume's descriptor (XCodecDisk::fd_), -1 none: a fresh disk */
+	bool close_fd;		/* the resolver opened fd for this call: the binding closes it */
+	bool head_known;	/* the host disk's write head (current_index_block_, index_block_next_) */
+	uint64_t head_block, head_next;
+
+	DiskInfo() : disk(NULL), bytes(0), xuid(-1), uuid(), fd(-1), close_fd(false), head_known(false),
+	             head_block(0), head_next(0) { }
+};
+
 struct Geometry {
 	CacheKind kind;
 	uint64_t limit_bytes;	/* the memory (primary) limit, bytes */
-	const void *disk;	/* KIND_PAIR: identity of the XCodecDisk under the disk level */
-	uint64_t disk_bytes;	/* its volume size */
+	DiskInfo disk;		/* KIND_PAIR: the disk level */
 	const char *why;	/* KIND_UNSUPPORTED: what is not mirrored */
 };
 
@@ -59,10 +75,12 @@ Geometry geometry_of(XCodecCache *cache);
 
 /*
  * A disk level class other than XCodecDiskCache (e.g. a test harness's
- * restatement of XCodecDisk) can be resolved to its disk identity and size by
- * a resolver; return false for objects it does not know.
+ * restatement of XCodecDisk) can be resolved to its disk by a resolver; return
+ * false for objects it does not know.  With want_volume it also gives a
+ * descriptor its volume file can be read from, as the file stands now, and the
+ * host disk's write head.
  */
-typedef bool (*DiskResolver)(XCodecCache *level, const void **disk, uint64_t *disk_bytes);
+typedef bool (*DiskResolver)(XCodecCache *level, DiskInfo *info, bool want_volume);
 void set_disk_resolver(DiskResolver fn);
 
 /* The GPU mirror of `cache`, created on first use; NULL if it cannot be made

@@ -20,6 +20,7 @@
 #include <ctype.h>
 #include <fcntl.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -83,6 +84,7 @@ public:
 	uint64_t entries(void) const { return index_.size(); }
 	uint64_t written(void) const;
 	RefDisk *disk(void) const { return disk_; }
+	uint16_t xuid(void) const { return xuid_; }
 };
 
 /*
@@ -173,6 +175,31 @@ public:
 		int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0600);
 		if (fd == -1)
 			return false;
+		bool ok = save_fd(fd);
+		close(fd);
+		return ok;
+	}
+
+	/* The volume file as it stands now, in an anonymous file (the descriptor
+	 * the reference's XCodecDisk keeps as fd_). */
+	int image_fd(void) const
+	{
+		int fd = memfd_create("refdisk", 0);
+		if (fd == -1)
+			return -1;
+		if (!save_fd(fd)) {
+			close(fd);
+			return -1;
+		}
+		return fd;
+	}
+
+	/* The write head (current_index_block_, index_block_next_). */
+	uint64_t head_block(void) const { return (clock_ / 204) % nb_; }
+	uint64_t head_next(void) const { return clock_ % 204; }
+
+	bool save_fd(int fd) const
+	{
 		bool ok = ftruncate(fd, (off_t)bytes_) == 0;
 		ok = ok && pwrite(fd, &reg_[0], reg_.size(), 0) == (ssize_t)reg_.size();
 		std::vector<uint8_t> ib(2048);
@@ -190,7 +217,6 @@ public:
 			ok = pwrite(fd, &ib[0], 2048, (off_t)((REG_BLOCKS + b) * 2048)) == 2048;
 		}
 		ok = ok && pwrite(fd, &data_[0], data_.size(), (off_t)((REG_BLOCKS + nb_) * 2048)) == (ssize_t)data_.size();
-		close(fd);
 		return ok;
 	}
 
@@ -434,14 +460,28 @@ static const bool segv_trace_set = getenv("XCG_SEGV_TRACE") != NULL &&
     (signal(SIGSEGV, segv_trace), signal(SIGABRT, segv_trace), true);
 
 /* The binding finds the XCodecDisk under an XCodecDiskCache by itself; this
- * harness's restated disk level is resolved here. */
-static bool ref_disk_resolver(XCodecCache *level, const void **disk, uint64_t *bytes)
+ * harness's restated disk level is resolved here: the front's xuid and UUID,
+ * and -- when the engine disk is made -- the volume file as it stands now (the
+ * reference's XCodecDisk has it on disk, written block by block; RefDisk keeps
+ * it in memory and writes the same image) and the write head. */
+static bool ref_disk_resolver(XCodecCache *level, xcgpu_binding::DiskInfo *info, bool want_volume)
 {
 	RefDiskCache *front = dynamic_cast<RefDiskCache *>(level);
 	if (front == NULL)
 		return false;
-	*disk = front->disk();
-	*bytes = front->disk()->bytes_;
+	info->disk = front->disk();
+	info->bytes = front->disk()->bytes_;
+	info->xuid = front->xuid();
+	info->uuid = front->get_uuid().string_;
+	if (want_volume) {
+		info->fd = front->disk()->image_fd();
+		info->close_fd = true;
+		info->head_known = true;
+		info->head_block = front->disk()->head_block();
+		info->head_next = front->disk()->head_next();
+		if (info->fd == -1)
+			return false;
+	}
 	return true;
 }
 static const bool ref_disk_resolver_set = (xcgpu_binding::set_disk_resolver(ref_disk_resolver), true);

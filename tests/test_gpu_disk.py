@@ -222,3 +222,104 @@ def test_host_tier_in_a_process_without_torch(ref_oracle, tmp_path):
     assert (st[1], st[2], st[8]) == est[0]
     assert (st[5], st[6], st[8]) == est[1]
     assert st[9] > 3 * 2 * 204, 'the shared disk never lapped'
+
+
+def test_volume_saved_after_its_fronts_are_gone(ref_oracle, tmp_path):
+    """Shutdown order: the contexts close first, then the disk is saved.  The
+    data blocks come from the disk's own allocation, so the volume equals the
+    one saved while the fronts were open (and the reference's), and a reopen
+    REFs what the first run declared."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, Disk
+    limit, disk = 40 * SEG, mpg.disk_bytes(4)
+    local = _uuid(0x5A7E)
+    d, parts = _vol_case(0x5A7, 2)
+    vref = str(tmp_path / 'ref.vol')
+    pa = ref_oracle.cache_open_pair(limit, disk, vref, local)
+    for o, l in parts[:1]:
+        ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa)
+    ref_oracle.disk_save(pa, vref)
+    K = Disk(disk)
+    ca = Context(0, memory_cache_limit=limit, disk=K, uuid=local)
+    for o, l in parts[:1]:
+        ca.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM)
+    open_ = str(tmp_path / 'open.vol')
+    K.save(open_)
+    ca.close()
+    closed = str(tmp_path / 'closed.vol')
+    K.save(closed)
+    K.close()
+    a, b, c = (open(p, 'rb').read() for p in (vref, open_, closed))
+    assert b == c, 'the volume saved after the front closed lost its data blocks'
+    assert a == b
+    K2 = Disk(disk, path=closed)
+    c2 = Context(0, memory_cache_limit=limit, disk=K2, uuid=local)
+    got = [c2.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts[:1]]
+    c2.close()
+    K2.close()
+    pa2 = ref_oracle.cache_open_pair(limit, disk, vref, _uuid(0x999))
+    exp = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa2) for o, l in parts[:1]]
+    assert got == exp
+    assert sum(map(len, got[0])) < sum(l for l in parts[0][1]) // 2
+
+
+def test_volume_of_a_front_without_uuid(ref_oracle, tmp_path):
+    """A front made without a UUID is XCodecDisk::local: on a fresh volume it
+    registers a generated local UUID at xuid 0 (registry_load,
+    xcodec_cache_disk.cc:575-596), so a saved and reopened volume keeps its
+    entries, and a front made without a UUID on the reopened volume is xuid 0
+    again (local()) and finds them -- as the reference's local front does."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, Disk
+    limit, disk = 40 * SEG, mpg.disk_bytes(5)
+    d, parts = _vol_case(0x10C, 2)
+    vgpu = str(tmp_path / 'gpu.vol')
+    K = Disk(disk)
+    c = Context(0, memory_cache_limit=limit, disk=K)
+    assert c.xuid() == 0
+    got1 = [c.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts[:1]]
+    c.close()
+    K.save(vgpu)
+    K.close()
+    reg = open(vgpu, 'rb').read(36)
+    assert reg[8:9] == b'-' and reg[14:15] == b'4', reg           # a version-4 UUID string at xuid 0
+    K2 = Disk(disk, path=vgpu)
+    assert K2.head()[1] == 0                                       # (a reload starts an index block)
+    c2 = Context(0, memory_cache_limit=limit, disk=K2)
+    assert c2.xuid() == 0
+    got2 = [c2.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts]
+    c3 = Context(0, memory_cache_limit=limit, disk=K2)              # a second unnamed front: a new xuid
+    assert c3.xuid() == 1
+    c3.close()
+    c2.close()
+    K2.close()
+    # the reference: the local front under the UUID the engine generated
+    vref = str(tmp_path / 'ref.vol')
+    pa = ref_oracle.cache_open_pair(limit, disk, vref, reg.decode())
+    exp1 = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa) for o, l in parts[:1]]
+    ref_oracle.disk_save(pa, vref)
+    assert open(vref, 'rb').read() == open(vgpu, 'rb').read()
+    pa2 = ref_oracle.cache_open_pair(limit, disk, vref, _uuid(0x998))
+    exp2 = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa2) for o, l in parts]
+    assert got1 == exp1 and got2 == exp2
+
+
+def test_front_by_xuid(tmp_path):
+    """xcg_ctx_create_pair_xuid binds the front a host XCodecDiskCache already
+    is (the drop-in's disks): that xuid, whatever order fronts bind in; a UUID
+    registered at another xuid, or a held xuid, is refused."""
+    from wanproxy_amd.xcgpu import XCGError, Context, Disk
+    limit, disk = 40 * SEG, mpg.disk_bytes(2)
+    K = Disk(disk)
+    c3 = Context(0, memory_cache_limit=limit, disk=K, uuid=_uuid(3), xuid=3)
+    c0 = Context(0, memory_cache_limit=limit, disk=K, xuid=0)
+    assert (c3.xuid(), c0.xuid()) == (3, 0)
+    with pytest.raises(XCGError):
+        Context(0, memory_cache_limit=limit, disk=K, uuid=_uuid(3), xuid=4)
+    with pytest.raises(XCGError):
+        Context(0, memory_cache_limit=limit, disk=K, uuid=_uuid(5), xuid=3)
+    c1 = Context(0, memory_cache_limit=limit, disk=K, uuid=_uuid(7))   # connect: the lowest free xuid
+    assert c1.xuid() == 1
+    for c in (c3, c0, c1):
+        c.close()
+    K.close()

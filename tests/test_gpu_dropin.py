@@ -109,6 +109,71 @@ def test_dropin_refmap_bounded_and_pair_like_reference(dropin, ref_oracle, kind)
         assert a == b, (kind, k)
 
 
+def _uuid(k):
+    return '%08x-0000-4000-8000-%012x' % (os.getpid() & 0xFFFFFFFF, k)
+
+
+@pytest.mark.parametrize('nb', [3, 10])
+def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path, nb):
+    """wanproxy restarted on its cache volume (XCodecDisk::open,
+    xcodec_cache_disk.cc:826-871): the first process encodes through the
+    drop-in on a pair over the volume (the local front and a peer's), the
+    volume is written and the caches go away; a second process opens the same
+    file -- the host XCodecDisk reloads it (:107-237) and the engine's disk is
+    read from the same file with the same reload -- and encodes on through the
+    local front and the peer's front, found again by UUID.  Every call's output
+    and refmap, the disk counters and the volume written by each process equal
+    the reference's.  A fresh engine disk would not do: the second process REFs
+    segments only the first declared."""
+    from wanproxy_amd import synth
+    limit, disk = 40 * 2048, (18 + nb * 205) * 2048
+    local, peer = _uuid(0x300 + nb), _uuid(0x400 + nb)
+    d = synth.stream(0x5E1 + nb, 9 << 20, 25, 0)
+    e = synth.stream(0x6E1 + nb, 6 << 20, 25, 0)
+    calls = lambda x, a, b: [x[k:k + 65536] for k in range(a << 20, b << 20, 65536)]
+
+    def run(o, tag):
+        vol = str(tmp_path / f'{tag}.vol')
+        out = []
+        pa = o.cache_open_pair(limit, disk, vol, local)
+        pb = o.cache_pair_front(pa, peer, limit)
+        ea, eb = o.encoder_new(pa), o.encoder_new(pb)
+        out += [o.encode_refmap(eb, p) for p in calls(e, 0, 3)]
+        out += [o.encode_refmap(ea, p) for p in calls(d, 0, 6)]
+        out.append(o.pair_stats(pa, disk_live=True))
+        o.disk_save(pa, vol)
+        first = open(vol, 'rb').read()
+        o.encoder_free(ea)
+        o.encoder_free(eb)
+        o.cache_free(pb)
+        o.cache_free(pa)
+        # the restart: a new process's XCodecDisk on the same file
+        pa2 = o.cache_open_pair(limit, disk, vol, _uuid(0x999))
+        pb2 = o.cache_pair_front(pa2, peer, limit)
+        ea2, eb2 = o.encoder_new(pa2), o.encoder_new(pb2)
+        second = [o.encode_refmap(ea2, p) for p in calls(d, 3, 9)]
+        second += [o.encode_refmap(eb2, p) for p in calls(e, 3, 6)]
+        second += [(o.pair_stats(pa2, disk_live=True), o.pair_stats(pb2, disk_live=True))]
+        o.disk_save(pa2, vol)
+        o.encoder_free(ea2)
+        o.encoder_free(eb2)
+        return out, first, second, open(vol, 'rb').read()
+
+    ref, gpu = run(ref_oracle, 'ref'), run(dropin, 'gpu')
+    for k, (a, b) in enumerate(zip(ref[0], gpu[0])):
+        assert a == b, ('first process', k)
+    assert ref[1] == gpu[1], 'the first process left a different volume'
+    for k, (a, b) in enumerate(zip(ref[2], gpu[2])):
+        assert a == b, ('after the reopen', k)
+    assert ref[3] == gpu[3], 'the second process left a different volume'
+    # the reload made a difference: on a fresh volume the same calls declare more
+    pf = ref_oracle.cache_new_pair(limit, disk)
+    ef = ref_oracle.encoder_new(pf)
+    fresh = [ref_oracle.encode_refmap(ef, p)[0] for p in calls(d, 3, 9)]
+    ref_oracle.encoder_free(ef)
+    assert sum(map(len, fresh)) > sum(len(r[0]) for r in ref[2][:len(fresh)]) + 20 * 2048
+
+
 def test_dropin_decode_bounded_like_reference(dropin, ref_oracle):
     """One persistent decoder on a bounded cache, frame by frame (the REF
     lookups refresh its LRU: the adapter replays them into the host cache)."""
@@ -127,3 +192,33 @@ def test_dropin_decode_bounded_like_reference(dropin, ref_oracle):
         o.decoder_free(dec)
         o.cache_free(dc)
     assert res[0] == res[1]
+
+
+@pytest.mark.parametrize('shift', [0, -1, 1, -2050, 8])
+def test_dropin_decode_op_at_the_piece_cut(dropin, ref_oracle, shift):
+    """A decode() of more than 1 MiB on a bounded cache is cut into pieces of
+    whole ops (integration/xcodec_decoder_xcgpu.cc cut_pieces).  An EXTRACT
+    whose payload ends in 0xF1 placed to end exactly at the 1 MiB cut (and
+    around it): the cut must not take the payload's last 0xF1 for an op start.
+    Output, consumed bytes and ASK set equal the reference decoder's."""
+    import random
+    r = random.Random(0xC07 + shift)
+    seg = bytearray(r.getrandbits(8) for _ in range(2048))
+    for k in range(0, 2048, 97):
+        seg[k] = 0xF1
+    seg[-1] = 0xF1
+    seg = bytes(seg)
+    h = ref_oracle.hash(seg)
+    lit = lambda n: bytes(r.randrange(0xF1) for _ in range(n))
+    ext = b'\xf1\x01' + seg
+    pre = (1 << 20) + shift - len(ext)
+    stream = lit(pre) + ext + b'\xf1\x02' + h.to_bytes(8, 'big') + lit(3000) + b'\xf1\x00' + lit(7) + ext + lit(100)
+    res = []
+    for o in (ref_oracle, dropin):
+        c = o.cache_new(300 * 2048)
+        dec = o.decoder_new(c)
+        res.append(o.decode(stream, c, decoder=dec))
+        o.decoder_free(dec)
+        o.cache_free(c)
+    assert res[0] == res[1]
+    assert res[0][0] and res[0][2] == len(stream) and res[0][1].count(seg) == 3

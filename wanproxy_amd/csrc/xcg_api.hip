@@ -590,6 +590,26 @@ int xcg_disk_open(const char* path, uint64_t disk_bytes, uint32_t flags, xcg_dis
   return XCG_OK;
 }
 
+int xcg_disk_open_fd(int fd, uint64_t disk_bytes, uint32_t flags, xcg_disk** out) {
+  if (!out || fd < 0 || (flags & ~(XCG_DISK_HOST | XCG_DISK_DEVICE)) ||
+      flags == (XCG_DISK_HOST | XCG_DISK_DEVICE))
+    return XCG_EINVAL;
+  *out = nullptr;
+  XcgDiskState* K = nullptr;
+  const int rc = xcg_disk_state_open_fd(fd, disk_bytes, flags, &K);
+  if (rc) return rc == -22 ? XCG_EINVAL : (rc == -2 ? XCG_ENOENT : XCG_ENOMEM);
+  *out = (xcg_disk*)K;
+  return XCG_OK;
+}
+
+int xcg_disk_head(const xcg_disk* d, uint64_t* index_block, uint64_t* next_entry) {
+  if (!d || !index_block || !next_entry) return XCG_EINVAL;
+  xcg_disk_state_head((const XcgDiskState*)d, index_block, next_entry);
+  return XCG_OK;
+}
+
+int xcg_pair_xuid(const xcg_ctx* c) { return c && c->pair ? (int)xcg_pair_state_xuid(c->pair) : XCG_EINVAL; }
+
 int xcg_disk_save(xcg_disk* d, const char* path) {
   if (!d || !path) return XCG_EINVAL;
   const int rc = xcg_disk_state_save((XcgDiskState*)d, path);
@@ -611,7 +631,12 @@ int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_lim
 
 int xcg_ctx_create_pair_uuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk* disk,
                              const char* uuid36, xcg_ctx** out) {
-  if (!out || !disk || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)))
+  return xcg_ctx_create_pair_xuid(device, flags, memory_cache_limit_bytes, disk, uuid36, -1, out);
+}
+
+int xcg_ctx_create_pair_xuid(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk* disk,
+                             const char* uuid36, int xuid, xcg_ctx** out) {
+  if (!out || !disk || memory_cache_limit_bytes == 0 || (flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) || xuid < -1)
     return XCG_EINVAL;
   *out = nullptr;
   uint64_t C = memory_cache_limit_bytes / XCG_SEGMENT_LENGTH;   // xcodec_cache.h:283-287
@@ -622,7 +647,7 @@ int xcg_ctx_create_pair_uuid(int device, uint32_t flags, uint64_t memory_cache_l
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XCG_EINVAL;
     DeviceGuard g(device);
-    const int prc = xcg_pair_state_create((uint32_t)C, (XcgDiskState*)disk, uuid36, &P);
+    const int prc = xcg_pair_state_create((uint32_t)C, (XcgDiskState*)disk, uuid36, xuid, &P);
     if (prc == -22) return XCG_EINVAL;
     if (prc) return XCG_ENOMEM;
   }

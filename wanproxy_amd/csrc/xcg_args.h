@@ -179,9 +179,13 @@ extern "C" int xcg_disk_state_create(uint64_t disk_bytes, uint32_t flags, XcgDis
 extern "C" int xcg_disk_state_tier(const XcgDiskState* K);
 extern "C" void xcg_disk_state_release(XcgDiskState* K);
 extern "C" void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st);
-extern "C" int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, XcgPairState** out);
+extern "C" int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, int want_xuid,
+                                     XcgPairState** out);
 extern "C" int xcg_disk_state_save(XcgDiskState* K, const char* path);
 extern "C" int xcg_disk_state_open(const char* path, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out);
+extern "C" int xcg_disk_state_open_fd(int fd, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out);
+extern "C" void xcg_disk_state_head(const XcgDiskState* K, uint64_t* index_block, uint64_t* next);
+extern "C" uint32_t xcg_pair_state_xuid(const XcgPairState* P);
 extern "C" void xcg_pair_state_destroy(XcgPairState* P);
 extern "C" int xcg_pair_state_clear(XcgPairState* P);
 extern "C" void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st);

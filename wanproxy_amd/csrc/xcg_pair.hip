@@ -71,6 +71,7 @@
 #include <string.h>
 
 #include <ctype.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -1000,6 +1001,9 @@ struct XcgDiskState {
   std::vector<uint64_t> h_key, h_ent;
   std::vector<uint32_t> h_xuid;
   std::vector<uint8_t> h_data;
+  // without HIP virtual memory every front has its own copy of the blocks: a
+  // front that goes away leaves the blocks it wrote here (shadow_ok: per block)
+  std::vector<uint8_t> shadow, shadow_ok;
   int refs = 1;                    // the creator's reference + one per front
 };
 
@@ -1608,8 +1612,64 @@ bool uuid_ok(const uint8_t* u) {
 // head's entry 0 is clock 204 * (nb + head), and a block b loaded from the last
 // lap holds entries numbered from 204 * (nb + head - ((head - b) mod nb)): each
 // dies when the head reaches b again, as the reference invalidates it.
-int load_volume(XcgDiskState* K, const std::vector<uint8_t>& vol) {
+//
+// Whole-range file I/O: one read()/write() moves at most 0x7ffff000 bytes on
+// Linux, so a volume past 2 GiB takes several.  A read that meets the end of
+// the file leaves the rest zero (the reference's ftruncate'd volume reads as
+// zeros there, xcodec_cache_disk.cc:853-860).
+bool pread_all(int fd, uint8_t* p, size_t n, off_t off) {
+  while (n > 0) {
+    const ssize_t r = pread(fd, p, n, off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r < 0) return false;
+    if (r == 0) {
+      memset(p, 0, n);
+      return true;
+    }
+    p += r;
+    n -= (size_t)r;
+    off += r;
+  }
+  return true;
+}
+
+bool pwrite_all(int fd, const uint8_t* p, size_t n, off_t off) {
+  while (n > 0) {
+    const ssize_t r = pwrite(fd, p, n, off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    n -= (size_t)r;
+    off += r;
+  }
+  return true;
+}
+
+// UUID::generate (common/uuid/uuid_libuuid.cc: uuid_generate + uuid_unparse):
+// a random (version 4) UUID in its 36-character lower-case form.
+bool gen_uuid(char out[37]) {
+  uint8_t b[16];
+  const int fd = ::open("/dev/urandom", O_RDONLY);
+  const bool ok = fd != -1 && pread_all(fd, b, 16, 0);
+  if (fd != -1) close(fd);
+  if (!ok) return false;
+  b[6] = (uint8_t)((b[6] & 0x0F) | 0x40);
+  b[8] = (uint8_t)((b[8] & 0x3F) | 0x80);
+  snprintf(out, 37, "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", b[0], b[1], b[2], b[3],
+           b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12], b[13], b[14], b[15]);
+  return true;
+}
+
+int load_volume(XcgDiskState* K, int fd) {
   const uint64_t nb = K->nb, D = K->D;
+  // the registry and index blocks; the data blocks go straight to h_data
+  std::vector<uint8_t> vol((REG_BLOCKS + nb) * 2048);
+  K->h_data.assign((size_t)D * SEG, 0);
+  if (!pread_all(fd, vol.data(), vol.size(), 0) ||
+      !pread_all(fd, K->h_data.data(), K->h_data.size(), (off_t)vol.size())) {
+    std::vector<uint8_t>().swap(K->h_data);
+    return -2;
+  }
   memcpy(&K->reg[0], &vol[0], K->reg.size());
   std::unordered_map<std::string, uint32_t> seen;
   for (uint32_t x = 0; x < REG_BLOCKS * REG_ENTRIES && x < XUIDS; ++x) {
@@ -1621,6 +1681,12 @@ int load_volume(XcgDiskState* K, const std::vector<uint8_t>& vol) {
     if (seen.count(us)) continue;
     seen[us] = x;
     K->uuid[x] = us;
+  }
+  if (seen.empty()) {                                       // registry_load: a local UUID (:575-596)
+    char u[37];
+    if (!gen_uuid(u)) return -2;
+    K->uuid[0] = std::string(u, 36);
+    registry_write(K, 0, u);
   }
   std::map<uint64_t, uint64_t> cmap;
   uint64_t ibc = 0;
@@ -1642,8 +1708,6 @@ int load_volume(XcgDiskState* K, const std::vector<uint8_t>& vol) {
   K->h_key.assign(D, NOKEY);
   K->h_ent.assign(D, NOENT);
   K->h_xuid.assign(D, 0xFFFFFFFFu);
-  K->h_data.assign((size_t)D * SEG, 0);
-  memcpy(&K->h_data[0], &vol[(REG_BLOCKS + nb) * 2048], (size_t)D * SEG);
   for (uint64_t o = 0; o < nb; ++o) {
     memcpy(&K->ctr[o], &vol[(REG_BLOCKS + o) * 2048], 8);
     const uint8_t* q = &vol[(REG_BLOCKS + o) * 2048 + 8];
@@ -1760,33 +1824,47 @@ void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
   st[3] = fronts;
 }
 
-// A pair front on disk K (XCodecDisk::local for the first, ::connect for the
-// others: the lowest free xuid, xcodec_cache_disk.cc:640-690), on the current
-// device.
-int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, XcgPairState** out) {
+// A pair front on disk K, on the current device.  Which front (xuid):
+//  * want_xuid >= 0: that one -- a host XCodecDiskCache's own xuid_, so the
+//    engine's fronts are the host disk's whatever order they bind in; uuid36,
+//    when given, must be registered there or nowhere;
+//  * uuid36: XCodecDisk::connect (xcodec_cache_disk.cc:640-690), the uuid's
+//    registered xuid, else the lowest xuid nothing holds (no registry entry, no
+//    front);
+//  * neither: XCodecDisk::local (:635-641), xuid 0 when it is registered and
+//    free (a reopened volume's local front), else the lowest free xuid under a
+//    generated UUID (registry_load's local UUID on a fresh volume, :575-596).
+// The registry entry is written once the front exists.
+int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, int want_xuid, XcgPairState** out) {
   if (C == 0 || !K || (uint64_t)K->D + C >= (1ull << 30)) return -22;
   if (uuid36 && (strlen(uuid36) != 36 || !uuid_ok((const uint8_t*)uuid36))) return -22;
+  if (want_xuid >= (int)XUIDS) return -22;
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return -5;
-  const int brc = disk_bind(K, device);
-  if (brc) return brc;
-  // XCodecDisk::connect (:640-690): a registered uuid's xuid, else the lowest
-  // xuid nothing holds (no registry entry, no front)
   auto bound = [&](uint32_t x) { return x < K->fronts.size() && K->fronts[x] != nullptr; };
   uint32_t xuid = XUIDS;
   if (uuid36)
     for (uint32_t x = 0; x < XUIDS; ++x)
       if (K->uuid[x] == uuid36) { xuid = x; break; }
+  if (want_xuid >= 0) {
+    if (xuid < XUIDS && xuid != (uint32_t)want_xuid) return -22;
+    xuid = (uint32_t)want_xuid;
+  } else if (!uuid36 && !K->uuid[0].empty() && !bound(0)) {
+    xuid = 0;
+  }
   if (xuid < XUIDS && bound(xuid)) return -22;               // (one engine front per disk front)
-  const bool registered = xuid < XUIDS;
-  if (!registered)
+  if (xuid >= XUIDS)
     for (xuid = 0; xuid < XUIDS && (bound(xuid) || !K->uuid[xuid].empty()); ++xuid) {
     }
   if (xuid >= XUIDS) return -22;                            // XCDFS_XUID_COUNT
-  if (uuid36 && !registered) {
-    K->uuid[xuid] = uuid36;
-    registry_write(K, xuid, uuid36);
+  char gen[37];
+  const char* name = uuid36;
+  if (!name && K->uuid[xuid].empty()) {
+    if (!gen_uuid(gen)) return -5;
+    name = gen;
   }
+  const int brc = disk_bind(K, device);
+  if (brc) return brc;
   XcgPairState* P = new XcgPairState;
   P->C = C;
   P->nb = (uint32_t)K->nb;
@@ -1795,40 +1873,53 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, XcgPa
   P->xuid = (uint16_t)xuid;
   P->gclock = K->dclock;
   const uint64_t ids = (uint64_t)C + P->D;
+  auto fail = [&](int rc) {
+    unmap_pool(P);
+    (void)hipFree(P->pkey); (void)hipFree(P->pdisk); (void)hipFree(P->lru); (void)hipFree(P->lru2);
+    (void)hipFree(P->ptime);
+    free_scratch(P);
+    delete P;
+    return rc;
+  };
   if (hipMalloc(&P->pkey, 8ull * C) != hipSuccess || hipMalloc(&P->pdisk, 8ull * C) != hipSuccess ||
       hipMalloc(&P->lru, 4ull * C) != hipSuccess || hipMalloc(&P->lru2, 4ull * C) != hipSuccess ||
       hipMalloc(&P->ptime, 8 * ids) != hipSuccess ||
       hipMalloc(&P->erep, 4 * ids) != hipSuccess ||
       hipMemset(P->pkey, 0xFF, 8ull * C) != hipSuccess || hipMemset(P->pdisk, 0xFF, 8ull * C) != hipSuccess ||
-      hipMemset(P->ptime, 0xFF, 8 * ids) != hipSuccess || ensure_front_arrays(P) != 0 || map_pool(P, device) != 0) {
-    (void)hipFree(P->pkey); (void)hipFree(P->pdisk); (void)hipFree(P->lru); (void)hipFree(P->lru2);
-    (void)hipFree(P->ptime);
-    free_scratch(P);
-    delete P;
-    return -12;
-  }
+      hipMemset(P->ptime, 0xFF, 8 * ids) != hipSuccess || ensure_front_arrays(P) != 0 || map_pool(P, device) != 0)
+    return fail(-12);
+  uint8_t* blocks = P->pool + (uint64_t)C * SEG;
+  const uint64_t D = K->D;
   if (!K->pending && !K->zeroed) {
-    if (hipMemset(P->pool + (uint64_t)C * SEG, 0, (uint64_t)K->D * SEG) != hipSuccess) return -5;
+    if (hipMemset(blocks, 0, D * SEG) != hipSuccess) return fail(-5);
     K->zeroed = K->vmm;
   }
   if (K->pending) {                                         // a reopened volume's ring and blocks
-    const uint64_t D = K->D;
     if (!K->ring_loaded &&
         (hipMemcpy(K->dkey, K->h_key.data(), 8 * D, hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(K->dent, K->h_ent.data(), 8 * D, hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(K->dxuid, K->h_xuid.data(), 4 * D, hipMemcpyHostToDevice) != hipSuccess))
-      return -5;
+      return fail(-5);
     K->ring_loaded = true;
-    if (hipMemcpy(P->pool + (uint64_t)C * SEG, K->h_data.data(), D * SEG, hipMemcpyHostToDevice) != hipSuccess)
-      return -5;
-    if (K->vmm) {                                            // (one copy serves every front)
-      K->pending = false;
-      K->zeroed = true;                                      // (the blocks hold the volume's bytes)
-      std::vector<uint64_t>().swap(K->h_key);
-      std::vector<uint64_t>().swap(K->h_ent);
-      std::vector<uint32_t>().swap(K->h_xuid);
-      std::vector<uint8_t>().swap(K->h_data);
-    }
+    if (hipMemcpy(blocks, K->h_data.data(), D * SEG, hipMemcpyHostToDevice) != hipSuccess) return fail(-5);
+  }
+  if (!P->pool_vmm && !K->shadow_ok.empty()) {               // blocks of fronts that went away
+    for (uint64_t i = 0; i < D; ++i)
+      if (K->shadow_ok[i] &&
+          hipMemcpy(blocks + i * SEG, &K->shadow[i * SEG], SEG, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(-5);
+  }
+  if (K->pending && K->vmm) {                                // (one copy serves every front)
+    K->pending = false;
+    K->zeroed = true;                                        // (the blocks hold the volume's bytes)
+    std::vector<uint64_t>().swap(K->h_key);
+    std::vector<uint64_t>().swap(K->h_ent);
+    std::vector<uint32_t>().swap(K->h_xuid);
+    std::vector<uint8_t>().swap(K->h_data);
+  }
+  if (name && K->uuid[xuid] != name) {
+    K->uuid[xuid] = std::string(name, 36);
+    registry_write(K, xuid, name);
   }
   P->gstale = true;                                          // (G from the disk's entries at the first call)
   if (xuid >= K->fronts.size()) K->fronts.resize(xuid + 1, nullptr);
@@ -1838,8 +1929,51 @@ int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, XcgPa
   return 0;
 }
 
+// Where the write head is: XCodecDisk's current_index_block_ and
+// index_block_next_ (xcodec_cache_disk.cc:701-727).
+void xcg_disk_state_head(const XcgDiskState* K, uint64_t* index_block, uint64_t* next) {
+  *index_block = (K->dclock / DISK_ENTRIES) % K->nb;
+  *next = K->dclock % DISK_ENTRIES;
+}
+
+uint32_t xcg_pair_state_xuid(const XcgPairState* P) { return P->xuid; }
+
 // Write the volume as the reference's file stands now (registry, every
 // written index block with its counter and entries, the data blocks).
+namespace {
+
+struct OnDevice {                 // run on `dev`, restore the caller's device after
+  int prev = -1;
+  explicit OnDevice(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
+  }
+  ~OnDevice() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// The disk's blocks through a mapping of its own physical allocation: the
+// bytes are there whether or not any front still maps them.
+int read_disk_blocks(const XcgDiskState* K, uint8_t* dst) {
+  void* va = nullptr;
+  bool mapped = false;
+  hipMemAccessDesc acc{};
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = K->device;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  bool ok = hipMemAddressReserve(&va, K->pool_bytes, 0, nullptr, 0) == hipSuccess;
+  ok = ok && (mapped = hipMemMap(va, K->pool_bytes, 0, K->pool_h, 0) == hipSuccess);
+  ok = ok && hipMemSetAccess(va, K->pool_bytes, &acc, 1) == hipSuccess;
+  ok = ok && hipMemcpy(dst, va, (size_t)K->D * SEG, hipMemcpyDeviceToHost) == hipSuccess;
+  if (mapped) (void)hipMemUnmap(va, K->pool_bytes);
+  if (va) (void)hipMemAddressFree(va, K->pool_bytes);
+  if (!ok) (void)hipGetLastError();
+  return ok ? 0 : -5;
+}
+
+}  // namespace
+
 int xcg_disk_state_save(XcgDiskState* K, const char* path) {
   const uint64_t nb = K->nb, D = K->D;
   std::vector<uint64_t> key(D, NOKEY);
@@ -1850,34 +1984,33 @@ int xcg_disk_state_save(XcgDiskState* K, const char* path) {
     xu = K->h_xuid;
     data = K->h_data;
   } else if (K->device >= 0) {
+    OnDevice on(K->device);
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(key.data(), K->dkey, 8 * D, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(xu.data(), K->dxuid, 4 * D, hipMemcpyDeviceToHost) != hipSuccess)
       return -5;
-    // the blocks' bytes: one mapping serves (shared blocks); per-front copies
-    // hold each front's own blocks
-    std::vector<uint8_t> tmp;
-    bool first = true;
-    for (XcgPairState* f : K->fronts) {
-      if (!f) continue;
-      if (K->vmm || first) {
-        if (hipMemcpy(data.data(), f->pool + (uint64_t)f->C * SEG, D * SEG, hipMemcpyDeviceToHost) != hipSuccess)
+    if (K->vmm) {
+      if (read_disk_blocks(K, data.data())) return -5;
+    } else {
+      // per-front copies: a block comes from the live front that wrote it,
+      // else from what a front that went away left, else from the volume
+      if (!K->h_data.empty()) data = K->h_data;
+      for (uint64_t i = 0; i < D && !K->shadow_ok.empty(); ++i)
+        if (K->shadow_ok[i]) memcpy(&data[i * SEG], &K->shadow[i * SEG], SEG);
+      std::vector<uint8_t> tmp((size_t)D * SEG);
+      for (XcgPairState* f : K->fronts) {
+        if (!f) continue;
+        if (hipMemcpy(tmp.data(), f->pool + (uint64_t)f->C * SEG, D * SEG, hipMemcpyDeviceToHost) != hipSuccess)
           return -5;
-        first = false;
-        if (K->vmm) break;
-        continue;
+        for (uint64_t i = 0; i < D; ++i)
+          if (xu[i] == f->xuid) memcpy(&data[i * SEG], &tmp[i * SEG], SEG);
       }
-      tmp.resize((size_t)D * SEG);
-      if (hipMemcpy(tmp.data(), f->pool + (uint64_t)f->C * SEG, D * SEG, hipMemcpyDeviceToHost) != hipSuccess)
-        return -5;
-      for (uint64_t i = 0; i < D; ++i)
-        if (xu[i] == f->xuid) memcpy(&data[i * SEG], &tmp[i * SEG], SEG);
     }
   }
   const int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0600);
   if (fd == -1) return -2;
   bool ok = ftruncate(fd, (off_t)K->bytes) == 0;
-  ok = ok && pwrite(fd, K->reg.data(), K->reg.size(), 0) == (ssize_t)K->reg.size();
+  ok = ok && pwrite_all(fd, K->reg.data(), K->reg.size(), 0);
   std::vector<uint8_t> ib(2048);
   for (uint64_t b = 0; ok && b < nb; ++b) {
     memset(ib.data(), 0, ib.size());
@@ -1893,32 +2026,43 @@ int xcg_disk_state_save(XcgDiskState* K, const char* path) {
         memcpy(q + 2, &h, 8);
       }
     }
-    ok = pwrite(fd, ib.data(), 2048, (off_t)((REG_BLOCKS + b) * 2048)) == 2048;
+    ok = pwrite_all(fd, ib.data(), 2048, (off_t)((REG_BLOCKS + b) * 2048));
   }
-  ok = ok && pwrite(fd, data.data(), data.size(), (off_t)((REG_BLOCKS + nb) * 2048)) == (ssize_t)data.size();
+  ok = ok && pwrite_all(fd, data.data(), data.size(), (off_t)((REG_BLOCKS + nb) * 2048));
   close(fd);
   return ok ? 0 : -5;
 }
 
-// Open a volume file: reloaded when it holds one, else a fresh disk.
-int xcg_disk_state_open(const char* path, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out) {
+// A volume read through an open descriptor (the reference's XCodecDisk keeps
+// its file open as fd_, xcodec_cache_disk.cc:840-871): reloaded when it holds
+// one (a non-empty file), else a fresh disk.
+int xcg_disk_state_open_fd(int fd, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out) {
   XcgDiskState* K = nullptr;
   const int rc = xcg_disk_state_create(disk_bytes, flags, &K);
   if (rc) return rc;
   struct stat st;
-  if (::stat(path, &st) == 0 && st.st_size > 0) {
-    std::vector<uint8_t> vol(disk_bytes, 0);
-    const int fd = ::open(path, O_RDONLY);
-    if (fd == -1 || pread(fd, vol.data(), vol.size(), 0) < 0) {
-      if (fd != -1) close(fd);
-      delete K;
-      return -2;
-    }
-    close(fd);
-    load_volume(K, vol);
+  if (fstat(fd, &st) != 0) {
+    delete K;
+    return -2;
+  }
+  if (st.st_size > 0 && load_volume(K, fd) != 0) {
+    delete K;
+    return -2;
   }
   *out = K;
   return 0;
+}
+
+// Open a volume file: reloaded when it holds one, else a fresh disk.
+int xcg_disk_state_open(const char* path, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out) {
+  const int fd = ::open(path, O_RDONLY);
+  if (fd == -1) {
+    if (errno == ENOENT) return xcg_disk_state_create(disk_bytes, flags, out);
+    return -2;
+  }
+  const int rc = xcg_disk_state_open_fd(fd, disk_bytes, flags, out);
+  close(fd);
+  return rc;
 }
 
 uint8_t* xcg_pair_state_pool(const XcgPairState* P) { return P->pool; }
@@ -1930,6 +2074,23 @@ void xcg_pair_state_destroy(XcgPairState* P) {
   if (!P) return;
   XcgDiskState* K = P->disk;
   (void)hipDeviceSynchronize();
+  if (K && K->dent && !P->pool_vmm) {                        // keep the blocks this front wrote
+    const uint64_t D = K->D;
+    std::vector<uint32_t> xu(D);
+    std::vector<uint8_t> tmp((size_t)D * SEG);
+    if (hipMemcpy(xu.data(), K->dxuid, 4 * D, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(tmp.data(), P->pool + (uint64_t)P->C * SEG, D * SEG, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (K->shadow_ok.empty()) {
+        K->shadow.assign((size_t)D * SEG, 0);
+        K->shadow_ok.assign(D, 0);
+      }
+      for (uint64_t i = 0; i < D; ++i)
+        if (xu[i] == P->xuid) {
+          memcpy(&K->shadow[i * SEG], &tmp[i * SEG], SEG);
+          K->shadow_ok[i] = 1;
+        }
+    }
+  }
   if (K && K->dent)
     hipLaunchKernelGGL(pair_drop_front_kernel, dim3(grid_for(K->D)), dim3(256), 0, nullptr, K->dkey, K->dent,
                        (const uint32_t*)K->dxuid, K->D, (uint32_t)P->xuid);

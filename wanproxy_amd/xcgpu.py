@@ -91,6 +91,15 @@ def lib():
     L.xcg_ctx_create_pair_uuid.restype = C.c_int
     L.xcg_ctx_create_pair_on.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.POINTER(C.c_void_p)]
     L.xcg_ctx_create_pair_on.restype = C.c_int
+    L.xcg_ctx_create_pair_xuid.argtypes = [C.c_int, C.c_uint32, C.c_uint64, vp, C.c_char_p, C.c_int,
+                                           C.POINTER(C.c_void_p)]
+    L.xcg_ctx_create_pair_xuid.restype = C.c_int
+    L.xcg_disk_open_fd.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.xcg_disk_open_fd.restype = C.c_int
+    L.xcg_disk_head.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.xcg_disk_head.restype = C.c_int
+    L.xcg_pair_xuid.argtypes = [vp]
+    L.xcg_pair_xuid.restype = C.c_int
     L.xcg_pair_stats.argtypes = [vp, vp]
     L.xcg_pair_stats.restype = C.c_int
     L.xcg_ctx_flags.argtypes = [vp, vp]
@@ -198,6 +207,13 @@ class Disk:
         """Write the volume as the reference's file stands now (xcg_disk_save)."""
         _check(lib().xcg_disk_save(self.h, path.encode()))
 
+    def head(self):
+        """The write head: (index block, next entry) -- XCodecDisk's
+        current_index_block_ / index_block_next_."""
+        b, n = C.c_uint64(), C.c_uint64()
+        _check(lib().xcg_disk_head(self.h, C.byref(b), C.byref(n)))
+        return int(b.value), int(n.value)
+
     def tier(self) -> int:
         """Where the data blocks live: 0 HBM, 1 pinned host memory (-1: no front yet)."""
         return int(lib().xcg_disk_tier(self.h))
@@ -225,21 +241,25 @@ class Context:
 
     def __init__(self, device: int = 0, out_of_band: bool = False, null_cache: bool = False,
                  cache_segments: int = 1 << 19, memory_cache_limit: int = 0, disk_bytes: int = 0,
-                 disk: Disk = None, uuid: str = None):
+                 disk: Disk = None, uuid: str = None, xuid: int = None):
         """memory_cache_limit (bytes): the bounded, LRU-evicting cache
         XCodecMemoryCache(uuid, memory_cache_limit) (xcodec/xcodec_cache.h:277)
         instead of an unbounded one of cache_segments capacity.  With
         disk_bytes too: wanproxy.conf's XCodecCachePair of that memory cache
         and a disk of disk_bytes (xcodec/xcodec_cache.h:140-237); with `disk`
         instead, the pair's secondary is the next front of that shared disk
-        (with `uuid`, that UUID's front: XCodecDisk::connect)."""
+        (with `uuid`, that UUID's front: XCodecDisk::connect; with `xuid`, that
+        front of the disk)."""
         import torch
         if not torch.cuda.is_available():
             raise XCGError('no GPU: the XCodec engine has no CPU path')
         self.device = device
         self.flags = (XCG_FLAG_OOB if out_of_band else 0) | (XCG_FLAG_NULLCACHE if null_cache else 0)
         h = C.c_void_p()
-        if disk is not None and uuid is not None:
+        if disk is not None and xuid is not None:
+            _check(lib().xcg_ctx_create_pair_xuid(device, self.flags, int(memory_cache_limit), disk.h,
+                                                  uuid.encode() if uuid else None, int(xuid), C.byref(h)))
+        elif disk is not None and uuid is not None:
             _check(lib().xcg_ctx_create_pair_uuid(device, self.flags, int(memory_cache_limit), disk.h, uuid.encode(),
                                                   C.byref(h)))
         elif disk is not None:
@@ -277,6 +297,12 @@ class Context:
         st = (C.c_uint64 * 4)()
         _check(lib().xcg_pair_stats(self.h, st))
         return tuple(int(v) for v in st)
+
+    def xuid(self) -> int:
+        """The disk front (xuid) of a pair context."""
+        x = lib().xcg_pair_xuid(self.h)
+        _check(min(x, 0))
+        return x
 
     def restart_counts(self):
         """(chunks resumed from their rows, chunks that rejoined their old parse)
