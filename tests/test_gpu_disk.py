@@ -17,6 +17,37 @@ _spec.loader.exec_module(mpg)
 SEG = 2048
 
 
+def _ops(b):
+    """The op list of an encoded stream: ('X', input offset) / ('R', offset, hash)."""
+    i, pos, out = 0, 0, []
+    while i < len(b):
+        if b[i] != 0xF1:
+            j = b.find(b'\xf1', i)
+            j = len(b) if j < 0 else j
+            pos += j - i
+            i = j
+            continue
+        op = b[i + 1]
+        if op == 0:
+            i, pos = i + 2, pos + 1
+        elif op == 1:
+            out.append(('X', pos))
+            i, pos = i + 2 + SEG, pos + SEG
+        else:
+            out.append(('R', pos, b[i + 2:i + 10].hex()))
+            i, pos = i + 10, pos + SEG
+    return out
+
+
+def _first_diff(got, exp):
+    for c, (a, b) in enumerate(zip(got, exp)):
+        if a != b:
+            oa, ob = _ops(a), _ops(b)
+            j = next((t for t in range(min(len(oa), len(ob))) if oa[t] != ob[t]), min(len(oa), len(ob)))
+            return f'chunk {c}: op {j}: engine {oa[j:j + 3]} reference {ob[j:j + 3]} ({len(oa)} / {len(ob)} ops)'
+    return f'{len(got)} / {len(exp)} chunks'
+
+
 def _uuid(k):
     return '%08x-0000-4000-8000-%012x' % (0xD15C, k)
 
@@ -252,15 +283,21 @@ def test_volume_saved_after_its_fronts_are_gone(ref_oracle, tmp_path):
     a, b, c = (open(p, 'rb').read() for p in (vref, open_, closed))
     assert b == c, 'the volume saved after the front closed lost its data blocks'
     assert a == b
+    # the second run sends the first run's last 16 chunks again (the newest
+    # entries, still on the disk) and goes on
+    tail = (parts[0][0][-16:], parts[0][1][-16:])
     K2 = Disk(disk, path=closed)
     c2 = Context(0, memory_cache_limit=limit, disk=K2, uuid=local)
-    got = [c2.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts[:1]]
+    got = [c2.encode_chunks(d, *p, semantics=XCG_SEM_STREAM) for p in (tail, parts[1])]
     c2.close()
     K2.close()
     pa2 = ref_oracle.cache_open_pair(limit, disk, vref, _uuid(0x999))
-    exp = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa2) for o, l in parts[:1]]
-    assert got == exp
-    assert sum(map(len, got[0])) < sum(l for l in parts[0][1]) // 2
+    exp = [ref_oracle.encode_batch(d, *p, mode=MODE_STREAM, cache=pa2) for p in (tail, parts[1])]
+    for g, e in zip(got, exp):
+        assert g == e, _first_diff(g, e)
+    pf = ref_oracle.cache_new_pair(limit, disk)
+    fresh = ref_oracle.encode_batch(d, *tail, mode=MODE_STREAM, cache=pf)
+    assert sum(map(len, got[0])) < sum(map(len, fresh)) - 100 * 2040, 'the reopened volume REFs nothing'
 
 
 def test_volume_of_a_front_without_uuid(ref_oracle, tmp_path):
@@ -287,7 +324,8 @@ def test_volume_of_a_front_without_uuid(ref_oracle, tmp_path):
     assert K2.head()[1] == 0                                       # (a reload starts an index block)
     c2 = Context(0, memory_cache_limit=limit, disk=K2)
     assert c2.xuid() == 0
-    got2 = [c2.encode_chunks(d, o, l, semantics=XCG_SEM_STREAM) for o, l in parts]
+    tail = (parts[0][0][-16:], parts[0][1][-16:])
+    got2 = [c2.encode_chunks(d, *p, semantics=XCG_SEM_STREAM) for p in (tail, parts[1])]
     c3 = Context(0, memory_cache_limit=limit, disk=K2)              # a second unnamed front: a new xuid
     assert c3.xuid() == 1
     c3.close()
@@ -300,8 +338,11 @@ def test_volume_of_a_front_without_uuid(ref_oracle, tmp_path):
     ref_oracle.disk_save(pa, vref)
     assert open(vref, 'rb').read() == open(vgpu, 'rb').read()
     pa2 = ref_oracle.cache_open_pair(limit, disk, vref, _uuid(0x998))
-    exp2 = [ref_oracle.encode_batch(d, o, l, mode=MODE_STREAM, cache=pa2) for o, l in parts]
-    assert got1 == exp1 and got2 == exp2
+    exp2 = [ref_oracle.encode_batch(d, *p, mode=MODE_STREAM, cache=pa2) for p in (tail, parts[1])]
+    assert got1 == exp1
+    for g, e in zip(got2, exp2):
+        assert g == e, _first_diff(g, e)
+    assert sum(map(len, got2[0])) < sum(tail[1]) * 3 // 4, 'the local front found nothing on the reopened volume'
 
 
 def test_front_by_xuid(tmp_path):

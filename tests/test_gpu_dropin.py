@@ -151,7 +151,7 @@ def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path
         pa2 = o.cache_open_pair(limit, disk, vol, _uuid(0x999))
         pb2 = o.cache_pair_front(pa2, peer, limit)
         ea2, eb2 = o.encoder_new(pa2), o.encoder_new(pb2)
-        second = [o.encode_refmap(ea2, p) for p in calls(d, 3, 9)]
+        second = [o.encode_refmap(ea2, p) for p in calls(d, 5, 9)]
         second += [o.encode_refmap(eb2, p) for p in calls(e, 3, 6)]
         second += [(o.pair_stats(pa2, disk_live=True), o.pair_stats(pb2, disk_live=True))]
         o.disk_save(pa2, vol)
@@ -169,9 +169,9 @@ def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path
     # the reload made a difference: on a fresh volume the same calls declare more
     pf = ref_oracle.cache_new_pair(limit, disk)
     ef = ref_oracle.encoder_new(pf)
-    fresh = [ref_oracle.encode_refmap(ef, p)[0] for p in calls(d, 3, 9)]
+    fresh = [ref_oracle.encode_refmap(ef, p)[0] for p in calls(d, 5, 6)]
     ref_oracle.encoder_free(ef)
-    assert sum(map(len, fresh)) > sum(len(r[0]) for r in ref[2][:len(fresh)]) + 20 * 2048
+    assert sum(map(len, fresh)) > sum(len(r[0]) for r in ref[2][:len(fresh)]) + 100 * 2040
 
 
 def test_dropin_decode_bounded_like_reference(dropin, ref_oracle):

@@ -985,6 +985,7 @@ struct XcgDiskState {
   bool vmm = false;
   hipMemGenericAllocationHandle_t pool_h{};
   size_t pool_bytes = 0;
+  void* dva = nullptr;             // the disk's own mapping of pool_h, for its whole life (xcg_disk_save)
   std::vector<XcgPairState*> fronts;   // by xuid (nullptr: free)
   // the volume (xcodec_cache_disk.cc:72-101): its size, per index block the
   // counter it was last written with, the counter of the block being filled,
@@ -1507,6 +1508,26 @@ int map_pool(XcgPairState* P, int device) {
       }
     }
     ok = ok && K->vmm;
+    if (ok && !K->dva) {
+      // The disk's own mapping of its blocks, held until the disk goes: the
+      // volume can be saved after every front is gone, and the allocation
+      // always has a mapping until it is released (fronts come and go).
+      void* va = nullptr;
+      hipMemAccessDesc acc{};
+      acc.location = prop.location;
+      acc.flags = hipMemAccessFlagsProtReadWrite;
+      bool m = false;
+      bool dok = hipMemAddressReserve(&va, K->pool_bytes, 0, nullptr, 0) == hipSuccess;
+      dok = dok && (m = hipMemMap(va, K->pool_bytes, 0, K->pool_h, 0) == hipSuccess);
+      dok = dok && hipMemSetAccess(va, K->pool_bytes, &acc, 1) == hipSuccess;
+      if (dok) {
+        K->dva = va;
+      } else {
+        if (m) (void)hipMemUnmap(va, K->pool_bytes);
+        if (va) (void)hipMemAddressFree(va, K->pool_bytes);
+        (void)hipGetLastError();
+      }
+    }
     const size_t sp = round_up((size_t)P->C * SEG, gran ? gran : 1);
     bool prim = false, reserved = false, m1 = false, m2 = false;
     if (ok) prim = ok = hipMemCreate(&P->prim_h, sp, &prop, 0) == hipSuccess;
@@ -1801,6 +1822,11 @@ int xcg_disk_state_create(uint64_t disk_bytes, uint32_t flags, XcgDiskState** ou
 void xcg_disk_state_release(XcgDiskState* K) {
   if (!K || --K->refs > 0) return;
   (void)hipFree(K->dkey); (void)hipFree(K->dent); (void)hipFree(K->dxuid);
+  if (K->dva) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemUnmap(K->dva, K->pool_bytes);
+    (void)hipMemAddressFree(K->dva, K->pool_bytes);
+  }
   if (K->vmm) (void)hipMemRelease(K->pool_h);
   delete K;
 }
@@ -1953,23 +1979,14 @@ struct OnDevice {                 // run on `dev`, restore the caller's device a
   }
 };
 
-// The disk's blocks through a mapping of its own physical allocation: the
+// The disk's blocks through its own mapping of the physical allocation: the
 // bytes are there whether or not any front still maps them.
 int read_disk_blocks(const XcgDiskState* K, uint8_t* dst) {
-  void* va = nullptr;
-  bool mapped = false;
-  hipMemAccessDesc acc{};
-  acc.location.type = hipMemLocationTypeDevice;
-  acc.location.id = K->device;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  bool ok = hipMemAddressReserve(&va, K->pool_bytes, 0, nullptr, 0) == hipSuccess;
-  ok = ok && (mapped = hipMemMap(va, K->pool_bytes, 0, K->pool_h, 0) == hipSuccess);
-  ok = ok && hipMemSetAccess(va, K->pool_bytes, &acc, 1) == hipSuccess;
-  ok = ok && hipMemcpy(dst, va, (size_t)K->D * SEG, hipMemcpyDeviceToHost) == hipSuccess;
-  if (mapped) (void)hipMemUnmap(va, K->pool_bytes);
-  if (va) (void)hipMemAddressFree(va, K->pool_bytes);
-  if (!ok) (void)hipGetLastError();
-  return ok ? 0 : -5;
+  const uint8_t* src = (const uint8_t*)K->dva;
+  for (const XcgPairState* f : K->fronts)            // (no mapping of its own: a live front's)
+    if (!src && f) src = f->pool + (uint64_t)f->C * SEG;
+  if (!src) return -5;
+  return hipMemcpy(dst, src, (size_t)K->D * SEG, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
 }
 
 }  // namespace
