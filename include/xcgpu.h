@@ -476,6 +476,15 @@ uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
  * corrected by the verification.  Same output either way.  mode: -1
  * automatic (default), 0 never seed, 1 always seed.  Returns the previous mode. */
 int xcg_debug_set_stream_seed(int mode);
+/* Diagnostics / tests: stream batches of small chunks (< 8 KiB) pass a screen
+ * first that gives every chunk none of whose windows can be found (nothing in
+ * the cache, the batch or its own earlier tiles) its cold parse -- the
+ * 2048-byte tiling -- and sends the rest to the parse; same output either way.
+ * mode 0 off, 1 on (default; env XCG_SCREEN), 2 on and counting:
+ * xcg_debug_screen_counts returns (and resets) the chunks screened and those
+ * sent on to the parse.  Returns the previous mode. */
+int xcg_debug_set_screen(int mode);
+int xcg_debug_screen_counts(uint64_t *screened, uint64_t *parsed);
 /* Diagnostics / bench: while on, every stream-parse kernel launch
  * (encode_stream_kernel) is bracketed by HIP events on its launch stream;
  * xcg_debug_stream_kernel_time returns (and resets) the summed milliseconds

@@ -126,6 +126,8 @@ struct BatchScratch {
   uint64_t* a_keys = nullptr;      // newly visible hashes -> chunk range (verification (a))
   uint64_t* a_vals = nullptr;
   uint32_t* a_bits = nullptr;
+  uint32_t* s_fold = nullptr;      // quiet-chunk screen: LDS fold of the lane filter
+  uint32_t* s_work = nullptr;      // [n + 1] its work list
   uint32_t last_maxd = 0;          // declaration stride of the last stream batch
   // bounded cache: every chunk's cache references (xcg_lru.hip)
   void* ev = nullptr;              // n_cap * maxe uint4
@@ -320,6 +322,7 @@ void free_scratch(BatchScratch& b) {
   (void)hipFree(b.b_count); (void)hipFree(b.b_ev); (void)hipFree(b.b_eo); (void)hipFree(b.b_hits);
   (void)hipFree(b.b_cnt); (void)hipFree(b.b_out); (void)hipFree(b.splice);
   (void)hipFree(b.a_keys); (void)hipFree(b.a_vals); (void)hipFree(b.a_bits);
+  (void)hipFree(b.s_fold); (void)hipFree(b.s_work);
   b = BatchScratch{};
 }
 
@@ -431,7 +434,8 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipMalloc(&b.need, 4ull * n) != hipSuccess || hipMalloc(&b.vflags, 16) != hipSuccess ||
       hipHostMalloc(&b.h_vflags, 16) != hipSuccess || hipMalloc(&b.a_keys, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
       hipMalloc(&b.a_vals, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
-      hipMalloc(&b.a_bits, 4ull * XCG_VERIFY_A_WORDS) != hipSuccess) {
+      hipMalloc(&b.a_bits, 4ull * XCG_VERIFY_A_WORDS) != hipSuccess ||
+      hipMalloc(&b.s_fold, 4ull * 32768) != hipSuccess || hipMalloc(&b.s_work, 4ull * (n + 1)) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
@@ -1089,6 +1093,8 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     a.a_vals = c->bs.a_vals;
     a.a_bits = getenv("XCG_NO_APROBE") ? nullptr : c->bs.a_bits;
     a.flags_ev = c->flags_ev;
+    a.s_fold = c->bs.s_fold;
+    a.s_work = c->bs.s_work;
     if (c->pair || c->bounded) {
       BatchScratch& b = c->bs;
       a.eo = b.eo; a.bad_t = b.bad_t; a.bad_hi = b.bad_hi; a.bslot = b.bslot; a.b_count = b.b_count;

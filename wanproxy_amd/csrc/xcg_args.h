@@ -89,6 +89,11 @@ struct XcgStreamArgs {
   // the context's event behind the verification flags' copy (hipEvent_t; null:
   // the driver makes one for the call)
   void* flags_ev;
+  // the quiet-chunk screen (small chunks): the 128 KiB LDS fold of the round's
+  // global lane filter, and the work list of chunks it sends to the parse
+  // ([0] count, [1..n] chunks); null: no screen
+  uint32_t* s_fold = nullptr;
+  uint32_t* s_work = nullptr;
 };
 
 // (a)-probe sizes: at most A_LIMIT newly visible hashes per verification (more:

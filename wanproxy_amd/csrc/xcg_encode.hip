@@ -148,6 +148,8 @@ struct EncParams {
   uint32_t maxe;
   uint32_t* eo;        // [n * maxe] output length after the REF a lookup made (~0: it made none)
   RestartArgs rs;      // re-parse from the previous pass's rows (bslot null: off)
+  // ---- (stream) parse only the chunks of a work list: work[0] = count, work[1..] chunks (null: all)
+  const uint32_t* work;
 };
 
 // ------------------------------------------------------------------ emission
@@ -1557,10 +1559,291 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
                    (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode, S.ro[wv], S.rsv[wv]};
   const uint32_t stride = gridDim.x * SW;
-  for (uint32_t chunk = blockIdx.x * SW + (uint32_t)wv; chunk < prm.n; chunk += stride) {
+  const uint32_t items = prm.work ? readfirst(prm.work[0]) : prm.n;
+  for (uint32_t i = blockIdx.x * SW + (uint32_t)wv; i < items; i += stride) {
+    const uint32_t chunk = prm.work ? readfirst(prm.work[1 + i]) : i;
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
     if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;   // verified: its parse stands
     encode_chunk<LOGNB, MAXD, true, LRU>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
+  }
+}
+
+// ------------------------------------------------------------ quiet-chunk screen
+//
+// Small stream chunks (C4's 4 KiB packets: 2049 window positions each, a wave
+// per packet, sixteen packets in turn per wave) spend their parse mostly in
+// per-chunk round trips, and in hash-bound traffic (few repeats) almost every
+// one of them ends as the cold parse: the 2048-byte tiling, with no lookup
+// finding anything ("the cold parse of unique data is an exact
+// 2048-aligned tiling").  That outcome is decided without the state machine:
+// when no window of the chunk can be found -- in the persistent cache, among
+// the batch's declarations, or among the chunk's own tiles declared before it
+// (a tile at t is declared while examining window t + 2048, xcodec_encoder.cc:
+// 183-190, so it is visible to the windows of every later piece) -- every lookup
+// misses, and encode() declares exactly the tiles (:222-261) and escapes the
+// tail (:267-269).  The screen rolls every window of a chunk through the round's
+// filters (a 128 KiB LDS fold of the global lane filter, then the global filter
+// and the fingerprint buckets for what passes), compares it with the chunk's
+// earlier tiles, and checks each tile's own window exactly (a tile is in the
+// batch table as this chunk's own declaration; anything else there or in the
+// persistent cache is a possible hit).  Chunks it cannot clear -- any possible
+// hit, an unaligned start, more than SCREEN_MAXD tiles -- go on a work list for
+// encode_stream_kernel, which parses them as always; the others get the tiling
+// output, declaration rows and counters here.  Either way the output is the
+// sequential encoder's: the screen only skips parses whose every lookup misses.
+constexpr int SCREEN_MAXD = 4;                       // chunks shorter than 4 tiles (< 8 KiB)
+constexpr uint32_t SCREEN_FOLD_WORDS = 32768;        // 128 KiB of LDS
+constexpr int SCREEN_W = 16;                         // waves per workgroup (one workgroup per CU)
+__device__ __forceinline__ uint32_t fold_word_of(uint32_t k, uint32_t fwm) { return (k >> 10) & fwm; }
+
+// The LDS fold of the global lane filter: word j of the fold = OR of the global
+// words j, j + F, j + 2F, ... (gfilt_word = K bits 10..; the fold keeps the
+// low bits of that index), so a key's two bits are set in the fold whenever
+// they are in its global word: no false negatives.
+__global__ __launch_bounds__(256) void screen_fold_kernel(const uint32_t* gf, uint32_t gwords, uint32_t* fold,
+                                                          uint32_t fwords) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= fwords) return;
+  uint32_t w = 0;
+  for (uint32_t j = i; j < gwords; j += fwords) w |= gf[j];
+  fold[i] = w;
+}
+
+__device__ __forceinline__ uint32_t sel4(int l, const uint32_t (&v)[SCREEN_MAXD]) {
+  return l == 0 ? v[0] : (l == 1 ? v[1] : (l == 2 ? v[2] : v[3]));
+}
+
+// Returns true when the chunk needs the full parse (the screen wrote nothing
+// that matters then: its speculative tile bodies are overwritten).
+__device__ __forceinline__ bool screen_chunk(const EncParams& prm, const uint32_t* F, uint32_t fwm, uint32_t chunk) {
+  const int l = lane_id();
+  const uint8_t* x = prm.in + prm.chunk_off[chunk];
+  const int L = (int)prm.chunk_len[chunk];
+  if ((uint32_t)L > prm.max_len || L / SEG >= SCREEN_MAXD || L / SEG >= (int)prm.maxd) return true;
+  uint8_t* const out = prm.out + prm.out_off[chunk];
+  const uint32_t nold = readfirst(prm.ndecl[chunk]);
+  if (L < SEG) {                                   // xcodec_encoder.cc:77-83: no window at all
+    const uint32_t olen = L > 0 ? escape_u(out, x, 0, (uint32_t)L) : 0u;
+    if (l == 0) {
+      prm.out_len[chunk] = olen;
+      prm.ndecl[chunk] = 0u;
+      prm.nhits[chunk] = 0u;
+      if (nold != 0u) atomicMin(prm.changed, chunk);
+      if (prm.stats) {
+        prm.stats[4 * chunk + 0] = 0u; prm.stats[4 * chunk + 1] = 0u;
+        prm.stats[4 * chunk + 2] = 0u; prm.stats[4 * chunk + 3] = 0u;
+      }
+    }
+    return false;
+  }
+  if (reinterpret_cast<uintptr_t>(x) & 15u) return true;   // (pieces = tiles needs an aligned start)
+  const int last = L - SEG;                        // last window start
+  const int nt = L / SEG;                          // tiles = pieces
+  uint32_t tlo[SCREEN_MAXD] = {0u, 0u, 0u, 0u}, thi[SCREEN_MAXD] = {0u, 0u, 0u, 0u};
+  uint32_t tk[SCREEN_MAXD] = {0u, 0u, 0u, 0u};
+  Piece P;
+  P.sxb = 0u; P.sqxb = 0u;
+  uint32_t totXA = 0, totTA = 0;
+  const uint32_t* const gf = prm.lf.gfilt;
+  const u32x4* const ftab = prm.lf.ftab;
+#pragma unroll 1
+  for (int i = 0; i < nt; ++i) {
+    const int p = SEG * i;
+    const int q0 = p + 32 * l;
+    const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
+    const bool one = pe - p == 1;                  // (a chunk of 2048 k bytes ends with a one-window piece)
+    if (i == 0) {
+      P.a0 = load16_aligned_safe(x, q0, L);
+      P.a1 = load16_aligned_safe(x, q0 + 16, L);
+      seg_sums(P.a0, P.a1, P.sxa, P.sqxa);
+    } else {
+      P.a0 = P.b0; P.a1 = P.b1;
+      P.sxa = P.sxb; P.sqxa = P.sqxb;
+    }
+    if (!one) {
+      P.b0 = load16_aligned_safe(x, q0 + SEG, L);
+      P.b1 = load16_aligned_safe(x, q0 + SEG + 16, L);
+      seg_sums(P.b0, P.b1, P.sxb, P.sqxb);
+    }
+    // start sums of the lane's first window (encode_chunk's piece setup)
+    const uint32_t qa = 32u * (uint32_t)l, qb = 2048u + 32u * (uint32_t)l;
+    const uint32_t ta = qa * P.sxa + P.sqxa, tb = one ? 0u : qb * P.sxb + P.sqxb;
+    if (i == 0) {
+      totXA = wave_sum(P.sxa);
+      totTA = wave_sum(ta);
+    }
+    const uint32_t dx = (one ? 0u : P.sxb) - P.sxa, dt = tb - ta;
+    const uint32_t ix = wave_incl_scan(dx), it = wave_incl_scan(dt);
+    const uint32_t X1 = totXA + ix - dx;
+    const uint32_t TT = totTA + it - dt;
+    const uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
+    const uint32_t totXB = totXA + readlane(ix, 63);
+    const uint32_t totTB = totTA + readlane(it, 63) - 2048u * totXB;
+    uint32_t NX1 = 0u - X1, NX2 = 0u - X2c;
+    // the tile at the piece start: its hash, and its EXTRACT written ahead
+    // (encode_declaration :300-302; the body is this piece's A half)
+    const uint32_t tki = readfirst((NX1 << 20) + NX2);
+    const uint32_t thii = readfirst(lane_window_hi(P, 0));
+#pragma unroll
+    for (int u = 0; u < SCREEN_MAXD; ++u)
+      if (u == i) { tk[u] = tki; tlo[u] = 0u - tki; thi[u] = thii; }
+    {
+      uint8_t* dst = out + (uint32_t)(2 + SEG) * (uint32_t)i;
+      if (l < 2) dst[l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);
+      *(u32x4_u*)(dst + 2 + 32 * l) = P.a0;
+      *(u32x4_u*)(dst + 2 + 32 * l + 16) = P.a1;
+    }
+    // the tile's own window against the earlier tiles
+    bool own = false;
+#pragma unroll
+    for (int t = 0; t < SCREEN_MAXD - 1; ++t)
+      if (t < i) own |= tki == tk[t];
+    if (own) return true;
+    if (one) {
+      totXA = totXB; totTA = totTB;
+      continue;
+    }
+    // every other window of the piece: the round's filters, the earlier tiles
+    const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
+    const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
+    uint32_t kk[32];
+    uint32_t pass = 0u;
+    uint64_t ownl = 0;   // lanes with a window equal to an earlier tile (lane masks: no VGPRs)
+    // groups of 4 positions, one group's LDS reads in flight while the next
+    // group rolls (as roll_probe; the sched_barrier bounds what is hoisted)
+    uint32_t fwc[4], fwn[4];
+    auto roll4 = [&](int g, uint32_t (&fw)[4]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = 4 * g + t;
+        kk[j] = (NX1 << 20) + NX2;
+        if (j < 31) {
+          const uint32_t xo = byte_of(xa[j >> 2], j & 3);
+          const uint32_t xn = byte_of(xb[j >> 2], j & 3);
+          NX1 += xo - xn;
+          NX2 += NX1 + (xo << 11);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fw[t] = F[fold_word_of(kk[4 * g + t], fwm)];
+    };
+    roll4(0, fwc);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if (g < 7) roll4(g + 1, fwn);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = 4 * g + t;
+        pass |= gfilt_test(fwc[t], kk[j]) << j;
+#pragma unroll
+        for (int u = 0; u < SCREEN_MAXD - 1; ++u)
+          if (u < i) ownl |= lanes_eq(kk[j], tk[u]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (g < 7) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fwc[t] = fwn[t];
+      }
+    }
+    // positions past the last window are not positions; the piece start is the
+    // tile itself (checked exactly below)
+    const int nvalid = pe - q0;
+    uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
+    if (l == 0) vm &= ~1u;
+    pass &= vm;
+    // (a window past the last one that equals an earlier tile only costs the
+    // screen this chunk)
+    if (ownl) return true;
+    if (ballot(pass != 0u)) {
+      // the global lane filter for what passed the fold (16 loads in flight at
+      // a time: registers)
+      uint32_t pass2 = 0u;
+#pragma unroll
+      for (int h = 0; h < 32; h += 8) {
+        uint32_t gw[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          gw[j] = 0u;
+          if ((pass >> (h + j)) & 1u) gw[j] = gf[gfilt_word(kk[h + j], prm.lf.gmask)];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pass2 |= ((pass >> (h + j)) & gfilt_test(gw[j], kk[h + j]) & 1u) << (h + j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ballot(pass2 != 0u)) {
+        // the fingerprint buckets for the few left
+        bool m = false;
+#pragma unroll
+        for (int h = 0; h < 32; h += 4) {
+          if (ballot(((pass2 >> h) & 15u) != 0u) == 0) continue;
+          u32x4 q[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            q[j] = u32x4{0u, 0u, 0u, 0u};
+            if ((pass2 >> (h + j)) & 1u) q[j] = ftab[fbucket(kk[h + j], prm.lf.fmask)];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m |= ((pass2 >> (h + j)) & 1u) && ftab_match(q[j], kk[h + j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (ballot(m)) return true;
+      }
+    }
+    totXA = totXB; totTA = totTB;
+  }
+  // Each tile's own window, exactly: in the persistent cache, or declared in the
+  // batch anywhere but here, it may be found.
+  const uint32_t mylo = sel4(l, tlo), myhi = sel4(l, thi);
+  bool hit = false;
+  if (l < nt) {
+    if (readfirst(*prm.nseg) != 0u && tab_lookup_t(prm.g, mylo, myhi) != ~0ull) hit = true;
+    if (prm.use_b) {
+      const uint64_t bv = tab_lookup_t(prm.b, mylo, myhi);
+      if (bv != ~0ull && ((uint32_t)(bv >> 32) < chunk || ((uint32_t)(bv >> 32) == chunk && (uint32_t)bv != (uint32_t)(SEG * l))))
+        hit = true;
+    }
+  }
+  if (ballot(hit)) return true;
+  // the cold parse: the tiles (written above), then the escaped tail
+  uint32_t olen = (uint32_t)(2 + SEG) * (uint32_t)nt;
+  if (SEG * nt < L) olen += escape_u(out + olen, x, (uint32_t)(SEG * nt), (uint32_t)L);
+  bool diff = nold != (uint32_t)nt;
+  if (l < nt) {
+    uint4* dl = prm.decl + (uint64_t)chunk * prm.maxd;
+    const uint4 nv = make_uint4(mylo, myhi, (uint32_t)(SEG * l), (uint32_t)(2 + SEG) * (uint32_t)(l + 1));
+    if ((uint32_t)l < nold) {
+      const uint4 ov = dl[l];
+      diff |= ov.x != nv.x || ov.y != nv.y || ov.z != nv.z;
+    }
+    dl[l] = nv;
+  }
+  if (ballot(diff) != 0 && l == 0) atomicMin(prm.changed, chunk);
+  if (l == 0) {
+    prm.ndecl[chunk] = (uint32_t)nt;
+    prm.nhits[chunk] = 0u;
+    prm.out_len[chunk] = olen;
+    if (prm.stats) {
+      prm.stats[4 * chunk + 0] = (uint32_t)nt; prm.stats[4 * chunk + 1] = 0u;
+      prm.stats[4 * chunk + 2] = 0u; prm.stats[4 * chunk + 3] = (uint32_t)nt;
+    }
+  }
+  return false;
+}
+
+// Persistent workgroups of SCREEN_W waves over the chunks (those a
+// verification round leaves standing are skipped); the ones that need the full
+// parse are appended to work[1..] (work[0] counts them).
+__global__ __launch_bounds__(64 * SCREEN_W) void stream_screen_kernel(EncParams prm, const uint32_t* fold,
+                                                                      uint32_t fwords, uint32_t* work) {
+  __shared__ uint32_t F[SCREEN_FOLD_WORDS];
+  for (uint32_t i = threadIdx.x; i < fwords / 4; i += blockDim.x) ((u32x4*)F)[i] = ((const u32x4*)fold)[i];
+  __syncthreads();
+  const int wv = (int)readfirst(threadIdx.x >> 6);
+  const uint32_t stride = gridDim.x * SCREEN_W;
+  for (uint32_t chunk = blockIdx.x * SCREEN_W + (uint32_t)wv; chunk < prm.n; chunk += stride) {
+    if (chunk < prm.skip_below) continue;
+    if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;
+    if (screen_chunk(prm, F, fwords - 1u, chunk) && lane_id() == 0) work[1 + atomicAdd(work, 1u)] = chunk;
   }
 }
 
@@ -2245,6 +2528,25 @@ extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// The quiet-chunk screen on (default) / off: XCG_SCREEN=0, or
+// xcg_debug_set_screen (tests run both ways).
+static int g_screen = [] {
+  const char* e = getenv("XCG_SCREEN");
+  return e ? atoi(e) : 1;
+}();
+static bool xcg_screen_on() { return __atomic_load_n(&g_screen, __ATOMIC_RELAXED) != 0; }
+// (2: on, and count what the screen sees -- a host sync per screened launch)
+static bool xcg_screen_counting() { return __atomic_load_n(&g_screen, __ATOMIC_RELAXED) == 2; }
+extern "C" int xcg_debug_set_screen(int mode) {
+  return __atomic_exchange_n(&g_screen, mode < 0 ? 0 : (mode > 2 ? 2 : mode), __ATOMIC_RELAXED);
+}
+static uint64_t g_screen_seen = 0, g_screen_parsed = 0;
+extern "C" int xcg_debug_screen_counts(uint64_t* seen, uint64_t* parsed) {
+  if (seen) *seen = __atomic_exchange_n(&g_screen_seen, 0ull, __ATOMIC_RELAXED);
+  if (parsed) *parsed = __atomic_exchange_n(&g_screen_parsed, 0ull, __ATOMIC_RELAXED);
+  return 0;
+}
+
 static bool stream_debug() {
   static const bool on = getenv("XCG_STREAM_DEBUG") != nullptr;
   return on;
@@ -2367,8 +2669,37 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       hipLaunchKernelGGL((encode_stream_kernel<8, 72, 16, R>), sgrid, sblock, 0, stream, prm);
     }
   };
+  // The quiet-chunk screen (stream_screen_kernel) in front of the parse: small
+  // chunks, in-band, not the bounded / pair variants (which record references).
+  const bool screen = a->s_fold && a->s_work && !a->ev && !(a->flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) &&
+                      a->maxd <= (uint32_t)SCREEN_MAXD && xcg_screen_on();
   // bounded cache: the variant that records the chunks' cache references (xcg_lru.hip)
   auto launch = [&]() {
+    if (screen) {
+      const uint32_t gwords = prm.lf.gmask + 1u;
+      const uint32_t fwords = gwords < SCREEN_FOLD_WORDS ? gwords : SCREEN_FOLD_WORDS;
+      hipLaunchKernelGGL(screen_fold_kernel, dim3((fwords + 255) / 256), dim3(256), 0, stream, prm.lf.gfilt, gwords,
+                         a->s_fold, fwords);
+      (void)hipMemsetAsync(a->s_work, 0, 4, stream);
+      hipLaunchKernelGGL(stream_screen_kernel, dim3(wgs), dim3(64 * SCREEN_W), 0, stream, prm, (const uint32_t*)a->s_fold,
+                         fwords, a->s_work);
+      prm.work = a->s_work;
+      if (xcg_screen_counting()) {
+        uint32_t w = 0;
+        (void)hipMemcpyAsync(&w, a->s_work, 4, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        uint32_t seen = n;
+        if (prm.need) {
+          std::vector<uint32_t> h(n);
+          (void)hipMemcpy(h.data(), prm.need, 4ull * n, hipMemcpyDeviceToHost);
+          seen = 0;
+          for (uint32_t v : h) seen += v != 0;
+        }
+        __atomic_add_fetch(&g_screen_seen, (uint64_t)(seen - (prm.skip_below < seen ? prm.skip_below : 0u)),
+                           __ATOMIC_RELAXED);
+        __atomic_add_fetch(&g_screen_parsed, (uint64_t)w, __ATOMIC_RELAXED);
+      }
+    }
     if (stream_debug()) {
       uint32_t cnt = n;
       if (prm.need) {
@@ -2384,6 +2715,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     if (prm.ev) launch_sw(std::integral_constant<bool, true>{});
     else launch_sw(std::integral_constant<bool, false>{});
     ktime_end(e0, stream);
+    prm.work = nullptr;
   };
   // lowest chunk whose declaration list changed in the round just run (~0u: none)
   auto changed_after = [&](uint32_t& fc) -> bool {
