@@ -128,6 +128,10 @@ struct BatchScratch {
   uint32_t* a_bits = nullptr;
   uint32_t* s_fold = nullptr;      // quiet-chunk screen: LDS fold of the lane filter
   uint32_t* s_work = nullptr;      // [n + 1] its work list
+  uint32_t* s_info = nullptr;      // [n] its verdicts
+  uint32_t* s_rows = nullptr;      // [n * 4] uint4: its staged rows
+  uint32_t* s_qcnt = nullptr;      // [n], [n * 1024]: its queued windows
+  uint32_t* s_qkeys = nullptr;
   uint32_t last_maxd = 0;          // declaration stride of the last stream batch
   // bounded cache: every chunk's cache references (xcg_lru.hip)
   void* ev = nullptr;              // n_cap * maxe uint4
@@ -322,7 +326,8 @@ void free_scratch(BatchScratch& b) {
   (void)hipFree(b.b_count); (void)hipFree(b.b_ev); (void)hipFree(b.b_eo); (void)hipFree(b.b_hits);
   (void)hipFree(b.b_cnt); (void)hipFree(b.b_out); (void)hipFree(b.splice);
   (void)hipFree(b.a_keys); (void)hipFree(b.a_vals); (void)hipFree(b.a_bits);
-  (void)hipFree(b.s_fold); (void)hipFree(b.s_work);
+  (void)hipFree(b.s_fold); (void)hipFree(b.s_work); (void)hipFree(b.s_info); (void)hipFree(b.s_rows);
+  (void)hipFree(b.s_qcnt); (void)hipFree(b.s_qkeys);
   b = BatchScratch{};
 }
 
@@ -435,7 +440,10 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipHostMalloc(&b.h_vflags, 16) != hipSuccess || hipMalloc(&b.a_keys, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
       hipMalloc(&b.a_vals, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
       hipMalloc(&b.a_bits, 4ull * XCG_VERIFY_A_WORDS) != hipSuccess ||
-      hipMalloc(&b.s_fold, 4ull * 32768) != hipSuccess || hipMalloc(&b.s_work, 4ull * (n + 1)) != hipSuccess) {
+      hipMalloc(&b.s_fold, 4ull * 32768) != hipSuccess || hipMalloc(&b.s_work, 4ull * (n + 1)) != hipSuccess ||
+      hipMalloc(&b.s_info, 4ull * n) != hipSuccess || hipMalloc(&b.s_rows, 64ull * n) != hipSuccess ||
+      (maxd <= 4 && (hipMalloc(&b.s_qcnt, 4ull * n) != hipSuccess ||
+                     hipMalloc(&b.s_qkeys, 4096ull * n) != hipSuccess))) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
@@ -1095,6 +1103,10 @@ int encode_batch_impl(xcg_ctx* c, int semantics, const uint8_t* d_in, const uint
     a.flags_ev = c->flags_ev;
     a.s_fold = c->bs.s_fold;
     a.s_work = c->bs.s_work;
+    a.s_info = c->bs.s_info;
+    a.s_rows = c->bs.s_rows;
+    a.s_qcnt = c->bs.s_qcnt;
+    a.s_qkeys = c->bs.s_qkeys;
     if (c->pair || c->bounded) {
       BatchScratch& b = c->bs;
       a.eo = b.eo; a.bad_t = b.bad_t; a.bad_hi = b.bad_hi; a.bslot = b.bslot; a.b_count = b.b_count;

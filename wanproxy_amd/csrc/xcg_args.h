@@ -94,6 +94,10 @@ struct XcgStreamArgs {
   // ([0] count, [1..n] chunks); null: no screen
   uint32_t* s_fold = nullptr;
   uint32_t* s_work = nullptr;
+  uint32_t* s_info = nullptr;    // [n] the screen's verdict per chunk
+  void* s_rows = nullptr;        // [n * 4] uint4: its staged rows
+  uint32_t* s_qcnt = nullptr;    // [n] and [n * 1024]: the windows it queues for the probe
+  uint32_t* s_qkeys = nullptr;
 };
 
 // (a)-probe sizes: at most A_LIMIT newly visible hashes per verification (more:

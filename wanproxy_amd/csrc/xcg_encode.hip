@@ -1581,19 +1581,24 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
 // (a tile at t is declared while examining window t + 2048, xcodec_encoder.cc:
 // 183-190, so it is visible to the windows of every later piece) -- every lookup
 // misses, and encode() declares exactly the tiles (:222-261) and escapes the
-// tail (:267-269).  The screen rolls every window of a chunk through the round's
+// tail (:267-269).
+//
+// stream_screen_kernel rolls every window of a chunk through the round's
 // filters (a 128 KiB LDS fold of the global lane filter, then the global filter
-// and the fingerprint buckets for what passes), compares it with the chunk's
-// earlier tiles, and checks each tile's own window exactly (a tile is in the
-// batch table as this chunk's own declaration; anything else there or in the
-// persistent cache is a possible hit).  Chunks it cannot clear -- any possible
-// hit, an unaligned start, more than SCREEN_MAXD tiles -- go on a work list for
-// encode_stream_kernel, which parses them as always; the others get the tiling
-// output, declaration rows and counters here.  Either way the output is the
+// and the fingerprint buckets for what passes) and compares it with the
+// chunk's earlier tiles; it writes the chunk's tiling output and stages its
+// rows, with no dependent lookups, the next chunk's loads in flight meanwhile.
+// screen_finish_kernel (a thread per chunk) checks each tile's own window
+// exactly -- a tile is in the batch table as this chunk's own declaration;
+// anything else there or in the persistent cache is a possible hit -- and
+// either commits the staged rows and counters or puts the chunk on the work
+// list encode_stream_kernel parses as always (any possible hit, an unaligned
+// start, more than SCREEN_MAXD tiles).  Either way the output is the
 // sequential encoder's: the screen only skips parses whose every lookup misses.
 constexpr int SCREEN_MAXD = 4;                       // chunks shorter than 4 tiles (< 8 KiB)
 constexpr uint32_t SCREEN_FOLD_WORDS = 32768;        // 128 KiB of LDS
-constexpr int SCREEN_W = 16;                         // waves per workgroup (one workgroup per CU)
+constexpr int SCREEN_W = 12;                         // waves per workgroup (one workgroup per CU)
+constexpr uint32_t SCR_NEEDY = 1u << 31, SCR_SKIP = 1u << 30;   // s_info flags
 __device__ __forceinline__ uint32_t fold_word_of(uint32_t k, uint32_t fwm) { return (k >> 10) & fwm; }
 
 // The LDS fold of the global lane filter: word j of the fold = OR of the global
@@ -1609,103 +1614,204 @@ __global__ __launch_bounds__(256) void screen_fold_kernel(const uint32_t* gf, ui
   fold[i] = w;
 }
 
-__device__ __forceinline__ uint32_t sel4(int l, const uint32_t (&v)[SCREEN_MAXD]) {
-  return l == 0 ? v[0] : (l == 1 ? v[1] : (l == 2 ? v[2] : v[3]));
+// What the screen stages: per chunk s_info = flags | tiles << 16 | output
+// length, its tiles' rows (lo, hi, position, output length after it), and the
+// keys of its windows that passed the LDS fold (qcnt of them), for the probe.
+constexpr uint32_t SCREEN_QCAP = 1024;               // fold passes kept per chunk (more: the parse)
+struct ScreenStage {
+  uint32_t* info;      // [n]
+  uint4* rows;         // [n * SCREEN_MAXD]
+  uint32_t* qcnt;      // [n]
+  uint32_t* qkeys;     // [n * SCREEN_QCAP]
+};
+
+// What the screen reads (a slim copy of EncParams: kernel arguments live in
+// SGPRs, and the screen needs few of them).
+struct ScreenParams {
+  const uint8_t* in;
+  const uint64_t* chunk_off;
+  const uint32_t* chunk_len;
+  const uint64_t* out_off;
+  uint8_t* out;
+  const uint4* decl;
+  const uint32_t* ndecl;
+  uint32_t* changed;
+  const uint32_t* need;
+  uint32_t n, skip_below, max_len, maxd;
+};
+
+// The lanes' chunk metadata for chunks base + k * stride (lane k).
+struct ScreenMeta {
+  uint64_t off, oo;
+  uint32_t len, nold, go;
+};
+
+__device__ __forceinline__ ScreenMeta screen_meta(const ScreenParams& prm, uint32_t ck) {
+  ScreenMeta m{0ull, 0ull, 0u, 0u, 0u};
+  if (ck < prm.n && ck >= prm.skip_below && (!prm.need || prm.need[ck] != 0u)) {
+    m.go = 1u;
+    m.off = prm.chunk_off[ck];
+    m.oo = prm.out_off[ck];
+    m.len = prm.chunk_len[ck];
+    m.nold = prm.ndecl[ck];
+  }
+  return m;
 }
 
-// Returns true when the chunk needs the full parse (the screen wrote nothing
-// that matters then: its speculative tile bodies are overwritten).
-__device__ __forceinline__ bool screen_chunk(const EncParams& prm, const uint32_t* F, uint32_t fwm, uint32_t chunk) {
+// Where a chunk is (wave-uniform, read from the lanes that loaded it: no
+// memory wait inside the chunk loop), its first piece's A and B halves and
+// its old rows (lane i: row i), all loaded while the chunk before it rolls.
+struct ScreenLoad {
+  uint64_t off, oo;    // input offset, output offset
+  int L;
+  uint32_t nold;       // its rows of the last round
+  bool go;             // screened (not skipped by the round)
+  u32x4 a0, a1, b0, b1;
+  uint4 ov;
+};
+
+__device__ __forceinline__ bool screen_shape(int L, uint64_t off, const uint8_t* in) {
+  return L >= SEG && !(L & (SEG - 1)) && L / SEG < SCREEN_MAXD && !(off & 15u) && !((uintptr_t)in & 15u);
+}
+
+__device__ __forceinline__ void screen_issue(const ScreenParams& prm, const ScreenMeta& m, int k, uint32_t chunk,
+                                             ScreenLoad& s) {
   const int l = lane_id();
-  const uint8_t* x = prm.in + prm.chunk_off[chunk];
-  const int L = (int)prm.chunk_len[chunk];
-  if ((uint32_t)L > prm.max_len || L / SEG >= SCREEN_MAXD || L / SEG >= (int)prm.maxd) return true;
-  uint8_t* const out = prm.out + prm.out_off[chunk];
-  const uint32_t nold = readfirst(prm.ndecl[chunk]);
-  if (L < SEG) {                                   // xcodec_encoder.cc:77-83: no window at all
-    const uint32_t olen = L > 0 ? escape_u(out, x, 0, (uint32_t)L) : 0u;
-    if (l == 0) {
-      prm.out_len[chunk] = olen;
-      prm.ndecl[chunk] = 0u;
-      prm.nhits[chunk] = 0u;
-      if (nold != 0u) atomicMin(prm.changed, chunk);
-      if (prm.stats) {
-        prm.stats[4 * chunk + 0] = 0u; prm.stats[4 * chunk + 1] = 0u;
-        prm.stats[4 * chunk + 2] = 0u; prm.stats[4 * chunk + 3] = 0u;
-      }
-    }
-    return false;
+  s.go = readlane(m.go, k) != 0u;
+  s.off = readlane64(m.off, k);
+  s.oo = readlane64(m.oo, k);
+  s.L = (int)readlane(m.len, k);
+  s.nold = readlane(m.nold, k);
+  s.a0 = s.a1 = s.b0 = s.b1 = u32x4{0u, 0u, 0u, 0u};
+  s.ov = make_uint4(0u, 0u, 0u, 0u);
+  if (!s.go || !screen_shape(s.L, s.off, prm.in)) return;
+  const uint8_t* x = prm.in + s.off;
+  const int q0 = 32 * l;
+  s.a0 = load16_stream(x + q0);
+  s.a1 = load16_stream(x + q0 + 16);
+  if (s.L > SEG + 1) {
+    s.b0 = load16_stream(x + q0 + SEG);
+    s.b1 = load16_stream(x + q0 + SEG + 16);
   }
-  if (reinterpret_cast<uintptr_t>(x) & 15u) return true;   // (pieces = tiles needs an aligned start)
+  if ((uint32_t)l < s.nold && l < SCREEN_MAXD) s.ov = prm.decl[(uint64_t)chunk * prm.maxd + l];
+}
+
+// Pass 1 of one chunk whose loads `cur` issued: every window rolled through
+// the LDS fold; the passes queued for the probe, the tiling written, the rows
+// staged.  No memory wait but the loads `cur` made (the next chunk's go out
+// here).
+__device__ __forceinline__ void screen_chunk(const ScreenParams& prm, const uint32_t* F, uint32_t fwm, uint32_t chunk,
+                                             const ScreenLoad& cur, ScreenStage st, ScreenLoad& nxt,
+                                             const ScreenMeta& meta, int knext, uint32_t next_chunk) {
+  const int l = lane_id();
+  const int L = cur.L;
+  const uint8_t* x = prm.in + cur.off;
+  uint8_t* const out = prm.out + cur.oo;
+  const uint4 ov = cur.ov;
+  Piece P;
+  P.a0 = cur.a0; P.a1 = cur.a1; P.b0 = cur.b0; P.b1 = cur.b1;
+  if (knext < 64) screen_issue(prm, meta, knext, next_chunk, nxt);
+  else nxt.go = false;
+  auto verdict = [&](uint32_t v) {
+    if (l == 0) st.info[chunk] = v;
+  };
+  // Longer than the launch's bound, shorter than a window (only an escape,
+  // xcodec_encoder.cc:77-83), a tail after the tiles (escaped by the parse),
+  // or an unaligned start (pieces = tiles needs an aligned one): the parse.
+  if ((uint32_t)L > prm.max_len || L / SEG >= (int)prm.maxd || !screen_shape(L, cur.off, prm.in)) {
+    verdict(SCR_NEEDY);
+    return;
+  }
+  const uint32_t nold = cur.nold;
   const int last = L - SEG;                        // last window start
   const int nt = L / SEG;                          // tiles = pieces
   uint32_t tlo[SCREEN_MAXD] = {0u, 0u, 0u, 0u}, thi[SCREEN_MAXD] = {0u, 0u, 0u, 0u};
   uint32_t tk[SCREEN_MAXD] = {0u, 0u, 0u, 0u};
-  Piece P;
   P.sxb = 0u; P.sqxb = 0u;
   uint32_t totXA = 0, totTA = 0;
-  const uint32_t* const gf = prm.lf.gfilt;
-  const u32x4* const ftab = prm.lf.ftab;
+  uint32_t qn = 0;                                 // passes queued so far
+  uint32_t* const q = st.qkeys + (uint64_t)chunk * SCREEN_QCAP;
+  bool needy = false;
+  // the old rows are the tiling (the seeded round): their hi halves stand
+  const bool rows_tiling = nold == (uint32_t)nt;
 #pragma unroll 1
-  for (int i = 0; i < nt; ++i) {
+  for (int i = 0; i < nt && !needy; ++i) {
     const int p = SEG * i;
     const int q0 = p + 32 * l;
     const int pe = min(p + SEG, last + 1);         // piece end (exclusive)
     const bool one = pe - p == 1;                  // (a chunk of 2048 k bytes ends with a one-window piece)
     if (i == 0) {
-      P.a0 = load16_aligned_safe(x, q0, L);
-      P.a1 = load16_aligned_safe(x, q0 + 16, L);
       seg_sums(P.a0, P.a1, P.sxa, P.sqxa);
     } else {
       P.a0 = P.b0; P.a1 = P.b1;
       P.sxa = P.sxb; P.sqxa = P.sqxb;
+      if (!one) {
+        P.b0 = load16_stream(x + q0 + SEG);
+        P.b1 = load16_stream(x + q0 + SEG + 16);
+      }
     }
-    if (!one) {
-      P.b0 = load16_aligned_safe(x, q0 + SEG, L);
-      P.b1 = load16_aligned_safe(x, q0 + SEG + 16, L);
-      seg_sums(P.b0, P.b1, P.sxb, P.sqxb);
-    }
-    // start sums of the lane's first window (encode_chunk's piece setup)
-    const uint32_t qa = 32u * (uint32_t)l, qb = 2048u + 32u * (uint32_t)l;
-    const uint32_t ta = qa * P.sxa + P.sqxa, tb = one ? 0u : qb * P.sxb + P.sqxb;
+    // start sums of the lane's first window (encode_chunk's piece setup); a
+    // one-window piece needs only lane 0's, which are the carried totals
+    uint32_t tki;
+    uint32_t NX1 = 0, NX2 = 0, totXB = 0, totTB = 0;
+    const uint32_t qa = 32u * (uint32_t)l;
     if (i == 0) {
       totXA = wave_sum(P.sxa);
-      totTA = wave_sum(ta);
+      totTA = wave_sum(qa * P.sxa + P.sqxa);
     }
-    const uint32_t dx = (one ? 0u : P.sxb) - P.sxa, dt = tb - ta;
-    const uint32_t ix = wave_incl_scan(dx), it = wave_incl_scan(dt);
-    const uint32_t X1 = totXA + ix - dx;
-    const uint32_t TT = totTA + it - dt;
-    const uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
-    const uint32_t totXB = totXA + readlane(ix, 63);
-    const uint32_t totTB = totTA + readlane(it, 63) - 2048u * totXB;
-    uint32_t NX1 = 0u - X1, NX2 = 0u - X2c;
-    // the tile at the piece start: its hash, and its EXTRACT written ahead
-    // (encode_declaration :300-302; the body is this piece's A half)
-    const uint32_t tki = readfirst((NX1 << 20) + NX2);
-    const uint32_t thii = readfirst(lane_window_hi(P, 0));
+    if (one) {
+      tki = (0u - totXA) * (1u << 20) + (0u - (2048u * totXA - totTA + CLO));
+    } else {
+      seg_sums(P.b0, P.b1, P.sxb, P.sqxb);
+      const uint32_t qb = 2048u + qa;
+      const uint32_t ta = qa * P.sxa + P.sqxa, tb = qb * P.sxb + P.sqxb;
+      const uint32_t dx = P.sxb - P.sxa, dt = tb - ta;
+      const uint32_t ix = wave_incl_scan(dx), it = wave_incl_scan(dt);
+      const uint32_t X1 = totXA + ix - dx;
+      const uint32_t TT = totTA + it - dt;
+      const uint32_t X2c = (2048u + qa) * X1 - TT + CLO;
+      totXB = totXA + readlane(ix, 63);
+      totTB = totTA + readlane(it, 63) - 2048u * totXB;
+      NX1 = 0u - X1;
+      NX2 = 0u - X2c;
+      tki = readfirst((NX1 << 20) + NX2);
+    }
+    // the tile at the piece start: its hash (the old row's hi when the row is
+    // this tile), and its EXTRACT (encode_declaration :300-302; the body is
+    // this piece's A half)
+    const uint32_t oz = readlane(ov.z, i), ox = readlane(ov.x, i), oy = readlane(ov.y, i);
+    const uint32_t thii = rows_tiling && oz == (uint32_t)p && ox == 0u - tki ? oy : readfirst(lane_window_hi(P, 0));
+    bool own = false;
 #pragma unroll
-    for (int u = 0; u < SCREEN_MAXD; ++u)
+    for (int u = 0; u < SCREEN_MAXD; ++u) {
+      if (u < i) own |= tki == tk[u];
       if (u == i) { tk[u] = tki; tlo[u] = 0u - tki; thi[u] = thii; }
+    }
     {
       uint8_t* dst = out + (uint32_t)(2 + SEG) * (uint32_t)i;
       if (l < 2) dst[l] = (uint8_t)(l == 0 ? MAGIC : OP_EXTRACT);
       *(u32x4_u*)(dst + 2 + 32 * l) = P.a0;
       *(u32x4_u*)(dst + 2 + 32 * l + 16) = P.a1;
     }
-    // the tile's own window against the earlier tiles
-    bool own = false;
-#pragma unroll
-    for (int t = 0; t < SCREEN_MAXD - 1; ++t)
-      if (t < i) own |= tki == tk[t];
-    if (own) return true;
-    if (one) {
-      totXA = totXB; totTA = totTB;
-      continue;
+    if (own) {                                     // the tile's own window = an earlier tile
+      needy = true;
+      break;
     }
+    if (one) continue;
     // every other window of the piece: the round's filters, the earlier tiles
     const uint32_t xa[8] = {P.a0[0], P.a0[1], P.a0[2], P.a0[3], P.a1[0], P.a1[1], P.a1[2], P.a1[3]};
     const uint32_t xb[8] = {P.b0[0], P.b0[1], P.b0[2], P.b0[3], P.b1[0], P.b1[1], P.b1[2], P.b1[3]};
+    // positions past the last window are not positions; the piece start is the
+    // tile itself (checked exactly by the probe).  (A window past the last one
+    // that equals an earlier tile only costs the screen this chunk.)
+    const int nvalid = pe - q0;
+    uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
+    if (l == 0) vm &= ~1u;
+    // own earlier tiles: only a full piece after the first has one (chunks are
+    // 2, 4 or 6 KiB; the last piece of each is one window), tile 0
+    const uint32_t ko = tk[0];
+    const uint32_t fbm = fwm << 2;                 // fold byte offset = K bits 10.. as a word index
+    const char* const Fb = (const char*)F;
     uint32_t kk[32];
     uint32_t pass = 0u;
     uint64_t ownl = 0;   // lanes with a window equal to an earlier tile (lane masks: no VGPRs)
@@ -1725,125 +1831,163 @@ __device__ __forceinline__ bool screen_chunk(const EncParams& prm, const uint32_
         }
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) fw[t] = F[fold_word_of(kk[4 * g + t], fwm)];
+      for (int t = 0; t < 4; ++t) fw[t] = *(const uint32_t*)(Fb + ((kk[4 * g + t] >> 8) & fbm));
     };
-    roll4(0, fwc);
+    auto roll = [&](auto own_t) {
+      constexpr bool OWN = decltype(own_t)::value;
+      roll4(0, fwc);
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      if (g < 7) roll4(g + 1, fwn);
+      for (int g = 0; g < 8; ++g) {
+        if (g < 7) roll4(g + 1, fwn);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = 4 * g + t;
-        pass |= gfilt_test(fwc[t], kk[j]) << j;
-#pragma unroll
-        for (int u = 0; u < SCREEN_MAXD - 1; ++u)
-          if (u < i) ownl |= lanes_eq(kk[j], tk[u]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (g < 7) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) fwc[t] = fwn[t];
-      }
-    }
-    // positions past the last window are not positions; the piece start is the
-    // tile itself (checked exactly below)
-    const int nvalid = pe - q0;
-    uint32_t vm = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)max(nvalid, 0)) - 1u);
-    if (l == 0) vm &= ~1u;
-    pass &= vm;
-    // (a window past the last one that equals an earlier tile only costs the
-    // screen this chunk)
-    if (ownl) return true;
-    if (ballot(pass != 0u)) {
-      // the global lane filter for what passed the fold (16 loads in flight at
-      // a time: registers)
-      uint32_t pass2 = 0u;
-#pragma unroll
-      for (int h = 0; h < 32; h += 8) {
-        uint32_t gw[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          gw[j] = 0u;
-          if ((pass >> (h + j)) & 1u) gw[j] = gf[gfilt_word(kk[h + j], prm.lf.gmask)];
+        for (int t = 0; t < 4; ++t) {
+          const int j = 4 * g + t;
+          // gfilt_test as two bit extracts (v_bfe takes the offset mod 32)
+          const uint32_t b = __builtin_amdgcn_ubfe(fwc[t], kk[j], 1u) & __builtin_amdgcn_ubfe(fwc[t], kk[j] >> 5, 1u);
+          pass |= b << j;
+          if (OWN) ownl |= lanes_eq(kk[j], ko);
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pass2 |= ((pass >> (h + j)) & gfilt_test(gw[j], kk[h + j]) & 1u) << (h + j);
         __builtin_amdgcn_sched_barrier(0);
-      }
-      if (ballot(pass2 != 0u)) {
-        // the fingerprint buckets for the few left
-        bool m = false;
+        if (g < 7) {
 #pragma unroll
-        for (int h = 0; h < 32; h += 4) {
-          if (ballot(((pass2 >> h) & 15u) != 0u) == 0) continue;
-          u32x4 q[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            q[j] = u32x4{0u, 0u, 0u, 0u};
-            if ((pass2 >> (h + j)) & 1u) q[j] = ftab[fbucket(kk[h + j], prm.lf.fmask)];
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) m |= ((pass2 >> (h + j)) & 1u) && ftab_match(q[j], kk[h + j]);
-          __builtin_amdgcn_sched_barrier(0);
+          for (int t = 0; t < 4; ++t) fwc[t] = fwn[t];
         }
-        if (ballot(m)) return true;
       }
+    };
+    if (i > 0) roll(std::integral_constant<bool, true>{});
+    else roll(std::integral_constant<bool, false>{});
+    pass &= vm;
+    if (ownl) {
+      needy = true;
+      break;
     }
+    // the fold's passes, queued for the probe (stores only: nothing waits)
+    const uint32_t cnt = (uint32_t)__builtin_popcount(pass);
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t tot = readlane(incl, 63);
+    if (qn + tot > SCREEN_QCAP) {
+      needy = true;
+      break;
+    }
+    uint32_t* const ql = q + qn + incl - cnt;
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if ((pass >> j) & 1u) ql[__builtin_popcount(pass & ((1u << j) - 1u))] = kk[j];
+    qn += tot;
     totXA = totXB; totTA = totTB;
   }
-  // Each tile's own window, exactly: in the persistent cache, or declared in the
-  // batch anywhere but here, it may be found.
-  const uint32_t mylo = sel4(l, tlo), myhi = sel4(l, thi);
-  bool hit = false;
-  if (l < nt) {
-    if (readfirst(*prm.nseg) != 0u && tab_lookup_t(prm.g, mylo, myhi) != ~0ull) hit = true;
-    if (prm.use_b) {
-      const uint64_t bv = tab_lookup_t(prm.b, mylo, myhi);
-      if (bv != ~0ull && ((uint32_t)(bv >> 32) < chunk || ((uint32_t)(bv >> 32) == chunk && (uint32_t)bv != (uint32_t)(SEG * l))))
-        hit = true;
-    }
+  if (needy) {
+    verdict(SCR_NEEDY);
+    return;
   }
-  if (ballot(hit)) return true;
-  // the cold parse: the tiles (written above), then the escaped tail
-  uint32_t olen = (uint32_t)(2 + SEG) * (uint32_t)nt;
-  if (SEG * nt < L) olen += escape_u(out + olen, x, (uint32_t)(SEG * nt), (uint32_t)L);
+  // the cold parse: the tiles (written above), no tail
+  const uint32_t olen = (uint32_t)(2 + SEG) * (uint32_t)nt;
+  // its rows, staged; against the round's old ones (a change flagged now is
+  // conservative: the chunk may still go to the parse)
   bool diff = nold != (uint32_t)nt;
+  uint4 nv = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int u = 0; u < SCREEN_MAXD; ++u)
+    if (l == u) nv = make_uint4(tlo[u], thi[u], (uint32_t)(SEG * u), (uint32_t)(2 + SEG) * (uint32_t)(u + 1));
   if (l < nt) {
-    uint4* dl = prm.decl + (uint64_t)chunk * prm.maxd;
-    const uint4 nv = make_uint4(mylo, myhi, (uint32_t)(SEG * l), (uint32_t)(2 + SEG) * (uint32_t)(l + 1));
-    if ((uint32_t)l < nold) {
-      const uint4 ov = dl[l];
-      diff |= ov.x != nv.x || ov.y != nv.y || ov.z != nv.z;
-    }
-    dl[l] = nv;
+    if ((uint32_t)l < nold) diff |= ov.x != nv.x || ov.y != nv.y || ov.z != nv.z;
+    st.rows[(uint64_t)chunk * SCREEN_MAXD + l] = nv;
   }
   if (ballot(diff) != 0 && l == 0) atomicMin(prm.changed, chunk);
-  if (l == 0) {
-    prm.ndecl[chunk] = (uint32_t)nt;
-    prm.nhits[chunk] = 0u;
-    prm.out_len[chunk] = olen;
-    if (prm.stats) {
-      prm.stats[4 * chunk + 0] = (uint32_t)nt; prm.stats[4 * chunk + 1] = 0u;
-      prm.stats[4 * chunk + 2] = 0u; prm.stats[4 * chunk + 3] = (uint32_t)nt;
-    }
-  }
-  return false;
+  if (l == 0) st.qcnt[chunk] = qn;
+  verdict(((uint32_t)nt << 16) | olen);
 }
 
-// Persistent workgroups of SCREEN_W waves over the chunks (those a
-// verification round leaves standing are skipped); the ones that need the full
-// parse are appended to work[1..] (work[0] counts them).
-__global__ __launch_bounds__(64 * SCREEN_W) void stream_screen_kernel(EncParams prm, const uint32_t* fold,
-                                                                      uint32_t fwords, uint32_t* work) {
+// Pass 1: persistent workgroups of SCREEN_W waves over the chunks; a wave's
+// chunks chunk0, chunk0 + stride, ... in groups of 64 whose metadata lane k
+// holds.
+__global__ __launch_bounds__(64 * SCREEN_W) void stream_screen_kernel(ScreenParams prm, const uint32_t* fold,
+                                                                      uint32_t fwords, ScreenStage st) {
   __shared__ uint32_t F[SCREEN_FOLD_WORDS];
   for (uint32_t i = threadIdx.x; i < fwords / 4; i += blockDim.x) ((u32x4*)F)[i] = ((const u32x4*)fold)[i];
-  __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
   const uint32_t stride = gridDim.x * SCREEN_W;
-  for (uint32_t chunk = blockIdx.x * SCREEN_W + (uint32_t)wv; chunk < prm.n; chunk += stride) {
-    if (chunk < prm.skip_below) continue;
-    if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;
-    if (screen_chunk(prm, F, fwords - 1u, chunk) && lane_id() == 0) work[1 + atomicAdd(work, 1u)] = chunk;
+  __syncthreads();
+  for (uint32_t base = blockIdx.x * SCREEN_W + (uint32_t)wv; base < prm.n; base += 64u * stride) {
+    const ScreenMeta meta = screen_meta(prm, base + (uint32_t)lane_id() * stride);
+    ScreenLoad cur, nxt;
+    screen_issue(prm, meta, 0, base, cur);
+    for (int k = 0; k < 64; ++k) {
+      const uint32_t chunk = base + (uint32_t)k * stride;
+      if (chunk >= prm.n) break;
+      if (!cur.go) {
+        if (lane_id() == 0) st.info[chunk] = SCR_SKIP;
+        if (k + 1 < 64) screen_issue(prm, meta, k + 1, chunk + stride, nxt);
+        else nxt.go = false;
+      } else {
+        screen_chunk(prm, F, fwords - 1u, chunk, cur, st, nxt, meta, k + 1, chunk + stride);
+      }
+      cur = nxt;
+    }
+  }
+}
+
+// Pass 2, a wave per chunk: the queued fold passes through the global lane
+// filter and the fingerprint buckets, the tiles' own windows exactly (the
+// persistent cache; the batch table, where a tile is this chunk's own
+// declaration and anything else a possible hit); then either the staged rows
+// and counters go in, or the chunk joins the work list (work[0] counts it).
+__global__ __launch_bounds__(256) void screen_finish_kernel(EncParams prm, ScreenStage st, uint32_t* work) {
+  const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
+  const int l = lane_id();
+  if (c >= prm.n) return;
+  const uint32_t info = readfirst(st.info[c]);
+  if (info & SCR_SKIP) return;
+  bool needy = (info & SCR_NEEDY) != 0u;
+  const uint32_t nt = (info >> 16) & 0xFFu;
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (!needy) {
+    const uint32_t qn = readfirst(st.qcnt[c]);
+    const uint32_t* const q = st.qkeys + (uint64_t)c * SCREEN_QCAP;
+    if ((uint32_t)l < nt) r = st.rows[(uint64_t)c * SCREEN_MAXD + l];
+    bool hit = false;
+    // up to 8 keys per lane in flight: their filter words, then (rarely) buckets
+    for (uint32_t j0 = 0; j0 < qn; j0 += 512) {
+      uint32_t k[8], w[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t j = j0 + 64u * t + (uint32_t)l;
+        k[t] = j < qn ? q[j] : 0u;
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t j = j0 + 64u * t + (uint32_t)l;
+        w[t] = j < qn ? prm.lf.gfilt[gfilt_word(k[t], prm.lf.gmask)] : 0u;
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t j = j0 + 64u * t + (uint32_t)l;
+        if (j < qn && gfilt_test(w[t], k[t])) hit |= ftab_match(prm.lf.ftab[fbucket(k[t], prm.lf.fmask)], k[t]);
+      }
+    }
+    if ((uint32_t)l < nt) {
+      if (*prm.nseg != 0u && tab_lookup_t(prm.g, r.x, r.y) != ~0ull) hit = true;
+      if (prm.use_b) {
+        const uint64_t bv = tab_lookup_t(prm.b, r.x, r.y);
+        if (bv != ~0ull && ((uint32_t)(bv >> 32) < c || ((uint32_t)(bv >> 32) == c && (uint32_t)bv != r.z)))
+          hit = true;
+      }
+    }
+    needy = ballot(hit) != 0;
+  }
+  if (needy) {
+    if (l == 0) work[1 + atomicAdd(work, 1u)] = c;
+    return;
+  }
+  if ((uint32_t)l < nt) prm.decl[(uint64_t)c * prm.maxd + l] = r;
+  if (l == 0) {
+    prm.ndecl[c] = nt;
+    prm.nhits[c] = 0u;
+    prm.out_len[c] = info & 0xFFFFu;
+    if (prm.stats) {
+      prm.stats[4 * c + 0] = nt; prm.stats[4 * c + 1] = 0u;
+      prm.stats[4 * c + 2] = 0u; prm.stats[4 * c + 3] = nt;
+    }
   }
 }
 
@@ -2671,7 +2815,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   };
   // The quiet-chunk screen (stream_screen_kernel) in front of the parse: small
   // chunks, in-band, not the bounded / pair variants (which record references).
-  const bool screen = a->s_fold && a->s_work && !a->ev && !(a->flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) &&
+  const bool screen = a->s_fold && a->s_work && a->s_info && a->s_rows && a->s_qcnt && a->s_qkeys && !a->ev && !(a->flags & (XCG_FLAG_OOB | XCG_FLAG_NULLCACHE)) &&
                       a->maxd <= (uint32_t)SCREEN_MAXD && xcg_screen_on();
   // bounded cache: the variant that records the chunks' cache references (xcg_lru.hip)
   auto launch = [&]() {
@@ -2681,8 +2825,12 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       hipLaunchKernelGGL(screen_fold_kernel, dim3((fwords + 255) / 256), dim3(256), 0, stream, prm.lf.gfilt, gwords,
                          a->s_fold, fwords);
       (void)hipMemsetAsync(a->s_work, 0, 4, stream);
-      hipLaunchKernelGGL(stream_screen_kernel, dim3(wgs), dim3(64 * SCREEN_W), 0, stream, prm, (const uint32_t*)a->s_fold,
-                         fwords, a->s_work);
+      const ScreenStage sst{a->s_info, (uint4*)a->s_rows, a->s_qcnt, a->s_qkeys};
+      const ScreenParams sp{prm.in, prm.chunk_off, prm.chunk_len, prm.out_off, prm.out, prm.decl, prm.ndecl,
+                            prm.changed, prm.need, prm.n, prm.skip_below, prm.max_len, prm.maxd};
+      hipLaunchKernelGGL(stream_screen_kernel, dim3(wgs), dim3(64 * SCREEN_W), 0, stream, sp, (const uint32_t*)a->s_fold,
+                         fwords, sst);
+      hipLaunchKernelGGL(screen_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, prm, sst, a->s_work);
       prm.work = a->s_work;
       if (xcg_screen_counting()) {
         uint32_t w = 0;
