@@ -445,6 +445,52 @@ def run_c5pair(args):
                        'decoded back (unbounded decoder)'}
 
 
+def run_c5dense(args):
+    """The C5-PAIR cache (wanproxy.conf's pair, --lru-mib / --disk-mib) on
+    REF-dense data: the shard's size drawn from a pool of --dense-pool
+    segments (synth.dense), so an entity takes thousands of references per
+    sub-batch -- the pair replay's long-run case.  Checked against the oracle's
+    pair and decoded back."""
+    from oracle.lib import Oracle
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import Context
+    nbytes = int(1 << 30 if args.scale >= 1 else max(1 << 22, int((1 << 30) * args.scale)))
+    data = np.frombuffer(synth.dense(0xC5D, nbytes, args.dense_pool), np.uint8).copy()
+    offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
+    limit = max(2048, int(args.lru_mib * MiB * min(1.0, args.scale * 8)))
+    disk = max(1 << 20, int(args.disk_mib * MiB * min(1.0, args.scale * 8)))
+    ctx = Context(torch_dev(args), memory_cache_limit=limit, disk_bytes=disk)
+    per = max(1, args.batch_mib * MiB // (128 * KiB))
+    B = Batches(ctx, data, offs, lens, per=per)
+    clock = {}
+    wall = timed_encode(B, args.reps, clock=clock)
+    got = B.outputs()
+    st = ctx.pair_stats()
+    k = min(len(got), max(64, int(args.lru_check * len(got))))
+    o = Oracle()
+    c = o.cache_new_pair(limit, disk)
+    exp = o.encode_batch(data, offs[:k], lens[:k], mode=1, cache=c)
+    o.cache_free(c)
+    if got[:k] != exp:
+        bad = next(i for i in range(k) if got[i] != exp[i])
+        raise SystemExit(f'PARITY FAILURE (c5dense) at chunk {bad}')
+    dec = data.tobytes()
+    if not args.no_decode:
+        dctx = Context(torch_dev(args), cache_segments=args.dense_pool + 4096)
+        dec, _ = decode_device(dctx, got, per=per, chunk=128 * KiB)
+        dctx.close()
+    if dec != data.tobytes():
+        raise SystemExit('ROUND TRIP FAILURE (c5dense)')
+    ctx.close()
+    inb = data.size
+    return {'config': 'REF-dense: %d MiB in 128 KiB chunks from a pool of %d segments, XCodecCachePair(%d MiB LRU '
+                      'memory, %d MiB disk)' % (nbytes >> 20, args.dense_pool, limit >> 20, disk >> 20),
+            'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
+            'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds, 'kernel': clock,
+            'pair_stats': {'primary_entries': st[0], 'disk_entries': st[1], 'disk_written': st[2]},
+            'checked': f'{checked(k, len(got))} vs the oracle with the same pair; decoded back'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('configs', nargs='*', default=['c2s', 'c3', 'c4', 'c5'])
@@ -456,11 +502,13 @@ def main():
     ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
     ap.add_argument('--disk-laps', type=float, default=0, help='c5pair: size the disk so the data laps it')
+    ap.add_argument('--dense-pool', type=int, default=4096, help='c5dense: distinct segments')
     ap.add_argument('--no-decode', action='store_true', help='skip the decode round trips (profiling runs)')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5, 'c5lru': run_c5lru, 'c5pair': run_c5pair}
+    fns = {'c2s': run_c2s, 'c3': run_c3, 'c4': run_c4, 'c5': run_c5, 'c5lru': run_c5lru, 'c5pair': run_c5pair,
+           'c5dense': run_c5dense}
     for c in args.configs:
         t0 = time.perf_counter()
         r = fns[c](args)

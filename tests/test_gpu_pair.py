@@ -129,3 +129,40 @@ def test_pair_create_rejects():
         Context(0, memory_cache_limit=1 << 20, disk_bytes=222 * 2048)     # no index block
     with pytest.raises(XCGError):
         Context(0, out_of_band=True, memory_cache_limit=1 << 20, disk_bytes=1 << 20)
+
+
+@pytest.mark.parametrize('geom', [(8, 1, 16), (40, 2, 64), (3, 1, 200), (150, 4, 1000)])
+def test_pair_ref_dense_vs_oracle(oracle, geom):
+    """REF-dense streams (synth.dense: blocks from a pool of `distinct`
+    segments): an entity takes hundreds of references per sub-batch, a small
+    primary evicts constantly and a one- or two-block disk dies and is touched
+    again many times -- the replay's runs are long (segmented scans, not walks).
+    Encode against the oracle's pair (output and disk counters), then a pair
+    decoder with the same geometry, in batches, decodes every frame back."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    lim, nb, distinct = geom
+    d = synth.dense(0xDE0 + distinct, 8 << 20, distinct)
+    offs, lens = synth.chunks_of(d, 65536)
+    limit, disk = lim * 2048, mpg.disk_bytes(nb)
+    c = oracle.cache_new_pair(limit, disk)
+    exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    est = oracle.pair_stats(c)
+    oracle.cache_free(c)
+    assert sum(map(len, exp)) < len(d) // 4           # (mostly REFs)
+    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    got = ctx.encode_chunks(d, offs, lens, semantics=XCG_SEM_STREAM)
+    st = ctx.pair_stats()
+    ctx.close()
+    bad = [i for i in range(len(got)) if got[i] != exp[i]]
+    assert not bad, (geom, bad[:5])
+    assert (st[1], st[2]) == est
+    dctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    outs = []
+    for a in range(0, len(exp), 16):
+        o, s, _, unk = dctx.decode_chunks(exp[a:a + 16])
+        assert not (s != 0).any() and not unk, (geom, a)
+        outs += o
+    dctx.close()
+    assert b''.join(outs) == d

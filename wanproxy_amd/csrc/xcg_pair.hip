@@ -154,6 +154,15 @@ struct PairDev {
   uint64_t* ddeath;                       // [np] death clock of the entity's disk entry current at the row
   uint32_t* erep;                         // [newb] (decode) position of the REPLACE that ends it (NIL)
   uint32_t* erun;                         // [etot] sorted index of the entity's first element (NIL)
+  uint32_t* erend;                        // [etot] one past its last element
+  uint64_t* einit;                        // [etot] disk entry current before the entity's first element
+  uint32_t* ecov;                         // [etot] (leave) initial coverage end (NIL: to the end)
+  uint32_t* egap;                         // [etot] (leave) first uncovered position found at a span start
+  uint32_t* etail;                        // [etot] (leave) coverage end after the entity's last element
+  uint64_t* sa;                           // [np + 1] segmented-scan input / output
+  uint64_t* sb;
+  uint32_t* nq;                           // [np + 1] next element of the run that can touch (NIL)
+  uint8_t* tnew;                          // [np + 1] touches of the running round
   uint32_t* slow;                         // positions for the block table
   uint32_t* tab;                          // [nbk * (nbk + 1)] 2-D prefix counts
   uint32_t bsh, nbk;                      // table block = 1 << bsh positions
@@ -370,26 +379,48 @@ __global__ __launch_bounds__(256) void pr_resolve_kernel(PairDev d) {
   if (pos == 0) { d.isr[d.np] = 0u; d.app[d.np] = 0u; }
 }
 
-// Decode HIT resolution over rows sorted by (hash, position): sk = hash rank
-// key is not needed -- the sort is by hash (64-bit keys, stable), values are
-// positions.  For every HIT: walk back in its hash run to the latest ENTER /
-// REPL; if none, the first GHIT of the run before it.
-__global__ __launch_bounds__(256) void pr_dec_hits_kernel(PairDev d, const uint64_t* hk, const uint32_t* hv,
-                                                          uint32_t m) {
+// Segmented scans.  Runs (an entity's elements in the entity-sorted order, a
+// hash's in the hash-sorted one) are numbered in ascending order, so a max-scan
+// of (run << 32 | v) never carries a value across runs: an element's scan value
+// belongs to its own run iff its upper half is the run's number.  v = 0 is
+// "none"; indices and positions are stored + 1.
+__device__ __forceinline__ uint64_t pk(uint32_t run, uint32_t v) { return ((uint64_t)run << 32) | v; }
+__device__ __forceinline__ uint32_t in_run(uint64_t s, uint32_t run) { return (uint32_t)(s >> 32) == run ? (uint32_t)s : 0u; }
+
+// Decode HIT resolution over rows sorted by (hash, position) (hk / hv, m rows):
+// a HIT resolves to the latest ENTER / REPL of its hash before it, else to the
+// first GHIT of the hash before it.  Step 1: run heads (-> run numbers by a
+// scan); step 2: per run the first GHIT (atomicMin) and per row the packed
+// latest-definer value (-> max-scan); step 3: the resolution.
+__global__ __launch_bounds__(256) void pr_dh_heads_kernel(const uint64_t* hk, uint32_t m, uint32_t* head) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= m) head[i] = (i < m && (i == 0 || hk[i - 1] != hk[i])) ? 1u : 0u;
+}
+__global__ __launch_bounds__(256) void pr_dh_vals_kernel(PairDev d, const uint32_t* hv, uint32_t m, const uint32_t* head,
+                                                         const uint32_t* hrank, uint32_t* fg) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t r = hrank[i] + head[i] - 1u;        // this row's run
+  const uint32_t q = hv[i];
+  const uint8_t kq = d.kind[q];
+  if (kq == K_LOOKUP && d.ent[q] != NIL && d.ent[q] < d.newb) atomicMin(fg + r, i);
+  d.sa[i] = pk(r, (kq == K_ENTER || kq == K_REPL) ? i + 1u : 0u);
+}
+__global__ __launch_bounds__(256) void pr_dec_hits_kernel(PairDev d, const uint32_t* hv, uint32_t m, const uint32_t* head,
+                                                          const uint32_t* hrank, const uint32_t* fg) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint32_t pos = hv[i];
   if (d.kind[pos] != K_LOOKUP || d.ent[pos] != NIL) return;
-  const uint64_t h = hk[i];
-  uint32_t x = NIL, first_ghit = NIL;
-  for (int64_t j = (int64_t)i - 1; j >= 0 && hk[j] == h; --j) {
-    const uint32_t q = hv[j];
-    const uint8_t kq = d.kind[q];
-    if (kq == K_ENTER) { x = d.ent[q]; break; }
-    if (kq == K_REPL) { x = d.yent[q]; break; }
-    if (kq == K_LOOKUP && d.ent[q] != NIL && d.ent[q] < d.newb) first_ghit = d.ent[q];
+  const uint32_t r = hrank[i] + head[i] - 1u;
+  const uint32_t v = in_run(d.sb[i], r);
+  uint32_t x = NIL;
+  if (v) {
+    const uint32_t q = hv[v - 1u];
+    x = d.kind[q] == K_ENTER ? d.ent[q] : d.yent[q];
+  } else if (fg[r] < i) {
+    x = d.ent[hv[fg[r]]];
   }
-  if (x == NIL) x = first_ghit;
   if (x == NIL) {
     atomicOr(&d.cnt->nohit, 1u);
     return;
@@ -398,24 +429,28 @@ __global__ __launch_bounds__(256) void pr_dec_hits_kernel(PairDev d, const uint6
 }
 
 // Per sorted element: the entity's previous / next reference (GMISS rows are
-// not references) and the first element of each entity's run.
+// not references) and the bounds of each entity's run.  prv = the latest
+// non-GMISS element before it in the run (an exclusive max-scan); each
+// reference's successor is written by that successor (nxt starts at -1).
+__global__ __launch_bounds__(256) void pr_link_vals_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = d.sk[i];
+  if (e >= d.etot) { d.sa[i] = pk(d.etot, 0u); return; }
+  if (i == 0 || d.sk[i - 1] != e) d.erun[e] = i;
+  if (i + 1 == d.np || d.sk[i + 1] != e) d.erend[e] = i + 1;
+  d.sa[i] = pk(e, d.kind[d.sv[i]] != K_GMISS ? i + 1u : 0u);
+}
 __global__ __launch_bounds__(256) void pr_links_kernel(PairDev d) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.np) return;
   const uint32_t e = d.sk[i];
   if (e >= d.etot) return;
   const uint32_t pos = d.sv[i];
-  if (i == 0 || d.sk[i - 1] != e) d.erun[e] = i;
-  int64_t j = (int64_t)i - 1;
-  while (j >= 0 && d.sk[j] == e && d.kind[d.sv[j]] == K_GMISS) --j;
-  d.prv[pos] = (j >= 0 && d.sk[j] == e) ? (int32_t)d.sv[j] : -1;
-  if (d.kind[pos] != K_GMISS) {
-    uint32_t q = i + 1;
-    while (q < d.np && d.sk[q] == e && d.kind[d.sv[q]] == K_GMISS) ++q;
-    d.nxt[pos] = (q < d.np && d.sk[q] == e) ? (int32_t)d.sv[q] : -1;
-  } else {
-    d.nxt[pos] = -1;
-  }
+  const uint32_t v = in_run(d.sb[i], e);
+  const int32_t p = v ? (int32_t)d.sv[v - 1u] : -1;
+  d.prv[pos] = p;
+  if (p >= 0 && d.kind[pos] != K_GMISS) d.nxt[p] = (int32_t)pos;
 }
 
 // Decode REPLACE rows: the new entity continues the replaced one's place in
@@ -537,50 +572,104 @@ __device__ __forceinline__ uint64_t repl_entry(const PairDev& d, uint32_t rp) {
   return d.dclock0 + d.clk[rp] + d.tflag[rp];
 }
 
-// One fixed-point round of the disk clock.  Per entity run, in stream order:
-// the entity's current disk entry (the initial one, its ENTER's, or its last
+// One fixed-point round of the disk clock.  Per entity, in stream order: the
+// entity's current disk entry (the initial one, its ENTER's, or its last
 // touch's) and, at every primary hit, a touch if that entry has died by the
 // row's clock (XCodecDisk::touch re-enters the hash; an entry can die and be
 // re-entered more than once when the sub-batch laps a small disk).  Each row
 // also records the death clock of the entry current at it (presence checks).
-__global__ __launch_bounds__(256) void pr_touch_kernel(PairDev d) {
+//
+// Without walking a run: the touches of an entity are a chain -- from the
+// current entry (clock c), the next touch is the first element that can touch
+// (nq: a primary-hit lookup / REPLACE) at or after the first element whose clock
+// reaches death(c) (a binary search: clocks grow along the run).  A chain is as
+// long as the entity's entries die, at most a few per sub-batch.  Then every
+// row's current entry is its run's latest setter (ENTER / touch) before it: an
+// exclusive max-scan (pr_touch_rows_kernel).
+__global__ __launch_bounds__(256) void pr_nq_vals_kernel(PairDev d) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.np) return;
-  const uint32_t e = d.sk[i];
-  if (e >= d.etot || (i > 0 && d.sk[i - 1] == e)) return;
-  uint64_t cur = e < d.newb ? e0_of(d, e) : NOENT;
-  uint32_t last = NIL;
-  bool first = true;
-  uint32_t chg = 0;
-  for (uint32_t q = i; q < d.np && d.sk[q] == e; ++q) {
-    const uint32_t pos = d.sv[q];
-    if (pos < d.P) continue;
-    const uint8_t kk = d.kind[pos];
-    if (first && e >= d.newb && kk != K_ENTER) {       // a REPLACE-made entity: its first row is a HIT
-      const int32_t rp = d.prv[pos];
+  const uint32_t e = min(d.sk[i], d.etot);
+  const uint32_t pos = d.sv[i];
+  const uint8_t kk = d.kind[pos];
+  const bool can = e < d.etot && pos >= d.P && (kk == K_LOOKUP || kk == K_REPL) && d.phit[pos];
+  d.sa[d.np - 1u - i] = pk(e, can ? i : NIL);        // (reversed: a min-scan finds the next one)
+}
+__global__ __launch_bounds__(256) void pr_nq_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint64_t s = d.sb[d.np - 1u - i];
+  d.nq[i] = (uint32_t)(s >> 32) == d.sk[i] ? (uint32_t)s : NIL;
+}
+__global__ __launch_bounds__(256) void pr_touch_chain_kernel(PairDev d) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.etot) return;
+  const uint32_t i0 = d.erun[e];
+  if (i0 == NIL) return;
+  const uint32_t i1 = d.erend[e];
+  uint64_t cur = NOENT;
+  uint32_t last = NIL, start = i0;
+  if (e < d.newb) {
+    cur = e0_of(d, e);
+  } else {
+    const uint32_t p0 = d.sv[i0];
+    if (d.kind[p0] == K_ENTER) {
+      last = p0;
+      start = i0 + 1u;
+    } else {                                         // a REPLACE-made entity: its first row is a HIT
+      const int32_t rp = d.prv[p0];
       if (rp >= 0 && d.kind[rp] == K_REPL) cur = repl_entry(d, (uint32_t)rp);
     }
-    first = false;
-    const uint64_t ck = d.dclock0 + d.clk[pos];
+  }
+  d.einit[e] = cur;
+  if (last != NIL) cur = d.dclock0 + d.clk[last];
+  for (int guard = 0; guard < (1 << 20) && start < i1; ++guard) {
     const uint64_t dth = death_of(cur, d.nb);
-    d.ddeath[pos] = dth;
-    uint8_t t = 0;
-    if ((kk == K_LOOKUP || kk == K_REPL) && d.phit[pos] && ck >= dth) {
-      t = 1;
-      cur = ck;
-      last = pos;
-    } else if (kk == K_ENTER) {
-      cur = ck;
-      last = pos;
+    uint32_t lo = start, hi = i1;                    // first element whose clock reaches dth
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (d.dclock0 + d.clk[d.sv[mid]] >= dth) hi = mid; else lo = mid + 1u;
     }
-    if (d.tflag[pos] != t) {
-      d.tflag[pos] = t;
-      ++chg;
-    }
-    d.app[pos] = ((kk == K_ENTER || kk == K_REPL) ? 1u : 0u) + t;
+    if (lo >= i1) break;
+    const uint32_t j = d.nq[lo];
+    if (j == NIL || j >= i1) break;
+    const uint32_t pos = d.sv[j];
+    d.tnew[pos] = 1u;
+    cur = d.dclock0 + d.clk[pos];
+    last = pos;
+    start = j + 1u;
   }
   d.elast[e] = last;
-  if (chg) atomicAdd(&d.cnt->changed, chg);
+}
+__global__ __launch_bounds__(256) void pr_setter_vals_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = min(d.sk[i], d.etot);
+  const uint32_t pos = d.sv[i];
+  const bool set = e < d.etot && pos >= d.P && (d.kind[pos] == K_ENTER || d.tnew[pos]);
+  d.sa[i] = pk(e, set ? d.clk[pos] + 1u : 0u);
+}
+__global__ __launch_bounds__(256) void pr_touch_rows_kernel(PairDev d) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t chg = 0;
+  if (i < d.np) {
+    const uint32_t e = d.sk[i], pos = d.sv[i];
+    if (e < d.etot && pos >= d.P) {
+      const uint32_t v = in_run(d.sb[i], e);
+      const uint64_t cur = v ? d.dclock0 + (v - 1u) : d.einit[e];
+      d.ddeath[pos] = death_of(cur, d.nb);
+      const uint8_t t = d.tnew[pos];
+      d.tnew[pos] = 0u;
+      if (d.tflag[pos] != t) {
+        d.tflag[pos] = t;
+        chg = 1u;
+      }
+      const uint8_t kk = d.kind[pos];
+      d.app[pos] = ((kk == K_ENTER || kk == K_REPL) ? 1u : 0u) + t;
+    }
+  }
+  const uint64_t m = ballot(chg != 0u);
+  if (lane_id() == 0 && m) atomicAdd(&d.cnt->changed, (uint32_t)__builtin_popcountll(m));
 }
 
 // Presence at every recorded lookup: primary residency or a live disk entry.
@@ -645,7 +734,53 @@ __device__ __forceinline__ uint32_t death_row(const PairDev& d, uint64_t death) 
 // first position no primary span [reference, its exit) and no disk span
 // [append, death) covers.  Decode: also whether anything moved (the
 // classification repeats until not).
-__global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d, uint32_t M) {
+//
+// Spans start at the entity's elements, which are in position order, so the
+// first uncovered position is found with a max-scan instead of a walk: X(k) =
+// max(P, initial coverage, ends of the spans of elements before k); the first
+// element k starting past X(k) leaves a gap at X(k); without one the coverage
+// ends at X after the last element.
+__global__ __launch_bounds__(256) void pr_cover_kernel(PairDev d) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= d.newb) return;
+  const uint64_t e0 = e0_of(d, id);
+  d.ecov[id] = e0 == NOENT ? d.P : death_row(d, death_of(e0, d.nb));
+  d.egap[id] = NIL;
+  d.etail[id] = NIL;
+}
+// encoded span end: 0 none, NIL to the end, else end + 1
+__device__ __forceinline__ uint32_t span_end(const PairDev& d, uint32_t pos, uint8_t kk, uint32_t M) {
+  if (kk == K_GMISS) return 0u;
+  if (kk == K_REPL) return NIL;                      // (gone at the REPLACE: pr_leave_kernel)
+  const int32_t nx = d.nxt[pos];
+  const uint32_t b = (nx >= 0 && d.phit[nx]) ? (uint32_t)nx : evict_pos(d, pos, M);
+  uint32_t end = b == NIL ? NIL : b + 1u;
+  if (pos >= d.P && d.tflag[pos]) {                  // a touch's disk span [touch, death)
+    const uint32_t t = death_row(d, death_of(d.dclock0 + d.clk[pos], d.nb));
+    end = max(end, t == NIL ? NIL : t + 1u);
+  }
+  return end;
+}
+__global__ __launch_bounds__(256) void pr_span_vals_kernel(PairDev d, uint32_t M) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = min(d.sk[i], d.etot);
+  d.sa[i] = pk(e, e < d.newb ? span_end(d, d.sv[i], d.kind[d.sv[i]], M) : 0u);
+}
+__global__ __launch_bounds__(256) void pr_gaps_kernel(PairDev d, uint32_t M) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.np) return;
+  const uint32_t e = d.sk[i];
+  if (e >= d.newb) return;
+  const uint32_t pos = d.sv[i];
+  const uint32_t v = in_run(d.sb[i], e);
+  uint32_t x = max(d.ecov[e], d.P);                  // (NIL: covered to the end)
+  if (v) x = max(x, v == NIL ? NIL : v - 1u);
+  const uint32_t own = (uint32_t)d.sa[i];            // (this element's encoded end)
+  if (own && x != NIL && pos > x) atomicMin(d.egap + e, x);
+  if (i + 1u == d.erend[e]) d.etail[e] = (own == 0u || x == NIL) ? x : max(x, own == NIL ? NIL : own - 1u);
+}
+__global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= d.newb) return;
   uint64_t pt = NEVERT;
@@ -659,42 +794,14 @@ __global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d, uint32_t M) {
              tab_lookup_t(d.g, (uint32_t)k, (uint32_t)(k >> 32)) == id;
   }
   if (entity) {
-    const uint64_t e0 = e0_of(d, id);
-    const bool present_at_start = id < d.C || e0 != NOENT;
+    const bool present_at_start = id < d.C || e0_of(d, id) != NOENT;
     if (!present_at_start) {
       pt = 0;
     } else {
-      const uint32_t r0 = d.erun[id];
-      const uint32_t dr0 = e0 == NOENT ? d.P : death_row(d, death_of(e0, d.nb));
-      uint32_t cur = d.P, lv = NIL;
-      for (int guard = 0; guard < (1 << 22); ++guard) {
-        uint32_t to = NIL;
-        bool cov = false;
-        if (e0 != NOENT && (dr0 == NIL || cur < dr0)) { cov = true; to = dr0; }
-        if (!cov && r0 != NIL) {                     // a primary span [reference, its exit)
-          for (uint32_t q = r0; q < d.np && d.sk[q] == id; ++q) {
-            const uint32_t a = d.sv[q];
-            const uint8_t kk = d.kind[a];
-            if (kk == K_GMISS) continue;
-            if (a >= d.P && a > cur) break;          // (references are in order)
-            if (kk == K_REPL) { cov = true; to = NIL; break; }   // (gone at the REPLACE: below)
-            const int32_t nx = d.nxt[a];
-            const uint32_t b = (nx >= 0 && d.phit[nx]) ? (uint32_t)nx : evict_pos(d, a, M);
-            if (b == NIL || b > cur) { cov = true; to = b; break; }
-          }
-        }
-        if (!cov && r0 != NIL) {                     // a touch's disk span [touch, death)
-          for (uint32_t q = r0; q < d.np && d.sk[q] == id; ++q) {
-            const uint32_t a = d.sv[q];
-            if (a < d.P || !d.tflag[a]) continue;
-            if (a > cur) break;
-            const uint32_t b = death_row(d, death_of(d.dclock0 + d.clk[a], d.nb));
-            if (b == NIL || b > cur) { cov = true; to = b; break; }
-          }
-        }
-        if (!cov) { lv = cur; break; }
-        if (to == NIL || to >= d.np) break;          // covered to the end
-        cur = to;
+      uint32_t lv = d.egap[id];
+      if (lv == NIL) {
+        const uint32_t x = d.erun[id] == NIL ? max(d.ecov[id], d.P) : d.etail[id];
+        lv = x < d.np ? x : NIL;
       }
       const uint32_t rp = d.dec ? d.erep[id] : NIL;  // replaced: gone right after its own lookup
       if (rp != NIL && (lv == NIL || lv > rp)) pt = d.tim[rp] + 1;
@@ -1044,6 +1151,13 @@ struct XcgPairState {
   uint64_t* ddeath = nullptr;      // [np]
   uint32_t* erep = nullptr;        // [C + D]
   uint32_t* erun = nullptr;        // [etot]
+  uint32_t* erend = nullptr;       // [etot]
+  uint64_t* einit = nullptr;       // [etot]
+  uint32_t* ecov = nullptr; uint32_t* egap = nullptr; uint32_t* etail = nullptr;   // [etot]
+  uint64_t* sa = nullptr; uint64_t* sb = nullptr;   // [np + 1] segmented scans
+  uint32_t* nq = nullptr;          // [np + 1]
+  uint8_t* tnew = nullptr;         // [np + 1]
+  uint64_t ex_cap = 0;
   uint32_t* tab = nullptr;         // block table + its segment sums
   uint32_t* occ = nullptr; uint32_t* freel = nullptr; uint32_t* ofl = nullptr; uint32_t* ofr = nullptr;
   uint64_t* hk = nullptr; uint64_t* hk2 = nullptr; uint32_t* hv = nullptr; uint32_t* hv2 = nullptr;
@@ -1095,8 +1209,8 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
                      (void**)&P->nxt, (void**)&P->isr, (void**)&P->rc, (void**)&P->phit, (void**)&P->app,
                      (void**)&P->clk, (void**)&P->slow, (void**)&P->f1, (void**)&P->f2, (void**)&P->r1,
                      (void**)&P->r2, (void**)&P->missrow, (void**)&P->moves, (void**)&P->tflag,
-                     (void**)&P->ddeath};
-    const size_t sz[] = {4, 4, 1, 8, 8, 4, 4, 4, 4, 4, 4, 4, 4, 1, 4, 4, 4, 4, 4, 4, 4, 4, 32, 1, 8};
+                     (void**)&P->ddeath, (void**)&P->sa, (void**)&P->sb, (void**)&P->nq, (void**)&P->tnew};
+    const size_t sz[] = {4, 4, 1, 8, 8, 4, 4, 4, 4, 4, 4, 4, 4, 1, 4, 4, 4, 4, 4, 4, 4, 4, 32, 1, 8, 8, 8, 4, 1};
     for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); ++k) {
       (void)hipFree(*arrs[k]);
       *arrs[k] = nullptr;
@@ -1118,13 +1232,29 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
   if (!grow(&P->erun, &ec, etot) || !grow(&P->elast, &lc, etot)) return -5;
   P->et_cap = ec;
   P->el_cap = lc;
+  if (etot > P->ex_cap) {
+    void** arrs[] = {(void**)&P->erend, (void**)&P->einit, (void**)&P->ecov, (void**)&P->egap, (void**)&P->etail};
+    const size_t sz[] = {4, 8, 4, 4, 4};
+    P->ex_cap = 0;
+    for (size_t k = 0; k < 5; ++k) {
+      (void)hipFree(*arrs[k]);
+      *arrs[k] = nullptr;
+    }
+    for (size_t k = 0; k < 5; ++k)
+      if (hipMalloc(arrs[k], etot * sz[k] + 8) != hipSuccess) return -5;
+    P->ex_cap = etot;
+  }
   // rocprim temporary storage for the largest sort / scan of this size
   size_t a = 0, b = 0, c = 0;
   (void)rocprim::radix_sort_pairs(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
   (void)rocprim::exclusive_scan(nullptr, b, P->isr, P->rc, 0u, (size_t)std::max(np, n) + 1,
                                 rocprim::plus<uint32_t>());
   (void)rocprim::radix_sort_pairs(nullptr, c, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)np, 0, 64);
-  const uint64_t want = std::max(std::max(a, b), c) + 256;
+  size_t e1 = 0, e2 = 0, e3 = 0;
+  (void)rocprim::exclusive_scan(nullptr, e1, P->sa, P->sb, (uint64_t)0, (size_t)np + 1, rocprim::maximum<uint64_t>());
+  (void)rocprim::inclusive_scan(nullptr, e2, P->sa, P->sb, (size_t)np + 1, rocprim::maximum<uint64_t>());
+  (void)rocprim::inclusive_scan(nullptr, e3, P->sa, P->sb, (size_t)np + 1, rocprim::minimum<uint64_t>());
+  const uint64_t want = std::max(std::max(std::max(a, b), c), std::max(std::max(e1, e2), e3)) + 256;
   if (want > P->tmp_cap) {
     (void)hipFree(P->tmp);
     P->tmp = nullptr;
@@ -1138,6 +1268,23 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
 int scan_u32(XcgPairState* P, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st) {
   size_t tb = P->tmp_cap;
   return rocprim::exclusive_scan(P->tmp, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), st) == hipSuccess
+             ? 0 : -5;
+}
+
+// Segmented max / min scans of the packed (run << 32 | v) values (sa -> sb).
+int scan_max_excl(XcgPairState* P, uint64_t n, hipStream_t st) {
+  size_t tb = P->tmp_cap;
+  return rocprim::exclusive_scan(P->tmp, tb, P->sa, P->sb, (uint64_t)0, (size_t)n, rocprim::maximum<uint64_t>(),
+                                 st) == hipSuccess ? 0 : -5;
+}
+int scan_max_incl(XcgPairState* P, uint64_t n, hipStream_t st) {
+  size_t tb = P->tmp_cap;
+  return rocprim::inclusive_scan(P->tmp, tb, P->sa, P->sb, (size_t)n, rocprim::maximum<uint64_t>(), st) == hipSuccess
+             ? 0 : -5;
+}
+int scan_min_incl(XcgPairState* P, uint64_t n, hipStream_t st) {
+  size_t tb = P->tmp_cap;
+  return rocprim::inclusive_scan(P->tmp, tb, P->sa, P->sb, (size_t)n, rocprim::minimum<uint64_t>(), st) == hipSuccess
              ? 0 : -5;
 }
 
@@ -1222,6 +1369,8 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
   d.f1 = P->f1; d.f2 = P->f2; d.r1 = P->r1; d.r2 = P->r2; d.missrow = P->missrow; d.moves = P->moves;
   d.pbase = P->pbase; d.pcnt = P->pcnt; d.cnt = P->cnt; d.elast = P->elast; d.tflag = P->tflag; d.ddeath = P->ddeath; d.erep = P->erep; d.erun = P->erun;
   d.lru2 = P->lru2; d.occ = P->occ; d.freel = P->freel;
+  d.erend = P->erend; d.einit = P->einit; d.ecov = P->ecov; d.egap = P->egap; d.etail = P->etail;
+  d.sa = P->sa; d.sb = P->sb; d.nq = P->nq; d.tnew = P->tnew;
   // encode: hash -> ENTER position
   if (!rs.dec) {
     const uint64_t want = std::max<uint64_t>(1024, 2ull << (64 - __builtin_clzll(R + 1)));
@@ -1248,8 +1397,16 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
     size_t tb = P->tmp_cap;
     if (rocprim::radix_sort_pairs(P->tmp, tb, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)R, 0, 64, st) != hipSuccess)
       return -5;
-    hipLaunchKernelGGL(pr_dec_hits_kernel, dim3(grid_for(R)), dim3(256), 0, st, d, (const uint64_t*)P->hk2,
-                       (const uint32_t*)P->hv2, (uint32_t)R);
+    // latest definer / first GHIT per hash run by scans (f1: run heads, f2: their prefix, r1: first GHIT)
+    hipLaunchKernelGGL(pr_dh_heads_kernel, dim3(grid_for(R + 1)), dim3(256), 0, st, (const uint64_t*)P->hk2,
+                       (uint32_t)R, P->f1);
+    if (scan_u32(P, P->f1, P->f2, R + 1, st)) return -5;
+    hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(R)), dim3(256), 0, st, P->r1, R, NIL);
+    hipLaunchKernelGGL(pr_dh_vals_kernel, dim3(grid_for(R)), dim3(256), 0, st, d, (const uint32_t*)P->hv2,
+                       (uint32_t)R, (const uint32_t*)P->f1, (const uint32_t*)P->f2, P->r1);
+    if (scan_max_incl(P, R, st)) return -5;
+    hipLaunchKernelGGL(pr_dec_hits_kernel, dim3(grid_for(R)), dim3(256), 0, st, d, (const uint32_t*)P->hv2,
+                       (uint32_t)R, (const uint32_t*)P->f1, (const uint32_t*)P->f2, (const uint32_t*)P->r1);
   }
   hipLaunchKernelGGL(pr_resolve_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
   // entity runs: sort positions by entity (stable: positions stay in order)
@@ -1260,6 +1417,9 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
         hipSuccess)
       return -5;
   }
+  hipLaunchKernelGGL(pr_fill32_kernel, dim3(grid_for(np)), dim3(256), 0, st, (uint32_t*)P->nxt, np, NIL);
+  hipLaunchKernelGGL(pr_link_vals_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (scan_max_excl(P, np, st)) return -5;
   hipLaunchKernelGGL(pr_links_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
   if (rs.dec) hipLaunchKernelGGL(pr_repl_links_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
   if (scan_u32(P, P->isr, P->rc, np + 1, st)) return -5;
@@ -1289,12 +1449,19 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
     hipLaunchKernelGGL(pr_tab_query_kernel, dim3((nslow + 3) / 4), dim3(256), 0, st, d);
   }
   // the disk clock: monotone rounds to the least fixed point
+  hipLaunchKernelGGL(pr_nq_vals_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (scan_min_incl(P, np, st)) return -5;
+  hipLaunchKernelGGL(pr_nq_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+  if (hipMemsetAsync(P->tnew, 0, np + 1, st) != hipSuccess) return -5;
   int rounds = 0;
   for (;; ++rounds) {
     if (scan_u32(P, P->app, P->clk, np + 1, st)) return -5;
     if (rounds >= 64) return -75;
     if (hipMemsetAsync(&P->cnt->changed, 0, 4, st) != hipSuccess) return -5;
-    hipLaunchKernelGGL(pr_touch_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(pr_touch_chain_kernel, dim3(grid_for(etot)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(pr_setter_vals_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
+    if (scan_max_excl(P, np, st)) return -5;
+    hipLaunchKernelGGL(pr_touch_rows_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
     if (read_cnt(P, st)) return -5;
     if (P->h_cnt->changed == 0) break;
   }
@@ -1320,7 +1487,11 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
     P->last_M = P->h_small[0];
     P->last_ranked = true;
     if (hipMemsetAsync(&P->cnt->changed, 0, 4, st) != hipSuccess) return -5;
-    hipLaunchKernelGGL(pr_leave_kernel, dim3(grid_for(newb)), dim3(256), 0, st, d, P->last_M);
+    hipLaunchKernelGGL(pr_cover_kernel, dim3(grid_for(newb)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(pr_span_vals_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, P->last_M);
+    if (scan_max_excl(P, np, st)) return -5;
+    hipLaunchKernelGGL(pr_gaps_kernel, dim3(grid_for(np)), dim3(256), 0, st, d, P->last_M);
+    hipLaunchKernelGGL(pr_leave_kernel, dim3(grid_for(newb)), dim3(256), 0, st, d);
     if (read_cnt(P, st)) return -5;
     out->changed = P->h_cnt->changed != 0;
   }
@@ -1578,7 +1749,7 @@ void unmap_pool(XcgPairState* P) {
 void free_scratch(XcgPairState* P) {
   void* arrs[] = {P->ent, P->yent, P->kind, P->tim, P->hsh, P->skey, P->sval, P->sk, P->sv, P->prv, P->nxt,
                   P->isr, P->rc, P->phit, P->app, P->clk, P->slow, P->f1, P->f2, P->r1, P->r2, P->missrow,
-                  P->moves, P->pbase, P->pcnt, P->elast, P->tflag, P->ddeath, P->erep, P->erun, P->tab, P->occ, P->freel, P->ofl, P->ofr, P->hk, P->hk2,
+                  P->moves, P->pbase, P->pcnt, P->elast, P->tflag, P->ddeath, P->erep, P->erun, P->erend, P->einit, P->ecov, P->egap, P->etail, P->sa, P->sb, P->nq, P->tnew, P->tab, P->occ, P->freel, P->ofl, P->ofr, P->hk, P->hk2,
                   P->hv, P->hv2, P->bm_keys, P->bm_vals, P->staging, P->tmp, P->cnt};
   for (void* p : arrs) (void)hipFree(p);
   if (P->h_small) (void)hipHostFree(P->h_small);

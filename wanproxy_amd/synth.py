@@ -130,6 +130,24 @@ def stream(seed: int, nbytes: int, dup_pct: int, magic_pct: int = 0) -> bytes:
     return stream_range(seed, dup_pct, magic_pct, 0, nbytes).tobytes()
 
 
+def dense(seed: int, nbytes: int, distinct: int, shift_every: int = 64) -> bytes:
+    """REF-dense input (not a BASELINE.md dataset): 2048-byte blocks drawn
+    uniformly from a pool of `distinct` random segments, with a short random
+    literal (1..300 bytes) after every `shift_every`-th block on average so the
+    alignment moves.  Every block after a pool entry's first use can be a REF:
+    per entity thousands of cache references in one batch (the pair replay's
+    long runs)."""
+    rng = np.random.default_rng(seed)
+    pool = rng.integers(0, 256, (distinct, SEG), dtype=np.uint8)
+    nblk = nbytes // SEG + 1
+    data = pool[rng.integers(0, distinct, nblk)].reshape(-1)
+    nins = max(1, nblk // shift_every)
+    at = np.sort(rng.integers(0, nblk, nins)) * SEG
+    lens = rng.integers(1, 301, nins)
+    data = np.insert(data, np.repeat(at, lens), rng.integers(0, 256, int(lens.sum()), dtype=np.uint8))
+    return data[:nbytes].tobytes()
+
+
 def stream_ref(seed: int, nbytes: int, dup_pct: int, magic_pct: int = 0) -> bytes:
     """The BASELINE.md generator verbatim in pure Python (slow; for tests)."""
     class SM:
