@@ -27,7 +27,7 @@ def rows(d, sub, name):
 
 
 def short(name):
-    return name.split('(')[0].replace('void ', '').strip()
+    return name.split('(')[0].replace('void ', '').strip() or name[:80]
 
 
 def hbm(agg):
@@ -81,7 +81,7 @@ for d in sorted(glob.glob(os.path.join(src, '*', ''))):
     out[cfg] = {'kernel_us_total': round(total, 1),
                 'kernels': dict(sorted(kern.items(), key=lambda kv: -kv[1]['us']))}
     if cfg == 'c2s':
-        sp = [hbm(dict(x)) for x in disp if x['kernel'] == K]
+        sp = [hbm(dict(x)) for x in disp if K in x['kernel']]
         out[cfg]['stream_launches'] = sp
         if sp and 'hbm_bytes' in sp[-1]:
             out['c2s_seeded'] = {'dispatches': 1, 'us_sum': sp[-1]['us'], 'hbm_bytes': sp[-1]['hbm_bytes'],

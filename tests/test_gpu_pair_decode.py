@@ -80,6 +80,32 @@ def test_pair_decoder_call_by_call(dropin, ref_oracle, geom):
         assert any(r[3] for r in res[0]), 'the small pair never asked: the case tests nothing'
 
 
+@pytest.mark.parametrize('geom', [(8, 1, 16), (3, 1, 200), (40, 2, 64)])
+def test_pair_decoder_ref_dense(dropin, ref_oracle, geom):
+    """REF-dense frames (synth.dense: 2 KiB blocks from a small pool) decoded
+    frame by frame on a pair of the encoder's geometry: hundreds of REFs per
+    entity in one frame, a disk of one or two index blocks that dies and is
+    touched again.  Output, consumed bytes, ASK sets and the disk counters
+    equal the reference decoder's (the drop-in cuts what one batch declines)."""
+    from wanproxy_amd import synth
+    lim, nb, distinct = geom
+    d = synth.dense(0xDE1 + distinct, 4 << 20, distinct)
+
+    def mk(o):
+        return o.cache_new_pair(lim * SEG, mpg.disk_bytes(nb))
+    frames = frames_of(ref_oracle, d, 65536, mk)
+    assert sum(map(len, frames)) < len(d)
+    res, stats = [], []
+    for o in (ref_oracle, dropin):
+        c = mk(o)
+        res.append(decode_calls(o, c, frames))
+        stats.append(o.pair_stats(c))
+        o.cache_free(c)
+    for k, (a, b) in enumerate(zip(*res)):
+        assert a == b, (geom, k, a[0], b[0], a[2], b[2], len(a[3]), len(b[3]))
+    assert stats[0] == stats[1]
+
+
 def test_pair_decode_batch_vs_reference(ref_oracle):
     """The engine's batch decode (many frames, one launch chain) on a pair
     context equals the reference decoder run over the same frames one call at
