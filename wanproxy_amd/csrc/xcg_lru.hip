@@ -161,11 +161,17 @@ __global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, EvRows R, c
 // the sequential encoder makes them: tile p is declared while examining window
 // p + 2048, or after the last window.  One wave per chunk; pass 0 counts the
 // chunk's enters (cnt) and records the hits, pass 1 places the enters in tau.
+// With ptime (the eviction times the previous guess implies): a cached tile
+// looked up at or after its entry's eviction is a miss and a declaration, as
+// the parse makes it (and a later tile of that hash whose earliest tile in the
+// batch was such a hit before the eviction declares it again).  The guess is
+// iterated so the first parse already sees the evictions its own declarations
+// cause (lru_seed_guess).
 __global__ __launch_bounds__(256) void lru_seed_classify_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
                                                                 uint32_t maxd, const uint32_t* chunk_len, HashTab g,
                                                                 HashTab b, uint32_t* cnt, const uint32_t* enter_base,
                                                                 const uint32_t* tot, uint32_t C, uint64_t* hmin,
-                                                                uint64_t* tau, int pass) {
+                                                                uint64_t* tau, int pass, const uint64_t* ptime) {
   const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
   if (c >= n) return;
   const uint32_t nd = ndecl[c], last = chunk_len[c] - SEG;
@@ -177,11 +183,14 @@ __global__ __launch_bounds__(256) void lru_seed_classify_kernel(uint32_t n, cons
     if (d < nd) {
       dd = decl[(uint64_t)c * maxd + d];
       const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
-      if (gv != ~0ull) {
-        if (pass == 0)
-          atomicMin((unsigned long long*)&hmin[gv], (unsigned long long)(((uint64_t)c << 21) | (2u * dd.z + 1u)));
+      const uint64_t th = ((uint64_t)c << 21) | (2u * dd.z + 1u);
+      if (gv != ~0ull && (!ptime || th < ptime[gv])) {
+        if (pass == 0) atomicMin((unsigned long long*)&hmin[gv], (unsigned long long)th);
       } else {
-        enter = tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z);   // the earliest tile with this hash
+        const uint64_t e = tab_lookup_t(b, dd.x, dd.y);
+        enter = e == (((uint64_t)c << 32) | dd.z);     // the earliest tile with this hash
+        if (!enter && gv != ~0ull)                     // the earliest was a hit on the entry, before its eviction
+          enter = ((((e >> 32) << 21) | (2u * (uint32_t)e + 1u)) < ptime[gv]);
       }
     }
     const uint64_t m = ballot(enter);
@@ -536,6 +545,17 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   return 0;
 }
 
+// Guesses of the seed's evictions (XCG_LRU_SEED_ITERS, default 3; 1 = the
+// round-4 single guess).
+int seed_iters() {
+  static const int v = [] {
+    const char* e = getenv("XCG_LRU_SEED_ITERS");
+    const int k = e ? atoi(e) : 3;
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+  }();
+  return v;
+}
+
 // ptime from the tiling seed (lru_seed_classify_kernel).  Asynchronous.
 int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   using namespace xcg;
@@ -550,15 +570,24 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
   uint32_t* cnt = a.nhits;                         // (scratch until the rounds: round 1 rewrites it)
   const dim3 wgrid((n + 3) / 4);
-  hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
-                     (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 0);
-  hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev, (const uint32_t*)cnt,
-                     a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base, a.need, L->tot);
-  hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
-                     (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1);
-  if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
+  // guess 0 takes every cached tile for a hit; each further guess classifies
+  // against the evictions the one before implies (lru_seed_classify_kernel)
+  for (int it = 0; it < seed_iters(); ++it) {
+    const uint64_t* pt = it ? (const uint64_t*)L->ptime : nullptr;
+    if (it) {
+      hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
+      hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
+    }
+    hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
+                       (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
+                       (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 0, pt);
+    hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev, (const uint32_t*)cnt,
+                       a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base, a.need, L->tot);
+    hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
+                       (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
+                       (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1, pt);
+    if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
+  }
   return 0;
 }
 
