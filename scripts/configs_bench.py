@@ -455,20 +455,25 @@ def run_c5dense(args):
     from wanproxy_amd import synth
     from wanproxy_amd.xcgpu import Context
     nbytes = int(1 << 30 if args.scale >= 1 else max(1 << 22, int((1 << 30) * args.scale)))
-    data = np.frombuffer(synth.dense(0xC5D, nbytes, args.dense_pool), np.uint8).copy()
+    if args.dense_pool:
+        data = np.frombuffer(synth.dense(0xC5D, nbytes, args.dense_pool), np.uint8).copy()
+    else:                                            # --dense-pool 0: an all-zero stream
+        data = np.zeros(nbytes, np.uint8)
     offs, lens = synth.chunks_of(data.tobytes(), 128 * KiB)
     limit = max(2048, int(args.lru_mib * MiB * min(1.0, args.scale * 8)))
     disk = max(1 << 20, int(args.disk_mib * MiB * min(1.0, args.scale * 8)))
-    ctx = Context(torch_dev(args), memory_cache_limit=limit, disk_bytes=disk)
+    unb = args.dense_cache == 'unbounded'
+    ctx = Context(torch_dev(args), cache_segments=1 << 20) if unb else \
+        Context(torch_dev(args), memory_cache_limit=limit, disk_bytes=disk)
     per = max(1, args.batch_mib * MiB // (128 * KiB))
     B = Batches(ctx, data, offs, lens, per=per)
     clock = {}
     wall = timed_encode(B, args.reps, clock=clock)
     got = B.outputs()
-    st = ctx.pair_stats()
+    st = (0, 0, 0) if unb else ctx.pair_stats()
     k = min(len(got), max(64, int(args.lru_check * len(got))))
     o = Oracle()
-    c = o.cache_new_pair(limit, disk)
+    c = o.cache_new() if unb else o.cache_new_pair(limit, disk)
     exp = o.encode_batch(data, offs[:k], lens[:k], mode=1, cache=c)
     o.cache_free(c)
     if got[:k] != exp:
@@ -476,15 +481,16 @@ def run_c5dense(args):
         raise SystemExit(f'PARITY FAILURE (c5dense) at chunk {bad}')
     dec = data.tobytes()
     if not args.no_decode:
-        dctx = Context(torch_dev(args), cache_segments=args.dense_pool + 4096)
+        dctx = Context(torch_dev(args), cache_segments=max(1, args.dense_pool) + 4096)
         dec, _ = decode_device(dctx, got, per=per, chunk=128 * KiB)
         dctx.close()
     if dec != data.tobytes():
         raise SystemExit('ROUND TRIP FAILURE (c5dense)')
     ctx.close()
     inb = data.size
-    return {'config': 'REF-dense: %d MiB in 128 KiB chunks from a pool of %d segments, XCodecCachePair(%d MiB LRU '
-                      'memory, %d MiB disk)' % (nbytes >> 20, args.dense_pool, limit >> 20, disk >> 20),
+    what = 'from a pool of %d segments' % args.dense_pool if args.dense_pool else 'all zero bytes'
+    cache = 'unbounded cache' if unb else 'XCodecCachePair(%d MiB LRU memory, %d MiB disk)' % (limit >> 20, disk >> 20)
+    return {'config': 'REF-dense: %d MiB in 128 KiB chunks %s, %s' % (nbytes >> 20, what, cache),
             'batch_chunks': per, 'encode_GiBps': round(inb / 2**30 / wall, 2), 'encode_ms': round(wall * 1e3, 2),
             'out_in': round(B.out_bytes() / inb, 5), 'rounds': B.rounds, 'kernel': clock,
             'pair_stats': {'primary_entries': st[0], 'disk_entries': st[1], 'disk_written': st[2]},
@@ -502,7 +508,8 @@ def main():
     ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')
     ap.add_argument('--disk-laps', type=float, default=0, help='c5pair: size the disk so the data laps it')
-    ap.add_argument('--dense-pool', type=int, default=4096, help='c5dense: distinct segments')
+    ap.add_argument('--dense-cache', default='pair', choices=['pair', 'unbounded'], help='c5dense: the cache')
+    ap.add_argument('--dense-pool', type=int, default=4096, help='c5dense: distinct segments (0: all-zero data)')
     ap.add_argument('--no-decode', action='store_true', help='skip the decode round trips (profiling runs)')
     args = ap.parse_args()
     import torch

@@ -1058,6 +1058,7 @@ int xcg_ctx_status(xcg_ctx* c) {
       hipStreamSynchronize(nullptr) != hipSuccess)
     return XCG_EHIP;
   st = *c->h_status;
+  if (st && getenv("XCG_STATUS_DEBUG")) fprintf(stderr, "xcg: context status word %#x\n", (unsigned)st);
   return st ? XCG_EOVERFLOW : XCG_OK;
 }
 

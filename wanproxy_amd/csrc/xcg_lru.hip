@@ -274,6 +274,7 @@ struct ScanArgs {
   uint32_t C;
   uint32_t* freel;
   uint32_t* part;
+  uint64_t* hmin_reset;                            // (SK_RANK) reset hmin behind the scan: the next guess's atomics
 };
 
 template <int K>
@@ -310,6 +311,7 @@ __device__ __forceinline__ void scan_emit(const ScanArgs& a, uint32_t i, uint32_
     const uint64_t w = j < P ? a.tau[j] : NEVER;
     a.wpop[v] = w;
     a.ptime[v] = f && a.hmin[v] < w ? NEVER : w;   // (a hit after the eviction did not happen)
+    if (a.hmin_reset) a.hmin_reset[v] = NEVER;
   } else if (K == SK_QUEUE) {
     if (f) a.queue2[p] = v;
   } else {
@@ -572,12 +574,12 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   const dim3 wgrid((n + 3) / 4);
   // guess 0 takes every cached tile for a hit; each further guess classifies
   // against the evictions the one before implies (lru_seed_classify_kernel)
-  for (int it = 0; it < seed_iters(); ++it) {
+  // (hmin: reset behind each scan but the last; tau needs no reset: the scan
+  // reads tau[j] for j below the eviction count only, and a guess's enters
+  // write every one of those)
+  const int iters = seed_iters();
+  for (int it = 0; it < iters; ++it) {
     const uint64_t* pt = it ? (const uint64_t*)L->ptime : nullptr;
-    if (it) {
-      hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
-      hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
-    }
     hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
                        (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
                        (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 0, pt);
@@ -586,7 +588,9 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
     hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
                        (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
                        (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1, pt);
-    if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
+    ScanArgs sa = scan_args(L, nullptr);
+    if (it + 1 < iters) sa.hmin_reset = L->hmin;
+    if (run_scan<SK_RANK>(L, sa, L->C, st)) return -5;
   }
   return 0;
 }
