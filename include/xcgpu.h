@@ -75,6 +75,7 @@ extern "C" {
 #define XCG_EOVERFLOW (-75)        /* internal table overflow (reported, never silent) */
 #define XCG_EPROTO (-71)           /* pipe protocol error (XCodecPipePair::decoder_error) */
 #define XCG_ENOTSUP (-95)
+#define XCG_EEXIST (-17)           /* (registry) the UUID is registered already */
 
 typedef struct xcg_ctx xcg_ctx;
 
@@ -380,6 +381,14 @@ typedef struct xcg_pipe_out {
   int peer_eos;                  /* encoder_produce_eos */
 } xcg_pipe_out;
 int xcg_pipe_create(xcg_ctx *enc, xcg_ctx *dec, const uint8_t *uuid, xcg_pipe **out);
+/* As xcg_pipe_create, with the decoder's cache connected when the peer's
+ * <HELLO> arrives, as XCodecPipePair::decoder_decode does
+ * (decoder_cache_ = XCodecCache::connect(uuid, codec_->cache()),
+ * xcodec/xcodec_pipe_pair.cc:182-203): xcg_ctx_connect(parent, <HELLO>'s UUID).
+ * Pipes whose peers send the same UUID decode on one context. */
+int xcg_pipe_create_connect(xcg_ctx *enc, xcg_ctx *parent, const uint8_t *uuid, xcg_pipe **out);
+/* The decoder context a pipe decodes on (NULL before a connecting pipe's <HELLO>). */
+xcg_ctx *xcg_pipe_decoder_ctx(const xcg_pipe *p);
 void xcg_pipe_destroy(xcg_pipe *p);
 int xcg_pipe_encoder_consume(xcg_pipe *p, const uint8_t *data, uint64_t len, xcg_pipe_out *out);
 int xcg_pipe_encoder_consume_many(xcg_pipe *const *pipes, const uint8_t *const *data, const uint64_t *len, uint32_t n,
@@ -387,6 +396,26 @@ int xcg_pipe_encoder_consume_many(xcg_pipe *const *pipes, const uint8_t *const *
 int xcg_pipe_decoder_consume(xcg_pipe *p, const uint8_t *data, uint64_t len, xcg_pipe_out *out);
 /* Frames whose REF segments the encoder still keeps for <ASK> (not yet <ADVANCE>d). */
 uint32_t xcg_pipe_pending_frames(const xcg_pipe *p);
+
+/*
+ * The process-wide cache registry of XCodecCache::connect / enter / lookup
+ * (xcodec/xcodec_cache.h:101-127, one std::map<UUID, XCodecCache*> per
+ * process).  xcg_ctx_connect returns the context registered under `uuid36`,
+ * else makes one with the parent's connect -- XCodecMemoryCache::connect: an
+ * empty cache of the parent's limit (unbounded or bounded, same flags);
+ * XCodecCachePair::connect: a new pair whose primary is such a cache and whose
+ * secondary is the front XCodecDisk::connect gives that UUID on the parent's
+ * disk (xcodec_cache_disk.cc:640-690) -- and registers it.  The registry owns
+ * what it made; xcg_ctx_register enters a caller's context (wanproxy registers
+ * its own codec cache under the local UUID) without taking it.
+ * xcg_connect_registry_clear destroys the contexts the registry made and
+ * forgets every entry (the reference never does; for tests and shutdown).
+ * XCG_EEXIST: the UUID is registered already.
+ */
+int xcg_ctx_connect(xcg_ctx *parent, const char *uuid36, xcg_ctx **out);
+int xcg_ctx_register(xcg_ctx *c, const char *uuid36);
+xcg_ctx *xcg_ctx_lookup(const char *uuid36);
+void xcg_connect_registry_clear(void);
 
 /* ------------------------------------------------------------------------
  * zlib stage: wanproxy's DeflatePipe after the XCodec encoder

@@ -178,3 +178,58 @@ def test_bounded_caches_like_wanproxy_conf(oracle):
     assert enc.cache_size() == bdec.cache_size() <= 600
     for c in (enc, adec, benc, bdec):
         c.close()
+
+
+UUID_C = b'5e2d8b4a-1c3f-4a6e-9b0d-7f1e3c5a8b2d'
+
+
+@pytest.mark.parametrize('kind', ['unbounded', 'pair'])
+def test_hello_connects_peer_cache_by_uuid(kind):
+    """XCodecPipePair::decoder_decode on <HELLO>: decoder_cache_ =
+    XCodecCache::connect(uuid, codec_->cache()) (xcodec/xcodec_pipe_pair.cc:
+    182-203; xcodec/xcodec_cache.h:101-111).  Two connections from one peer
+    (its UUID in both <HELLO>s) decode on ONE connected cache: the second
+    connection's frames REF what only the first declared and decode without an
+    <ASK>.  A peer with another UUID gets a cache of its own (the codec cache's
+    connect: same kind and limit; a pair's is a new front on the same disk) and
+    asks; its <LEARN> answers complete the decode."""
+    from wanproxy_amd.xcgpu import Context, PipePair, connect_registry_clear, ctx_lookup
+    connect_registry_clear()
+    if kind == 'pair':
+        codec = Context(0, memory_cache_limit=4 << 20, disk_bytes=(18 + 4 * 205) * 2048)
+    else:
+        codec = Context(0, cache_segments=1 << 15)
+    lenc = Context(0, cache_segments=1 << 15)            # the local codec's encoder (unused direction)
+    penc = Context(0, cache_segments=1 << 15)            # the peer codec's cache, shared by its connections
+    pdec = Context(0, cache_segments=1 << 15)
+    try:
+        p1, p2, p3 = PipePair(penc, pdec, UUID_A), PipePair(penc, pdec, UUID_A), PipePair(penc, pdec, UUID_C)
+        l1, l2, l3 = (PipePair(lenc, codec, UUID_B, connect=True) for _ in range(3))
+        assert l1.decoder_ctx() is None
+        m = payload(5, 600_000)
+        _, got, _, _ = l1.decoder_consume(p1.encoder_consume(m))
+        assert got == m
+        assert l1.decoder_ctx() == ctx_lookup(UUID_A) and l1.decoder_ctx() not in (None, codec.h.value)
+        w2 = p2.encoder_consume(m)                        # REFs to what p1's frames declared
+        assert w2.count(b'\xf1\x01') == 0 and w2.count(b'\xf1\x02') > 100
+        back, got, _, _ = l2.decoder_consume(w2)
+        assert got == m and not back.startswith(b'\xf0')
+        assert l2.decoder_ctx() == l1.decoder_ctx()
+        back, got, _, _ = l3.decoder_consume(p3.encoder_consume(m))
+        assert back.startswith(b'\xf0') and got == b''    # a fresh cache for UUID_C: <ASK>
+        assert l3.decoder_ctx() == ctx_lookup(UUID_C) != l1.decoder_ctx()
+        out = b''
+        for _ in range(8):                                # <ASK> -> <LEARN> until nothing is unknown
+            if not back.startswith(b'\xf0'):
+                break
+            learn, _, _, _ = p3.decoder_consume(back)
+            assert learn.startswith(b'\xf1')
+            back, got, _, _ = l3.decoder_consume(learn)
+            out += got
+        assert out == m
+        for p in (p1, p2, p3, l1, l2, l3):
+            p.close()
+    finally:
+        connect_registry_clear()
+        for c in (codec, lenc, penc, pdec):
+            c.close()

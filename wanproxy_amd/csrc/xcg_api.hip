@@ -10,9 +10,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <ctype.h>
+
 #include <algorithm>
 #include <chrono>
+#include <iterator>
+#include <map>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/xcgpu.h"
@@ -228,6 +233,33 @@ namespace {
 
 // Stream-round seeding: -1 automatic, 0 never, 1 always (tests exercise both).
 int g_stream_seed = -1;
+
+// XCodecCache's process-wide UUID map (xcodec/xcodec_cache.h:101-127):
+// lowercase UUID -> context, and whether the registry made (owns) it.
+struct RegEntry {
+  xcg_ctx* ctx;
+  bool owned;
+};
+std::mutex g_reg_mu;
+std::map<std::string, RegEntry> g_reg;
+
+bool uuid_key(const char* u, std::string* key) {     // the 8-4-4-4-12 form UUID::decode takes
+  if (!u) return false;
+  std::string k(36, ' ');
+  for (int i = 0; i < 36; ++i) {
+    const char c = u[i];
+    const bool dash = i == 8 || i == 13 || i == 18 || i == 23;
+    if (dash ? c != '-' : !isxdigit((unsigned char)c)) return false;
+    k[i] = (char)tolower((unsigned char)c);
+  }
+  *key = k;
+  return true;
+}
+
+void registry_forget(xcg_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (auto it = g_reg.begin(); it != g_reg.end();) it = it->second.ctx == c ? g_reg.erase(it) : std::next(it);
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -549,6 +581,7 @@ const char* xcg_strerror(int status) {
     case XCG_ENOTSUP: return "not supported";
     case XCG_ENOENT: return "no such segment";
     case XCG_EPROTO: return "pipe protocol error";
+    case XCG_EEXIST: return "already registered";
     default: return "unknown status";
   }
 }
@@ -685,6 +718,64 @@ int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_
   return rc;
 }
 
+// XCodecCache::connect(uuid, parent) (xcodec/xcodec_cache.h:101-111) with
+// the parent's connect: XCodecMemoryCache::connect (:340-346, an empty cache
+// of the same limit), XCodecCachePair::connect (:158-161: the primary's connect
+// over XCodecDisk::connect(uuid), xcodec_cache_disk.cc:640-690).
+int xcg_ctx_connect(xcg_ctx* parent, const char* uuid36, xcg_ctx** out) {
+  std::string key;
+  if (!parent || !out || !uuid_key(uuid36, &key)) return XCG_EINVAL;
+  *out = nullptr;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find(key);
+  if (it != g_reg.end()) {
+    *out = it->second.ctx;
+    return XCG_OK;
+  }
+  xcg_ctx* c = nullptr;
+  int rc;
+  if (parent->pair)
+    rc = xcg_ctx_create_pair_uuid(parent->device, parent->flags, (uint64_t)parent->pair_C * XCG_SEGMENT_LENGTH,
+                                  (xcg_disk*)xcg_pair_state_disk(parent->pair), key.c_str(), &c);
+  else if (parent->bounded)
+    rc = xcg_ctx_create_bounded(parent->device, parent->flags, (uint64_t)parent->lru.C * XCG_SEGMENT_LENGTH, &c);
+  else
+    rc = xcg_ctx_create_ex(parent->device, parent->flags, parent->cache_segments, &c);
+  if (rc != XCG_OK) return rc;
+  g_reg[key] = RegEntry{c, true};
+  *out = c;
+  return XCG_OK;
+}
+
+// XCodecCache::enter(uuid, cache) (:113-117): a context the caller keeps.
+int xcg_ctx_register(xcg_ctx* c, const char* uuid36) {
+  std::string key;
+  if (!c || !uuid_key(uuid36, &key)) return XCG_EINVAL;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  if (g_reg.count(key)) return XCG_EEXIST;
+  g_reg[key] = RegEntry{c, false};
+  return XCG_OK;
+}
+
+xcg_ctx* xcg_ctx_lookup(const char* uuid36) {
+  std::string key;
+  if (!uuid_key(uuid36, &key)) return nullptr;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find(key);
+  return it == g_reg.end() ? nullptr : it->second.ctx;
+}
+
+void xcg_connect_registry_clear(void) {
+  std::vector<xcg_ctx*> owned;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (auto& e : g_reg)
+      if (e.second.owned) owned.push_back(e.second.ctx);
+    g_reg.clear();
+  }
+  for (xcg_ctx* c : owned) xcg_ctx_destroy(c);
+}
+
 int xcg_pair_stats(xcg_ctx* c, uint64_t* st) {
   if (!c || !c->pair || !st) return XCG_EINVAL;
   xcg_pair_state_stats(c->pair, st);
@@ -718,6 +809,7 @@ int xcg_ctx_create_ex(int device, uint32_t flags, uint64_t cache_segments, xcg_c
 
 void xcg_ctx_destroy(xcg_ctx* c) {
   if (!c) return;
+  registry_forget(c);
   DeviceGuard g(c->device);
   (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);

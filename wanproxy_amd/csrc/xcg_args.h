@@ -201,6 +201,7 @@ extern "C" void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st);
 extern "C" uint32_t xcg_pair_state_last_base(const XcgPairState* P);
 extern "C" uint32_t xcg_pair_state_limit(const XcgPairState* P);
 extern "C" uint32_t xcg_pair_state_disk_blocks(const XcgPairState* P);
+extern "C" XcgDiskState* xcg_pair_state_disk(const XcgPairState* P);
 extern "C" const uint64_t* xcg_pair_state_ptime(const XcgPairState* P);
 extern "C" int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st);
 extern "C" int xcg_pair_encode_stream(const XcgStreamArgs* a, XcgPairState* P, int* rounds_out, hipStream_t st);

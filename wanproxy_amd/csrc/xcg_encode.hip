@@ -750,6 +750,10 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     if (s0 != ke && s1 != ke) {
       if (novf < (uint32_t)ovf_cap<MAXD>()) ++novf;
       else if (l == 0 && prm.status) atomicOr(prm.status, 1);
+#ifdef XCG_DEBUG_OVF
+      if (l == 0 && novf >= (uint32_t)ovf_cap<MAXD>())
+        printf("ovf chunk %u decl %u lo %08x hi %08x at %u bucket %u\n", chunk, d, lo, hi, c, b);
+#endif
     }
     __builtin_amdgcn_wave_barrier();
   };

@@ -2335,6 +2335,7 @@ void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st) {
 uint32_t xcg_pair_state_last_base(const XcgPairState* P) { return P->last_base; }
 uint32_t xcg_pair_state_limit(const XcgPairState* P) { return P->C; }
 uint32_t xcg_pair_state_disk_blocks(const XcgPairState* P) { return P->D; }
+XcgDiskState* xcg_pair_state_disk(const XcgPairState* P) { return P->disk; }
 const uint64_t* xcg_pair_state_ptime(const XcgPairState* P) { return P->ptime; }
 
 int xcg_pair_sync(XcgPairState* P, const PairGpu* G, hipStream_t st) { return pair_sync_front(P, *G, st); }

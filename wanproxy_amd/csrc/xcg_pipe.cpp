@@ -126,7 +126,8 @@ uint64_t decoded_bound(const uint8_t* enc, uint64_t n) {
 
 struct xcg_pipe {
   xcg_ctx* enc;
-  xcg_ctx* dec;
+  xcg_ctx* dec;                    // (connecting pipes: set at <HELLO>)
+  xcg_ctx* parent = nullptr;       // codec_->cache() of a connecting pipe
   xcg_window* win;                 // the decoder's BACKREF window (one per XCodecDecoder)
   uint8_t uuid[UUID_LEN];
   // encoder side
@@ -177,7 +178,17 @@ int xcg_pipe::decode_ops() {
       const uint8_t len = b[1];
       if (avail < 2u + len) break;
       if (len != UUID_LEN || !uuid_ok(b + 2)) { rc = XCG_EPROTO; break; }
-      decoder = true;                                                // XCodecCache::connect(uuid)
+      if (parent) {                                                  // XCodecCache::connect(uuid, codec cache)
+        char u[UUID_LEN + 1];
+        memcpy(u, b + 2, UUID_LEN);
+        u[UUID_LEN] = 0;
+        xcg_ctx* c = nullptr;
+        rc = xcg_ctx_connect(parent, u, &c);
+        if (rc == XCG_OK) rc = xcg_window_create(c, &win);
+        if (rc != XCG_OK) break;
+        dec = c;
+      }
+      decoder = true;
       i += 2 + len;
     } else if (op == OP_ASK) {
       if (!encoder) { rc = XCG_EPROTO; break; }
@@ -329,9 +340,23 @@ int xcg_pipe_create(xcg_ctx* enc, xcg_ctx* dec, const uint8_t* uuid, xcg_pipe** 
   return XCG_OK;
 }
 
+int xcg_pipe_create_connect(xcg_ctx* enc, xcg_ctx* parent, const uint8_t* uuid, xcg_pipe** out) {
+  if (!enc || !parent || !uuid || !out || !uuid_ok(uuid)) return XCG_EINVAL;
+  xcg_pipe* p = new xcg_pipe;
+  p->enc = enc;
+  p->dec = nullptr;
+  p->parent = parent;
+  p->win = nullptr;
+  memcpy(p->uuid, uuid, UUID_LEN);
+  *out = p;
+  return XCG_OK;
+}
+
+xcg_ctx* xcg_pipe_decoder_ctx(const xcg_pipe* p) { return p ? p->dec : nullptr; }
+
 void xcg_pipe_destroy(xcg_pipe* p) {
   if (!p) return;
-  xcg_window_destroy(p->win);
+  if (p->win) xcg_window_destroy(p->win);
   delete p;
 }
 

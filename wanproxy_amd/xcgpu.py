@@ -139,6 +139,18 @@ def lib():
     L.xcg_pipe_create.restype = C.c_int
     L.xcg_pipe_destroy.argtypes = [vp]
     L.xcg_pipe_destroy.restype = None
+    L.xcg_pipe_create_connect.argtypes = [vp, vp, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.xcg_pipe_create_connect.restype = C.c_int
+    L.xcg_pipe_decoder_ctx.argtypes = [vp]
+    L.xcg_pipe_decoder_ctx.restype = vp
+    L.xcg_ctx_connect.argtypes = [vp, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.xcg_ctx_connect.restype = C.c_int
+    L.xcg_ctx_register.argtypes = [vp, C.c_char_p]
+    L.xcg_ctx_register.restype = C.c_int
+    L.xcg_ctx_lookup.argtypes = [C.c_char_p]
+    L.xcg_ctx_lookup.restype = vp
+    L.xcg_connect_registry_clear.argtypes = []
+    L.xcg_connect_registry_clear.restype = None
     L.xcg_pipe_encoder_consume.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(_PipeOut)]
     L.xcg_pipe_encoder_consume.restype = C.c_int
     L.xcg_pipe_encoder_consume_many.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
@@ -533,11 +545,19 @@ class PipePair:
     is the codec's context (cache shared by its pipes), `dec` the context of the
     peer's cache; `uuid` the 36-byte UUID string sent in <HELLO>."""
 
-    def __init__(self, enc: Context, dec: Context, uuid: bytes):
+    def __init__(self, enc: Context, dec: Context, uuid: bytes, connect: bool = False):
+        """connect=True: `dec` is the codec's cache (codec_->cache()) and the
+        decoder context is connected at the peer's <HELLO>
+        (xcg_pipe_create_connect: XCodecCache::connect(uuid, parent))."""
         self.enc, self.dec = enc, dec
         h = C.c_void_p()
-        _check(lib().xcg_pipe_create(enc.h, dec.h, uuid, C.byref(h)))
+        fn = lib().xcg_pipe_create_connect if connect else lib().xcg_pipe_create
+        _check(fn(enc.h, dec.h, uuid, C.byref(h)))
         self.h = h
+
+    def decoder_ctx(self):
+        """Handle (int) of the context this pipe decodes on, None before <HELLO>."""
+        return lib().xcg_pipe_decoder_ctx(self.h)
 
     def close(self):
         if getattr(self, 'h', None):
@@ -573,3 +593,22 @@ class PipePair:
 
     def pending_frames(self) -> int:
         return int(lib().xcg_pipe_pending_frames(self.h))
+
+
+def ctx_connect(parent: Context, uuid: bytes):
+    """xcg_ctx_connect: handle (int) of the registry's context for `uuid`."""
+    h = C.c_void_p()
+    _check(lib().xcg_ctx_connect(parent.h, uuid, C.byref(h)))
+    return h.value
+
+
+def ctx_register(ctx: Context, uuid: bytes):
+    _check(lib().xcg_ctx_register(ctx.h, uuid))
+
+
+def ctx_lookup(uuid: bytes):
+    return lib().xcg_ctx_lookup(uuid)
+
+
+def connect_registry_clear():
+    lib().xcg_connect_registry_clear()
