@@ -683,6 +683,12 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   uint32_t* const keyt = (uint32_t*)(kblk + kofs);
   for (int k = l; k < 2 * NB; k += 64) keyt[k] = DM ? dm_empty<LOGNB>((uint32_t)k) : kempty<LOGNB>((uint32_t)k >> 1);
   uint32_t ndecl = 0, novf = 0;
+  // (stream) the own key table overflowed: this parse may have missed one of
+  // its own declarations.  The chunk's hit count becomes maxh + 1, which the
+  // verification treats as "always re-parse" (structured data can put a
+  // transient round's many declarations into few buckets; the re-parse sees the
+  // round's lists); a result no verification follows is checked by the driver.
+  bool own_ovf = false;
 
   const int last = L - SEG;                        // last window start
   const int mis = (int)(reinterpret_cast<uintptr_t>(x) & 15u);
@@ -749,6 +755,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     }
     if (s0 != ke && s1 != ke) {
       if (novf < (uint32_t)ovf_cap<MAXD>()) ++novf;
+      else if (STREAM) own_ovf = true;
       else if (l == 0 && prm.status) atomicOr(prm.status, 1);
 #ifdef XCG_DEBUG_OVF
       if (l == 0 && novf >= (uint32_t)ovf_cap<MAXD>())
@@ -1490,7 +1497,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
     if (ballot(diff) != 0 && l == 0) atomicMin(prm.changed, chunk);
     if (l == 0) {
       prm.ndecl[chunk] = ndecl;
-      prm.nhits[chunk] = nh;
+      prm.nhits[chunk] = own_ovf ? prm.maxh + 1u : nh;
       if (LRU) prm.nev[chunk] = ne;
     }
   }
@@ -2352,6 +2359,12 @@ __global__ __launch_bounds__(256) void verify_diff_kernel(HashTab tv, HashTab tt
     atomicOr(status, 2);
 }
 
+__global__ __launch_bounds__(256) void own_ovf_check_kernel(const uint32_t* nhits, uint32_t n, uint32_t maxh,
+                                                            int32_t* status) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n && nhits[c] == maxh + 1u && status) atomicOr(status, 1);
+}
+
 // need[k] for every chunk: the conservative (a) (no probe, or too many newly
 // visible hashes) or overflowed hit / reference lists -- such a chunk re-parses
 // from its start (bad_t 0); then (a) by the probe and (b), which also give
@@ -3065,6 +3078,10 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     }
     if (!converged) return -75;
   }
+  // A result no verification passed over (one chunk, or round 0 declared
+  // nothing): an own-table overflow in it is reported (status bit 0).
+  if (!committed) hipLaunchKernelGGL(own_ovf_check_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
+                                     (const uint32_t*)a->nhits, n, a->maxh, a->status);
   if (!committed) commit(nullptr);
   if (rounds_out) *rounds_out = rounds;
   return hipGetLastError() == hipSuccess ? 0 : -5;

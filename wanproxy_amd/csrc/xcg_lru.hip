@@ -549,13 +549,10 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
 
 // Guesses of the seed's evictions (XCG_LRU_SEED_ITERS, default 3; 1 = the
 // round-4 single guess).
-int seed_iters() {
-  static const int v = [] {
-    const char* e = getenv("XCG_LRU_SEED_ITERS");
-    const int k = e ? atoi(e) : 3;
-    return k < 1 ? 1 : (k > 8 ? 8 : k);
-  }();
-  return v;
+int seed_iters() {                                // (read per sub-batch: tests switch it)
+  const char* e = getenv("XCG_LRU_SEED_ITERS");
+  const int k = e ? atoi(e) : 3;
+  return k < 1 ? 1 : (k > 8 ? 8 : k);
 }
 
 // ptime from the tiling seed (lru_seed_classify_kernel).  Asynchronous.
