@@ -16,7 +16,9 @@ DUP = int(os.environ.get('DUP', 50))
 SEED = int(os.environ.get('SEED', '0xC2'), 0)
 phases = bool(os.environ.get('XCGPU_LIB'))
 dev = torch.device('cuda', 0)
-data = np.frombuffer(synth.stream(SEED, N * CH, DUP, 0), dtype=np.uint8)
+DENSE = int(os.environ.get('DENSE', 0))            # synth.dense pool size instead of the C2 generator
+data = np.frombuffer(synth.dense(SEED, N * CH, DENSE) if DENSE else synth.stream(SEED, N * CH, DUP, 0),
+                     dtype=np.uint8)
 d_in = torch.from_numpy(data.copy()).to(dev)
 d_len = torch.full((N,), CH, dtype=torch.int32, device=dev)
 d_off = torch.arange(N, dtype=torch.int64, device=dev) * CH
@@ -47,4 +49,8 @@ for seed in (0, 1):
               f'vector {np.median(vec):.0f} {slot1} {np.median(evt):.0f} ({np.median(nev):.0f} events, '
               f'{np.median(evt / np.maximum(nev, 1)):.1f} us each) rest {np.median(rest):.0f}; pieces {np.median(pcs):.0f} '
               f'(mean {pcs.mean():.1f}, events mean {nev.mean():.1f})')
+        top = np.argsort(-tot)[:6]
+        print('  slowest chunks (us total / vector / events / pieces / events n):',
+              [(int(c), round(tot[c]), round(vec[c]), round(evt[c]), int(pcs[c]), int(nev[c])) for c in top],
+              'p99 %.0f max %.0f' % (np.percentile(tot, 99), tot.max()))
     ctx.close()

@@ -1571,11 +1571,18 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
                    (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode, S.ro[wv], S.rsv[wv]};
   const uint32_t stride = gridDim.x * SW;
   const uint32_t items = prm.work ? readfirst(prm.work[0]) : prm.n;
+  // The batch's first chunk sees no batch declaration: on an empty cache it
+  // probes nothing.  (The filter holds every chunk's keys; in a seeded round
+  // of REF-dense data the first chunk's windows match thousands of later
+  // chunks' tiles, each an exact lookup that finds nothing visible.)
+  const bool g_empty = readfirst(*prm.nseg) == 0u;
   for (uint32_t i = blockIdx.x * SW + (uint32_t)wv; i < items; i += stride) {
     const uint32_t chunk = prm.work ? readfirst(prm.work[1 + i]) : i;
     if (chunk < prm.skip_below) continue;      // input unchanged since its last parse
     if (prm.need && readfirst(prm.need[chunk]) == 0u) continue;   // verified: its parse stands
-    encode_chunk<LOGNB, MAXD, true, LRU>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gs);
+    GlbView gv = gs;
+    if (chunk == 0 && g_empty) gv.fmode = 0;
+    encode_chunk<LOGNB, MAXD, true, LRU>(prm, (char*)S.key, (uint32_t)wv << (LOGNB + 3), S.rec[wv], chunk, gv);
   }
 }
 
