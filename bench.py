@@ -507,9 +507,14 @@ def other_configs():
     # C5-PAIR-LAPS: the same with a disk the shard laps ~3 times (FIFO eviction
     # and re-entry inside the measured figure)
     lap = argparse.Namespace(**{**vars(a), 'disk_laps': 3})
+    # C5-PAIR-DENSE: the pair on REF-dense data -- 1 GiB drawn from 16 hot 2 KiB
+    # segments (synth.dense), thousands of references per entity per sub-batch
+    # (not a BASELINE dataset: the replay's long-run case; a prefix checked)
+    dense = argparse.Namespace(**{**vars(a), 'dense_pool': 16, 'dense_cache': 'pair', 'lru_check': 0.1})
     out = {}
     for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, a),
-                         ('C5-PAIR', cb.run_c5pair, a), ('C5-PAIR-LAPS', cb.run_c5pair, lap)):
+                         ('C5-PAIR', cb.run_c5pair, a), ('C5-PAIR-LAPS', cb.run_c5pair, lap),
+                         ('C5-PAIR-DENSE', cb.run_c5dense, dense)):
         try:
             out[name] = fn(ar)
         except BaseException as e:          # SystemExit from a parity check included

@@ -429,18 +429,22 @@ __global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const u
   const uint32_t c = (uint32_t)(w / maxd), d = (uint32_t)(w % maxd);
   if (c >= n || d >= ndecl[c]) return;
   const uint4 dd = decl[(uint64_t)c * maxd + d];
+  // the segment's loads first: a returning atomic (the table insert) waits for
+  // every older memory operation of the wave on gfx9, so loads issued after it
+  // would add their latency to the insert's
+  const uint8_t* src = in + chunk_off[c] + dd.z;
+  const int l = lane_id();
+  const u32x4 v0 = *(const u32x4_u*)(src + 32 * l), v1 = *(const u32x4_u*)(src + 32 * l + 16);
   const uint32_t s = freel[enter_base[c] + d];
-  if (lane_id() == 0) {
+  if (l == 0) {
     skey[s] = ((uint64_t)dd.y << 32) | dd.x;
     alive[s] = 1u;
     if (!tab_insert_min(g, dd.x, dd.y, s)) atomicOr(status, 2);
     filt_insert(fs, dd.x, dd.y);
   }
-  const uint8_t* src = in + chunk_off[c] + dd.z;
   uint8_t* dst = pool + (uint64_t)s * SEG;
-  const int l = lane_id();
-  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
-  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+  *(u32x4_u*)(dst + 32 * l) = v0;
+  *(u32x4_u*)(dst + 32 * l + 16) = v1;
 }
 
 // Every reference's slot (evslot, in stream order) and time; lastref = the
