@@ -1024,25 +1024,47 @@ __global__ __launch_bounds__(256) void pair_seed_table_kernel(uint32_t n, const 
 }
 __global__ __launch_bounds__(256) void pair_seed_events_kernel(uint32_t n, const uint4* decl, const uint32_t* ndecl,
                                                                uint32_t maxd, const uint32_t* chunk_len, HashTab g,
-                                                               HashTab b, uint4* ev, uint32_t* nev, uint32_t maxe) {
+                                                               HashTab b, uint4* ev, uint32_t* nev, uint32_t maxe,
+                                                               const uint64_t* ptime) {
   const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
   if (c >= n) return;
-  const uint32_t nd = min(ndecl[c], maxe), last = chunk_len[c] - SEG;
-  for (uint32_t k = (uint32_t)lane_id(); k < nd; k += 64) {
-    const uint4 dd = decl[(uint64_t)c * maxd + k];
-    const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
-    uint4 e;
-    if (gv != ~0ull) {
-      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, (EV_GHIT << 30) | (uint32_t)gv);
-    } else if (tab_lookup_t(b, dd.x, dd.y) == (((uint64_t)c << 32) | dd.z)) {
-      const uint32_t t = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
-      e = make_uint4(dd.x, dd.y, t, (EV_ENTER << 30) | k);
-    } else {
-      e = make_uint4(dd.x, dd.y, 2u * dd.z + 1u, EV_HIT << 30);
+  const uint32_t nd = min(ndecl[c], maxe / 2u), last = chunk_len[c] - SEG;
+  uint32_t row = 0;
+  for (uint32_t k0 = 0; k0 < nd; k0 += 64) {
+    const uint32_t k = k0 + (uint32_t)lane_id();
+    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+    uint32_t nr = 0;
+    if (k < nd) {
+      const uint4 dd = decl[(uint64_t)c * maxd + k];
+      const uint64_t gv = tab_lookup_t(g, dd.x, dd.y);
+      const uint32_t th = 2u * dd.z + 1u, te = dd.z + SEG <= last ? 2u * (dd.z + SEG) : 2u * (last + 1u);
+      if (gv != ~0ull && (!ptime || ((((uint64_t)c << 21) | th) < ptime[gv]))) {
+        r0 = make_uint4(dd.x, dd.y, th, (EV_GHIT << 30) | (uint32_t)gv);
+        nr = 1;
+      } else {
+        // gone from both levels by now (with ptime: the guess before this one)
+        // or never cached: a declaration if it is the batch's earliest tile of
+        // the hash, or if that earliest tile found the entry before it left
+        const uint64_t e = tab_lookup_t(b, dd.x, dd.y);
+        bool enter = e == (((uint64_t)c << 32) | dd.z);
+        if (!enter && gv != ~0ull)
+          enter = ((((e >> 32) << 21) | (2u * (uint32_t)e + 1u)) < ptime[gv]);
+        if (gv != ~0ull) r0 = make_uint4(dd.x, dd.y, th, (EV_GMISS << 30) | (uint32_t)gv);
+        const uint4 second = enter ? make_uint4(dd.x, dd.y, te, (EV_ENTER << 30) | k)
+                                   : make_uint4(dd.x, dd.y, th, EV_HIT << 30);
+        if (gv != ~0ull) { r1 = second; nr = 2; }
+        else { r0 = second; nr = 1; }
+      }
     }
-    ev[(uint64_t)c * maxe + k] = e;
+    // rows in tile order (a GMISS precedes its tile's ENTER; an ENTER at window
+    // + 2048 precedes the next tile's lookup one position later)
+    const uint32_t inc = wave_incl_scan(nr);
+    const uint32_t o = row + inc - nr;
+    if (nr > 0) ev[(uint64_t)c * maxe + o] = r0;
+    if (nr > 1) ev[(uint64_t)c * maxe + o + 1] = r1;
+    row += readlane(inc, 63);
   }
-  if (lane_id() == 0) nev[c] = nd;
+  if (lane_id() == 0) nev[c] = row;
 }
 
 // Statistics: this front's live disk entries (xuid) or every live entry (xuid ~0).
@@ -1188,6 +1210,14 @@ bool pair_debug() {
 }
 
 unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
+
+// Guesses of a sub-batch's tiling seed replayed before its first parse
+// (read per sub-batch: tests switch it; 1 = round 4's single guess).
+int pair_seed_iters() {
+  const char* e = getenv("XCG_PAIR_SEED_ITERS");
+  const int k = e ? atoi(e) : 3;
+  return k < 1 ? 1 : (k > 8 ? 8 : k);
+}
 
 template <class T>
 bool grow(T** p, uint64_t* cap, uint64_t want) {
@@ -2426,12 +2456,20 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
       hipLaunchKernelGGL(pr_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, (uint64_t)b.mask + 1, ~0ull);
       hipLaunchKernelGGL(pair_seed_table_kernel, dim3(grid_for((uint64_t)m * a.maxd)), dim3(256), 0, st, m,
                          (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
-      hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
-                         (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe);
-      if (!clear_flags()) { done_scratch(); return -5; }
-      PassOut o;
-      const int rc = replay(P, rs, g, true, &o, st);
-      if (rc) { done_scratch(); return rc; }
+      // guess 0 takes every cached tile for a hit; each further guess
+      // classifies against the departure times the one before implies
+      // (XCG_PAIR_SEED_ITERS, default 3)
+      const int iters = pair_seed_iters();
+      for (int it = 0; it < iters; ++it) {
+        hipLaunchKernelGGL(pair_seed_events_kernel, dim3((m + 3) / 4), dim3(256), 0, st, m, (const uint4*)a.decl,
+                           (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, (uint4*)a.ev, a.nev, a.maxe,
+                           it ? (const uint64_t*)P->ptime : nullptr);
+        if (!clear_flags()) { done_scratch(); return -5; }
+        PassOut o;
+        const int rc = replay(P, rs, g, true, &o, st);
+        if (rc) { done_scratch(); return rc; }
+        if (o.split) break;                        // (a guess the replay declines: keep the last times)
+      }
     }
     const clk::time_point t2 = clk::now();
     double t_parse = 0, t_replay = 0;
