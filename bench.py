@@ -511,8 +511,12 @@ def other_configs():
     # segments (synth.dense), thousands of references per entity per sub-batch
     # (not a BASELINE dataset: the replay's long-run case; a prefix checked)
     dense = argparse.Namespace(**{**vars(a), 'dense_pool': 16, 'dense_cache': 'pair', 'lru_check': 0.1})
+    # C5-LRU in one call of the shard's 8192 chunks: its sub-batches (N + H <= C,
+    # ~900 chunks) then split 8192 into 9 equal parts instead of 4096 into 5
+    # twice -- a launch costs one chunk's serial parse however few it holds
+    lru1 = argparse.Namespace(**{**vars(a), 'batch_mib': 1024})
     out = {}
-    for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, a),
+    for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, lru1),
                          ('C5-PAIR', cb.run_c5pair, a), ('C5-PAIR-LAPS', cb.run_c5pair, lap),
                          ('C5-PAIR-DENSE', cb.run_c5dense, dense)):
         try:

@@ -127,6 +127,7 @@ struct XcgLruState {
   uint32_t* part;         // per-tile counts of the multi-workgroup scans (grown on demand)
   uint32_t part_cap;
   uint32_t last_base;     // first chunk of the last committed sub-batch (its rows stay in the scratch)
+  uint32_t fit_hint;      // chunks x maxd a full-cache sub-batch held last (0: none yet)
 };
 
 // A batch's cache references for the LRU pass: enters as declaration rows

@@ -35,6 +35,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <chrono>
 
 #include "xcg_cache.h"
@@ -659,6 +660,11 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
   // 2048 bytes at most once; collision lookups aside), then from what the last
   // sub-batch used
   uint32_t per = C / a0->maxd ? C / a0->maxd : 1u;
+  if (L->fit_hint >= a0->maxd) {                   // equal parts at what the last sub-batches held
+    const uint32_t hint = L->fit_hint / a0->maxd;
+    const uint32_t k = (n + hint - 1) / hint;
+    per = (n + k - 1) / k;
+  }
   constexpr int MAX_PASSES = 12;
   uint32_t i0 = 0;
   while (i0 < n) {
@@ -718,8 +724,22 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     // (a sub-batch that started below the limit saw fewer cached entries to
     // look up than the next will: size the next one more cautiously)
     const uint64_t used = (uint64_t)L->h_tot[T_N] + L->h_tot[T_H];
-    const uint64_t pct = L->h_tot[T_A] < C ? 75 : 88;
-    const uint64_t want = used ? (uint64_t)C * pct / 100 * m / used : (uint64_t)n;
+    // The most chunks that fit under 95 % of the bound at this sub-batch's use
+    // per chunk (75 % while the cache is still filling: a sub-batch that
+    // started below the limit saw fewer cached entries to look up than the
+    // next will), then what is left in equal parts of that size or less: a
+    // launch costs about one chunk's serial parse however few chunks it holds,
+    // so the count of sub-batches is what matters.
+    const uint64_t rest = n - i0;
+    uint64_t want = (uint64_t)n;
+    if (used) {
+      const uint64_t pct = L->h_tot[T_A] < C ? 75 : 95;
+      uint64_t fit = (uint64_t)C * pct / 100 * m / used;
+      if (fit < 1) fit = 1;
+      L->fit_hint = pct == 95 ? (uint32_t)std::min<uint64_t>(fit * a0->maxd, 1u << 31) : 0u;
+      const uint64_t k = rest ? (rest + fit - 1) / fit : 1;
+      want = rest ? (rest + k - 1) / k : fit;
+    }
     per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
   }
   if (rounds_out) *rounds_out = rounds;
