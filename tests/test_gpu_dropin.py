@@ -222,3 +222,46 @@ def test_dropin_decode_op_at_the_piece_cut(dropin, ref_oracle, shift):
         o.cache_free(c)
     assert res[0] == res[1]
     assert res[0][0] and res[0][2] == len(stream) and res[0][1].count(seg) == 3
+
+
+def _crafted_streams(ref_oracle):
+    """Frames that stress the per-call decode's op walk (decode_small_kernel,
+    parallel pointer-jumping walk): escapes next to ops, 0xF1 bytes inside
+    EXTRACT payloads and REF hashes, a lone 0xF1 at the end, EXTRACT / REF cut
+    short, an unknown opcode, a BACKREF (the batch path), no 0xF1 at all, an
+    empty call, and payloads full of 0xF1 (more candidate op starts than the
+    parallel walk holds: the sequential walk)."""
+    import random
+    r = random.Random(0x5A1C)
+    lit = lambda n: bytes(r.randrange(0xF1) for _ in range(n))
+    seg = lambda f1: bytes(0xF1 if r.random() < f1 else r.randrange(256) for _ in range(2048))
+    s1, s2, s3 = seg(0.01), seg(0.3), seg(1.0)
+    h = lambda s: ref_oracle.hash(s).to_bytes(8, 'big')
+    ext = lambda s: b'\xf1\x01' + s
+    ref = lambda s: b'\xf1\x02' + h(s)
+    esc = b'\xf1\x00'
+    out = [
+        lit(100) + ext(s1) + esc + ref(s1) + esc + esc + lit(3) + ext(s2) + ref(s2) + ref(s1) + lit(50) + esc,
+        esc + ext(s1) + ref(s1) * 40 + lit(7) + b'\xf1',
+        lit(9) + ext(s2) + ext(s1)[:1000],
+        lit(9) + ext(s1) + ref(s1)[:6],
+        lit(20) + ext(s1) + b'\xf1\x07' + lit(30),
+        lit(20) + ext(s1) + b'\xf1\x03\x05' + lit(30),
+        lit(5000),
+        b'',
+        ext(s3) + ext(seg(0.99)) + ref(s3) + lit(11),
+        (ext(s2) + ref(s2) + esc + lit(1)) * 30,
+    ]
+    return out
+
+
+def test_dropin_decode_call_walk_edges(dropin, ref_oracle):
+    """Each crafted frame decoded by one decode() call on a fresh unbounded
+    cache: output, consumed bytes and ASK set equal the reference decoder's."""
+    for k, stream in enumerate(_crafted_streams(ref_oracle)):
+        res = []
+        for o in (ref_oracle, dropin):
+            c = o.cache_new()
+            res.append(o.decode(stream, c))
+            o.cache_free(c)
+        assert res[0][:3] == res[1][:3] and sorted(res[0][3]) == sorted(res[1][3]), k

@@ -1021,10 +1021,9 @@ __device__ __forceinline__ void decode_small_body(const SmallDec& a) {
     s_nunk = 0; s_fb = 0; s_stop = ~0ull; s_next = 0;
     a.res[8 + SD_UMAX + SD_EMAX] = (uint64_t)(uint32_t)*a.status;   // (the paths that return early)
   }
-  if (a.tim) {
-    __syncthreads();
-    SD_STAMP(1);
-  }
+  // (wave 0's walk reads input bytes every wave staged)
+  __syncthreads();
+  SD_STAMP(1);
   // ---- walk (wave 0): op list, output offsets, declare numbers
   auto walk = [&](auto xp) {
     uint32_t i = 0, k = 0, dn = 0, st = 0, fb = 0;
