@@ -173,3 +173,38 @@ def test_pair_ref_dense_vs_oracle(oracle, geom):
         outs += o
     dctx.close()
     assert b''.join(outs) == d
+
+
+def test_pair_ref_dense_random_sweep(oracle):
+    """Random REF-dense geometries (pool 4-300 segments, primary 2-200 slots,
+    a disk of 1-6 index blocks, chunks of 4-128 KiB, one to three calls): every
+    chunk and the disk counters equal the oracle's pair -- touch chains with
+    several deaths per entity, departures of entities referenced hundreds of
+    times, and primaries smaller than one chunk's declarations."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    rng = np.random.default_rng(0xD5)
+    for t in range(12):
+        pool = int(rng.integers(4, 300))
+        chunk = int(rng.choice([4096, 16384, 65536, 131072]))
+        lim = int(rng.integers(max(2, chunk // 2048 + 1), 200))
+        nb = int(rng.integers(1, 7))
+        d = synth.dense(int(rng.integers(1 << 30)), int(rng.integers(1, 5)) << 20, pool,
+                        shift_every=int(rng.integers(4, 128)))
+        offs, lens = synth.chunks_of(d, chunk)
+        limit, disk = lim * 2048, mpg.disk_bytes(nb)
+        c = oracle.cache_new_pair(limit, disk)
+        exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+        est = oracle.pair_stats(c)
+        oracle.cache_free(c)
+        ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+        calls = sorted(set([0, offs.size] + [int(x) for x in rng.integers(0, offs.size, int(rng.integers(0, 3)))]))
+        got = []
+        for a, b in zip(calls, calls[1:]):
+            got += ctx.encode_chunks(d, offs[a:b], lens[a:b], semantics=XCG_SEM_STREAM)
+        st = ctx.pair_stats()
+        ctx.close()
+        bad = [i for i in range(len(got)) if got[i] != exp[i]]
+        assert not bad, (t, pool, chunk, lim, nb, bad[:5])
+        assert (st[1], st[2]) == est, (t, pool, chunk, lim, nb)
