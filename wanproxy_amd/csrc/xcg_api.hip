@@ -323,6 +323,7 @@ void free_lru(XcgLruState& L) {
   (void)hipFree(L.alive); (void)hipFree(L.freel); (void)hipFree(L.part);
   (void)hipFree(L.tot);
   if (L.h_tot) (void)hipHostFree(L.h_tot);
+  if (L.tev) (void)hipEventDestroy((hipEvent_t)L.tev);
   const uint32_t C = L.C;
   L = XcgLruState{};
   L.C = C;

@@ -128,6 +128,7 @@ struct XcgLruState {
   uint32_t part_cap;
   uint32_t last_base;     // first chunk of the last committed sub-batch (its rows stay in the scratch)
   uint32_t fit_hint;      // chunks x maxd a full-cache sub-batch held last (0: none yet)
+  void* tev;              // hipEvent_t behind the eviction times' totals (lazily made)
 };
 
 // A batch's cache references for the LRU pass: enters as declaration rows

@@ -44,7 +44,7 @@
 namespace xcg {
 
 constexpr uint64_t NEVER = ~0ull;
-enum : uint32_t { T_E = 0, T_N, T_P, T_A, T_BAD, T_OVF, T_A2, T_NFREE, T_H, T_WORDS = 16 };
+enum : uint32_t { T_E = 0, T_N, T_P, T_A, T_BAD, T_OVF, T_A2, T_NFREE, T_H, T_GATE = 15, T_WORDS = 16 };
 
 // Ordered scan by one 1024-thread workgroup over i in [0, n): emit(i, p, v)
 // with p = carry + sum of val(j) for j < i.  Returns carry + the total.
@@ -251,6 +251,13 @@ __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, co
   }
 }
 
+// The batch stands (no overflow, within the bound, no inconsistent lookup):
+// tot[T_GATE] = 0, which lets a commit queued behind it act.
+__global__ void lru_gate_kernel(uint32_t* tot, uint32_t C) {
+  if (threadIdx.x == 0)
+    tot[T_GATE] = (tot[T_OVF] == 0u && (uint64_t)tot[T_N] + tot[T_H] <= C && tot[T_BAD] == 0u) ? 0u : 1u;
+}
+
 // ---- ordered scans over many workgroups (rank walk, free list, new LRU order)
 //
 // Two launches instead of one workgroup walking everything (whose dependent
@@ -276,6 +283,7 @@ struct ScanArgs {
   uint32_t* freel;
   uint32_t* part;
   uint64_t* hmin_reset;                            // (SK_RANK) reset hmin behind the scan: the next guess's atomics
+  const uint32_t* gate;                            // (commit scans) nonzero: the commit does nothing
 };
 
 template <int K>
@@ -330,6 +338,7 @@ __device__ __forceinline__ void scan_total(const ScanArgs& a, uint32_t total) {
 template <int K>
 __global__ __launch_bounds__(256) void scan_count_kernel(ScanArgs a) {
   __shared__ uint32_t ws[4];
+  if (a.gate && *a.gate) return;
   const uint32_t n = scan_n<K>(a), i0 = blockIdx.x * 1024u + 4u * threadIdx.x;
   if (blockIdx.x * 1024u >= n && blockIdx.x != 0) return;
   uint32_t c = 0, v;
@@ -345,6 +354,7 @@ __global__ __launch_bounds__(256) void scan_count_kernel(ScanArgs a) {
 template <int K>
 __global__ __launch_bounds__(256) void scan_emit_kernel(ScanArgs a) {
   __shared__ uint32_t ws[4], s_base;
+  if (a.gate && *a.gate) return;
   const uint32_t n = scan_n<K>(a), ntiles = (n + 1023u) / 1024u, tile = blockIdx.x;
   if (tile >= ntiles && !(tile == 0 && n == 0)) return;
   // base = counts of the tiles before this one
@@ -384,10 +394,17 @@ __global__ __launch_bounds__(256) void scan_emit_kernel(ScanArgs a) {
 
 // ---- commit
 
+// (commit kernels: gate nonzero = the eviction pass found the batch
+// inconsistent; the commit, queued before the host has read that, does nothing)
+__global__ __launch_bounds__(256) void lru_unmark_kernel(uint32_t* alive, uint32_t n, const uint32_t* gate) {
+  if (gate && *gate) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) alive[i] = 0u;
+}
 __global__ __launch_bounds__(256) void lru_mark_kernel(const uint32_t* tot, const uint32_t* queue,
-                                                       const uint64_t* hmin, const uint64_t* wpop, uint32_t* alive) {
+                                                       const uint64_t* hmin, const uint64_t* wpop, uint32_t* alive,
+                                                       const uint32_t* gate) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= tot[T_A]) return;
+  if ((gate && *gate) || r >= tot[T_A]) return;
   const uint32_t s = queue[r];
   alive[s] = (hmin[s] == NEVER && wpop[s] != NEVER) ? 0u : 1u;   // evicted in the batch
 }
@@ -399,7 +416,8 @@ struct Wipe {
   u32x4* ftab; uint32_t ftab_n;
   uint32_t* gfilt; uint32_t gfilt_n;
 };
-__global__ __launch_bounds__(256) void lru_wipe_kernel(Wipe w) {
+__global__ __launch_bounds__(256) void lru_wipe_kernel(Wipe w, const uint32_t* gate) {
+  if (gate && *gate) return;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint64_t i = i0; i <= w.g.mask; i += stride) { w.g.keys[i] = EMPTY_KEY; w.g.vals[i] = ~0ull; }
@@ -410,9 +428,9 @@ __global__ __launch_bounds__(256) void lru_wipe_kernel(Wipe w) {
 
 __global__ __launch_bounds__(256) void lru_insert_alive_kernel(uint32_t C, const uint32_t* alive,
                                                                const uint64_t* skey, HashTab g, FiltSet fs,
-                                                               int32_t* status) {
+                                                               int32_t* status, const uint32_t* gate) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= C || !alive[s]) return;
+  if ((gate && *gate) || s >= C || !alive[s]) return;
   const uint64_t k = skey[s];
   if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), s)) atomicOr(status, 2);
   filt_insert(fs, (uint32_t)k, (uint32_t)(k >> 32));
@@ -425,10 +443,10 @@ __global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const u
                                                              const uint32_t* freel, const uint8_t* in,
                                                              const uint64_t* chunk_off, uint64_t* skey,
                                                              uint32_t* alive, HashTab g, uint8_t* pool, FiltSet fs,
-                                                             int32_t* status) {
+                                                             int32_t* status, const uint32_t* gate) {
   const uint64_t w = (uint64_t)blockIdx.x * 4 + readfirst(threadIdx.x >> 6);
   const uint32_t c = (uint32_t)(w / maxd), d = (uint32_t)(w % maxd);
-  if (c >= n || d >= ndecl[c]) return;
+  if ((gate && readfirst(*gate)) || c >= n || d >= ndecl[c]) return;
   const uint4 dd = decl[(uint64_t)c * maxd + d];
   // the segment's loads first: a returning atomic (the table insert) waits for
   // every older memory operation of the wave on gfx9, so loads issued after it
@@ -452,9 +470,10 @@ __global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const u
 // latest reference of each slot.
 __global__ __launch_bounds__(256) void lru_lastref_kernel(uint32_t n, EvRows R, const uint32_t* enter_base,
                                                           const uint32_t* freel, HashTab g, uint64_t clock,
-                                                          uint64_t* lastref, uint32_t* evslot, uint64_t* evtime) {
+                                                          uint64_t* lastref, uint32_t* evslot, uint64_t* evtime,
+                                                          const uint32_t* gate) {
   const uint32_t c = wave_chunk();
-  if (c >= n) return;
+  if ((gate && readfirst(*gate)) || c >= n) return;
   const uint64_t r0 = R.row(c);
   const uint32_t cnt = R.count(c);
   for (uint32_t k = lane_id(); k < cnt; k += 64) {
@@ -530,7 +549,7 @@ LruBatch batch_of(const XcgStreamArgs& a) {
 // Eviction times from a batch's references: tau, first hits, the LRU-order
 // scan (ptime, wpop), and -- check != 0 -- every recorded persistent lookup
 // against them.  h_tot gets the totals.  Synchronises `st`.
-int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
+int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st, bool sync = true) {
   using namespace xcg;
   const uint32_t n = b.n;
   hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, b.nev, b.ndecl, b.maxe, L->C,
@@ -546,6 +565,14 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st) {
   if (check)
     hipLaunchKernelGGL(lru_check_kernel, wgrid, dim3(256), 0, st, n, R, (const uint64_t*)L->hmin,
                        (const uint64_t*)L->wpop, b.need, L->tot, b.bad_t, b.bad_hi);
+  if (!sync) {                                     // (the caller waits on L->tev after queueing more)
+    hipLaunchKernelGGL(lru_gate_kernel, dim3(1), dim3(64), 0, st, L->tot, L->C);
+    if (!L->tev && hipEventCreateWithFlags((hipEvent_t*)&L->tev, hipEventDisableTiming) != hipSuccess) return -5;
+    if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord((hipEvent_t)L->tev, st) != hipSuccess)
+      return -5;
+    return 0;
+  }
   if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return -5;
@@ -602,38 +629,56 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
 // Commit a consistent batch (its references as lru_times last saw them):
 // evict, number the new entries, rebuild table + probe structures, new LRU
 // order.  Asynchronous.
-extern "C" int xcg_lru_commit(const LruBatch* bp, XcgLruState* L, hipStream_t st) {
+namespace {
+// The device part of a commit; gate (nullable): a device word that, nonzero,
+// makes every kernel of it do nothing.
+int lru_commit_dev(const LruBatch* bp, XcgLruState* L, const uint32_t* gate, hipStream_t st) {
   using namespace xcg;
   const LruBatch& b = *bp;
   const uint32_t n = b.n, C = L->C;
   const unsigned cg = grid_for(C) < 1024 ? grid_for(C) : 1024;
-  hipLaunchKernelGGL(lru_fill32_kernel, dim3(cg), dim3(256), 0, st, L->alive, C, 0u);
+  hipLaunchKernelGGL(lru_unmark_kernel, dim3(cg), dim3(256), 0, st, L->alive, C, gate);
   hipLaunchKernelGGL(lru_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, (const uint32_t*)L->tot,
-                     (const uint32_t*)L->queue, (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->alive);
-  if (run_scan<SK_FREE>(L, scan_args(L, nullptr), C, st)) return -5;
+                     (const uint32_t*)L->queue, (const uint64_t*)L->hmin, (const uint64_t*)L->wpop, L->alive, gate);
+  ScanArgs fa = scan_args(L, nullptr);
+  fa.gate = gate;
+  if (run_scan<SK_FREE>(L, fa, C, st)) return -5;
   const HashTab g{b.g_keys, b.g_vals, b.g_mask};
   const FiltSet fs{b.g_filt, b.g_ftab, b.fmask, b.g_gfilt, b.gmask};
   Wipe w{g, b.g_filt, (u32x4*)b.g_ftab, b.fmask + 1, b.g_gfilt, b.gmask + 1};
-  hipLaunchKernelGGL(lru_wipe_kernel, dim3(1024), dim3(256), 0, st, w);
+  hipLaunchKernelGGL(lru_wipe_kernel, dim3(1024), dim3(256), 0, st, w, gate);
   hipLaunchKernelGGL(lru_insert_alive_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, (const uint32_t*)L->alive,
-                     (const uint64_t*)L->skey, g, fs, b.status);
+                     (const uint64_t*)L->skey, g, fs, b.status, gate);
   const uint64_t waves = (uint64_t)n * b.maxd;
   hipLaunchKernelGGL(lru_insert_new_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, n,
                      (const uint4*)b.decl, b.ndecl, b.maxd, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->freel, b.in, b.chunk_off, L->skey, L->alive, g, b.pool, fs, b.status);
+                     (const uint32_t*)L->freel, b.in, b.chunk_off, L->skey, L->alive, g, b.pool, fs, b.status, gate);
   const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
   hipLaunchKernelGGL(lru_lastref_kernel, dim3((n + 3) / 4), dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->freel, g, L->clock, L->lastref, L->evslot, L->evtime);
+                     (const uint32_t*)L->freel, g, L->clock, L->lastref, L->evslot, L->evtime, gate);
   {
-    if (run_scan<SK_QUEUE>(L, scan_args(L, b.nseg), (uint64_t)C + b.ev_bound, st)) return -5;
+    ScanArgs qa = scan_args(L, b.nseg);
+    qa.gate = gate;
+    if (run_scan<SK_QUEUE>(L, qa, (uint64_t)C + b.ev_bound, st)) return -5;
   }
-  if (hipGetLastError() != hipSuccess) return -5;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The host side of a commit that happened: the new LRU order, the clock.
+void lru_commit_host(XcgLruState* L, uint32_t n) {
   uint32_t* q = L->queue;
   L->queue = L->queue2;
   L->queue2 = q;
   L->clock += ((uint64_t)n << 21) + 4;
+}
+}  // namespace
+
+extern "C" int xcg_lru_commit(const LruBatch* bp, XcgLruState* L, hipStream_t st) {
+  if (lru_commit_dev(bp, L, nullptr, st)) return -5;
+  lru_commit_host(L, bp->n);
   return 0;
 }
+
 
 // Eviction times of a batch whose references are already classified (the
 // decoder's: fixed by the stream).  h_tot: totals.  Synchronises.
@@ -696,7 +741,13 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       rounds += r;
       if (rc) return rc;
       const clk::time_point q1 = dsync();
-      if (lru_times(batch_of(a), L, true, st)) return -5;
+      // The commit is queued behind the eviction pass, gated on its verdict
+      // (tot[T_GATE]), before the host has read the totals: it runs in the
+      // time the host waits for them.
+      const LruBatch b = batch_of(a);
+      if (lru_times(b, L, true, st, false)) return -5;
+      if (lru_commit_dev(&b, L, L->tot + T_GATE, st)) return -5;
+      if (hipEventSynchronize((hipEvent_t)L->tev) != hipSuccess) return -5;
       const clk::time_point q2 = dsync();
       if (lru_debug()) {
         int32_t stw = 0;
@@ -715,10 +766,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       per = m / 2;                                   // redo this part in halves
       continue;
     }
-    const LruBatch b = batch_of(a);
-    const clk::time_point c0 = dsync();
-    if (xcg_lru_commit(&b, L, st)) return -5;
-    if (lru_debug()) fprintf(stderr, "lru: commit %.3f ms\n", ms(c0, dsync()));
+    lru_commit_host(L, m);
     L->last_base = i0;
     i0 += m;
     // (a sub-batch that started below the limit saw fewer cached entries to
