@@ -146,6 +146,17 @@ __device__ __forceinline__ void tab_lookup2(const HashTab& a, const HashTab& b, 
   vb = ub == key ? readfirst64(xb) : (ub == EMPTY_KEY ? ~0ull : tab_probe_rest(b, key, ib));
 }
 
+// Per-thread probe on from slot i (whose key was neither `key` nor empty).
+__device__ __forceinline__ uint64_t tab_probe_rest_t(const HashTab& t, uint64_t key, uint32_t i) {
+  for (uint32_t n = 1; n <= t.mask; ++n) {
+    i = (i + 1) & t.mask;
+    const uint64_t k = t.keys[i];
+    if (k == key) return t.vals[i];
+    if (k == EMPTY_KEY) break;
+  }
+  return ~0ull;
+}
+
 // Per-thread exact lookup (each lane its own key): value or ~0 when absent.
 __device__ __forceinline__ uint64_t tab_lookup_t(const HashTab& t, uint32_t lo, uint32_t hi) {
   const uint64_t key = ((uint64_t)hi << 32) | lo;

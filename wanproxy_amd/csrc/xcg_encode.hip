@@ -1615,7 +1615,7 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
 // sequential encoder's: the screen only skips parses whose every lookup misses.
 constexpr int SCREEN_MAXD = 4;                       // chunks shorter than 4 tiles (< 8 KiB)
 constexpr uint32_t SCREEN_FOLD_WORDS = 32768;        // 128 KiB of LDS
-constexpr int SCREEN_W = 12;                         // waves per workgroup (one workgroup per CU)
+constexpr int SCREEN_W = 12;                         // waves per workgroup (one workgroup per CU; 16: 3 % slower)
 constexpr uint32_t SCR_NEEDY = 1u << 31, SCR_SKIP = 1u << 30;   // s_info flags
 __device__ __forceinline__ uint32_t fold_word_of(uint32_t k, uint32_t fwm) { return (k >> 10) & fwm; }
 
@@ -1916,17 +1916,18 @@ __device__ __forceinline__ void screen_chunk(const ScreenParams& prm, const uint
   verdict(((uint32_t)nt << 16) | olen);
 }
 
-// Pass 1: persistent workgroups of SCREEN_W waves over the chunks; a wave's
+// Pass 1: persistent workgroups of W waves over the chunks; a wave's
 // chunks chunk0, chunk0 + stride, ... in groups of 64 whose metadata lane k
 // holds.
-__global__ __launch_bounds__(64 * SCREEN_W) void stream_screen_kernel(ScreenParams prm, const uint32_t* fold,
-                                                                      uint32_t fwords, ScreenStage st) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void stream_screen_kernel(ScreenParams prm, const uint32_t* fold,
+                                                               uint32_t fwords, ScreenStage st) {
   __shared__ uint32_t F[SCREEN_FOLD_WORDS];
   for (uint32_t i = threadIdx.x; i < fwords / 4; i += blockDim.x) ((u32x4*)F)[i] = ((const u32x4*)fold)[i];
   const int wv = (int)readfirst(threadIdx.x >> 6);
-  const uint32_t stride = gridDim.x * SCREEN_W;
+  const uint32_t stride = gridDim.x * W;
   __syncthreads();
-  for (uint32_t base = blockIdx.x * SCREEN_W + (uint32_t)wv; base < prm.n; base += 64u * stride) {
+  for (uint32_t base = blockIdx.x * W + (uint32_t)wv; base < prm.n; base += 64u * stride) {
     const ScreenMeta meta = screen_meta(prm, base + (uint32_t)lane_id() * stride);
     ScreenLoad cur, nxt;
     screen_issue(prm, meta, 0, base, cur);
@@ -1954,15 +1955,32 @@ __global__ __launch_bounds__(256) void screen_finish_kernel(EncParams prm, Scree
   const uint32_t c = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
   const int l = lane_id();
   if (c >= prm.n) return;
-  const uint32_t info = readfirst(st.info[c]);
+  // One round trip for the verdict and what a screened chunk's check starts
+  // from (the staged count and rows are read whatever the verdict; a skipped
+  // or needy chunk ignores them).
+  const uint32_t info0 = st.info[c];
+  const uint32_t qn0 = st.qcnt[c];
+  const uint4 r0 = l < SCREEN_MAXD ? st.rows[(uint64_t)c * SCREEN_MAXD + l] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t ns0 = *prm.nseg;
+  const uint32_t info = readfirst(info0);
   if (info & SCR_SKIP) return;
   bool needy = (info & SCR_NEEDY) != 0u;
   const uint32_t nt = (info >> 16) & 0xFFu;
   uint4 r = make_uint4(0u, 0u, 0u, 0u);
   if (!needy) {
-    const uint32_t qn = readfirst(st.qcnt[c]);
+    const uint32_t qn = readfirst(qn0);
     const uint32_t* const q = st.qkeys + (uint64_t)c * SCREEN_QCAP;
-    if ((uint32_t)l < nt) r = st.rows[(uint64_t)c * SCREEN_MAXD + l];
+    const bool tile = (uint32_t)l < nt;
+    if (tile) r = r0;
+    // the tiles' own windows: their first probe slots in the persistent cache
+    // and the batch table load with the first keys (a second round trip, not
+    // a chain of them after the keys')
+    const uint64_t key = ((uint64_t)r.y << 32) | r.x;
+    const bool gl = tile && readfirst(ns0) != 0u, bl = tile && prm.use_b;
+    const uint32_t ig = tab_slot(r.x, r.y, prm.g.mask), ib = prm.use_b ? tab_slot(r.x, r.y, prm.b.mask) : 0u;
+    uint64_t kg = EMPTY_KEY, vg = 0ull, kb = EMPTY_KEY, vb = 0ull;
+    if (gl) { kg = prm.g.keys[ig]; vg = prm.g.vals[ig]; }
+    if (bl) { kb = prm.b.keys[ib]; vb = prm.b.vals[ib]; }
     bool hit = false;
     // up to 8 keys per lane in flight: their filter words, then (rarely) buckets
     for (uint32_t j0 = 0; j0 < qn; j0 += 512) {
@@ -1983,13 +2001,12 @@ __global__ __launch_bounds__(256) void screen_finish_kernel(EncParams prm, Scree
         if (j < qn && gfilt_test(w[t], k[t])) hit |= ftab_match(prm.lf.ftab[fbucket(k[t], prm.lf.fmask)], k[t]);
       }
     }
-    if ((uint32_t)l < nt) {
-      if (*prm.nseg != 0u && tab_lookup_t(prm.g, r.x, r.y) != ~0ull) hit = true;
-      if (prm.use_b) {
-        const uint64_t bv = tab_lookup_t(prm.b, r.x, r.y);
-        if (bv != ~0ull && ((uint32_t)(bv >> 32) < c || ((uint32_t)(bv >> 32) == c && (uint32_t)bv != r.z)))
-          hit = true;
-      }
+    // (a tile is in the batch table as this chunk's own declaration; anything
+    // else there or in the persistent cache is a possible hit)
+    if (gl && (kg == key ? vg : (kg == EMPTY_KEY ? ~0ull : tab_probe_rest_t(prm.g, key, ig))) != ~0ull) hit = true;
+    if (bl) {
+      const uint64_t bv = kb == key ? vb : (kb == EMPTY_KEY ? ~0ull : tab_probe_rest_t(prm.b, key, ib));
+      if (bv != ~0ull && ((uint32_t)(bv >> 32) < c || ((uint32_t)(bv >> 32) == c && (uint32_t)bv != r.z))) hit = true;
     }
     needy = ballot(hit) != 0;
   }
@@ -2852,8 +2869,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       const ScreenStage sst{a->s_info, (uint4*)a->s_rows, a->s_qcnt, a->s_qkeys};
       const ScreenParams sp{prm.in, prm.chunk_off, prm.chunk_len, prm.out_off, prm.out, prm.decl, prm.ndecl,
                             prm.changed, prm.need, prm.n, prm.skip_below, prm.max_len, prm.maxd};
-      hipLaunchKernelGGL(stream_screen_kernel, dim3(wgs), dim3(64 * SCREEN_W), 0, stream, sp, (const uint32_t*)a->s_fold,
-                         fwords, sst);
+      hipLaunchKernelGGL(stream_screen_kernel<SCREEN_W>, dim3(wgs), dim3(64 * SCREEN_W), 0, stream, sp,
+                         (const uint32_t*)a->s_fold, fwords, sst);
       hipLaunchKernelGGL(screen_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, prm, sst, a->s_work);
       prm.work = a->s_work;
       if (xcg_screen_counting()) {
