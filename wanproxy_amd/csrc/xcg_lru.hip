@@ -86,6 +86,19 @@ __device__ __forceinline__ uint64_t ev_time(uint32_t c, uint4 e) { return ((uint
 __global__ __launch_bounds__(256) void lru_fill64_kernel(uint64_t* p, uint32_t n, uint64_t v) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
+// Several fills in one launch (each launch costs ~4 us of the sub-batch).
+struct Fill64 {
+  uint64_t* p;
+  uint32_t n;
+  uint64_t v;
+};
+__global__ __launch_bounds__(256) void lru_fill64x4_kernel(Fill64 f0, Fill64 f1, Fill64 f2, Fill64 f3) {
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, step = gridDim.x * blockDim.x;
+  for (uint32_t i = i0; i < f0.n; i += step) f0.p[i] = f0.v;
+  for (uint32_t i = i0; i < f1.n; i += step) f1.p[i] = f1.v;
+  for (uint32_t i = i0; i < f2.n; i += step) f2.p[i] = f2.v;
+  for (uint32_t i = i0; i < f3.n; i += step) f3.p[i] = f3.v;
+}
 __global__ __launch_bounds__(256) void lru_fill32_kernel(uint32_t* p, uint32_t n, uint32_t v) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
@@ -555,8 +568,8 @@ int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st, boo
   hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, b.nev, b.ndecl, b.maxe, L->C,
                      (const uint32_t*)b.nseg, L->ev_base, L->enter_base, b.need, L->tot);
   const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
+  hipLaunchKernelGGL(lru_fill64x4_kernel, dim3(cg), dim3(256), 0, st, Fill64{L->hmin, L->C, NEVER},
+                     Fill64{L->tau, L->C, NEVER}, Fill64{nullptr, 0u, 0ull}, Fill64{nullptr, 0u, 0ull});
   const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
   const dim3 wgrid((n + 3) / 4);
   hipLaunchKernelGGL(lru_events_kernel, wgrid, dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
@@ -593,12 +606,11 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   const uint32_t n = a.n;
   const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
   const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};   // (b: the rounds rebuild it)
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(1024), dim3(256), 0, st, b.keys, b.mask + 1, EMPTY_KEY);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(1024), dim3(256), 0, st, b.vals, b.mask + 1, ~0ull);
+  (void)cg;
+  hipLaunchKernelGGL(lru_fill64x4_kernel, dim3(1024), dim3(256), 0, st, Fill64{b.keys, b.mask + 1, EMPTY_KEY},
+                     Fill64{b.vals, b.mask + 1, ~0ull}, Fill64{L->hmin, L->C, NEVER}, Fill64{L->tau, L->C, NEVER});
   hipLaunchKernelGGL(lru_seed_table_kernel, dim3(grid_for((uint64_t)n * a.maxd)), dim3(256), 0, st, n,
                      (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->hmin, L->C, NEVER);
-  hipLaunchKernelGGL(lru_fill64_kernel, dim3(cg), dim3(256), 0, st, L->tau, L->C, NEVER);
   uint32_t* cnt = a.nhits;                         // (scratch until the rounds: round 1 rewrites it)
   const dim3 wgrid((n + 3) / 4);
   // guess 0 takes every cached tile for a hit; each further guess classifies
