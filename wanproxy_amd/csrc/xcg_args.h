@@ -98,6 +98,10 @@ struct XcgStreamArgs {
   void* s_rows = nullptr;        // [n * 4] uint4: its staged rows
   uint32_t* s_qcnt = nullptr;    // [n] and [n * 1024]: the windows it queues for the probe
   uint32_t* s_qkeys = nullptr;
+  // (bounded cache) called behind each Jacobi verification, before the host
+  // reads its flags: queues work gated on vflags[1] == 0 (the round converged)
+  int (*post_verify)(void* user, const uint32_t* vbusy, hipStream_t st) = nullptr;
+  void* post_user = nullptr;
 };
 
 // (a)-probe sizes: at most A_LIMIT newly visible hashes per verification (more:

@@ -3081,6 +3081,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
       const hipEvent_t vev = flags_ev.ev;
       if (!vev || hipEventRecord(vev, stream) != hipSuccess) return -5;
       commit(a->vflags + 1);
+      if (a->post_verify && a->post_verify(a->post_user, a->vflags + 1, stream)) return -5;
       if (hipEventSynchronize(vev) != hipSuccess) return -5;
       if (a->decls_out) *a->decls_out = a->h_vflags[2];
       if (stream_debug())

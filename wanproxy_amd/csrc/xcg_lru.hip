@@ -92,7 +92,9 @@ struct Fill64 {
   uint32_t n;
   uint64_t v;
 };
-__global__ __launch_bounds__(256) void lru_fill64x4_kernel(Fill64 f0, Fill64 f1, Fill64 f2, Fill64 f3) {
+__global__ __launch_bounds__(256) void lru_fill64x4_kernel(Fill64 f0, Fill64 f1, Fill64 f2, Fill64 f3,
+                                                           const uint32_t* skip) {
+  if (skip && *skip) return;
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, step = gridDim.x * blockDim.x;
   for (uint32_t i = i0; i < f0.n; i += step) f0.p[i] = f0.v;
   for (uint32_t i = i0; i < f1.n; i += step) f1.p[i] = f1.v;
@@ -107,7 +109,8 @@ __global__ __launch_bounds__(256) void lru_fill32_kernel(uint32_t* p, uint32_t n
 __global__ __launch_bounds__(1024) void lru_prep_kernel(uint32_t n, const uint32_t* nev, const uint32_t* ndecl,
                                                         uint32_t maxe, uint32_t C, const uint32_t* nseg,
                                                         uint32_t* ev_base, uint32_t* enter_base, uint32_t* need,
-                                                        uint32_t* tot) {
+                                                        uint32_t* tot, const uint32_t* skip) {
+  if (skip && *skip) return;
   if (threadIdx.x == 0) tot[T_OVF] = 0;
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) need[i] = 0u;
   __syncthreads();
@@ -151,9 +154,9 @@ __device__ __forceinline__ uint32_t wave_chunk() { return blockIdx.x * 4u + read
 
 __global__ __launch_bounds__(256) void lru_events_kernel(uint32_t n, EvRows R, const uint32_t* enter_base,
                                                          const uint32_t* tot, uint32_t C, uint64_t* hmin,
-                                                         uint64_t* tau) {
+                                                         uint64_t* tau, const uint32_t* skip) {
   const uint32_t c = wave_chunk();
-  if (c >= n) return;
+  if ((skip && readfirst(*skip)) || c >= n) return;
   const uint64_t r0 = R.row(c);
   const uint32_t cnt = R.count(c);
   for (uint32_t k = lane_id(); k < cnt; k += 64) {
@@ -236,9 +239,9 @@ __global__ __launch_bounds__(256) void lru_seed_table_kernel(uint32_t n, const u
 // after the last, encode_chunk "Re-parse restart").
 __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, const uint64_t* hmin,
                                                         const uint64_t* wpop, uint32_t* need, uint32_t* tot,
-                                                        uint32_t* bad_t, uint32_t* bad_hi) {
+                                                        uint32_t* bad_t, uint32_t* bad_hi, const uint32_t* skip) {
   const uint32_t c = wave_chunk();
-  if (c >= n) return;
+  if ((skip && readfirst(*skip)) || c >= n) return;
   const uint64_t r0 = R.row(c);
   const uint32_t cnt = R.count(c);
   uint32_t lo = ~0u, hi = 0u;
@@ -266,9 +269,12 @@ __global__ __launch_bounds__(256) void lru_check_kernel(uint32_t n, EvRows R, co
 
 // The batch stands (no overflow, within the bound, no inconsistent lookup):
 // tot[T_GATE] = 0, which lets a commit queued behind it act.
-__global__ void lru_gate_kernel(uint32_t* tot, uint32_t C) {
+// (skip set: the pass itself was skipped -- the Jacobi round it followed did
+// not converge -- so nothing stands)
+__global__ void lru_gate_kernel(uint32_t* tot, uint32_t C, const uint32_t* skip) {
   if (threadIdx.x == 0)
-    tot[T_GATE] = (tot[T_OVF] == 0u && (uint64_t)tot[T_N] + tot[T_H] <= C && tot[T_BAD] == 0u) ? 0u : 1u;
+    tot[T_GATE] = !(skip && *skip) && tot[T_OVF] == 0u && (uint64_t)tot[T_N] + tot[T_H] <= C && tot[T_BAD] == 0u
+                      ? 0u : 1u;
 }
 
 // ---- ordered scans over many workgroups (rank walk, free list, new LRU order)
@@ -562,24 +568,29 @@ LruBatch batch_of(const XcgStreamArgs& a) {
 // Eviction times from a batch's references: tau, first hits, the LRU-order
 // scan (ptime, wpop), and -- check != 0 -- every recorded persistent lookup
 // against them.  h_tot gets the totals.  Synchronises `st`.
-int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st, bool sync = true) {
+// skip (nullable, !sync only): a device word that, nonzero, makes the whole
+// pass do nothing (and the gate refuse the commit).
+int lru_times(const LruBatch& b, XcgLruState* L, bool check, hipStream_t st, bool sync = true,
+              const uint32_t* skip = nullptr) {
   using namespace xcg;
   const uint32_t n = b.n;
   hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, b.nev, b.ndecl, b.maxe, L->C,
-                     (const uint32_t*)b.nseg, L->ev_base, L->enter_base, b.need, L->tot);
+                     (const uint32_t*)b.nseg, L->ev_base, L->enter_base, b.need, L->tot, skip);
   const unsigned cg = grid_for(L->C) < 1024 ? grid_for(L->C) : 1024;
   hipLaunchKernelGGL(lru_fill64x4_kernel, dim3(cg), dim3(256), 0, st, Fill64{L->hmin, L->C, NEVER},
-                     Fill64{L->tau, L->C, NEVER}, Fill64{nullptr, 0u, 0ull}, Fill64{nullptr, 0u, 0ull});
+                     Fill64{L->tau, L->C, NEVER}, Fill64{nullptr, 0u, 0ull}, Fill64{nullptr, 0u, 0ull}, skip);
   const EvRows R{(const uint4*)b.ev, b.nev, (const uint32_t*)L->ev_base, b.maxe, b.dense != 0};
   const dim3 wgrid((n + 3) / 4);
   hipLaunchKernelGGL(lru_events_kernel, wgrid, dim3(256), 0, st, n, R, (const uint32_t*)L->enter_base,
-                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau);
-  if (run_scan<SK_RANK>(L, scan_args(L, nullptr), L->C, st)) return -5;
+                     (const uint32_t*)L->tot, L->C, L->hmin, L->tau, skip);
+  ScanArgs ra = scan_args(L, nullptr);
+  ra.gate = skip;
+  if (run_scan<SK_RANK>(L, ra, L->C, st)) return -5;
   if (check)
     hipLaunchKernelGGL(lru_check_kernel, wgrid, dim3(256), 0, st, n, R, (const uint64_t*)L->hmin,
-                       (const uint64_t*)L->wpop, b.need, L->tot, b.bad_t, b.bad_hi);
+                       (const uint64_t*)L->wpop, b.need, L->tot, b.bad_t, b.bad_hi, skip);
   if (!sync) {                                     // (the caller waits on L->tev after queueing more)
-    hipLaunchKernelGGL(lru_gate_kernel, dim3(1), dim3(64), 0, st, L->tot, L->C);
+    hipLaunchKernelGGL(lru_gate_kernel, dim3(1), dim3(64), 0, st, L->tot, L->C, skip);
     if (!L->tev && hipEventCreateWithFlags((hipEvent_t*)&L->tev, hipEventDisableTiming) != hipSuccess) return -5;
     if (hipMemcpyAsync(L->h_tot, L->tot, 4 * T_WORDS, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord((hipEvent_t)L->tev, st) != hipSuccess)
@@ -608,7 +619,8 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
   const HashTab g{a.g_keys, a.g_vals, a.g_mask}, b{a.b_keys, a.b_vals, a.b_mask};   // (b: the rounds rebuild it)
   (void)cg;
   hipLaunchKernelGGL(lru_fill64x4_kernel, dim3(1024), dim3(256), 0, st, Fill64{b.keys, b.mask + 1, EMPTY_KEY},
-                     Fill64{b.vals, b.mask + 1, ~0ull}, Fill64{L->hmin, L->C, NEVER}, Fill64{L->tau, L->C, NEVER});
+                     Fill64{b.vals, b.mask + 1, ~0ull}, Fill64{L->hmin, L->C, NEVER}, Fill64{L->tau, L->C, NEVER},
+                     nullptr);
   hipLaunchKernelGGL(lru_seed_table_kernel, dim3(grid_for((uint64_t)n * a.maxd)), dim3(256), 0, st, n,
                      (const uint4*)a.decl, (const uint32_t*)a.ndecl, a.maxd, b, a.status);
   uint32_t* cnt = a.nhits;                         // (scratch until the rounds: round 1 rewrites it)
@@ -625,7 +637,8 @@ int lru_seed_guess(const XcgStreamArgs& a, XcgLruState* L, hipStream_t st) {
                        (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
                        (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 0, pt);
     hipLaunchKernelGGL(lru_prep_kernel, dim3(1), dim3(1024), 0, st, n, (const uint32_t*)a.nev, (const uint32_t*)cnt,
-                       a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base, a.need, L->tot);
+                       a.maxe, L->C, (const uint32_t*)a.nseg, L->ev_base, L->enter_base, a.need, L->tot,
+                       (const uint32_t*)nullptr);
     hipLaunchKernelGGL(lru_seed_classify_kernel, wgrid, dim3(256), 0, st, n, (const uint4*)a.decl,
                        (const uint32_t*)a.ndecl, a.maxd, a.chunk_len, g, b, cnt, (const uint32_t*)L->enter_base,
                        (const uint32_t*)L->tot, L->C, L->hmin, L->tau, 1, pt);
@@ -735,6 +748,22 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
     if (a.stats) a.stats += 4ull * i0;
     a.ptime = L->ptime;
     a.no_commit = 1;
+    // Behind each Jacobi verification, before the host has read its flags: the
+    // eviction pass and the gated commit, both doing nothing unless the round
+    // converged (vflags[1] == 0).  The host then waits once, on the totals.
+    struct Hook {
+      XcgLruState* L;
+      const XcgStreamArgs* a;
+      bool fired;
+    } hook{L, &a, false};
+    a.post_user = &hook;
+    a.post_verify = [](void* u, const uint32_t* vbusy, hipStream_t s) -> int {
+      Hook* h = (Hook*)u;
+      const LruBatch b = batch_of(*h->a);
+      h->fired = true;
+      if (lru_times(b, h->L, true, s, false, vbusy)) return -5;
+      return lru_commit_dev(&b, h->L, h->L->tot + T_GATE, s);
+    };
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
     auto dsync = [&]() { if (lru_debug()) (void)hipStreamSynchronize(st); return clk::now(); };
@@ -749,6 +778,7 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       a.need_given = pass > 0;                       // re-parse the chunks with an inconsistent lookup
       int r = 0;
       const clk::time_point q0 = dsync();
+      hook.fired = false;
       const int rc = xcg_launch_encode_stream(&a, &r, st);
       rounds += r;
       if (rc) return rc;
@@ -756,9 +786,11 @@ extern "C" int xcg_lru_encode_stream(const XcgStreamArgs* a0, XcgLruState* L, in
       // The commit is queued behind the eviction pass, gated on its verdict
       // (tot[T_GATE]), before the host has read the totals: it runs in the
       // time the host waits for them.
-      const LruBatch b = batch_of(a);
-      if (lru_times(b, L, true, st, false)) return -5;
-      if (lru_commit_dev(&b, L, L->tot + T_GATE, st)) return -5;
+      if (!hook.fired) {                             // (no verification ran: one chunk, or nothing declared)
+        const LruBatch b = batch_of(a);
+        if (lru_times(b, L, true, st, false)) return -5;
+        if (lru_commit_dev(&b, L, L->tot + T_GATE, st)) return -5;
+      }
       if (hipEventSynchronize((hipEvent_t)L->tev) != hipSuccess) return -5;
       const clk::time_point q2 = dsync();
       if (lru_debug()) {
