@@ -499,6 +499,12 @@ int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in
  * else through a global (L2-resident) one; both give the same output.
  * Returns the previous threshold (default 220000, or XCG_LDS_FILTER_KEYS). */
 uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
+/* Diagnostics / tests: past that threshold, and while the cache + batch hold at
+ * most this many keys, the LDS filter still goes first and only the positions
+ * it passes load the global filter (fewer L2 requests); beyond it the global
+ * filter alone.  Same output either way.  Returns the previous threshold
+ * (default 700000, or XCG_LDS_PREFILTER_KEYS). */
+uint32_t xcg_debug_set_lds_prefilter_keys(uint32_t keys);
 /* Diagnostics / tests: stream batches start either with a parse round against
  * the cache alone, or -- automatically when the context's previous batch
  * declared segments -- from each chunk's 2048-byte tiling (its cold parse),

@@ -37,6 +37,12 @@ def hbm(agg):
             agg['hbm_GBps'] = round(agg['hbm_bytes'] / (agg['us'] * 1e3), 1)
     if 'SQ_WAVE_CYCLES' in agg and 'SQ_WAIT_ANY' in agg and agg['SQ_WAVE_CYCLES']:
         agg['wait_any_frac'] = round(agg['SQ_WAIT_ANY'] / agg['SQ_WAVE_CYCLES'], 3)
+    # L2 hit rate (MI355X_MICROARCH.md "L2 per XCD": hit / (hit + miss))
+    h, m = agg.get('TCC_HIT_sum'), agg.get('TCC_MISS_sum')
+    if h is not None and m is not None and h + m:
+        agg['l2_hit_rate'] = round(h / (h + m), 3)
+        if agg.get('us'):
+            agg['l2_req_G_per_s'] = round((h + m) / (agg['us'] * 1e3), 1)
     return agg
 
 
@@ -49,7 +55,7 @@ for d in sorted(glob.glob(os.path.join(src, '*', ''))):
     disp = [{'kernel': short(r['Kernel_Name']), 'grid': int(r['Grid_Size_X']),
              'us': (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3} for r in trace]
     # counters per dispatch, matched to the trace in launch order per kernel
-    for sub in ('fetch', 'write', 'sq', 'sq2'):
+    for sub in ('fetch', 'write', 'sq', 'sq2', 'l2', 'tcp'):
         per = collections.OrderedDict()
         for r in rows(d, sub, 'run_counter_collection.csv'):
             per.setdefault(int(r['Dispatch_Id']), [short(r['Kernel_Name']), {}])[1][r['Counter_Name']] = \
@@ -86,6 +92,9 @@ for d in sorted(glob.glob(os.path.join(src, '*', ''))):
         if sp and 'hbm_bytes' in sp[-1]:
             out['c2s_seeded'] = {'dispatches': 1, 'us_sum': sp[-1]['us'], 'hbm_bytes': sp[-1]['hbm_bytes'],
                                  'hbm_GBps': sp[-1].get('hbm_GBps'), 'wait_any_frac': sp[-1].get('wait_any_frac')}
+    if cfg != 'c2s':
+        # every stream-parse launch of the configuration, one by one
+        out[cfg]['stream_launches'] = [hbm(dict(x)) for x in disp if K in x['kernel']]
 json.dump(out, open(dst, 'w'), indent=1)
 print(json.dumps({c: {'total_us': v['kernel_us_total'], 'top': list(v['kernels'])[:6]} for c, v in out.items()
                   if 'kernels' in v}, indent=1))

@@ -2,9 +2,10 @@
 (SURVEY.md 8d C3, C4, C5), bit-exact against the CPU oracle run with the same
 sequential XCodecEncoder semantics over the whole input, and decoded back.
 
-Each runs with both lane-filter modes of the stream encoder forced (the 64 KiB
-LDS filter, and the global L2-resident filter used above ~220 k keys), so the
-large-cache path is covered at sizes the oracle finishes in seconds.
+Each runs with every lane-filter mode of the stream encoder forced (the 64 KiB
+LDS filter; the LDS filter in front of the global L2-resident one, used above
+~220 k keys; the global filter alone, above ~700 k), so the large-cache paths
+are covered at sizes the oracle finishes in seconds.
 """
 import numpy as np
 import pytest
@@ -12,15 +13,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KiB, MiB = 1024, 1 << 20
-MODES = {'lds': 1 << 30, 'global': 0}
+# (LDS filter threshold, LDS-prefilter threshold) in keys
+MODES = {'lds': (1 << 30, 1 << 30), 'prefilter': (0, 1 << 30), 'global': (0, 0)}
 
 
 @pytest.fixture(params=sorted(MODES))
 def filter_mode(request):
     from wanproxy_amd.xcgpu import lib
-    old = lib().xcg_debug_set_lds_filter_keys(MODES[request.param])
+    old = lib().xcg_debug_set_lds_filter_keys(MODES[request.param][0])
+    oldp = lib().xcg_debug_set_lds_prefilter_keys(MODES[request.param][1])
     yield request.param
     lib().xcg_debug_set_lds_filter_keys(old)
+    lib().xcg_debug_set_lds_prefilter_keys(oldp)
 
 
 def encode_in_batches(ctx, data, offs, lens, per):

@@ -133,6 +133,7 @@ struct EncParams {
   uint32_t maxd;
   uint32_t* changed;   // lowest chunk whose declaration list differs from the last round (~0: none)
   uint32_t lds_filter_keys;  // LDS lane filter up to this many keys, else the global one
+  uint32_t lds_prefilter_keys;  // up to this many: the LDS filter in front of the global one (fmode 3)
   const uint32_t* nseg;    // segments in the persistent cache
   const uint32_t* bcount;  // [64] partial counts of the batch table's declarations (use_b)
   uint32_t skip_below; // chunks below this keep their last parse (their batch input is unchanged)
@@ -360,8 +361,15 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
 // the 16-bit fingerprint buckets (an L2-resident table), all of a lane's
 // loads in flight together instead of one round trip per group of positions.
 // Passes beyond GSLOTS in one half are reported as events unchecked.
+// FM 3 (caches past the LDS filter's ~220 k keys): the global filter mode is
+// bound by L2 requests, one per window position (rocprofv3 TCC_READ ~430 M per
+// 512 MiB C5 sub-batch at a 97 % L2 hit rate, profiles/r06_l2_*), so the
+// saturated LDS filter (FP ~0.4 at 260 k keys, ~0.7 at 470 k) goes first and
+// only the lanes it passes load their global word (exec-masked: the other
+// lanes send no request).
 constexpr int GSLOTS = 8;
 constexpr uint32_t LDS_FILTER_KEYS_DEFAULT = 220000;
+constexpr uint32_t LDS_PREFILTER_KEYS_DEFAULT = 700000;
 struct GlbQ {
   char* lds;        // LDS base of the workgroup's struct (offset 0)
   uint32_t lfo;     // byte offset of the lane filter (FM 1)
@@ -461,12 +469,19 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) e[t] = *(const uint2*)(kblk + ((kv[t] & KM) | kofs));
-    if (FM == 1) {
+    if (FM == 1 || FM == 3) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) fw[t] = *(const uint32_t*)(gq.lds + gq.lfo + filt_word_ofs(kv[t]));
     } else if (FM == 2) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) fw[t] = gq.gf[gfilt_word(kv[t], gq.gmask)];
+    }
+    if (FM == 3) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t w = filt_test(fw[t], kv[t]) ? gq.gf[gfilt_word(kv[t], gq.gmask)] : 0u;
+        fw[t] = w;
+      }
     }
   };
   uint32_t kc[4], fc[4];
@@ -481,7 +496,7 @@ __device__ __forceinline__ uint32_t roll_probe(const Piece& P, uint32_t NX1, uin
       // Persistent cache + batch declarations, pass 1: queue filter passes.
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const uint32_t p = FM == 1 ? filt_test(fc[t], kc[t]) : gfilt_test(fc[t], kc[t]);
+        const uint32_t p = FM == 1 ? filt_test(fc[t], kc[t]) : gfilt_test(fc[t], kc[t]);   // (FM 3: 0 if the LDS one failed)
         *(uint32_t*)(gq.lds + gq.sa) = kc[t];
         gq.sa = min(gq.sa + (p << 8), gq.salim);
         gq.pm |= p << (4 * g + t);
@@ -628,7 +643,7 @@ struct GlbView {
   char* lds;
   uint32_t lfo;
   uint32_t sofs;
-  int fmode;   // 0: no probe, 1: LDS lane filter, 2: global lane filter
+  int fmode;   // 0: no probe, 1: LDS lane filter, 2: global lane filter, 3: LDS filter, then global
   uint32_t* ro;   // (stream) the wave's per-declaration output lengths, LDS
   uint32_t* rsv;  // (stream) the wave's restart state, LDS: slot, old nev, nhits, olen, ndecl, restart ndecl
 };
@@ -835,7 +850,7 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
   // false negatives; the global-filter mode goes to the exact tables)
   auto glb_pass = [&](uint32_t k) -> bool {
     if (gs.fmode == 0) return false;
-    if (gs.fmode == 2) return true;
+    if (gs.fmode == 2) return true;   // (1 and 3: the LDS filter)
     return readfirst(filt_test(*(const uint32_t*)(gs.lds + gs.lfo + filt_word_ofs(k)), k)) != 0u;
   };
   bool chain = false;                              // the last op was a REF
@@ -1288,6 +1303,8 @@ __device__ __forceinline__ void encode_chunk(const EncParams& prm, char* kblk, c
           ev = by_novf(std::integral_constant<int, STREAM ? 1 : 0>{});
         } else if (STREAM && gs.fmode == 2) {
           ev = by_novf(std::integral_constant<int, STREAM ? 2 : 0>{});
+        } else if (STREAM && gs.fmode == 3) {
+          ev = by_novf(std::integral_constant<int, STREAM ? 3 : 0>{});
         } else {
           ev = by_novf(std::integral_constant<int, 0>{});
         }
@@ -1560,8 +1577,8 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   // up to LDS_FILTER_KEYS keys (FP <~10 %), else the global one.
   uint32_t keys = readfirst(*prm.nseg);
   if (prm.use_b) keys += readfirst(wave_sum(prm.bcount[lane_id()]));
-  const int fmode = keys == 0 ? 0 : (keys <= prm.lds_filter_keys ? 1 : 2);
-  if (fmode == 1) {
+  const int fmode = keys == 0 ? 0 : (keys <= prm.lds_filter_keys ? 1 : (keys <= prm.lds_prefilter_keys ? 3 : 2));
+  if (fmode == 1 || fmode == 3) {
     for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
       ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
   }
@@ -2700,6 +2717,15 @@ static uint32_t xcg_lds_filter_keys() { return __atomic_load_n(&g_lds_filter_key
 extern "C" uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys) {
   return __atomic_exchange_n(&g_lds_filter_keys, keys, __ATOMIC_RELAXED);
 }
+// Past that, the LDS filter still screens the global one's loads up to this
+// many keys (XCG_LDS_PREFILTER_KEYS, xcg_debug_set_lds_prefilter_keys).
+static uint32_t g_lds_prefilter_keys = [] {
+  const char* e = getenv("XCG_LDS_PREFILTER_KEYS");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : xcg::LDS_PREFILTER_KEYS_DEFAULT;
+}();
+extern "C" uint32_t xcg_debug_set_lds_prefilter_keys(uint32_t keys) {
+  return __atomic_exchange_n(&g_lds_prefilter_keys, keys, __ATOMIC_RELAXED);
+}
 
 // The tiling seed alone (decl / ndecl / nhits / changed), for a caller that
 // looks at it before the rounds (the bounded cache's first eviction guess);
@@ -2820,6 +2846,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.nseg = a->nseg;
   prm.bcount = a->bcount;
   prm.lds_filter_keys = xcg_lds_filter_keys();
+  prm.lds_prefilter_keys = __atomic_load_n(&g_lds_prefilter_keys, __ATOMIC_RELAXED);
   prm.ptime = a->ptime;
   prm.ev = (uint4*)a->ev;
   prm.nev = a->nev;

@@ -170,6 +170,8 @@ def lib():
     L.xcg_debug_restart_counts.restype = C.c_int
     L.xcg_debug_set_lds_filter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
+    L.xcg_debug_set_lds_prefilter_keys.argtypes = [C.c_uint32]
+    L.xcg_debug_set_lds_prefilter_keys.restype = C.c_uint32
     L.xcg_debug_set_screen.argtypes = [C.c_int]
     L.xcg_debug_set_screen.restype = C.c_int
     L.xcg_debug_screen_counts.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
