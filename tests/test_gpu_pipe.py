@@ -233,3 +233,38 @@ def test_hello_connects_peer_cache_by_uuid(kind):
         connect_registry_clear()
         for c in (codec, lenc, penc, pdec):
             c.close()
+
+
+def test_registry_clear_under_a_connected_pipe():
+    """A registry clear while a pipe still decodes on the context it connected
+    at <HELLO> (advisor round 5): the context stays alive for that pipe -- its
+    next frames REF what its first ones declared and decode -- and is destroyed
+    when the pipe closes; a new connect after the clear gets a fresh cache."""
+    from wanproxy_amd.xcgpu import Context, PipePair, connect_registry_clear, ctx_lookup
+    connect_registry_clear()
+    codec = Context(0, cache_segments=1 << 15)
+    lenc = Context(0, cache_segments=1 << 15)
+    penc = Context(0, cache_segments=1 << 15)
+    pdec = Context(0, cache_segments=1 << 15)
+    try:
+        p1 = PipePair(penc, pdec, UUID_A)
+        l1 = PipePair(lenc, codec, UUID_B, connect=True)
+        m = payload(11, 300_000)
+        _, got, _, _ = l1.decoder_consume(p1.encoder_consume(m))
+        assert got == m and l1.decoder_ctx() == ctx_lookup(UUID_A)
+        connect_registry_clear()                          # the pipe still holds its context
+        assert ctx_lookup(UUID_A) is None
+        w = p1.encoder_consume(m)                         # all REFs to what the first frames declared
+        assert w.count(b'\xf1\x02') > 100
+        back, got, _, _ = l1.decoder_consume(w)
+        assert got == m and not back.startswith(b'\xf0')
+        l1.close()                                        # the deferred destroy happens here
+        l2 = PipePair(lenc, codec, UUID_B, connect=True)
+        back, got, _, _ = l2.decoder_consume(PipePair(penc, pdec, UUID_A).encoder_consume(payload(12, 10_000)))
+        assert l2.decoder_ctx() == ctx_lookup(UUID_A)
+        l2.close()
+        p1.close()
+    finally:
+        connect_registry_clear()
+        for c in (codec, lenc, penc, pdec):
+            c.close()

@@ -112,3 +112,32 @@ def test_warm_cache_refs(screen_mode, oracle):
     offs2 = np.concatenate([offs, offs])
     lens2 = np.concatenate([lens, lens])
     _check(oracle, data, offs2, lens2, 1024)
+
+
+def test_screen_after_large_chunks_on_one_context(screen_mode, oracle):
+    """A context whose scratch was grown by a batch of 64 KiB chunks still
+    screens its later 4 KiB packets (advisor round 5: the queues used to be
+    allocated only by a small-chunk call that grew the scratch), and both
+    batches equal the oracle's sequential encoder over the same calls."""
+    import ctypes as C
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context, lib
+    big = synth.stream(0xB6, 64 * 64 * KiB, 10, 0)
+    small = synth.stream(0xC4, 2048 * 4 * KiB, 4, 0)
+    data = big + small
+    bo, bl = synth.chunks_of(big, 64 * KiB)
+    so, sl = synth.chunks_of(small, 4 * KiB)
+    so = so + len(big)
+    offs = np.concatenate([bo, so])
+    lens = np.concatenate([bl, sl])
+    exp = oracle.encode_batch(data, offs, lens, mode=1)
+    ctx = Context(0, cache_segments=1 << 15)
+    got = ctx.encode_chunks(data, bo, bl, semantics=XCG_SEM_STREAM)
+    s, p = C.c_uint64(), C.c_uint64()
+    lib().xcg_debug_screen_counts(C.byref(s), C.byref(p))
+    got += ctx.encode_chunks(data, so, sl, semantics=XCG_SEM_STREAM)
+    lib().xcg_debug_screen_counts(C.byref(s), C.byref(p))
+    ctx.close()
+    bad = next((i for i in range(len(exp)) if got[i] != exp[i]), None)
+    assert bad is None, bad
+    assert s.value >= len(so) and p.value < s.value // 3, (s.value, p.value)

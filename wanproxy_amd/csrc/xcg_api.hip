@@ -17,6 +17,7 @@
 #include <iterator>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -242,6 +243,11 @@ struct RegEntry {
 };
 std::mutex g_reg_mu;
 std::map<std::string, RegEntry> g_reg;
+// A pipe that connected a registry context at <HELLO> holds it until the pipe
+// is destroyed (xcg_pipe.cpp); clearing the registry destroys a held context
+// only when its last holder lets go (g_deferred), never under a live pipe.
+std::map<xcg_ctx*, int> g_holds;
+std::set<xcg_ctx*> g_deferred;
 
 bool uuid_key(const char* u, std::string* key) {     // the 8-4-4-4-12 form UUID::decode takes
   if (!u) return false;
@@ -273,6 +279,7 @@ struct DeviceGuard {
 };
 
 constexpr uint32_t FILT_WORDS = (1u << 19) / 32;   // xcg_cache.h FILT_LOG2
+constexpr uint32_t PREFIX_FILTERS = 16;             // xcg_cache.h: slices of a round's LDS filter
 
 // The context's last call was enqueued on last_mark; done_ev is recorded
 // behind it only when another stream or a host wait needs it.  Recording it
@@ -450,9 +457,22 @@ int ensure_cache(xcg_ctx* c) {
   return rc;
 }
 
+// The quiet-chunk screen's key queues (small-chunk calls, maxd <= 4): 4 KiB
+// per chunk of the scratch's capacity (SCREEN_QCAP keys; ~ the input's size
+// for 4 KiB packets), allocated by the first such call on the context --
+// whatever size of chunks grew the scratch before it -- and kept with it.
+int ensure_screen_queues(BatchScratch& b, uint32_t maxd) {
+  if (maxd > 4 || (b.s_qcnt && b.s_qkeys)) return XCG_OK;
+  if (hipMalloc(&b.s_qcnt, 4ull * b.n_cap) != hipSuccess || hipMalloc(&b.s_qkeys, 4096ull * b.n_cap) != hipSuccess) {
+    (void)hipFree(b.s_qcnt); (void)hipFree(b.s_qkeys);
+    b.s_qcnt = nullptr; b.s_qkeys = nullptr;      // (the screen stays off; the parse decides alone)
+  }
+  return XCG_OK;
+}
+
 int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
   BatchScratch& b = c->bs;
-  if (b.decl && n <= b.n_cap && maxd <= b.maxd) return XCG_OK;
+  if (b.decl && n <= b.n_cap && maxd <= b.maxd) return ensure_screen_queues(b, maxd);
   free_scratch(b);
   b.n_cap = n;
   b.maxd = maxd;
@@ -461,7 +481,7 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
   b.r_mask = 2 * cap - 1;          // union of two rounds' hashes
   b.maxh = maxd + 8;
   if (hipMalloc(&b.b_keys, 8ull * cap) != hipSuccess || hipMalloc(&b.b_vals, 8ull * cap) != hipSuccess ||
-      hipMalloc(&b.r_filt, 4ull * FILT_WORDS) != hipSuccess ||
+      hipMalloc(&b.r_filt, 4ull * FILT_WORDS * PREFIX_FILTERS) != hipSuccess ||
       hipMalloc(&b.r_ftab, 16ull * (c->g.fmask + 1)) != hipSuccess ||
       hipMalloc(&b.decl, 16ull * n * maxd) != hipSuccess || hipMalloc(&b.ndecl, 4ull * n) != hipSuccess ||
       hipMalloc(&b.changed, 16) != hipSuccess || hipHostMalloc(&b.h_changed, 16) != hipSuccess ||
@@ -474,12 +494,11 @@ int ensure_scratch(xcg_ctx* c, uint32_t n, uint32_t maxd) {
       hipMalloc(&b.a_vals, 8ull * XCG_VERIFY_A_CAP) != hipSuccess ||
       hipMalloc(&b.a_bits, 4ull * XCG_VERIFY_A_WORDS) != hipSuccess ||
       hipMalloc(&b.s_fold, 4ull * 32768) != hipSuccess || hipMalloc(&b.s_work, 4ull * (n + 1)) != hipSuccess ||
-      hipMalloc(&b.s_info, 4ull * n) != hipSuccess || hipMalloc(&b.s_rows, 64ull * n) != hipSuccess ||
-      (maxd <= 4 && (hipMalloc(&b.s_qcnt, 4ull * n) != hipSuccess ||
-                     hipMalloc(&b.s_qkeys, 4096ull * n) != hipSuccess))) {
+      hipMalloc(&b.s_info, 4ull * n) != hipSuccess || hipMalloc(&b.s_rows, 64ull * n) != hipSuccess) {
     free_scratch(b);
     return XCG_ENOMEM;
   }
+  ensure_screen_queues(b, maxd);
   if (c->bounded || c->pair) {
     b.maxe = 2 * maxd + 64;        // declarations + REFs + collision lookups of one chunk
     if (hipMalloc(&b.ev, 16ull * n * b.maxe) != hipSuccess || hipMalloc(&b.nev, 4ull * n) != hipSuccess ||
@@ -770,11 +789,33 @@ void xcg_connect_registry_clear(void) {
   std::vector<xcg_ctx*> owned;
   {
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (auto& e : g_reg)
-      if (e.second.owned) owned.push_back(e.second.ctx);
+    for (auto& e : g_reg) {
+      if (!e.second.owned) continue;
+      if (g_holds.count(e.second.ctx)) g_deferred.insert(e.second.ctx);   // (a pipe still uses it)
+      else owned.push_back(e.second.ctx);
+    }
     g_reg.clear();
   }
   for (xcg_ctx* c : owned) xcg_ctx_destroy(c);
+}
+
+// (xcg_pipe.cpp, not part of the ABI) a connecting pipe takes and drops its context
+extern "C" void xcg_registry_hold(xcg_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  ++g_holds[c];
+}
+extern "C" void xcg_registry_release(xcg_ctx* c) {
+  bool destroy = false;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_holds.find(c);
+    if (it == g_holds.end()) return;
+    if (--it->second == 0) {
+      g_holds.erase(it);
+      destroy = g_deferred.erase(c) != 0;
+    }
+  }
+  if (destroy) xcg_ctx_destroy(c);
 }
 
 int xcg_pair_stats(xcg_ctx* c, uint64_t* st) {

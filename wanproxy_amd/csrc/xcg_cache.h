@@ -20,6 +20,12 @@ namespace xcg {
 constexpr uint64_t EMPTY_KEY = ~0ull;
 constexpr int FILT_LOG2 = 19;                       // 2^19 bits = 64 KiB of LDS
 constexpr uint32_t FILT_WORDS = (1u << FILT_LOG2) / 32;
+// A round's LDS lane filter comes in PREFIX_FILTERS slices: slice j holds the
+// cache and the batch declarations of chunks < (j + 1) * pfdiv, so a workgroup
+// whose chunks all lie below that copies slice j -- on average half the
+// batch's keys, and far fewer for the first chunks (xcg_encode.hip
+// filt_prefix_kernel).
+constexpr uint32_t PREFIX_FILTERS = 16;
 constexpr uint32_t FOVF16 = 2u;                     // bucket-overflow flag in slot 7 (even: never a fingerprint)
 
 // Bounded (LRU) cache: kinds of the cache references a stream chunk records
@@ -45,6 +51,7 @@ struct LaneFilter {   // what a lane probes: LDS bitmap (copied from filt) or th
   uint32_t fmask;     // fbuckets - 1
   const uint32_t* gfilt;
   uint32_t gmask;     // gfilt words - 1
+  uint32_t pfdiv = 0; // filt is PREFIX_FILTERS slices of pfdiv chunks each (0: one filter)
 };
 
 // Every filter kept over a set of hashes (the persistent cache's, or a round's

@@ -96,6 +96,7 @@ struct StreamLDS {
   WaveRecs<LOGNB, MAXD> rec[W];
   uint32_t ro[W][MAXD];                      // output length after each declaration's op (restart points)
   uint32_t rsv[W][8];                        // restart state (kept out of registers)
+  uint32_t cmax;                             // the workgroup's highest chunk (prefix filter slice)
 };
 
 // Re-parse restart (bounded / pair passes after the first; the driver backs up
@@ -1575,19 +1576,35 @@ __global__ __launch_bounds__(64 * SW) void encode_stream_kernel(EncParams prm) {
   __shared__ L S;
   // Which lane filter the cache + batch declarations fit: the 64 KiB LDS one
   // up to LDS_FILTER_KEYS keys (FP <~10 %), else the global one.
-  uint32_t keys = readfirst(*prm.nseg);
-  if (prm.use_b) keys += readfirst(wave_sum(prm.bcount[lane_id()]));
-  const int fmode = keys == 0 ? 0 : (keys <= prm.lds_filter_keys ? 1 : (keys <= prm.lds_prefilter_keys ? 3 : 2));
-  if (fmode == 1 || fmode == 3) {
-    for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x)
-      ((u32x4*)S.lfilt)[i] = ((const u32x4*)prm.lf.filt)[i];
-  }
-  __syncthreads();
   const int wv = (int)readfirst(threadIdx.x >> 6);
-  const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
-                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode, S.ro[wv], S.rsv[wv]};
   const uint32_t stride = gridDim.x * SW;
   const uint32_t items = prm.work ? readfirst(prm.work[0]) : prm.n;
+  // Prefix slices of the round's LDS filter (xcg_cache.h PREFIX_FILTERS): the
+  // slice that covers the workgroup's highest chunk holds every batch key its
+  // chunks can see.  (The cache's and the batch's key counts pick the mode.)
+  uint32_t slice = 0, bkeys = prm.use_b ? readfirst(wave_sum(prm.bcount[lane_id()])) : 0u;
+  if (prm.lf.pfdiv) {
+    uint32_t cmax = 0;
+    for (uint32_t i = blockIdx.x * SW + (uint32_t)wv; i < items; i += stride)
+      cmax = max(cmax, prm.work ? readfirst(prm.work[1 + i]) : i);
+    if (threadIdx.x == 0) S.cmax = 0u;
+    __syncthreads();
+    if (lane_id() == 0) atomicMax(&S.cmax, cmax);
+    __syncthreads();
+    slice = min(readfirst(S.cmax) / prm.lf.pfdiv, PREFIX_FILTERS - 1u);
+    // (batch keys below the slice's end, taken as spread evenly over the chunks)
+    const uint32_t cend = min(prm.n, (slice + 1u) * prm.lf.pfdiv);
+    bkeys = (uint32_t)((uint64_t)bkeys * cend / max(prm.n, 1u));
+  }
+  const uint32_t keys = readfirst(*prm.nseg) + bkeys;
+  const int fmode = keys == 0 ? 0 : (keys <= prm.lds_filter_keys ? 1 : (keys <= prm.lds_prefilter_keys ? 3 : 2));
+  if (fmode == 1 || fmode == 3) {
+    const u32x4* src = (const u32x4*)(prm.lf.filt + (uint64_t)slice * FILT_WORDS);
+    for (uint32_t i = threadIdx.x; i < FILT_WORDS / 4; i += blockDim.x) ((u32x4*)S.lfilt)[i] = src[i];
+  }
+  __syncthreads();
+  const GlbView gs{(char*)&S, (uint32_t)offsetof(L, lfilt),
+                   (uint32_t)(offsetof(L, scr) + (size_t)wv * sizeof(S.scr[0])), fmode, S.ro[wv], S.rsv[wv]};
   // The batch's first chunk sees no batch declaration: on an empty cache it
   // probes nothing.  (The filter holds every chunk's keys; in a seeded round
   // of REF-dense data the first chunk's windows match thousands of later
@@ -2086,12 +2103,29 @@ namespace xcg {
 // (chunk, declaration).
 constexpr uint32_t PREP_TABLE = 1, PREP_FILTERS = 2;   // (what a round's prep / build covers)
 
+// The round's LDS-filter slices (xcg_cache.h PREFIX_FILTERS): a batch key of
+// chunk c goes into slice c / pfdiv, then every slice is ORed into the ones
+// above it, so slice j = the cache + the keys of chunks < (j + 1) pfdiv.
+__device__ __forceinline__ FiltSet prefix_slice(FiltSet f, uint32_t c, uint32_t pfdiv) {
+  if (pfdiv) f.filt += (uint64_t)min(c / pfdiv, PREFIX_FILTERS - 1u) * FILT_WORDS;
+  return f;
+}
+__global__ __launch_bounds__(256) void filt_prefix_kernel(uint32_t* f) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t w = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < PREFIX_FILTERS; ++j) {
+    w |= f[(uint64_t)j * FILT_WORDS + i];
+    f[(uint64_t)j * FILT_WORDS + i] = w;
+  }
+}
+
 // what: PREP_TABLE (the table and the counters), PREP_FILTERS, or both.  A
 // verification builds the table alone: the filters of its declarations are
 // only needed if a re-parse follows (then a filters-only pass adds them).
 __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* decl, const uint32_t* ndecl, uint32_t n,
                                                                 uint32_t maxd, HashTab b, FiltSet fs, uint32_t* bcount,
-                                                                int32_t* status, uint32_t what) {
+                                                                int32_t* status, uint32_t what, uint32_t pfdiv) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = (uint32_t)(i / maxd), k = (uint32_t)(i % maxd);
   const bool have = c < n && k < ndecl[c];
@@ -2100,11 +2134,11 @@ __global__ __launch_bounds__(256) void build_batch_table_kernel(const uint4* dec
   if (!have) return;
   const uint4 d = decl[i];
   if (what == (PREP_TABLE | PREP_FILTERS)) {
-    if (!tab_insert_min_filt(b, fs, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
+    if (!tab_insert_min_filt(b, prefix_slice(fs, c, pfdiv), d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
   } else if (what == PREP_TABLE) {
     if (!tab_insert_min(b, d.x, d.y, ((uint64_t)c << 32) | d.z)) atomicOr(status, 2);
   } else {
-    filt_insert(fs, d.x, d.y);
+    filt_insert(prefix_slice(fs, c, pfdiv), d.x, d.y);
   }
 }
 
@@ -2201,7 +2235,7 @@ __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, con
                                                           const uint32_t* chunk_len, uint32_t n, uint32_t maxd,
                                                           uint4* decl, uint32_t* ndecl, uint32_t* nhits,
                                                           uint32_t* changed, HashTab b, FiltSet fs, uint32_t* bcount,
-                                                          int32_t* status) {
+                                                          int32_t* status, uint32_t pfdiv) {
   const uint32_t wpc = (maxd + SEED_TILES - 1) / SEED_TILES;       // waves per chunk
   const uint32_t w = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
   const uint32_t c = w / wpc, k0 = (w % wpc) * SEED_TILES;
@@ -2270,7 +2304,8 @@ __global__ __launch_bounds__(256) void seed_tiling_kernel(const uint8_t* in, con
   if ((uint32_t)l < tiles) {
     const uint32_t k = k0 + (uint32_t)l;
     decl[(uint64_t)c * maxd + k] = make_uint4(mlo, mhi, k * SEG, 0u);
-    if (b.keys && !tab_insert_min_filt(b, fs, mlo, mhi, ((uint64_t)c << 32) | (k * SEG))) atomicOr(status, 2);
+    if (b.keys && !tab_insert_min_filt(b, prefix_slice(fs, c, pfdiv), mlo, mhi, ((uint64_t)c << 32) | (k * SEG)))
+      atomicOr(status, 2);
   }
   if (b.keys && l == 0 && k0 == 0) atomicAdd(bcount + (c & 63u), m);   // (the chunk's count, once)
 }
@@ -2303,7 +2338,10 @@ __global__ __launch_bounds__(256) void round_prep_kernel(RoundPrep a) {
   const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool g_empty = *a.nseg == 0u;
   if (a.what & PREP_FILTERS) {
-    for (uint64_t i = i0; i < FILT_WORDS; i += stride) a.r_filt[i] = g_empty ? 0u : a.g_filt[i];
+    // slice 0 starts as the cache's filter, the others empty (filt_prefix_kernel
+    // ORs each slice into the ones above it once the batch keys are in)
+    for (uint64_t i = i0; i < (uint64_t)FILT_WORDS * PREFIX_FILTERS; i += stride)
+      a.r_filt[i] = (g_empty || i >= FILT_WORDS) ? 0u : a.g_filt[i];
     for (uint64_t i = i0; i < a.ftab_n; i += stride) a.r_ftab[i] = g_empty ? u32x4{0u, 0u, 0u, 0u} : a.g_ftab[i];
     for (uint64_t i = i0; i < a.gfilt_n; i += stride) a.r_gfilt[i] = g_empty ? 0u : a.g_gfilt[i];
   }
@@ -2735,7 +2773,7 @@ extern "C" int xcg_launch_seed_tiling(const XcgStreamArgs* a, hipStream_t stream
   const uint32_t seed_waves = a->n * ((a->maxd + xcg::SEED_TILES - 1) / xcg::SEED_TILES);
   hipLaunchKernelGGL(xcg::seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
                      a->chunk_len, a->n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed,
-                     xcg::HashTab{nullptr, nullptr, 0u}, xcg::FiltSet{}, nullptr, nullptr);
+                     xcg::HashTab{nullptr, nullptr, 0u}, xcg::FiltSet{}, nullptr, nullptr, 0u);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -2967,6 +3005,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   // later rounds resume flagged chunks too (bounded / pair: the verification
   // gives the affected lookups' times)
   const bool rs_rounds = a->ev && a->restart && a->bslot && prm.eo && a->bad_t;
+  static const bool pf_off = getenv("XCG_NO_PREFIX_FILTERS") != nullptr;   // (A/B runs: one slice)
+  const uint32_t pfdiv = pf_off ? 0u : (n + PREFIX_FILTERS - 1) / PREFIX_FILTERS;   // chunks per slice of the round's LDS filter
   auto prep = [&](int t, bool verify, uint32_t what) -> bool {
     RoundPrep rp{tabs[t], a->r_filt, a->g_filt, (u32x4*)a->r_ftab, (const u32x4*)a->g_ftab, (uint32_t)(tbytes / 16),
                  a->r_gfilt, a->g_gfilt, (uint32_t)(gbytes / 4), a->nseg, a->bcount, a->changed,
@@ -2993,7 +3033,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     hipLaunchKernelGGL(seed_tiling_kernel, dim3((seed_waves + 3) / 4), dim3(256), 0, stream, a->in, a->chunk_off,
                        a->chunk_len, n, a->maxd, (uint4*)a->decl, a->ndecl, a->nhits, a->changed,
                        fuse ? tabs[cur] : HashTab{nullptr, nullptr, 0u},
-                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status);
+                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status, pfdiv);
+    if (fuse) hipLaunchKernelGGL(filt_prefix_kernel, dim3(FILT_WORDS / 256), dim3(256), 0, stream, a->r_filt);
     seed_built = fuse;
   } else {
     launch();
@@ -3030,7 +3071,10 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     const uint64_t nthreads = (uint64_t)n * a->maxd;
     hipLaunchKernelGGL(build_batch_table_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream,
                        (const uint4*)a->decl, (const uint32_t*)a->ndecl, n, a->maxd, tabs[t],
-                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status, what);
+                       FiltSet{a->r_filt, a->r_ftab, a->fmask, a->r_gfilt, a->gmask}, a->bcount, a->status, what,
+                       pfdiv);
+    if (what & PREP_FILTERS)
+      hipLaunchKernelGGL(filt_prefix_kernel, dim3(FILT_WORDS / 256), dim3(256), 0, stream, a->r_filt);
     return hipGetLastError() == hipSuccess;
   };
   // A re-parse round whose flagged chunks (their first contradicted lookup in
@@ -3063,7 +3107,7 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
     prm.use_b = true;
     prm.b = tabs[cur];
     prm.skip_below = seeded ? 0 : fc + 1;            // (seeded: round 1 parses every chunk)
-    prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask};
+    prm.lf = LaneFilter{a->r_filt, (const u32x4*)a->r_ftab, a->fmask, a->r_gfilt, a->gmask, pfdiv};
     if (keep && a->need_given) prm.need = a->need;   // the rest stand under the kept lists
     const bool rs = keep && a->need_given && a->restart && a->bslot && prm.eo;
     if (rs) run_restarted();

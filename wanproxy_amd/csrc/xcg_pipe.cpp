@@ -124,6 +124,10 @@ uint64_t decoded_bound(const uint8_t* enc, uint64_t n) {
 
 }  // namespace
 
+// (xcg_api.hip) registry contexts a connecting pipe holds while it lives
+extern "C" void xcg_registry_hold(xcg_ctx* c);
+extern "C" void xcg_registry_release(xcg_ctx* c);
+
 struct xcg_pipe {
   xcg_ctx* enc;
   xcg_ctx* dec;                    // (connecting pipes: set at <HELLO>)
@@ -186,6 +190,7 @@ int xcg_pipe::decode_ops() {
         rc = xcg_ctx_connect(parent, u, &c);
         if (rc == XCG_OK) rc = xcg_window_create(c, &win);
         if (rc != XCG_OK) break;
+        xcg_registry_hold(c);                                        // (until xcg_pipe_destroy)
         dec = c;
       }
       decoder = true;
@@ -357,6 +362,7 @@ xcg_ctx* xcg_pipe_decoder_ctx(const xcg_pipe* p) { return p ? p->dec : nullptr; 
 void xcg_pipe_destroy(xcg_pipe* p) {
   if (!p) return;
   if (p->win) xcg_window_destroy(p->win);
+  if (p->parent && p->dec) xcg_registry_release(p->dec);   // (a cleared registry's context goes now)
   delete p;
 }
 
