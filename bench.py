@@ -219,6 +219,17 @@ def pmc_stream_traffic():
     return None, None
 
 
+def pmc_decode_traffic():
+    """HBM bytes of one C2-S2 batch decode (every decode kernel of one call)
+    from the committed scripts/profile_decode.sh summary."""
+    p = os.path.join(ROOT, 'profiles', 'r06_decode_summary.json')
+    if os.path.exists(p):
+        g = json.load(open(p)).get('decode_step', {})
+        if 'hbm_bytes_per_call' in g:
+            return int(g['hbm_bytes_per_call']), 'profiles/r06_decode_summary.json decode_step (rocprofv3 --pmc)'
+    return None, None
+
+
 def timed(fn, steps, stream, kernel_time=False):
     """(wall s / step, HIP-event s / step on `stream`, stream-parse kernel ms /
     step, its launches / step) over `steps` calls after 2 untimed ones."""
@@ -327,12 +338,29 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
                                       C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
                                       C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
                                       tot.ctypes.data, C.c_void_p(stream.cuda_stream)))
-    wall, _, _, _ = timed(dec, 5, stream)
+    steps = 5
+    lib().xcg_debug_decode_kernel_timing(1)
+    wall, _, _, _ = timed(dec, steps, stream)
+    lib().xcg_debug_decode_kernel_timing(0)
+    step_ms, emit_ms, segs = C.c_double(), C.c_double(), C.c_uint32()
+    lib().xcg_debug_decode_kernel_time(C.byref(step_ms), C.byref(emit_ms), C.byref(segs))
+    calls = max(1, segs.value // 3)                   # (three device segments per decode call)
     if int(tot[0]) != in_bytes or d_dout[:in_bytes].cpu().numpy().tobytes() != data.tobytes():
         raise SystemExit('PARITY FAILURE (decode round trip)')
+    # Roofline (decode): algorithmic bytes = encoded bytes read + decoded bytes written.
+    dms, ems = step_ms.value / calls, emit_ms.value / calls
+    alg = out_bytes + in_bytes
+    traffic, tsrc = pmc_decode_traffic()
     res['decode'] = {'metric': 'XCodec decode GiB/s of decoded bytes (that stream, fresh decoder cache)',
                      'value': round(in_bytes / 2**30 / wall, 3), 'ms_per_step': round(wall * 1e3, 3),
-                     'includes': 'cache clear + scan + size + emit + commit, one host sync'}
+                     'includes': 'cache clear + scan + size + emit + commit, two host readbacks (sizes)',
+                     'roofline': {'bound': 'hbm', 'achieved': round(alg / (dms * 1e-3) / 1e9, 2), 'peak': PEAK_HBM_GBS,
+                                  'unit': 'GB/s', 'frac': round(alg / (dms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5),
+                                  'kernel': 'decode step: scan + refcheck/sizing + emit + commit kernels '
+                                            '(HIP events per device segment, host readbacks excluded)',
+                                  'kernel_ms_per_step': round(dms, 4), 'emit_kernel_ms': round(ems, 4),
+                                  'emit_frac': round(alg / (ems * 1e-3) / 1e9 / PEAK_HBM_GBS, 5) if ems else None,
+                                  'algorithmic_bytes_per_step': alg, 'traffic': traffic, 'traffic_source': tsrc}}
     sctx.close()
     dctx.close()
     del d_enc, d_dout

@@ -189,6 +189,16 @@ int xcg_ctx_create_pair_xuid(int device, uint32_t flags, uint64_t memory_cache_l
                              const char *uuid36, int xuid, xcg_ctx **out);
 int xcg_disk_head(const xcg_disk *disk, uint64_t *index_block, uint64_t *next_entry);
 int xcg_pair_xuid(const xcg_ctx *ctx);
+/* XCodecCachePair over an UNBOUNDED XCodecMemoryCache (a memory cache without
+ * a size: XCodecMemoryCache(uuid, 0) never evicts, xcodec/xcodec_cache.h:
+ * 303-318) and `disk`: the pair's policy as above -- a primary miss goes to the
+ * disk, a disk hit is promoted, a primary hit touches the disk (:208-237) --
+ * over a primary that holds up to capacity_segments (0: XCG_DEFAULT_CACHE_
+ * SEGMENTS); a batch that would need more fails with XCG_EOVERFLOW instead of
+ * evicting.  uuid36 / xuid as for xcg_ctx_create_pair_xuid.  A connect
+ * (xcg_ctx_connect) on such a context makes another one. */
+int xcg_ctx_create_pair_unbounded(int device, uint32_t flags, uint64_t capacity_segments, xcg_disk *disk,
+                                  const char *uuid36, int xuid, xcg_ctx **out);
 void xcg_disk_destroy(xcg_disk *disk);
 int xcg_disk_stats(const xcg_disk *disk, uint64_t *st);
 int xcg_ctx_create_pair_on(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, xcg_disk *disk,
@@ -497,7 +507,7 @@ int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,
  * else through a global (L2-resident) one; both give the same output.
- * Returns the previous threshold (default 220000, or XCG_LDS_FILTER_KEYS). */
+ * Returns the previous threshold (default 150000, or XCG_LDS_FILTER_KEYS). */
 uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
 /* Diagnostics / tests: past that threshold, and while the cache + batch hold at
  * most this many keys, the LDS filter still goes first and only the positions
@@ -505,6 +515,14 @@ uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
  * filter alone.  Same output either way.  Returns the previous threshold
  * (default 700000, or XCG_LDS_PREFILTER_KEYS). */
 uint32_t xcg_debug_set_lds_prefilter_keys(uint32_t keys);
+/* Diagnostics (bench.py's decode roofline): while on, every xcg_decode_batch on
+ * an unbounded cache brackets its device work with HIP events on its stream --
+ * the scan, the reference check / sizing, and the emit + commit segments (the
+ * host's two readbacks between them excluded) -- and the emit kernel alone.
+ * xcg_debug_decode_kernel_time returns the sums in ms since the last call and
+ * the number of segments, and resets them.  Returns the previous setting. */
+int xcg_debug_decode_kernel_timing(int on);
+int xcg_debug_decode_kernel_time(double *step_ms, double *emit_ms, uint32_t *segments);
 /* Diagnostics / tests: stream batches start either with a parse round against
  * the cache alone, or -- automatically when the context's previous batch
  * declared segments -- from each chunk's 2048-byte tiling (its cold parse),

@@ -212,20 +212,12 @@ Geometry geometry_of(XCodecCache *cache)
 		g.why = "an XCodecCachePair whose secondary is not a disk cache";
 		return g;
 	}
-	if (limit == 0) {
-		/* An unbounded primary never evicts, so the pair behaves as an
-		 * unbounded memory cache as long as the disk holds nothing the
-		 * primary lacks.  It can: XCodecCachePair::lookup sends a primary miss
-		 * to the secondary (xcodec_cache.h:217-229), and the disk may hold
-		 * what an earlier pair on the same disk front entered (a peer uuid's
-		 * earlier connection: XCodecDisk::connect returns its existing front)
-		 * or what a reloaded volume held.  The engine mirrors this pair as an
-		 * unbounded memory cache and does not see those entries: it emits an
-		 * EXTRACT where the reference emits a REF (known
-		 * departures). */
-		g.kind = KIND_MEMORY;
-		return g;
-	}
+	/* An unbounded primary (limit 0) never evicts; the pair is still a pair:
+	 * a primary miss goes to the disk, which may hold what an earlier pair on
+	 * the same front entered (XCodecDisk::connect returns its existing front)
+	 * or what a reloaded volume held, and a disk hit is promoted
+	 * (xcodec_cache.h:208-230).  The engine runs it as a pair whose primary
+	 * never evicts (xcg_ctx_create_pair_unbounded, limit_bytes 0 here). */
 	g.kind = KIND_PAIR;
 	g.limit_bytes = (uint64_t)limit * XCG_SEGMENT_LENGTH;
 	return g;
@@ -263,7 +255,11 @@ xcg_ctx *ctx_for(XCodecCache *cache, bool out_of_band)
 		xcg_disk *disk = NULL;
 		rc = engine_disk(level, g.disk, &disk, &why);
 		if (rc == XCG_OK)
-			rc = xcg_ctx_create_pair_xuid(device, flags, g.limit_bytes, disk,
+			rc = g.limit_bytes == 0 ?
+			     xcg_ctx_create_pair_unbounded(device, flags, 0, disk,
+			                                   g.disk.uuid.length() == 36 ? g.disk.uuid.c_str() : NULL, g.disk.xuid,
+			                                   &ctx) :
+			     xcg_ctx_create_pair_xuid(device, flags, g.limit_bytes, disk,
 			                              g.disk.uuid.length() == 36 ? g.disk.uuid.c_str() : NULL, g.disk.xuid,
 			                              &ctx);
 		break;

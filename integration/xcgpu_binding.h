@@ -45,7 +45,7 @@ enum CacheKind {
 	KIND_NULL,		/* tack's TackNullCache: lookups miss (programs/tack/tack.cc:70-101) */
 	KIND_MEMORY,		/* XCodecMemoryCache, no limit (xcodec/xcodec_cache.h:245-365) */
 	KIND_BOUNDED,		/* XCodecMemoryCache with a limit: LRU eviction */
-	KIND_PAIR		/* XCodecCachePair(bounded memory, disk front-end) (:140-237) */
+	KIND_PAIR		/* XCodecCachePair(memory -- bounded, or unbounded: limit_bytes 0 --, disk front-end) (:140-237) */
 };
 
 /* The disk level of a pair: the XCodecDisk under it and which front it is. */

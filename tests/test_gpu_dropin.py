@@ -113,9 +113,15 @@ def _uuid(k):
     return '%08x-0000-4000-8000-%012x' % (os.getpid() & 0xFFFFFFFF, k)
 
 
+@pytest.mark.parametrize('limit_segs', [40, 0], ids=['bounded', 'unbounded'])
 @pytest.mark.parametrize('nb', [3, 10])
-def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path, nb):
-    """wanproxy restarted on its cache volume (XCodecDisk::open,
+def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path, nb, limit_segs):
+    """(limit_segs 0: the pair's primary is an unbounded XCodecMemoryCache,
+    which never evicts -- the engine still runs it as a pair, so a primary
+    miss finds the reopened volume's entries and the peer's front, loaded from
+    the volume, serves the new pair over it: REFs where a plain memory cache
+    would EXTRACT, xcodec/xcodec_cache.h:208-230.)
+    wanproxy restarted on its cache volume (XCodecDisk::open,
     xcodec_cache_disk.cc:826-871): the first process encodes through the
     drop-in on a pair over the volume (the local front and a peer's), the
     volume is written and the caches go away; a second process opens the same
@@ -126,8 +132,8 @@ def test_dropin_pair_reopened_volume_like_reference(dropin, ref_oracle, tmp_path
     the reference's.  A fresh engine disk would not do: the second process REFs
     segments only the first declared."""
     from wanproxy_amd import synth
-    limit, disk = 40 * 2048, (18 + nb * 205) * 2048
-    local, peer = _uuid(0x300 + nb), _uuid(0x400 + nb)
+    limit, disk = limit_segs * 2048, (18 + nb * 205) * 2048
+    local, peer = _uuid(0x300 + nb + 0x20 * (limit_segs == 0)), _uuid(0x400 + nb + 0x20 * (limit_segs == 0))
     d = synth.stream(0x5E1 + nb, 9 << 20, 25, 0)
     e = synth.stream(0x6E1 + nb, 6 << 20, 25, 0)
     calls = lambda x, a, b: [x[k:k + 65536] for k in range(a << 20, b << 20, 65536)]

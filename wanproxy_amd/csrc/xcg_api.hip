@@ -727,6 +727,16 @@ int xcg_ctx_create_pair_xuid(int device, uint32_t flags, uint64_t memory_cache_l
   return XCG_OK;
 }
 
+int xcg_ctx_create_pair_unbounded(int device, uint32_t flags, uint64_t capacity_segments, xcg_disk* disk,
+                                  const char* uuid36, int xuid, xcg_ctx** out) {
+  if (capacity_segments == 0) capacity_segments = XCG_DEFAULT_CACHE_SEGMENTS;
+  if (capacity_segments > (1ull << 28)) return XCG_EINVAL;
+  const int rc = xcg_ctx_create_pair_xuid(device, flags, capacity_segments * XCG_SEGMENT_LENGTH, disk, uuid36, xuid,
+                                          out);
+  if (rc == XCG_OK) xcg_pair_state_set_unbounded((*out)->pair);
+  return rc;
+}
+
 int xcg_ctx_create_pair(int device, uint32_t flags, uint64_t memory_cache_limit_bytes, uint64_t disk_bytes,
                         xcg_ctx** out) {
   if (!out) return XCG_EINVAL;
@@ -754,7 +764,10 @@ int xcg_ctx_connect(xcg_ctx* parent, const char* uuid36, xcg_ctx** out) {
   }
   xcg_ctx* c = nullptr;
   int rc;
-  if (parent->pair)
+  if (parent->pair && xcg_pair_state_unbounded(parent->pair))
+    rc = xcg_ctx_create_pair_unbounded(parent->device, parent->flags, parent->pair_C,
+                                       (xcg_disk*)xcg_pair_state_disk(parent->pair), key.c_str(), -1, &c);
+  else if (parent->pair)
     rc = xcg_ctx_create_pair_uuid(parent->device, parent->flags, (uint64_t)parent->pair_C * XCG_SEGMENT_LENGTH,
                                   (xcg_disk*)xcg_pair_state_disk(parent->pair), key.c_str(), &c);
   else if (parent->bounded)

@@ -201,6 +201,8 @@ extern "C" int xcg_disk_state_open(const char* path, uint64_t disk_bytes, uint32
 extern "C" int xcg_disk_state_open_fd(int fd, uint64_t disk_bytes, uint32_t flags, XcgDiskState** out);
 extern "C" void xcg_disk_state_head(const XcgDiskState* K, uint64_t* index_block, uint64_t* next);
 extern "C" uint32_t xcg_pair_state_xuid(const XcgPairState* P);
+extern "C" void xcg_pair_state_set_unbounded(XcgPairState* P);
+extern "C" int xcg_pair_state_unbounded(const XcgPairState* P);
 extern "C" void xcg_pair_state_destroy(XcgPairState* P);
 extern "C" int xcg_pair_state_clear(XcgPairState* P);
 extern "C" void xcg_pair_state_stats(const XcgPairState* P, uint64_t* st);

@@ -32,6 +32,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "xcg_cache.h"
 #include "xcg_args.h"
 
@@ -67,6 +71,10 @@ struct DecParams {
   uint4* D;                    // declare records (lo, hi, src lo, src hi), batch indices [D_lo, ...)
   uint64_t D_lo;               // (tail mode: D_lo = max(t_end - 256, 0), read from *t_end)
   bool D_tail;
+  // (emit, no stop point) the window's tail records written by the emit pass
+  // itself: declares [tail_lo, tail_hi) into tail_D (null: decl_record_kernel)
+  uint4* tail_D;
+  uint64_t tail_lo, tail_hi;
   uint64_t* win_hash;          // the decoder's window: 256 hashes (0 = empty slot)
   uint8_t* win_seg;            //   and the bytes of each slot
   uint64_t win_count;          // declares made before this batch
@@ -398,6 +406,13 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
       const uint8_t* seg = x + i + 2;
       if (EMIT) {
         wave_copy2048(out + olen, seg);
+        const uint64_t t = dbase + ndecl;
+        if (prm.tail_D && t >= prm.tail_lo && t < prm.tail_hi) {   // (the window's tail: its hash here)
+          const uint2 h = dec_window_hash(seg);
+          const uint64_t src = (uint64_t)seg;
+          if (l == 0) prm.tail_D[t - prm.tail_lo] = make_uint4(readfirst(h.x), readfirst(h.y), (uint32_t)src,
+                                                               (uint32_t)(src >> 32));
+        }
       } else {
         const uint2 h = dec_window_hash(seg);
         bool existed = false;
@@ -427,6 +442,10 @@ __global__ __launch_bounds__(256) void decode_kernel(DecParams prm) {
           stop = true;
         }
         copy_segments(out + olen, src, r);
+        const uint64_t tl = dbase + ndecl + (uint64_t)l;
+        if (prm.tail_D && (uint32_t)l < r && tl >= prm.tail_lo && tl < prm.tail_hi)
+          prm.tail_D[tl - prm.tail_lo] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(uint64_t)src,
+                                                    (uint32_t)((uint64_t)src >> 32));
       }
       olen += (uint64_t)SEG * r;
       i += 10u * r;
@@ -668,7 +687,7 @@ __global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint64_t* le
 // atomic per block), then the block's waves copy the segments.
 __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8_t* pool, uint32_t* nseg,
                                                             uint32_t seg_cap, FiltSet fs) {
-  __shared__ uint32_t s_cnt, s_base, s_njob;
+  __shared__ uint32_t s_cnt, s_base, s_njob, s_rest;
   __shared__ uint4 s_job[256];   // (slot, destination segment, kind, -)
   const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint64_t blockp = min(*prm.block_pos, *prm.berr_pos);
@@ -690,7 +709,7 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
     }
   }
   const uint32_t seg = block_alloc_segs(kind == 1, nseg, &s_cnt, &s_base);
-  if (threadIdx.x == 0) s_njob = 0;
+  if (threadIdx.x == 0) { s_njob = 0; s_rest = 0; }
   __syncthreads();
   if (kind == 1 && seg >= seg_cap) {
     atomicOr(prm.status, 4);
@@ -707,10 +726,55 @@ __global__ __launch_bounds__(256) void decode_commit_kernel(DecParams prm, uint8
   }
   __syncthreads();
   const uint32_t njob = s_njob;
-  for (uint32_t j = readfirst(threadIdx.x >> 6); j < njob; j += 4) {
+  const uint32_t wv = readfirst(threadIdx.x >> 6);
+  const int l = lane_id();
+  // Plain enters (one EXTRACT of the hash, not cached): four of the wave's
+  // segments loaded together, then stored (one round trip per four copies
+  // instead of one per copy); everything else one job at a time below.
+  bool rest = false;
+  for (uint32_t j0 = 4u * wv; j0 < njob; j0 += 16u) {
+    u32x4 v[4][2];
+    uint8_t* dst[4];
+    bool plain[4];
+    uint64_t first[4], last[4], coff[4];
+    uint4 jb[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {                  // (the four jobs' table reads in flight together)
+      const uint32_t j = min(j0 + (uint32_t)t, njob - 1u);
+      jb[t] = s_job[j];
+      const uint32_t slot = readfirst(jb[t].x);
+      first[t] = prm.x.vals[slot];
+      last[t] = prm.x_latest[slot];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) coff[t] = prm.chunk_off[readfirst64(last[t]) >> 32];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint64_t f = readfirst64(first[t]), la = readfirst64(last[t]);
+      plain[t] = j0 + (uint32_t)t < njob && readfirst(jb[t].z) == 1u && la == f;
+      if (j0 + (uint32_t)t < njob && !plain[t]) rest = true;
+      dst[t] = pool + (uint64_t)readfirst(jb[t].y) * SEG;
+      const uint8_t* src = prm.in + readfirst64(coff[t]) + (uint32_t)la;
+      if (plain[t]) {
+        v[t][0] = *(const u32x4_u*)(src + 32 * l);
+        v[t][1] = *(const u32x4_u*)(src + 32 * l + 16);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (plain[t]) {
+        *(u32x4_u*)(dst[t] + 32 * l) = v[t][0];
+        *(u32x4_u*)(dst[t] + 32 * l + 16) = v[t][1];
+      }
+  }
+  if (rest && l == 0) s_rest = 1u;
+  __syncthreads();
+  if (s_rest == 0u) return;
+  for (uint32_t j = wv; j < njob; j += 4) {
     const uint4 jb = s_job[j];
     const uint32_t slot = readfirst(jb.x), dseg = readfirst(jb.y), jkind = readfirst(jb.z);
     const uint64_t first = readfirst64(prm.x.vals[slot]), last = readfirst64(prm.x_latest[slot]);
+    if (jkind == 1u && last == first) continue;   // (copied above)
     const uint8_t* src = prm.in + prm.chunk_off[last >> 32] + (uint32_t)last;
     if (last != first) {
       // name reuse inside the batch with different bytes would need per-REF
@@ -1484,6 +1548,61 @@ struct XcgDecodeArgs {
 
 // Returns 0, -75 (output too small) or -5.  Outputs: total decoded bytes, the
 // REF block and BACKREF error positions (~0 = none), unknown-REF count.
+// Diagnostics (bench.py's decode roofline): HIP events bracket the batch
+// decode's three device segments on its stream -- scan, refcheck / sizing,
+// emit + commit (the host's two readbacks between them are not device time)
+// -- and the emit kernel alone; xcg_debug_decode_kernel_time sums them.
+namespace {
+std::mutex g_dt_mu;
+bool g_dt_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_dt_step, g_dt_emit;
+struct DecTimer {
+  hipStream_t s;
+  hipEvent_t e0 = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>>* dst;
+  DecTimer(hipStream_t st, std::vector<std::pair<hipEvent_t, hipEvent_t>>* d) : s(st), dst(d) {
+    std::lock_guard<std::mutex> g(g_dt_mu);
+    if (g_dt_on && hipEventCreate(&e0) == hipSuccess) (void)hipEventRecord(e0, s);
+  }
+  ~DecTimer() {
+    if (e0) (void)hipEventDestroy(e0);   // (a path that did not reach its end: not counted)
+  }
+  void end() {
+    if (!e0) return;
+    std::lock_guard<std::mutex> g(g_dt_mu);
+    hipEvent_t e1 = nullptr;
+    if (hipEventCreate(&e1) == hipSuccess && hipEventRecord(e1, s) == hipSuccess) dst->emplace_back(e0, e1);
+    e0 = nullptr;
+  }
+};
+double dt_sum(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+  double tot = 0;
+  for (auto& e : v) {
+    float t = 0;
+    if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&t, e.first, e.second) == hipSuccess)
+      tot += t;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  v.clear();
+  return tot;
+}
+}  // namespace
+extern "C" int xcg_debug_decode_kernel_timing(int on) {
+  std::lock_guard<std::mutex> g(g_dt_mu);
+  const int old = g_dt_on;
+  g_dt_on = on != 0;
+  return old;
+}
+extern "C" int xcg_debug_decode_kernel_time(double* step_ms, double* emit_ms, uint32_t* segments) {
+  std::lock_guard<std::mutex> g(g_dt_mu);
+  if (segments) *segments = (uint32_t)g_dt_step.size();
+  const double s = dt_sum(g_dt_step), e = dt_sum(g_dt_emit);
+  if (step_ms) *step_ms = s;
+  if (emit_ms) *emit_ms = e;
+  return 0;
+}
+
 extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, uint64_t* block_pos_out,
                                  uint64_t* berr_pos_out, uint32_t* nunknown_out, hipStream_t stream) {
   using namespace xcg;
@@ -1520,6 +1639,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
   p.win_seg = a->win_seg;
   p.win_count = a->win_count;
   const dim3 grid((n + 3) / 4), block(256);
+  DecTimer seg1(stream, &g_dt_step);
   if (hipMemsetAsync(a->x_keys, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->x_vals, 0xFF, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
       hipMemsetAsync(a->x_latest, 0, 8ull * (a->x_mask + 1), stream) != hipSuccess ||
@@ -1533,6 +1653,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
                      (uint64_t*)p.decl_base, n, a->scratch + 3);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)p.n_bref,
                      p.n_decl_emit, n, a->scratch + 4);          // (n_decl_emit: scratch output here)
+  seg1.end();
   if (hipMemcpyAsync(a->h_scratch + 3, a->scratch + 3, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return -5;
@@ -1651,12 +1772,14 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     p.D_tail = false;
     hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
   }
+  DecTimer seg2(stream, &g_dt_step);
   hipLaunchKernelGGL(decode_refcheck_kernel, grid, block, 0, stream, p);
   if (nbref > 0) hipLaunchKernelGGL(decode_brefcheck_kernel, grid, block, 0, stream, p);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)a->out_len, a->out_off,
                      n, a->scratch);
   hipLaunchKernelGGL(dec_precheck_kernel, dim3((unsigned)(((uint64_t)a->x_mask + 256) / 256)), dim3(256), 0, stream,
                      p);
+  seg2.end();
   a->h_scratch[10] = 0;
   if (hipMemcpyAsync(a->h_scratch, a->scratch, 24, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipMemcpyAsync(a->h_scratch + 6, a->nunknown, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
@@ -1685,13 +1808,24 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     if (pair_mem) (void)hipFreeAsync(pair_mem, stream);
     return -75;
   }
+  DecTimer seg3(stream, &g_dt_step), emit(stream, &g_dt_emit);
+  // No stop point: the declares end at ndecl, so the window's tail is known
+  // now and the emit pass records it (no second walk over the ops).
+  const bool fuse_tail = !a->no_window && !dfull && *block_pos_out == ~0ull && *berr_pos_out == ~0ull;
+  if (fuse_tail) {
+    p.tail_D = a->d_tail;
+    p.tail_hi = ndecl;
+    p.tail_lo = ndecl > 256u ? ndecl - 256u : 0u;
+  }
   hipLaunchKernelGGL(decode_kernel<true>, grid, block, 0, stream, p);
+  emit.end();
+  p.tail_D = nullptr;
   hipLaunchKernelGGL(decode_tend_kernel, dim3(1), dim3(1), 0, stream, p, ndecl);
   if (!a->no_window) {
     if (!dfull) {
       p.D = a->d_tail;
       p.D_tail = true;
-      hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
+      if (!fuse_tail) hipLaunchKernelGGL(decl_record_kernel, grid, block, 0, stream, p, ndecl);
     }
     hipLaunchKernelGGL(window_update_kernel, dim3(64), dim3(256), 0, stream, p);
   }
@@ -1714,6 +1848,7 @@ extern "C" int xcg_launch_decode(const XcgDecodeArgs* a, uint64_t* total_out, ui
     const uint64_t slots = (uint64_t)a->x_mask + 1;
     hipLaunchKernelGGL(decode_commit_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, stream, p,
                        a->pool, a->nseg, a->seg_cap, FiltSet{a->g_filt, a->g_ftab, a->fmask, a->g_gfilt, a->gmask});
+    seg3.end();
   }
   if (dfull) (void)hipFreeAsync(dfull, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -369,7 +369,9 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t ev, uint64_t m) {
 // only the lanes it passes load their global word (exec-masked: the other
 // lanes send no request).
 constexpr int GSLOTS = 8;
-constexpr uint32_t LDS_FILTER_KEYS_DEFAULT = 220000;
+// (with the prefix slices; measured on C2-S2 / C5, profiles/r06_filter_modes.txt:
+// the two-level mode beats the LDS filter alone beyond ~150 k keys)
+constexpr uint32_t LDS_FILTER_KEYS_DEFAULT = 150000;
 constexpr uint32_t LDS_PREFILTER_KEYS_DEFAULT = 700000;
 struct GlbQ {
   char* lds;        // LDS base of the workgroup's struct (offset 0)

@@ -1139,6 +1139,10 @@ struct XcgDiskState {
 
 struct XcgPairState {
   uint32_t C = 0;                  // primary limit in segments
+  // XCodecCachePair over an unbounded XCodecMemoryCache (limit 0: enter never
+  // evicts, xcodec_cache.h:303-318): C is then only the primary's capacity,
+  // and a commit that would evict fails (XCG_EOVERFLOW) instead
+  bool unbounded = false;
   uint32_t D = 0, nb = 0;
   XcgDiskState* disk = nullptr;
   uint16_t xuid = 0;
@@ -1279,7 +1283,9 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
   // rocprim temporary storage for the largest sort / scan of this size
   size_t a = 0, b = 0, c = 0;
   (void)rocprim::radix_sort_pairs(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
-  (void)rocprim::exclusive_scan(nullptr, b, P->isr, P->rc, 0u, (size_t)std::max(np, n) + 1,
+  // (the commit also scans the primary's C + 1 free-slot flags, pair_commit)
+  (void)rocprim::exclusive_scan(nullptr, b, P->isr, P->rc, 0u,
+                                (size_t)std::max<uint64_t>(std::max<uint64_t>(np, n), P->C) + 1,
                                 rocprim::plus<uint32_t>());
   (void)rocprim::radix_sort_pairs(nullptr, c, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)np, 0, 64);
   size_t e1 = 0, e2 = 0, e3 = 0;
@@ -1574,6 +1580,7 @@ int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   }
   const uint32_t M = P->last_M;
   const int64_t E64 = (int64_t)d.P + (int64_t)M - (int64_t)P->C;
+  if (P->unbounded && E64 > 0) return -75;         // (the primary never evicts: its capacity is exceeded)
   const uint32_t E = E64 > 0 ? (uint32_t)E64 : 0u;
   const uint64_t dend = K->dclock + P->last_appends;
   if (hipMemsetAsync(P->occ, 0, 4ull * P->C, st) != hipSuccess ||
@@ -2064,6 +2071,9 @@ void xcg_disk_state_stats(const XcgDiskState* K, uint64_t* st) {
 //    free (a reopened volume's local front), else the lowest free xuid under a
 //    generated UUID (registry_load's local UUID on a fresh volume, :575-596).
 // The registry entry is written once the front exists.
+void xcg_pair_state_set_unbounded(XcgPairState* P) { P->unbounded = true; }
+int xcg_pair_state_unbounded(const XcgPairState* P) { return P && P->unbounded ? 1 : 0; }
+
 int xcg_pair_state_create(uint32_t C, XcgDiskState* K, const char* uuid36, int want_xuid, XcgPairState** out) {
   if (C == 0 || !K || (uint64_t)K->D + C >= (1ull << 30)) return -22;
   if (uuid36 && (strlen(uuid36) != 36 || !uuid_ok((const uint8_t*)uuid36))) return -22;
@@ -2513,7 +2523,7 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     }
     const clk::time_point t3 = clk::now();
     const PairGpu G = gpu_of(a);
-    if (pair_commit(P, G, st)) { done_scratch(); return -5; }
+    if (const int crc = pair_commit(P, G, st)) { done_scratch(); return crc == -75 ? -75 : -5; }
     done_scratch();
     if (pair_debug())
       fprintf(stderr, "pair: ms seed %.2f seed-replay %.2f parse %.2f replay %.2f commit %.2f (primary %u, clock %llu)\n",

@@ -172,6 +172,10 @@ def lib():
     L.xcg_debug_set_lds_filter_keys.restype = C.c_uint32
     L.xcg_debug_set_lds_prefilter_keys.argtypes = [C.c_uint32]
     L.xcg_debug_set_lds_prefilter_keys.restype = C.c_uint32
+    L.xcg_debug_decode_kernel_timing.argtypes = [C.c_int]
+    L.xcg_debug_decode_kernel_timing.restype = C.c_int
+    L.xcg_debug_decode_kernel_time.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+    L.xcg_debug_decode_kernel_time.restype = C.c_int
     L.xcg_debug_set_screen.argtypes = [C.c_int]
     L.xcg_debug_set_screen.restype = C.c_int
     L.xcg_debug_screen_counts.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
