@@ -338,11 +338,16 @@ def side_measurements(ctx, data, offs, lens, d_in, d_off, d_len, d_oo, d_out, d_
                                       C.c_void_p(d_dol.data_ptr()), C.c_void_p(d_dst.data_ptr()),
                                       C.c_void_p(d_dcons.data_ptr()), unk.ctypes.data, unk.size, nunk.ctypes.data,
                                       tot.ctypes.data, C.c_void_p(stream.cuda_stream)))
-    steps = 5
-    lib().xcg_debug_decode_kernel_timing(1)
-    wall, _, _, _ = timed(dec, steps, stream)
-    lib().xcg_debug_decode_kernel_timing(0)
+    wall, _, _, _ = timed(dec, 5, stream)
+    # device time of the decode kernels: HIP events around each device segment
+    # of 5 more calls (after the warm-up ones above)
     step_ms, emit_ms, segs = C.c_double(), C.c_double(), C.c_uint32()
+    lib().xcg_debug_decode_kernel_time(None, None, None)
+    lib().xcg_debug_decode_kernel_timing(1)
+    for _ in range(5):
+        dec()
+    torch.cuda.synchronize()
+    lib().xcg_debug_decode_kernel_timing(0)
     lib().xcg_debug_decode_kernel_time(C.byref(step_ms), C.byref(emit_ms), C.byref(segs))
     calls = max(1, segs.value // 3)                   # (three device segments per decode call)
     if int(tot[0]) != in_bytes or d_dout[:in_bytes].cpu().numpy().tobytes() != data.tobytes():

@@ -90,7 +90,11 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 	uint32_t e = 0;
 	while (i + 1 < b) {
 		if (in[i] != XCODEC_MAGIC) {
-			i++;
+			/* (literal bytes up to the next op: memchr, not a byte loop) */
+			const uint8_t *m = (const uint8_t *)memchr(&in[i], XCODEC_MAGIC, b - i);
+			if (m == NULL)
+				break;
+			i = (uint64_t)(m - &in[0]);
 			continue;
 		}
 		const uint8_t op = in[i + 1];
@@ -98,9 +102,9 @@ mirror_extracts(XCodecCache *cache, const std::vector<uint8_t>& in, uint64_t a, 
 			const uint8_t *p = &in[i + 2];
 			const uint64_t hash = hashes != NULL && e < nh ? hashes[e] : XCodecHash::hash(p);
 			e++;
-			Buffer tmp(p, XCODEC_SEGMENT_LENGTH);
-			BufferSegment *seg;
-			tmp.copyout(&seg, XCODEC_SEGMENT_LENGTH);
+			/* one segment made straight from the input (as Buffer + copyout
+			 * would, without the Buffer around it) */
+			BufferSegment *seg = BufferSegment::create(p, XCODEC_SEGMENT_LENGTH);
 			BufferSegment *oseg = cache->lookup(hash);
 			if (oseg == NULL) {
 				cache->enter(hash, seg);

@@ -41,7 +41,9 @@ class Oracle:
         ref = self.ref
         if dropin:
             import torch  # noqa: F401  (one HIP runtime shared with libxcgpu.so)
-            path = os.path.join(HERE, '_ref/libxcdropin.so')
+            # (XCGPU_DROPIN_LIB: a diagnostics build of the same harness, e.g.
+            # _ref/libxcdropin_at.so with the adapter's phase timers)
+            path = os.environ.get('XCGPU_DROPIN_LIB') or os.path.join(HERE, '_ref/libxcdropin.so')
         else:
             path = os.path.join(HERE, '_ref/libxcref.so' if ref else 'build/liboracle.so')
         if not os.path.exists(path):

@@ -45,14 +45,17 @@ namespace xcg {
 // (non-temporal) loads: each byte is read once, and the headline launch runs
 // ~5 % faster so (the stream kernel, whose probes read L2-resident tables,
 // measured no gain: C4 654 vs 636 us, C2-S2 294 vs 297).
+#ifndef XCG_STREAM_NT
+#define XCG_STREAM_NT 0
+#endif
 template <bool STREAM>
 __device__ __forceinline__ u32x4 piece_ld_safe(const uint8_t* x, int q, int len) {
-  if constexpr (STREAM) return load16_aligned_safe(x, q, len);
+  if constexpr (STREAM && !XCG_STREAM_NT) return load16_aligned_safe(x, q, len);
   else return load16_aligned_safe_stream(x, q, len);
 }
 template <bool STREAM>
 __device__ __forceinline__ u32x4 piece_ld(const uint8_t* p) {
-  if constexpr (STREAM) return *(const u32x4*)p;
+  if constexpr (STREAM && !XCG_STREAM_NT) return *(const u32x4*)p;
   else return load16_stream(p);
 }
 
