@@ -193,7 +193,7 @@ def pmc_traffic(n):
     summary (scripts/profile.sh + scripts/prof_summary.py: FETCH_SIZE doubled
     per MI355X_MICROARCH.md "HBM", plus WRITE_SIZE), when it was taken on this
     same workload; PMC counters cannot be read from inside the timed run."""
-    for name in ('r05_c2_independent_summary.json', 'r04_c2_independent_summary.json',
+    for name in ('r06_c2_independent_summary.json', 'r05_c2_independent_summary.json', 'r04_c2_independent_summary.json',
                  'r03_c2_independent_summary.json', 'r02_c2_independent_summary.json',
                  'r01_c2_independent_summary.json'):
         p = os.path.join(ROOT, 'profiles', name)
@@ -208,7 +208,8 @@ def pmc_traffic(n):
 def pmc_stream_traffic():
     """HBM bytes of the seeded C2-S2 stream-parse launch (the bench's S2 step)
     from the committed scripts/profile_stream.sh summary."""
-    for name in ('r05_stream_pmc_summary.json', 'r04_stream_pmc_summary.json', 'r03_stream_pmc_summary.json',
+    for name in ('r06_stream_pmc_summary.json', 'r05_stream_pmc_summary.json', 'r04_stream_pmc_summary.json',
+                 'r03_stream_pmc_summary.json',
                  'r02_stream_pmc_summary.json'):
         p = os.path.join(ROOT, 'profiles', name)
         if not os.path.exists(p):
