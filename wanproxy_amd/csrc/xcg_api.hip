@@ -203,7 +203,9 @@ struct xcg_ctx {
   xcg_window* own_win = nullptr;   // default window (lazily allocated)
   xcg_window* cur_win = nullptr;   // window used by decodes (own_win unless set)
   int32_t* h_status = nullptr;     // pinned copy of d_status
-  bool seed_next = false;          // the last stream batch declared something: seed the next one
+  // seed the next stream batch with the chunks' tilings: a fresh cache is cold (every
+  // first batch declares), and later the last batch declared something
+  bool seed_next = true;
   bool bounded = false;            // XCodecMemoryCache with a limit: LRU eviction (xcg_lru.hip)
   XcgLruState lru{};
   // Completion of the context's last enqueued work (recorded on the caller's
