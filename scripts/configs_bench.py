@@ -203,7 +203,7 @@ def run_c2s(args):
     n = max(16, int(4096 * args.scale))
     data = np.frombuffer(synth.stream(0xC2, n * 64 * KiB, 50, 0), np.uint8).copy()
     offs, lens = synth.chunks_of(data.tobytes(), 64 * KiB)
-    ctx = Context(0, cache_segments=1 << 18)
+    ctx = Context(0, cache_segments=args.c2s_segs)
     B = Batches(ctx, data, offs, lens, per=n)
     clock = {}
     wall = timed_encode(B, args.reps, clock=clock)
@@ -504,6 +504,7 @@ def main():
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--batch-mib', type=int, default=512)
     ap.add_argument('--c4-batch', type=int, default=65536)
+    ap.add_argument('--c2s-segs', type=int, default=1 << 18, help='c2s: the context\'s cache capacity in segments')
     ap.add_argument('--lru-mib', type=int, default=128)
     ap.add_argument('--disk-mib', type=int, default=1024)
     ap.add_argument('--lru-check', type=float, default=1.0, help='share of c5lru chunks checked vs the oracle')

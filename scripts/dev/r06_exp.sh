@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-6 experiments (GPU box), one step per argument:
+#   segs     C2-S2 at three cache capacities (the probe tables scale with them)
+#   pairdbg  C5-PAIR with XCG_PAIR_DEBUG (per sub-batch phase ms; syncs added)
+#   trace    rocprofv3 kernel trace of c5pair and c2s (CFGS overrides)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for step in "$@"; do
+	case "$step" in
+	segs)
+		for s in 131072 262144 524288; do
+			timeout -k 10 200 python3 scripts/configs_bench.py c2s --reps 5 --no-decode --c2s-segs $s \
+				> gpurun_out/segs_$s.json 2> gpurun_out/segs_$s.err || exit $?
+			echo "segs $s $(head -c 400 gpurun_out/segs_$s.json)"
+		done ;;
+	pairdbg)
+		XCG_PAIR_DEBUG=1 timeout -k 10 200 python3 scripts/configs_bench.py c5pair --reps 2 --no-decode \
+			> gpurun_out/pairdbg.json 2> gpurun_out/pairdbg.err || exit $?
+		grep -E '^pair' gpurun_out/pairdbg.err | tail -12 ;;
+	trace)
+		for cfg in ${CFGS:-c5pair c2s}; do
+			timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/tr_$cfg -o run --output-format csv -- \
+				python3 scripts/configs_bench.py $cfg --reps 2 --no-decode > gpurun_out/tr_$cfg.log 2>&1 || exit $?
+			echo "traced $cfg"
+		done ;;
+	*) echo "unknown step $step"; exit 2 ;;
+	esac
+done
