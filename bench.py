@@ -549,9 +549,13 @@ def other_configs():
     # ~900 chunks) then split 8192 into 9 equal parts instead of 4096 into 5
     # twice -- a launch costs one chunk's serial parse however few it holds
     lru1 = argparse.Namespace(**{**vars(a), 'batch_mib': 1024})
+    # C5-PAIR likewise in one call: once the pair has measured its disk write
+    # rate (the first sub-batch), the shard fits one sub-batch under a disk lap
+    # instead of two (each costs a replay and a commit; profiles/r06_pair_*)
+    pair1 = argparse.Namespace(**{**vars(a), 'batch_mib': 1024})
     out = {}
     for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, lru1),
-                         ('C5-PAIR', cb.run_c5pair, a), ('C5-PAIR-LAPS', cb.run_c5pair, lap),
+                         ('C5-PAIR', cb.run_c5pair, pair1), ('C5-PAIR-LAPS', cb.run_c5pair, lap),
                          ('C5-PAIR-DENSE', cb.run_c5dense, dense)):
         try:
             out[name] = fn(ar)
@@ -649,7 +653,7 @@ def sharded_configs(world, rank, dev, backend='nccl'):
         t = torch.tensor([w], dtype=torch.float64, device=dev if backend == 'nccl' else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, world=world, rank=rank, reduce=reduce,
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=1024, c4_batch=65536, world=world, rank=rank, reduce=reduce,
                            no_decode=False, lru_mib=128, disk_mib=1024, lru_check=1.0, disk_laps=0)
     out = {}
     # C5 as BASELINE.json configs[4] words it: "cold cache with xcodec_cache_disk

@@ -25,6 +25,19 @@ for step in "$@"; do
 				python3 scripts/configs_bench.py $cfg --reps 2 --no-decode > gpurun_out/tr_$cfg.log 2>&1 || exit $?
 			echo "traced $cfg"
 		done ;;
+	ab)
+		# A/B of the main library against wanproxy_amd/libxcgpu.$VAR.so (CFGS, two alternations)
+		for rep in 1 2; do
+			for lib in libxcgpu.so libxcgpu.${VAR:-nodefer}.so; do
+				XCGPU_LIB=$PWD/wanproxy_amd/$lib timeout -k 10 300 python3 scripts/configs_bench.py ${CFGS:-c5lru c5pair} \
+					--reps 3 --no-decode $ARGS > gpurun_out/ab_${lib}_$rep.json 2> gpurun_out/ab_${lib}_$rep.err || exit $?
+				python3 -c "import json,sys; [print(sys.argv[1], json.loads(l)['config'][:18], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds')) for l in open(sys.argv[2]) if l.startswith('{')]" $lib gpurun_out/ab_${lib}_$rep.json
+			done
+		done ;;
+	big)
+		timeout -k 10 300 python3 scripts/configs_bench.py c5pair --reps 3 --no-decode --batch-mib 1024 \
+			> gpurun_out/big.json 2> gpurun_out/big.err || exit $?
+		head -c 600 gpurun_out/big.json ;;
 	*) echo "unknown step $step"; exit 2 ;;
 	esac
 done

@@ -451,8 +451,8 @@ __global__ __launch_bounds__(256) void lru_insert_alive_kernel(uint32_t C, const
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if ((gate && *gate) || s >= C || !alive[s]) return;
   const uint64_t k = skey[s];
-  if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), s)) atomicOr(status, 2);
-  filt_insert(fs, (uint32_t)k, (uint32_t)(k >> 32));
+  // (table + filters with the short chain of returning atomics, xcg_cache.h)
+  if (!tab_insert_min_filt(g, fs, (uint32_t)k, (uint32_t)(k >> 32), s)) atomicOr(status, 2);
 }
 
 // One wave per declaration: its pool slot from the free list, key, table,
@@ -477,8 +477,7 @@ __global__ __launch_bounds__(256) void lru_insert_new_kernel(uint32_t n, const u
   if (l == 0) {
     skey[s] = ((uint64_t)dd.y << 32) | dd.x;
     alive[s] = 1u;
-    if (!tab_insert_min(g, dd.x, dd.y, s)) atomicOr(status, 2);
-    filt_insert(fs, dd.x, dd.y);
+    if (!tab_insert_min_filt(g, fs, dd.x, dd.y, s)) atomicOr(status, 2);
   }
   uint8_t* dst = pool + (uint64_t)s * SEG;
   *(u32x4_u*)(dst + 32 * l) = v0;

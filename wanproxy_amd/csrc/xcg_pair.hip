@@ -1000,10 +1000,9 @@ __global__ __launch_bounds__(256) void pair_rebuild_kernel(const uint64_t* pkey,
     if (dxuid[i] == xuid && e != NOENT && dclock < death_of(e, nb)) k = dkey[i];
   }
   const bool have = k != EMPTY_KEY;
-  if (have) {
-    if (!tab_insert_min(g, (uint32_t)k, (uint32_t)(k >> 32), id)) atomicOr(status, 2);
-    filt_insert(fs, (uint32_t)k, (uint32_t)(k >> 32));
-  }
+  // (the table insert and the three filters with the short chain of returning
+  // atomics: two round trips per key instead of about four)
+  if (have && !tab_insert_min_filt(g, fs, (uint32_t)k, (uint32_t)(k >> 32), id)) atomicOr(status, 2);
   const uint64_t m = ballot(have);
   if (lane_id() == 0 && m) atomicAdd(nseg, (uint32_t)__builtin_popcountll(m));
 }
@@ -1202,6 +1201,9 @@ struct XcgPairState {
   uint64_t appends = 0;            // disk blocks the last committed sub-batch wrote
   uint32_t last_base = 0;
   int prev_passes = 1;
+  // chunks per sub-batch the last committed sub-batch's disk writes imply (90 %
+  // of a lap at its rate; 0: none yet); the next call starts from it
+  uint32_t fit_per = 0;
 };
 
 namespace {
@@ -2422,7 +2424,9 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
   // of disk blocks, nothing it declared can leave both levels within it (a
   // chunk writes at most maxd declarations plus its touches).
   const uint64_t lap = P->D > 2 * DISK_ENTRIES ? P->D - 2 * DISK_ENTRIES : 1;
-  uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, lap / a0->maxd));
+  // (maxd writes per chunk at most; the rate a previous sub-batch measured is
+  // used when it allows more -- a sub-batch that still laps the disk is split)
+  uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, std::max<uint64_t>(lap / a0->maxd, P->fit_per)));
   constexpr int MAX_PASSES = 12;
   uint32_t i0 = 0;
   using clk = std::chrono::steady_clock;
@@ -2430,7 +2434,10 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
   const HashTab g{a0->g_keys, a0->g_vals, a0->g_mask};
   while (i0 < n) {
     const clk::time_point t0 = clk::now();
-    const uint32_t m = per < n - i0 ? per : n - i0;
+    // what is left in equal parts of at most `per` chunks (no short tail
+    // sub-batch: each costs a replay and a commit whatever its size)
+    const uint32_t rem = n - i0, parts = (rem + per - 1) / per;
+    const uint32_t m = (rem + parts - 1) / parts;
     XcgStreamArgs a = *a0;
     a.n = m;
     a.chunk_off += i0;
@@ -2517,6 +2524,7 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
       done_scratch();
       if (m == 1) return split ? -95 : -75;
       per = m / 2;                                 // redo this part in halves
+      P->fit_per = 0;                              // (and size the next call from the worst case again)
       P->prev_passes = MAX_PASSES;
       if (fill_ptime(P, st)) return -5;
       continue;
@@ -2537,7 +2545,10 @@ int xcg_pair_encode_stream(const XcgStreamArgs* a0, XcgPairState* P, int* rounds
     // size the next sub-batch from the disk blocks this one wrote
     const uint64_t useD = P->appends;
     uint64_t want = (uint64_t)n;
-    if (useD) want = std::min<uint64_t>(want, lap * 9 / 10 * m / useD);
+    if (useD) {
+      want = std::min<uint64_t>(want, lap * 9 / 10 * m / useD);
+      P->fit_per = (uint32_t)std::min<uint64_t>(lap * 9 / 10 * m / useD, 1u << 30);
+    }
     per = (uint32_t)(want < 1 ? 1 : (want > n ? n : want));
   }
   if (rounds_out) *rounds_out = rounds;
