@@ -38,6 +38,15 @@ for step in "$@"; do
 		timeout -k 10 300 python3 scripts/configs_bench.py c5pair --reps 3 --no-decode --batch-mib 1024 \
 			> gpurun_out/big.json 2> gpurun_out/big.err || exit $?
 		head -c 600 gpurun_out/big.json ;;
+	pairs)
+		# the pair configurations as the bench runs them (1 GiB calls; LAPS in 512 MiB; DENSE)
+		timeout -k 10 300 python3 scripts/configs_bench.py c5pair --reps 3 --no-decode --batch-mib 1024 \
+			> gpurun_out/pairs.json 2> gpurun_out/pairs.err || exit $?
+		timeout -k 10 300 python3 scripts/configs_bench.py c5pair --reps 2 --no-decode --disk-laps 3 \
+			>> gpurun_out/pairs.json 2>> gpurun_out/pairs.err || exit $?
+		timeout -k 10 300 python3 scripts/configs_bench.py c5dense --reps 2 --no-decode --dense-pool 16 --lru-check 0.1 \
+			>> gpurun_out/pairs.json 2>> gpurun_out/pairs.err || exit $?
+		python3 -c "import json,sys; [print(json.loads(l)['config'][:60], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds'), json.loads(l).get('kernel')) for l in open(sys.argv[1]) if l.startswith('{')]" gpurun_out/pairs.json ;;
 	*) echo "unknown step $step"; exit 2 ;;
 	esac
 done

@@ -100,6 +100,40 @@ def test_pair_random_vs_oracle(oracle):
         assert (st[1], st[2]) == est, (t, chunk, limit, disk)
 
 
+def test_pair_fit_hint_overshoot_still_exact(oracle):
+    """A call's first sub-batch is sized from the disk write rate the last
+    sub-batch measured (xcg_pair.hip fit_per, kept across calls): a dup-heavy
+    call (few disk writes per chunk) is followed by fresh data that laps the
+    disk and then repeats its start.  The hint lets the first sub-batch
+    overshoot the lap, the replay finds a lookup of an entry the sub-batch made
+    and lost, the part is redone in halves -- and the output and the disk
+    counters are still the sequential encoder's."""
+    from oracle.lib import MODE_STREAM
+    from wanproxy_amd import synth
+    from wanproxy_amd.xcgpu import XCG_SEM_STREAM, Context
+    d1 = synth.stream(0xF17, 2 << 20, 95, 0)
+    u = synth.stream(0xF18, 3 << 20, 0, 0)
+    d = d1 + u + u[:1 << 20]
+    offs, lens = synth.chunks_of(d, 65536)
+    k = len(d1) // 65536
+    limit, disk = 40 * 2048, mpg.disk_bytes(5)
+    ctx = Context(0, memory_cache_limit=limit, disk_bytes=disk)
+    got = ctx.encode_chunks(d, offs[:k], lens[:k], semantics=XCG_SEM_STREAM)
+    got += ctx.encode_chunks(d, offs[k:], lens[k:], semantics=XCG_SEM_STREAM)
+    # and a third call after the split reset the hint
+    got += ctx.encode_chunks(d, offs[:k], lens[:k], semantics=XCG_SEM_STREAM)
+    st = ctx.pair_stats()
+    ctx.close()
+    c = oracle.cache_new_pair(limit, disk)
+    exp = oracle.encode_batch(d, offs, lens, mode=MODE_STREAM, cache=c)
+    exp += oracle.encode_batch(d, offs[:k], lens[:k], mode=MODE_STREAM, cache=c)
+    est = oracle.pair_stats(c)
+    oracle.cache_free(c)
+    bad = [i for i in range(len(got)) if got[i] != exp[i]]
+    assert not bad, bad[:5]
+    assert (st[1], st[2]) == est
+
+
 def test_pair_scaled_c5_decodes(oracle):
     """A scaled C5-PAIR (16 MiB stream, 128 KiB chunks, 1 MiB primary, 8 MiB
     disk): oracle parity and a GPU decode round trip (unbounded decoder)."""

@@ -64,6 +64,7 @@
 // writes the appended disk blocks and rebuilds G -- all on the device.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort_config.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 #include <stdio.h>
@@ -1210,6 +1211,14 @@ namespace {
 
 using namespace xcg;
 
+// The replay's sorts (a few hundred thousand rows of 20-bit entity keys, or
+// 64-bit hashes) as rocPRIM's Onesweep radix sort: a histogram, a scan and one
+// pass per 8 bits.  The default config takes merge sort up to 2^20 items, ~20
+// launches of block merges for a C5 sub-batch (profiles/r06_s3_*).  Both are
+// stable, which the entity runs need (positions stay in order).
+using PairSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                               rocprim::default_config, 0>;
+
 bool pair_debug() {
   static const bool on = getenv("XCG_PAIR_DEBUG") != nullptr;
   return on;
@@ -1284,12 +1293,12 @@ int ensure_scratch(XcgPairState* P, uint64_t np, uint64_t n, uint64_t etot) {
   }
   // rocprim temporary storage for the largest sort / scan of this size
   size_t a = 0, b = 0, c = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
+  (void)rocprim::radix_sort_pairs<PairSortCfg>(nullptr, a, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, 32);
   // (the commit also scans the primary's C + 1 free-slot flags, pair_commit)
   (void)rocprim::exclusive_scan(nullptr, b, P->isr, P->rc, 0u,
                                 (size_t)std::max<uint64_t>(std::max<uint64_t>(np, n), P->C) + 1,
                                 rocprim::plus<uint32_t>());
-  (void)rocprim::radix_sort_pairs(nullptr, c, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)np, 0, 64);
+  (void)rocprim::radix_sort_pairs<PairSortCfg>(nullptr, c, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)np, 0, 64);
   size_t e1 = 0, e2 = 0, e3 = 0;
   (void)rocprim::exclusive_scan(nullptr, e1, P->sa, P->sb, (uint64_t)0, (size_t)np + 1, rocprim::maximum<uint64_t>());
   (void)rocprim::inclusive_scan(nullptr, e2, P->sa, P->sb, (size_t)np + 1, rocprim::maximum<uint64_t>());
@@ -1435,7 +1444,7 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
     // values: positions P .. np-1
     hipLaunchKernelGGL(pr_iota_kernel, dim3(grid_for(R)), dim3(256), 0, st, P->hv, (uint32_t)R, P->pcount);
     size_t tb = P->tmp_cap;
-    if (rocprim::radix_sort_pairs(P->tmp, tb, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)R, 0, 64, st) != hipSuccess)
+    if (rocprim::radix_sort_pairs<PairSortCfg>(P->tmp, tb, P->hk, P->hk2, P->hv, P->hv2, (uint32_t)R, 0, 64, st) != hipSuccess)
       return -5;
     // latest definer / first GHIT per hash run by scans (f1: run heads, f2: their prefix, r1: first GHIT)
     hipLaunchKernelGGL(pr_dh_heads_kernel, dim3(grid_for(R + 1)), dim3(256), 0, st, (const uint64_t*)P->hk2,
@@ -1453,7 +1462,7 @@ int replay(XcgPairState* P, const RowSrc& rs, const HashTab& g, bool want_leave,
   {
     const uint32_t bits = 32 - __builtin_clz(etot | 1u);
     size_t tb = P->tmp_cap;
-    if (rocprim::radix_sort_pairs(P->tmp, tb, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, bits, st) !=
+    if (rocprim::radix_sort_pairs<PairSortCfg>(P->tmp, tb, P->skey, P->sk, P->sval, P->sv, (uint32_t)np, 0, bits, st) !=
         hipSuccess)
       return -5;
   }
