@@ -817,9 +817,13 @@ __global__ __launch_bounds__(256) void pr_leave_kernel(PairDev d) {
 
 // Commit, step 1: the final primary residents -- last references that are
 // terminal and not evicted -- and the slots initial residents keep.
-__global__ __launch_bounds__(256) void pr_final_kernel(PairDev d, uint32_t E) {
+// E = P + M - C primary evictions, M (the misses) read on the device: the
+// commit needs no readback before it.
+__global__ __launch_bounds__(256) void pr_final_kernel(PairDev d, const uint32_t* Mp) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k > d.np) return;
+  const int64_t e64 = (int64_t)d.P + (int64_t)*Mp - (int64_t)d.C;
+  const uint32_t E = e64 > 0 ? (uint32_t)e64 : 0u;
   uint32_t fin = 0, nw = 0;
   if (k < d.np && d.isr[k] && d.nxt[k] < 0 && d.r2[k] >= E) {
     const uint32_t x = d.kind[k] == K_REPL ? d.yent[k] : d.ent[k];
@@ -954,18 +958,46 @@ __global__ __launch_bounds__(256) void pair_stage_kernel(const uint4* w, const P
   *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
 }
 
+// Four moves per wave (MOVES_PER_WAVE): their job words, then their source
+// addresses, then all eight 16-byte loads per lane are in flight before the
+// first store -- one chain of round trips per four 2 KiB copies instead of one
+// per copy (the commit's largest kernel: ~2 GB per GiB of C5).
+constexpr uint32_t MOVES_PER_WAVE = 4;
 __global__ __launch_bounds__(256) void pair_move_kernel(const uint4* w, const PairCnt* cnt, const uint8_t* in,
                                                         const uint64_t* chunk_off, const uint4* decl, uint32_t maxd,
                                                         const uint8_t* staging, uint8_t* pool) {
-  const uint32_t j = blockIdx.x * 4u + readfirst(threadIdx.x >> 6);
-  if (j >= cnt->nmove) return;
-  const uint4 m = w[j];
-  const uint8_t* src = m.y == 0u ? in + chunk_off[m.z] + decl[(uint64_t)m.z * maxd + m.w].z
-                                 : staging + (uint64_t)m.w * SEG;
-  uint8_t* dst = pool + (uint64_t)m.x * SEG;
+  const uint32_t j0 = (blockIdx.x * 4u + readfirst(threadIdx.x >> 6)) * MOVES_PER_WAVE;
+  const uint32_t nm = readfirst(cnt->nmove);
+  if (j0 >= nm) return;
   const int l = lane_id();
-  *(u32x4_u*)(dst + 32 * l) = *(const u32x4_u*)(src + 32 * l);
-  *(u32x4_u*)(dst + 32 * l + 16) = *(const u32x4_u*)(src + 32 * l + 16);
+  uint4 m[MOVES_PER_WAVE];
+#pragma unroll
+  for (int t = 0; t < (int)MOVES_PER_WAVE; ++t) m[t] = w[min(j0 + (uint32_t)t, nm - 1u)];
+  uint64_t co[MOVES_PER_WAVE];
+  uint32_t dz[MOVES_PER_WAVE];
+#pragma unroll
+  for (int t = 0; t < (int)MOVES_PER_WAVE; ++t) {     // (kind 0: where the declaration's bytes are)
+    co[t] = 0ull;
+    dz[t] = 0u;
+    if (m[t].y == 0u) {
+      co[t] = chunk_off[m[t].z];
+      dz[t] = decl[(uint64_t)m[t].z * maxd + m[t].w].z;
+    }
+  }
+  u32x4 v[MOVES_PER_WAVE][2];
+#pragma unroll
+  for (int t = 0; t < (int)MOVES_PER_WAVE; ++t) {
+    const uint8_t* src = m[t].y == 0u ? in + co[t] + dz[t] : staging + (uint64_t)m[t].w * SEG;
+    v[t][0] = *(const u32x4_u*)(src + 32 * l);
+    v[t][1] = *(const u32x4_u*)(src + 32 * l + 16);
+  }
+#pragma unroll
+  for (int t = 0; t < (int)MOVES_PER_WAVE; ++t) {
+    if (j0 + (uint32_t)t >= nm) break;
+    uint8_t* dst = pool + (uint64_t)m[t].x * SEG;
+    *(u32x4_u*)(dst + 32 * l) = v[t][0];
+    *(u32x4_u*)(dst + 32 * l + 16) = v[t][1];
+  }
 }
 
 struct PairWipe {
@@ -1586,19 +1618,19 @@ int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
     hipLaunchKernelGGL(pr_missterm_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d);
     if (scan_u32(P, P->f1, P->r1, np + 1, st) || scan_u32(P, P->f2, P->r2, np + 1, st)) return -5;
     hipLaunchKernelGGL(pr_missrow_kernel, dim3(grid_for(np)), dim3(256), 0, st, d);
-    if (read_small(P, P->r1 + np, 4, st)) return -5;
-    P->last_M = P->h_small[0];
+    if (P->unbounded) {                            // (only this check needs M on the host)
+      if (read_small(P, P->r1 + np, 4, st)) return -5;
+      P->last_M = P->h_small[0];
+    }
   }
-  const uint32_t M = P->last_M;
-  const int64_t E64 = (int64_t)d.P + (int64_t)M - (int64_t)P->C;
-  if (P->unbounded && E64 > 0) return -75;         // (the primary never evicts: its capacity is exceeded)
-  const uint32_t E = E64 > 0 ? (uint32_t)E64 : 0u;
+  // the primary never evicts: its capacity is exceeded
+  if (P->unbounded && (int64_t)d.P + (int64_t)P->last_M - (int64_t)P->C > 0) return -75;
   const uint64_t dend = K->dclock + P->last_appends;
   if (hipMemsetAsync(P->occ, 0, 4ull * P->C, st) != hipSuccess ||
       hipMemsetAsync(&P->cnt->nmove, 0, 8, st) != hipSuccess)
     return -5;
   // (terminal ranks r2 are consumed by pr_final before f1 / f2 / r1 / r2 are reused)
-  hipLaunchKernelGGL(pr_final_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d, E);
+  hipLaunchKernelGGL(pr_final_kernel, dim3(grid_for(np + 1)), dim3(256), 0, st, d, (const uint32_t*)P->r1 + np);
   if (scan_u32(P, P->f1, P->r1, np + 1, st) || scan_u32(P, P->f2, P->r2, np + 1, st)) return -5;
   hipLaunchKernelGGL(pr_notocc_kernel, dim3(grid_for(P->C + 1)), dim3(256), 0, st, (const uint32_t*)P->occ, P->C,
                      P->ofl);
@@ -1617,7 +1649,8 @@ int pair_commit(XcgPairState* P, const PairGpu& G, hipStream_t st) {
   if (nmove) {
     hipLaunchKernelGGL(pair_stage_kernel, dim3((nmove + 3) / 4), dim3(256), 0, st, (const uint4*)P->moves,
                        (const PairCnt*)P->cnt, (const uint8_t*)G.pool, P->staging);
-    hipLaunchKernelGGL(pair_move_kernel, dim3((nmove + 3) / 4), dim3(256), 0, st, (const uint4*)P->moves,
+    hipLaunchKernelGGL(pair_move_kernel, dim3((nmove + 4 * MOVES_PER_WAVE - 1) / (4 * MOVES_PER_WAVE)), dim3(256), 0, st,
+                       (const uint4*)P->moves,
                        (const PairCnt*)P->cnt, G.in, G.chunk_off, (const uint4*)G.decl, G.maxd,
                        (const uint8_t*)P->staging, G.pool);
   }
