@@ -47,6 +47,32 @@ for step in "$@"; do
 		timeout -k 10 300 python3 scripts/configs_bench.py c5dense --reps 2 --no-decode --dense-pool 16 --lru-check 0.1 \
 			>> gpurun_out/pairs.json 2>> gpurun_out/pairs.err || exit $?
 		python3 -c "import json,sys; [print(json.loads(l)['config'][:60], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds'), json.loads(l).get('kernel')) for l in open(sys.argv[1]) if l.startswith('{')]" gpurun_out/pairs.json ;;
+	sizes)
+		# call sizes: C5 in 512 vs 1024 MiB calls, C4 in 65536 vs 131072 packets
+		for a in "c5 --batch-mib 512" "c5 --batch-mib 1024" "c4 --c4-batch 65536" "c4 --c4-batch 131072"; do
+			timeout -k 10 300 python3 scripts/configs_bench.py $a --reps 3 --no-decode > gpurun_out/sizes.json 2> gpurun_out/sizes.err || exit $?
+			python3 -c "import json,sys; [print(sys.argv[1], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds')) for l in open(sys.argv[2]) if l.startswith('{')]" "$a" gpurun_out/sizes.json
+		done ;;
+	lfk)
+		# the LDS-alone threshold (XCG_LDS_FILTER_KEYS) on the big-cache configurations
+		for k in 150000 40000 0; do
+			for a in "c5pair --batch-mib 1024" "c5 --batch-mib 512" "c5lru --batch-mib 1024" "c2s"; do
+				XCG_LDS_FILTER_KEYS=$k timeout -k 10 300 python3 scripts/configs_bench.py $a --reps 3 --no-decode > gpurun_out/lfk.json 2> gpurun_out/lfk.err || exit $?
+				python3 -c "import json,sys; [print(sys.argv[1], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds'), json.loads(l).get('kernel',{}).get('stream_kernel_ms')) for l in open(sys.argv[2]) if l.startswith('{')]" "lfk=$k $a" gpurun_out/lfk.json
+			done
+		done ;;
+	auto)
+		# the automatic LDS-alone threshold against the old fixed 150000, alternating
+		for rep in 1 2; do
+			for k in auto 150000; do
+				for a in "c4 --c4-batch 65536" "c4 --c4-batch 131072" "c5 --batch-mib 512" "c3"; do
+					if [ $k = auto ]; then unset XCG_LDS_FILTER_KEYS; else export XCG_LDS_FILTER_KEYS=$k; fi
+					timeout -k 10 300 python3 scripts/configs_bench.py $a --reps 3 --no-decode > gpurun_out/auto.json 2> gpurun_out/auto.err || exit $?
+					python3 -c "import json,sys; [print(sys.argv[1], json.loads(l)['encode_GiBps'], json.loads(l).get('rounds')) for l in open(sys.argv[2]) if l.startswith('{')]" "$k $a" gpurun_out/auto.json
+				done
+			done
+		done
+		unset XCG_LDS_FILTER_KEYS ;;
 	*) echo "unknown step $step"; exit 2 ;;
 	esac
 done

@@ -10,7 +10,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/profs
+OUT=${PROF_OUT:-gpurun_out/profs}
 rm -rf $OUT; mkdir -p $OUT
 declare -A PMC=(
 	[fetch]="FETCH_SIZE"
