@@ -536,7 +536,9 @@ def other_configs():
     # eviction), every chunk checked against the oracle's bounded cache
     # C5-PAIR: C5 on wanproxy.conf's whole cache, the 128 MiB memory cache over
     # a 1 GiB disk (XCodecCachePair), every chunk checked against the oracle's pair
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=65536, lru_mib=128, lru_check=1.0,
+    # (C4: the shard's 131072 packets in one call -- one seed, screen and commit
+    # instead of two: +4 %, profiles/r06_s3_lfk.txt)
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=512, c4_batch=131072, lru_mib=128, lru_check=1.0,
                            disk_mib=1024, no_decode=False, disk_laps=0)
     # C5-PAIR-LAPS: the same with a disk the shard laps ~3 times (FIFO eviction
     # and re-entry inside the measured figure)
@@ -653,7 +655,7 @@ def sharded_configs(world, rank, dev, backend='nccl'):
         t = torch.tensor([w], dtype=torch.float64, device=dev if backend == 'nccl' else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
-    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=1024, c4_batch=65536, world=world, rank=rank, reduce=reduce,
+    a = argparse.Namespace(scale=1.0, reps=2, batch_mib=1024, c4_batch=131072, world=world, rank=rank, reduce=reduce,
                            no_decode=False, lru_mib=128, disk_mib=1024, lru_check=1.0, disk_laps=0)
     out = {}
     # C5 as BASELINE.json configs[4] words it: "cold cache with xcodec_cache_disk

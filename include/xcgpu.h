@@ -507,7 +507,8 @@ int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in
 /* Diagnostics / tests: stream-semantics batches probe the cache through a
  * 64 KiB LDS lane filter while the cache + batch hold at most this many keys,
  * else through a global (L2-resident) one; both give the same output.
- * Returns the previous threshold (default 150000, or XCG_LDS_FILTER_KEYS). */
+ * Returns the previous threshold (default ~0u = automatic: 150000, or 0 for a
+ * cache whose fingerprint buckets exceed 2 MiB; or XCG_LDS_FILTER_KEYS). */
 uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys);
 /* Diagnostics / tests: past that threshold, and while the cache + batch hold at
  * most this many keys, the LDS filter still goes first and only the positions

@@ -2752,9 +2752,16 @@ __global__ __launch_bounds__(256) void commit_kernel(const uint4* decl, const ui
 
 // LDS / global lane filter threshold (keys): XCG_LDS_FILTER_KEYS at load
 // time, or xcg_debug_set_lds_filter_keys (tests force either mode with it).
+// Default (LFK_AUTO): per cache -- LDS_FILTER_KEYS_DEFAULT while its fingerprint
+// buckets fit 2 MiB of L2, else 0: with a larger bucket table (unbounded caches
+// of 2^19+ segments, pairs) an LDS-filter pass costs fewer HBM misses as a
+// probe of the L2-resident global filter than as a bucket load (C5 308 -> 316
+// GiB/s; C2-S2 and the LRU cache, 2 MiB of buckets, lose with 0:
+// profiles/r06_s3_lfk.txt).
+constexpr uint32_t LFK_AUTO = ~0u;
 static uint32_t g_lds_filter_keys = [] {
   const char* e = getenv("XCG_LDS_FILTER_KEYS");
-  return e ? (uint32_t)strtoul(e, nullptr, 10) : xcg::LDS_FILTER_KEYS_DEFAULT;
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : LFK_AUTO;
 }();
 static uint32_t xcg_lds_filter_keys() { return __atomic_load_n(&g_lds_filter_keys, __ATOMIC_RELAXED); }
 extern "C" uint32_t xcg_debug_set_lds_filter_keys(uint32_t keys) {
@@ -2889,6 +2896,8 @@ extern "C" int xcg_launch_encode_stream(const XcgStreamArgs* a, int* rounds_out,
   prm.nseg = a->nseg;
   prm.bcount = a->bcount;
   prm.lds_filter_keys = xcg_lds_filter_keys();
+  if (prm.lds_filter_keys == LFK_AUTO)
+    prm.lds_filter_keys = 16ull * ((uint64_t)a->fmask + 1) > (2ull << 20) ? 0u : xcg::LDS_FILTER_KEYS_DEFAULT;
   prm.lds_prefilter_keys = __atomic_load_n(&g_lds_prefilter_keys, __ATOMIC_RELAXED);
   prm.ptime = a->ptime;
   prm.ev = (uint4*)a->ev;
