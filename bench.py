@@ -554,7 +554,10 @@ def other_configs():
     # C5-PAIR likewise in one call: once the pair has measured its disk write
     # rate (the first sub-batch), the shard fits one sub-batch under a disk lap
     # instead of two (each costs a replay and a commit; profiles/r06_pair_*)
-    pair1 = argparse.Namespace(**{**vars(a), 'batch_mib': 1024})
+    # (three reps: the first, without the fit hint, runs two sub-batches and
+    # sizes the scratch for them; the second then grows it for one 8192-chunk
+    # sub-batch inside its timed region)
+    pair1 = argparse.Namespace(**{**vars(a), 'batch_mib': 1024, 'reps': 3})
     out = {}
     for name, fn, ar in (('C3', cb.run_c3, a), ('C4', cb.run_c4, a), ('C5', cb.run_c5, a), ('C5-LRU', cb.run_c5lru, lru1),
                          ('C5-PAIR', cb.run_c5pair, pair1), ('C5-PAIR-LAPS', cb.run_c5pair, lap),

@@ -14,7 +14,7 @@ for s in range(S):
 ctx = zpipe.InflatePipes(S)
 L = zpipe._lib()
 L.xcg_debug_zi_times.argtypes = [C.c_void_p]
-t = np.zeros(10, np.uint64)
+t = np.zeros(16, np.uint64)
 for k in range(2):
     L.xcg_debug_zi_times(t.ctypes.data)
     t0 = time.perf_counter()

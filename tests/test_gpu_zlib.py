@@ -176,6 +176,16 @@ def test_errors():
 
 
 # ---------------------------------------------------------------- InflatePipe
+@pytest.fixture(params=[1, 2], ids=['wave', 'workgroup'])
+def inflate_mode(request):
+    """Both inflate kernels: a wave per call (batches of many streams) and a
+    workgroup per call (the per-call path: speculative Huffman regions)."""
+    from wanproxy_amd.zpipe import set_inflate_mode
+    set_inflate_mode(request.param)
+    yield request.param
+    set_inflate_mode(0)
+
+
 def inflate_streams(streams, out_cap=None):
     """streams: [[input cut bytes...]] -> [[(produced, status)...]], call k of
     every stream in batch k (InflatePipe::consume per cut).  out_cap: the first
@@ -202,7 +212,7 @@ def cuts(rng, z: bytes, mode: str):
     return out
 
 
-def test_inflate_zlib_streams_any_cut():
+def test_inflate_zlib_streams_any_cut(inflate_mode):
     """zlib-made streams (stored, static, dynamic blocks; levels 1-9) cut at
     random points; every call's output equals zlib's inflate on the same cuts."""
     from oracle.zlib_pipe import InflatePipeRef
@@ -226,7 +236,7 @@ def test_inflate_zlib_streams_any_cut():
         assert got[si][-1] == (b'', 1)     # EOS after the end: produce_eos
 
 
-def test_inflate_byte_by_byte_and_small():
+def test_inflate_byte_by_byte_and_small(inflate_mode):
     streams = []
     srcs = []
     for i, data in enumerate([b'', b'a', b'hello hello hello hello', bytes(1000), random.Random(3).randbytes(700)]):
@@ -239,7 +249,7 @@ def test_inflate_byte_by_byte_and_small():
         assert got[si][-1][1] == 1
 
 
-def test_gpu_deflate_then_gpu_inflate():
+def test_gpu_deflate_then_gpu_inflate(inflate_mode):
     """wanproxy's zlib stage both ways on the GPU: DeflatePipe output, cut
     into frames, through InflatePipe, for 64 streams."""
     rng = random.Random(8)
@@ -251,7 +261,7 @@ def test_gpu_deflate_then_gpu_inflate():
         assert b''.join(o for o, _ in got[i]) == b''.join(streams[i])
 
 
-def test_inflate_errors():
+def test_inflate_errors(inflate_mode):
     good = zlib.compress(b'payload ' * 100, 6)
     bad_adler = good[:-1] + bytes([good[-1] ^ 1])
     bad_header = bytes([0x78, 0x9d]) + good[2:]
@@ -284,7 +294,7 @@ def test_distance_boundaries_both_ways():
     assert got[-1][1] == 1
 
 
-def test_inflate_retry_after_no_room():
+def test_inflate_retry_after_no_room(inflate_mode):
     """Status -2 (output room too small) commits nothing, wherever it strikes:
     inside a stored block, inside a Huffman block, right after the next
     dynamic block's header.  Calls start with 256 bytes of room and are
@@ -315,7 +325,7 @@ def test_inflate_retry_after_no_room():
         assert b''.join(o for o, _ in got[si]) == src
 
 
-def test_inflate_slot_reuse_after_reset():
+def test_inflate_slot_reuse_after_reset(inflate_mode):
     """A slot whose stream ended (or failed) serves a fresh InflatePipe after
     xcg_zinflate_reset -- the adapter's constructor on a reused slot."""
     from wanproxy_amd.zpipe import InflatePipes
@@ -332,6 +342,110 @@ def test_inflate_slot_reuse_after_reset():
     assert ctx.consume_many([(0, b), (1, a[:10])]) == [(b'second stream ' * 70, 1), (head, 0)]
     assert ctx.consume_many([(1, a[10:])]) == [((b'first stream ' * 50)[len(head):], 1)]
     ctx.close()
+
+
+def _text(rng, n):
+    words = [bytes(rng.choice(b'etaoinshrdlucmfwyp') for _ in range(rng.randint(1, 9))) for _ in range(400)]
+    out = bytearray()
+    while len(out) < n:
+        out += rng.choice(words) + rng.choice([b' ', b' ', b', ', b'.\n'])
+    return bytes(out[:n])
+
+
+def _inflate_both(streams, out_cap=None):
+    """Every stream through both kernels: (wave per call, workgroup per call)."""
+    from wanproxy_amd.zpipe import set_inflate_mode
+    got = []
+    try:
+        for mode in (1, 2):
+            set_inflate_mode(mode)
+            got.append(inflate_streams(streams, out_cap=out_cap))
+    finally:
+        set_inflate_mode(0)
+    return got
+
+
+def test_inflate_workgroup_regions_vs_zlib():
+    """The workgroup kernel's speculative regions on the data that exercises
+    them: 64 KiB-and-larger consumes of text, of runs (matches on matches,
+    distance 1, chains thousands deep), of incompressible bytes (stored and
+    Huffman blocks of literals), skewed alphabets (long codes past the primary
+    tables), fixed blocks (level 1 on short calls) -- one call, frames and
+    random cuts; every call equals zlib's inflate on the same cuts, and the
+    wave-per-call kernel's, byte for byte and status for status."""
+    from oracle.zlib_pipe import InflatePipeRef
+    rng = random.Random(2024)
+    datas = [_text(rng, 300000), b'a' * 200000 + b'b' * 70000, bytes(range(256)) * 900,
+             rng.randbytes(150000), _text(rng, 5000) * 40,
+             bytes(rng.choice(b'\x00\x01\x02\x03' * 50 + bytes(range(256))) for _ in range(120000)),
+             b''.join(rng.randbytes(rng.randint(1, 40)) * rng.randint(1, 300) for _ in range(3000))]
+    srcs, streams = [], []
+    for i, d in enumerate(datas):
+        for level in (1, 6, 9):
+            z = zlib.compress(d, level)
+            for mode in ('whole', 'frames', 'random'):
+                srcs.append(d)
+                streams.append(([z] if mode == 'whole' else cuts(rng, z, mode)) + [b''])
+    # fixed Huffman blocks: zlib's Z_FIXED strategy
+    for d in datas[:3]:
+        c = zlib.compressobj(6, zlib.DEFLATED, 15, 8, zlib.Z_FIXED)
+        z = c.compress(d) + c.flush()
+        srcs.append(d)
+        streams.append([z, b''])
+    wave, wg = _inflate_both(streams)
+    for si, (src, cs) in enumerate(zip(srcs, streams)):
+        assert wg[si] == wave[si], si
+        ref = InflatePipeRef()
+        for k, c in enumerate(cs[:-1]):
+            assert wg[si][k] == (ref.consume(c), wg[si][k][1]), (si, k)
+            assert wg[si][k][1] in (0, 1), (si, k)
+        assert b''.join(o for o, _ in wg[si]) == src, si
+
+
+def test_inflate_workgroup_errors_mid_region():
+    """Errors deep inside a region decide the call as the one-wave decoder
+    does: a distance before the stream's start (a raw stream made against a
+    preset dictionary, behind a plain zlib header) after 40 KiB of good output,
+    a corrupt code in a long dynamic block, and a bad adler32 after a large
+    call.  Both kernels give the same output and status."""
+    rng = random.Random(5)
+    dic = _text(rng, 8000)
+    body = _text(random.Random(6), 40000).upper()   # no match into the (lower-case) dictionary before it
+    c = zlib.compressobj(6, zlib.DEFLATED, -15, zdict=dic)
+    raw = c.compress(body + dic[1000:3000] + body[:5000]) + c.flush()
+    far = bytes([0x78, 0x9c]) + raw + b'\0\0\0\0'
+    good = zlib.compress(_text(rng, 200000), 6)
+    corrupt = bytearray(good)
+    for k in range(20):
+        corrupt[len(good) // 2 + k] ^= 0xA5
+    bad_adler = good[:-1] + bytes([good[-1] ^ 1])
+    streams = [[far], [bytes(corrupt)], [bad_adler], [far[:30000], far[30000:]], [good[:65536], good[65536:], b'']]
+    wave, wg = _inflate_both(streams)
+    assert wg == wave
+    assert wg[0][0][1] == -1 and wg[2][0][1] == -1
+    assert wg[1][0][1] == -1
+    assert wg[4][-1] == (b'', 1)
+
+
+def test_inflate_workgroup_small_room():
+    """Output room smaller than a region's output: the region commits the
+    threads that fit, the careful path returns -2 where the wave kernel does,
+    and the retried calls match zlib."""
+    from oracle.zlib_pipe import InflatePipeRef
+    rng = random.Random(12)
+    srcs, streams = [], []
+    for i in range(6):
+        d = _text(rng, 150000) if i % 2 else b'xyz' * 60000
+        z = zlib.compress(d, 6)
+        srcs.append(d)
+        streams.append(cuts(rng, z, 'frames') + [b''])
+    wave, wg = _inflate_both(streams, out_cap=3000)
+    assert wg == wave
+    for si, (src, cs) in enumerate(zip(srcs, streams)):
+        ref = InflatePipeRef()
+        for k, c in enumerate(cs[:-1]):
+            assert wg[si][k][0] == ref.consume(c), (si, k)
+        assert b''.join(o for o, _ in wg[si]) == src
 
 
 # ------------------------------------------------- drop-in classes (adapter)

@@ -82,6 +82,7 @@ struct IArgs {
   IRes* res;
   uint32_t* out_len;
   int32_t* status;
+  uint32_t* pres;           // NW > 1: RES_CAP resolve slots per call
 };
 
 // carried bytes ++ new input into the scratch, 16 bytes per thread (the
@@ -133,53 +134,96 @@ struct Lds {
   uint8_t lens[320];        // fixed / code-length tree lengths
   uint8_t dlens[320];       // the dynamic block's literal/length + distance lengths
   uint16_t codes[320];
-  int ok;
+  uint16_t bfirst[16], boffs[16];   // build(): first code, first symbol slot of each length
 };
+
+// The decoder's own barrier: the whole workgroup for the one-wave kernel; for
+// the many-wave kernel the decoder's control runs in wave 0 alone, so its
+// barriers order that wave's LDS traffic only (the other waves wait in
+// helper_loop until wave 0 hands them a region).
+template <int NW>
+__device__ __forceinline__ void wsync() {
+  if constexpr (NW == 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
 
 // Canonical decoder from code lengths (inflate_table's rules: over-subscribed
 // sets are errors, incomplete ones too unless the only code has length 1).
-template <class Tree>
+// One wave, no serial loop over the symbols: per-length counts and each
+// symbol's rank among the symbols of its length come from ballots over chunks
+// of 64 symbols (canonical codes are assigned in symbol order within a
+// length), the first code and table offset of each length from the counts.
+template <int NW, class Tree>
 __device__ bool build(Lds& L, Tree& T, const uint8_t* lens, int n) {
   constexpr int PB = Tree::BITS;
   const int lane = threadIdx.x;
   for (int i = lane; i < (1 << PB); i += 64) T.pri[i] = 0;
-  if (lane == 0) {
-    for (int l = 0; l < 16; l++) T.cnt[l] = 0;
-    for (int i = 0; i < n; i++) T.cnt[lens[i]]++;
-    T.cnt[0] = 0;
-    int left = 1, maxl = 0;
-    bool ok = true;
-    for (int l = 1; l < 16; l++) {
-      left = (left << 1) - T.cnt[l];
-      if (left < 0) ok = false;
-      if (T.cnt[l]) maxl = l;
+  const int nch = (n + 63) >> 6;
+  uint32_t cnt = 0;                  // lane l in 1..15: codes of length l
+  for (int ch = 0; ch < nch; ch++) {
+    const int i = (ch << 6) + lane;
+    const int l = i < n ? lens[i] : 0;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+      const uint32_t c = (uint32_t)__popcll(ballot(l == k));
+      if (lane == k) cnt += c;
     }
-    if (ok && left > 0 && maxl != 1) ok = false;
-    uint16_t offs[16], next[16];
-    offs[1] = 0;
-    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + T.cnt[l];
-    uint32_t code = 0;   // first code of each length (RFC 1951 3.2.2)
-    for (int l = 1; l < 16; l++) {
-      code = (code + T.cnt[l - 1]) << 1;
-      next[l] = (uint16_t)code;
-    }
-    for (int i = 0; i < n; i++) {
-      int l = lens[i];
-      if (!l) continue;
-      T.sym[offs[l]++] = (uint16_t)i;
-      L.codes[i] = next[l]++;
-    }
-    L.ok = ok;
   }
-  __syncthreads();
+  // Kraft check, first code and symbol offset of each length (lane l)
+  int left = 1, maxl = 0;
+  bool ok = true;
+  uint32_t first = 0, offs = 0;
+#pragma unroll
+  for (int k = 1; k < 16; k++) {
+    const uint32_t ck = readlane(cnt, k);
+    left = (left << 1) - (int)ck;
+    if (left < 0) ok = false;
+    if (ck) maxl = k;
+    if (k < lane) {
+      first += ck << (lane - k);   // RFC 1951 3.2.2: code(l) = (code(l-1) + count(l-1)) << 1
+      offs += ck;
+    }
+  }
+  if (ok && left > 0 && maxl != 1) ok = false;
+  if (lane < 16) {
+    T.cnt[lane] = (uint16_t)(lane ? cnt : 0);
+    L.bfirst[lane] = (uint16_t)first;
+    L.boffs[lane] = (uint16_t)offs;
+  }
+  wsync<NW>();
+  uint32_t run = 0;                  // lane l: symbols of length l placed so far
+  const uint64_t below = (1ull << lane) - 1;
+  for (int ch = 0; ch < nch; ch++) {
+    const int i = (ch << 6) + lane;
+    const int l = i < n ? lens[i] : 0;
+    uint32_t rank = 0, add = 0;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+      const uint64_t b = ballot(l == k);
+      const uint32_t base = readlane(run, k);
+      if (l == k) rank = base + (uint32_t)__popcll(b & below);
+      if (lane == k) add = (uint32_t)__popcll(b);
+    }
+    run += add;
+    if (l) {
+      T.sym[L.boffs[l] + rank] = (uint16_t)i;
+      L.codes[i] = (uint16_t)(L.bfirst[l] + rank);
+    }
+  }
+  wsync<NW>();
   for (int i = lane; i < n; i += 64) {
     int l = lens[i];
     if (!l || l > PB) continue;
     uint32_t r = __brev((uint32_t)L.codes[i]) >> (32 - l);
     for (uint32_t k = r; k < (1u << PB); k += 1u << l) T.pri[k] = (uint16_t)((i << 4) | l);
   }
-  __syncthreads();
-  return L.ok;
+  wsync<NW>();
+  return ok;
 }
 
 // bits [q, q + 64) of the call's input (zero past its end)
@@ -232,10 +276,150 @@ __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// One call on a whole workgroup (the per-call path: a consume() with few
+// others in its batch).  Wave 0 runs the decoder above; inside a Huffman block
+// it hands the workgroup a region of the block's input (up to IN_CAP bytes,
+// ending 128 bits before the call's input end, where the careful path takes
+// over).  The region is cut into equal bit ranges, one per thread; thread t
+// decodes from its range start as if a symbol began there (Huffman codes
+// resynchronise within a few symbols) and ends at the first symbol boundary
+// past its range.  Thread t's start is then replaced by thread t-1's end and
+// the changed threads decode again until no start moves (a fixed point:
+// thread 0 starts on a true boundary, so by induction every start is one).
+// The threads before the first one that met an end of block or an invalid
+// code commit: a scan of their byte counts places them, a second decode
+// writes literal bytes and, for every match byte, the position it copies
+// (dist back, modulo dist inside an overlapping match, so each points before
+// its own match); pointer jumping over those resolves every byte (log of the
+// match-on-match depth rounds).  Wave 0 resumes from the first uncommitted
+// thread's start -- its end of block, its error, its input end -- exactly as
+// the one-wave decoder would have reached it.
+constexpr uint32_t IN_CAP = 32768;    // region input bytes
+constexpr uint32_t SMIN = 128;        // bits per thread at least (> a 48-bit symbol)
+constexpr uint32_t RES_CAP = 131072;  // region output bytes (the call's u32 resolve slots)
+constexpr uint32_t RES_FLAG = 0x80000000u;
+constexpr uint32_t PBIAS = 1u << 20;  // resolve slot: PBIAS + source index (may be < 0: before the region)
+constexpr uint32_t F_STOP = 1, F_BAD = 2;
+constexpr uint64_t PAR_MIN_BITS = 8 * 2048;
+constexpr uint32_t WARM = 384;        // bits decoded before a thread's range to find the true path
+
+template <int NW>
+struct ParT {
+  static constexpr int NT = 64 * NW;
+  uint64_t stg[IN_CAP / 8 + 8];       // the region's input, 8-byte words from byte b0
+  uint32_t endp[NT];                  // bit where thread t's decode ended
+  uint8_t flag[NT];                   // ... and whether at an end of block / invalid code
+  uint32_t incl[NT];                  // inclusive scan of the committed threads' byte counts
+  uint32_t lx[29], dx[30];            // (base << 4) | extra bits: length / distance symbols
+  uint32_t wsum[NW];
+  uint32_t any[2], f, f2, f3;
+  uint32_t chg[2], fm[2];             // fixed point: first thread whose start moved / that stopped
+  uint32_t cmd;                       // 0 done, 1 Huffman region, 2 stored copy
+  uint64_t q0, qlim, pos0, room, n, soff;
+  uint32_t R;
+  uint64_t qn;
+  uint64_t t_ol;                      // the tail's history update: output length, and whether to do it
+  uint32_t t_do;
+};
+template <>
+struct ParT<1> {};
+
+__device__ __forceinline__ uint32_t ld_ws(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_ws(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// bits [r, r + 64) of the staged region
+__device__ __forceinline__ uint64_t get64(const uint64_t* stg, uint32_t r) {
+  const uint32_t w = r >> 6, sh = r & 63;
+  const uint64_t lo = stg[w], hi = stg[w + 1];
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// one lane's Huffman decode (as decode(), per lane)
+template <class Tree>
+__device__ __forceinline__ uint32_t ldec(const Tree& T, uint64_t v) {
+  const uint32_t e = T.pri[v & ((1u << Tree::BITS) - 1)];
+  if (e & 15) return e;
+  int code = 0, first = 0, index = 0;
+  for (int l = 1; l < 16; l++) {
+    code |= (int)((v >> (l - 1)) & 1);
+    const int count = (int)T.cnt[l];
+    if (code - first < count) return ((uint32_t)T.sym[index + code - first] << 4) | (uint32_t)l;
+    index += count;
+    first = (first + count) << 1;
+    code <<= 1;
+  }
+  return 0;
+}
+
+// Decode from bit r while r < lim: e = the bit after the last symbol, n = the
+// bytes produced, fl = F_STOP at an end of block / invalid code (e = its
+// start), F_BAD (WRITE) at a distance past the stream's start.  WRITE: slot
+// o + i of res gets byte i (RES_FLAG | byte) or its source (PBIAS + index).
+template <bool WRITE, int NW>
+__device__ __forceinline__ void spec(const Lds& L, const ParT<NW>& P, uint32_t r, const uint32_t lim, uint32_t& e,
+                                     uint32_t& n, uint32_t& fl, uint32_t* res, uint32_t o, uint64_t pos0) {
+  n = 0;
+  fl = 0;
+  // a 64-bit buffer of the bits from r, refilled from LDS when fewer than the
+  // 48 a length/distance pair may take remain (every ~5 literals)
+  uint64_t v = 0;
+  uint32_t vb = 0;
+  while (r < lim) {
+    if (vb < 48) {
+      v = get64(P.stg, r);
+      vb = 64;
+    }
+    const uint32_t el = ldec(L.lt, v);
+    const uint32_t l1 = el & 15, sym = el >> 4;
+    if (!el) { fl = F_STOP; break; }
+    if (sym < 256) {
+      if (WRITE) st_ws(res + o + n, RES_FLAG | sym);
+      n++;
+      r += l1;
+      v >>= l1;
+      vb -= l1;
+      continue;
+    }
+    if (sym == 256 || sym > 285) { fl = F_STOP; break; }
+    const uint32_t lx = P.lx[sym - 257], xl = lx & 15;
+    const uint32_t length = (lx >> 4) + ((uint32_t)(v >> l1) & ((1u << xl) - 1));
+    const uint64_t v2 = v >> (l1 + xl);
+    const uint32_t ed = ldec(L.dt, v2);
+    const uint32_t l2 = ed & 15, dsym = ed >> 4;
+    if (!ed || dsym > 29) { fl = F_STOP; break; }
+    const uint32_t dx = P.dx[dsym], xd = dx & 15;
+    const uint32_t dist = (dx >> 4) + ((uint32_t)(v2 >> l2) & ((1u << xd) - 1));
+    if (WRITE) {
+      const uint32_t at = o + n;
+      if ((uint64_t)dist > pos0 + at) { fl = F_BAD; break; }   // too far back (inflate's "invalid distance")
+      const uint32_t sb = at + PBIAS - dist;
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < length; j++) {
+        st_ws(res + at + j, sb + k);
+        if (++k == dist) k = 0;
+      }
+    }
+    n += length;
+    const uint32_t used = l1 + xl + l2 + xd;
+    r += used;
+    v >>= used;
+    vb -= used;
+  }
+  e = r;
+}
+
+// A Huffman region: P.q0 (a symbol start, bits into the call's input) ..
+// P.qlim; output from P.pos0 (absolute), at most P.room bytes.  Every thread
+// of the workgroup calls it; results in P.R (bytes) and P.qn (next symbol).
 #ifdef XCG_ZI_TIMING
 // diagnostics build: cycles per phase, summed over calls (setup, fast literals,
 // fast matches, careful path, flushes, stored copies, tail) and symbol counts
-__device__ unsigned long long g_zi_t[10];
+__device__ unsigned long long g_zi_t[16];   // 0-8 decoder phases, 10-15 region phases
 #define ZT_NOW() __builtin_readcyclecounter()
 #define ZT_ADD(i, t0)                                                         \
   do {                                                                        \
@@ -247,13 +431,188 @@ __device__ unsigned long long g_zi_t[10];
 #define ZT_NOW() 0ull
 #define ZT_ADD(i, t0) (void)(t0)
 #endif
+#ifdef XCG_ZI_TIMING
+#define RT_ADD(i, t0)                                                         \
+  do {                                                                        \
+    uint64_t t1_ = ZT_NOW();                                                  \
+    if (threadIdx.x == 0) atomicAdd(&g_zi_t[10 + (i)], (unsigned long long)(t1_ - (t0))); \
+    t0 = t1_;                                                                 \
+  } while (0)
+#else
+#define RT_ADD(i, t0) (void)(t0)
+#endif
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi_inflate_kernel(IArgs a) {
+// region statistics (xcg_debug_zinflate_regions): regions, fixed-point
+// iterations, bytes committed, resolve rounds
+__device__ unsigned long long g_zi_reg[4];
+
+template <int NW>
+__device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, const uint8_t* hist, uint64_t total0,
+                       uint32_t* res) {
+  constexpr int NT = 64 * NW;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  uint64_t rt = ZT_NOW();
+  const uint64_t q0 = P.q0, pos0 = P.pos0;
+  const uint64_t b0 = (q0 >> 3) & ~7ull;
+  const uint32_t r0 = (uint32_t)(q0 - 8 * b0), rl = (uint32_t)(P.qlim - 8 * b0);
+  const uint32_t nwd = (rl >> 6) + 4;
+  for (uint32_t k = t; k < nwd; k += NT) P.stg[k] = *(const uint64_t*)(I + b0 + 8ull * k);
+  if (t < 29) P.lx[t] = ((uint32_t)LBASE[t] << 4) | LEXT[t];
+  if (t >= 64 && t < 94) P.dx[t - 64] = ((uint32_t)DBASE[t - 64] << 4) | DEXT[t - 64];
+  const uint32_t span = rl - r0;
+  const uint32_t nact = min((uint32_t)NT, span / SMIN);
+  const uint32_t S = span / nact;
+  if (t == 0) {
+    P.any[0] = P.any[1] = 0;
+    P.f = nact;
+    P.f2 = P.f3 = 0xffffffffu;
+  }
+  __syncthreads();
+  const bool act = (uint32_t)t < nact;
+  const uint32_t lim = (uint32_t)t + 1 == nact ? rl : r0 + ((uint32_t)t + 1) * S;
+  uint32_t s = r0 + (uint32_t)t * S, e = 0, n = 0, fl = 0;
+  RT_ADD(0, rt);
+  // Warm-up: a thread first decodes the WARM bits before its range and starts
+  // at the first symbol boundary that decode reaches inside its range.  A
+  // decode from a wrong bit usually falls onto the true symbol boundaries
+  // within ~100 bits (rarely past 500), so most threads start on the true
+  // path at once and the fixed point takes ~2 passes instead of ~8.
+  if (act && t > 0) {
+    const uint32_t ws = s - r0 > WARM ? s - WARM : r0;
+    spec<false, NW>(L, P, ws, s, e, n, fl, nullptr, 0, 0);
+    if (!fl) s = e;
+  }
+  bool dirty = act;
+  int iters = 0;
+  for (int it = 0;; it++) {   // speculative decode to the fixed point of the starts
+    iters = it + 1;
+    if (dirty) {
+      spec<false, NW>(L, P, s, lim, e, n, fl, nullptr, 0, 0);
+      P.endp[t] = e;
+      P.flag[t] = (uint8_t)fl;
+    }
+    if (t == 0) {
+      P.chg[it & 1] = NT;
+      P.fm[it & 1] = NT;
+    }
+    __syncthreads();
+    dirty = false;
+    // a thread behind a stopped one keeps its start: if the stop is real (an
+    // end of block on the true path) nothing after it commits, and if not,
+    // the stopped thread's own start moves and it reports a new end later
+    // (without this an end of block would walk one thread per iteration)
+    if (act && t > 0 && !P.flag[t - 1]) {
+      const uint32_t ns = P.endp[t - 1];
+      if (ns != s) {
+        s = ns;
+        dirty = true;
+        atomicMin(&P.chg[it & 1], (uint32_t)t);
+      }
+    }
+    if (act && P.flag[t]) atomicMin(&P.fm[it & 1], (uint32_t)t);
+    __syncthreads();
+    // done when no start moved, or when the first stopped thread lies before
+    // the first moved one (every start up to it is final; what follows it
+    // never commits)
+    if (P.chg[it & 1] >= (uint32_t)NT || P.fm[it & 1] < P.chg[it & 1]) break;
+  }
+  RT_ADD(1, rt);
+  if (t == 0) {
+    atomicAdd(&g_zi_reg[0], 1ull);
+    atomicAdd(&g_zi_reg[1], (unsigned long long)iters);
+  }
+  if (act && fl) atomicMin(&P.f, (uint32_t)t);
+  __syncthreads();
+  uint32_t f = P.f;
+  // exclusive offsets of the committed threads' bytes
+  const uint32_t v = (uint32_t)t < f ? n : 0;
+  uint32_t x = wave_incl_scan(v);
+  if (lane == 63) P.wsum[wid] = x;
+  __syncthreads();
+  for (int w = 0; w < wid; w++) x += P.wsum[w];
+  P.incl[t] = x;
+  const uint64_t cap = P.room < RES_CAP ? P.room : RES_CAP;
+  if ((uint32_t)t < f && x > cap) atomicMin(&P.f2, (uint32_t)t);
+  __syncthreads();
+  f = min(f, P.f2);
+  RT_ADD(2, rt);
+  if ((uint32_t)t < f) {
+    uint32_t e2, n2, fl2;
+    spec<true, NW>(L, P, s, lim, e2, n2, fl2, res, x - v, pos0);
+    if (fl2 & F_BAD) atomicMin(&P.f3, (uint32_t)t);
+  }
+  __syncthreads();
+  f = min(f, P.f3);
+  RT_ADD(3, rt);
+  const uint32_t R = f ? P.incl[f - 1] : 0;
+  const uint32_t qn = f ? P.endp[f - 1] : r0;
+  // resolve: every slot to its byte (pointer jumping; sources lie before the slot)
+  for (int it = 0;; it++) {
+    if (t == 0) P.any[it & 1] = 0;
+    __syncthreads();
+    bool more = false;
+    for (uint32_t i = t; i < R; i += NT) {
+      const uint32_t y = ld_ws(res + i);
+      if (y & RES_FLAG) continue;
+      const int32_t src = (int32_t)(y - PBIAS);
+      uint32_t w;
+      if (src < 0) {
+        const uint64_t ab = pos0 - (uint64_t)(-(int64_t)src);
+        w = RES_FLAG | (ab >= total0 ? out[ab - total0] : hist[WSIZE - (total0 - ab)]);
+      } else {
+        w = ld_ws(res + src);
+        more |= !(w & RES_FLAG);
+      }
+      st_ws(res + i, w);
+    }
+    if (more) P.any[it & 1] = 1;
+    __syncthreads();
+    if (t == 0) atomicAdd(&g_zi_reg[3], 1ull);
+    if (!P.any[it & 1]) break;
+  }
+  RT_ADD(4, rt);
+  if (t == 0) atomicAdd(&g_zi_reg[2], (unsigned long long)R);
+  const uint64_t pos1 = pos0 + R;
+  uint8_t* o = out + (pos0 - total0);
+  for (uint32_t i = t; i < R; i += NT) o[i] = (uint8_t)ld_ws(res + i);
+  const uint64_t lo = pos1 - pos0 > RMASK + 1 ? pos1 - (RMASK + 1) : pos0;
+  for (uint64_t p = lo + t; p < pos1; p += NT) L.ring[p & RMASK] = (uint8_t)ld_ws(res + (p - pos0));
+  if (t == 0) {
+    P.R = R;
+    P.qn = 8 * b0 + qn;
+  }
+  __threadfence();   // the region's bytes are read back by later far matches
+  __syncthreads();
+  RT_ADD(5, rt);
+}
+
+// A stored block's bytes straight to the output, the last 4 KiB also into the ring.
+template <int NW>
+__device__ void stored_copy(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, uint64_t total0) {
+  constexpr int NT = 64 * NW;
+  const int t = threadIdx.x;
+  const uint64_t n = P.n, pos = P.pos0;
+  const uint8_t* src = I + P.soff;
+  uint8_t* dst = out + (pos - total0);
+  for (uint64_t i = t; i < n; i += NT) dst[i] = src[i];
+  const uint64_t keep = n < (uint64_t)(RMASK + 1) ? n : (uint64_t)(RMASK + 1);
+  for (uint64_t i = t; i < keep; i += NT) L.ring[(pos + n - keep + i) & RMASK] = src[n - keep + i];
+  __threadfence();
+  __syncthreads();
+}
+
+
+// NW = 1: one wave per call (batches of many streams).  NW > 1: one workgroup
+// per call, wave 0 decoding, the workgroup on Huffman regions and stored
+// copies (region(), stored_copy()) -- the per-call path.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void zi_inflate_kernel(IArgs a) {
 #ifdef XCG_ZI_TIMING
   uint64_t zt[10] = {0};
 #endif
   uint64_t tz = ZT_NOW();
   __shared__ Lds L;
+  __shared__ ParT<NW> P;
   const uint32_t ci = blockIdx.x;
   const ICall c = a.calls[ci];
   const int lane = threadIdx.x;
@@ -265,24 +624,49 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
   const uint64_t qend = 8ull * (npend + c.len);
   uint64_t q = sp->pend_bit;
   Reader R{a.I + c.i_off, 0, 0};
+  const uint8_t* hist = a.hist + (uint64_t)c.stream * WSIZE;
+  uint64_t pos = total0, flushed = total0;
+  int32_t status = 0;
+  uint32_t trailer = 0, have_trailer = 0;
+  uint8_t* out = a.out + c.out_off;
+  uint32_t* res = NW > 1 ? a.pres + (uint64_t)ci * RES_CAP : nullptr;
+  bool do_hist = false;
+  uint64_t ol = 0;
+  if (NW > 1 && threadIdx.x >= 64) {   // helper waves: regions and copies until wave 0 is done
+    if constexpr (NW > 1) {
+      for (;;) {
+        __syncthreads();
+        const uint32_t cmd = P.cmd;
+        if (cmd == 0) break;
+        if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res);
+        else stored_copy<NW>(L, P, R.I, out, total0);
+      }
+    }
+  } else {
   R.load(0);
   // history -> ring
-  const uint8_t* hist = a.hist + (uint64_t)c.stream * WSIZE;
   const uint64_t hn = total0 < (uint64_t)(RMASK + 1) ? total0 : (uint64_t)(RMASK + 1);
   for (uint64_t i = lane; i < hn; i += 64) {
     uint64_t pos = total0 - hn + i;
     L.ring[pos & RMASK] = hist[WSIZE - hn + i];
   }
-  uint64_t pos = total0, flushed = total0;
-  int32_t status = 0;
-  uint32_t trailer = 0, have_trailer = 0;
-  uint8_t* out = a.out + c.out_off;
   auto flush = [&]() {
-    __syncthreads();
+    wsync<NW>();
     for (uint64_t p = flushed + lane; p < pos; p += 64) out[p - total0] = L.ring[p & RMASK];
     flushed = pos;
     __threadfence();   // the flushed bytes are read back by far matches
   };
+  // the workgroup's turn (NW > 1): P's parameters set by lane 0, then every
+  // wave runs the command
+  auto help = [&](uint32_t cmd) {
+    if constexpr (NW > 1) {
+      if (lane == 0) P.cmd = cmd;
+      __syncthreads();
+      if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res);
+      else stored_copy<NW>(L, P, R.I, out, total0);
+    }
+  };
+  bool par_ok = true;   // a region may help in this Huffman block
   // a match of `length` bytes from `dist` back, at pos
   auto copy_match = [&](uint32_t dist, uint32_t length) {
     if (dist >= length && dist <= NEAR) {
@@ -305,24 +689,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
   auto tables_for_block = [&]() -> bool {   // (re)build the block's trees
     if (btype == 1) {
       for (int i = lane; i < 288; i += 64) L.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-      __syncthreads();
-      build(L, L.lt, L.lens, 288);
+      wsync<NW>();
+      build<NW>(L, L.lt, L.lens, 288);
       for (int i = lane; i < 30; i += 64) L.lens[i] = 5;
-      __syncthreads();
-      build(L, L.dt, L.lens, 30);
+      wsync<NW>();
+      build<NW>(L, L.dt, L.lens, 30);
       return true;
     }
-    bool ok = build(L, L.lt, L.dlens, nlen);
-    ok = build(L, L.dt, L.dlens + nlen, ndist) && ok;
+    bool ok = build<NW>(L, L.lt, L.dlens, nlen);
+    ok = build<NW>(L, L.dt, L.dlens + nlen, ndist) && ok;
     return ok;
   };
   ZT_ADD(0, tz);
   if (mode == M_HUFF) {   // resume inside a block: rebuild its trees
     for (int i = lane; i < 320; i += 64) L.dlens[i] = sp->lens[i];
-    __syncthreads();
+    wsync<NW>();
     if (!tables_for_block()) mode = M_ERROR;
   }
-  __syncthreads();
+  wsync<NW>();
   bool stall = false;
   while (!stall && mode != M_ERROR && mode != M_DONE) {
     if (mode == M_HEADER) {   // zlib header: CMF FLG (RFC 1950)
@@ -333,6 +717,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       q += 16;
       mode = M_BLOCK;
     } else if (mode == M_BLOCK) {
+      ZT_ADD(3, tz);
       const uint64_t q0 = q;
       if (q + 3 > qend) { stall = true; break; }
       uint64_t v = R.get(q);
@@ -351,6 +736,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       } else if (btype == 1) {
         tables_for_block();
         mode = M_HUFF;
+        par_ok = true;
       } else if (btype == 2) {
         if (q + 14 > qend) { q = q0; stall = true; break; }
         v = R.get(q);
@@ -361,14 +747,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
         if (nlen > 286 || ndist > 30) { mode = M_ERROR; break; }
         if (q + 3 * ncl > qend) { q = q0; stall = true; break; }
         if (lane < 19) L.lens[lane] = 0;
-        __syncthreads();
+        wsync<NW>();
         for (uint32_t i = 0; i < ncl; i++) {
           uint32_t l = (R.get(q) & 7);
           if (lane == 0) L.lens[CL_ORDER[i]] = (uint8_t)l;
           q += 3;
         }
-        __syncthreads();
-        if (!build(L, L.ct, L.lens, 19)) { mode = M_ERROR; break; }
+        wsync<NW>();
+        if (!build<NW>(L, L.ct, L.lens, 19)) { mode = M_ERROR; break; }
         // the literal/length and distance code lengths, with repeats
         uint32_t n = 0;
         bool bad = false;
@@ -389,7 +775,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
           uint32_t x = (uint32_t)(b >> cl) & ((1u << xb) - 1);
           if (sym == 16) {
             if (n == 0) { bad = true; break; }
-            __syncthreads();
+            wsync<NW>();
             val = L.dlens[n - 1];
             rep = 3 + x;
           } else rep = (sym == 17 ? 3 : 11) + x;
@@ -400,9 +786,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
         }
         if (bad) { mode = M_ERROR; break; }
         if (stall) { q = q0; break; }
-        __syncthreads();
+        wsync<NW>();
         if (L.dlens[256] == 0 || !tables_for_block()) { mode = M_ERROR; break; }
         mode = M_HUFF;   // (its lengths reach sp->lens only when the call commits)
+        par_ok = true;
+        ZT_ADD(7, tz);
       } else {
         mode = M_ERROR;
         break;
@@ -414,15 +802,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       // straight to the output (HBM), the ring's earlier bytes flushed first;
       // then the last 8 KiB also into the ring for later near matches
       flush();
-      const uint8_t* src = R.I + (q >> 3);
-      uint8_t* dst = out + (pos - total0);
-      for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
-      const uint64_t keep = n < (uint64_t)(RMASK + 1) ? n : (uint64_t)(RMASK + 1);
-      for (uint64_t i = lane; i < keep; i += 64) L.ring[(pos + n - keep + i) & RMASK] = src[n - keep + i];
+      if constexpr (NW > 1) {
+        if (lane == 0) {
+          P.n = n;
+          P.pos0 = pos;
+          P.soff = q >> 3;
+        }
+        help(2);
+      } else {
+        const uint8_t* src = R.I + (q >> 3);
+        uint8_t* dst = out + (pos - total0);
+        for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+        const uint64_t keep = n < (uint64_t)(RMASK + 1) ? n : (uint64_t)(RMASK + 1);
+        for (uint64_t i = lane; i < keep; i += 64) L.ring[(pos + n - keep + i) & RMASK] = src[n - keep + i];
+      }
       pos += n;
       flushed = pos;
       __threadfence();   // readable by far matches
-      __syncthreads();
+      wsync<NW>();
       q += 8 * n;
       ZT_ADD(5, tz);
       stored_left -= (uint32_t)n;
@@ -431,6 +828,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       R.load(q >> 3);
     } else if (mode == M_HUFF) {
       for (;;) {
+        if constexpr (NW > 1) {   // the workgroup on the block's middle
+          const uint64_t qlim = qend > 128 ? qend - 128 : 0;
+          if (par_ok && q + PAR_MIN_BITS <= qlim && pos - total0 < c.out_cap) {
+            ZT_ADD(3, tz);
+            flush();
+            if (lane == 0) {
+              P.q0 = q;
+              P.qlim = qlim - q > 8ull * IN_CAP ? q + 8ull * IN_CAP : qlim;
+              P.pos0 = pos;
+              P.room = c.out_cap - (pos - total0);
+            }
+            help(1);
+            const uint32_t rn = su(P.R);
+            const uint64_t qn = ((uint64_t)su((uint32_t)(P.qn >> 32)) << 32) | su((uint32_t)P.qn);
+            ZT_ADD(8, tz);
+            if (!rn) par_ok = false;   // the block ends (or fails) within a thread's range: the careful path
+            pos += rn;
+            flushed = pos;
+            q = qn;
+            R.load(q >> 3);
+            continue;
+          }
+        }
         // fast path (as zlib's inflate_fast): while 128 input bits, 516 bytes of
         // output room and the ring before its next flush are guaranteed, decode
         // without per-field checks; literals straight from a 64-bit bit buffer
@@ -513,9 +933,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
         uint32_t dist = DBASE[dsym] + ((uint32_t)(vd >> l2) & ((1u << xd) - 1));
         if (dist > pos || dist > (uint32_t)WSIZE) { mode = M_ERROR; break; }   // too far back
         if (pos + length - total0 > c.out_cap) { status = -2; break; }
-        __syncthreads();
+        wsync<NW>();
         copy_match(dist, length);
-        __syncthreads();
+        wsync<NW>();
         pos += length;
         q = qd + l2 + xd;
       }
@@ -537,7 +957,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
   if (status == 0 && mode == M_DONE && q < qend && c.len) status = -1;
   if (status == 0 && mode == M_DONE) status = 1;
   flush();
-  __syncthreads();
+  wsync<NW>();
   if (status == -1 && lane == 0) sp->mode = M_ERROR;   // InflatePipe::produce_error: the pipe is done
   if (status >= 0) {
     // the carried input for the next call
@@ -554,22 +974,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       // resumes in is then still the one sp->lens describes.
       if (mode == M_HUFF && btype == 2)
         for (uint32_t i = lane; i < nlen + ndist; i += 64) sp->lens[i] = L.dlens[i];
-      // history = the last 32 KiB of output: the old history moved down by this
-      // call's output length (ascending, so no lane reads what another wrote),
-      // then the output itself (flushed and fenced above)
-      const uint64_t ol = pos - total0;
-      uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
-      if (ol < (uint64_t)WSIZE) {
-        for (uint64_t i0 = 0; ol && i0 < WSIZE - ol; i0 += 64) {
-          const uint64_t i = i0 + lane;
-          const uint8_t b = i < WSIZE - ol ? h[i + ol] : 0;
-          __syncthreads();
-          if (i < WSIZE - ol) h[i] = b;
-        }
-        for (uint64_t i = lane; i < ol; i += 64) h[WSIZE - ol + i] = out[i];
-      } else {
-        for (uint64_t i = lane; i < (uint64_t)WSIZE; i += 64) h[i] = out[ol - WSIZE + i];
-      }
+      do_hist = true;
+      ol = pos - total0;
       if (lane == 0) {
         sp->total_out = pos;
         sp->mode = mode;
@@ -583,10 +989,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zi
       }
     }
   }
+  if constexpr (NW > 1) {   // release the helper waves for the history update
+    if (lane == 0) {
+      P.t_do = do_hist;
+      P.t_ol = ol;
+      P.cmd = 0;
+    }
+    __syncthreads();
+  }
+  }   // wave 0 (every wave when NW == 1)
+  // history = the last 32 KiB of output: the old history moved down by this
+  // call's output length, then the output itself (flushed and fenced above)
+  {
+    constexpr int NT = 64 * NW;
+    const int t = threadIdx.x;
+    if constexpr (NW > 1) {
+      do_hist = P.t_do;
+      ol = P.t_ol;
+    }
+    uint8_t* h = a.hist + (uint64_t)c.stream * WSIZE;
+    if (do_hist) {
+      if (ol < (uint64_t)WSIZE) {
+        constexpr int PER = NW > 1 ? WSIZE / NT : 16;   // bytes per thread and pass: read, then write
+        for (uint64_t i0 = 0; ol && i0 < WSIZE - ol; i0 += (uint64_t)NT * PER) {
+          uint8_t b[PER];
+#pragma unroll
+          for (int k = 0; k < PER; k++) {
+            const uint64_t i = i0 + (uint64_t)k * NT + t;
+            b[k] = i < WSIZE - ol ? h[i + ol] : 0;
+          }
+          __syncthreads();
+#pragma unroll
+          for (int k = 0; k < PER; k++) {
+            const uint64_t i = i0 + (uint64_t)k * NT + t;
+            if (i < WSIZE - ol) h[i] = b[k];
+          }
+        }
+        for (uint64_t i = t; i < ol; i += NT) h[WSIZE - ol + i] = out[i];
+      } else {
+        for (uint64_t i = t; i < (uint64_t)WSIZE; i += NT) h[i] = out[ol - WSIZE + i];
+      }
+    }
+  }
   ZT_ADD(6, tz);
 #ifdef XCG_ZI_TIMING
   if (lane == 0)
-    for (int i = 0; i < 7; i++) atomicAdd(&g_zi_t[i], (unsigned long long)zt[i]);
+    for (int i = 0; i < 10; i++) atomicAdd(&g_zi_t[i], (unsigned long long)zt[i]);
 #endif
   if (lane == 0) {
     IRes r;
@@ -712,6 +1160,8 @@ int igrow(void** p, size_t* cap, size_t want, bool pinned) {
   return XCG_OK;
 }
 inline size_t ial(size_t v, size_t a) { return (v + a - 1) / a * a; }
+int g_zi_par = 0;                    // 0: by batch size, 1: a wave per call, 2: a workgroup per call
+constexpr uint32_t ZI_PAR_CALLS = 256;
 }  // namespace
 
 extern "C" {
@@ -780,7 +1230,11 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
     io += ial((size_t)PEND_CAP + c.len + IPAD, 256);
     maxlen = std::max(maxlen, c.len);
   }
-  size_t o_I = 0, o_res = ial(io, 256), o_end = ial(o_res + sizeof(IRes) * n, 256);
+  // few calls: a workgroup per call (zi_inflate_kernel<16>) with RES_CAP
+  // resolve slots each; many: a wave per call
+  const bool par = g_zi_par == 2 || (g_zi_par == 0 && n <= ZI_PAR_CALLS);
+  size_t o_I = 0, o_res = ial(io, 256), o_pres = ial(o_res + sizeof(IRes) * n, 256),
+         o_end = par ? o_pres + 4ull * RES_CAP * n : o_pres;
   if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
   if (igrow((void**)&z->scratch, &z->scratch_cap, o_end, false)) return XCG_ENOMEM;
   size_t m_end = ial(sizeof(ICall) * n, 256);
@@ -797,9 +1251,11 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.res = (IRes*)(z->scratch + o_res);
   a.out_len = d_out_len;
   a.status = d_status;
+  a.pres = par ? (uint32_t*)(z->scratch + o_pres) : nullptr;
   uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 4095) / 4096);   // 4 KiB per block
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(zi_inflate_kernel, dim3(n), dim3(64), 0, st, a);
+  if (par) hipLaunchKernelGGL(zi_inflate_kernel<16>, dim3(n), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL(zi_inflate_kernel<1>, dim3(n), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
@@ -862,10 +1318,22 @@ int xcg_zinflate_host(xcg_zinflate* z, const uint8_t* h_in, const uint64_t* h_in
   return XCG_OK;
 }
 
+int xcg_debug_zinflate_regions(uint64_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zi_reg), 8 * 4) != hipSuccess) return XCG_EHIP;
+  uint64_t z[4] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_zi_reg), z, sizeof z) == hipSuccess ? XCG_OK : XCG_EHIP;
+}
+
+int xcg_debug_set_zinflate_mode(int mode) {
+  if (mode < 0 || mode > 2) return XCG_EINVAL;
+  g_zi_par = mode;
+  return XCG_OK;
+}
+
 #ifdef XCG_ZI_TIMING
 int xcg_debug_zi_times(uint64_t* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zi_t), 8 * 10) != hipSuccess) return XCG_EHIP;
-  uint64_t z[10] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zi_t), 8 * 16) != hipSuccess) return XCG_EHIP;
+  uint64_t z[16] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_zi_t), z, sizeof z) == hipSuccess ? XCG_OK : XCG_EHIP;
 }
 #endif

@@ -55,8 +55,16 @@ def _lib():
         L.xcg_zinflate_reset.restype = C.c_int
         L.xcg_zinflate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.xcg_zinflate_batch.restype = C.c_int
+        L.xcg_debug_set_zinflate_mode.argtypes = [C.c_int]
+        L.xcg_debug_set_zinflate_mode.restype = C.c_int
         L._zd_bound = True
     return L
+
+
+def set_inflate_mode(mode: int) -> None:
+    """Which inflate kernel runs (xcg_debug_set_zinflate_mode): 0 by batch
+    size, 1 a wave per call, 2 a workgroup per call."""
+    _check(_lib().xcg_debug_set_zinflate_mode(mode))
 
 
 def bound(n: int) -> int:
