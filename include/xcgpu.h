@@ -504,7 +504,7 @@ int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in
                       const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
                       const uint32_t *h_out_cap, uint32_t *h_out_len, int32_t *h_status);
 /* Tests / A-B: which inflate kernel runs -- 0 by batch size (a workgroup per
- * call up to 256 calls, a wave per call beyond), 1 always a wave per call,
+ * call up to 4096 calls, a wave per call beyond), 1 always a wave per call,
  * 2 always a workgroup per call. */
 int xcg_debug_set_zinflate_mode(int mode);
 /* Workgroup-kernel regions since the last call (then reset): regions,

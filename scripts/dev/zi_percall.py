@@ -44,7 +44,7 @@ def main():
         ok = b''.join(out) == b''.join(data)
         if timing:
             L.xcg_debug_zi_times(zt.ctypes.data)
-            names = ['setup', 'fastlit', 'fastmatch', 'careful', 'flush', 'stored', 'tail', 'header', 'region']
+            names = ['setup', 'fastlit', 'fastmatch', 'careful', 'flush', 'stored', 'tail', 'header', 'region', 'cl_loop']
             print(f'mode {mode} cycles per call:', {n: int(zt[i]) // len(zs) for i, n in enumerate(names)})
             rn = ['stage', 'fixpoint', 'scan', 'write', 'resolve', 'out']
             print(f'mode {mode} region cycles per call:', {n: int(zt[10 + i]) // len(zs) for i, n in enumerate(rn)})

@@ -297,21 +297,25 @@ __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
 // the one-wave decoder would have reached it.
 constexpr uint32_t IN_CAP = 32768;    // region input bytes
 constexpr uint32_t SMIN = 128;        // bits per thread at least (> a 48-bit symbol)
-constexpr uint32_t RES_CAP = 131072;  // region output bytes (the call's u32 resolve slots)
+constexpr uint32_t RES_CAP = 65536;   // region output bytes (the call's u32 resolve slots: 256 KiB)
 constexpr uint32_t RES_FLAG = 0x80000000u;
 constexpr uint32_t PBIAS = 1u << 20;  // resolve slot: PBIAS + source index (may be < 0: before the region)
 constexpr uint32_t F_STOP = 1, F_BAD = 2;
 constexpr uint64_t PAR_MIN_BITS = 8 * 2048;
-constexpr uint32_t WARM = 384;        // bits decoded before a thread's range to find the true path
+constexpr uint32_t WARM = 128;        // bits decoded before a thread's range to find the true path
 
 template <int NW>
 struct ParT {
   static constexpr int NT = 64 * NW;
   uint64_t stg[IN_CAP / 8 + 8];       // the region's input, 8-byte words from byte b0
+  uint32_t st[NT], nst[NT];           // thread t's start, and the one it moves to
   uint32_t endp[NT];                  // bit where thread t's decode ended
+  uint32_t cnt[NT];                   // ... the bytes it produced
+  uint16_t list[NT];                  // threads whose start moves in this pass
+  uint32_t nd;
   uint8_t flag[NT];                   // ... and whether at an end of block / invalid code
   uint32_t incl[NT];                  // inclusive scan of the committed threads' byte counts
-  uint32_t lx[29], dx[30];            // (base << 4) | extra bits: length / distance symbols
+  uint32_t flt[1 << 10], fdt[1 << PRI];   // the block's primary tables as lfast / dfast entries
   uint32_t wsum[NW];
   uint32_t any[2], f, f2, f3;
   uint32_t chg[2], fm[2];             // fixed point: first thread whose start moved / that stopped
@@ -356,6 +360,24 @@ __device__ __forceinline__ uint32_t ldec(const Tree& T, uint64_t v) {
   return 0;
 }
 
+// Region tables (ParT::flt / fdt), 32 bits per primary entry: code length in
+// bits 0-3 (0: a longer code), FT_STOP for an end of block / invalid symbol,
+// FT_MATCH for a length.  Literal: byte in bits 8-15; length: base in bits
+// 8-16, extra bits in 20-23; distance: base in bits 8-23, extra bits in 24-27.
+constexpr uint32_t FT_MATCH = 16, FT_STOP = 32;
+__device__ __forceinline__ uint32_t lfast(uint32_t e) {   // e: (sym << 4) | len, 0: no code
+  const uint32_t len = e & 15, sym = e >> 4;
+  if (!e) return FT_STOP | 1;
+  if (sym < 256) return len | (sym << 8);
+  if (sym == 256 || sym > 285) return len | FT_STOP;
+  return len | FT_MATCH | ((uint32_t)LBASE[sym - 257] << 8) | ((uint32_t)LEXT[sym - 257] << 20);
+}
+__device__ __forceinline__ uint32_t dfast(uint32_t e) {
+  const uint32_t len = e & 15, sym = e >> 4;
+  if (!e || sym > 29) return FT_STOP | 1;
+  return len | ((uint32_t)DBASE[sym] << 8) | ((uint32_t)DEXT[sym] << 24);
+}
+
 // Decode from bit r while r < lim: e = the bit after the last symbol, n = the
 // bytes produced, fl = F_STOP at an end of block / invalid code (e = its
 // start), F_BAD (WRITE) at a distance past the stream's start.  WRITE: slot
@@ -374,26 +396,29 @@ __device__ __forceinline__ void spec(const Lds& L, const ParT<NW>& P, uint32_t r
       v = get64(P.stg, r);
       vb = 64;
     }
-    const uint32_t el = ldec(L.lt, v);
-    const uint32_t l1 = el & 15, sym = el >> 4;
-    if (!el) { fl = F_STOP; break; }
-    if (sym < 256) {
-      if (WRITE) st_ws(res + o + n, RES_FLAG | sym);
+    // the region's 32-bit tables: one lookup gives a literal, or a length's
+    // base and extra bits (a distance likewise); codes past the primary bits
+    // go the canonical way
+    uint32_t fe = P.flt[v & ((1u << LTree::BITS) - 1)];
+    if (!(fe & 15)) fe = lfast(ldec(L.lt, v));
+    const uint32_t l1 = fe & 15;
+    if (!(fe & (FT_MATCH | FT_STOP))) {
+      if (WRITE) st_ws(res + o + n, RES_FLAG | ((fe >> 8) & 255));
       n++;
       r += l1;
       v >>= l1;
       vb -= l1;
       continue;
     }
-    if (sym == 256 || sym > 285) { fl = F_STOP; break; }
-    const uint32_t lx = P.lx[sym - 257], xl = lx & 15;
-    const uint32_t length = (lx >> 4) + ((uint32_t)(v >> l1) & ((1u << xl) - 1));
+    if (fe & FT_STOP) { fl = F_STOP; break; }
+    const uint32_t xl = (fe >> 20) & 15;
+    const uint32_t length = ((fe >> 8) & 511) + ((uint32_t)(v >> l1) & ((1u << xl) - 1));
     const uint64_t v2 = v >> (l1 + xl);
-    const uint32_t ed = ldec(L.dt, v2);
-    const uint32_t l2 = ed & 15, dsym = ed >> 4;
-    if (!ed || dsym > 29) { fl = F_STOP; break; }
-    const uint32_t dx = P.dx[dsym], xd = dx & 15;
-    const uint32_t dist = (dx >> 4) + ((uint32_t)(v2 >> l2) & ((1u << xd) - 1));
+    uint32_t fd = P.fdt[v2 & ((1u << DTree::BITS) - 1)];
+    if (!(fd & 15)) fd = dfast(ldec(L.dt, v2));
+    if (fd & FT_STOP) { fl = F_STOP; break; }
+    const uint32_t l2 = fd & 15, xd = (fd >> 24) & 15;
+    const uint32_t dist = ((fd >> 8) & 0xffff) + ((uint32_t)(v2 >> l2) & ((1u << xd) - 1));
     if (WRITE) {
       const uint32_t at = o + n;
       if ((uint64_t)dist > pos0 + at) { fl = F_BAD; break; }   // too far back (inflate's "invalid distance")
@@ -457,8 +482,14 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
   const uint32_t r0 = (uint32_t)(q0 - 8 * b0), rl = (uint32_t)(P.qlim - 8 * b0);
   const uint32_t nwd = (rl >> 6) + 4;
   for (uint32_t k = t; k < nwd; k += NT) P.stg[k] = *(const uint64_t*)(I + b0 + 8ull * k);
-  if (t < 29) P.lx[t] = ((uint32_t)LBASE[t] << 4) | LEXT[t];
-  if (t >= 64 && t < 94) P.dx[t - 64] = ((uint32_t)DBASE[t - 64] << 4) | DEXT[t - 64];
+  for (int i = t; i < (1 << LTree::BITS); i += NT) {
+    const uint32_t e = L.lt.pri[i];
+    P.flt[i] = (e & 15) ? lfast(e) : 0;
+  }
+  for (int i = t; i < (1 << DTree::BITS); i += NT) {
+    const uint32_t e = L.dt.pri[i];
+    P.fdt[i] = (e & 15) ? dfast(e) : 0;
+  }
   const uint32_t span = rl - r0;
   const uint32_t nact = min((uint32_t)NT, span / SMIN);
   const uint32_t S = span / nact;
@@ -475,37 +506,40 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
   // Warm-up: a thread first decodes the WARM bits before its range and starts
   // at the first symbol boundary that decode reaches inside its range.  A
   // decode from a wrong bit usually falls onto the true symbol boundaries
-  // within ~100 bits (rarely past 500), so most threads start on the true
-  // path at once and the fixed point takes ~2 passes instead of ~8.
-  if (act && t > 0) {
-    const uint32_t ws = s - r0 > WARM ? s - WARM : r0;
-    spec<false, NW>(L, P, ws, s, e, n, fl, nullptr, 0, 0);
-    if (!fl) s = e;
-  }
-  bool dirty = act;
-  int iters = 0;
-  for (int it = 0;; it++) {   // speculative decode to the fixed point of the starts
-    iters = it + 1;
-    if (dirty) {
-      spec<false, NW>(L, P, s, lim, e, n, fl, nullptr, 0, 0);
-      P.endp[t] = e;
-      P.flag[t] = (uint8_t)fl;
+  // within ~100 bits, so most threads start on the true path at once.
+  if (act) {
+    if (t > 0) {
+      const uint32_t ws = s - r0 > WARM ? s - WARM : r0;
+      spec<false, NW>(L, P, ws, s, e, n, fl, nullptr, 0, 0);
+      if (!fl) s = e;
     }
+    spec<false, NW>(L, P, s, lim, e, n, fl, nullptr, 0, 0);
+    P.st[t] = s;
+    P.endp[t] = e;
+    P.cnt[t] = n;
+    P.flag[t] = (uint8_t)fl;
+  }
+  // Fixed point of the starts: a thread whose predecessor's end differs from
+  // its start decodes again from that end.  The (few) threads that move are
+  // listed and re-decoded by the first threads of the workgroup, so a pass
+  // costs the waves it needs, not all sixteen.
+  int iters = 1;
+  for (int it = 0;; it++) {
     if (t == 0) {
+      P.nd = 0;
       P.chg[it & 1] = NT;
       P.fm[it & 1] = NT;
     }
     __syncthreads();
-    dirty = false;
     // a thread behind a stopped one keeps its start: if the stop is real (an
     // end of block on the true path) nothing after it commits, and if not,
     // the stopped thread's own start moves and it reports a new end later
-    // (without this an end of block would walk one thread per iteration)
+    // (without this an end of block would walk one thread per pass)
     if (act && t > 0 && !P.flag[t - 1]) {
       const uint32_t ns = P.endp[t - 1];
-      if (ns != s) {
-        s = ns;
-        dirty = true;
+      if (ns != P.st[t]) {
+        P.nst[t] = ns;
+        P.list[atomicAdd(&P.nd, 1u)] = (uint16_t)t;
         atomicMin(&P.chg[it & 1], (uint32_t)t);
       }
     }
@@ -514,16 +548,32 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
     // done when no start moved, or when the first stopped thread lies before
     // the first moved one (every start up to it is final; what follows it
     // never commits)
-    if (P.chg[it & 1] >= (uint32_t)NT || P.fm[it & 1] < P.chg[it & 1]) break;
+    const uint32_t chg = P.chg[it & 1], fm = P.fm[it & 1];
+    if (chg >= (uint32_t)NT || fm < chg) break;
+    iters++;
+    const uint32_t nd = P.nd;
+    for (uint32_t k = t; k < nd; k += NT) {
+      const uint32_t u = P.list[k];
+      const uint32_t su0 = P.nst[u], lu = u + 1 == nact ? rl : r0 + (u + 1) * S;
+      uint32_t eu, nu, fu;
+      spec<false, NW>(L, P, su0, lu, eu, nu, fu, nullptr, 0, 0);
+      P.st[u] = su0;
+      P.endp[u] = eu;
+      P.cnt[u] = nu;
+      P.flag[u] = (uint8_t)fu;
+    }
+    __syncthreads();
   }
   RT_ADD(1, rt);
   if (t == 0) {
     atomicAdd(&g_zi_reg[0], 1ull);
     atomicAdd(&g_zi_reg[1], (unsigned long long)iters);
   }
-  if (act && fl) atomicMin(&P.f, (uint32_t)t);
-  __syncthreads();
-  uint32_t f = P.f;
+  uint32_t f = min(P.fm[(iters - 1) & 1], nact);
+  if (act) {
+    s = P.st[t];
+    n = P.cnt[t];
+  }
   // exclusive offsets of the committed threads' bytes
   const uint32_t v = (uint32_t)t < f ? n : 0;
   uint32_t x = wave_incl_scan(v);
@@ -594,7 +644,10 @@ __device__ void stored_copy(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out,
   const uint64_t n = P.n, pos = P.pos0;
   const uint8_t* src = I + P.soff;
   uint8_t* dst = out + (pos - total0);
-  for (uint64_t i = t; i < n; i += NT) dst[i] = src[i];
+  // 16 bytes per thread and step (unaligned vector access), the tail bytewise
+  const uint64_t nv = n / 16;
+  for (uint64_t i = t; i < nv; i += NT) *(u32x4_u*)(dst + 16 * i) = *(const u32x4_u*)(src + 16 * i);
+  for (uint64_t i = 16 * nv + t; i < n; i += NT) dst[i] = src[i];
   const uint64_t keep = n < (uint64_t)(RMASK + 1) ? n : (uint64_t)(RMASK + 1);
   for (uint64_t i = t; i < keep; i += NT) L.ring[(pos + n - keep + i) & RMASK] = src[n - keep + i];
   __threadfence();
@@ -748,25 +801,41 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (q + 3 * ncl > qend) { q = q0; stall = true; break; }
         if (lane < 19) L.lens[lane] = 0;
         wsync<NW>();
-        for (uint32_t i = 0; i < ncl; i++) {
-          uint32_t l = (R.get(q) & 7);
-          if (lane == 0) L.lens[CL_ORDER[i]] = (uint8_t)l;
-          q += 3;
+        {   // 3 bits per code-length code length, all 19 within one 64-bit read
+          const uint64_t cv = R.get(q);
+          if (lane < (int)ncl) L.lens[CL_ORDER[lane]] = (uint8_t)((cv >> (3 * lane)) & 7);
+          q += 3 * ncl;
         }
         wsync<NW>();
         if (!build<NW>(L, L.ct, L.lens, 19)) { mode = M_ERROR; break; }
-        // the literal/length and distance code lengths, with repeats
-        uint32_t n = 0;
+        // the code-length code's 128-entry table (codes of at most 7 bits: no
+        // canonical path) in one register, two entries per lane, read with
+        // v_readlane instead of an LDS round trip per symbol
+        const uint32_t ctw = ((uint32_t)L.ct.pri[2 * lane + 1] << 16) | L.ct.pri[2 * lane];
+        ZT_ADD(7, tz);
+        // the literal/length and distance code lengths, with repeats; the bits
+        // come from a 64-bit buffer refilled when fewer than a code (7) and
+        // its extra bits (7) remain
+        uint32_t n = 0, prev = 0;
         bool bad = false;
+        uint64_t b = 0;
+        uint32_t bb = 0;
         while (n < nlen + ndist) {
           if (q >= qend) { stall = true; break; }
-          uint64_t b = R.get(q);
-          uint32_t e = decode(L.ct, b);
+          if (bb < 14) {
+            b = R.get(q);
+            bb = 64;
+          }
+          const uint32_t ci = (uint32_t)b & 127;
+          const uint32_t e = (readlane(ctw, (int)(ci >> 1)) >> (16 * (ci & 1))) & 0xffff;
           uint32_t cl = e & 15, sym = e >> 4;
           if (!e || q + cl > qend) { if (!e) bad = true; else stall = true; break; }
           if (sym < 16) {
             q += cl;
+            b >>= cl;
+            bb -= cl;
             if (lane == 0) L.dlens[n] = (uint8_t)sym;
+            prev = sym;
             n++;
             continue;
           }
@@ -775,15 +844,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
           uint32_t x = (uint32_t)(b >> cl) & ((1u << xb) - 1);
           if (sym == 16) {
             if (n == 0) { bad = true; break; }
-            wsync<NW>();
-            val = L.dlens[n - 1];
+            val = prev;
             rep = 3 + x;
           } else rep = (sym == 17 ? 3 : 11) + x;
           if (n + rep > nlen + ndist) { bad = true; break; }
-          if (lane == 0) for (uint32_t r = 0; r < rep; r++) L.dlens[n + r] = (uint8_t)val;
+          for (uint32_t r = lane; r < rep; r += 64) L.dlens[n + r] = (uint8_t)val;
+          prev = val;
           n += rep;
           q += cl + xb;
+          b >>= cl + xb;
+          bb -= cl + xb;
         }
+        ZT_ADD(9, tz);
         if (bad) { mode = M_ERROR; break; }
         if (stall) { q = q0; break; }
         wsync<NW>();
@@ -1161,7 +1233,11 @@ int igrow(void** p, size_t* cap, size_t want, bool pinned) {
 }
 inline size_t ial(size_t v, size_t a) { return (v + a - 1) / a * a; }
 int g_zi_par = 0;                    // 0: by batch size, 1: a wave per call, 2: a workgroup per call
-constexpr uint32_t ZI_PAR_CALLS = 256;
+// A workgroup per call up to this many calls: per call it is 10x faster on
+// Huffman data; batched, 1.4x on text and within 5 % on stored blocks
+// (profiles/r06_zinflate_modes.txt).  Beyond it the 256 KiB of resolve
+// scratch per call is not worth holding.
+constexpr uint32_t ZI_PAR_CALLS = 4096;
 }  // namespace
 
 extern "C" {
@@ -1169,6 +1245,7 @@ extern "C" {
 int xcg_zinflate_create(int device, uint32_t nstreams, xcg_zinflate** out) {
   if (!out || nstreams == 0) return XCG_EINVAL;
   if (hipSetDevice(device) != hipSuccess) return XCG_EHIP;
+  if (const char* m = getenv("XCG_ZINFLATE_MODE")) g_zi_par = atoi(m) & 3;   // A/B runs (xcg_debug_set_zinflate_mode)
   xcg_zinflate* z = new xcg_zinflate();
   z->device = device;
   z->nstreams = nstreams;
