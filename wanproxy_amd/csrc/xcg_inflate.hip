@@ -83,6 +83,7 @@ struct IArgs {
   uint32_t* out_len;
   int32_t* status;
   uint32_t* pres;           // NW > 1: RES_CAP resolve slots per call
+  uint32_t warm, maxthr;    // NW > 1: warm-up bits, threads per region (A/B: XCG_ZI_WARM, XCG_ZI_THREADS)
 };
 
 // carried bytes ++ new input into the scratch, 16 bytes per thread (the
@@ -302,7 +303,7 @@ constexpr uint32_t RES_FLAG = 0x80000000u;
 constexpr uint32_t PBIAS = 1u << 20;  // resolve slot: PBIAS + source index (may be < 0: before the region)
 constexpr uint32_t F_STOP = 1, F_BAD = 2;
 constexpr uint64_t PAR_MIN_BITS = 8 * 2048;
-constexpr uint32_t WARM = 128;        // bits decoded before a thread's range to find the true path
+constexpr uint32_t WARM_DEFAULT = 128;   // bits decoded before a thread's range to find the true path
 
 template <int NW>
 struct ParT {
@@ -473,7 +474,7 @@ __device__ unsigned long long g_zi_reg[4];
 
 template <int NW>
 __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, const uint8_t* hist, uint64_t total0,
-                       uint32_t* res) {
+                       uint32_t* res, const uint32_t WARM, const uint32_t maxthr) {
   constexpr int NT = 64 * NW;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   uint64_t rt = ZT_NOW();
@@ -491,7 +492,7 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
     P.fdt[i] = (e & 15) ? dfast(e) : 0;
   }
   const uint32_t span = rl - r0;
-  const uint32_t nact = min((uint32_t)NT, span / SMIN);
+  const uint32_t nact = max(1u, min(min((uint32_t)NT, maxthr), span / SMIN));
   const uint32_t S = span / nact;
   if (t == 0) {
     P.any[0] = P.any[1] = 0;
@@ -691,7 +692,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         __syncthreads();
         const uint32_t cmd = P.cmd;
         if (cmd == 0) break;
-        if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res);
+        if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res, a.warm, a.maxthr);
         else stored_copy<NW>(L, P, R.I, out, total0);
       }
     }
@@ -715,7 +716,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
     if constexpr (NW > 1) {
       if (lane == 0) P.cmd = cmd;
       __syncthreads();
-      if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res);
+      if (cmd == 1) region<NW>(L, P, R.I, out, hist, total0, res, a.warm, a.maxthr);
       else stored_copy<NW>(L, P, R.I, out, total0);
     }
   };
@@ -1233,6 +1234,7 @@ int igrow(void** p, size_t* cap, size_t want, bool pinned) {
 }
 inline size_t ial(size_t v, size_t a) { return (v + a - 1) / a * a; }
 int g_zi_par = 0;                    // 0: by batch size, 1: a wave per call, 2: a workgroup per call
+uint32_t g_zi_warm = xcg::zi::WARM_DEFAULT, g_zi_threads = 1024;   // region shape (A/B runs)
 // A workgroup per call up to this many calls: per call it is 10x faster on
 // Huffman data; batched, 1.4x on text and within 5 % on stored blocks
 // (profiles/r06_zinflate_modes.txt).  Beyond it the 256 KiB of resolve
@@ -1246,6 +1248,8 @@ int xcg_zinflate_create(int device, uint32_t nstreams, xcg_zinflate** out) {
   if (!out || nstreams == 0) return XCG_EINVAL;
   if (hipSetDevice(device) != hipSuccess) return XCG_EHIP;
   if (const char* m = getenv("XCG_ZINFLATE_MODE")) g_zi_par = atoi(m) & 3;   // A/B runs (xcg_debug_set_zinflate_mode)
+  if (const char* m = getenv("XCG_ZI_WARM")) g_zi_warm = (uint32_t)atoi(m);
+  if (const char* m = getenv("XCG_ZI_THREADS")) g_zi_threads = std::max(64, std::min(1024, atoi(m)));
   xcg_zinflate* z = new xcg_zinflate();
   z->device = device;
   z->nstreams = nstreams;
@@ -1329,6 +1333,8 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.out_len = d_out_len;
   a.status = d_status;
   a.pres = par ? (uint32_t*)(z->scratch + o_pres) : nullptr;
+  a.warm = g_zi_warm;
+  a.maxthr = g_zi_threads;
   uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 4095) / 4096);   // 4 KiB per block
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
   if (par) hipLaunchKernelGGL(zi_inflate_kernel<16>, dim3(n), dim3(1024), 0, st, a);
