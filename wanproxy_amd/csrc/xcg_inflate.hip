@@ -277,6 +277,66 @@ __device__ __forceinline__ uint32_t decode(const Tree& T, uint64_t v) {
   return 0;
 }
 
+// A dynamic block's literal/length and distance code lengths, with repeats
+// (RFC 1951 3.2.7), into L.dlens: the serial loop of the decoder, in a function
+// of its own so that its few live values stay in registers (the decoder around
+// it spills SGPRs into VGPR lanes).  The bits come from a 64-bit buffer
+// refilled when fewer than a code (7) and its extra bits (7) remain; the code-
+// length code's 128-entry table sits in `ctw`, two entries per lane.  Returns
+// 0 with q past the sequence, 1 when the input ends inside it, 2 on bad data.
+__device__ __attribute__((noinline)) int cl_sequence(Lds& L, const uint8_t* I, uint64_t& q_io, uint64_t qend_in,
+                                                     uint32_t N, uint32_t ctw) {
+  const int lane = threadIdx.x;
+  uint64_t q = ((uint64_t)readfirst((uint32_t)(q_io >> 32)) << 32) | readfirst((uint32_t)q_io);
+  const uint64_t qend = ((uint64_t)readfirst((uint32_t)(qend_in >> 32)) << 32) | readfirst((uint32_t)qend_in);
+  N = readfirst(N);
+  Reader R{I, 0, 0};
+  R.load(q >> 3);
+  uint32_t n = 0, prev = 0;
+  int rc = 0;
+  uint64_t b = 0;
+  uint32_t bb = 0;
+  while (n < N) {
+    if (q >= qend) { rc = 1; break; }
+    if (bb < 14) {
+      b = R.get(q);
+      bb = 64;
+    }
+    const uint32_t ci = (uint32_t)b & 127;
+    const uint32_t e = (readlane(ctw, (int)(ci >> 1)) >> (16 * (ci & 1))) & 0xffff;
+    const uint32_t cl = e & 15, sym = e >> 4;
+    if (!e) { rc = 2; break; }
+    if (q + cl > qend) { rc = 1; break; }
+    if (sym < 16) {
+      q += cl;
+      b >>= cl;
+      bb -= cl;
+      if (lane == 0) L.dlens[n] = (uint8_t)sym;
+      prev = sym;
+      n++;
+      continue;
+    }
+    uint32_t rep, val = 0;
+    const uint32_t xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+    if (q + cl + xb > qend) { rc = 1; break; }
+    const uint32_t x = (uint32_t)(b >> cl) & ((1u << xb) - 1);
+    if (sym == 16) {
+      if (n == 0) { rc = 2; break; }
+      val = prev;
+      rep = 3 + x;
+    } else rep = (sym == 17 ? 3 : 11) + x;
+    if (n + rep > N) { rc = 2; break; }
+    for (uint32_t r = lane; r < rep; r += 64) L.dlens[n + r] = (uint8_t)val;
+    prev = val;
+    n += rep;
+    q += cl + xb;
+    b >>= cl + xb;
+    bb -= cl + xb;
+  }
+  q_io = q;
+  return rc;
+}
+
 // ---------------------------------------------------------------------------
 // One call on a whole workgroup (the per-call path: a consume() with few
 // others in its batch).  Wave 0 runs the decoder above; inside a Huffman block
@@ -817,44 +877,50 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         // the literal/length and distance code lengths, with repeats; the bits
         // come from a 64-bit buffer refilled when fewer than a code (7) and
         // its extra bits (7) remain
-        uint32_t n = 0, prev = 0;
         bool bad = false;
-        uint64_t b = 0;
-        uint32_t bb = 0;
-        while (n < nlen + ndist) {
-          if (q >= qend) { stall = true; break; }
-          if (bb < 14) {
-            b = R.get(q);
-            bb = 64;
+        if constexpr (NW > 1) {   // (the one-wave kernel keeps it inline: the call costs it 20 %)
+          const int cr = cl_sequence(L, R.I, q, qend, nlen + ndist, ctw);
+          if (cr == 2) bad = true;
+          else if (cr == 1) stall = true;
+        } else {
+          uint32_t n = 0, prev = 0;
+          uint64_t b = 0;
+          uint32_t bb = 0;
+          while (n < nlen + ndist) {
+            if (q >= qend) { stall = true; break; }
+            if (bb < 14) {
+              b = R.get(q);
+              bb = 64;
+            }
+            const uint32_t ci = (uint32_t)b & 127;
+            const uint32_t e = (readlane(ctw, (int)(ci >> 1)) >> (16 * (ci & 1))) & 0xffff;
+            uint32_t cl = e & 15, sym = e >> 4;
+            if (!e || q + cl > qend) { if (!e) bad = true; else stall = true; break; }
+            if (sym < 16) {
+              q += cl;
+              b >>= cl;
+              bb -= cl;
+              if (lane == 0) L.dlens[n] = (uint8_t)sym;
+              prev = sym;
+              n++;
+              continue;
+            }
+            uint32_t rep, val = 0, xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+            if (q + cl + xb > qend) { stall = true; break; }
+            uint32_t x = (uint32_t)(b >> cl) & ((1u << xb) - 1);
+            if (sym == 16) {
+              if (n == 0) { bad = true; break; }
+              val = prev;
+              rep = 3 + x;
+            } else rep = (sym == 17 ? 3 : 11) + x;
+            if (n + rep > nlen + ndist) { bad = true; break; }
+            for (uint32_t r = lane; r < rep; r += 64) L.dlens[n + r] = (uint8_t)val;
+            prev = val;
+            n += rep;
+            q += cl + xb;
+            b >>= cl + xb;
+            bb -= cl + xb;
           }
-          const uint32_t ci = (uint32_t)b & 127;
-          const uint32_t e = (readlane(ctw, (int)(ci >> 1)) >> (16 * (ci & 1))) & 0xffff;
-          uint32_t cl = e & 15, sym = e >> 4;
-          if (!e || q + cl > qend) { if (!e) bad = true; else stall = true; break; }
-          if (sym < 16) {
-            q += cl;
-            b >>= cl;
-            bb -= cl;
-            if (lane == 0) L.dlens[n] = (uint8_t)sym;
-            prev = sym;
-            n++;
-            continue;
-          }
-          uint32_t rep, val = 0, xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-          if (q + cl + xb > qend) { stall = true; break; }
-          uint32_t x = (uint32_t)(b >> cl) & ((1u << xb) - 1);
-          if (sym == 16) {
-            if (n == 0) { bad = true; break; }
-            val = prev;
-            rep = 3 + x;
-          } else rep = (sym == 17 ? 3 : 11) + x;
-          if (n + rep > nlen + ndist) { bad = true; break; }
-          for (uint32_t r = lane; r < rep; r += 64) L.dlens[n + r] = (uint8_t)val;
-          prev = val;
-          n += rep;
-          q += cl + xb;
-          b >>= cl + xb;
-          bb -= cl + xb;
         }
         ZT_ADD(9, tz);
         if (bad) { mode = M_ERROR; break; }
