@@ -759,10 +759,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
   } else {
   R.load(0);
   // history -> ring
+  // (16 bytes per lane and step, every step's load issued before its stores:
+  // one memory latency per 1 KiB instead of one per 64 bytes)
   const uint64_t hn = total0 < (uint64_t)(RMASK + 1) ? total0 : (uint64_t)(RMASK + 1);
-  for (uint64_t i = lane; i < hn; i += 64) {
-    uint64_t pos = total0 - hn + i;
-    L.ring[pos & RMASK] = hist[WSIZE - hn + i];
+  for (uint64_t i0 = 0; i0 < hn; i0 += 1024) {
+    const uint64_t i = i0 + 16 * (uint64_t)lane;
+    const uint8_t* src = hist + (WSIZE - hn + i);
+    if (i + 16 <= hn) {
+      const u32x4 w = *(const u32x4_u*)src;
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 16; k++) L.ring[(total0 - hn + i + k) & RMASK] = (uint8_t)(ww[k >> 2] >> (8 * (k & 3)));
+    } else {
+      for (uint64_t k = i; k < hn; k++) L.ring[(total0 - hn + k) & RMASK] = hist[WSIZE - hn + k];
+    }
   }
   auto flush = [&]() {
     wsync<NW>();
@@ -1189,8 +1199,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
 // check (one wave per call)
 // adler32 of the call's output (four waves per call, consecutive 4-byte words:
 // coalesced), combined with the stream's, checked against a trailer.
-__global__ __launch_bounds__(256) void zi_adler_kernel(IArgs a) {
-  __shared__ uint64_t red[2][4];
+template <int AW>
+__global__ __launch_bounds__(64 * AW) void zi_adler_kernel(IArgs a) {
+  constexpr int AT = 64 * AW;
+  __shared__ uint64_t red[2][AW];
   const uint32_t ci = blockIdx.x;
   const ICall c = a.calls[ci];
   IRes r = a.res[ci];
@@ -1203,7 +1215,7 @@ __global__ __launch_bounds__(256) void zi_adler_kernel(IArgs a) {
     const uint64_t words = n / 4;
     uint32_t since = 0;
 #pragma unroll 4
-    for (uint64_t w = t; w < words; w += 256) {
+    for (uint64_t w = t; w < words; w += AT) {
       const uint32_t v = *(const u32_u*)(d + 4 * w);
       const uint32_t s = (v & 0xff) + ((v >> 8) & 0xff) + ((v >> 16) & 0xff) + (v >> 24);
       A += s;
@@ -1214,7 +1226,7 @@ __global__ __launch_bounds__(256) void zi_adler_kernel(IArgs a) {
         since = 0;
       }
     }
-    for (uint64_t i = 4 * words + t; i < n; i += 256) {
+    for (uint64_t i = 4 * words + t; i < n; i += AT) {
       const uint32_t v = d[i];
       A += v;
       B += i * v;
@@ -1233,8 +1245,13 @@ __global__ __launch_bounds__(256) void zi_adler_kernel(IArgs a) {
   __syncthreads();
   if (t == 0 && r.status >= 0) {
     const uint64_t n = r.out_len;
-    uint64_t A = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) % 65521u;
-    uint64_t B = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) % 65521u;
+    uint64_t A = 0, B = 0;
+    for (int w = 0; w < AW; w++) {
+      A += red[0][w];
+      B += red[1][w];
+    }
+    A %= 65521u;
+    B %= 65521u;
     {
       uint32_t old = sp->adler;
       uint64_t s1 = old & 0xffff, s2 = old >> 16, nn = n % 65521u;
@@ -1405,7 +1422,8 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
   if (par) hipLaunchKernelGGL(zi_inflate_kernel<16>, dim3(n), dim3(1024), 0, st, a);
   else hipLaunchKernelGGL(zi_inflate_kernel<1>, dim3(n), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(zi_adler_kernel, dim3(n), dim3(256), 0, st, a);
+  if (par) hipLaunchKernelGGL(zi_adler_kernel<16>, dim3(n), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL(zi_adler_kernel<4>, dim3(n), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return XCG_EHIP;
   if (hipEventRecord(z->done, st) != hipSuccess) return XCG_EHIP;
   return XCG_OK;
