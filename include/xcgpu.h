@@ -503,9 +503,10 @@ int xcg_zinflate_batch(xcg_zinflate *z, const uint8_t *d_in, const uint64_t *h_i
 int xcg_zinflate_host(xcg_zinflate *z, const uint8_t *h_in, const uint64_t *h_in_off, const uint32_t *h_len,
                       const uint32_t *h_stream, uint32_t n, uint8_t *h_out, const uint64_t *h_out_off,
                       const uint32_t *h_out_cap, uint32_t *h_out_len, int32_t *h_status);
-/* Tests / A-B: which inflate kernel runs -- 0 by batch size (a workgroup per
- * call up to 4096 calls, a wave per call beyond), 1 always a wave per call,
- * 2 always a workgroup per call. */
+/* Tests / A-B: which inflate kernel runs -- 0 by batch size (a 1024-thread
+ * workgroup per call up to 256 calls, 256 threads up to 4096, a wave per call
+ * beyond), 1 always a wave per call, 2 always a 1024-thread workgroup per call,
+ * 3 always a 256-thread workgroup per call. */
 int xcg_debug_set_zinflate_mode(int mode);
 /* Workgroup-kernel regions since the last call (then reset): regions,
  * fixed-point iterations, bytes committed, resolve rounds. */

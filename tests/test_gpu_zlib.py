@@ -176,10 +176,11 @@ def test_errors():
 
 
 # ---------------------------------------------------------------- InflatePipe
-@pytest.fixture(params=[1, 2], ids=['wave', 'workgroup'])
+@pytest.fixture(params=[1, 2, 3], ids=['wave', 'workgroup', 'quarter-workgroup'])
 def inflate_mode(request):
-    """Both inflate kernels: a wave per call (batches of many streams) and a
-    workgroup per call (the per-call path: speculative Huffman regions)."""
+    """Every inflate kernel: a wave per call (batches beyond 4096 streams), a
+    1024-thread workgroup per call (the per-call path: speculative Huffman
+    regions) and a 256-thread one (batches of 257-4096 calls, 16 KiB regions)."""
     from wanproxy_amd.zpipe import set_inflate_mode
     set_inflate_mode(request.param)
     yield request.param
@@ -353,11 +354,11 @@ def _text(rng, n):
 
 
 def _inflate_both(streams, out_cap=None):
-    """Every stream through both kernels: (wave per call, workgroup per call)."""
+    """Every stream through every kernel: (wave, workgroup, quarter workgroup per call)."""
     from wanproxy_amd.zpipe import set_inflate_mode
     got = []
     try:
-        for mode in (1, 2):
+        for mode in (1, 2, 3):
             set_inflate_mode(mode)
             got.append(inflate_streams(streams, out_cap=out_cap))
     finally:
@@ -392,7 +393,8 @@ def test_inflate_workgroup_regions_vs_zlib():
         z = c.compress(d) + c.flush()
         srcs.append(d)
         streams.append([z, b''])
-    wave, wg = _inflate_both(streams)
+    wave, wg, quarter = _inflate_both(streams)
+    assert quarter == wg
     for si, (src, cs) in enumerate(zip(srcs, streams)):
         assert wg[si] == wave[si], si
         ref = InflatePipeRef()
@@ -420,8 +422,8 @@ def test_inflate_workgroup_errors_mid_region():
         corrupt[len(good) // 2 + k] ^= 0xA5
     bad_adler = good[:-1] + bytes([good[-1] ^ 1])
     streams = [[far], [bytes(corrupt)], [bad_adler], [far[:30000], far[30000:]], [good[:65536], good[65536:], b'']]
-    wave, wg = _inflate_both(streams)
-    assert wg == wave
+    wave, wg, quarter = _inflate_both(streams)
+    assert wg == wave and quarter == wave
     assert wg[0][0][1] == -1 and wg[2][0][1] == -1
     assert wg[1][0][1] == -1
     assert wg[4][-1] == (b'', 1)
@@ -439,8 +441,8 @@ def test_inflate_workgroup_small_room():
         z = zlib.compress(d, 6)
         srcs.append(d)
         streams.append(cuts(rng, z, 'frames') + [b''])
-    wave, wg = _inflate_both(streams, out_cap=3000)
-    assert wg == wave
+    wave, wg, quarter = _inflate_both(streams, out_cap=3000)
+    assert wg == wave and quarter == wave
     for si, (src, cs) in enumerate(zip(srcs, streams)):
         ref = InflatePipeRef()
         for k, c in enumerate(cs[:-1]):

@@ -368,7 +368,8 @@ constexpr uint32_t WARM_DEFAULT = 128;   // bits decoded before a thread's range
 template <int NW>
 struct ParT {
   static constexpr int NT = 64 * NW;
-  uint64_t stg[IN_CAP / 8 + 8];       // the region's input, 8-byte words from byte b0
+  static constexpr uint32_t INC = NW >= 8 ? IN_CAP : IN_CAP * NW / 8;   // (smaller workgroups: more per CU by LDS)
+  uint64_t stg[INC / 8 + 8];          // the region's input, 8-byte words from byte b0
   uint32_t st[NT], nst[NT];           // thread t's start, and the one it moves to
   uint32_t endp[NT];                  // bit where thread t's decode ended
   uint32_t cnt[NT];                   // ... the bytes it produced
@@ -984,7 +985,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             flush();
             if (lane == 0) {
               P.q0 = q;
-              P.qlim = qlim - q > 8ull * IN_CAP ? q + 8ull * IN_CAP : qlim;
+              P.qlim = qlim - q > 8ull * ParT<NW>::INC ? q + 8ull * ParT<NW>::INC : qlim;
               P.pos0 = pos;
               P.room = c.out_cap - (pos - total0);
             }
@@ -1318,11 +1319,12 @@ int igrow(void** p, size_t* cap, size_t want, bool pinned) {
 inline size_t ial(size_t v, size_t a) { return (v + a - 1) / a * a; }
 int g_zi_par = 0;                    // 0: by batch size, 1: a wave per call, 2: a workgroup per call
 uint32_t g_zi_warm = xcg::zi::WARM_DEFAULT, g_zi_threads = 1024;   // region shape (A/B runs)
-// A workgroup per call up to this many calls: per call it is 10x faster on
-// Huffman data; batched, 1.4x on text and within 5 % on stored blocks
-// (profiles/r06_zinflate_modes.txt).  Beyond it the 256 KiB of resolve
-// scratch per call is not worth holding.
+// A workgroup per call up to this many calls: per call (1024 threads) it is
+// 13x faster on Huffman data; batched (256 threads, four calls per CU), 2.6x on
+// text and 1.8x on stored blocks (profiles/r06_zinflate_modes.txt).  Beyond it
+// the 256 KiB of resolve scratch per call is not worth holding.
 constexpr uint32_t ZI_PAR_CALLS = 4096;
+constexpr uint32_t ZI_QUARTER_CALLS = 256;
 }  // namespace
 
 extern "C" {
@@ -1396,7 +1398,10 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   }
   // few calls: a workgroup per call (zi_inflate_kernel<16>) with RES_CAP
   // resolve slots each; many: a wave per call
-  const bool par = g_zi_par == 2 || (g_zi_par == 0 && n <= ZI_PAR_CALLS);
+  const bool par = g_zi_par >= 2 || (g_zi_par == 0 && n <= ZI_PAR_CALLS);
+  // quarter workgroups (four calls per CU: one call's serial stretches overlap
+  // the others') once the batch fills the CUs
+  const bool quarter = g_zi_par == 3 || (g_zi_par == 0 && n > ZI_QUARTER_CALLS);
   size_t o_I = 0, o_res = ial(io, 256), o_pres = ial(o_res + sizeof(IRes) * n, 256),
          o_end = par ? o_pres + 4ull * RES_CAP * n : o_pres;
   if (hipEventSynchronize(z->done) != hipSuccess) return XCG_EHIP;
@@ -1420,7 +1425,8 @@ int xcg_zinflate_batch(xcg_zinflate* z, const uint8_t* d_in, const uint64_t* h_i
   a.maxthr = g_zi_threads;
   uint32_t tiles = std::min<uint32_t>(64, (PEND_CAP + maxlen + IPAD + 4095) / 4096);   // 4 KiB per block
   hipLaunchKernelGGL(zi_prep_kernel, dim3(tiles, n), dim3(256), 0, st, a);
-  if (par) hipLaunchKernelGGL(zi_inflate_kernel<16>, dim3(n), dim3(1024), 0, st, a);
+  if (par && quarter) hipLaunchKernelGGL(zi_inflate_kernel<4>, dim3(n), dim3(256), 0, st, a);
+  else if (par) hipLaunchKernelGGL(zi_inflate_kernel<16>, dim3(n), dim3(1024), 0, st, a);
   else hipLaunchKernelGGL(zi_inflate_kernel<1>, dim3(n), dim3(64), 0, st, a);
   if (par) hipLaunchKernelGGL(zi_adler_kernel<16>, dim3(n), dim3(1024), 0, st, a);
   else hipLaunchKernelGGL(zi_adler_kernel<4>, dim3(n), dim3(256), 0, st, a);
@@ -1492,7 +1498,7 @@ int xcg_debug_zinflate_regions(uint64_t* out) {
 }
 
 int xcg_debug_set_zinflate_mode(int mode) {
-  if (mode < 0 || mode > 2) return XCG_EINVAL;
+  if (mode < 0 || mode > 3) return XCG_EINVAL;
   g_zi_par = mode;
   return XCG_OK;
 }

@@ -63,7 +63,8 @@ def _lib():
 
 def set_inflate_mode(mode: int) -> None:
     """Which inflate kernel runs (xcg_debug_set_zinflate_mode): 0 by batch
-    size, 1 a wave per call, 2 a workgroup per call."""
+    size, 1 a wave per call, 2 a 1024-thread workgroup per call, 3 a
+    256-thread workgroup per call."""
     _check(_lib().xcg_debug_set_zinflate_mode(mode))
 
 
