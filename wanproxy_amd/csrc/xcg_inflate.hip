@@ -383,7 +383,7 @@ struct ParT {
   uint32_t chg[2], fm[2];             // fixed point: first thread whose start moved / that stopped
   uint32_t cmd;                       // 0 done, 1 Huffman region, 2 stored copy
   uint64_t q0, qlim, pos0, room, n, soff;
-  uint32_t R;
+  uint32_t R, stopped;
   uint64_t qn;
   uint64_t t_ol;                      // the tail's history update: output length, and whether to do it
   uint32_t t_do;
@@ -631,7 +631,11 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
     atomicAdd(&g_zi_reg[0], 1ull);
     atomicAdd(&g_zi_reg[1], (unsigned long long)iters);
   }
-  uint32_t f = min(P.fm[(iters - 1) & 1], nact);
+  // Threads before the first stopped one commit, and that one too up to its
+  // stop (an end of block or an invalid code on the true path: its bytes
+  // before it are the decoder's): wave 0 resumes at the stopping symbol.
+  const uint32_t fstop = min(P.fm[(iters - 1) & 1], nact);
+  uint32_t f = fstop < nact ? fstop + 1 : nact;
   if (act) {
     s = P.st[t];
     n = P.cnt[t];
@@ -692,6 +696,7 @@ __device__ void region(Lds& L, ParT<NW>& P, const uint8_t* I, uint8_t* out, cons
   if (t == 0) {
     P.R = R;
     P.qn = 8 * b0 + qn;
+    P.stopped = fstop < nact && f > fstop;   // resumes at the stopping symbol
   }
   __threadfence();   // the region's bytes are read back by later far matches
   __syncthreads();
@@ -993,7 +998,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             const uint32_t rn = su(P.R);
             const uint64_t qn = ((uint64_t)su((uint32_t)(P.qn >> 32)) << 32) | su((uint32_t)P.qn);
             ZT_ADD(8, tz);
-            if (!rn) par_ok = false;   // the block ends (or fails) within a thread's range: the careful path
+            // the block ends (or fails) at the region's end, or within its first
+            // thread's range: the careful path takes it from here
+            if (!rn || su(P.stopped)) par_ok = false;
             pos += rn;
             flushed = pos;
             q = qn;
