@@ -337,6 +337,137 @@ __device__ __attribute__((noinline)) int cl_sequence(Lds& L, const uint8_t* I, u
   return rc;
 }
 
+// The same sequence decoded speculatively by wave 0's 64 lanes (the
+// workgroup kernels): lane l owns bits [36 l, 36 l + 36) of the next 2304 (more
+// than the longest sequence, 316 lengths x 7 bits).  It decodes the 48 bits
+// before its range to fall onto the true symbol starts, decodes its range,
+// and the lanes move to their predecessors' ends until the starts are fixed
+// up to the lane that completes the nlen + ndist lengths (or stops).  A scan of
+// the lanes' repeat counts places them; each lane then writes its lengths and
+// checks the serial loop's conditions in its order, and the first lane with an
+// event decides.  Returns 0 (q past the sequence), 1 (input ends inside it),
+// 2 (bad data), or 3 to leave it to cl_sequence.
+constexpr uint32_t CL_LANE_BITS = 36, CL_WARM = 48, CL_INV = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t cl_at(const Lds& L, const uint32_t* bits, uint32_t sh0, uint32_t j) {
+  const uint32_t bp = sh0 + j, w = bp >> 5;
+  const uint64_t v = (((uint64_t)bits[w + 1] << 32) | bits[w]) >> (bp & 31);
+  const uint32_t e = L.ct.pri[v & 127];
+  if (!(e & 15)) return CL_INV;
+  const uint32_t cl = e & 15, sym = e >> 4;
+  const uint32_t xb = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
+  const uint32_t x = (uint32_t)(v >> cl) & ((1u << xb) - 1);
+  const uint32_t rep = sym < 16 ? 1 : sym == 18 ? 11 + x : 3 + x;
+  return sym | (rep << 8) | (cl << 16) | (xb << 20);
+}
+
+// decode from s while s < lim: the end; cnt = lengths produced; fl: stopped at
+// an invalid code; lv / hv: value of the last non-16 symbol, and whether any
+__device__ __forceinline__ uint32_t cl_run(const Lds& L, const uint32_t* bits, uint32_t sh0, uint32_t s, uint32_t lim,
+                                           uint32_t& cnt, uint32_t& fl, uint32_t& lv, uint32_t& hv) {
+  cnt = 0;
+  fl = 0;
+  lv = 0;
+  hv = 0;
+  while (s < lim) {
+    const uint32_t in = cl_at(L, bits, sh0, s);
+    if (in == CL_INV) {
+      fl = 1;
+      break;
+    }
+    const uint32_t sym = in & 255;
+    cnt += (in >> 8) & 255;
+    if (sym != 16) {
+      lv = sym < 16 ? sym : 0;
+      hv = 1;
+    }
+    s += ((in >> 16) & 15) + ((in >> 20) & 15);
+  }
+  return s;
+}
+
+template <int NW>
+__device__ __attribute__((noinline)) int cl_spec(Lds& L, uint32_t* bits, const uint8_t* I, uint64_t& q_io,
+                                                 uint64_t qend_in, uint32_t N) {
+  const int lane = threadIdx.x;
+  const uint64_t q = ((uint64_t)readfirst((uint32_t)(q_io >> 32)) << 32) | readfirst((uint32_t)q_io);
+  const uint64_t qend = ((uint64_t)readfirst((uint32_t)(qend_in >> 32)) << 32) | readfirst((uint32_t)qend_in);
+  N = readfirst(N);
+  const uint64_t qw = q >> 5;
+  for (int k = lane; k < 80; k += 64) bits[k] = ((const uint32_t*)I)[qw + k];
+  wsync<NW>();
+  const uint32_t sh0 = (uint32_t)(q & 31);
+  const uint32_t c0 = (uint32_t)lane * CL_LANE_BITS, c1 = c0 + CL_LANE_BITS;
+  uint32_t s = c0, cnt, fl, lv, hv;
+  if (lane > 0) {
+    uint32_t wc, wf, wl, wh;
+    const uint32_t we = cl_run(L, bits, sh0, c0 > CL_WARM ? c0 - CL_WARM : 0, c0, wc, wf, wl, wh);
+    if (!wf) s = we;
+  }
+  uint32_t e = cl_run(L, bits, sh0, s, c1, cnt, fl, lv, hv);
+  for (int it = 0; it < 64; it++) {   // fixed point of the lanes' starts
+    const uint32_t pe = __shfl_up(e, 1), pf = __shfl_up(fl, 1);
+    const bool mv = lane > 0 && !pf && pe != s;
+    const uint64_t bm = ballot(mv);
+    if (!bm) break;
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint64_t bt = ballot(incl >= N) | ballot(fl != 0);
+    if (bt && __builtin_ctzll(bt) < __builtin_ctzll(bm)) break;   // every start up to the deciding lane is final
+    if (mv) {
+      s = pe;
+      e = cl_run(L, bits, sh0, s, c1, cnt, fl, lv, hv);
+    }
+  }
+  const uint32_t incl = wave_incl_scan(cnt);
+  const uint32_t base = incl - cnt;
+  // the value of the last non-16 symbol below this lane (the "previous length" a 16 repeats)
+  uint32_t tag = hv ? (uint32_t)lane + 1 : 0u;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(tag, o);
+    if (lane >= o) tag = max(tag, y);
+  }
+  uint32_t ex = __shfl_up(tag, 1);
+  if (lane == 0) ex = 0;
+  const uint32_t pv = __shfl(lv, ex ? (int)ex - 1 : 0);
+  uint32_t prev = ex ? pv : 0;
+  // write and check, in stream order within the lane
+  uint32_t ev = 0, evbits = 0;   // 1 stall, 2 bad, 3 complete (evbits: bits consumed)
+  if (base < N) {
+    uint32_t r = s, o = base;
+    while (r < c1) {
+      const uint64_t pos = q + r;
+      if (pos >= qend) { ev = 1; break; }
+      const uint32_t in = cl_at(L, bits, sh0, r);
+      if (in == CL_INV) { ev = 2; break; }
+      const uint32_t sym = in & 255, rep = (in >> 8) & 255, cl = (in >> 16) & 15, xb = (in >> 20) & 15;
+      if (pos + cl > qend) { ev = 1; break; }
+      if (sym >= 16 && pos + cl + xb > qend) { ev = 1; break; }
+      if (sym == 16 && o == 0) { ev = 2; break; }
+      if (o + rep > N) { ev = 2; break; }
+      const uint32_t val = sym < 16 ? sym : sym == 16 ? prev : 0;
+      for (uint32_t k = 0; k < rep; k++) L.dlens[o + k] = (uint8_t)val;
+      prev = val;
+      o += rep;
+      r += cl + xb;
+      if (o == N) {
+        ev = 3;
+        evbits = r;
+        break;
+      }
+    }
+  }
+  const uint64_t bev = ballot(ev != 0);
+  wsync<NW>();
+  if (!bev) return 3;
+  const int dl = __builtin_ctzll(bev);
+  const uint32_t dev = readlane(ev, dl), dbits = readlane(evbits, dl);
+  if (dev == 3) {
+    q_io = q + dbits;
+    return 0;
+  }
+  return (int)dev;
+}
+
 // ---------------------------------------------------------------------------
 // One call on a whole workgroup (the per-call path: a consume() with few
 // others in its batch).  Wave 0 runs the decoder above; inside a Huffman block
@@ -895,7 +1026,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         // its extra bits (7) remain
         bool bad = false;
         if constexpr (NW > 1) {   // (the one-wave kernel keeps it inline: the call costs it 20 %)
-          const int cr = cl_sequence(L, R.I, q, qend, nlen + ndist, ctw);
+          int cr = cl_spec<NW>(L, (uint32_t*)P.stg, R.I, q, qend, nlen + ndist);
+          if (cr == 3) cr = cl_sequence(L, R.I, q, qend, nlen + ndist, ctw);
           if (cr == 2) bad = true;
           else if (cr == 1) stall = true;
         } else {
