@@ -429,6 +429,57 @@ def test_inflate_workgroup_errors_mid_region():
     assert wg[4][-1] == (b'', 1)
 
 
+def _dyn_header_stream(syms, nlen=257, ndist=1):
+    """A zlib stream whose one dynamic block header codes the code-length
+    symbols `syms` [(symbol, extra value)] with a 2-bit code over {0, 8, 16,
+    18} (RFC 1951 3.2.7), nothing after it."""
+    bits = []
+
+    def put(v, n):                      # LSB first
+        bits.extend((v >> i) & 1 for i in range(n))
+
+    def put_code(c, n):                 # Huffman codes MSB first
+        bits.extend((c >> (n - 1 - i)) & 1 for i in range(n))
+    put(1, 1)
+    put(2, 2)
+    put(nlen - 257, 5)
+    put(ndist - 1, 5)
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    lens = {0: 2, 8: 2, 16: 2, 18: 2}
+    put(len(order) - 4, 4)
+    for sym in order:
+        put(lens.get(sym, 0), 3)
+    code = {0: 0, 8: 1, 16: 2, 18: 3}
+    for sym, x in syms:
+        put_code(code[sym], 2)
+        if sym == 16:
+            put(x, 2)
+        elif sym == 18:
+            put(x, 7)
+    bits.extend([0] * (-len(bits) % 8))
+    body = bytes(sum(bits[i + k] << k for k in range(8)) for i in range(0, len(bits), 8))
+    return bytes([0x78, 0x9c]) + body + bytes(8)
+
+
+def test_inflate_dynamic_header_errors_both_kernels():
+    """Code-length sequences the decoder must refuse, through the serial loop
+    (wave kernel) and the lane-speculative decode (workgroup kernels): a first
+    symbol 16 (nothing to repeat), a repeat past nlen + ndist, and a sequence
+    that leaves the literal/length code incomplete (zlib refuses all three);
+    plus a header cut every third byte (the input ends inside it: the call
+    stalls, the next one decides).  Every kernel gives the same outputs and
+    statuses."""
+    first16 = _dyn_header_stream([(16, 0)] + [(8, 0)] * 257)
+    over = _dyn_header_stream([(18, 127)] * 2 + [(8, 0)] * 3)
+    no_eob = _dyn_header_stream([(18, 127), (18, 107), (8, 0), (8, 0)])   # 256 zeros: length[256] == 0
+    cut = _dyn_header_stream([(8, 0)] * 100 + [(16, 3)] * 20 + [(18, 50)] * 2)
+    streams = [[first16], [over], [no_eob]] + [[cut[:k], cut[k:]] for k in range(2, len(cut) - 8, 3)]
+    wave, wg, quarter = _inflate_both(streams)
+    assert wg == wave and quarter == wave
+    for si in range(3):
+        assert wave[si][0][1] == -1, si
+
+
 def test_inflate_workgroup_small_room():
     """Output room smaller than a region's output: the region commits the
     threads that fit, the careful path returns -2 where the wave kernel does,
