@@ -957,7 +957,7 @@ struct TreeLds {
 };
 // one TreeLds per lane-owned block, at a stride of 4 mod 64 words (16-byte aligned, no bank conflicts
 // between the TB lanes)
-constexpr int TB = 2;   // blocks per wave
+constexpr int TB_BATCH = 2;   // blocks per wave in batches (one per wave when few blocks)
 constexpr uint32_t TSTRIDE = ((sizeof(TreeLds) + 255) / 256) * 256 + 16;
 
 __device__ __forceinline__ uint32_t hkey(uint32_t e) { return e >> 10; }
@@ -1127,6 +1127,7 @@ __device__ void scan_tree(TreeLds& s, const uint16_t* dl, int max_code) {
 // then lane t runs block t's trees (the heap work is a serial chain per
 // block; one lane per block spends the wave's VALU issue slots on TB chains
 // instead of one), then the code tables leave with the whole wave.
+template <int TB>
 __global__ __launch_bounds__(64) void zd_trees_kernel(ZArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[TB * TSTRIDE];
   __shared__ int ttype[TB];
@@ -2012,7 +2013,10 @@ int xcg_zdeflate_batch_seg(xcg_zdeflate* z, const uint8_t* d_in, const uint64_t*
     }
     z->last_rounds = rounds;
   }
-  hipLaunchKernelGGL(zd_trees_kernel, dim3((bo + TB - 1) / TB), dim3(64), 0, st, a);
+  // few blocks (one consume at a time): a wave per block, whose heap chains
+  // then run without a second lane's diverging beside them; many: two per wave
+  if (bo <= 64) hipLaunchKernelGGL(zd_trees_kernel<1>, dim3(bo), dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(zd_trees_kernel<TB_BATCH>, dim3((bo + TB_BATCH - 1) / TB_BATCH), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_layout_kernel, dim3(n), dim3(64), 0, st, a);
   hipLaunchKernelGGL(zd_emit_kernel, dim3(bo), dim3(64), 0, st, a);
   if (fast) hipLaunchKernelGGL(zd_ring_kernel, dim3(n), dim3(256), 0, st, a);   // (before commit moves the state)
